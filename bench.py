@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark of the GN hot path (J+H build) on MI355X — BASELINE.json metric:
+"GN iterations/sec + observations/sec (J+H build) at 1/2/4/8 GPUs vs CPU".
+
+A *step* is one J+H build (reference slam/solver.cpp:28-69) over the whole synthetic
+config-3 world (100k poses / 200k landmarks / 1M bearings / 99 999 odometry edges), inputs
+resident in HBM. ``value`` = observations (bearings + odometry edges) processed per second by
+the whole job. With ``--gpus N > 1`` the same world is sharded across N ranks (strong scaling)
+and a step includes the RCCL exchange of every rank's rows of H and b.
+
+Also reported: GN iterations/s (full steps: J+H + exchange + sparse Cholesky + box-plus),
+the J+H kernel's HBM roofline fraction (algorithmic bytes) and the CPU
+baseline (the oracle, oracle/bos_oracle.cpp, timed on this host).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|fp64]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "prb-project-bearing-only-slam_amd"))
+
+import numpy as np  # noqa: E402
+
+import bos  # noqa: E402
+
+METRIC = "GN iterations/sec + observations/sec (J+H build) at 1/2/4/8 GPUs vs CPU"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, HBM3E peak (spec)
+CONFIG3 = dict(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(P, precision, budget_s=12.0):
+    """The oracle's J+H build on this host (bounded sample), best of 1 thread / all threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    from helpers import to_oracle
+    Q = to_oracle(P)
+    prec = 32 if precision == bos.BOS_FP32 else 64
+    nobs = len(P.b_z) + len(P.o_z)
+    best = None
+    threads_all = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    for th in sorted({1, threads_all}):
+        O.linearize(Q, precision=prec, threads=th)   # warm-up
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < budget_s / 2:
+            O.linearize(Q, precision=prec, threads=th)
+            n += 1
+        dt = (time.perf_counter() - t0) / n
+        rate = nobs / dt
+        log(f"cpu oracle J+H threads={th}: {dt * 1e3:.1f} ms/step, {rate / 1e6:.2f} Mobs/s ({n} steps)")
+        if best is None or rate > best[0]:
+            best = (rate, th, n)
+    return {"value": best[0], "unit": "obs/s", "cores": best[1], "kind": "port",
+            "sample": f"{best[2]} full J+H builds of config 3 ({nobs} obs each, {prec}-bit) by the C++ "
+                      f"oracle, ~{budget_s / 2:.0f} s per thread count, best of 1/{threads_all} threads"}
+
+
+def cpu_gn_baseline(P, budget_s=10.0):
+    """Full CPU GN steps (oracle J+H + SciPy sparse solve + box-plus), bounded sample."""
+    import oracle as O
+    from helpers import to_oracle
+    Q = to_oracle(P)
+    p, l = Q.copy_state()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < budget_s or n == 0:
+        O.step(Q, p, l, threads=1)
+        n += 1
+    dt = (time.perf_counter() - t0) / n
+    return {"value": 1.0 / dt, "unit": "it/s", "cores": 1, "kind": "port",
+            "sample": f"{n} GN iterations of config 3 (oracle J+H fp64 + scipy spsolve + box-plus)"}
+
+
+def traffic_from_profile(precision):
+    """HBM bytes per launch of the J+H kernel from the committed rocprofv3 PMC summary."""
+    name = "r01_pmc_linearize_fp32.json" if precision == bos.BOS_FP32 else "r01_pmc_linearize_fp64.json"
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return float(json.load(f)["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
+    ap.add_argument("--gn-steps", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    precision = bos.BOS_FP32 if args.precision == "fp32" else bos.BOS_FP64
+
+    t_gen = time.perf_counter()
+    P = bos.synthetic(**CONFIG3)
+    nobs = len(P.b_z) + len(P.o_z)
+    log(f"rank {rank}: config 3 world NP={P.NP} NL={P.NL} Mb={len(P.b_z)} Mo={len(P.o_z)} "
+        f"({time.perf_counter() - t_gen:.1f} s)")
+
+    nccl_id = None
+    if world > 1:
+        obj = [bos.nccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        nccl_id = obj[0]
+    # a dedicated (non-null) stream: the handle launches every kernel on it, and the timing
+    # events below are recorded on the same stream
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    t_create = time.perf_counter()
+    S = bos.Solver(P, precision=precision, device=local_rank, stream=stream.cuda_stream, rank=rank,
+                   world_size=world, nccl_id=nccl_id)
+    info = S.system_info()
+    log(f"rank {rank}: bos_create {time.perf_counter() - t_create:.1f} s, n={info['n']} "
+        f"nnz(H lower)={info['nnz_lower']} nnz(L)={info['nnz_factor']}")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # ---- J+H build throughput
+    for _ in range(args.warmup):
+        S.linearize_async()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        S.linearize_async()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        t = torch.tensor([wall], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    ms_per_step = wall / args.steps * 1e3
+    value = nobs * args.steps / wall
+
+    # ---- full GN iterations (J+H + exchange + solve + update)
+    S2 = S
+    gn = S2.step()   # includes the one-time rocSOLVER analysis
+    barrier()
+    torch.cuda.synchronize()
+    tg = time.perf_counter()
+    gn_stats = []
+    for _ in range(args.gn_steps):
+        gn_stats.append(S2.step())
+    barrier()
+    gn_wall = time.perf_counter() - tg
+    if world > 1:
+        t = torch.tensor([gn_wall], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gn_wall = float(t.item())
+    gn_it_s = args.gn_steps / gn_wall
+    phase = {k: float(np.median([g[k] for g in gn_stats])) for k in
+             ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
+
+    if rank == 0:
+        algo = info["algorithmic_bytes"]
+        achieved = algo / (kernel_ms * 1e-3) / 1e9
+        traffic = traffic_from_profile(precision) if world == 1 else None
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "obs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32" if precision == bos.BOS_FP32 else "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": "config 3: synthetic 100k poses / 200k landmarks / 1M bearings / 99999 odometry "
+                            "edges; J+H build " + ("fp32" if precision == bos.BOS_FP32 else "fp64") +
+                            " (solve fp64)",
+                "poses": P.NP, "landmarks": P.NL, "bearings": int(len(P.b_z)), "odometry": int(len(P.o_z)),
+                "parallelism": f"observation-sharded x{world}" if world > 1 else "single GPU",
+            },
+            "gn_iters_per_s": gn_it_s,
+            "gn_phase_ms": phase,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": algo,
+                "kernel_ms": kernel_ms,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(P, precision)
+            line["cpu_baseline_gn"] = cpu_gn_baseline(P)
+            line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+            line["gn_speedup_vs_cpu"] = gn_it_s / line["cpu_baseline_gn"]["value"]
+        print(json.dumps(line), flush=True)
+    S.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+/*
+ * bos.h — C ABI of the MI355X-native Gauss-Newton solver for 2-D bearing-only SLAM.
+ *
+ * Drop-in boundary for the reference's `proj02::Solver` (torchipeppo/prb-project-bearing-only-slam,
+ * slam/solver.hpp:21-92). Plain pointers and sizes only, no exceptions across the boundary,
+ * status 0 = OK, < 0 = error with a message from bos_last_error().
+ *
+ * Ownership and semantics follow the reference:
+ *  - bos_create COPIES the problem (the reference's Solver ctor copies State and observation
+ *    vectors, slam/solver.cpp:5-8); the caller's arrays are not referenced afterwards.
+ *  - bos_step is synchronous: on return the state held by the handle has been updated
+ *    (Solver::step, slam/solver.cpp:27-97).
+ *  - one handle = one host thread; concurrent calls on one handle are undefined (the reference
+ *    mutates its members H, b and the LDLT object in step(), slam/solver.hpp:58-82).
+ *
+ * Reference-side binding: see INTEGRATION.md.
+ */
+#ifndef BOS_H_
+#define BOS_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BOS_ABI_VERSION 1
+
+/* status codes */
+#define BOS_OK 0
+#define BOS_ERR_INVALID -1      /* bad argument / malformed problem                         */
+#define BOS_ERR_DEVICE -2       /* HIP runtime error or no device                            */
+#define BOS_ERR_SOLVER -3       /* rocSOLVER / rocBLAS failure                               */
+#define BOS_ERR_IO -4           /* file not found / parse error                              */
+#define BOS_ERR_UNSUPPORTED -5  /* input the build does not handle (see bos_last_error)     */
+#define BOS_ERR_COMM -6         /* RCCL failure                                              */
+
+/* arithmetic of the J+H build (the solve is always fp64) */
+#define BOS_FP64 64
+#define BOS_FP32 32
+
+/* linear solver for H_nf dx = -b_nf */
+#define BOS_SOLVER_SPARSE_CHOL 0  /* rocSOLVER csrrf refactchol/solve on a host-analysed pattern */
+#define BOS_SOLVER_DENSE_CHOL 1   /* rocSOLVER potrf/potrs on a dense copy (small problems)      */
+
+/*
+ * Problem in stix order (framework/state.hpp:47-53): poses in file order, landmarks in
+ * ascending-id order (slam/triangulation.cpp:68-73). Replaces the (State, BearingObservationVector,
+ * OdometryObservationVector, fixed_pose_id) arguments of Solver::Solver (slam/solver.hpp:30);
+ * ids are resolved to stix once here instead of std::map::at per observation per iteration
+ * (framework/state.cpp:43-63).
+ */
+typedef struct bos_problem {
+    int32_t num_poses;              /* NP                                                        */
+    int32_t num_landmarks;          /* NL                                                        */
+    int32_t num_bearings;           /* M_b                                                       */
+    int32_t num_odometry;           /* M_o                                                       */
+    const double* pose_xyt;         /* [NP*3] x, y, theta                                        */
+    const double* landmark_xy;      /* [NL*2]                                                    */
+    const int32_t* bearing_pose;    /* [M_b] pose stix                                           */
+    const int32_t* bearing_landmark;/* [M_b] landmark stix                                       */
+    const double* bearing_z;        /* [M_b] bearing, already smallestAngle-wrapped              */
+    const double* bearing_omega;    /* [M_b] information, or NULL for 1 (observation.hpp:16,22)  */
+    const int32_t* odom_src;        /* [M_o] pose stix                                           */
+    const int32_t* odom_dst;        /* [M_o] pose stix                                           */
+    const double* odom_z;           /* [M_o*3] x, y, theta in the source frame                   */
+    const double* odom_omega;       /* [M_o*9] row-major symmetric information matrix            */
+    int32_t fixed_pose;             /* stix of the pose held fixed (solver.cpp:99-125)           */
+} bos_problem;
+
+typedef struct bos_options {
+    int32_t precision;              /* BOS_FP64 (default) or BOS_FP32                            */
+    int32_t solver;                 /* BOS_SOLVER_SPARSE_CHOL (default) / BOS_SOLVER_DENSE_CHOL  */
+    int32_t device;                 /* HIP device ordinal, -1 = current                          */
+    int32_t rank;                   /* shard index (0 for one GPU)                               */
+    int32_t world_size;             /* number of shards (1 for one GPU)                          */
+    const void* nccl_unique_id;     /* 128-byte ncclUniqueId when world_size > 1, else NULL      */
+    double kernel_threshold;        /* robust kernel threshold, reference default 1.0 (:16)      */
+    double damping;                 /* damping factor, reference default 0.01 (:17)              */
+    void* stream;                   /* hipStream_t to launch on, NULL = the handle's own stream  */
+} bos_options;
+
+/* Per-iteration statistics (the reference prints nothing; step() returns void). */
+typedef struct bos_step_stats {
+    double chi2;                    /* sum e^T Omega e over all edges before the robust kernel   */
+    int32_t n_robust;               /* observations scaled by the robust kernel                  */
+    int32_t solver_info;            /* 0 ok, >0 factorization reported a non-SPD pivot           */
+    double max_abs_dx;              /* max |dx| of the applied update                            */
+    double t_linearize_ms;          /* J+H build (incl. exchange when sharded), hipEvent timed   */
+    double t_exchange_ms;           /* RCCL exchange part (0 on one GPU)                         */
+    double t_solve_ms;              /* factorization + triangular solves                         */
+    double t_update_ms;             /* box-plus                                                  */
+} bos_step_stats;
+
+/* Static sizes of the linear system built by bos_create (for export buffers / roofline). */
+typedef struct bos_system_info {
+    int64_t n;                      /* N - 3 (fixed pose removed)                                */
+    int64_t nnz_lower;              /* stored entries of the lower triangle of H_nf              */
+    int64_t nnz_factor;             /* entries of the Cholesky factor (sparse solver)            */
+    int64_t algorithmic_bytes;      /* SURVEY §8(d) J+H bytes for this problem and precision      */
+    int64_t num_items_pose;         /* pose-centric work items (bearings + 2 x odometry)         */
+    int64_t num_items_landmark;     /* landmark-centric work items (bearings)                    */
+    int32_t owned_first_row;        /* this shard's rows of H_nf [first, last)                   */
+    int32_t owned_last_row;
+} bos_system_info;
+
+void bos_default_options(bos_options* opt);
+const char* bos_last_error(void);
+int bos_abi_version(void);
+int bos_device_count(void);
+/* ncclGetUniqueId for world_size > 1: rank 0 creates it, the caller distributes the bytes */
+int bos_nccl_unique_id(void* out, int64_t len);
+
+/* Solver::Solver (slam/solver.hpp:30, slam/solver.cpp:5-18) */
+int bos_create(const bos_problem* problem, const bos_options* options, struct bos_solver** out);
+/* ~Solver */
+int bos_destroy(struct bos_solver* s);
+/* Solver::set_kernel_threshold / set_damping_factor (slam/solver.hpp:33-34) */
+int bos_set_kernel_threshold(struct bos_solver* s, double kt);
+int bos_set_damping_factor(struct bos_solver* s, double df);
+/* Solver::step (slam/solver.hpp:36, slam/solver.cpp:27-97): one synchronous GN iteration */
+int bos_step(struct bos_solver* s, bos_step_stats* stats);
+/* bos_step repeated n times with one host synchronisation at the end (UI batch of 50,
+ * executables/bearing_only_slam.cpp:95-98); stats of the last iteration */
+int bos_step_n(struct bos_solver* s, int n, bos_step_stats* last);
+/* The J+H build alone (slam/solver.cpp:28-69) — H and b stay on the device */
+int bos_linearize(struct bos_solver* s, bos_step_stats* stats);
+/* Enqueue the J+H build on the handle's stream without synchronising (benchmarking) */
+int bos_linearize_async(struct bos_solver* s);
+int bos_synchronize(struct bos_solver* s);
+int bos_system_info_get(const struct bos_solver* s, bos_system_info* info);
+/*
+ * Export the last linearization in the reference's dof order (poses 3*stix, landmarks
+ * 3*NP + 2*stix, slam/solver_jacobians.cpp:70-71): the lower triangle of H with the fixed pose's
+ * rows/cols removed (H_nofixed, slam/solver.cpp:72, indices still in full N numbering) as COO
+ * (capacity = nnz_lower), and the full b[N] (slam/solver.cpp:45,61).
+ */
+int bos_export_system(const struct bos_solver* s, int64_t capacity, int32_t* rows, int32_t* cols, double* vals,
+                      double* b);
+/* State read/write in stix order (State::poses / landmarks, framework/state.hpp:47-48) */
+int bos_get_state(const struct bos_solver* s, double* pose_xyt, double* landmark_xy);
+int bos_set_state(struct bos_solver* s, const double* pose_xyt, const double* landmark_xy);
+/* The dx of the last bos_step in the reference's dof order (slam/solver.cpp:88-94) */
+int bos_get_last_dx(const struct bos_solver* s, double* dx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BOS_H_ */

@@ -1,0 +1,63 @@
+/*
+ * bos_host.h — host-side utilities of libbos.so (no GPU needed): the reference's g2o loader and
+ * landmark triangulation, the synthetic world generator, and plan inspection for tests.
+ *
+ *   bos_dataset_load_g2o   <- parse_g2o           (utils/g2o_utils.hpp:29, g2o_utils.cpp:10-146)
+ *                            + default fixed pose (executables/bearing_only_slam.cpp:63-65)
+ *                            + triangulate_landmarks (slam/triangulation.hpp:8, triangulation.cpp:65-74)
+ *   bos_dataset_write_g2o  <- (no reference counterpart: the checkpoint artefact of SURVEY.md §5)
+ */
+#ifndef BOS_HOST_H_
+#define BOS_HOST_H_
+
+#include "bos.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bos_dataset bos_dataset;
+
+/* Parse a g2o file, default the fixed pose to the first pose and (if triangulate) append the
+ * triangulated landmarks in ascending-id order. verbose prints the reference's warnings. */
+int bos_dataset_load_g2o(const char* path, int triangulate, int verbose, bos_dataset** out);
+/* Synthetic world: initial guess = dead-reckoned odometry chain, landmarks
+ * triangulated from it; ground truth available through bos_dataset_ground_truth. */
+int bos_dataset_synthetic(int32_t num_poses, int32_t num_landmarks, int32_t bearings_per_pose, uint64_t seed,
+                          bos_dataset** out);
+/* Problem view (pointers owned by the dataset, valid until bos_dataset_free). */
+int bos_dataset_problem(const bos_dataset* ds, bos_problem* view);
+const int32_t* bos_dataset_pose_ids(const bos_dataset* ds);
+const int32_t* bos_dataset_landmark_ids(const bos_dataset* ds);
+int32_t bos_dataset_fixed_pose_id(const bos_dataset* ds);
+float bos_dataset_bound(const bos_dataset* ds);
+/* Ground truth of a synthetic dataset in stix order; BOS_ERR_INVALID for loaded files. */
+int bos_dataset_ground_truth(const bos_dataset* ds, const double** pose_xyt, const double** landmark_xy);
+/* Write the dataset as g2o; pose_xyt / landmark_xy override the state (NULL = dataset state). */
+int bos_dataset_write_g2o(const bos_dataset* ds, const char* path, const double* pose_xyt, const double* landmark_xy,
+                          int with_landmarks);
+void bos_dataset_free(bos_dataset* ds);
+
+typedef struct bos_plan_info {
+    int64_t n;
+    int64_t nnz_lower;
+    int64_t nnz_factor;
+    int64_t num_tasks_pose;
+    int64_t num_tasks_landmark;
+    double flops_temporal;
+    double flops_nested_dissection;
+    char ordering[32];
+} bos_plan_info;
+
+/* Build the static plan on the host (what bos_create does before touching the GPU).
+ * If ref_rows/ref_cols/owned are given (capacity >= nnz_lower) they receive, for every stored
+ * entry of the lower triangle of H_nf, its (row, col) in the reference dof numbering
+ * (row >= col) and whether rank `rank` of `world` writes it; b_owned (n + 3 entries, reference
+ * order of the N dofs minus nothing: indexed by reference dof) marks the b entries it writes. */
+int bos_plan_inspect(const bos_problem* problem, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
+                     int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, bos_plan_info* info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BOS_HOST_H_ */

@@ -1,0 +1,399 @@
+"""ctypes binding of libbos.so (include/bos.h, include/bos_host.h).
+
+Python mirror of the reference's host interface for the GN path
+(torchipeppo/prb-project-bearing-only-slam):
+
+* :func:`load_g2o`  — ``parse_g2o`` + default fixed pose + ``triangulate_landmarks``
+  (utils/g2o_utils.cpp:10-146, executables/bearing_only_slam.cpp:62-71,
+  slam/triangulation.cpp:65-74), implemented in C++ inside libbos.so.
+* :class:`Solver`   — ``proj02::Solver`` (slam/solver.hpp:21-92): ``step()``,
+  ``set_kernel_threshold``, ``set_damping_factor``, ``state``.
+
+There is no CPU fallback: constructing a :class:`Solver` without a visible HIP device raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbos.so")
+
+BOS_OK = 0
+BOS_FP64 = 64
+BOS_FP32 = 32
+BOS_SOLVER_SPARSE_CHOL = 0
+BOS_SOLVER_DENSE_CHOL = 1
+
+# every symbol declared in include/bos.h and include/bos_host.h
+EXPORTED_SYMBOLS = [
+    "bos_default_options", "bos_last_error", "bos_abi_version", "bos_device_count", "bos_nccl_unique_id",
+    "bos_create", "bos_destroy", "bos_set_kernel_threshold", "bos_set_damping_factor", "bos_step", "bos_step_n",
+    "bos_linearize", "bos_linearize_async", "bos_synchronize", "bos_system_info_get", "bos_export_system",
+    "bos_get_state", "bos_set_state", "bos_get_last_dx",
+    "bos_dataset_load_g2o", "bos_dataset_synthetic", "bos_dataset_problem", "bos_dataset_pose_ids",
+    "bos_dataset_landmark_ids", "bos_dataset_fixed_pose_id", "bos_dataset_bound", "bos_dataset_ground_truth",
+    "bos_dataset_write_g2o", "bos_dataset_free", "bos_plan_inspect",
+]
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+
+
+class BosError(RuntimeError):
+    pass
+
+
+class bos_problem(ctypes.Structure):
+    _fields_ = [("num_poses", ctypes.c_int32), ("num_landmarks", ctypes.c_int32),
+                ("num_bearings", ctypes.c_int32), ("num_odometry", ctypes.c_int32),
+                ("pose_xyt", _dp), ("landmark_xy", _dp), ("bearing_pose", _ip), ("bearing_landmark", _ip),
+                ("bearing_z", _dp), ("bearing_omega", _dp), ("odom_src", _ip), ("odom_dst", _ip),
+                ("odom_z", _dp), ("odom_omega", _dp), ("fixed_pose", ctypes.c_int32)]
+
+
+class bos_options(ctypes.Structure):
+    _fields_ = [("precision", ctypes.c_int32), ("solver", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32), ("nccl_unique_id", ctypes.c_void_p),
+                ("kernel_threshold", ctypes.c_double), ("damping", ctypes.c_double), ("stream", ctypes.c_void_p)]
+
+
+class bos_step_stats(ctypes.Structure):
+    _fields_ = [("chi2", ctypes.c_double), ("n_robust", ctypes.c_int32), ("solver_info", ctypes.c_int32),
+                ("max_abs_dx", ctypes.c_double), ("t_linearize_ms", ctypes.c_double),
+                ("t_exchange_ms", ctypes.c_double), ("t_solve_ms", ctypes.c_double), ("t_update_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class bos_system_info(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("nnz_lower", ctypes.c_int64), ("nnz_factor", ctypes.c_int64),
+                ("algorithmic_bytes", ctypes.c_int64), ("num_items_pose", ctypes.c_int64),
+                ("num_items_landmark", ctypes.c_int64), ("owned_first_row", ctypes.c_int32),
+                ("owned_last_row", ctypes.c_int32)]
+
+
+class bos_plan_info(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("nnz_lower", ctypes.c_int64), ("nnz_factor", ctypes.c_int64),
+                ("num_tasks_pose", ctypes.c_int64), ("num_tasks_landmark", ctypes.c_int64),
+                ("flops_temporal", ctypes.c_double), ("flops_nested_dissection", ctypes.c_double),
+                ("ordering", ctypes.c_char * 32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libbos.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BosError(f"{LIB_PATH} not built: run `make -C {_HERE}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    sig = {
+        "bos_default_options": (None, [ctypes.POINTER(bos_options)]),
+        "bos_last_error": (ctypes.c_char_p, []),
+        "bos_abi_version": (ctypes.c_int, []),
+        "bos_device_count": (ctypes.c_int, []),
+        "bos_nccl_unique_id": (ctypes.c_int, [vp, ctypes.c_int64]),
+        "bos_create": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options), ctypes.POINTER(vp)]),
+        "bos_destroy": (ctypes.c_int, [vp]),
+        "bos_set_kernel_threshold": (ctypes.c_int, [vp, ctypes.c_double]),
+        "bos_set_damping_factor": (ctypes.c_int, [vp, ctypes.c_double]),
+        "bos_step": (ctypes.c_int, [vp, ctypes.POINTER(bos_step_stats)]),
+        "bos_step_n": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(bos_step_stats)]),
+        "bos_linearize": (ctypes.c_int, [vp, ctypes.POINTER(bos_step_stats)]),
+        "bos_linearize_async": (ctypes.c_int, [vp]),
+        "bos_synchronize": (ctypes.c_int, [vp]),
+        "bos_system_info_get": (ctypes.c_int, [vp, ctypes.POINTER(bos_system_info)]),
+        "bos_export_system": (ctypes.c_int, [vp, ctypes.c_int64, _ip, _ip, _dp, _dp]),
+        "bos_get_state": (ctypes.c_int, [vp, _dp, _dp]),
+        "bos_set_state": (ctypes.c_int, [vp, _dp, _dp]),
+        "bos_get_last_dx": (ctypes.c_int, [vp, _dp]),
+        "bos_dataset_load_g2o": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
+        "bos_dataset_synthetic": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+                                                 ctypes.POINTER(vp)]),
+        "bos_dataset_problem": (ctypes.c_int, [vp, ctypes.POINTER(bos_problem)]),
+        "bos_dataset_pose_ids": (_ip, [vp]),
+        "bos_dataset_landmark_ids": (_ip, [vp]),
+        "bos_dataset_fixed_pose_id": (ctypes.c_int32, [vp]),
+        "bos_dataset_bound": (ctypes.c_float, [vp]),
+        "bos_dataset_ground_truth": (ctypes.c_int, [vp, ctypes.POINTER(_dp), ctypes.POINTER(_dp)]),
+        "bos_dataset_write_g2o": (ctypes.c_int, [vp, ctypes.c_char_p, _dp, _dp, ctypes.c_int]),
+        "bos_dataset_free": (None, [vp]),
+        "bos_plan_inspect": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int64, _ip, _ip, ctypes.POINTER(ctypes.c_uint8),
+                                            ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(bos_plan_info)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str):
+    if rc != BOS_OK:
+        raise BosError(f"{what} failed ({rc}): {lib().bos_last_error().decode()}")
+
+
+def _ptr(a, ct):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def device_count() -> int:
+    return lib().bos_device_count()
+
+
+class Problem:
+    """SoA problem in stix order (include/bos.h bos_problem). Owns its numpy arrays."""
+
+    def __init__(self, pose_xyt, lm_xy, b_pose, b_lm, b_z, o_src, o_dst, o_z, o_omega, fixed, b_omega=None,
+                 pose_ids=None, lm_ids=None):
+        self.pose_xyt = np.ascontiguousarray(pose_xyt, dtype=np.float64).reshape(-1, 3)
+        self.lm_xy = np.ascontiguousarray(lm_xy, dtype=np.float64).reshape(-1, 2)
+        self.b_pose = np.ascontiguousarray(b_pose, dtype=np.int32)
+        self.b_lm = np.ascontiguousarray(b_lm, dtype=np.int32)
+        self.b_z = np.ascontiguousarray(b_z, dtype=np.float64)
+        self.b_omega = None if b_omega is None else np.ascontiguousarray(b_omega, dtype=np.float64)
+        self.o_src = np.ascontiguousarray(o_src, dtype=np.int32)
+        self.o_dst = np.ascontiguousarray(o_dst, dtype=np.int32)
+        self.o_z = np.ascontiguousarray(o_z, dtype=np.float64).reshape(-1, 3)
+        self.o_omega = np.ascontiguousarray(o_omega, dtype=np.float64).reshape(-1, 3, 3)
+        self.fixed = int(fixed)
+        self.pose_ids = pose_ids
+        self.lm_ids = lm_ids
+
+    @property
+    def NP(self):
+        return len(self.pose_xyt)
+
+    @property
+    def NL(self):
+        return len(self.lm_xy)
+
+    @property
+    def N(self):
+        return 3 * self.NP + 2 * self.NL
+
+    def c_struct(self) -> bos_problem:
+        p = bos_problem()
+        p.num_poses, p.num_landmarks = self.NP, self.NL
+        p.num_bearings, p.num_odometry = len(self.b_z), len(self.o_z)
+        p.pose_xyt = _ptr(self.pose_xyt, ctypes.c_double)
+        p.landmark_xy = _ptr(self.lm_xy, ctypes.c_double) if self.NL else None
+        p.bearing_pose = _ptr(self.b_pose, ctypes.c_int32)
+        p.bearing_landmark = _ptr(self.b_lm, ctypes.c_int32)
+        p.bearing_z = _ptr(self.b_z, ctypes.c_double)
+        p.bearing_omega = _ptr(self.b_omega, ctypes.c_double)
+        p.odom_src = _ptr(self.o_src, ctypes.c_int32)
+        p.odom_dst = _ptr(self.o_dst, ctypes.c_int32)
+        p.odom_z = _ptr(self.o_z, ctypes.c_double)
+        p.odom_omega = _ptr(self.o_omega, ctypes.c_double)
+        p.fixed_pose = self.fixed
+        return p
+
+
+def _problem_from_dataset(h) -> Problem:
+    L = lib()
+    v = bos_problem()
+    _check(L.bos_dataset_problem(h, ctypes.byref(v)), "bos_dataset_problem")
+    NP, NL, Mb, Mo = v.num_poses, v.num_landmarks, v.num_bearings, v.num_odometry
+
+    def arr(p, n, dt):
+        if n == 0 or not p:
+            return np.zeros(0, dtype=dt)
+        return np.ctypeslib.as_array(p, shape=(n,)).astype(dt, copy=True)
+
+    pose_ids = arr(L.bos_dataset_pose_ids(h), NP, np.int32)
+    lm_ids = arr(L.bos_dataset_landmark_ids(h), NL, np.int32)
+    return Problem(arr(v.pose_xyt, 3 * NP, np.float64), arr(v.landmark_xy, 2 * NL, np.float64),
+                   arr(v.bearing_pose, Mb, np.int32), arr(v.bearing_landmark, Mb, np.int32),
+                   arr(v.bearing_z, Mb, np.float64), arr(v.odom_src, Mo, np.int32), arr(v.odom_dst, Mo, np.int32),
+                   arr(v.odom_z, 3 * Mo, np.float64), arr(v.odom_omega, 9 * Mo, np.float64), v.fixed_pose,
+                   pose_ids=pose_ids, lm_ids=lm_ids)
+
+
+def load_g2o(path: str, triangulate: bool = True, verbose: bool = False) -> Problem:
+    """parse_g2o + default FIX + triangulate_landmarks, in libbos.so's C++ host code."""
+    L = lib()
+    h = ctypes.c_void_p()
+    _check(L.bos_dataset_load_g2o(path.encode(), int(triangulate), int(verbose), ctypes.byref(h)), "load_g2o")
+    try:
+        P = _problem_from_dataset(h)
+        P.fixed_pose_id = L.bos_dataset_fixed_pose_id(h)
+        P.bound = L.bos_dataset_bound(h)
+    finally:
+        L.bos_dataset_free(h)
+    return P
+
+
+def synthetic(num_poses: int, num_landmarks: int, bearings_per_pose: int, seed: int = 0xB05EED01) -> Problem:
+    """Deterministic synthetic world; P.gt_pose_xyt / P.gt_lm_xy hold ground truth."""
+    L = lib()
+    h = ctypes.c_void_p()
+    _check(L.bos_dataset_synthetic(num_poses, num_landmarks, bearings_per_pose, seed, ctypes.byref(h)), "synthetic")
+    try:
+        P = _problem_from_dataset(h)
+        gp, gl = _dp(), _dp()
+        _check(L.bos_dataset_ground_truth(h, ctypes.byref(gp), ctypes.byref(gl)), "ground_truth")
+        P.gt_pose_xyt = np.ctypeslib.as_array(gp, shape=(3 * P.NP,)).reshape(-1, 3).copy()
+        P.gt_lm_xy = np.ctypeslib.as_array(gl, shape=(2 * P.NL,)).reshape(-1, 2).copy()
+        P.fixed_pose_id = L.bos_dataset_fixed_pose_id(h)
+    finally:
+        L.bos_dataset_free(h)
+    return P
+
+
+def write_g2o(P: Problem, path: str, pose_xyt=None, lm_xy=None, with_landmarks=True, source: Optional[str] = None):
+    """Write a problem (and optionally a state) as g2o via the C++ writer."""
+    L = lib()
+    h = ctypes.c_void_p()
+    if source is None:
+        raise BosError("write_g2o needs the source g2o path (or use bearing_only_slam --dump)")
+    _check(L.bos_dataset_load_g2o(source.encode(), 1, 0, ctypes.byref(h)), "load_g2o")
+    try:
+        pp = None if pose_xyt is None else np.ascontiguousarray(pose_xyt, dtype=np.float64)
+        ll = None if lm_xy is None else np.ascontiguousarray(lm_xy, dtype=np.float64)
+        _check(L.bos_dataset_write_g2o(h, path.encode(), _ptr(pp, ctypes.c_double), _ptr(ll, ctypes.c_double),
+                                       int(with_landmarks)), "write_g2o")
+    finally:
+        L.bos_dataset_free(h)
+
+
+def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = False):
+    """Host-only plan build (ordering, CSR layout, shard ownership) — no GPU needed."""
+    L = lib()
+    cs = P.c_struct()
+    info = bos_plan_info()
+    _check(L.bos_plan_inspect(ctypes.byref(cs), rank, world, 0, None, None, None, None, ctypes.byref(info)),
+           "plan_inspect")
+    out = {"n": info.n, "nnz_lower": info.nnz_lower, "nnz_factor": info.nnz_factor,
+           "num_tasks_pose": info.num_tasks_pose, "num_tasks_landmark": info.num_tasks_landmark,
+           "flops_temporal": info.flops_temporal, "flops_nested_dissection": info.flops_nested_dissection,
+           "ordering": info.ordering.decode()}
+    if entries:
+        nnz = info.nnz_lower
+        rows = np.zeros(nnz, dtype=np.int32)
+        cols = np.zeros(nnz, dtype=np.int32)
+        owned = np.zeros(nnz, dtype=np.uint8)
+        b_owned = np.zeros(P.N, dtype=np.uint8)
+        _check(L.bos_plan_inspect(ctypes.byref(cs), rank, world, nnz, _ptr(rows, ctypes.c_int32),
+                                  _ptr(cols, ctypes.c_int32), _ptr(owned, ctypes.c_uint8),
+                                  _ptr(b_owned, ctypes.c_uint8), None), "plan_inspect")
+        out.update(rows=rows, cols=cols, owned=owned.astype(bool), b_owned=b_owned.astype(bool))
+    return out
+
+
+def nccl_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().bos_nccl_unique_id(buf, 128), "bos_nccl_unique_id")
+    return buf.raw
+
+
+class Solver:
+    """``proj02::Solver`` over the HIP path. ``state`` is downloaded after every ``step()``."""
+
+    def __init__(self, P: Problem, precision: int = BOS_FP64, solver: int = BOS_SOLVER_SPARSE_CHOL,
+                 device: int = -1, kernel_threshold: float = 1.0, damping: float = 0.01, stream: int = 0,
+                 rank: int = 0, world_size: int = 1, nccl_id: Optional[bytes] = None):
+        L = lib()
+        self.P = P
+        opt = bos_options()
+        L.bos_default_options(ctypes.byref(opt))
+        opt.precision, opt.solver, opt.device = precision, solver, device
+        opt.kernel_threshold, opt.damping = kernel_threshold, damping
+        opt.stream = stream or None
+        opt.rank, opt.world_size = rank, world_size
+        self._nid = None
+        if nccl_id is not None:
+            self._nid = ctypes.create_string_buffer(nccl_id, len(nccl_id))
+            opt.nccl_unique_id = ctypes.cast(self._nid, ctypes.c_void_p)
+        self._h = ctypes.c_void_p()
+        cs = P.c_struct()
+        _check(L.bos_create(ctypes.byref(cs), ctypes.byref(opt), ctypes.byref(self._h)), "bos_create")
+        self.last_stats = None
+
+    def close(self):
+        if self._h:
+            lib().bos_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_kernel_threshold(self, kt: float):
+        _check(lib().bos_set_kernel_threshold(self._h, kt), "set_kernel_threshold")
+
+    def set_damping_factor(self, df: float):
+        _check(lib().bos_set_damping_factor(self._h, df), "set_damping_factor")
+
+    def step(self) -> dict:
+        st = bos_step_stats()
+        _check(lib().bos_step(self._h, ctypes.byref(st)), "bos_step")
+        self.last_stats = st.as_dict()
+        return self.last_stats
+
+    def step_n(self, n: int) -> dict:
+        st = bos_step_stats()
+        _check(lib().bos_step_n(self._h, n, ctypes.byref(st)), "bos_step_n")
+        self.last_stats = st.as_dict()
+        return self.last_stats
+
+    def linearize(self) -> dict:
+        st = bos_step_stats()
+        _check(lib().bos_linearize(self._h, ctypes.byref(st)), "bos_linearize")
+        return st.as_dict()
+
+    def linearize_async(self):
+        _check(lib().bos_linearize_async(self._h), "bos_linearize_async")
+
+    def synchronize(self):
+        _check(lib().bos_synchronize(self._h), "bos_synchronize")
+
+    def system_info(self) -> dict:
+        info = bos_system_info()
+        _check(lib().bos_system_info_get(self._h, ctypes.byref(info)), "system_info")
+        return {k: getattr(info, k) for k, _ in info._fields_}
+
+    def export_system(self):
+        """(rows, cols, vals, b): lower triangle of H_nf in reference dof numbering + full b."""
+        info = self.system_info()
+        nnz = info["nnz_lower"]
+        rows = np.zeros(nnz, dtype=np.int32)
+        cols = np.zeros(nnz, dtype=np.int32)
+        vals = np.zeros(nnz)
+        b = np.zeros(self.P.N)
+        _check(lib().bos_export_system(self._h, nnz, _ptr(rows, ctypes.c_int32), _ptr(cols, ctypes.c_int32),
+                                       _ptr(vals, ctypes.c_double), _ptr(b, ctypes.c_double)), "export_system")
+        return rows, cols, vals, b
+
+    def get_state(self):
+        pose = np.zeros((self.P.NP, 3))
+        lm = np.zeros((self.P.NL, 2))
+        _check(lib().bos_get_state(self._h, _ptr(pose, ctypes.c_double), _ptr(lm, ctypes.c_double)), "get_state")
+        return pose, lm
+
+    def set_state(self, pose_xyt, lm_xy):
+        pose = np.ascontiguousarray(pose_xyt, dtype=np.float64)
+        lm = np.ascontiguousarray(lm_xy, dtype=np.float64)
+        _check(lib().bos_set_state(self._h, _ptr(pose, ctypes.c_double), _ptr(lm, ctypes.c_double)), "set_state")
+
+    def last_dx(self):
+        dx = np.zeros(self.P.N)
+        _check(lib().bos_get_last_dx(self._h, _ptr(dx, ctypes.c_double)), "get_last_dx")
+        return dx
+
+    @property
+    def state(self):
+        return self.get_state()

@@ -1,0 +1,706 @@
+// C ABI implementation (include/bos.h): the handle owns every device buffer, the static plan
+// (host/plan.hpp), the rocSOLVER refactorization state and the RCCL communicator.
+//
+// One GN iteration (reference Solver::step, slam/solver.cpp:27-97):
+//   1. linearize_kernel          J+H build straight into the CSR of P^T H_nf P (+ damping)
+//   2. [world > 1] RCCL broadcasts of every rank's owned rows of H and b (the exchange step)
+//   3. sparse Cholesky refactorization + solve (rocSOLVER csrrf; pattern analysed once, like
+//      SimplicialLDLT::analyzePattern at solver.cpp:77-80) or dense potrf/potrs
+//   4. boxplus_kernel            left-multiplicative box-plus with dx = -x (state.cpp:69-80)
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/bos.h"
+#include "../host/bos_math.hpp"
+#include "../host/error.hpp"
+#include "../host/plan.hpp"
+#include "kernels.hpp"
+
+namespace {
+
+int fail(int code, const std::string& msg) { return bos::set_error(code, msg); }
+
+#define HIP_TRY(expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess) return fail(BOS_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define RB_TRY(expr)                                                                                   \
+    do {                                                                                               \
+        rocblas_status s_ = (expr);                                                                    \
+        if (s_ != rocblas_status_success)                                                              \
+            return fail(BOS_ERR_SOLVER, std::string(#expr) + ": " + rocblas_status_to_string(s_));     \
+    } while (0)
+#define NC_TRY(expr)                                                                                   \
+    do {                                                                                               \
+        ncclResult_t r_ = (expr);                                                                      \
+        if (r_ != ncclSuccess) return fail(BOS_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+template <typename X> int dalloc(X** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return BOS_OK;
+    HIP_TRY(hipMalloc((void**)p, count * sizeof(X)));
+    return BOS_OK;
+}
+template <typename X> int upload(X** p, const std::vector<X>& v) {
+    int rc = dalloc(p, v.size());
+    if (rc) return rc;
+    if (!v.empty()) HIP_TRY(hipMemcpy(*p, v.data(), v.size() * sizeof(X), hipMemcpyHostToDevice));
+    return BOS_OK;
+}
+
+}  // namespace
+
+struct bos_solver {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int precision = BOS_FP64;
+    int solver_kind = BOS_SOLVER_SPARSE_CHOL;
+    int rank = 0, world = 1;
+    double kt = 1.0, damping = 0.01;
+    bos::Plan plan;
+    int NP = 0, NL = 0, Mb = 0, Mo = 0;
+    bool has_w = false, has_groups = false;
+    size_t tsize = 8;   // sizeof(T)
+    // state
+    double* d_pose = nullptr;
+    double* d_lm = nullptr;
+    void* d_pc = nullptr;
+    void* d_pth = nullptr;
+    void* d_lc = nullptr;
+    // pose-centric list
+    int32_t *a_task = nullptr, *a_seg_item = nullptr, *a_seg_node = nullptr, *a_other = nullptr, *a_slot = nullptr,
+            *a_grp = nullptr;
+    void *a_z = nullptr, *a_w = nullptr;
+    // landmark-centric list
+    int32_t *b_task = nullptr, *b_seg_item = nullptr, *b_seg_node = nullptr, *b_other = nullptr, *b_slot = nullptr,
+            *b_grp = nullptr;
+    void *b_z = nullptr, *b_w = nullptr;
+    // odometry
+    int32_t *o_src = nullptr, *o_dst = nullptr;
+    void *o_z = nullptr, *o_om = nullptr;
+    // node layout
+    int32_t *p_row0 = nullptr, *p_base = nullptr, *p_bpos = nullptr, *l_row0 = nullptr, *l_base = nullptr,
+            *l_bpos = nullptr, *node_dof = nullptr;
+    // system
+    void* d_val = nullptr;      // T
+    void* d_b = nullptr;        // T, n + 3
+    double* d_val64 = nullptr;  // fp32 build: fp64 copy for the solver
+    double* d_rhs = nullptr;    // n, solution in place
+    int32_t *d_rowptr = nullptr, *d_colind = nullptr;
+    int32_t *d_Lptr = nullptr, *d_Lind = nullptr, *d_pivQ = nullptr;
+    double* d_Lval = nullptr;
+    double* d_dense = nullptr;
+    int32_t* d_info = nullptr;
+    double* d_chi_part = nullptr;
+    int32_t* d_nrob_part = nullptr;
+    double* d_chi = nullptr;
+    int32_t* d_nrob = nullptr;
+    unsigned long long* d_maxdx = nullptr;
+    rocblas_handle rb = nullptr;
+    rocsolver_rfinfo rf = nullptr;
+    bool analyzed = false;
+    ncclComm_t comm = nullptr;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    std::vector<int32_t> ref_dof;   // permuted dof -> reference dof (size n + 3)
+    bool have_dx = false;
+};
+
+namespace {
+
+template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
+    bos::dev::LinParams<T> p;
+    p.pc = (const T*)s->d_pc;
+    p.pth = (const T*)s->d_pth;
+    p.lc = (const T*)s->d_lc;
+    p.ntask_pose = s->plan.pose_list.ntask();
+    p.nblk_pose = (p.ntask_pose + bos::dev::kWavesPerBlock - 1) / bos::dev::kWavesPerBlock;
+    p.a_task = s->a_task; p.a_seg_item = s->a_seg_item; p.a_seg_node = s->a_seg_node;
+    p.a_other = s->a_other; p.a_slot = s->a_slot; p.a_grp = s->a_grp;
+    p.a_z = (const T*)s->a_z; p.a_w = (const T*)s->a_w;
+    p.ntask_lm = s->plan.lm_list.ntask();
+    p.b_task = s->b_task; p.b_seg_item = s->b_seg_item; p.b_seg_node = s->b_seg_node;
+    p.b_other = s->b_other; p.b_slot = s->b_slot; p.b_grp = s->b_grp;
+    p.b_z = (const T*)s->b_z; p.b_w = (const T*)s->b_w;
+    p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
+    p.p_row0 = s->p_row0; p.p_base = s->p_base; p.p_bpos = s->p_bpos;
+    p.l_row0 = s->l_row0; p.l_base = s->l_base; p.l_bpos = s->l_bpos;
+    p.val = (T*)s->d_val;
+    p.b = (T*)s->d_b;
+    p.chi2_part = s->d_chi_part;
+    p.nrob_part = s->d_nrob_part;
+    p.kt = (T)s->kt;
+    p.lambda = (T)s->damping;
+    return p;
+}
+
+template <typename T> bos::dev::UpdateParams<T> upd_params(const bos_solver* s) {
+    bos::dev::UpdateParams<T> u;
+    u.NP = s->NP; u.NL = s->NL; u.fixed = s->plan.fixed;
+    u.node_dof = s->node_dof;
+    u.x = s->d_rhs;
+    u.pose = s->d_pose; u.lm = s->d_lm;
+    u.pc = (T*)s->d_pc; u.pth = (T*)s->d_pth; u.lc = (T*)s->d_lc;
+    u.max_dx_bits = s->d_maxdx;
+    return u;
+}
+
+template <typename T> int upload_T(void** p, const std::vector<double>& v) {
+    std::vector<T> t(v.begin(), v.end());
+    T* d = nullptr;
+    int rc = upload(&d, t);
+    *p = d;
+    return rc;
+}
+
+int enqueue_linearize(bos_solver* s) {
+    hipError_t e;
+    if (s->precision == BOS_FP32) e = bos::dev::launch_linearize<float>(lin_params<float>(s), s->has_w, s->has_groups, s->stream);
+    else e = bos::dev::launch_linearize<double>(lin_params<double>(s), s->has_w, s->has_groups, s->stream);
+    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("linearize launch: ") + hipGetErrorString(e));
+    return BOS_OK;
+}
+
+// RCCL exchange: every rank owns a contiguous range of rows of P^T H_nf P (and of b); broadcast
+// each range from its owner so every rank holds the full system for the replicated solve.
+int enqueue_exchange(bos_solver* s) {
+    if (s->world <= 1) return BOS_OK;
+    const ncclDataType_t ty = s->precision == BOS_FP32 ? ncclFloat : ncclDouble;
+    const std::vector<int32_t>& rr = s->plan.rank_row_begin;
+    NC_TRY(ncclGroupStart());
+    for (int r = 0; r < s->world; ++r) {
+        const int64_t v0 = s->plan.rowptr[rr[r]], v1 = s->plan.rowptr[rr[r + 1]];
+        char* vb = (char*)s->d_val + v0 * s->tsize;
+        if (v1 > v0) NC_TRY(ncclBroadcast(vb, vb, (size_t)(v1 - v0), ty, r, s->comm, s->stream));
+        char* bb = (char*)s->d_b + (int64_t)rr[r] * s->tsize;
+        if (rr[r + 1] > rr[r]) NC_TRY(ncclBroadcast(bb, bb, (size_t)(rr[r + 1] - rr[r]), ty, r, s->comm, s->stream));
+    }
+    NC_TRY(ncclGroupEnd());
+    return BOS_OK;
+}
+
+int enqueue_stats(bos_solver* s) {
+    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->plan.pose_list.ntask(), s->d_chi,
+                                          s->d_nrob, s->stream));
+    if (s->world > 1) {
+        NC_TRY(ncclGroupStart());
+        NC_TRY(ncclAllReduce(s->d_chi, s->d_chi, 1, ncclDouble, ncclSum, s->comm, s->stream));
+        NC_TRY(ncclAllReduce(s->d_nrob, s->d_nrob, 1, ncclInt32, ncclSum, s->comm, s->stream));
+        NC_TRY(ncclGroupEnd());
+    }
+    return BOS_OK;
+}
+
+int enqueue_solve(bos_solver* s, bool& ran_analysis) {
+    const int64_t n = s->plan.n;
+    ran_analysis = false;
+    if (n == 0) return BOS_OK;
+    double* A = nullptr;
+    if (s->precision == BOS_FP32) {
+        HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.nnzA(), s->stream));
+        HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_b, s->d_rhs, n, s->stream));
+        A = s->d_val64;
+    } else {
+        HIP_TRY(hipMemcpyAsync(s->d_rhs, s->d_b, n * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
+        A = (double*)s->d_val;
+    }
+    const rocblas_int nn = (rocblas_int)n;
+    if (s->solver_kind == BOS_SOLVER_DENSE_CHOL) {
+        HIP_TRY(hipMemsetAsync(s->d_dense, 0, (size_t)n * n * sizeof(double), s->stream));
+        HIP_TRY(bos::dev::launch_scatter_dense(s->d_rowptr, s->d_colind, A, nn, s->d_dense, s->stream));
+        RB_TRY(rocsolver_dpotrf(s->rb, rocblas_fill_lower, nn, s->d_dense, nn, s->d_info));
+        RB_TRY(rocsolver_dpotrs(s->rb, rocblas_fill_lower, nn, 1, s->d_dense, nn, s->d_rhs, nn));
+        return BOS_OK;
+    }
+    const rocblas_int nnzA = (rocblas_int)s->plan.nnzA(), nnzT = (rocblas_int)s->plan.nnzL();
+    if (!s->analyzed) {
+        RB_TRY(rocsolver_dcsrrf_analysis(s->rb, nn, 1, nnzA, s->d_rowptr, s->d_colind, A, nnzT, s->d_Lptr, s->d_Lind,
+                                         s->d_Lval, nullptr, s->d_pivQ, s->d_rhs, nn, s->rf));
+        s->analyzed = true;
+        ran_analysis = true;
+    }
+    RB_TRY(rocsolver_dcsrrf_refactchol(s->rb, nn, nnzA, s->d_rowptr, s->d_colind, A, nnzT, s->d_Lptr, s->d_Lind,
+                                       s->d_Lval, s->d_pivQ, s->rf));
+    RB_TRY(rocsolver_dcsrrf_solve(s->rb, nn, 1, nnzT, s->d_Lptr, s->d_Lind, s->d_Lval, nullptr, s->d_pivQ, s->d_rhs,
+                                  nn, s->rf));
+    return BOS_OK;
+}
+
+int enqueue_update(bos_solver* s) {
+    HIP_TRY(hipMemsetAsync(s->d_maxdx, 0, sizeof(unsigned long long), s->stream));
+    hipError_t e = s->precision == BOS_FP32 ? bos::dev::launch_boxplus<float>(upd_params<float>(s), s->stream)
+                                            : bos::dev::launch_boxplus<double>(upd_params<double>(s), s->stream);
+    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("boxplus launch: ") + hipGetErrorString(e));
+    return BOS_OK;
+}
+
+int refresh_cache(bos_solver* s) {
+    hipError_t e = s->precision == BOS_FP32 ? bos::dev::launch_refresh_cache<float>(upd_params<float>(s), s->stream)
+                                            : bos::dev::launch_refresh_cache<double>(upd_params<double>(s), s->stream);
+    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("cache launch: ") + hipGetErrorString(e));
+    return BOS_OK;
+}
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+    return ms;
+}
+
+int read_stats(bos_solver* s, bos_step_stats* st, bool with_update, bool with_solve) {
+    double chi = 0;
+    int32_t nrob = 0, info = 0;
+    unsigned long long mdx = 0;
+    HIP_TRY(hipMemcpyAsync(&chi, s->d_chi, sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(&nrob, s->d_nrob, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    if (with_update) HIP_TRY(hipMemcpyAsync(&mdx, s->d_maxdx, sizeof(mdx), hipMemcpyDeviceToHost, s->stream));
+    if (with_solve && s->solver_kind == BOS_SOLVER_DENSE_CHOL)
+        HIP_TRY(hipMemcpyAsync(&info, s->d_info, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->chi2 = chi;
+        st->n_robust = nrob;
+        st->solver_info = info;
+        double m = 0;
+        std::memcpy(&m, &mdx, sizeof(m));
+        st->max_abs_dx = m;
+    }
+    return BOS_OK;
+}
+
+int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
+    int rc;
+    HIP_TRY(hipEventRecord(s->ev[0], s->stream));
+    if ((rc = enqueue_linearize(s))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[1], s->stream));
+    if ((rc = enqueue_exchange(s))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[2], s->stream));
+    bool analysed_now = false;
+    if ((rc = enqueue_solve(s, analysed_now))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[3], s->stream));
+    if ((rc = enqueue_update(s))) return rc;
+    if ((rc = enqueue_stats(s))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[4], s->stream));
+    s->have_dx = true;
+    if (!sync) return BOS_OK;
+    if ((rc = read_stats(s, st, true, true))) return rc;
+    if (st) {
+        st->t_linearize_ms = elapsed(s->ev[0], s->ev[2]);
+        st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
+        st->t_solve_ms = elapsed(s->ev[2], s->ev[3]);
+        st->t_update_ms = elapsed(s->ev[3], s->ev[4]);
+    }
+    return BOS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bos_abi_version(void) { return BOS_ABI_VERSION; }
+
+int bos_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void bos_default_options(bos_options* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->precision = BOS_FP64;
+    o->solver = BOS_SOLVER_SPARSE_CHOL;
+    o->device = -1;
+    o->rank = 0;
+    o->world_size = 1;
+    o->kernel_threshold = 1.0;
+    o->damping = 0.01;
+}
+
+int bos_nccl_unique_id(void* out, int64_t len) {
+    if (!out || len < (int64_t)sizeof(ncclUniqueId)) return fail(BOS_ERR_INVALID, "bos_nccl_unique_id: buffer too small");
+    ncclUniqueId id;
+    NC_TRY(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof(id));
+    return BOS_OK;
+}
+
+int bos_destroy(bos_solver* s) {
+    if (!s) return BOS_OK;
+    if (s->device >= 0) (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->a_task, s->a_seg_item, s->a_seg_node,
+                    s->a_other, s->a_slot, s->a_grp, s->a_z, s->a_w, s->b_task, s->b_seg_item, s->b_seg_node,
+                    s->b_other, s->b_slot, s->b_grp, s->b_z, s->b_w, s->o_src, s->o_dst, s->o_z, s->o_om,
+                    s->p_row0, s->p_base, s->p_bpos, s->l_row0, s->l_base, s->l_bpos, s->node_dof, s->d_val,
+                    s->d_b, s->d_val64, s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
+                    s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_chi, s->d_nrob,
+                    s->d_maxdx};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (s->rf) rocsolver_destroy_rfinfo(s->rf);
+    if (s->rb) rocblas_destroy_handle(s->rb);
+    if (s->comm) ncclCommDestroy(s->comm);
+    for (hipEvent_t& e : s->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+    return BOS_OK;
+}
+
+int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** out) {
+    if (!pb || !out) return fail(BOS_ERR_INVALID, "bos_create: null argument");
+    *out = nullptr;
+    bos_options opt;
+    bos_default_options(&opt);
+    if (opt_in) opt = *opt_in;
+    if (opt.precision != BOS_FP64 && opt.precision != BOS_FP32) return fail(BOS_ERR_INVALID, "precision must be 32 or 64");
+    if (opt.solver != BOS_SOLVER_SPARSE_CHOL && opt.solver != BOS_SOLVER_DENSE_CHOL)
+        return fail(BOS_ERR_INVALID, "unknown solver");
+    if (pb->num_poses <= 0 || pb->num_landmarks < 0 || pb->num_bearings < 0 || pb->num_odometry < 0)
+        return fail(BOS_ERR_INVALID, "bad problem sizes");
+    if (!pb->pose_xyt || (pb->num_landmarks && !pb->landmark_xy) ||
+        (pb->num_bearings && (!pb->bearing_pose || !pb->bearing_landmark || !pb->bearing_z)) ||
+        (pb->num_odometry && (!pb->odom_src || !pb->odom_dst || !pb->odom_z || !pb->odom_omega)))
+        return fail(BOS_ERR_INVALID, "null problem array");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(BOS_ERR_DEVICE, "no HIP device visible (the HIP path has no CPU fallback)");
+    if (opt.world_size > 1 && !opt.nccl_unique_id) return fail(BOS_ERR_INVALID, "world_size > 1 needs nccl_unique_id");
+
+    bos_solver* s = new bos_solver();
+    auto bail = [&](int rc) { bos_destroy(s); return rc; };
+    s->precision = opt.precision;
+    s->tsize = opt.precision == BOS_FP32 ? 4 : 8;
+    s->solver_kind = opt.solver;
+    s->rank = opt.rank;
+    s->world = opt.world_size;
+    s->kt = opt.kernel_threshold;
+    s->damping = opt.damping;
+    s->NP = pb->num_poses; s->NL = pb->num_landmarks; s->Mb = pb->num_bearings; s->Mo = pb->num_odometry;
+    if (opt.device >= 0) {
+        if (opt.device >= ndev) return bail(fail(BOS_ERR_DEVICE, "device ordinal out of range"));
+        if (hipSetDevice(opt.device) != hipSuccess) return bail(fail(BOS_ERR_DEVICE, "hipSetDevice failed"));
+        s->device = opt.device;
+    } else {
+        if (hipGetDevice(&s->device) != hipSuccess) return bail(fail(BOS_ERR_DEVICE, "hipGetDevice failed"));
+    }
+
+    // ---- static plan (host)
+    bos::ProblemIndex pi;
+    pi.NP = s->NP; pi.NL = s->NL; pi.Mb = s->Mb; pi.Mo = s->Mo; pi.fixed = pb->fixed_pose;
+    pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
+    std::string err;
+    int rc = bos::build_plan(pi, s->rank, s->world, s->solver_kind == BOS_SOLVER_SPARSE_CHOL, s->plan, err);
+    if (rc) return bail(fail(rc, "plan: " + err));
+    const bos::Plan& P = s->plan;
+    if (s->solver_kind == BOS_SOLVER_DENSE_CHOL && P.n > 40000)
+        return bail(fail(BOS_ERR_UNSUPPORTED, "dense solver limited to n <= 40000"));
+    s->has_groups = P.pose_list.has_groups || P.lm_list.has_groups;
+    s->has_w = false;
+    if (pb->bearing_omega)
+        for (int k = 0; k < s->Mb; ++k)
+            if (pb->bearing_omega[k] != 1.0) { s->has_w = true; break; }
+
+    // ---- streams / events / libraries
+    if (opt.stream) {
+        s->stream = (hipStream_t)opt.stream;
+    } else {
+        if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
+            return bail(fail(BOS_ERR_DEVICE, "hipStreamCreate failed"));
+        s->own_stream = true;
+    }
+    for (hipEvent_t& e : s->ev)
+        if (hipEventCreate(&e) != hipSuccess) return bail(fail(BOS_ERR_DEVICE, "hipEventCreate failed"));
+    if (rocblas_create_handle(&s->rb) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "rocblas_create_handle"));
+    if (rocblas_set_stream(s->rb, s->stream) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "rocblas_set_stream"));
+    if (s->solver_kind == BOS_SOLVER_SPARSE_CHOL) {
+        if (rocsolver_create_rfinfo(&s->rf, s->rb) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "create_rfinfo"));
+        if (rocsolver_set_rfinfo_mode(s->rf, rocsolver_rfinfo_mode_cholesky) != rocblas_status_success)
+            return bail(fail(BOS_ERR_SOLVER, "set_rfinfo_mode"));
+    }
+    if (s->world > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, opt.nccl_unique_id, sizeof(id));
+        ncclResult_t r = ncclCommInitRank(&s->comm, s->world, id, s->rank);
+        if (r != ncclSuccess) return bail(fail(BOS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
+    }
+
+    // ---- upload
+    const int NP = s->NP, NL = s->NL;
+    std::vector<double> pose(pb->pose_xyt, pb->pose_xyt + 3 * (size_t)NP);
+    for (int i = 0; i < NP; ++i) pose[3 * i + 2] = bos::normalized_angle<double>(bos::smallest_angle<double>(pose[3 * i + 2]));
+    std::vector<double> lm(pb->landmark_xy ? pb->landmark_xy : nullptr,
+                           pb->landmark_xy ? pb->landmark_xy + 2 * (size_t)NL : nullptr);
+    if ((rc = upload(&s->d_pose, pose)) || (rc = upload(&s->d_lm, lm))) return bail(rc);
+    const bool f32 = s->precision == BOS_FP32;
+    auto alloc_T = [&](void** p, size_t count) -> int {
+        if (f32) return dalloc((float**)p, count);
+        return dalloc((double**)p, count);
+    };
+    auto upload_Tv = [&](void** p, const std::vector<double>& v) -> int {
+        return f32 ? upload_T<float>(p, v) : upload_T<double>(p, v);
+    };
+    if ((rc = alloc_T(&s->d_pc, 4 * (size_t)NP)) || (rc = alloc_T(&s->d_pth, NP)) || (rc = alloc_T(&s->d_lc, 2 * (size_t)NL)))
+        return bail(rc);
+
+    auto up_list = [&](const bos::WorkList& W, bool pose_side, int32_t** task, int32_t** seg_item, int32_t** seg_node,
+                       int32_t** other, int32_t** slot, int32_t** grp, void** z, void** w) -> int {
+        int r;
+        if ((r = upload(task, W.task_seg)) || (r = upload(seg_item, W.seg_item)) || (r = upload(seg_node, W.seg_node)) ||
+            (r = upload(other, W.item_other)) || (r = upload(slot, W.item_slot)))
+            return r;
+        if (W.has_groups && (r = upload(grp, W.item_grp))) return r;
+        const size_t ni = W.item_other.size();
+        std::vector<double> zz(ni, 0.0), ww;
+        for (size_t i = 0; i < ni; ++i) {
+            const bool bearing = !pose_side || W.item_other[i] >= 0;
+            if (bearing) zz[i] = pb->bearing_z[W.item_obs[i]];
+        }
+        if ((r = upload_Tv(z, zz))) return r;
+        if (s->has_w) {
+            ww.assign(ni, 1.0);
+            for (size_t i = 0; i < ni; ++i) {
+                const bool bearing = !pose_side || W.item_other[i] >= 0;
+                if (bearing) ww[i] = pb->bearing_omega[W.item_obs[i]];
+            }
+            if ((r = upload_Tv(w, ww))) return r;
+        }
+        return BOS_OK;
+    };
+    if ((rc = up_list(P.pose_list, true, &s->a_task, &s->a_seg_item, &s->a_seg_node, &s->a_other, &s->a_slot, &s->a_grp,
+                      &s->a_z, &s->a_w)))
+        return bail(rc);
+    if ((rc = up_list(P.lm_list, false, &s->b_task, &s->b_seg_item, &s->b_seg_node, &s->b_other, &s->b_slot, &s->b_grp,
+                      &s->b_z, &s->b_w)))
+        return bail(rc);
+    if (s->has_groups) {   // kernels read grp for both lists when either has groups
+        if (!s->a_grp && (rc = upload(&s->a_grp, P.pose_list.item_grp))) return bail(rc);
+        if (!s->b_grp && (rc = upload(&s->b_grp, P.lm_list.item_grp))) return bail(rc);
+    }
+    {
+        std::vector<int32_t> os(pb->odom_src, pb->odom_src + s->Mo), od(pb->odom_dst, pb->odom_dst + s->Mo);
+        std::vector<double> oz(pb->odom_z, pb->odom_z + 3 * (size_t)s->Mo), om(6 * (size_t)s->Mo);
+        for (int k = 0; k < s->Mo; ++k) {
+            const double* m = pb->odom_omega + 9 * (size_t)k;
+            const double u[6] = {m[0], m[1], m[2], m[4], m[5], m[8]};
+            for (int q = 0; q < 6; ++q) om[6 * (size_t)k + q] = u[q];
+        }
+        if ((rc = upload(&s->o_src, os)) || (rc = upload(&s->o_dst, od)) || (rc = upload_Tv(&s->o_z, oz)) ||
+            (rc = upload_Tv(&s->o_om, om)))
+            return bail(rc);
+    }
+    {
+        std::vector<int32_t> pr0(NP), pba(NP), pbp(NP), lr0(NL), lba(NL), lbp(NL);
+        for (int i = 0; i < NP; ++i) { pr0[i] = P.node_row0[i]; pba[i] = P.node_base[i]; pbp[i] = P.node_dof[i]; }
+        for (int j = 0; j < NL; ++j) { lr0[j] = P.node_row0[NP + j]; lba[j] = P.node_base[NP + j]; lbp[j] = P.node_dof[NP + j]; }
+        if ((rc = upload(&s->p_row0, pr0)) || (rc = upload(&s->p_base, pba)) || (rc = upload(&s->p_bpos, pbp)) ||
+            (rc = upload(&s->l_row0, lr0)) || (rc = upload(&s->l_base, lba)) || (rc = upload(&s->l_bpos, lbp)) ||
+            (rc = upload(&s->node_dof, P.node_dof)))
+            return bail(rc);
+    }
+    if ((rc = alloc_T(&s->d_val, std::max<int64_t>(P.nnzA(), 1))) || (rc = alloc_T(&s->d_b, P.n + 3)) ||
+        (rc = dalloc(&s->d_rhs, std::max<int64_t>(P.n, 1))))
+        return bail(rc);
+    if (f32 && (rc = dalloc(&s->d_val64, std::max<int64_t>(P.nnzA(), 1)))) return bail(rc);
+    HIP_TRY(hipMemset(s->d_val, 0, std::max<int64_t>(P.nnzA(), 1) * s->tsize));
+    HIP_TRY(hipMemset(s->d_b, 0, (P.n + 3) * s->tsize));
+    if ((rc = upload(&s->d_rowptr, P.rowptr)) || (rc = upload(&s->d_colind, P.colind))) return bail(rc);
+    if (s->solver_kind == BOS_SOLVER_SPARSE_CHOL) {
+        std::vector<int32_t> piv(P.n);
+        for (int64_t i = 0; i < P.n; ++i) piv[i] = (int32_t)i;   // ordering already applied in the layout
+        if ((rc = upload(&s->d_Lptr, P.Lptr)) || (rc = upload(&s->d_Lind, P.Lind)) || (rc = upload(&s->d_pivQ, piv)) ||
+            (rc = dalloc(&s->d_Lval, std::max<int64_t>(P.nnzL(), 1))))
+            return bail(rc);
+        HIP_TRY(hipMemset(s->d_Lval, 0, std::max<int64_t>(P.nnzL(), 1) * sizeof(double)));
+    } else {
+        if ((rc = dalloc(&s->d_dense, (size_t)P.n * P.n))) return bail(rc);
+    }
+    const int nt = std::max(1, P.pose_list.ntask());
+    if ((rc = dalloc(&s->d_info, 1)) || (rc = dalloc(&s->d_chi_part, nt)) || (rc = dalloc(&s->d_nrob_part, nt)) ||
+        (rc = dalloc(&s->d_chi, 1)) || (rc = dalloc(&s->d_nrob, 1)) || (rc = dalloc(&s->d_maxdx, 1)))
+        return bail(rc);
+    HIP_TRY(hipMemset(s->d_chi_part, 0, nt * sizeof(double)));
+    HIP_TRY(hipMemset(s->d_nrob_part, 0, nt * sizeof(int32_t)));
+    HIP_TRY(hipMemset(s->d_info, 0, sizeof(int32_t)));
+    // permuted dof -> reference dof
+    s->ref_dof.assign(P.n + 3, 0);
+    for (int u = 0; u < NP + NL; ++u) {
+        const int sz = u < NP ? 3 : 2;
+        const int ref0 = u < NP ? 3 * u : 3 * NP + 2 * (u - NP);
+        for (int d = 0; d < sz; ++d) s->ref_dof[P.node_dof[u] + d] = ref0 + d;
+    }
+    if ((rc = refresh_cache(s))) return bail(rc);
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    *out = s;
+    return BOS_OK;
+}
+
+int bos_set_kernel_threshold(bos_solver* s, double kt) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    s->kt = kt;
+    return BOS_OK;
+}
+
+int bos_set_damping_factor(bos_solver* s, double df) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    s->damping = df;
+    return BOS_OK;
+}
+
+int bos_step(bos_solver* s, bos_step_stats* st) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(s->device));
+    return do_step(s, st, true);
+}
+
+int bos_step_n(bos_solver* s, int n, bos_step_stats* last) {
+    if (!s || n < 0) return fail(BOS_ERR_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(s->device));
+    for (int i = 0; i < n; ++i) {
+        int rc = do_step(s, last, i + 1 == n);
+        if (rc) return rc;
+    }
+    return BOS_OK;
+}
+
+int bos_linearize_async(bos_solver* s) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    int rc = enqueue_linearize(s);
+    if (rc) return rc;
+    return enqueue_exchange(s);
+}
+
+int bos_synchronize(bos_solver* s) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return BOS_OK;
+}
+
+int bos_linearize(bos_solver* s, bos_step_stats* st) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(s->device));
+    int rc;
+    HIP_TRY(hipEventRecord(s->ev[0], s->stream));
+    if ((rc = enqueue_linearize(s))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[1], s->stream));
+    if ((rc = enqueue_exchange(s))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[2], s->stream));
+    if ((rc = enqueue_stats(s))) return rc;
+    if ((rc = read_stats(s, st, false, false))) return rc;
+    if (st) {
+        st->t_linearize_ms = elapsed(s->ev[0], s->ev[2]);
+        st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
+    }
+    return BOS_OK;
+}
+
+int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
+    if (!s || !info) return fail(BOS_ERR_INVALID, "null argument");
+    std::memset(info, 0, sizeof(*info));
+    const bos::Plan& P = s->plan;
+    info->n = P.n;
+    info->nnz_lower = P.nnzA();
+    info->nnz_factor = P.nnzL();
+    const int64_t Mb = s->Mb, Mo = s->Mo, NP = s->NP, NL = s->NL;
+    // compulsory reads of inputs + state, one write of every output block
+    info->algorithmic_bytes = s->precision == BOS_FP32 ? 36 * Mb + 80 * Mo + 60 * NP + 32 * NL
+                                                       : 64 * Mb + 152 * Mo + 120 * NP + 64 * NL;
+    info->num_items_pose = P.pose_list.nitem();
+    info->num_items_landmark = P.lm_list.nitem();
+    info->owned_first_row = P.row_begin;
+    info->owned_last_row = P.row_end;
+    return BOS_OK;
+}
+
+int bos_export_system(const bos_solver* s, int64_t capacity, int32_t* rows, int32_t* cols, double* vals, double* b) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    const bos::Plan& P = s->plan;
+    const int64_t nnz = P.nnzA();
+    if ((rows || cols || vals) && capacity < nnz) return fail(BOS_ERR_INVALID, "export capacity < nnz_lower");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (vals) {
+        if (s->precision == BOS_FP32) {
+            std::vector<float> v(nnz);
+            if (nnz) HIP_TRY(hipMemcpy(v.data(), s->d_val, nnz * sizeof(float), hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < nnz; ++i) vals[i] = v[i];
+        } else if (nnz) {
+            HIP_TRY(hipMemcpy(vals, s->d_val, nnz * sizeof(double), hipMemcpyDeviceToHost));
+        }
+    }
+    if (rows || cols) {
+        for (int64_t r = 0; r < P.n; ++r)
+            for (int64_t e = P.rowptr[r]; e < P.rowptr[r + 1]; ++e) {
+                const int32_t a = s->ref_dof[r], c = s->ref_dof[P.colind[e]];
+                if (rows) rows[e] = std::max(a, c);
+                if (cols) cols[e] = std::min(a, c);
+            }
+    }
+    if (b) {
+        const int64_t nb = P.n + 3;
+        std::vector<double> bb(nb);
+        if (s->precision == BOS_FP32) {
+            std::vector<float> v(nb);
+            HIP_TRY(hipMemcpy(v.data(), s->d_b, nb * sizeof(float), hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < nb; ++i) bb[i] = v[i];
+        } else {
+            HIP_TRY(hipMemcpy(bb.data(), s->d_b, nb * sizeof(double), hipMemcpyDeviceToHost));
+        }
+        for (int64_t i = 0; i < nb; ++i) b[s->ref_dof[i]] = bb[i];
+    }
+    return BOS_OK;
+}
+
+int bos_get_state(const bos_solver* s, double* pose_xyt, double* landmark_xy) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (pose_xyt) HIP_TRY(hipMemcpy(pose_xyt, s->d_pose, 3 * (size_t)s->NP * sizeof(double), hipMemcpyDeviceToHost));
+    if (landmark_xy && s->NL)
+        HIP_TRY(hipMemcpy(landmark_xy, s->d_lm, 2 * (size_t)s->NL * sizeof(double), hipMemcpyDeviceToHost));
+    return BOS_OK;
+}
+
+int bos_set_state(bos_solver* s, const double* pose_xyt, const double* landmark_xy) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (pose_xyt) {
+        std::vector<double> p(pose_xyt, pose_xyt + 3 * (size_t)s->NP);
+        for (int i = 0; i < s->NP; ++i) p[3 * i + 2] = bos::normalized_angle<double>(bos::smallest_angle<double>(p[3 * i + 2]));
+        HIP_TRY(hipMemcpy(s->d_pose, p.data(), p.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    if (landmark_xy && s->NL)
+        HIP_TRY(hipMemcpy(s->d_lm, landmark_xy, 2 * (size_t)s->NL * sizeof(double), hipMemcpyHostToDevice));
+    int rc = refresh_cache(s);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return BOS_OK;
+}
+
+int bos_get_last_dx(const bos_solver* s, double* dx) {
+    if (!s || !dx) return fail(BOS_ERR_INVALID, "null argument");
+    if (!s->have_dx) return fail(BOS_ERR_INVALID, "no step has been run");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    const int64_t n = s->plan.n;
+    std::vector<double> x(n);
+    if (n) HIP_TRY(hipMemcpy(x.data(), s->d_rhs, n * sizeof(double), hipMemcpyDeviceToHost));
+    const int64_t N = n + 3;
+    for (int64_t i = 0; i < N; ++i) dx[i] = 0.0;
+    for (int64_t i = 0; i < n; ++i) dx[s->ref_dof[i]] = -x[i];
+    return BOS_OK;
+}
+
+}  // extern "C"

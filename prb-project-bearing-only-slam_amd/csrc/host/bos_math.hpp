@@ -1,0 +1,101 @@
+// Per-observation math of the GN hot path, shared by the HIP kernels (hip/linearize.hip) and the
+// host façade (proj02::Solver::error_and_jacobian). Header-only, __host__ __device__.
+//
+// Conventions (reference torchipeppo/prb-project-bearing-only-slam):
+//  - pose (x, y, theta) with R = [[c, -s], [s, c]], c = cos(theta), s = sin(theta); theta is the
+//    angle t2v() would return (framework/definitions.hpp:39-43), kept wrapped to [-pi, pi).
+//  - perturbation is left-multiplicative: X' = v2t(dx) * X (framework/state.hpp:11-13).
+#pragma once
+
+#include <cmath>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define BOS_HD __host__ __device__ __forceinline__
+#else
+#define BOS_HD inline
+#endif
+
+namespace bos {
+
+// CV_PI / CV_2PI are double constants in the reference (slam/solver_jacobians.cpp:325-333).
+constexpr double kPi = 3.1415926535897932384626433832795;
+constexpr double k2Pi = 6.283185307179586476925286766559;
+
+// Solver::normalized_angle (slam/solver_jacobians.cpp:325-333): [-pi, pi), compared in double.
+template <typename T> BOS_HD T normalized_angle(T a) {
+    while ((double)a < -kPi) a = (T)((double)a + k2Pi);
+    while ((double)a >= kPi) a = (T)((double)a - k2Pi);
+    return a;
+}
+
+// Rotation2D::smallestAngle (framework/definitions.hpp:42; slam/solver_jacobians.cpp:18).
+template <typename T> BOS_HD T smallest_angle(T a) {
+    const T two_pi = (T)k2Pi, pi = (T)kPi;
+    T t = std::fmod(a, two_pi);
+    if (t > pi) t -= two_pi;
+    else if (t < -pi) t += two_pi;
+    return t;
+}
+
+template <typename T> BOS_HD T bos_atan2(T y, T x) { return atan2(y, x); }
+#if defined(__HIPCC__) || defined(__HIP__)
+template <> BOS_HD float bos_atan2<float>(float y, float x) { return atan2f(y, x); }
+#endif
+
+// Bearing error and analytic Jacobian (slam/solver_jacobians.cpp:9-95).
+// Inputs: pose translation (px, py), cached c = cos(theta), s = sin(theta); landmark (lx, ly);
+// measured z (smallestAngle-wrapped). Outputs: e = normalized(atan2(g) - z) and
+// J = [dJ/dt_x, dJ/dt_y, dJ/dtheta, dJ/dl_x, dJ/dl_y]. Returns e.
+template <typename T>
+BOS_HD T bearing_error_jacobian(T px, T py, T c, T s, T lx, T ly, T z, T J[5]) {
+    // g = X^-1 l, Isometry inverse (R^T, -R^T t) (:32, :302)
+    const T itx = -(c * px + s * py);
+    const T ity = -(-s * px + c * py);
+    const T gx = (c * lx + s * ly) + itx;
+    const T gy = (-s * lx + c * ly) + ity;
+    const T e = normalized_angle<T>(bos_atan2<T>(gy, gx) - z);          // :15, :18
+    const T f = (T)1 / (gx * gx + gy * gy);                              // :35
+    const T a0 = f * (-gy), a1 = f * gx;                                 // :47-48
+    const T gth_x = c * ly + s * (-lx);                                  // R^T [[0,1],[-1,0]] l (:60)
+    const T gth_y = -s * ly + c * (-lx);
+    J[0] = a0 * (-c) + a1 * (s);                                         // -R^T (:59)
+    J[1] = a0 * (-s) + a1 * (-c);
+    J[2] = a0 * gth_x + a1 * gth_y;
+    J[3] = a0 * c + a1 * (-s);                                           // R^T (:64)
+    J[4] = a0 * s + a1 * c;
+    return e;
+}
+
+// Odometry error and Jacobian (slam/solver_jacobians.cpp:97-168), J row-major 3x6 with columns
+// [dx_s, dy_s, dth_s, dx_d, dy_d, dth_d]. The prediction is predict_odometry (:307-323).
+template <typename T>
+BOS_HD void odometry_error_jacobian(T xs, T ys, T ths, T cs, T ss, T xd, T yd, T thd, T z0, T z1, T z2,
+                                    T e[3], T J[18]) {
+    const T tx = xd - xs, ty = yd - ys;
+    const T p0 = cs * tx + ss * ty;                                      // R_s^T (t_d - t_s) (:319)
+    const T p1 = -ss * tx + cs * ty;
+    const T p2 = normalized_angle<T>(thd - ths);                         // :321
+    e[0] = p0 - z0;                                                      // :106
+    e[1] = p1 - z1;
+    e[2] = normalized_angle<T>(p2 - z2);                                 // :107
+    J[0] = -cs; J[1] = -ss; J[2] = -ss * xd + cs * yd;                   // :137, :139
+    J[3] = cs;  J[4] = ss;  J[5] = ss * xd - cs * yd;                    // :143, :145
+    J[6] = ss;  J[7] = -cs; J[8] = -cs * xd - ss * yd;
+    J[9] = -ss; J[10] = cs; J[11] = ss * yd + cs * xd;
+    J[12] = 0;  J[13] = 0;  J[14] = (T)-1;                               // :140
+    J[15] = 0;  J[16] = 0;  J[17] = (T)1;                                // :146
+}
+
+// Left-multiplicative box-plus (framework/state.hpp:11-13 + definitions.hpp:45-53):
+// R <- dR R, t <- dR t + dt; theta kept wrapped.
+template <typename T> BOS_HD void boxplus_pose(T& x, T& y, T& th, T dx, T dy, T dth) {
+    const T c = cos(dth), s = sin(dth);
+    const T nx = c * x - s * y + dx;
+    const T ny = s * x + c * y + dy;
+    x = nx;
+    y = ny;
+    th = normalized_angle<T>(th + dth);
+}
+
+}  // namespace bos

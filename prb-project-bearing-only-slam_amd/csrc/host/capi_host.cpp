@@ -1,0 +1,218 @@
+// Host-side C ABI (include/bos_host.h): datasets (g2o / synthetic) and plan inspection.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/bos_host.h"
+#include "g2o_utils.hpp"
+#include "plan.hpp"
+#include "synthetic.hpp"
+#include "triangulation.hpp"
+
+#include "error.hpp"
+
+namespace {
+int hfail(int code, const std::string& m) { return bos::set_error(code, m); }
+}  // namespace
+
+struct bos_dataset {
+    proj02::State state;
+    proj02::BearingObservationVector bearings;
+    proj02::OdometryObservationVector odometry;
+    int fixed_pose_id = -1;
+    float bound = 0;
+    // SoA problem view
+    std::vector<double> pose_xyt, lm_xy, b_z, o_z, o_om;
+    std::vector<int32_t> b_pose, b_lm, o_src, o_dst, pose_ids, lm_ids;
+    int32_t fixed_stix = 0;
+    bool has_gt = false;
+    std::vector<double> gt_pose, gt_lm;
+
+    int finalize() {
+        const proj02::NEPoseVector& P = state.poses_vec();
+        const proj02::LMPosVector& L = state.landmarks_vec();
+        pose_xyt.resize(3 * P.size());
+        for (size_t i = 0; i < P.size(); ++i) {
+            pose_xyt[3 * i] = P[i].x; pose_xyt[3 * i + 1] = P[i].y; pose_xyt[3 * i + 2] = P[i].theta;
+        }
+        lm_xy.resize(2 * L.size());
+        for (size_t j = 0; j < L.size(); ++j) { lm_xy[2 * j] = L[j].x; lm_xy[2 * j + 1] = L[j].y; }
+        pose_ids.assign(state.pose_ids().begin(), state.pose_ids().end());
+        lm_ids.assign(state.landmark_ids().begin(), state.landmark_ids().end());
+        try {
+            b_pose.resize(bearings.size()); b_lm.resize(bearings.size()); b_z.resize(bearings.size());
+            for (size_t k = 0; k < bearings.size(); ++k) {
+                b_pose[k] = state.pose_stix(bearings[k].get_pose_id());
+                b_lm[k] = state.landmark_stix(bearings[k].get_lm_id());
+                b_z[k] = bearings[k].get_bearing_angle();
+            }
+            o_src.resize(odometry.size()); o_dst.resize(odometry.size());
+            o_z.resize(3 * odometry.size()); o_om.resize(9 * odometry.size());
+            for (size_t k = 0; k < odometry.size(); ++k) {
+                o_src[k] = state.pose_stix(odometry[k].get_source_id());
+                o_dst[k] = state.pose_stix(odometry[k].get_dest_id());
+                const proj02::EPose z = odometry[k].get_transformation();
+                o_z[3 * k] = z.x; o_z[3 * k + 1] = z.y; o_z[3 * k + 2] = z.z;
+                const proj02::Mat3 m = odometry[k].get_omega();
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) o_om[9 * k + 3 * r + c] = m(r, c);
+            }
+            fixed_stix = state.pose_stix(fixed_pose_id);
+        } catch (const std::out_of_range&) {
+            return hfail(BOS_ERR_INVALID, "an observation or FIX references an unknown id");
+        }
+        return BOS_OK;
+    }
+};
+
+extern "C" {
+
+int bos_dataset_load_g2o(const char* path, int triangulate, int verbose, bos_dataset** out) {
+    if (!path || !out) return hfail(BOS_ERR_INVALID, "null argument");
+    *out = nullptr;
+    bos_dataset* d = new bos_dataset();
+    const int rc = proj02::parse_g2o(path, d->state, d->bearings, d->odometry, d->fixed_pose_id, d->bound);
+    if (rc) { delete d; return hfail(BOS_ERR_IO, rc == -1 ? "cannot open g2o file" : "malformed g2o line"); }
+    if (d->state.number_of_poses() == 0) { delete d; return hfail(BOS_ERR_INVALID, "no poses"); }
+    if (d->fixed_pose_id < 0) d->fixed_pose_id = d->state.default_pose_id();   // bearing_only_slam.cpp:63-65
+    if (triangulate) proj02::triangulate_landmarks(d->state, d->bearings, verbose != 0);
+    const int r2 = d->finalize();
+    if (r2) { delete d; return r2; }
+    *out = d;
+    return BOS_OK;
+}
+
+int bos_dataset_synthetic(int32_t num_poses, int32_t num_landmarks, int32_t bearings_per_pose, uint64_t seed,
+                          bos_dataset** out) {
+    if (!out) return hfail(BOS_ERR_INVALID, "null argument");
+    *out = nullptr;
+    proj02::SyntheticParams p;
+    p.num_poses = num_poses;
+    p.num_landmarks = num_landmarks;
+    p.bearings_per_pose = bearings_per_pose;
+    p.seed = seed;
+    proj02::SyntheticWorld w;
+    if (!proj02::make_synthetic(p, w)) return hfail(BOS_ERR_INVALID, "infeasible synthetic sizes");
+    bos_dataset* d = new bos_dataset();
+    d->state = w.initial_guess;
+    d->bearings = std::move(w.bearings);
+    d->odometry = std::move(w.odometry);
+    d->fixed_pose_id = w.fixed_pose_id;
+    proj02::triangulate_landmarks(d->state, d->bearings, false);
+    const int rc = d->finalize();
+    if (rc) { delete d; return rc; }
+    // ground truth in the same stix order (landmark ids ascending in both states)
+    d->has_gt = true;
+    for (const proj02::NEPose& q : w.ground_truth.poses_vec()) {
+        d->gt_pose.push_back(q.x); d->gt_pose.push_back(q.y); d->gt_pose.push_back(q.theta);
+    }
+    d->gt_lm.resize(2 * d->lm_ids.size());
+    for (size_t j = 0; j < d->lm_ids.size(); ++j) {
+        const proj02::LMPos l = w.ground_truth.get_landmark_by_id(d->lm_ids[j]);
+        d->gt_lm[2 * j] = l.x; d->gt_lm[2 * j + 1] = l.y;
+    }
+    double b = 0;
+    for (double v : d->gt_pose) b = std::max(b, std::fabs(v));
+    d->bound = (float)b + 3.0f;
+    *out = d;
+    return BOS_OK;
+}
+
+int bos_dataset_problem(const bos_dataset* d, bos_problem* v) {
+    if (!d || !v) return hfail(BOS_ERR_INVALID, "null argument");
+    std::memset(v, 0, sizeof(*v));
+    v->num_poses = (int32_t)d->pose_ids.size();
+    v->num_landmarks = (int32_t)d->lm_ids.size();
+    v->num_bearings = (int32_t)d->b_pose.size();
+    v->num_odometry = (int32_t)d->o_src.size();
+    v->pose_xyt = d->pose_xyt.data();
+    v->landmark_xy = d->lm_xy.empty() ? nullptr : d->lm_xy.data();
+    v->bearing_pose = d->b_pose.data();
+    v->bearing_landmark = d->b_lm.data();
+    v->bearing_z = d->b_z.data();
+    v->bearing_omega = nullptr;
+    v->odom_src = d->o_src.data();
+    v->odom_dst = d->o_dst.data();
+    v->odom_z = d->o_z.data();
+    v->odom_omega = d->o_om.data();
+    v->fixed_pose = d->fixed_stix;
+    return BOS_OK;
+}
+
+const int32_t* bos_dataset_pose_ids(const bos_dataset* d) { return d ? d->pose_ids.data() : nullptr; }
+const int32_t* bos_dataset_landmark_ids(const bos_dataset* d) { return d ? d->lm_ids.data() : nullptr; }
+int32_t bos_dataset_fixed_pose_id(const bos_dataset* d) { return d ? d->fixed_pose_id : -1; }
+float bos_dataset_bound(const bos_dataset* d) { return d ? d->bound : 0.f; }
+
+int bos_dataset_ground_truth(const bos_dataset* d, const double** pose_xyt, const double** landmark_xy) {
+    if (!d || !d->has_gt) return hfail(BOS_ERR_INVALID, "no ground truth");
+    if (pose_xyt) *pose_xyt = d->gt_pose.data();
+    if (landmark_xy) *landmark_xy = d->gt_lm.data();
+    return BOS_OK;
+}
+
+int bos_dataset_write_g2o(const bos_dataset* d, const char* path, const double* pose_xyt, const double* landmark_xy,
+                          int with_landmarks) {
+    if (!d || !path) return hfail(BOS_ERR_INVALID, "null argument");
+    proj02::State st((int)d->pose_ids.size(), (int)d->lm_ids.size());
+    const double* P = pose_xyt ? pose_xyt : d->pose_xyt.data();
+    const double* L = landmark_xy ? landmark_xy : d->lm_xy.data();
+    for (size_t i = 0; i < d->pose_ids.size(); ++i) st.add_pose(P[3 * i], P[3 * i + 1], P[3 * i + 2], d->pose_ids[i]);
+    for (size_t j = 0; j < d->lm_ids.size(); ++j) st.add_landmark(L[2 * j], L[2 * j + 1], d->lm_ids[j]);
+    if (proj02::write_g2o(path, st, d->bearings, d->odometry, d->fixed_pose_id, with_landmarks != 0))
+        return hfail(BOS_ERR_IO, "cannot write g2o file");
+    return BOS_OK;
+}
+
+void bos_dataset_free(bos_dataset* d) { delete d; }
+
+int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
+                     int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, bos_plan_info* info) {
+    if (!pb) return hfail(BOS_ERR_INVALID, "null problem");
+    bos::ProblemIndex pi;
+    pi.NP = pb->num_poses; pi.NL = pb->num_landmarks; pi.Mb = pb->num_bearings; pi.Mo = pb->num_odometry;
+    pi.fixed = pb->fixed_pose;
+    pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
+    bos::Plan P;
+    std::string err;
+    const int rc = bos::build_plan(pi, rank, world, true, P, err);
+    if (rc) return hfail(rc, err);
+    const int NP = pi.NP;
+    std::vector<int32_t> ref(P.n + 3);
+    for (int u = 0; u < pi.NP + pi.NL; ++u) {
+        const int sz = u < NP ? 3 : 2;
+        const int r0 = u < NP ? 3 * u : 3 * NP + 2 * (u - NP);
+        for (int d = 0; d < sz; ++d) ref[P.node_dof[u] + d] = r0 + d;
+    }
+    if (info) {
+        std::memset(info, 0, sizeof(*info));
+        info->n = P.n;
+        info->nnz_lower = P.nnzA();
+        info->nnz_factor = P.nnzL();
+        info->num_tasks_pose = P.pose_list.ntask();
+        info->num_tasks_landmark = P.lm_list.ntask();
+        info->flops_temporal = P.ordering.flops_temporal;
+        info->flops_nested_dissection = P.ordering.flops_nd;
+        std::strncpy(info->ordering, P.ordering.chosen.c_str(), sizeof(info->ordering) - 1);
+    }
+    if (ref_rows || ref_cols || owned) {
+        if (capacity < P.nnzA()) return hfail(BOS_ERR_INVALID, "capacity < nnz_lower");
+        for (int64_t r = 0; r < P.n; ++r)
+            for (int64_t e = P.rowptr[r]; e < P.rowptr[r + 1]; ++e) {
+                const int32_t a = ref[r], c = ref[P.colind[e]];
+                if (ref_rows) ref_rows[e] = std::max(a, c);
+                if (ref_cols) ref_cols[e] = std::min(a, c);
+                if (owned) owned[e] = (r >= P.row_begin && r < P.row_end) ? 1 : 0;
+            }
+    }
+    if (b_owned) {
+        for (int64_t i = 0; i < P.n + 3; ++i)
+            b_owned[ref[i]] = (i >= P.row_begin && i < P.row_end) || (i >= P.n && rank == world - 1) ? 1 : 0;
+    }
+    return BOS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,651 @@
+#include "plan.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <numeric>
+
+#include "../../../include/bos.h"
+
+namespace bos {
+
+namespace {
+
+constexpr int kWave = 64;             // wavefront width on CDNA4
+constexpr int kMaxPoseSegs = 7;       // 7 poses x 9 reduced values <= 64 lanes (one pass)
+constexpr int kMaxLmSegs = 12;        // 12 landmarks x 5 reduced values <= 64 lanes
+
+inline int node_size(int u, int NP) { return u < NP ? 3 : 2; }
+
+struct Graph {
+    int n = 0;
+    std::vector<int64_t> ptr;
+    std::vector<int32_t> adj;
+};
+
+// Node-level adjacency of H_nf (symmetric, no self loops, the fixed pose has no edges).
+Graph build_graph(const ProblemIndex& pi) {
+    Graph g;
+    g.n = pi.NP + pi.NL;
+    std::vector<int64_t> deg(g.n + 1, 0);
+    auto each_edge = [&](auto&& f) {
+        for (int k = 0; k < pi.Mb; ++k) {
+            const int p = pi.b_pose[k];
+            if (p == pi.fixed) continue;
+            f(p, pi.NP + pi.b_lm[k]);
+        }
+        for (int k = 0; k < pi.Mo; ++k) {
+            const int s = pi.o_src[k], d = pi.o_dst[k];
+            if (s == d || s == pi.fixed || d == pi.fixed) continue;
+            f(s, d);
+        }
+    };
+    each_edge([&](int a, int b) { ++deg[a]; ++deg[b]; });
+    g.ptr.assign(g.n + 1, 0);
+    for (int u = 0; u < g.n; ++u) g.ptr[u + 1] = g.ptr[u] + deg[u];
+    g.adj.resize(g.ptr[g.n]);
+    std::vector<int64_t> fill(g.ptr.begin(), g.ptr.end() - 1);
+    each_edge([&](int a, int b) { g.adj[fill[a]++] = b; g.adj[fill[b]++] = a; });
+    // sort + unique each list, compact
+    std::vector<int64_t> nptr(g.n + 1, 0);
+    int64_t w = 0;
+    for (int u = 0; u < g.n; ++u) {
+        const int64_t b = g.ptr[u], e = g.ptr[u + 1];
+        std::sort(g.adj.begin() + b, g.adj.begin() + e);
+        nptr[u] = w;
+        int32_t last = -1;
+        for (int64_t i = b; i < e; ++i) {
+            if (g.adj[i] == last) continue;
+            last = g.adj[i];
+            g.adj[w++] = last;
+        }
+    }
+    nptr[g.n] = w;
+    g.adj.resize(w);
+    g.ptr.swap(nptr);
+    return g;
+}
+
+struct SymbCost {
+    int64_t nnz = 0;     // scalar entries of L (lower incl. diagonal)
+    double flops = 0;    // ~ sum over columns of (scalar column count)^2
+};
+
+// Elimination tree + row structures (Liu / ereach) for the node ordering inv (position -> node).
+// If rows_ptr/rows is given, stores the node-level row structures (positions, sorted).
+SymbCost symbolic(const Graph& g, int NP, const std::vector<int32_t>& pos, const std::vector<int32_t>& inv,
+                  std::vector<int64_t>* rows_ptr, std::vector<int32_t>* rows) {
+    const int m = (int)inv.size();
+    std::vector<int32_t> parent(m, -1), anc(m, -1);
+    for (int i = 0; i < m; ++i) {
+        const int u = inv[i];
+        for (int64_t e = g.ptr[u]; e < g.ptr[u + 1]; ++e) {
+            int r = pos[g.adj[e]];
+            if (r < 0 || r >= i) continue;
+            while (anc[r] != -1 && anc[r] != i) {
+                const int t = anc[r];
+                anc[r] = i;
+                r = t;
+            }
+            if (anc[r] == -1) { anc[r] = i; parent[r] = i; }
+        }
+    }
+    std::vector<int32_t> mark(m, -1);
+    std::vector<int64_t> colcnt(m, 0);
+    SymbCost c;
+    if (rows_ptr) { rows_ptr->assign(m + 1, 0); rows->clear(); }
+    std::vector<int32_t> row;
+    for (int i = 0; i < m; ++i) {
+        const int u = inv[i];
+        const int su = node_size(u, NP);
+        mark[i] = i;
+        row.clear();
+        int64_t rowW = 0;
+        for (int64_t e = g.ptr[u]; e < g.ptr[u + 1]; ++e) {
+            int j = pos[g.adj[e]];
+            if (j < 0 || j >= i) continue;
+            while (mark[j] != i) {
+                mark[j] = i;
+                row.push_back(j);
+                rowW += node_size(inv[j], NP);
+                colcnt[j] += su;
+                j = parent[j];
+            }
+        }
+        c.nnz += su * rowW + su * (su + 1) / 2;
+        if (rows_ptr) {
+            std::sort(row.begin(), row.end());
+            rows->insert(rows->end(), row.begin(), row.end());
+            (*rows_ptr)[i + 1] = (int64_t)rows->size();
+        }
+    }
+    for (int j = 0; j < m; ++j) {
+        const double s = node_size(inv[j], NP);
+        const double cc = (double)colcnt[j] + s;
+        c.flops += s * cc * cc;
+    }
+    return c;
+}
+
+// Nested dissection with BFS level-structure vertex separators (graph-based, no coordinates).
+void nested_dissection(const Graph& g, const std::vector<char>& active, std::vector<int32_t>& order, int leaf) {
+    const int n = g.n;
+    std::vector<int32_t> stamp(n, -1), level(n, -1);
+    int next_stamp = 0;
+    struct Job { std::vector<int32_t> nodes; bool emit; };
+    std::vector<Job> stack;
+    {
+        Job root;
+        for (int u = 0; u < n; ++u) if (active[u]) root.nodes.push_back(u);
+        root.emit = false;
+        stack.push_back(std::move(root));
+    }
+    std::vector<int32_t> queue;
+    auto bfs = [&](int src, int st, std::vector<int32_t>& out, int& depth) {
+        // BFS restricted to nodes with stamp == st; level[] valid for visited nodes
+        out.clear();
+        out.push_back(src);
+        level[src] = 0;
+        stamp[src] = st + 1;   // visited marker (st + 1), reset by the caller
+        size_t h = 0;
+        depth = 0;
+        while (h < out.size()) {
+            const int v = out[h++];
+            depth = std::max(depth, (int)level[v]);
+            for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
+                const int w = g.adj[e];
+                if (stamp[w] != st) continue;
+                stamp[w] = st + 1;
+                level[w] = level[v] + 1;
+                out.push_back(w);
+            }
+        }
+        for (int v : out) stamp[v] = st;
+    };
+    std::vector<int32_t> comp, tmp;
+    while (!stack.empty()) {
+        Job job = std::move(stack.back());
+        stack.pop_back();
+        if (job.emit || (int)job.nodes.size() <= leaf) {
+            order.insert(order.end(), job.nodes.begin(), job.nodes.end());
+            continue;
+        }
+        const int st = next_stamp;
+        next_stamp += 2;
+        for (int v : job.nodes) stamp[v] = st;
+        // connected components
+        std::vector<std::vector<int32_t>> comps;
+        for (int v : job.nodes) {
+            if (stamp[v] != st) continue;
+            int d;
+            bfs(v, st, comp, d);
+            for (int w : comp) stamp[w] = st + 1;   // retire this component
+            comps.push_back(comp);
+        }
+        if (comps.size() > 1) {
+            for (auto& c : comps) stack.push_back(Job{std::move(c), false});
+            continue;
+        }
+        std::vector<int32_t>& C = comps[0];
+        for (int v : C) stamp[v] = st;
+        // pseudo-peripheral start node
+        int start = C[0];
+        for (int v : C)
+            if (g.ptr[v + 1] - g.ptr[v] < g.ptr[start + 1] - g.ptr[start]) start = v;
+        int depth = 0, best_depth = -1;
+        for (int it = 0; it < 6; ++it) {
+            bfs(start, st, tmp, depth);
+            if (depth <= best_depth) break;
+            best_depth = depth;
+            int cand = tmp.back();
+            for (int v : tmp)
+                if (level[v] == depth && g.ptr[v + 1] - g.ptr[v] < g.ptr[cand + 1] - g.ptr[cand]) cand = v;
+            start = cand;
+        }
+        bfs(start, st, tmp, depth);
+        const int h = depth + 1;
+        if (h <= 2) {   // no useful level separator
+            order.insert(order.end(), tmp.begin(), tmp.end());
+            continue;
+        }
+        std::vector<int64_t> cnt(h, 0);
+        for (int v : tmp) ++cnt[level[v]];
+        std::vector<int64_t> cum(h, 0);
+        for (int k = 0; k < h; ++k) cum[k] = cnt[k] + (k ? cum[k - 1] : 0);
+        const int64_t tot = (int64_t)tmp.size();
+        int bestk = -1;
+        for (int k = 1; k + 1 < h; ++k) {
+            const int64_t below = cum[k - 1], above = tot - cum[k];
+            if (below * 5 < tot || above * 5 < tot) continue;
+            if (bestk < 0 || cnt[k] < cnt[bestk]) bestk = k;
+        }
+        if (bestk < 0) {
+            bestk = 1;
+            while (bestk + 1 < h - 1 && cum[bestk] * 2 < tot) ++bestk;
+        }
+        std::vector<int32_t> lower, upper, sep;
+        for (int v : tmp) {
+            const int lv = level[v];
+            if (lv < bestk) lower.push_back(v);
+            else if (lv > bestk) upper.push_back(v);
+            else {
+                bool up = false;
+                for (int64_t e = g.ptr[v]; e < g.ptr[v + 1] && !up; ++e) {
+                    const int w = g.adj[e];
+                    up = stamp[w] == st && level[w] == bestk + 1;
+                }
+                (up ? sep : lower).push_back(v);
+            }
+        }
+        stack.push_back(Job{std::move(sep), true});
+        stack.push_back(Job{std::move(upper), false});
+        stack.push_back(Job{std::move(lower), false});
+    }
+}
+
+}  // namespace
+
+int order_nodes(const ProblemIndex& pi, std::vector<int32_t>& node_pos, OrderingReport& rep, std::string& err) {
+    const int NP = pi.NP, NL = pi.NL, n = NP + NL;
+    const Graph g = build_graph(pi);
+    // last pose observing each landmark (temporal key)
+    std::vector<int32_t> last_obs(NL, -1);
+    for (int k = 0; k < pi.Mb; ++k) last_obs[pi.b_lm[k]] = std::max(last_obs[pi.b_lm[k]], pi.b_pose[k]);
+    auto order_to_pos = [&](const std::vector<int32_t>& order, std::vector<int32_t>& pos) {
+        pos.assign(n, -1);
+        for (size_t i = 0; i < order.size(); ++i) pos[order[i]] = (int32_t)i;
+    };
+    std::vector<int32_t> active_nodes;
+    for (int u = 0; u < n; ++u) if (u != pi.fixed) active_nodes.push_back(u);
+
+    // candidate 1: temporal — poses in file order, each landmark right after its last observer
+    std::vector<int32_t> ord_t = active_nodes;
+    auto tkey = [&](int u) -> int64_t {
+        if (u < NP) return 2LL * u;
+        return 2LL * std::max(0, (int)last_obs[u - NP]) + 1;
+    };
+    std::stable_sort(ord_t.begin(), ord_t.end(), [&](int a, int b) { return tkey(a) < tkey(b); });
+    // candidate 2: landmarks first (the Schur-complement order), then poses in file order
+    std::vector<int32_t> ord_s;
+    for (int u = NP; u < n; ++u) ord_s.push_back(u);
+    for (int u = 0; u < NP; ++u) if (u != pi.fixed) ord_s.push_back(u);
+    // candidate 3: nested dissection
+    std::vector<char> active(n, 1);
+    if (pi.fixed >= 0) active[pi.fixed] = 0;
+    std::vector<int32_t> ord_n;
+    nested_dissection(g, active, ord_n, 64);
+    if (ord_n.size() != active_nodes.size()) { err = "nested dissection lost nodes"; return BOS_ERR_INVALID; }
+
+    struct Cand { const char* name; std::vector<int32_t>* ord; SymbCost c; };
+    Cand cands[3] = {{"temporal", &ord_t, {}}, {"landmarks-first", &ord_s, {}}, {"nested-dissection", &ord_n, {}}};
+    int best = 0;
+    std::vector<int32_t> pos;
+    for (int c = 0; c < 3; ++c) {
+        order_to_pos(*cands[c].ord, pos);
+        cands[c].c = symbolic(g, NP, pos, *cands[c].ord, nullptr, nullptr);
+        if (cands[c].c.flops < cands[best].c.flops) best = c;
+    }
+    rep.flops_temporal = cands[0].c.flops;
+    rep.nnz_temporal = cands[0].c.nnz;
+    rep.flops_nd = cands[2].c.flops;
+    rep.nnz_nd = cands[2].c.nnz;
+    rep.chosen = cands[best].name;
+    order_to_pos(*cands[best].ord, node_pos);
+    return BOS_OK;
+}
+
+int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err);
+
+int build_plan(const ProblemIndex& pi, int rank, int world, bool want_factor, Plan& P, std::string& err) {
+    const int NP = pi.NP, NL = pi.NL, n_nodes = NP + NL;
+    if (NP <= 0) { err = "no poses"; return BOS_ERR_INVALID; }
+    if (pi.fixed < 0 || pi.fixed >= NP) { err = "fixed pose stix out of range"; return BOS_ERR_INVALID; }
+    if (world < 1 || rank < 0 || rank >= world) { err = "bad rank/world_size"; return BOS_ERR_INVALID; }
+    for (int k = 0; k < pi.Mb; ++k)
+        if (pi.b_pose[k] < 0 || pi.b_pose[k] >= NP || pi.b_lm[k] < 0 || pi.b_lm[k] >= NL) {
+            err = "bearing " + std::to_string(k) + " references an unknown pose/landmark stix";
+            return BOS_ERR_INVALID;
+        }
+    for (int k = 0; k < pi.Mo; ++k) {
+        if (pi.o_src[k] < 0 || pi.o_src[k] >= NP || pi.o_dst[k] < 0 || pi.o_dst[k] >= NP) {
+            err = "odometry edge " + std::to_string(k) + " references an unknown pose stix";
+            return BOS_ERR_INVALID;
+        }
+        if (pi.o_src[k] == pi.o_dst[k]) {
+            err = "odometry edge " + std::to_string(k) + " is a self loop (not supported)";
+            return BOS_ERR_UNSUPPORTED;
+        }
+    }
+    P = Plan();
+    P.NP = NP; P.NL = NL; P.Mb = pi.Mb; P.Mo = pi.Mo; P.fixed = pi.fixed;
+    int rc = order_nodes(pi, P.node_pos, P.ordering, err);
+    if (rc) return rc;
+    const Graph g = build_graph(pi);
+    const int m = n_nodes - 1;
+    std::vector<int32_t> inv(m);
+    for (int u = 0; u < n_nodes; ++u) if (P.node_pos[u] >= 0) inv[P.node_pos[u]] = u;
+
+    // dof offsets in elimination order
+    P.node_dof.assign(n_nodes, 0);
+    int64_t dof = 0;
+    for (int i = 0; i < m; ++i) { P.node_dof[inv[i]] = (int32_t)dof; dof += node_size(inv[i], NP); }
+    P.n = dof;
+    P.node_dof[pi.fixed] = (int32_t)dof;
+    if (dof + 3 > INT32_MAX) { err = "system too large for 32-bit indices"; return BOS_ERR_UNSUPPORTED; }
+
+    // lower neighbours (by position) of every node, with their offsets inside the node's rows
+    std::vector<int64_t> lptr(n_nodes + 1, 0);
+    std::vector<int32_t> lnb;              // neighbour node ids, sorted by position
+    std::vector<int32_t> loff;             // entry offset of that neighbour's block in each row
+    lnb.reserve(g.adj.size() / 2 + 1);
+    P.node_base.assign(n_nodes, -1);
+    P.node_row0.assign(n_nodes, -1);
+    P.rowptr.assign(P.n + 1, 0);
+    for (int i = 0; i < m; ++i) {
+        const int u = inv[i];
+        std::vector<int32_t> nb;
+        for (int64_t e = g.ptr[u]; e < g.ptr[u + 1]; ++e)
+            if (P.node_pos[g.adj[e]] < i) nb.push_back(g.adj[e]);
+        std::sort(nb.begin(), nb.end(), [&](int a, int b) { return P.node_pos[a] < P.node_pos[b]; });
+        lptr[u] = (int64_t)lnb.size();
+        int32_t off = 0;
+        for (int v : nb) { lnb.push_back(v); loff.push_back(off); off += node_size(v, NP); }
+        P.node_base[u] = off;
+        const int su = node_size(u, NP);
+        const int64_t r0 = P.node_dof[u];
+        for (int d = 0; d < su; ++d) P.rowptr[r0 + d + 1] = off + d + 1;   // row lengths for now
+    }
+    // per-node end pointers for lookups
+    std::vector<int64_t> lend(n_nodes, 0);
+    for (int i = 0; i < m; ++i) {
+        const int u = inv[i];
+        lend[u] = (i + 1 < m) ? lptr[inv[i + 1]] : (int64_t)lnb.size();
+    }
+    for (int64_t r = 0; r < P.n; ++r) P.rowptr[r + 1] += P.rowptr[r];
+    if (P.rowptr[P.n] > INT32_MAX) { err = "H has too many entries for 32-bit indices"; return BOS_ERR_UNSUPPORTED; }
+    P.colind.resize(P.rowptr[P.n]);
+    for (int i = 0; i < m; ++i) {
+        const int u = inv[i];
+        const int su = node_size(u, NP);
+        const int64_t r0 = P.node_dof[u];
+        P.node_row0[u] = P.rowptr[r0];
+        for (int d = 0; d < su; ++d) {
+            int64_t w = P.rowptr[r0 + d];
+            for (int64_t e = lptr[u]; e < lend[u]; ++e) {
+                const int v = lnb[e];
+                for (int c = 0; c < node_size(v, NP); ++c) P.colind[w++] = P.node_dof[v] + c;
+            }
+            for (int c = 0; c <= d; ++c) P.colind[w++] = (int32_t)(r0 + c);
+        }
+    }
+    auto block_offset = [&](int owner, int other) -> int32_t {
+        // offset of other's block inside owner's rows (binary search by position)
+        int64_t lo = lptr[owner], hi = lend[owner];
+        const int key = P.node_pos[other];
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (P.node_pos[lnb[mid]] < key) lo = mid + 1; else hi = mid;
+        }
+        return (lo < lend[owner] && lnb[lo] == other) ? loff[lo] : -1;
+    };
+
+    // symbolic Cholesky factor, scalar CSR (lower incl. diagonal)
+    if (want_factor) {
+        std::vector<int64_t> rptr;
+        std::vector<int32_t> rows;
+        symbolic(g, NP, P.node_pos, inv, &rptr, &rows);
+        P.Lptr.assign(P.n + 1, 0);
+        for (int i = 0; i < m; ++i) {
+            const int u = inv[i];
+            int64_t W = 0;
+            for (int64_t e = rptr[i]; e < rptr[i + 1]; ++e) W += node_size(inv[rows[e]], NP);
+            for (int d = 0; d < node_size(u, NP); ++d) P.Lptr[P.node_dof[u] + d + 1] = W + d + 1;
+        }
+        for (int64_t r = 0; r < P.n; ++r) P.Lptr[r + 1] += P.Lptr[r];
+        if (P.Lptr[P.n] > INT32_MAX) { err = "Cholesky factor exceeds 32-bit indices"; return BOS_ERR_UNSUPPORTED; }
+        P.Lind.resize(P.Lptr[P.n]);
+        for (int i = 0; i < m; ++i) {
+            const int u = inv[i];
+            for (int d = 0; d < node_size(u, NP); ++d) {
+                int64_t w = P.Lptr[P.node_dof[u] + d];
+                for (int64_t e = rptr[i]; e < rptr[i + 1]; ++e) {
+                    const int v = inv[rows[e]];
+                    for (int c = 0; c < node_size(v, NP); ++c) P.Lind[w++] = P.node_dof[v] + c;
+                }
+                for (int c = 0; c <= d; ++c) P.Lind[w++] = P.node_dof[u] + c;
+            }
+        }
+    }
+
+    // incidence lists
+    std::vector<int32_t> pb_ptr(NP + 1, 0), lb_ptr(NL + 1, 0), po_ptr(NP + 1, 0);
+    for (int k = 0; k < pi.Mb; ++k) { ++pb_ptr[pi.b_pose[k] + 1]; ++lb_ptr[pi.b_lm[k] + 1]; }
+    for (int k = 0; k < pi.Mo; ++k) { ++po_ptr[pi.o_src[k] + 1]; ++po_ptr[pi.o_dst[k] + 1]; }
+    for (int i = 0; i < NP; ++i) { pb_ptr[i + 1] += pb_ptr[i]; po_ptr[i + 1] += po_ptr[i]; }
+    for (int j = 0; j < NL; ++j) lb_ptr[j + 1] += lb_ptr[j];
+    std::vector<int32_t> pb(pi.Mb), lb(pi.Mb), po(2 * (size_t)pi.Mo);
+    {
+        std::vector<int32_t> a(pb_ptr.begin(), pb_ptr.end() - 1), b(lb_ptr.begin(), lb_ptr.end() - 1),
+            c(po_ptr.begin(), po_ptr.end() - 1);
+        for (int k = 0; k < pi.Mb; ++k) { pb[a[pi.b_pose[k]]++] = k; lb[b[pi.b_lm[k]]++] = k; }
+        for (int k = 0; k < pi.Mo; ++k) { po[c[pi.o_src[k]]++] = 2 * k; po[c[pi.o_dst[k]]++] = 2 * k + 1; }
+    }
+
+    // ownership: contiguous position ranges balanced by work (incident items)
+    std::vector<int64_t> work(m);
+    int64_t total = 0;
+    for (int i = 0; i < m; ++i) {
+        const int u = inv[i];
+        work[i] = 1 + (u < NP ? (pb_ptr[u + 1] - pb_ptr[u]) + (po_ptr[u + 1] - po_ptr[u]) : (lb_ptr[u - NP + 1] - lb_ptr[u - NP]));
+        total += work[i];
+    }
+    std::vector<int32_t> cut(world + 1, 0);
+    {
+        int64_t acc = 0;
+        int r = 1;
+        for (int i = 0; i < m && r < world; ++i) {
+            acc += work[i];
+            while (r < world && acc * world >= total * r) cut[r++] = i + 1;
+        }
+        while (r < world) cut[r++] = m;
+        cut[world] = m;
+    }
+    P.rank_row_begin.assign(world + 1, 0);
+    for (int r = 0; r <= world; ++r) P.rank_row_begin[r] = cut[r] < m ? P.node_dof[inv[cut[r]]] : (int32_t)P.n;
+    P.row_begin = P.rank_row_begin[rank];
+    P.row_end = P.rank_row_begin[rank + 1];
+    P.val_begin = P.rowptr[P.row_begin];
+    P.val_end = P.rowptr[P.row_end];
+
+    // work lists
+    auto build_list = [&](bool pose_side, WorkList& W) -> int {
+        W = WorkList();
+        W.task_seg.push_back(0);
+        W.seg_item.push_back(0);
+        const int max_segs = pose_side ? kMaxPoseSegs : kMaxLmSegs;
+        int task_items = 0, task_segs = 0;
+        struct It { int32_t other, obs, slot, key; };
+        std::vector<It> its;
+        auto slot_of = [&](int owner, int other) -> int32_t {
+            const int32_t off = block_offset(owner, other);
+            return off < 0 ? -2 : P.node_row0[owner] + off;
+        };
+        auto add_node = [&](int u) -> int {
+            its.clear();
+            const bool write_ok = u != pi.fixed;
+            if (pose_side) {
+                for (int32_t e = pb_ptr[u]; e < pb_ptr[u + 1]; ++e) {
+                    const int k = pb[e];
+                    const int v = NP + pi.b_lm[k];
+                    int32_t slot = -1;
+                    if (write_ok && P.node_pos[u] > P.node_pos[v]) slot = slot_of(u, v);
+                    its.push_back({pi.b_lm[k], k, slot, P.node_pos[v]});
+                }
+                for (int32_t e = po_ptr[u]; e < po_ptr[u + 1]; ++e) {
+                    const int k = po[e] >> 1, side = po[e] & 1;
+                    const int v = side ? pi.o_src[k] : pi.o_dst[k];
+                    int32_t slot = -1;
+                    if (write_ok && v != pi.fixed && P.node_pos[u] > P.node_pos[v])
+                        slot = slot_of(u, v);
+                    its.push_back({-(2 * k + side) - 1, k, slot, v == pi.fixed ? INT32_MAX : P.node_pos[v]});
+                }
+            } else {
+                const int l = u - NP;
+                for (int32_t e = lb_ptr[l]; e < lb_ptr[l + 1]; ++e) {
+                    const int k = lb[e];
+                    const int v = pi.b_pose[k];
+                    int32_t slot = -1;
+                    if (v != pi.fixed && P.node_pos[u] > P.node_pos[v]) slot = slot_of(u, v);
+                    its.push_back({v, k, slot, v == pi.fixed ? INT32_MAX : P.node_pos[v]});
+                }
+            }
+            std::stable_sort(its.begin(), its.end(), [](const It& a, const It& b) { return a.key < b.key; });
+            for (const It& it : its)
+                if (it.slot < -1) return -3;   // block missing from the pattern (internal error)
+            const int cnt = (int)its.size();
+            // close the current task if this node does not fit
+            if (task_segs > 0 && (task_items + cnt > kWave || task_segs + 1 > max_segs)) {
+                W.task_seg.push_back((int32_t)W.seg_node.size());
+                W.max_items_per_task = std::max(W.max_items_per_task, task_items);
+                task_items = 0;
+                task_segs = 0;
+            }
+            const int32_t base = (int32_t)W.item_other.size();
+            for (int i = 0; i < cnt; ++i) {
+                W.item_other.push_back(its[i].other);
+                W.item_obs.push_back(its[i].obs);
+                W.item_slot.push_back(its[i].slot);
+                W.item_grp.push_back(base + i);
+            }
+            // off-diagonal groups: consecutive writing items with the same block
+            for (int i = 1; i < cnt; ++i) {
+                if (its[i].slot >= 0 && its[i].slot == its[i - 1].slot) {
+                    W.item_grp[base + i] = W.item_grp[base + i - 1];
+                    W.item_slot[base + i - 1] = -1;   // only the group's last item writes
+                    W.has_groups = true;
+                    // a group must not straddle a 64-item chunk boundary of its task
+                    const int first_in_task = W.item_grp[base + i] - W.seg_item[W.task_seg.back()];
+                    const int me_in_task = base + i - W.seg_item[W.task_seg.back()];
+                    if (first_in_task / kWave != me_in_task / kWave) return -2;
+                }
+            }
+            W.seg_node.push_back(pose_side ? u : u - NP);
+            W.seg_item.push_back((int32_t)W.item_other.size());
+            task_items += cnt;
+            task_segs += 1;
+            return 0;
+        };
+        for (int i = cut[rank]; i < cut[rank + 1]; ++i) {
+            const int u = inv[i];
+            if ((u < NP) != pose_side) continue;
+            const int a = add_node(u);
+            if (a == -2) { err = "duplicate observations straddle a 64-item chunk"; return BOS_ERR_UNSUPPORTED; }
+            if (a) { err = "internal error: off-diagonal block missing from the pattern"; return BOS_ERR_INVALID; }
+        }
+        if (pose_side && rank == world - 1) {   // the fixed pose: only its b entries (export)
+            if (add_node(pi.fixed)) { err = "duplicate observations straddle a 64-item chunk"; return BOS_ERR_UNSUPPORTED; }
+        }
+        if (task_segs > 0) {
+            W.task_seg.push_back((int32_t)W.seg_node.size());
+            W.max_items_per_task = std::max(W.max_items_per_task, task_items);
+        }
+        return BOS_OK;
+    };
+    rc = build_list(true, P.pose_list);
+    if (rc) return rc;
+    rc = build_list(false, P.lm_list);
+    if (rc) return rc;
+    return validate_plan(pi, P, err);
+}
+
+// Proves, on the host, that every address the J+H kernel writes (hip/kernels.hip diag_pos /
+// off_pos) lies inside the intended CSR row at the intended column, so a kernel launch can
+// never write out of bounds. O(items).
+int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
+    const int NP = pi.NP;
+    const int64_t nnz = P.nnzA();
+    auto check_entry = [&](int owner, int r, int64_t pos, int32_t want_col) -> bool {
+        const int64_t row = (int64_t)P.node_dof[owner] + r;
+        if (row < 0 || row >= P.n) return false;
+        if (pos < P.rowptr[row] || pos >= P.rowptr[row + 1] || pos >= nnz) return false;
+        return P.colind[pos] == want_col;
+    };
+    auto pos_off = [](int64_t slot, int base, int r, int c) { return slot + (int64_t)r * base + r * (r + 1) / 2 + c; };
+    auto pos_diag = [](int64_t row0, int base, int r, int c) { return row0 + (int64_t)r * base + r * (r + 1) / 2 + base + c; };
+    for (int u = 0; u < NP + pi.NL; ++u) {
+        if (u == pi.fixed) {
+            if (P.node_row0[u] != -1) { err = "fixed pose has rows"; return BOS_ERR_INVALID; }
+            continue;
+        }
+        const int su = node_size(u, NP);
+        for (int r = 0; r < su; ++r)
+            for (int c = 0; c <= r; ++c)
+                if (!check_entry(u, r, pos_diag(P.node_row0[u], P.node_base[u], r, c), P.node_dof[u] + c)) {
+                    err = "diagonal block of node " + std::to_string(u) + " misplaced";
+                    return BOS_ERR_INVALID;
+                }
+    }
+    auto check_list = [&](const WorkList& W, bool pose_side) -> bool {
+        for (int s = 0; s + 1 < (int)W.seg_item.size(); ++s) {
+            const int node = pose_side ? W.seg_node[s] : NP + W.seg_node[s];
+            for (int i = W.seg_item[s]; i < W.seg_item[s + 1]; ++i) {
+                if (W.item_grp[i] > i || W.item_grp[i] < W.seg_item[s]) return false;
+                const int slot = W.item_slot[i];
+                if (slot < 0) continue;
+                int other;
+                if (!pose_side) other = W.item_other[i];
+                else if (W.item_other[i] >= 0) other = NP + W.item_other[i];
+                else {
+                    const int code = -W.item_other[i] - 1, k = code >> 1, side = code & 1;
+                    other = side ? pi.o_src[k] : pi.o_dst[k];
+                }
+                const int su = node_size(node, NP), so = node_size(other, NP);
+                for (int r = 0; r < su; ++r)
+                    for (int c = 0; c < so; ++c)
+                        if (!check_entry(node, r, pos_off(slot, P.node_base[node], r, c), P.node_dof[other] + c))
+                            return false;
+            }
+        }
+        return true;
+    };
+    if (!check_list(P.pose_list, true) || !check_list(P.lm_list, false)) {
+        err = "off-diagonal write slot misplaced";
+        return BOS_ERR_INVALID;
+    }
+    // every stored entry of the rows this rank owns is written exactly once per iteration (no
+    // stale values survive), and nothing outside them is written
+    std::vector<uint8_t> hit(nnz, 0);
+    auto mark_list = [&](const WorkList& W, bool pose_side) {
+        for (int s = 0; s + 1 < (int)W.seg_item.size(); ++s) {
+            const int node = pose_side ? W.seg_node[s] : NP + W.seg_node[s];
+            if (node == pi.fixed) continue;
+            const int su = node_size(node, NP);
+            for (int r = 0; r < su; ++r)
+                for (int c = 0; c <= r; ++c) ++hit[pos_diag(P.node_row0[node], P.node_base[node], r, c)];
+            for (int i = W.seg_item[s]; i < W.seg_item[s + 1]; ++i) {
+                const int slot = W.item_slot[i];
+                if (slot < 0) continue;
+                int other;
+                if (!pose_side) other = W.item_other[i];
+                else if (W.item_other[i] >= 0) other = NP + W.item_other[i];
+                else {
+                    const int code = -W.item_other[i] - 1, k = code >> 1, side = code & 1;
+                    other = side ? pi.o_src[k] : pi.o_dst[k];
+                }
+                for (int r = 0; r < su; ++r)
+                    for (int c = 0; c < node_size(other, NP); ++c) ++hit[pos_off(slot, P.node_base[node], r, c)];
+            }
+        }
+    };
+    mark_list(P.pose_list, true);
+    mark_list(P.lm_list, false);
+    for (int64_t e = 0; e < nnz; ++e) {
+        const bool owned = e >= P.val_begin && e < P.val_end;
+        if (hit[e] != (owned ? 1 : 0)) {
+            err = "CSR entry " + std::to_string(e) + " written " + std::to_string((int)hit[e]) + " times";
+            return BOS_ERR_INVALID;
+        }
+    }
+    return BOS_OK;
+}
+
+}  // namespace bos

@@ -1,0 +1,76 @@
+// Static structure of the GN normal system, built once per solver handle (bos_create).
+//
+// The reference rebuilds H from scratch every iteration with Eigen sparse additions
+// (slam/solver.cpp:28-69) and runs SimplicialLDLT::analyzePattern once (:77-80). Here the
+// pattern is fixed up front: H_nf (the fixed pose's rows/cols removed, solver.cpp:71-73) is laid
+// out as the lower triangle of P^T H_nf P in CSR, where P is a fill-reducing node ordering, so
+// the J+H kernels scatter straight into the array the sparse Cholesky consumes (no per-step
+// permutation pass), and every observation knows its destination slots in advance.
+//
+// Nodes: pose stix u in [0, NP) (3 dofs), landmark stix l as node NP + l (2 dofs).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace bos {
+
+struct ProblemIndex {
+    int NP = 0, NL = 0, Mb = 0, Mo = 0, fixed = -1;
+    const int32_t* b_pose = nullptr;
+    const int32_t* b_lm = nullptr;
+    const int32_t* o_src = nullptr;
+    const int32_t* o_dst = nullptr;
+};
+
+struct WorkList {
+    // task -> segments -> items. A task is processed by one wavefront; a segment is one node
+    // (pose for the pose-centric list, landmark for the landmark-centric list); an item is one
+    // observation (or one side of an odometry edge) incident to that node.
+    std::vector<int32_t> task_seg;     // [ntask + 1]
+    std::vector<int32_t> seg_item;     // [nseg + 1]
+    std::vector<int32_t> seg_node;     // [nseg]  pose stix / landmark stix
+    std::vector<int32_t> item_other;   // pose list: lm stix (>= 0) or -(2*edge + side) - 1; lm list: pose stix
+    std::vector<int32_t> item_obs;     // bearing index (or edge index for odometry items)
+    std::vector<int32_t> item_slot;    // CSR position (row 0 of the owner) of the off-diagonal block, -1 none
+    std::vector<int32_t> item_grp;     // first item of this item's off-diagonal group (== own index if alone)
+    bool has_groups = false;           // some off-diagonal block has > 1 contributing item
+    int max_items_per_task = 0;
+    int ntask() const { return task_seg.empty() ? 0 : (int)task_seg.size() - 1; }
+    int nitem() const { return seg_item.empty() ? 0 : seg_item.back(); }
+};
+
+struct OrderingReport {
+    std::string chosen;                // "temporal" or "nested-dissection"
+    double flops_temporal = 0, flops_nd = 0;
+    int64_t nnz_temporal = 0, nnz_nd = 0;
+};
+
+struct Plan {
+    int NP = 0, NL = 0, Mb = 0, Mo = 0, fixed = -1;
+    int64_t n = 0;                         // system size N - 3
+    std::vector<int32_t> node_pos;         // elimination position; -1 for the fixed pose
+    std::vector<int32_t> node_dof;         // first dof in the permuted system; fixed pose -> n
+    std::vector<int32_t> node_row0;        // CSR position of the node's first row start; -1 fixed
+    std::vector<int32_t> node_base;        // entries before the diagonal block in each of its rows
+    std::vector<int32_t> rowptr, colind;   // lower triangle of P^T H_nf P, n rows
+    std::vector<int32_t> Lptr, Lind;       // symbolic Cholesky factor (lower, with diagonal)
+    WorkList pose_list, lm_list;
+    OrderingReport ordering;
+    // ownership for observation sharding: this rank writes rows [row_begin, row_end)
+    int32_t row_begin = 0, row_end = 0;
+    int64_t val_begin = 0, val_end = 0;
+    std::vector<int32_t> rank_row_begin;   // [world + 1] row split of every rank
+    int64_t nnzA() const { return rowptr.empty() ? 0 : rowptr.back(); }
+    int64_t nnzL() const { return Lptr.empty() ? 0 : Lptr.back(); }
+};
+
+// Builds the plan. want_factor: compute the symbolic Cholesky pattern (sparse solver).
+// Returns 0 or a negative BOS_ERR_* code with a message in err.
+int build_plan(const ProblemIndex& pi, int rank, int world, bool want_factor, Plan& out, std::string& err);
+
+// Exposed for tests: node ordering only (positions), and its symbolic cost.
+int order_nodes(const ProblemIndex& pi, std::vector<int32_t>& node_pos, OrderingReport& rep, std::string& err);
+
+}  // namespace bos

@@ -1,0 +1,185 @@
+#include "solver.hpp"
+
+#include <string>
+
+#include "bos_math.hpp"
+
+namespace proj02 {
+
+namespace {
+void check(int rc, const char* what) {
+    if (rc != BOS_OK) throw std::runtime_error(std::string(what) + ": " + bos_last_error());
+}
+}  // namespace
+
+double JacobianRow::coeff(int col) const {
+    double v = 0;
+    for (int k = 0; k < 5; ++k)
+        if (cols[k] == col) v += values[k];
+    return v;
+}
+
+double Jacobian3::coeff(int row, int col) const {
+    double v = 0;
+    for (int k = 0; k < 6; ++k)
+        if (cols[k] == col) v += values[row][k];
+    return v;
+}
+
+Solver::Solver(const State& st, const BearingObservationVector& bear_obs, const OdometryObservationVector& odom_obs,
+               const int& fixed_pose_id, const bos_options* options)
+    : state(st), bearing_observations(bear_obs), odometry_observations(odom_obs), fixed_pose_id_(fixed_pose_id) {
+    // SoA problem in stix order; ids resolved once (std::map::at throws on unknown ids like the reference)
+    const int NP = state.number_of_poses(), NL = state.number_of_landmarks();
+    std::vector<double> pose(3 * (size_t)NP), lm(2 * (size_t)NL);
+    for (int i = 0; i < NP; ++i) {
+        const NEPose& p = state.poses_vec()[i];
+        pose[3 * i] = p.x; pose[3 * i + 1] = p.y; pose[3 * i + 2] = p.theta;
+    }
+    for (int j = 0; j < NL; ++j) { lm[2 * j] = state.landmarks_vec()[j].x; lm[2 * j + 1] = state.landmarks_vec()[j].y; }
+    const size_t Mb = bearing_observations.size(), Mo = odometry_observations.size();
+    std::vector<int32_t> bp(Mb), bl(Mb), os(Mo), od(Mo);
+    std::vector<double> bz(Mb), bw(Mb), oz(3 * Mo), om(9 * Mo);
+    bool w1 = true;
+    for (size_t k = 0; k < Mb; ++k) {
+        const BearingObservation& o = bearing_observations[k];
+        bp[k] = state.pose_stix(o.get_pose_id());
+        bl[k] = state.landmark_stix(o.get_lm_id());
+        bz[k] = o.get_bearing_angle();
+        bw[k] = o.get_omega();
+        w1 = w1 && bw[k] == 1.0;
+    }
+    for (size_t k = 0; k < Mo; ++k) {
+        const OdometryObservation& o = odometry_observations[k];
+        os[k] = state.pose_stix(o.get_source_id());
+        od[k] = state.pose_stix(o.get_dest_id());
+        const EPose z = o.get_transformation();
+        oz[3 * k] = z.x; oz[3 * k + 1] = z.y; oz[3 * k + 2] = z.z;
+        const Mat3 m = o.get_omega();
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) om[9 * k + 3 * r + c] = m(r, c);
+    }
+    bos_problem pb;
+    pb.num_poses = NP; pb.num_landmarks = NL; pb.num_bearings = (int32_t)Mb; pb.num_odometry = (int32_t)Mo;
+    pb.pose_xyt = pose.data(); pb.landmark_xy = lm.data();
+    pb.bearing_pose = bp.data(); pb.bearing_landmark = bl.data(); pb.bearing_z = bz.data();
+    pb.bearing_omega = w1 ? nullptr : bw.data();
+    pb.odom_src = os.data(); pb.odom_dst = od.data(); pb.odom_z = oz.data(); pb.odom_omega = om.data();
+    pb.fixed_pose = state.pose_stix(fixed_pose_id);
+    check(bos_create(&pb, options, &h_), "bos_create");
+}
+
+Solver::~Solver() { bos_destroy(h_); }
+
+void Solver::set_kernel_threshold(float kt) { check(bos_set_kernel_threshold(h_, kt), "set_kernel_threshold"); }
+void Solver::set_damping_factor(float df) { check(bos_set_damping_factor(h_, df), "set_damping_factor"); }
+
+void Solver::sync_state() {
+    const int NP = state.number_of_poses(), NL = state.number_of_landmarks();
+    std::vector<double> pose(3 * (size_t)NP), lm(2 * (size_t)NL);
+    check(bos_get_state(h_, pose.data(), lm.data()), "bos_get_state");
+    for (int i = 0; i < NP; ++i) state.poses_vec()[i] = NEPose(pose[3 * i], pose[3 * i + 1], pose[3 * i + 2]);
+    for (int j = 0; j < NL; ++j) state.landmarks_vec()[j] = LMPos(lm[2 * j], lm[2 * j + 1]);
+}
+
+void Solver::step() {
+    check(bos_step(h_, &stats_), "bos_step");
+    sync_state();
+}
+
+void Solver::step_n(int n) {
+    check(bos_step_n(h_, n, &stats_), "bos_step_n");
+    sync_state();
+}
+
+double Solver::normalized_angle(double a) { return bos::normalized_angle<double>(a); }
+
+double Solver::predict_bearing(const NEPose& pose, const LMPos& lm) {
+    const Vec2 g = pose.inverse_apply(lm);
+    return std::atan2(g.y, g.x);
+}
+
+EPose Solver::predict_odometry(const NEPose& src, const NEPose& dst) {
+    const EPose es = t2v(src), ed = t2v(dst);
+    const double c = std::cos(src.theta), s = std::sin(src.theta);
+    const double tx = ed.x - es.x, ty = ed.y - es.y;
+    return EPose(c * tx + s * ty, -s * tx + c * ty, normalized_angle(ed.z - es.z));
+}
+
+void Solver::error_and_jacobian(const State& st, const BearingObservation& obs, double& error, JacobianRow& J) {
+    const NEPose p = st.get_pose_by_id(obs.get_pose_id());
+    const LMPos l = st.get_landmark_by_id(obs.get_lm_id());
+    error = bos::bearing_error_jacobian<double>(p.x, p.y, std::cos(p.theta), std::sin(p.theta), l.x, l.y,
+                                                obs.get_bearing_angle(), J.values);
+    const int pc = 3 * st.pose_stix(obs.get_pose_id());
+    const int lc = 3 * st.number_of_poses() + 2 * st.landmark_stix(obs.get_lm_id());
+    const int cols[5] = {pc, pc + 1, pc + 2, lc, lc + 1};
+    for (int k = 0; k < 5; ++k) J.cols[k] = cols[k];
+}
+
+void Solver::error_and_jacobian(const State& st, const OdometryObservation& obs, EPose& error, Jacobian3& J) {
+    const NEPose s = st.get_pose_by_id(obs.get_source_id());
+    const NEPose d = st.get_pose_by_id(obs.get_dest_id());
+    const EPose z = obs.get_transformation();
+    double e[3], JJ[18];
+    bos::odometry_error_jacobian<double>(s.x, s.y, s.theta, std::cos(s.theta), std::sin(s.theta), d.x, d.y, d.theta,
+                                         z.x, z.y, z.z, e, JJ);
+    error = EPose(e[0], e[1], e[2]);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 6; ++c) J.values[r][c] = JJ[6 * r + c];
+    const int sc = 3 * st.pose_stix(obs.get_source_id()), dc = 3 * st.pose_stix(obs.get_dest_id());
+    const int cols[6] = {sc, sc + 1, sc + 2, dc, dc + 1, dc + 2};
+    for (int k = 0; k < 6; ++k) J.cols[k] = cols[k];
+}
+
+// slam/solver_jacobians.cpp:170-222 (central differences through boxplus)
+void Solver::error_and_numerical_jacobian(const State& st, const BearingObservation& obs, double& error,
+                                          JacobianRow& J, double eps) {
+    const NEPose p = st.get_pose_by_id(obs.get_pose_id());
+    const LMPos l = st.get_landmark_by_id(obs.get_lm_id());
+    const double z = obs.get_bearing_angle();
+    auto err = [&](const EPose& dp, const LMPos& dl) {
+        const NEPose q = boxplus(p, dp);
+        return normalized_angle(predict_bearing(q, l + dl) - z);
+    };
+    error = err(EPose(0, 0, 0), LMPos(0, 0));
+    const EPose sel_p[3] = {EPose(1, 0, 0), EPose(0, 1, 0), EPose(0, 0, 1)};
+    for (int k = 0; k < 3; ++k) {
+        const EPose d(eps * sel_p[k].x, eps * sel_p[k].y, eps * sel_p[k].z), m(-d.x, -d.y, -d.z);
+        J.values[k] = (err(d, LMPos(0, 0)) - err(m, LMPos(0, 0))) / (2 * eps);
+    }
+    J.values[3] = (err(EPose(0, 0, 0), LMPos(eps, 0)) - err(EPose(0, 0, 0), LMPos(-eps, 0))) / (2 * eps);
+    J.values[4] = (err(EPose(0, 0, 0), LMPos(0, eps)) - err(EPose(0, 0, 0), LMPos(0, -eps))) / (2 * eps);
+    const int pc = 3 * st.pose_stix(obs.get_pose_id());
+    const int lc = 3 * st.number_of_poses() + 2 * st.landmark_stix(obs.get_lm_id());
+    const int cols[5] = {pc, pc + 1, pc + 2, lc, lc + 1};
+    for (int k = 0; k < 5; ++k) J.cols[k] = cols[k];
+}
+
+// slam/solver_jacobians.cpp:224-299
+void Solver::error_and_numerical_jacobian(const State& st, const OdometryObservation& obs, EPose& error, Jacobian3& J,
+                                          double eps) {
+    const NEPose s = st.get_pose_by_id(obs.get_source_id());
+    const NEPose d = st.get_pose_by_id(obs.get_dest_id());
+    const EPose z = obs.get_transformation();
+    auto err = [&](const EPose& ds, const EPose& dd) {
+        const EPose pr = predict_odometry(boxplus(s, ds), boxplus(d, dd));
+        return EPose(pr.x - z.x, pr.y - z.y, normalized_angle(pr.z - z.z));
+    };
+    error = err(EPose(0, 0, 0), EPose(0, 0, 0));
+    for (int k = 0; k < 6; ++k) {
+        double v[3] = {0, 0, 0};
+        v[k % 3] = eps;
+        const EPose dp(v[0], v[1], v[2]), dm(-v[0], -v[1], -v[2]), zero(0, 0, 0);
+        const EPose a = k < 3 ? err(dp, zero) : err(zero, dp);
+        const EPose b = k < 3 ? err(dm, zero) : err(zero, dm);
+        J.values[0][k] = (a.x - b.x) / (2 * eps);
+        J.values[1][k] = (a.y - b.y) / (2 * eps);
+        J.values[2][k] = (a.z - b.z) / (2 * eps);
+    }
+    const int sc = 3 * st.pose_stix(obs.get_source_id()), dc = 3 * st.pose_stix(obs.get_dest_id());
+    const int cols[6] = {sc, sc + 1, sc + 2, dc, dc + 1, dc + 2};
+    for (int k = 0; k < 6; ++k) J.cols[k] = cols[k];
+}
+
+}  // namespace proj02

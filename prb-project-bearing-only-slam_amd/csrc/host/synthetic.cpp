@@ -1,0 +1,147 @@
+#include "synthetic.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <random>
+
+namespace proj02 {
+
+namespace {
+
+struct Rng {
+    std::mt19937_64 g;
+    explicit Rng(uint64_t s) : g(s) {}
+    double uniform() { return (double)(g() >> 11) * (1.0 / 9007199254740992.0); }   // [0, 1)
+    double uniform(double a, double b) { return a + (b - a) * uniform(); }
+    double normal() {   // Box-Muller, deterministic across standard libraries
+        double u1 = uniform();
+        while (u1 <= 1e-300) u1 = uniform();
+        const double u2 = uniform();
+        return std::sqrt(-2.0 * std::log(u1)) * std::cos(2.0 * bos::kPi * u2);
+    }
+    uint64_t below(uint64_t n) { return n ? g() % n : 0; }
+};
+
+}  // namespace
+
+bool make_synthetic(const SyntheticParams& p, SyntheticWorld& out) {
+    const int NP = p.num_poses, NL = p.num_landmarks, K = p.bearings_per_pose;
+    if (NP < 2 || K < 1 || NL < K || (long long)NP * K < 2LL * NL) return false;
+    Rng rng(p.seed);
+    const double W = p.world_extent > 0 ? p.world_extent : std::min(1000.0, std::max(40.0, 3.0 * std::sqrt((double)NP)));
+    const double half = 0.5 * W, margin = std::min(20.0, 0.15 * W);
+
+    // ---- ground-truth trajectory and noisy odometry
+    std::vector<double> gx(NP), gy(NP), gth(NP);
+    gx[0] = 0; gy[0] = 0; gth[0] = 0;
+    std::vector<double> zx(NP), zy(NP), zt(NP);
+    double turn = 0;
+    for (int i = 0; i + 1 < NP; ++i) {
+        const double u = rng.uniform(0.75, 1.0);
+        turn = 0.8 * turn + 0.02 * rng.normal();
+        // steer towards the centre when close to the border
+        const double nx = gx[i] + std::cos(gth[i]) * 4.0, ny = gy[i] + std::sin(gth[i]) * 4.0;
+        if (std::fabs(nx) > half - margin || std::fabs(ny) > half - margin) {
+            const double want = std::atan2(-gy[i], -gx[i]);
+            const double d = bos::normalized_angle<double>(want - gth[i]);
+            turn = std::max(-0.12, std::min(0.12, 0.25 * d));
+        }
+        const double dth = std::max(-0.15, std::min(0.15, turn));
+        gx[i + 1] = gx[i] + std::cos(gth[i]) * u;
+        gy[i + 1] = gy[i] + std::sin(gth[i]) * u;
+        gth[i + 1] = bos::normalized_angle<double>(gth[i] + dth);
+        // measurement in the source frame: R_s^T (t_d - t_s), theta_d - theta_s (+ noise)
+        zx[i] = u + rng.normal() / std::sqrt(p.odom_info_xy);
+        zy[i] = 0.0 + rng.normal() / std::sqrt(p.odom_info_xy);
+        zt[i] = dth + rng.normal() / std::sqrt(p.odom_info_theta);
+    }
+
+    // ---- landmark windows: K lanes, each a composition of [0, NP) into windows of length >= 2
+    std::vector<int> per_lane(K, NL / K);
+    for (int k = 0; k < NL % K; ++k) per_lane[k] += 1;
+    struct Win { int lane, first, last; };
+    std::vector<Win> wins;
+    wins.reserve(NL);
+    for (int k = 0; k < K; ++k) {
+        const int n = per_lane[k];
+        const int extra = NP - 2 * n;
+        std::vector<int> cuts(n - 1);
+        for (int& c : cuts) c = (int)rng.below((uint64_t)extra + 1);
+        std::sort(cuts.begin(), cuts.end());
+        int start = 0, prev = 0;
+        for (int j = 0; j < n; ++j) {
+            const int e = (j + 1 < n) ? cuts[j] : extra;
+            const int len = 2 + (e - prev);
+            prev = e;
+            wins.push_back({k, start, start + len - 1});
+            start += len;
+        }
+    }
+    // deterministic landmark order: by window start, then lane
+    std::stable_sort(wins.begin(), wins.end(), [](const Win& a, const Win& b) {
+        return a.first != b.first ? a.first < b.first : a.lane < b.lane;
+    });
+
+    std::vector<double> lx(NL), ly(NL);
+    std::vector<std::vector<int>> seen_by(NP);
+    for (int j = 0; j < NL; ++j) {
+        const Win& w = wins[j];
+        const int L = w.last;
+        const double side = (w.lane % 2) ? 1.0 : -1.0;
+        double bx = 0, by = 0;
+        for (int attempt = 0; attempt < 24; ++attempt) {
+            const double f = rng.uniform(0.8, 3.0);
+            const double lat = side * rng.uniform(0.6, 4.0);
+            bx = gx[L] + std::cos(gth[L]) * f - std::sin(gth[L]) * lat;
+            by = gy[L] + std::sin(gth[L]) * f + std::cos(gth[L]) * lat;
+            bool ok = true;
+            for (int i = w.first; i <= L && ok; ++i) {
+                const double c = std::cos(gth[i]), s = std::sin(gth[i]);
+                const double qx = c * (bx - gx[i]) + s * (by - gy[i]);
+                const double qy = -s * (bx - gx[i]) + c * (by - gy[i]);
+                const double r = std::hypot(qx, qy);
+                ok = r > 0.5 && qx > 0.08 * r;
+            }
+            if (ok) break;
+        }
+        lx[j] = bx;
+        ly[j] = by;
+        for (int i = w.first; i <= L; ++i) seen_by[i].push_back(j);
+    }
+
+    // ---- assemble the two states and the measurements (bearings listed per pose, like the dataset)
+    out = SyntheticWorld();
+    out.fixed_pose_id = 0;
+    const int lm_id0 = NP;   // ids unique across poses and landmarks (g2o convention)
+    double ix = gx[0], iy = gy[0], ith = gth[0];
+    for (int i = 0; i < NP; ++i) {
+        out.ground_truth.add_pose(gx[i], gy[i], gth[i], i);
+        out.initial_guess.add_pose(ix, iy, ith, i);
+        if (i + 1 < NP) {   // dead reckoning with the noisy odometry (predict_odometry inverted)
+            const double c = std::cos(ith), s = std::sin(ith);
+            ix += c * zx[i] - s * zy[i];
+            iy += s * zx[i] + c * zy[i];
+            ith = bos::normalized_angle<double>(ith + zt[i]);
+        }
+    }
+    for (int j = 0; j < NL; ++j) out.ground_truth.add_landmark(lx[j], ly[j], lm_id0 + j);
+    Mat3 om;
+    om(0, 0) = p.odom_info_xy; om(1, 1) = p.odom_info_xy; om(2, 2) = p.odom_info_theta;
+    om(0, 1) = om(0, 2) = om(1, 0) = om(1, 2) = om(2, 0) = om(2, 1) = 0;
+    out.bearings.reserve((size_t)NP * K);
+    for (int i = 0; i < NP; ++i) {
+        std::vector<int>& v = seen_by[i];
+        std::sort(v.begin(), v.end());
+        const double c = std::cos(gth[i]), s = std::sin(gth[i]);
+        for (int j : v) {
+            const double qx = c * (lx[j] - gx[i]) + s * (ly[j] - gy[i]);
+            const double qy = -s * (lx[j] - gx[i]) + c * (ly[j] - gy[i]);
+            const double z = bos::normalized_angle<double>(std::atan2(qy, qx) + p.sigma_bearing * rng.normal());
+            out.bearings.emplace_back(i, lm_id0 + j, z);
+        }
+        if (i + 1 < NP) out.odometry.emplace_back(i, i + 1, zx[i], zy[i], zt[i], om);
+    }
+    return true;
+}
+
+}  // namespace proj02

@@ -1,0 +1,27 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "prb-project-bearing-only-slam_amd")
+for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+DATA = os.path.join(ROOT, "tests", "golden", "data")
+C1 = os.path.join(DATA, "slam2D_bearing_only_initial_guess.g2o")
+C1_GT = os.path.join(DATA, "slam2D_bearing_only_ground_truth.g2o")
+MINI = os.path.join(DATA, "mini_initial_guess.g2o")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and runs the HIP path")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    def load(name):
+        return np.load(os.path.join(ROOT, "tests", "golden", f"{name}.npz"))
+    return load

@@ -1,0 +1,44 @@
+"""Shared helpers for the parity tests: convert between the product's problem (bos.Problem)
+and the oracle's (oracle.Problem), and bring both H's into one comparable form."""
+import numpy as np
+import scipy.sparse as sp
+
+import bos
+import oracle as O
+
+
+def to_oracle(P: "bos.Problem") -> "O.Problem":
+    """Same arrays, same initial state: parity tests start the oracle and the HIP path from
+    identical inputs (the product's own triangulation is checked separately)."""
+    return O.Problem(pose_ids=P.pose_ids, lm_ids=P.lm_ids, pose_xyt=P.pose_xyt.copy(), lm_xy=P.lm_xy.copy(),
+                     b_pose=P.b_pose.copy(), b_lm=P.b_lm.copy(), b_z=P.b_z.copy(),
+                     b_omega=None if P.b_omega is None else P.b_omega.copy(), o_src=P.o_src.copy(),
+                     o_dst=P.o_dst.copy(), o_z=P.o_z.copy(), o_omega=P.o_omega.copy(), fixed=P.fixed)
+
+
+def oracle_lower_nf(Q: "O.Problem", lin) -> sp.csr_matrix:
+    """Lower triangle of H with the fixed pose's rows/cols removed (kept in N numbering)."""
+    H = O.assemble_H(Q, lin).tocoo()
+    keep = np.ones(Q.N, dtype=bool)
+    keep[3 * Q.fixed:3 * Q.fixed + 3] = False
+    m = (H.row >= H.col) & keep[H.row] & keep[H.col]
+    return sp.coo_matrix((H.data[m], (H.row[m], H.col[m])), shape=H.shape).tocsr()
+
+
+def gpu_lower(rows, cols, vals, N) -> sp.csr_matrix:
+    return sp.coo_matrix((vals, (rows.astype(np.int64), cols.astype(np.int64))), shape=(N, N)).tocsr()
+
+
+def rel_err(a: sp.spmatrix, b: sp.spmatrix) -> float:
+    d = (a - b).tocoo()
+    scale = max(abs(a).max(), abs(b).max(), 1e-300)
+    return (np.abs(d.data).max() if d.nnz else 0.0) / scale
+
+
+def state_rel_err(pa, la, pb, lb, floor=1e-9):
+    """max |a - b| / max(|b|, floor) over poses (x, y, wrapped theta) and landmarks."""
+    dp = pa - pb
+    dp[:, 2] = (dp[:, 2] + np.pi) % (2 * np.pi) - np.pi
+    e1 = np.abs(dp) / np.maximum(np.abs(pb), floor)
+    e2 = np.abs(la - lb) / np.maximum(np.abs(lb), floor) if len(lb) else np.zeros(1)
+    return max(e1.max(), e2.max())
