@@ -40,9 +40,11 @@ extern "C" {
 #define BOS_FP64 64
 #define BOS_FP32 32
 
-/* linear solver for H_nf dx = -b_nf */
-#define BOS_SOLVER_SPARSE_CHOL 0  /* rocSOLVER csrrf refactchol/solve on a host-analysed pattern */
-#define BOS_SOLVER_DENSE_CHOL 1   /* rocSOLVER potrf/potrs on a dense copy (small problems)      */
+/* linear solver for H_nf dx = -b_nf (the reference: Eigen SimplicialLDLT, slam/solver.hpp:71-72) */
+#define BOS_SOLVER_SUPERNODAL 0   /* GPU multifrontal supernodal Cholesky, nested dissection (default) */
+#define BOS_SOLVER_DENSE_CHOL 1   /* rocSOLVER potrf/potrs on a dense copy (small problems)          */
+#define BOS_SOLVER_ROCSOLVER_RF 2 /* rocSOLVER csrrf analysis/refactchol/solve (level-scheduled)      */
+#define BOS_SOLVER_SPARSE_CHOL BOS_SOLVER_SUPERNODAL
 
 /*
  * Problem in stix order (framework/state.hpp:47-53): poses in file order, landmarks in
@@ -71,7 +73,7 @@ typedef struct bos_problem {
 
 typedef struct bos_options {
     int32_t precision;              /* BOS_FP64 (default) or BOS_FP32                            */
-    int32_t solver;                 /* BOS_SOLVER_SPARSE_CHOL (default) / BOS_SOLVER_DENSE_CHOL  */
+    int32_t solver;                 /* BOS_SOLVER_SUPERNODAL (default) / _DENSE_CHOL / _ROCSOLVER_RF */
     int32_t device;                 /* HIP device ordinal, -1 = current                          */
     int32_t rank;                   /* shard index (0 for one GPU)                               */
     int32_t world_size;             /* number of shards (1 for one GPU)                          */

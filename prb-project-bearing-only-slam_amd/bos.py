@@ -25,8 +25,10 @@ LIB_PATH = os.path.join(_HERE, "lib", "libbos.so")
 BOS_OK = 0
 BOS_FP64 = 64
 BOS_FP32 = 32
-BOS_SOLVER_SPARSE_CHOL = 0
+BOS_SOLVER_SUPERNODAL = 0
 BOS_SOLVER_DENSE_CHOL = 1
+BOS_SOLVER_ROCSOLVER_RF = 2
+BOS_SOLVER_SPARSE_CHOL = BOS_SOLVER_SUPERNODAL
 
 # every symbol declared in include/bos.h and include/bos_host.h
 EXPORTED_SYMBOLS = [
@@ -36,7 +38,7 @@ EXPORTED_SYMBOLS = [
     "bos_get_state", "bos_set_state", "bos_get_last_dx",
     "bos_dataset_load_g2o", "bos_dataset_synthetic", "bos_dataset_problem", "bos_dataset_pose_ids",
     "bos_dataset_landmark_ids", "bos_dataset_fixed_pose_id", "bos_dataset_bound", "bos_dataset_ground_truth",
-    "bos_dataset_write_g2o", "bos_dataset_free", "bos_plan_inspect",
+    "bos_dataset_write_g2o", "bos_dataset_free", "bos_plan_inspect", "bos_plan_mf_selftest",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -81,7 +83,9 @@ class bos_plan_info(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("nnz_lower", ctypes.c_int64), ("nnz_factor", ctypes.c_int64),
                 ("num_tasks_pose", ctypes.c_int64), ("num_tasks_landmark", ctypes.c_int64),
                 ("flops_temporal", ctypes.c_double), ("flops_nested_dissection", ctypes.c_double),
-                ("ordering", ctypes.c_char * 32)]
+                ("ordering", ctypes.c_char * 32), ("mf_supernodes", ctypes.c_int64),
+                ("mf_levels", ctypes.c_int64), ("mf_max_front", ctypes.c_int64), ("mf_flops", ctypes.c_double),
+                ("mf_update_bytes", ctypes.c_int64)]
 
 
 _lib = None
@@ -129,7 +133,8 @@ def lib():
         "bos_dataset_free": (None, [vp]),
         "bos_plan_inspect": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_int64, _ip, _ip, ctypes.POINTER(ctypes.c_uint8),
-                                            ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(bos_plan_info)]),
+                                            ctypes.POINTER(ctypes.c_uint8), _ip, ctypes.POINTER(bos_plan_info)]),
+        "bos_plan_mf_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), _dp, _dp, _dp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -273,23 +278,37 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
     L = lib()
     cs = P.c_struct()
     info = bos_plan_info()
-    _check(L.bos_plan_inspect(ctypes.byref(cs), rank, world, 0, None, None, None, None, ctypes.byref(info)),
+    _check(L.bos_plan_inspect(ctypes.byref(cs), rank, world, 0, None, None, None, None, None, ctypes.byref(info)),
            "plan_inspect")
     out = {"n": info.n, "nnz_lower": info.nnz_lower, "nnz_factor": info.nnz_factor,
            "num_tasks_pose": info.num_tasks_pose, "num_tasks_landmark": info.num_tasks_landmark,
            "flops_temporal": info.flops_temporal, "flops_nested_dissection": info.flops_nested_dissection,
-           "ordering": info.ordering.decode()}
+           "ordering": info.ordering.decode(), "mf_supernodes": info.mf_supernodes,
+           "mf_levels": info.mf_levels, "mf_max_front": info.mf_max_front, "mf_flops": info.mf_flops,
+           "mf_update_bytes": info.mf_update_bytes}
     if entries:
         nnz = info.nnz_lower
         rows = np.zeros(nnz, dtype=np.int32)
         cols = np.zeros(nnz, dtype=np.int32)
         owned = np.zeros(nnz, dtype=np.uint8)
         b_owned = np.zeros(P.N, dtype=np.uint8)
+        perm = np.zeros(P.N, dtype=np.int32)
         _check(L.bos_plan_inspect(ctypes.byref(cs), rank, world, nnz, _ptr(rows, ctypes.c_int32),
                                   _ptr(cols, ctypes.c_int32), _ptr(owned, ctypes.c_uint8),
-                                  _ptr(b_owned, ctypes.c_uint8), None), "plan_inspect")
-        out.update(rows=rows, cols=cols, owned=owned.astype(bool), b_owned=b_owned.astype(bool))
+                                  _ptr(b_owned, ctypes.c_uint8), _ptr(perm, ctypes.c_int32), None), "plan_inspect")
+        out.update(rows=rows, cols=cols, owned=owned.astype(bool), b_owned=b_owned.astype(bool), perm_to_ref=perm)
     return out
+
+
+def plan_mf_selftest(P: Problem, vals, rhs):
+    """Host re-run of the GPU multifrontal algorithm on the plan's tree (test hook)."""
+    cs = P.c_struct()
+    v = np.ascontiguousarray(vals, dtype=np.float64)
+    b = np.ascontiguousarray(rhs, dtype=np.float64)
+    x = np.zeros_like(b)
+    _check(lib().bos_plan_mf_selftest(ctypes.byref(cs), _ptr(v, ctypes.c_double), _ptr(b, ctypes.c_double),
+                                      _ptr(x, ctypes.c_double)), "plan_mf_selftest")
+    return x
 
 
 def nccl_unique_id() -> bytes:

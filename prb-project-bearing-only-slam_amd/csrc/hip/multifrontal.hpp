@@ -1,0 +1,25 @@
+// GPU supernodal multifrontal Cholesky (hip/multifrontal.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+namespace bos {
+struct Multifrontal;
+namespace dev {
+
+struct MfDevice;
+
+// Upload the static tree / maps and allocate factor buffers. Returns 0 or < 0 with err.
+int mf_create(const Multifrontal& F, MfDevice** out, std::string& err);
+void mf_destroy(MfDevice* d);
+// Numeric factorization of H (CSR values in nested-dissection order, fp64).
+hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s);
+// x <- H^{-1} x (x in the same permuted order) using the last factorization.
+hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s);
+// device counter of non-positive pivots met by the last factorization
+const int32_t* mf_info_ptr(const MfDevice* d);
+
+}  // namespace dev
+}  // namespace bos

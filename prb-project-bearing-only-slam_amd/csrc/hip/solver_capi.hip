@@ -22,6 +22,7 @@
 #include "../host/error.hpp"
 #include "../host/plan.hpp"
 #include "kernels.hpp"
+#include "multifrontal.hpp"
 
 namespace {
 
@@ -64,7 +65,7 @@ struct bos_solver {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int precision = BOS_FP64;
-    int solver_kind = BOS_SOLVER_SPARSE_CHOL;
+    int solver_kind = BOS_SOLVER_SUPERNODAL;
     int rank = 0, world = 1;
     double kt = 1.0, damping = 0.01;
     bos::Plan plan;
@@ -108,6 +109,7 @@ struct bos_solver {
     unsigned long long* d_maxdx = nullptr;
     rocblas_handle rb = nullptr;
     rocsolver_rfinfo rf = nullptr;
+    bos::dev::MfDevice* mf = nullptr;
     bool analyzed = false;
     ncclComm_t comm = nullptr;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -214,6 +216,11 @@ int enqueue_solve(bos_solver* s, bool& ran_analysis) {
         A = (double*)s->d_val;
     }
     const rocblas_int nn = (rocblas_int)n;
+    if (s->solver_kind == BOS_SOLVER_SUPERNODAL) {
+        HIP_TRY(bos::dev::mf_factor(s->mf, A, s->stream));
+        HIP_TRY(bos::dev::mf_solve(s->mf, s->d_rhs, s->stream));
+        return BOS_OK;
+    }
     if (s->solver_kind == BOS_SOLVER_DENSE_CHOL) {
         HIP_TRY(hipMemsetAsync(s->d_dense, 0, (size_t)n * n * sizeof(double), s->stream));
         HIP_TRY(bos::dev::launch_scatter_dense(s->d_rowptr, s->d_colind, A, nn, s->d_dense, s->stream));
@@ -265,6 +272,8 @@ int read_stats(bos_solver* s, bos_step_stats* st, bool with_update, bool with_so
     if (with_update) HIP_TRY(hipMemcpyAsync(&mdx, s->d_maxdx, sizeof(mdx), hipMemcpyDeviceToHost, s->stream));
     if (with_solve && s->solver_kind == BOS_SOLVER_DENSE_CHOL)
         HIP_TRY(hipMemcpyAsync(&info, s->d_info, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    if (with_solve && s->solver_kind == BOS_SOLVER_SUPERNODAL)
+        HIP_TRY(hipMemcpyAsync(&info, bos::dev::mf_info_ptr(s->mf), sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     if (st) {
         std::memset(st, 0, sizeof(*st));
@@ -349,6 +358,7 @@ int bos_destroy(bos_solver* s) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (s->rf) rocsolver_destroy_rfinfo(s->rf);
+    if (s->mf) bos::dev::mf_destroy(s->mf);
     if (s->rb) rocblas_destroy_handle(s->rb);
     if (s->comm) ncclCommDestroy(s->comm);
     for (hipEvent_t& e : s->ev)
@@ -365,7 +375,8 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     bos_default_options(&opt);
     if (opt_in) opt = *opt_in;
     if (opt.precision != BOS_FP64 && opt.precision != BOS_FP32) return fail(BOS_ERR_INVALID, "precision must be 32 or 64");
-    if (opt.solver != BOS_SOLVER_SPARSE_CHOL && opt.solver != BOS_SOLVER_DENSE_CHOL)
+    if (opt.solver != BOS_SOLVER_SUPERNODAL && opt.solver != BOS_SOLVER_DENSE_CHOL &&
+        opt.solver != BOS_SOLVER_ROCSOLVER_RF)
         return fail(BOS_ERR_INVALID, "unknown solver");
     if (pb->num_poses <= 0 || pb->num_landmarks < 0 || pb->num_bearings < 0 || pb->num_odometry < 0)
         return fail(BOS_ERR_INVALID, "bad problem sizes");
@@ -401,7 +412,10 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     pi.NP = s->NP; pi.NL = s->NL; pi.Mb = s->Mb; pi.Mo = s->Mo; pi.fixed = pb->fixed_pose;
     pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
     std::string err;
-    int rc = bos::build_plan(pi, s->rank, s->world, s->solver_kind == BOS_SOLVER_SPARSE_CHOL, s->plan, err);
+    const int fmode = s->solver_kind == BOS_SOLVER_SUPERNODAL    ? bos::kFactorMultifrontal
+                      : s->solver_kind == BOS_SOLVER_ROCSOLVER_RF ? bos::kFactorScalar
+                                                                  : bos::kFactorNone;
+    int rc = bos::build_plan(pi, s->rank, s->world, fmode, s->plan, err);
     if (rc) return bail(fail(rc, "plan: " + err));
     const bos::Plan& P = s->plan;
     if (s->solver_kind == BOS_SOLVER_DENSE_CHOL && P.n > 40000)
@@ -424,7 +438,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         if (hipEventCreate(&e) != hipSuccess) return bail(fail(BOS_ERR_DEVICE, "hipEventCreate failed"));
     if (rocblas_create_handle(&s->rb) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "rocblas_create_handle"));
     if (rocblas_set_stream(s->rb, s->stream) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "rocblas_set_stream"));
-    if (s->solver_kind == BOS_SOLVER_SPARSE_CHOL) {
+    if (s->solver_kind == BOS_SOLVER_ROCSOLVER_RF) {
         if (rocsolver_create_rfinfo(&s->rf, s->rb) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "create_rfinfo"));
         if (rocsolver_set_rfinfo_mode(s->rf, rocsolver_rfinfo_mode_cholesky) != rocblas_status_success)
             return bail(fail(BOS_ERR_SOLVER, "set_rfinfo_mode"));
@@ -516,7 +530,10 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     HIP_TRY(hipMemset(s->d_val, 0, std::max<int64_t>(P.nnzA(), 1) * s->tsize));
     HIP_TRY(hipMemset(s->d_b, 0, (P.n + 3) * s->tsize));
     if ((rc = upload(&s->d_rowptr, P.rowptr)) || (rc = upload(&s->d_colind, P.colind))) return bail(rc);
-    if (s->solver_kind == BOS_SOLVER_SPARSE_CHOL) {
+    if (s->solver_kind == BOS_SOLVER_SUPERNODAL) {
+        std::string merr;
+        if (bos::dev::mf_create(P.mf, &s->mf, merr)) return bail(fail(BOS_ERR_DEVICE, merr));
+    } else if (s->solver_kind == BOS_SOLVER_ROCSOLVER_RF) {
         std::vector<int32_t> piv(P.n);
         for (int64_t i = 0; i < P.n; ++i) piv[i] = (int32_t)i;   // ordering already applied in the layout
         if ((rc = upload(&s->d_Lptr, P.Lptr)) || (rc = upload(&s->d_Lind, P.Lind)) || (rc = upload(&s->d_pivQ, piv)) ||
@@ -611,7 +628,7 @@ int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
     const bos::Plan& P = s->plan;
     info->n = P.n;
     info->nnz_lower = P.nnzA();
-    info->nnz_factor = P.nnzL();
+    info->nnz_factor = s->solver_kind == BOS_SOLVER_SUPERNODAL ? P.mf.L_size : P.nnzL();
     const int64_t Mb = s->Mb, Mo = s->Mo, NP = s->NP, NL = s->NL;
     // compulsory reads of inputs + state, one write of every output block
     info->algorithmic_bytes = s->precision == BOS_FP32 ? 36 * Mb + 80 * Mo + 60 * NP + 32 * NL

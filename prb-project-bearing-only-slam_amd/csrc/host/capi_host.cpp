@@ -170,7 +170,8 @@ int bos_dataset_write_g2o(const bos_dataset* d, const char* path, const double* 
 void bos_dataset_free(bos_dataset* d) { delete d; }
 
 int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
-                     int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, bos_plan_info* info) {
+                     int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref,
+                     bos_plan_info* info) {
     if (!pb) return hfail(BOS_ERR_INVALID, "null problem");
     bos::ProblemIndex pi;
     pi.NP = pb->num_poses; pi.NL = pb->num_landmarks; pi.Mb = pb->num_bearings; pi.Mo = pb->num_odometry;
@@ -178,7 +179,7 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
     pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
     bos::Plan P;
     std::string err;
-    const int rc = bos::build_plan(pi, rank, world, true, P, err);
+    const int rc = bos::build_plan(pi, rank, world, bos::kFactorMultifrontal, P, err);
     if (rc) return hfail(rc, err);
     const int NP = pi.NP;
     std::vector<int32_t> ref(P.n + 3);
@@ -191,11 +192,16 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
         std::memset(info, 0, sizeof(*info));
         info->n = P.n;
         info->nnz_lower = P.nnzA();
-        info->nnz_factor = P.nnzL();
+        info->nnz_factor = P.mf.L_size;
         info->num_tasks_pose = P.pose_list.ntask();
         info->num_tasks_landmark = P.lm_list.ntask();
         info->flops_temporal = P.ordering.flops_temporal;
         info->flops_nested_dissection = P.ordering.flops_nd;
+        info->mf_supernodes = P.mf.nsuper;
+        info->mf_levels = P.mf.nlevels;
+        info->mf_max_front = P.mf.max_m;
+        info->mf_flops = P.mf.flops;
+        info->mf_update_bytes = P.mf.U_size * 8;
         std::strncpy(info->ordering, P.ordering.chosen.c_str(), sizeof(info->ordering) - 1);
     }
     if (ref_rows || ref_cols || owned) {
@@ -208,10 +214,83 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
                 if (owned) owned[e] = (r >= P.row_begin && r < P.row_end) ? 1 : 0;
             }
     }
+    if (perm_to_ref)
+        for (int64_t i = 0; i < P.n + 3; ++i) perm_to_ref[i] = ref[i];
     if (b_owned) {
         for (int64_t i = 0; i < P.n + 3; ++i)
             b_owned[ref[i]] = (i >= P.row_begin && i < P.row_end) || (i >= P.n && rank == world - 1) ? 1 : 0;
     }
+    return BOS_OK;
+}
+
+// Test hook: runs the multifrontal algorithm of hip/multifrontal.hip on the host with the plan's
+// tree and maps (validates the symbolic structure without a GPU). vals: CSR values of the plan's
+// H layout (as ordered by bos_plan_inspect), rhs / x: permuted order of length n. Not used by
+// any solve path.
+int bos_plan_mf_selftest(const bos_problem* pb, const double* vals, const double* rhs, double* x) {
+    if (!pb || !vals || !rhs || !x) return hfail(BOS_ERR_INVALID, "null argument");
+    bos::ProblemIndex pi;
+    pi.NP = pb->num_poses; pi.NL = pb->num_landmarks; pi.Mb = pb->num_bearings; pi.Mo = pb->num_odometry;
+    pi.fixed = pb->fixed_pose;
+    pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
+    bos::Plan P;
+    std::string err;
+    const int rc = bos::build_plan(pi, 0, 1, bos::kFactorMultifrontal, P, err);
+    if (rc) return hfail(rc, err);
+    const bos::Multifrontal& F = P.mf;
+    std::vector<double> L(F.L_size), U(F.U_size), u(F.u_size);
+    for (int64_t i = 0; i < P.n; ++i) x[i] = rhs[i];
+    for (int lv = 0; lv < F.nlevels; ++lv)
+        for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
+            const int s = F.level[q], k = F.k[s], r = F.r[s], m = k + r;
+            std::vector<double> W((size_t)m * m, 0.0);
+            for (int a = F.amap_ptr[s]; a < F.amap_ptr[s + 1]; ++a) W[F.amap_dst[a]] = vals[F.amap_src[a]];
+            for (int ci = F.child_ptr[s]; ci < F.child_ptr[s + 1]; ++ci) {
+                const int c = F.child[ci], rc2 = F.r[c];
+                const int32_t* map = F.rmap.data() + F.rmap_off[c];
+                for (int j = 0; j < rc2; ++j)
+                    for (int i = j; i < rc2; ++i) W[map[i] + (size_t)map[j] * m] += U[F.U_off[c] + i + (size_t)j * rc2];
+            }
+            for (int j = 0; j < k; ++j) {
+                const double d = std::sqrt(std::max(W[j + (size_t)j * m], 1e-300));
+                W[j + (size_t)j * m] = d;
+                for (int i = j + 1; i < m; ++i) W[i + (size_t)j * m] /= d;
+                for (int l = j + 1; l < m; ++l)
+                    for (int i = l; i < m; ++i) W[i + (size_t)l * m] -= W[i + (size_t)j * m] * W[l + (size_t)j * m];
+            }
+            for (int j = 0; j < k; ++j)
+                for (int i = 0; i < m; ++i) L[F.L_off[s] + i + (size_t)j * m] = W[i + (size_t)j * m];
+            for (int j = 0; j < r; ++j)
+                for (int i = 0; i < r; ++i) U[F.U_off[s] + i + (size_t)j * r] = W[(k + i) + (size_t)(k + j) * m];
+        }
+    for (int lv = 0; lv < F.nlevels; ++lv)
+        for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
+            const int s = F.level[q], k = F.k[s], r = F.r[s], m = k + r;
+            std::vector<double> w(m, 0.0);
+            for (int i = 0; i < k; ++i) w[i] = x[F.col0[s] + i];
+            for (int ci = F.child_ptr[s]; ci < F.child_ptr[s + 1]; ++ci) {
+                const int c = F.child[ci];
+                for (int t = 0; t < F.r[c]; ++t) w[F.rmap[F.rmap_off[c] + t]] += u[F.u_off[c] + t];
+            }
+            const double* Ls = L.data() + F.L_off[s];
+            for (int j = 0; j < k; ++j) {
+                w[j] /= Ls[j + (size_t)j * m];
+                for (int i = j + 1; i < m; ++i) w[i] -= Ls[i + (size_t)j * m] * w[j];
+            }
+            for (int i = 0; i < k; ++i) x[F.col0[s] + i] = w[i];
+            for (int t = 0; t < r; ++t) u[F.u_off[s] + t] = w[k + t];
+        }
+    for (int lv = F.nlevels - 1; lv >= 0; --lv)
+        for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
+            const int s = F.level[q], k = F.k[s], m = k + F.r[s];
+            const double* Ls = L.data() + F.L_off[s];
+            const int32_t* fi = F.findex.data() + F.findex_off[s];
+            for (int j = k - 1; j >= 0; --j) {
+                double acc = x[F.col0[s] + j];
+                for (int i = j + 1; i < m; ++i) acc -= Ls[i + (size_t)j * m] * x[fi[i]];
+                x[F.col0[s] + j] = acc / Ls[j + (size_t)j * m];
+            }
+        }
     return BOS_OK;
 }
 

@@ -13,6 +13,7 @@ namespace {
 constexpr int kWave = 64;             // wavefront width on CDNA4
 constexpr int kMaxPoseSegs = 7;       // 7 poses x 9 reduced values <= 64 lanes (one pass)
 constexpr int kMaxLmSegs = 12;        // 12 landmarks x 5 reduced values <= 64 lanes
+constexpr int kMfLeaf = 12;           // nested-dissection leaf size (nodes) for the multifrontal solver
 
 inline int node_size(int u, int NP) { return u < NP ? 3 : 2; }
 
@@ -127,7 +128,14 @@ SymbCost symbolic(const Graph& g, int NP, const std::vector<int32_t>& pos, const
 }
 
 // Nested dissection with BFS level-structure vertex separators (graph-based, no coordinates).
-void nested_dissection(const Graph& g, const std::vector<char>& active, std::vector<int32_t>& order, int leaf) {
+void nested_dissection(const Graph& g, const std::vector<char>& active, std::vector<int32_t>& order, int leaf,
+                       std::vector<std::pair<int32_t, int32_t>>* blocks) {
+    auto emit = [&](const std::vector<int32_t>& nodes) {
+        if (nodes.empty()) return;
+        const int32_t a = (int32_t)order.size();
+        order.insert(order.end(), nodes.begin(), nodes.end());
+        if (blocks) blocks->push_back({a, (int32_t)order.size()});
+    };
     const int n = g.n;
     std::vector<int32_t> stamp(n, -1), level(n, -1);
     int next_stamp = 0;
@@ -166,7 +174,7 @@ void nested_dissection(const Graph& g, const std::vector<char>& active, std::vec
         Job job = std::move(stack.back());
         stack.pop_back();
         if (job.emit || (int)job.nodes.size() <= leaf) {
-            order.insert(order.end(), job.nodes.begin(), job.nodes.end());
+            emit(job.nodes);
             continue;
         }
         const int st = next_stamp;
@@ -204,7 +212,7 @@ void nested_dissection(const Graph& g, const std::vector<char>& active, std::vec
         bfs(start, st, tmp, depth);
         const int h = depth + 1;
         if (h <= 2) {   // no useful level separator
-            order.insert(order.end(), tmp.begin(), tmp.end());
+            emit(tmp);
             continue;
         }
         std::vector<int64_t> cnt(h, 0);
@@ -244,7 +252,8 @@ void nested_dissection(const Graph& g, const std::vector<char>& active, std::vec
 
 }  // namespace
 
-int order_nodes(const ProblemIndex& pi, std::vector<int32_t>& node_pos, OrderingReport& rep, std::string& err) {
+int order_nodes(const ProblemIndex& pi, bool nd_only, std::vector<int32_t>& node_pos,
+                std::vector<std::pair<int32_t, int32_t>>* blocks, OrderingReport& rep, std::string& err) {
     const int NP = pi.NP, NL = pi.NL, n = NP + NL;
     const Graph g = build_graph(pi);
     // last pose observing each landmark (temporal key)
@@ -272,8 +281,18 @@ int order_nodes(const ProblemIndex& pi, std::vector<int32_t>& node_pos, Ordering
     std::vector<char> active(n, 1);
     if (pi.fixed >= 0) active[pi.fixed] = 0;
     std::vector<int32_t> ord_n;
-    nested_dissection(g, active, ord_n, 64);
+    nested_dissection(g, active, ord_n, nd_only ? kMfLeaf : 64, nd_only ? blocks : nullptr);
     if (ord_n.size() != active_nodes.size()) { err = "nested dissection lost nodes"; return BOS_ERR_INVALID; }
+    if (nd_only) {
+        std::vector<int32_t> pos;
+        order_to_pos(ord_n, pos);
+        const SymbCost c = symbolic(g, NP, pos, ord_n, nullptr, nullptr);
+        rep.flops_nd = c.flops;
+        rep.nnz_nd = c.nnz;
+        rep.chosen = "nested-dissection";
+        node_pos = pos;
+        return BOS_OK;
+    }
 
     struct Cand { const char* name; std::vector<int32_t>* ord; SymbCost c; };
     Cand cands[3] = {{"temporal", &ord_t, {}}, {"landmarks-first", &ord_s, {}}, {"nested-dissection", &ord_n, {}}};
@@ -295,7 +314,11 @@ int order_nodes(const ProblemIndex& pi, std::vector<int32_t>& node_pos, Ordering
 
 int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err);
 
-int build_plan(const ProblemIndex& pi, int rank, int world, bool want_factor, Plan& P, std::string& err) {
+int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
+                       const std::vector<std::pair<int32_t, int32_t>>& blocks, std::string& err);
+
+int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& P, std::string& err) {
+    const bool want_factor = factor_mode == kFactorScalar;
     const int NP = pi.NP, NL = pi.NL, n_nodes = NP + NL;
     if (NP <= 0) { err = "no poses"; return BOS_ERR_INVALID; }
     if (pi.fixed < 0 || pi.fixed >= NP) { err = "fixed pose stix out of range"; return BOS_ERR_INVALID; }
@@ -317,7 +340,8 @@ int build_plan(const ProblemIndex& pi, int rank, int world, bool want_factor, Pl
     }
     P = Plan();
     P.NP = NP; P.NL = NL; P.Mb = pi.Mb; P.Mo = pi.Mo; P.fixed = pi.fixed;
-    int rc = order_nodes(pi, P.node_pos, P.ordering, err);
+    std::vector<std::pair<int32_t, int32_t>> blocks;
+    int rc = order_nodes(pi, factor_mode == kFactorMultifrontal, P.node_pos, &blocks, P.ordering, err);
     if (rc) return rc;
     const Graph g = build_graph(pi);
     const int m = n_nodes - 1;
@@ -554,7 +578,149 @@ int build_plan(const ProblemIndex& pi, int rank, int world, bool want_factor, Pl
     if (rc) return rc;
     rc = build_list(false, P.lm_list);
     if (rc) return rc;
+    if (factor_mode == kFactorMultifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, err))) return rc;
     return validate_plan(pi, P, err);
+}
+
+int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
+                       const std::vector<std::pair<int32_t, int32_t>>& blocks, std::string& err) {
+    const int m = (int)inv.size();
+    Multifrontal& F = P.mf;
+    F = Multifrontal();
+    // node-level row structures of L -> column structures (rows ascending)
+    std::vector<int64_t> rptr;
+    std::vector<int32_t> rows;
+    symbolic(g, NP, P.node_pos, inv, &rptr, &rows);
+    std::vector<int64_t> cptr(m + 1, 0);
+    for (int32_t j : rows) ++cptr[j + 1];
+    for (int i = 0; i < m; ++i) cptr[i + 1] += cptr[i];
+    std::vector<int32_t> cols(rows.size());
+    {
+        std::vector<int64_t> w(cptr.begin(), cptr.end() - 1);
+        for (int i = 0; i < m; ++i)
+            for (int64_t e = rptr[i]; e < rptr[i + 1]; ++e) cols[w[rows[e]]++] = i;
+    }
+    const int ns = (int)blocks.size();
+    std::vector<int32_t> blk(m, -1);
+    for (int b = 0; b < ns; ++b)
+        for (int q = blocks[b].first; q < blocks[b].second; ++q) {
+            if (blk[q] != -1) { err = "multifrontal: overlapping supernodes"; return BOS_ERR_INVALID; }
+            blk[q] = b;
+        }
+    for (int q = 0; q < m; ++q)
+        if (blk[q] < 0) { err = "multifrontal: position not covered by a supernode"; return BOS_ERR_INVALID; }
+    F.nsuper = ns;
+    F.col0.resize(ns); F.k.resize(ns); F.r.resize(ns); F.parent.assign(ns, -1);
+    F.findex_off.resize(ns + 1);
+    std::vector<int32_t> stamp(m, -1), R;
+    for (int s = 0; s < ns; ++s) {
+        const int a = blocks[s].first, e = blocks[s].second;
+        R.clear();
+        for (int q = a; q < e; ++q)
+            for (int64_t t = cptr[q]; t < cptr[q + 1]; ++t) {
+                const int i = cols[t];
+                if (i >= e && stamp[i] != s) { stamp[i] = s; R.push_back(i); }
+            }
+        std::sort(R.begin(), R.end());
+        F.parent[s] = R.empty() ? -1 : blk[R[0]];
+        F.col0[s] = P.node_dof[inv[a]];
+        int k = 0;
+        for (int q = a; q < e; ++q) k += node_size(inv[q], NP);
+        F.k[s] = k;
+        F.findex_off[s] = (int64_t)F.findex.size();
+        for (int d = 0; d < k; ++d) F.findex.push_back(F.col0[s] + d);
+        int r = 0;
+        for (int q : R) {
+            const int u = inv[q];
+            for (int d = 0; d < node_size(u, NP); ++d) F.findex.push_back(P.node_dof[u] + d);
+            r += node_size(u, NP);
+        }
+        F.r[s] = r;
+    }
+    F.findex_off[ns] = (int64_t)F.findex.size();
+    auto front_pos = [&](int s, int32_t dof) -> int32_t {
+        const int k = F.k[s];
+        if (dof >= F.col0[s] && dof < F.col0[s] + k) return dof - F.col0[s];
+        const int32_t* b = F.findex.data() + F.findex_off[s] + k;
+        const int32_t* e = F.findex.data() + F.findex_off[s + 1];
+        const int32_t* it = std::lower_bound(b, e, dof);
+        if (it == e || *it != dof) return -1;
+        return k + (int32_t)(it - b);
+    };
+    // children, relative maps, offsets, levels
+    F.child_ptr.assign(ns + 1, 0);
+    for (int s = 0; s < ns; ++s) if (F.parent[s] >= 0) ++F.child_ptr[F.parent[s] + 1];
+    for (int s = 0; s < ns; ++s) F.child_ptr[s + 1] += F.child_ptr[s];
+    F.child.resize(F.child_ptr[ns]);
+    {
+        std::vector<int32_t> w(F.child_ptr.begin(), F.child_ptr.end() - 1);
+        for (int s = 0; s < ns; ++s) if (F.parent[s] >= 0) F.child[w[F.parent[s]]++] = s;
+    }
+    F.rmap_off.resize(ns + 1);
+    F.L_off.resize(ns); F.U_off.resize(ns); F.u_off.resize(ns);
+    std::vector<int32_t> lev(ns, 0);
+    for (int s = 0; s < ns; ++s) {
+        const int k = F.k[s], r = F.r[s], mm = k + r;
+        F.max_m = std::max(F.max_m, mm);
+        F.L_off[s] = F.L_size; F.L_size += (int64_t)mm * k;
+        F.U_off[s] = F.U_size; F.U_size += (int64_t)r * r;
+        F.u_off[s] = F.u_size; F.u_size += r;
+        F.flops += (double)k * k * k / 3.0 + (double)k * k * r + (double)k * r * r;
+        F.rmap_off[s] = (int64_t)F.rmap.size();
+        const int p = F.parent[s];
+        if (p >= 0) {
+            if (p <= s) { err = "multifrontal: parent precedes child"; return BOS_ERR_INVALID; }
+            for (int t = k; t < mm; ++t) {
+                const int32_t fp = front_pos(p, F.findex[F.findex_off[s] + t]);
+                if (fp < 0) { err = "multifrontal: update row missing from the parent front"; return BOS_ERR_INVALID; }
+                F.rmap.push_back(fp);
+            }
+            lev[p] = std::max(lev[p], lev[s] + 1);
+        } else if (r != 0) {
+            err = "multifrontal: root with update rows";
+            return BOS_ERR_INVALID;
+        }
+    }
+    F.rmap_off[ns] = (int64_t)F.rmap.size();
+    F.nlevels = 0;
+    for (int s = 0; s < ns; ++s) F.nlevels = std::max(F.nlevels, lev[s] + 1);
+    F.level_ptr.assign(F.nlevels + 1, 0);
+    for (int s = 0; s < ns; ++s) ++F.level_ptr[lev[s] + 1];
+    for (int l = 0; l < F.nlevels; ++l) F.level_ptr[l + 1] += F.level_ptr[l];
+    F.level.resize(ns);
+    {
+        std::vector<int32_t> w(F.level_ptr.begin(), F.level_ptr.end() - 1);
+        for (int s = 0; s < ns; ++s) F.level[w[lev[s]]++] = s;
+    }
+    // assembly map: every stored entry of H (row i >= col j) goes to the front of col j's supernode
+    std::vector<int32_t> sn_of_dof(P.n);
+    for (int s = 0; s < ns; ++s)
+        for (int d = 0; d < F.k[s]; ++d) sn_of_dof[F.col0[s] + d] = s;
+    const int64_t nnz = P.nnzA();
+    std::vector<int32_t> tgt(nnz), dst(nnz);
+    F.amap_ptr.assign(ns + 1, 0);
+    for (int64_t row = 0; row < P.n; ++row)
+        for (int64_t e = P.rowptr[row]; e < P.rowptr[row + 1]; ++e) {
+            const int32_t j = P.colind[e];
+            const int s = sn_of_dof[j];
+            const int32_t li = front_pos(s, (int32_t)row);
+            if (li < 0) { err = "multifrontal: H entry outside its front"; return BOS_ERR_INVALID; }
+            tgt[e] = s;
+            dst[e] = li + (j - F.col0[s]) * (F.k[s] + F.r[s]);
+            ++F.amap_ptr[s + 1];
+        }
+    for (int s = 0; s < ns; ++s) F.amap_ptr[s + 1] += F.amap_ptr[s];
+    F.amap_src.resize(nnz);
+    F.amap_dst.resize(nnz);
+    {
+        std::vector<int32_t> w(F.amap_ptr.begin(), F.amap_ptr.end() - 1);
+        for (int64_t e = 0; e < nnz; ++e) {
+            const int32_t q = w[tgt[e]]++;
+            F.amap_src[q] = (int32_t)e;
+            F.amap_dst[q] = dst[e];
+        }
+    }
+    return BOS_OK;
 }
 
 // Proves, on the host, that every address the J+H kernel writes (hip/kernels.hip diag_pos /

@@ -47,6 +47,29 @@ struct OrderingReport {
     int64_t nnz_temporal = 0, nnz_nd = 0;
 };
 
+// Supernodal multifrontal Cholesky structure (GPU solver, hip/multifrontal.hip). Supernodes are
+// the blocks of the nested-dissection ordering (contiguous position ranges); the assembly tree
+// links each supernode to the one holding the first row of its update matrix. Fronts are dense,
+// column-major, index list = [k own dofs | r update rows].
+struct Multifrontal {
+    int nsuper = 0, nlevels = 0, max_m = 0;
+    std::vector<int32_t> col0, k, r;        // per supernode: first dof, #own dofs, #update rows
+    std::vector<int64_t> findex_off;        // into findex (m = k + r entries; first k = col0..col0+k-1)
+    std::vector<int32_t> findex;
+    std::vector<int64_t> L_off;             // dense m x k panel (col-major) in the factor buffer
+    std::vector<int64_t> U_off;             // dense r x r update matrix (col-major)
+    std::vector<int64_t> u_off;             // r-vector (forward solve update)
+    std::vector<int32_t> parent;            // -1 for roots
+    std::vector<int32_t> child_ptr, child;  // children CSR
+    std::vector<int64_t> rmap_off;          // per supernode: r positions of its rows in the parent's front
+    std::vector<int32_t> rmap;
+    std::vector<int32_t> amap_ptr;          // per supernode: range into amap_src / amap_dst
+    std::vector<int32_t> amap_src, amap_dst;// value index in the CSR of H -> column-major front position
+    std::vector<int32_t> level_ptr, level;  // supernodes grouped by tree level (leaves first)
+    int64_t L_size = 0, U_size = 0, u_size = 0;
+    double flops = 0;
+};
+
 struct Plan {
     int NP = 0, NL = 0, Mb = 0, Mo = 0, fixed = -1;
     int64_t n = 0;                         // system size N - 3
@@ -56,6 +79,7 @@ struct Plan {
     std::vector<int32_t> node_base;        // entries before the diagonal block in each of its rows
     std::vector<int32_t> rowptr, colind;   // lower triangle of P^T H_nf P, n rows
     std::vector<int32_t> Lptr, Lind;       // symbolic Cholesky factor (lower, with diagonal)
+    Multifrontal mf;                       // built when factor_mode == kFactorMultifrontal
     WorkList pose_list, lm_list;
     OrderingReport ordering;
     // ownership for observation sharding: this rank writes rows [row_begin, row_end)
@@ -66,11 +90,18 @@ struct Plan {
     int64_t nnzL() const { return Lptr.empty() ? 0 : Lptr.back(); }
 };
 
-// Builds the plan. want_factor: compute the symbolic Cholesky pattern (sparse solver).
-// Returns 0 or a negative BOS_ERR_* code with a message in err.
-int build_plan(const ProblemIndex& pi, int rank, int world, bool want_factor, Plan& out, std::string& err);
+enum FactorMode {
+    kFactorNone = 0,          // dense solver: pattern only
+    kFactorScalar = 1,        // scalar CSR Cholesky pattern (rocSOLVER csrrf), cheapest-flops ordering
+    kFactorMultifrontal = 2,  // nested dissection + supernodal multifrontal structure (GPU solver)
+};
 
-// Exposed for tests: node ordering only (positions), and its symbolic cost.
-int order_nodes(const ProblemIndex& pi, std::vector<int32_t>& node_pos, OrderingReport& rep, std::string& err);
+// Builds the plan. Returns 0 or a negative BOS_ERR_* code with a message in err.
+int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& out, std::string& err);
+
+// Node ordering only (positions) and its symbolic cost. nd_only: force nested dissection and
+// return its blocks (contiguous position ranges: leaves and separators) in `blocks`.
+int order_nodes(const ProblemIndex& pi, bool nd_only, std::vector<int32_t>& node_pos,
+                std::vector<std::pair<int32_t, int32_t>>* blocks, OrderingReport& rep, std::string& err);
 
 }  // namespace bos

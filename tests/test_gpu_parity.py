@@ -120,18 +120,24 @@ def test_step_dx_matches_oracle(c1):
     dxg = S.last_dx()
     po, lo = Q.copy_state()
     _, _, dxo = O.step(Q, po, lo)
-    assert np.allclose(dxg, dxo, rtol=1e-9, atol=1e-12)
+    # two different direct factorizations (supernodal multifrontal vs SciPy SuperLU) of the same
+    # system: normwise agreement to ~cond(H_nf) * eps (host re-run of the same tree: 1.1e-10)
+    assert np.abs(dxg - dxo).max() <= 1e-8 * np.abs(dxo).max()
 
 
-def test_dense_solver_matches_sparse(c1):
-    A = bos.Solver(c1, solver=bos.BOS_SOLVER_SPARSE_CHOL)
-    B = bos.Solver(c1, solver=bos.BOS_SOLVER_DENSE_CHOL)
+@pytest.mark.parametrize("other", [bos.BOS_SOLVER_DENSE_CHOL, bos.BOS_SOLVER_ROCSOLVER_RF])
+def test_solvers_agree(c1, other):
+    """The supernodal multifrontal solver (default) against rocSOLVER dense potrf and
+    rocSOLVER csrrf on the same iterations."""
+    A = bos.Solver(c1, solver=bos.BOS_SOLVER_SUPERNODAL)
+    B = bos.Solver(c1, solver=other)
     A.step_n(5)
     B.step_n(5)
     pa, la = A.get_state()
     pb, lb = B.get_state()
-    ok, ep, el = _close_state(pa, la, pb, lb, rtol=1e-9, atol=1e-12)
+    ok, ep, el = _close_state(pa, la, pb, lb, rtol=1e-8, atol=1e-10)
     assert ok, (ep, el)
+    assert A.last_stats["solver_info"] == 0
 
 
 def test_step_n_equals_repeated_step(c1):
