@@ -63,18 +63,28 @@ bool make_synthetic(const SyntheticParams& p, SyntheticWorld& out) {
     std::vector<Win> wins;
     wins.reserve(NL);
     for (int k = 0; k < K; ++k) {
+        // balanced composition of NP poses into n windows (lengths within ~[base/2, 3*base/2],
+        // every length >= 2) so that ranges stay sensor-like (the dataset's max range is 5 m)
         const int n = per_lane[k];
-        const int extra = NP - 2 * n;
-        std::vector<int> cuts(n - 1);
-        for (int& c : cuts) c = (int)rng.below((uint64_t)extra + 1);
-        std::sort(cuts.begin(), cuts.end());
-        int start = 0, prev = 0;
+        const int base = NP / n;
+        std::vector<int> len(n);
+        // stagger the lanes: a random first window, the rest balanced
+        len[0] = n > 1 ? std::max(2, std::min(NP - 2 * (n - 1), 2 + (int)rng.below((uint64_t)std::max(1, base))))
+                       : NP;
+        if (n > 1) {
+            const int rem = NP - len[0], m = n - 1;
+            for (int j = 1; j < n; ++j) len[j] = rem / m + ((j - 1) < rem % m ? 1 : 0);
+            const int b2 = rem / m;
+            const int lo = std::max(2, b2 - b2 / 2), hi = b2 + b2 / 2 + 1;
+            for (int t = 0; t < 2 * m; ++t) {   // random neighbour transfers add jitter, keep the sum
+                const int a = 1 + (int)rng.below((uint64_t)m), b = a + 1 < n ? a + 1 : 1;
+                if (a != b && len[a] > lo && len[b] < hi) { --len[a]; ++len[b]; }
+            }
+        }
+        int st = 0;
         for (int j = 0; j < n; ++j) {
-            const int e = (j + 1 < n) ? cuts[j] : extra;
-            const int len = 2 + (e - prev);
-            prev = e;
-            wins.push_back({k, start, start + len - 1});
-            start += len;
+            wins.push_back({k, st, st + len[j] - 1});
+            st += len[j];
         }
     }
     // deterministic landmark order: by window start, then lane
@@ -89,9 +99,9 @@ bool make_synthetic(const SyntheticParams& p, SyntheticWorld& out) {
         const int L = w.last;
         const double side = (w.lane % 2) ? 1.0 : -1.0;
         double bx = 0, by = 0;
-        for (int attempt = 0; attempt < 24; ++attempt) {
-            const double f = rng.uniform(0.8, 3.0);
-            const double lat = side * rng.uniform(0.6, 4.0);
+        for (int attempt = 0; attempt < 64; ++attempt) {
+            const double f = rng.uniform(0.8, attempt < 32 ? 3.0 : 6.0);
+            const double lat = side * rng.uniform(0.4, attempt < 32 ? 4.0 : 6.0);
             bx = gx[L] + std::cos(gth[L]) * f - std::sin(gth[L]) * lat;
             by = gy[L] + std::sin(gth[L]) * f + std::cos(gth[L]) * lat;
             bool ok = true;

@@ -1,0 +1,207 @@
+"""The CPU oracle pinned against the reference's own checks and the independent NumPy restatement.
+
+Reference checks (no reference binary can be built here — Eigen3/OpenCV are absent):
+  * predict_bearing known answers            tests/solver_stuff.cpp:25-38
+  * predict_odometry(IG) == measurement      tests/solver_stuff.cpp:93-114
+  * analytic vs numerical Jacobians          tests/solver_stuff.cpp:42-89, :117-163 (recorded fp32 bounds)
+  * "converged in ~20 iterations"            README.md:22-24
+Independent restatement: tests/golden/make_golden.py -> tests/golden/{mini,c1}.npz.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import C1, C1_GT, MINI
+
+PI = math.pi
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_predict_bearing_kats(precision):
+    tol = 1e-12 if precision == 64 else 1e-6
+    f = lambda p, l: O.predict_bearing(p, l, precision)  # noqa: E731
+    assert abs(f((0, 0, 0), (1, 0))) <= tol
+    assert abs(f((0, 0, 0), (0, 1)) - PI / 2) <= tol
+    assert abs(abs(f((0, 0, 0), (-1, 0))) - PI) <= tol
+    assert abs(f((0, 0, 0), (0, -1)) + PI / 2) <= tol
+    assert abs(f((0, 0, 0), (1, 1)) - PI / 4) <= tol
+    assert abs(f((0, 0, PI / 2), (1, 1)) + PI / 4) <= tol
+    assert abs(abs(f((0, 0, PI), (1, 0))) - PI) <= tol
+
+
+def test_normalized_angle_half_open():
+    # slam/solver_jacobians.cpp:325-333: [-pi, pi), compared against double CV_PI
+    assert O.normalized_angle(PI) == pytest.approx(-PI)
+    assert O.normalized_angle(-PI) == pytest.approx(-PI)
+    assert O.normalized_angle(3 * PI + 0.1) == pytest.approx(-PI + 0.1)
+    assert O.normalized_angle(-7.0) == pytest.approx(-7.0 + 2 * PI)
+    # float argument compared in double: (float)pi > CV_PI, so it wraps
+    f_pi = np.float32(PI)
+    assert float(f_pi) > PI
+    assert O.normalized_angle(float(f_pi), 32) < 0
+
+
+def test_smallest_angle():
+    assert O.smallest_angle(0.5) == 0.5
+    assert O.smallest_angle(7.0) == pytest.approx(7.0 - 2 * PI)
+    assert O.smallest_angle(-4.0) == pytest.approx(-4.0 + 2 * PI)
+
+
+@pytest.fixture(scope="module")
+def c1():
+    return O.load(C1)
+
+
+def test_dataset_sizes(c1):
+    assert (c1.NP, c1.NL, len(c1.b_z), len(c1.o_z), c1.N) == (301, 141, 2132, 300, 1185)
+    assert int(c1.pose_ids[c1.fixed]) == 1498
+    # single-observation landmarks noted by the reference (slam/triangulation.cpp:38-42)
+    cnt = np.bincount(c1.b_lm, minlength=c1.NL)
+    assert set(int(i) for i in c1.lm_ids[cnt == 1]) == {69, 112, 114}
+
+
+def test_single_observation_landmarks_basic_solution(c1):
+    cnt = np.bincount(c1.b_lm, minlength=c1.NL)
+    for j in np.nonzero(cnt == 1)[0]:
+        # column-pivoted QR on one row: the non-pivot component is exactly 0
+        assert (c1.lm_xy[j] == 0.0).sum() == 1
+
+
+def test_predict_odometry_reproduces_ig(c1):
+    """tests/solver_stuff.cpp:93-114: the IG poses are the dead-reckoned odometry chain."""
+    err = 0.0
+    for k in range(len(c1.o_z)):
+        pred = O.predict_odometry(c1.pose_xyt[c1.o_src[k]], c1.pose_xyt[c1.o_dst[k]])
+        d = pred - c1.o_z[k]
+        d[2] = (d[2] + PI) % (2 * PI) - PI
+        err = max(err, np.abs(d).max())
+    assert err < 2.5e-4   # the g2o file prints 6 significant digits (coordinates up to ~30 m)
+
+
+def _gt_problem():
+    g = O.parse_g2o(C1_GT)
+    ig = O.load(C1)
+    lid = {int(i): k for k, i in enumerate(g.lm_vertex_ids)}
+    lm = np.array([g.lm_vertex_xy[lid[int(i)]] for i in ig.lm_ids])
+    pose = np.array(g.pose_xyt, dtype=np.float64)
+    pose[:, 2] = [O.normalized_angle(t) for t in pose[:, 2]]
+    return ig, pose, lm
+
+
+def test_bearing_jacobian_numerical_fp64():
+    ig, pose, lm = _gt_problem()
+    eps = 1e-6
+    worst = 0.0
+    for k in range(len(ig.b_z)):
+        p, l, z = pose[ig.b_pose[k]], lm[ig.b_lm[k]], ig.b_z[k]
+        _, J = O.bearing_error_and_jacobian(p, l, z)
+        num = np.zeros(5)
+        for c in range(5):
+            d = np.zeros(5)
+            d[c] = eps
+            # boxplus: pose X' = v2t(dx) X (left), landmark l' = l + dl
+            def err(dd):
+                th = dd[2]
+                cs, sn = math.cos(th), math.sin(th)
+                q = np.array([cs * p[0] - sn * p[1] + dd[0], sn * p[0] + cs * p[1] + dd[1], p[2] + th])
+                e, _ = O.bearing_error_and_jacobian(q, l + dd[3:], z)
+                return e
+            ep, em = err(d), err(-d)
+            de = (ep - em + PI) % (2 * PI) - PI
+            num[c] = de / (2 * eps)
+        worst = max(worst, np.abs(num - J).max() / max(1.0, np.abs(J).max()))
+    assert worst < 1e-6
+
+
+def test_odometry_jacobian_numerical_fp64(c1):
+    eps = 1e-6
+    worst = 0.0
+    for k in range(len(c1.o_z)):
+        s, d, z = c1.pose_xyt[c1.o_src[k]], c1.pose_xyt[c1.o_dst[k]], c1.o_z[k]
+        _, J = O.odometry_error_and_jacobian(s, d, z)
+
+        def box(p, dd):
+            cs, sn = math.cos(dd[2]), math.sin(dd[2])
+            return np.array([cs * p[0] - sn * p[1] + dd[0], sn * p[0] + cs * p[1] + dd[1], p[2] + dd[2]])
+
+        num = np.zeros((3, 6))
+        for c in range(6):
+            dd = np.zeros(6)
+            dd[c] = eps
+            ep, _ = O.odometry_error_and_jacobian(box(s, dd[:3]), box(d, dd[3:]), z)
+            em, _ = O.odometry_error_and_jacobian(box(s, -dd[:3]), box(d, -dd[3:]), z)
+            de = ep - em
+            de[2] = (de[2] + PI) % (2 * PI) - PI
+            num[:, c] = de / (2 * eps)
+        worst = max(worst, np.abs(num - J).max() / max(1.0, np.abs(J).max()))
+    assert worst < 1e-6
+
+
+def test_bearing_jacobian_fp32_within_reference_bounds():
+    """The reference's own harness (fp32, eps = 1e-3, GT state) recorded highest_max 0.0131645
+    and average_max 0.000166852 (tests/solver_stuff.cpp:82-88)."""
+    ig, pose, lm = _gt_problem()
+    eps = np.float32(1e-3)
+    maxs = []
+    for k in range(len(ig.b_z)):
+        p = pose[ig.b_pose[k]].astype(np.float32)
+        l = lm[ig.b_lm[k]].astype(np.float32)
+        z = np.float32(ig.b_z[k])
+        _, J = O.bearing_error_and_jacobian(p, l, z, 32)
+        num = np.zeros(5, dtype=np.float32)
+        for c in range(5):
+            def err(sign):
+                dd = np.zeros(5, dtype=np.float32)
+                dd[c] = sign * eps
+                cs, sn = np.float32(math.cos(dd[2])), np.float32(math.sin(dd[2]))
+                q = np.array([cs * p[0] - sn * p[1] + dd[0], sn * p[0] + cs * p[1] + dd[1], p[2] + dd[2]],
+                             dtype=np.float32)
+                e, _ = O.bearing_error_and_jacobian(q, l + dd[3:], z, 32)
+                return np.float32(e)
+            num[c] = (err(1) - err(-1)) / (np.float32(2) * eps)
+        maxs.append(float(np.abs(num - J).max()))
+    assert max(maxs) <= 0.0131645 * 1.5
+    assert np.mean(maxs) <= 0.000166852 * 1.5
+
+
+def test_golden_crosscheck(golden):
+    """Oracle (C++) vs the independent vectorised NumPy restatement."""
+    for name, path in (("mini", MINI), ("c1", C1)):
+        g = golden(name)
+        P = O.load(path)
+        assert np.abs(P.lm_xy - g["L0"]).max() < 1e-9
+        lin = O.linearize(P)
+        H = O.assemble_H(P, lin)
+        assert H.nnz == int(g["H_nnz"])
+        hv = H @ g["H_V"]
+        assert np.abs(hv - g["H_HV"]).max() <= 1e-12 * np.abs(g["H_HV"]).max()
+        assert np.abs(lin.b - g["b0"]).max() <= 1e-11 * np.abs(g["b0"]).max()
+        X, L, chi = O.run(P, 50)
+        assert np.allclose(chi, g["chi2"], rtol=1e-9, atol=1e-15)
+        for it in (50,):
+            assert np.abs(X - g[f"X{it}"]).max() < 1e-8
+            assert np.abs(L - g[f"L{it}"]).max() < 1e-8
+
+
+def test_convergence_pins(c1):
+    """chi^2 before the robust kernel: 96.864254 at iteration 0 and 5.882761 at 49 (an
+    independent survey-time restatement); ~20 iterations to converge (README)."""
+    _, _, chi = O.run(c1, 50)
+    assert chi[0] == pytest.approx(96.864254, abs=1e-5)
+    assert chi[49] == pytest.approx(5.882761, abs=1e-5)
+    assert abs(chi[19] - chi[49]) < 1e-4
+    assert all(chi[i + 1] <= chi[i] + 1e-9 for i in range(49))
+
+
+def test_accuracy_vs_ground_truth(c1):
+    """Accuracy, not parity: the gauge is shared (pose 1498 fixed at the same value in both
+    files); the optimum roughly halves the initial guess's median pose error (measured:
+    1.69 m -> 0.74 m median, 3.32 m -> 1.89 m max)."""
+    _, pose_gt, lm_gt = _gt_problem()
+    X, L, _ = O.run(c1, 50)
+    e0 = np.linalg.norm(c1.pose_xyt[:, :2] - pose_gt[:, :2], axis=1)
+    e1 = np.linalg.norm(X[:, :2] - pose_gt[:, :2], axis=1)
+    assert np.median(e1) < 0.5 * np.median(e0)
+    assert e1.max() < e0.max()
