@@ -1,18 +1,17 @@
 // HIP kernels of one Gauss-Newton iteration for 2-D bearing-only SLAM on MI355X (gfx950).
 //
-// J+H build (the hot path, reference slam/solver.cpp:28-69 + solver_jacobians.cpp:9-168):
-// ONE launch, two kinds of workgroups:
-//   * pose-centric tasks: a wavefront owns a run of whole poses; lane = one bearing or one side
-//     of an odometry edge incident to those poses. It evaluates e and J, applies the robust
-//     kernel (scales e only, solver.cpp:37-41/54-58), reduces the pose-diagonal 3x3 blocks and
-//     b_pose across its lanes through LDS in a fixed order (deterministic, no atomics), writes
-//     the off-diagonal blocks whose CSR row belongs to the pose, and the chi^2 partial.
-//   * landmark-centric tasks: the same for whole landmarks (2x2 diagonal, b_landmark and the
-//     landmark-row off-diagonal blocks). A bearing is evaluated once on each side instead of
-//     being scattered with atomics: recomputing ~100 flops is cheaper than a scattered 40-byte
-//     atomic/partial round trip through HBM.
-// All outputs of the two task kinds are disjoint, so the launch has no inter-workgroup
-// communication. Damping (solver.cpp:64-69) is folded into the diagonal writes.
+// J+H build (the hot path, reference slam/solver.cpp:28-69 + solver_jacobians.cpp:9-168), one
+// launch. A wavefront owns a task = a contiguous range of nodes in elimination order (host/plan.cpp
+// build_tasks), so the CSR rows it produces are ONE contiguous span of the value array:
+//   1. lane = one observation incident to the task's nodes: error, Jacobian, robust kernel
+//      (scales e only, solver.cpp:37-41/54-58); its per-side contributions (diagonal block + b)
+//      go to LDS slots and its off-diagonal block, when the block's row lives in this task, goes
+//      straight into the LDS image of the rows;
+//   2. lanes (node, value) reduce the slots in a fixed order (deterministic, no atomics) into the
+//      diagonal blocks (+ damping, solver.cpp:64-69) and b;
+//   3. the row image and b are stored with coalesced writes.
+// An observation whose endpoints lie in two tasks is evaluated in both; no workgroup reads what
+// another writes, so the launch has no inter-workgroup communication.
 #include "kernels.hpp"
 
 #include "../host/bos_math.hpp"
@@ -28,16 +27,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// position of entry (r, c) of the diagonal block of a node whose rows start at row0 with `base`
-// entries of off-diagonal blocks before the diagonal (host/plan.cpp layout)
-__device__ __forceinline__ int diag_pos(int row0, int base, int r, int c) {
-    return row0 + r * base + ((r * (r + 1)) >> 1) + base + c;
-}
-// position of entry (r, c) of an off-diagonal block whose row-0 entry is at slot
-__device__ __forceinline__ int off_pos(int slot, int base, int r, int c) {
-    return slot + r * base + ((r * (r + 1)) >> 1) + c;
-}
-
 template <typename T> __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -50,227 +39,259 @@ __device__ __forceinline__ void tri_rc(int rv, int& r, int& c) {
     c = rv - ((r * (r + 1)) >> 1);
 }
 
-template <typename T, bool HAS_W, bool HAS_GROUPS>
-__device__ __forceinline__ void pose_task(const LinParams<T>& P, int t, int lane, T (*red)[64], T (*offr)[64]) {
-    const int s0 = P.a_task[t], s1 = P.a_task[t + 1];
-    const int i0 = P.a_seg_item[s0], i1 = P.a_seg_item[s1];
-    const int nseg = s1 - s0;
-    // reducer role: lane -> (segment rs, value rv) of the 9 reduced values per pose
-    const int rs = lane / 9, rv = lane - 9 * (lane / 9);
-    const bool reducer = rs < nseg;
-    int r_beg = 0, r_end = 0;
-    if (reducer) { r_beg = P.a_seg_item[s0 + rs]; r_end = P.a_seg_item[s0 + rs + 1]; }
-    T acc = (T)0;
+// Contributions of one side of an observation go to slots[v][2 * entry + side]: pose side 9
+// values (H 00,10,11,20,21,22, b 0..2), landmark side 5 values (H 00,10,11, b 0,1).
+
+template <typename T, bool HAS_W, bool HAS_DUPS>
+__device__ __forceinline__ void eval_bearing(const LinParams<T>& P, int i, int ll, T* rows, T (*slots)[kSlots],
+                                             double& chi, int& nrob) {
+    const int meta = P.be_meta[i];
+    const int p = P.be_pose[i], l = P.be_lm[i];
+    const T px = P.pc[4 * p], py = P.pc[4 * p + 1], c = P.pc[4 * p + 2], sn = P.pc[4 * p + 3];
+    const T lx = P.lc[2 * l], ly = P.lc[2 * l + 1];
+    T J[5];
+    T e = bos::bearing_error_jacobian<T>(px, py, c, sn, lx, ly, P.be_z[i], J);   // solver_jacobians.cpp:9-95
+    const T w = HAS_W ? P.be_w[i] : (T)1;
+    const T rho = e * w * e;                                                        // solver.cpp:37
+    if (meta & 4) chi += (double)rho;
+    if (rho > P.kt) {                                                               // solver.cpp:38-40
+        e *= sqrt(P.kt / rho);
+        if (meta & 4) ++nrob;
+    }
+    // H += (J^T w) J, b += (J^T w) e  (solver.cpp:44-45)
+    const T wJ0 = J[0] * w, wJ1 = J[1] * w, wJ2 = J[2] * w, wJ3 = J[3] * w, wJ4 = J[4] * w;
+    if (meta & 1) {
+        slots[0][2 * ll] = wJ0 * J[0];
+        slots[1][2 * ll] = wJ1 * J[0];
+        slots[2][2 * ll] = wJ1 * J[1];
+        slots[3][2 * ll] = wJ2 * J[0];
+        slots[4][2 * ll] = wJ2 * J[1];
+        slots[5][2 * ll] = wJ2 * J[2];
+        slots[6][2 * ll] = wJ0 * e;
+        slots[7][2 * ll] = wJ1 * e;
+        slots[8][2 * ll] = wJ2 * e;
+    }
+    if (meta & 2) {
+        slots[0][2 * ll + 1] = wJ3 * J[3];
+        slots[1][2 * ll + 1] = wJ4 * J[3];
+        slots[2][2 * ll + 1] = wJ4 * J[4];
+        slots[3][2 * ll + 1] = wJ3 * e;
+        slots[4][2 * ll + 1] = wJ4 * e;
+    }
+    if (meta & 8) {
+        const T wo = HAS_DUPS ? P.be_woff[i] : w;
+        T* blk = rows + (meta >> 8);
+        if (meta & 16) {   // landmark rows (2) x pose cols (3)
+            const int base = P.node_base[P.NP + l];
+            const T a0 = J[3] * wo, a1 = J[4] * wo;
+            blk[0] = a0 * J[0]; blk[1] = a0 * J[1]; blk[2] = a0 * J[2];
+            blk += base + 1;
+            blk[0] = a1 * J[0]; blk[1] = a1 * J[1]; blk[2] = a1 * J[2];
+        } else {           // pose rows (3) x landmark cols (2)
+            const int base = P.node_base[p];
+            const T a0 = J[0] * wo, a1 = J[1] * wo, a2 = J[2] * wo;
+            blk[0] = a0 * J[3]; blk[1] = a0 * J[4];
+            blk += base + 1;
+            blk[0] = a1 * J[3]; blk[1] = a1 * J[4];
+            blk += base + 2;
+            blk[0] = a2 * J[3]; blk[1] = a2 * J[4];
+        }
+    }
+}
+
+// Odometry edge (solver_jacobians.cpp:97-168). J_dst = -J_src exactly in the reference's
+// Jacobian (:137-146: (DR' R_s)^T = -R_s^T DR' since DR' is antisymmetric), so
+// H_ss = H_dd = J_s^T Omega J_s, H_sd = -H_ss, b_d = -b_s.
+template <typename T, bool HAS_DUPS>
+__device__ __forceinline__ void eval_odometry(const LinParams<T>& P, int j, int ll, T* rows, T (*slots)[kSlots],
+                                              double& chi, int& nrob) {
+    const int meta = P.oe_meta[j];
+    const int k = P.oe_edge[j];
+    const int ps = P.o_src[k], pd = P.o_dst[k];
+    const T xs = P.pc[4 * ps], ys = P.pc[4 * ps + 1], cs = P.pc[4 * ps + 2], ss = P.pc[4 * ps + 3];
+    const T xd = P.pc[4 * pd], yd = P.pc[4 * pd + 1];
+    const T tx = xd - xs, ty = yd - ys;
+    const T e0 = (cs * tx + ss * ty) - P.o_z[3 * k];                                // :106, :319
+    const T e1 = (-ss * tx + cs * ty) - P.o_z[3 * k + 1];
+    const T e2 = bos::normalized_angle<T>(bos::normalized_angle<T>(P.pth[pd] - P.pth[ps]) - P.o_z[3 * k + 2]);
+    const T t0 = -ss * xd + cs * yd, t1 = -cs * xd - ss * yd;                       // :139
+    // J_s = [[-cs, -ss, t0], [ss, -cs, t1], [0, 0, -1]]
+    const T* u = P.o_om + 6 * k;
+    const T o00 = u[0], o01 = u[1], o02 = u[2], o11 = u[3], o12 = u[4], o22 = u[5];
+    T Oe0 = o00 * e0 + o01 * e1 + o02 * e2;
+    T Oe1 = o01 * e0 + o11 * e1 + o12 * e2;
+    T Oe2 = o02 * e0 + o12 * e1 + o22 * e2;
+    const T rho = e0 * Oe0 + e1 * Oe1 + e2 * Oe2;                                   // solver.cpp:54
+    if (meta & 4) chi += (double)rho;
+    if (rho > P.kt) {                                                               // :55-57
+        const T sc = sqrt(P.kt / rho);
+        Oe0 *= sc; Oe1 *= sc; Oe2 *= sc;
+        if (meta & 4) ++nrob;
+    }
+    // Omega J_s, column by column
+    const T a00 = -o00 * cs + o01 * ss, a01 = -o00 * ss - o01 * cs, a02 = o00 * t0 + o01 * t1 - o02;
+    const T a10 = -o01 * cs + o11 * ss, a11 = -o01 * ss - o11 * cs, a12 = o01 * t0 + o11 * t1 - o12;
+    const T a20 = -o02 * cs + o12 * ss, a21 = -o02 * ss - o12 * cs, a22 = o02 * t0 + o12 * t1 - o22;
+    // H_ss = J_s^T (Omega J_s): J_s^T row r = column r of J_s
+    const T h00 = -cs * a00 + ss * a10;
+    const T h10 = -ss * a00 - cs * a10;
+    const T h11 = -ss * a01 - cs * a11;
+    const T h20 = t0 * a00 + t1 * a10 - a20;
+    const T h21 = t0 * a01 + t1 * a11 - a21;
+    const T h22 = t0 * a02 + t1 * a12 - a22;
+    const T b0 = -cs * Oe0 + ss * Oe1, b1 = -ss * Oe0 - cs * Oe1, b2 = t0 * Oe0 + t1 * Oe1 - Oe2;
+    if (meta & 1) {
+        slots[0][2 * ll] = h00; slots[1][2 * ll] = h10; slots[2][2 * ll] = h11;
+        slots[3][2 * ll] = h20; slots[4][2 * ll] = h21; slots[5][2 * ll] = h22;
+        slots[6][2 * ll] = b0; slots[7][2 * ll] = b1; slots[8][2 * ll] = b2;
+    }
+    if (meta & 2) {
+        slots[0][2 * ll + 1] = h00; slots[1][2 * ll + 1] = h10; slots[2][2 * ll + 1] = h11;
+        slots[3][2 * ll + 1] = h20; slots[4][2 * ll + 1] = h21; slots[5][2 * ll + 1] = h22;
+        slots[6][2 * ll + 1] = -b0; slots[7][2 * ll + 1] = -b1; slots[8][2 * ll + 1] = -b2;
+    }
+    if (meta & 8) {
+        T g00 = h00, g10 = h10, g11 = h11, g20 = h20, g21 = h21, g22 = h22;
+        if (HAS_DUPS) {   // summed information of a duplicate group
+            const T* v = P.oe_omoff + 6 * j;
+            const T q00 = -v[0] * cs + v[1] * ss, q01 = -v[0] * ss - v[1] * cs, q02 = v[0] * t0 + v[1] * t1 - v[2];
+            const T q10 = -v[1] * cs + v[3] * ss, q11 = -v[1] * ss - v[3] * cs, q12 = v[1] * t0 + v[3] * t1 - v[4];
+            const T q20 = -v[2] * cs + v[4] * ss, q21 = -v[2] * ss - v[4] * cs, q22 = v[2] * t0 + v[4] * t1 - v[5];
+            g00 = -cs * q00 + ss * q10; g10 = -ss * q00 - cs * q10; g11 = -ss * q01 - cs * q11;
+            g20 = t0 * q00 + t1 * q10 - q20; g21 = t0 * q01 + t1 * q11 - q21; g22 = t0 * q02 + t1 * q12 - q22;
+        }
+        // H_sd = -H_ss (symmetric), rows of the owner x cols of the other pose
+        const int base = P.node_base[(meta & 16) ? pd : ps];
+        T* blk = rows + (meta >> 8);
+        blk[0] = -g00; blk[1] = -g10; blk[2] = -g20;
+        blk += base + 1;
+        blk[0] = -g10; blk[1] = -g11; blk[2] = -g21;
+        blk += base + 2;
+        blk[0] = -g20; blk[1] = -g21; blk[2] = -g22;
+    }
+}
+
+// per-wave LDS tables of a task (kMaxTaskNodes nodes, <= 2 x 64 contribution slots)
+struct TaskTables {
+    int32_t node_base[kMaxTaskNodes];
+    int16_t node_rel[kMaxTaskNodes];    // row start relative to the task's first value (< kStageCap)
+    int16_t node_dof[kMaxTaskNodes];    // relative to the task's first dof
+    int16_t node_cl[kMaxTaskNodes + 1]; // contribution-list range, relative to the task's first
+    uint8_t node_pose[kMaxTaskNodes];
+    uint8_t pair_node[9 * kMaxTaskNodes];
+    uint8_t pair_val[9 * kMaxTaskNodes];
+    uint16_t cl[kSlots];
+};
+
+template <typename T, bool HAS_W, bool HAS_DUPS>
+__device__ __forceinline__ void range_task(const LinParams<T>& P, int t, int lane, T* rowimg, T (*slots)[kSlots],
+                                           T* bimg, TaskTables& tb) {
+    const int q0 = P.task_q[t], q1 = P.task_q[t + 1];
+    const int flags = P.task_flags[t];
+    const bool staged = flags & 1, single = flags & 2;
+    const int v0 = P.pos_row0[q0], v1 = P.pos_row0[q1];
+    const int d0 = P.pos_dof[q0], d1 = P.pos_dof[q1];
+    T* rows = staged ? rowimg : P.val + v0;
+    T* bb = staged ? bimg : P.b + d0;
+    const int be0 = P.task_be[t], nb = P.task_be[t + 1] - be0;
+    const int oe0 = P.task_oe[t], ne = nb + P.task_oe[t + 1] - oe0;
+    const int nn = q1 - q0;
+    // prologue: node table and contribution lists into LDS (independent of the entry loads)
+    int npairs = 0;
+    if (!single) {
+        const int cl0 = P.cl_ptr[q0], ncl = P.cl_ptr[q1] - cl0;
+        int nv = 0;
+        if (lane < nn) {
+            const int q = q0 + lane;
+            const bool pose = P.pos_node[q] < P.NP;
+            nv = pose ? 9 : 5;
+            tb.node_rel[lane] = (int16_t)(P.pos_row0[q] - v0);
+            tb.node_base[lane] = P.pos_base[q];
+            tb.node_dof[lane] = (int16_t)(P.pos_dof[q] - d0);
+            tb.node_cl[lane] = (int16_t)(P.cl_ptr[q] - cl0);
+            tb.node_pose[lane] = pose;
+        }
+        if (lane == 0) tb.node_cl[nn] = (int16_t)ncl;
+        for (int x = lane; x < ncl; x += 64) tb.cl[x] = P.cl[cl0 + x];
+        // exclusive prefix sum of the value counts -> pair table
+        int incl = nv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        npairs = __shfl(incl, 63);
+        for (int v = 0; v < nv; ++v) {
+            tb.pair_node[incl - nv + v] = (uint8_t)lane;
+            tb.pair_val[incl - nv + v] = (uint8_t)v;
+        }
+    }
     double chi = 0.0;
     int nrob = 0;
-    for (int c0 = i0; c0 < i1; c0 += 64) {
-        const int i = c0 + lane;
-        T v[9], off[9];
+    T acc = (T)0;   // single-node tasks: lane v < size accumulates value v over all chunks
+    for (int c0 = 0; c0 < ne; c0 += 64) {
+        const int e = c0 + lane;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) { v[k] = (T)0; off[k] = (T)0; }
-        int slot = -1, grp = i, ncol = 0, base = 0;
-        if (i < i1) {
-            int s = s0;
-            while (s + 1 < s1 && P.a_seg_item[s + 1] <= i) ++s;
-            const int p = P.a_seg_node[s];
-            const int other = P.a_other[i];
-            slot = P.a_slot[i];
-            if (HAS_GROUPS) grp = P.a_grp[i];
-            if (slot >= 0) base = P.p_base[p];
-            if (other >= 0) {
-                // ---- bearing (solver_jacobians.cpp:9-95), pose side
-                const T px = P.pc[4 * p], py = P.pc[4 * p + 1], c = P.pc[4 * p + 2], sn = P.pc[4 * p + 3];
-                const T lx = P.lc[2 * other], ly = P.lc[2 * other + 1];
-                T J[5];
-                T e = bos::bearing_error_jacobian<T>(px, py, c, sn, lx, ly, P.a_z[i], J);
-                const T w = HAS_W ? P.a_w[i] : (T)1;
-                const T rho = e * w * e;                                    // solver.cpp:37
-                chi += (double)rho;
-                if (rho > P.kt) { e *= sqrt(P.kt / rho); ++nrob; }          // :38-40
-                T wJ[3];
-#pragma unroll
-                for (int r = 0; r < 3; ++r) wJ[r] = J[r] * w;
-                v[0] = wJ[0] * J[0];
-                v[1] = wJ[1] * J[0]; v[2] = wJ[1] * J[1];
-                v[3] = wJ[2] * J[0]; v[4] = wJ[2] * J[1]; v[5] = wJ[2] * J[2];
-                v[6] = wJ[0] * e; v[7] = wJ[1] * e; v[8] = wJ[2] * e;       // :45
-#pragma unroll
-                for (int r = 0; r < 3; ++r) { off[3 * r] = wJ[r] * J[3]; off[3 * r + 1] = wJ[r] * J[4]; }
-                ncol = 2;
-            } else {
-                // ---- odometry edge side (solver_jacobians.cpp:97-168)
-                const int code = -other - 1;
-                const int k = code >> 1, side = code & 1;
-                const int ps = P.o_src[k], pd = P.o_dst[k];
-                const T xs = P.pc[4 * ps], ys = P.pc[4 * ps + 1], cs = P.pc[4 * ps + 2], ss = P.pc[4 * ps + 3];
-                const T xd = P.pc[4 * pd], yd = P.pc[4 * pd + 1];
-                T e[3], J[18];
-                bos::odometry_error_jacobian<T>(xs, ys, P.pth[ps], cs, ss, xd, yd, P.pth[pd], P.o_z[3 * k],
-                                                P.o_z[3 * k + 1], P.o_z[3 * k + 2], e, J);
-                const T* u = P.o_om + 6 * k;
-                const T Om[9] = {u[0], u[1], u[2], u[1], u[3], u[4], u[2], u[4], u[5]};
-                T Oe[3];
-#pragma unroll
-                for (int r = 0; r < 3; ++r) Oe[r] = Om[3 * r] * e[0] + Om[3 * r + 1] * e[1] + Om[3 * r + 2] * e[2];
-                const T rho = e[0] * Oe[0] + e[1] * Oe[1] + e[2] * Oe[2];  // solver.cpp:54
-                if (side == 0) chi += (double)rho;
-                if (rho > P.kt) {                                           // :55-57
-                    const T sc = sqrt(P.kt / rho);
-#pragma unroll
-                    for (int r = 0; r < 3; ++r) Oe[r] *= sc;
-                    if (side == 0) ++nrob;
-                }
-                const int me = 3 * side, ot = 3 - me;
-                T OJ[9];   // Omega * J_me
-#pragma unroll
-                for (int r = 0; r < 3; ++r)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c)
-                        OJ[3 * r + c] = Om[3 * r] * J[me + c] + Om[3 * r + 1] * J[6 + me + c] + Om[3 * r + 2] * J[12 + me + c];
-#pragma unroll
-                for (int rv2 = 0; rv2 < 6; ++rv2) {
-                    int r, c;
-                    tri_rc(rv2, r, c);
-                    v[rv2] = J[me + r] * OJ[c] + J[6 + me + r] * OJ[3 + c] + J[12 + me + r] * OJ[6 + c];
-                }
-#pragma unroll
-                for (int r = 0; r < 3; ++r) v[6 + r] = J[me + r] * Oe[0] + J[6 + me + r] * Oe[1] + J[12 + me + r] * Oe[2];
-#pragma unroll
-                for (int r = 0; r < 3; ++r)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c)
-                        off[3 * r + c] = OJ[r] * J[ot + c] + OJ[3 + r] * J[6 + ot + c] + OJ[6 + r] * J[12 + ot + c];
-                ncol = 3;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 9; ++k) red[k][lane] = v[k];
-        if (HAS_GROUPS) {
-#pragma unroll
-            for (int k = 0; k < 9; ++k) offr[k][lane] = off[k];
-        }
+        for (int v = 0; v < 9; ++v) { slots[v][2 * lane] = (T)0; slots[v][2 * lane + 1] = (T)0; }
+        if (e < nb) eval_bearing<T, HAS_W, HAS_DUPS>(P, be0 + e, lane, rows, slots, chi, nrob);
+        else if (e < ne) eval_odometry<T, HAS_DUPS>(P, oe0 + (e - nb), lane, rows, slots, chi, nrob);
         wave_lds_sync();
-        if (slot >= 0) {
-            if (HAS_GROUPS) {
-                for (int j = grp - c0; j < lane; ++j)
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) off[k] += offr[k][j];
-            }
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < ncol; ++c) P.val[off_pos(slot, base, r, c)] = off[3 * r + c];
+        if (single) {
+            const int cnt = min(64, ne - c0);
+            if (lane < 9)
+                for (int j = 0; j < cnt; ++j) acc += slots[lane][2 * j] + slots[lane][2 * j + 1];
+            wave_lds_sync();
         }
-        if (reducer) {
-            const int lo = max(r_beg, c0) - c0, hi = min(r_end, c0 + 64) - c0;
-            for (int j = lo; j < hi; ++j) acc += red[rv][j];
-        }
-        wave_lds_sync();
     }
-    if (reducer) {
-        const int p = P.a_seg_node[s0 + rs];
-        if (rv < 6) {
-            const int row0 = P.p_row0[p];
-            if (row0 >= 0) {
+    // reduce per node in a fixed order and write the diagonal blocks (+ damping) and b
+    if (single) {
+        const bool pose = P.pos_node[q0] < P.NP;
+        const int base = P.pos_base[q0];
+        if (lane < (pose ? 9 : 5)) {
+            const int nh = pose ? 6 : 3;
+            if (lane < nh) {
                 int r, c;
-                tri_rc(rv, r, c);
-                P.val[diag_pos(row0, P.p_base[p], r, c)] = acc + (r == c ? P.lambda : (T)0);
+                tri_rc(lane, r, c);
+                rows[r * base + ((r * (r + 1)) >> 1) + base + c] = acc + (r == c ? P.lambda : (T)0);
+            } else {
+                bb[lane - nh] = acc;
             }
-        } else {
-            P.b[P.p_bpos[p] + rv - 6] = acc;
         }
+    } else {
+        for (int pj = lane; pj < npairs; pj += 64) {
+            const int j = tb.pair_node[pj], v = tb.pair_val[pj];
+            T sum = (T)0;
+            for (int x = tb.node_cl[j]; x < tb.node_cl[j + 1]; ++x) sum += slots[v][tb.cl[x]];
+            const int base = tb.node_base[j], rel = tb.node_rel[j];
+            const int nh = tb.node_pose[j] ? 6 : 3;
+            if (v < nh) {
+                int r, c;
+                tri_rc(v, r, c);
+                rows[rel + r * base + ((r * (r + 1)) >> 1) + base + c] = sum + (r == c ? P.lambda : (T)0);
+            } else {
+                bb[tb.node_dof[j] + v - nh] = sum;
+            }
+        }
+    }
+    wave_lds_sync();
+    if (staged) {
+        for (int x = lane; x < v1 - v0; x += 64) P.val[v0 + x] = rowimg[x];
+        for (int x = lane; x < d1 - d0; x += 64) P.b[d0 + x] = bimg[x];
     }
     chi = wave_sum(chi);
     const int nr = (int)wave_sum((double)nrob);
     if (lane == 0) { P.chi2_part[t] = chi; P.nrob_part[t] = nr; }
 }
 
-template <typename T, bool HAS_W, bool HAS_GROUPS>
-__device__ __forceinline__ void lm_task(const LinParams<T>& P, int t, int lane, T (*red)[64], T (*offr)[64]) {
-    const int s0 = P.b_task[t], s1 = P.b_task[t + 1];
-    const int i0 = P.b_seg_item[s0], i1 = P.b_seg_item[s1];
-    const int nseg = s1 - s0;
-    const int rs = lane / 5, rv = lane - 5 * (lane / 5);
-    const bool reducer = rs < nseg;
-    int r_beg = 0, r_end = 0;
-    if (reducer) { r_beg = P.b_seg_item[s0 + rs]; r_end = P.b_seg_item[s0 + rs + 1]; }
-    T acc = (T)0;
-    for (int c0 = i0; c0 < i1; c0 += 64) {
-        const int i = c0 + lane;
-        T v[5], off[6];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) v[k] = (T)0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) off[k] = (T)0;
-        int slot = -1, grp = i, base = 0;
-        if (i < i1) {
-            int s = s0;
-            while (s + 1 < s1 && P.b_seg_item[s + 1] <= i) ++s;
-            const int l = P.b_seg_node[s];
-            const int p = P.b_other[i];
-            slot = P.b_slot[i];
-            if (HAS_GROUPS) grp = P.b_grp[i];
-            if (slot >= 0) base = P.l_base[l];
-            const T px = P.pc[4 * p], py = P.pc[4 * p + 1], c = P.pc[4 * p + 2], sn = P.pc[4 * p + 3];
-            const T lx = P.lc[2 * l], ly = P.lc[2 * l + 1];
-            T J[5];
-            T e = bos::bearing_error_jacobian<T>(px, py, c, sn, lx, ly, P.b_z[i], J);
-            const T w = HAS_W ? P.b_w[i] : (T)1;
-            const T rho = e * w * e;
-            if (rho > P.kt) e *= sqrt(P.kt / rho);
-            const T wJ3 = J[3] * w, wJ4 = J[4] * w;
-            v[0] = wJ3 * J[3];
-            v[1] = wJ4 * J[3]; v[2] = wJ4 * J[4];
-            v[3] = wJ3 * e; v[4] = wJ4 * e;
-            // landmark rows (2) x pose cols (3): H(l, p) = (J_l w) J_p
-#pragma unroll
-            for (int c2 = 0; c2 < 3; ++c2) { off[c2] = wJ3 * J[c2]; off[3 + c2] = wJ4 * J[c2]; }
-        }
-#pragma unroll
-        for (int k = 0; k < 5; ++k) red[k][lane] = v[k];
-        if (HAS_GROUPS) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) offr[k][lane] = off[k];
-        }
-        wave_lds_sync();
-        if (slot >= 0) {
-            if (HAS_GROUPS) {
-                for (int j = grp - c0; j < lane; ++j)
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) off[k] += offr[k][j];
-            }
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-#pragma unroll
-                for (int c2 = 0; c2 < 3; ++c2) P.val[off_pos(slot, base, r, c2)] = off[3 * r + c2];
-        }
-        if (reducer) {
-            const int lo = max(r_beg, c0) - c0, hi = min(r_end, c0 + 64) - c0;
-            for (int j = lo; j < hi; ++j) acc += red[rv][j];
-        }
-        wave_lds_sync();
-    }
-    if (reducer) {
-        const int l = P.b_seg_node[s0 + rs];
-        if (rv < 3) {
-            const int r = rv >= 1, cc = rv - r;
-            P.val[diag_pos(P.l_row0[l], P.l_base[l], r, cc)] = acc + (r == cc ? P.lambda : (T)0);
-        } else {
-            P.b[P.l_bpos[l] + rv - 3] = acc;
-        }
-    }
-}
-
-template <typename T, bool HAS_W, bool HAS_GROUPS>
+template <typename T, bool HAS_W, bool HAS_DUPS>
 __global__ __launch_bounds__(kBlock) void linearize_kernel(const LinParams<T> P) {
-    __shared__ T red[kWavesPerBlock][9][64];
-    __shared__ T offr[kWavesPerBlock][HAS_GROUPS ? 9 : 1][64];
+    __shared__ T rowimg[kWavesPerBlock][kStageCap];
+    __shared__ T slots[kWavesPerBlock][9][kSlots];
+    __shared__ T bimg[kWavesPerBlock][kBCap];
+    __shared__ TaskTables tables[kWavesPerBlock];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if ((int)blockIdx.x < P.nblk_pose) {
-        const int t = blockIdx.x * kWavesPerBlock + wave;
-        if (t < P.ntask_pose) pose_task<T, HAS_W, HAS_GROUPS>(P, t, lane, red[wave], offr[wave]);
-    } else {
-        const int t = (blockIdx.x - P.nblk_pose) * kWavesPerBlock + wave;
-        if (t < P.ntask_lm) lm_task<T, HAS_W, HAS_GROUPS>(P, t, lane, red[wave], offr[wave]);
-    }
+    const int t = blockIdx.x * kWavesPerBlock + wave;
+    if (t < P.ntask) range_task<T, HAS_W, HAS_DUPS>(P, t, lane, rowimg[wave], slots[wave], bimg[wave], tables[wave]);
 }
 
 template <typename T> __global__ void refresh_cache_kernel(const UpdateParams<T> U) {
@@ -359,15 +380,14 @@ __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colin
 }  // namespace
 
 template <typename T>
-hipError_t launch_linearize(const LinParams<T>& p, bool has_w, bool has_groups, hipStream_t s) {
-    const int nblk_lm = (p.ntask_lm + kWavesPerBlock - 1) / kWavesPerBlock;
-    const int grid = p.nblk_pose + nblk_lm;
+hipError_t launch_linearize(const LinParams<T>& p, bool has_w, bool has_dups, hipStream_t s) {
+    const int grid = (p.ntask + kWavesPerBlock - 1) / kWavesPerBlock;
     if (grid == 0) return hipSuccess;
     if (has_w) {
-        if (has_groups) hipLaunchKernelGGL((linearize_kernel<T, true, true>), dim3(grid), dim3(kBlock), 0, s, p);
+        if (has_dups) hipLaunchKernelGGL((linearize_kernel<T, true, true>), dim3(grid), dim3(kBlock), 0, s, p);
         else hipLaunchKernelGGL((linearize_kernel<T, true, false>), dim3(grid), dim3(kBlock), 0, s, p);
     } else {
-        if (has_groups) hipLaunchKernelGGL((linearize_kernel<T, false, true>), dim3(grid), dim3(kBlock), 0, s, p);
+        if (has_dups) hipLaunchKernelGGL((linearize_kernel<T, false, true>), dim3(grid), dim3(kBlock), 0, s, p);
         else hipLaunchKernelGGL((linearize_kernel<T, false, false>), dim3(grid), dim3(kBlock), 0, s, p);
     }
     return hipGetLastError();

@@ -11,50 +11,51 @@ namespace dev {
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;
 
+// LDS staging capacities of one wavefront (must match host/plan.cpp kStageCap / kMaxTaskNodes)
+constexpr int kStageCap = 1024;      // CSR values of a task's rows
+constexpr int kBCap = 144;           // b entries of a task (<= kMaxTaskNodes x 3)
+constexpr int kSlots = 128;          // contribution slots: 2 sides x 64 entries
+constexpr int kMaxTaskNodes = 48;    // nodes of one multi-node task (host/plan.cpp kMaxTaskNodes)
+
 template <typename T> struct LinParams {
     // state caches (T precision), refreshed by the box-plus kernel
     const T* pc;          // [NP][4] x, y, cos(theta), sin(theta)
     const T* pth;         // [NP] theta
     const T* lc;          // [NL][2]
-    // pose-centric work list
-    int ntask_pose, nblk_pose;
-    const int32_t* a_task;
-    const int32_t* a_seg_item;
-    const int32_t* a_seg_node;
-    const int32_t* a_other;
-    const int32_t* a_slot;
-    const int32_t* a_grp;     // may be null when the list has no groups
-    const T* a_z;
-    const T* a_w;             // null => omega = 1
-    // landmark-centric work list
-    int ntask_lm;
-    const int32_t* b_task;
-    const int32_t* b_seg_item;
-    const int32_t* b_seg_node;
-    const int32_t* b_other;
-    const int32_t* b_slot;
-    const int32_t* b_grp;
-    const T* b_z;
-    const T* b_w;
-    // odometry edges
+    int NP;
+    // node-range tasks (host/plan.hpp RangeTasks)
+    int ntask;
+    const int32_t* task_q;
+    const int32_t* task_be;
+    const int32_t* task_oe;
+    const uint8_t* task_flags;
+    const int32_t* be_pose;
+    const int32_t* be_lm;
+    const int32_t* be_meta;
+    const T* be_z;
+    const T* be_w;        // null => omega = 1
+    const T* be_woff;     // duplicate groups only
+    const int32_t* oe_edge;
+    const int32_t* oe_meta;
+    const T* oe_omoff;    // duplicate groups only
     const int32_t* o_src;
     const int32_t* o_dst;
-    const T* o_z;             // [M_o][3]
-    const T* o_om;            // [M_o][6] upper triangle (00, 01, 02, 11, 12, 22)
-    // node layout
-    const int32_t* p_row0;
-    const int32_t* p_base;
-    const int32_t* p_bpos;
-    const int32_t* l_row0;
-    const int32_t* l_base;
-    const int32_t* l_bpos;
+    const T* o_z;         // [M_o][3]
+    const T* o_om;        // [M_o][6] upper triangle (00, 01, 02, 11, 12, 22)
+    const int32_t* pos_node;
+    const int32_t* pos_row0;
+    const int32_t* pos_base;
+    const int32_t* pos_dof;
+    const int32_t* node_base;   // per node id (pose stix, NP + landmark stix)
+    const int32_t* cl_ptr;
+    const uint16_t* cl;
     // outputs
-    T* val;                   // lower triangle of P^T H_nf P (CSR value array)
-    T* b;                     // [n + 3], permuted dof order, fixed pose last
-    double* chi2_part;        // [ntask_pose]
-    int32_t* nrob_part;       // [ntask_pose]
-    T kt;                     // robust kernel threshold
-    T lambda;                 // damping
+    T* val;               // lower triangle of P^T H_nf P (CSR value array)
+    T* b;                 // [n + 3], permuted dof order, fixed pose last (not written)
+    double* chi2_part;    // [ntask]
+    int32_t* nrob_part;   // [ntask]
+    T kt;                 // robust kernel threshold
+    T lambda;             // damping
 };
 
 template <typename T> struct UpdateParams {
@@ -70,7 +71,7 @@ template <typename T> struct UpdateParams {
 };
 
 template <typename T>
-hipError_t launch_linearize(const LinParams<T>& p, bool has_w, bool has_groups, hipStream_t s);
+hipError_t launch_linearize(const LinParams<T>& p, bool has_w, bool has_dups, hipStream_t s);
 template <typename T> hipError_t launch_refresh_cache(const UpdateParams<T>& p, hipStream_t s);
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s);
 hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double* chi_out,

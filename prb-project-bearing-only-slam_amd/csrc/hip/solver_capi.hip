@@ -70,7 +70,7 @@ struct bos_solver {
     double kt = 1.0, damping = 0.01;
     bos::Plan plan;
     int NP = 0, NL = 0, Mb = 0, Mo = 0;
-    bool has_w = false, has_groups = false;
+    bool has_w = false, has_dups = false;
     size_t tsize = 8;   // sizeof(T)
     // state
     double* d_pose = nullptr;
@@ -78,20 +78,18 @@ struct bos_solver {
     void* d_pc = nullptr;
     void* d_pth = nullptr;
     void* d_lc = nullptr;
-    // pose-centric list
-    int32_t *a_task = nullptr, *a_seg_item = nullptr, *a_seg_node = nullptr, *a_other = nullptr, *a_slot = nullptr,
-            *a_grp = nullptr;
-    void *a_z = nullptr, *a_w = nullptr;
-    // landmark-centric list
-    int32_t *b_task = nullptr, *b_seg_item = nullptr, *b_seg_node = nullptr, *b_other = nullptr, *b_slot = nullptr,
-            *b_grp = nullptr;
-    void *b_z = nullptr, *b_w = nullptr;
+    // node-range tasks
+    int32_t *task_q = nullptr, *task_be = nullptr, *task_oe = nullptr, *be_pose = nullptr, *be_lm = nullptr,
+            *be_meta = nullptr, *oe_edge = nullptr, *oe_meta = nullptr, *pos_node = nullptr, *pos_row0 = nullptr,
+            *pos_base = nullptr, *pos_dof = nullptr, *node_base = nullptr, *cl_ptr = nullptr;
+    uint8_t* task_flags = nullptr;
+    uint16_t* cl = nullptr;
+    void *be_z = nullptr, *be_w = nullptr, *be_woff = nullptr, *oe_omoff = nullptr;
     // odometry
     int32_t *o_src = nullptr, *o_dst = nullptr;
     void *o_z = nullptr, *o_om = nullptr;
     // node layout
-    int32_t *p_row0 = nullptr, *p_base = nullptr, *p_bpos = nullptr, *l_row0 = nullptr, *l_base = nullptr,
-            *l_bpos = nullptr, *node_dof = nullptr;
+    int32_t* node_dof = nullptr;
     // system
     void* d_val = nullptr;      // T
     void* d_b = nullptr;        // T, n + 3
@@ -124,18 +122,15 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.pc = (const T*)s->d_pc;
     p.pth = (const T*)s->d_pth;
     p.lc = (const T*)s->d_lc;
-    p.ntask_pose = s->plan.pose_list.ntask();
-    p.nblk_pose = (p.ntask_pose + bos::dev::kWavesPerBlock - 1) / bos::dev::kWavesPerBlock;
-    p.a_task = s->a_task; p.a_seg_item = s->a_seg_item; p.a_seg_node = s->a_seg_node;
-    p.a_other = s->a_other; p.a_slot = s->a_slot; p.a_grp = s->a_grp;
-    p.a_z = (const T*)s->a_z; p.a_w = (const T*)s->a_w;
-    p.ntask_lm = s->plan.lm_list.ntask();
-    p.b_task = s->b_task; p.b_seg_item = s->b_seg_item; p.b_seg_node = s->b_seg_node;
-    p.b_other = s->b_other; p.b_slot = s->b_slot; p.b_grp = s->b_grp;
-    p.b_z = (const T*)s->b_z; p.b_w = (const T*)s->b_w;
+    p.NP = s->NP;
+    p.ntask = s->plan.tasks.ntask();
+    p.task_q = s->task_q; p.task_be = s->task_be; p.task_oe = s->task_oe; p.task_flags = s->task_flags;
+    p.be_pose = s->be_pose; p.be_lm = s->be_lm; p.be_meta = s->be_meta;
+    p.be_z = (const T*)s->be_z; p.be_w = (const T*)s->be_w; p.be_woff = (const T*)s->be_woff;
+    p.oe_edge = s->oe_edge; p.oe_meta = s->oe_meta; p.oe_omoff = (const T*)s->oe_omoff;
     p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
-    p.p_row0 = s->p_row0; p.p_base = s->p_base; p.p_bpos = s->p_bpos;
-    p.l_row0 = s->l_row0; p.l_base = s->l_base; p.l_bpos = s->l_bpos;
+    p.pos_node = s->pos_node; p.pos_row0 = s->pos_row0; p.pos_base = s->pos_base; p.pos_dof = s->pos_dof;
+    p.node_base = s->node_base; p.cl_ptr = s->cl_ptr; p.cl = s->cl;
     p.val = (T*)s->d_val;
     p.b = (T*)s->d_b;
     p.chi2_part = s->d_chi_part;
@@ -166,8 +161,8 @@ template <typename T> int upload_T(void** p, const std::vector<double>& v) {
 
 int enqueue_linearize(bos_solver* s) {
     hipError_t e;
-    if (s->precision == BOS_FP32) e = bos::dev::launch_linearize<float>(lin_params<float>(s), s->has_w, s->has_groups, s->stream);
-    else e = bos::dev::launch_linearize<double>(lin_params<double>(s), s->has_w, s->has_groups, s->stream);
+    if (s->precision == BOS_FP32) e = bos::dev::launch_linearize<float>(lin_params<float>(s), s->has_w, s->has_dups, s->stream);
+    else e = bos::dev::launch_linearize<double>(lin_params<double>(s), s->has_w, s->has_dups, s->stream);
     if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("linearize launch: ") + hipGetErrorString(e));
     return BOS_OK;
 }
@@ -191,7 +186,7 @@ int enqueue_exchange(bos_solver* s) {
 }
 
 int enqueue_stats(bos_solver* s) {
-    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->plan.pose_list.ntask(), s->d_chi,
+    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->plan.tasks.ntask(), s->d_chi,
                                           s->d_nrob, s->stream));
     if (s->world > 1) {
         NC_TRY(ncclGroupStart());
@@ -348,10 +343,10 @@ int bos_destroy(bos_solver* s) {
     if (!s) return BOS_OK;
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->a_task, s->a_seg_item, s->a_seg_node,
-                    s->a_other, s->a_slot, s->a_grp, s->a_z, s->a_w, s->b_task, s->b_seg_item, s->b_seg_node,
-                    s->b_other, s->b_slot, s->b_grp, s->b_z, s->b_w, s->o_src, s->o_dst, s->o_z, s->o_om,
-                    s->p_row0, s->p_base, s->p_bpos, s->l_row0, s->l_base, s->l_bpos, s->node_dof, s->d_val,
+    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->task_q, s->task_be, s->task_oe,
+                    s->be_pose, s->be_lm, s->be_meta, s->oe_edge, s->oe_meta, s->pos_node, s->pos_row0, s->pos_base,
+                    s->pos_dof, s->node_base, s->cl_ptr, s->task_flags, s->cl, s->be_z, s->be_w, s->be_woff,
+                    s->oe_omoff, s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val,
                     s->d_b, s->d_val64, s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_chi, s->d_nrob,
                     s->d_maxdx};
@@ -411,6 +406,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     bos::ProblemIndex pi;
     pi.NP = s->NP; pi.NL = s->NL; pi.Mb = s->Mb; pi.Mo = s->Mo; pi.fixed = pb->fixed_pose;
     pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
+    pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
     std::string err;
     const int fmode = s->solver_kind == BOS_SOLVER_SUPERNODAL    ? bos::kFactorMultifrontal
                       : s->solver_kind == BOS_SOLVER_ROCSOLVER_RF ? bos::kFactorScalar
@@ -420,7 +416,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     const bos::Plan& P = s->plan;
     if (s->solver_kind == BOS_SOLVER_DENSE_CHOL && P.n > 40000)
         return bail(fail(BOS_ERR_UNSUPPORTED, "dense solver limited to n <= 40000"));
-    s->has_groups = P.pose_list.has_groups || P.lm_list.has_groups;
+    s->has_dups = P.tasks.has_dups;
     s->has_w = false;
     if (pb->bearing_omega)
         for (int k = 0; k < s->Mb; ++k)
@@ -468,39 +464,26 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     if ((rc = alloc_T(&s->d_pc, 4 * (size_t)NP)) || (rc = alloc_T(&s->d_pth, NP)) || (rc = alloc_T(&s->d_lc, 2 * (size_t)NL)))
         return bail(rc);
 
-    auto up_list = [&](const bos::WorkList& W, bool pose_side, int32_t** task, int32_t** seg_item, int32_t** seg_node,
-                       int32_t** other, int32_t** slot, int32_t** grp, void** z, void** w) -> int {
-        int r;
-        if ((r = upload(task, W.task_seg)) || (r = upload(seg_item, W.seg_item)) || (r = upload(seg_node, W.seg_node)) ||
-            (r = upload(other, W.item_other)) || (r = upload(slot, W.item_slot)))
-            return r;
-        if (W.has_groups && (r = upload(grp, W.item_grp))) return r;
-        const size_t ni = W.item_other.size();
-        std::vector<double> zz(ni, 0.0), ww;
-        for (size_t i = 0; i < ni; ++i) {
-            const bool bearing = !pose_side || W.item_other[i] >= 0;
-            if (bearing) zz[i] = pb->bearing_z[W.item_obs[i]];
-        }
-        if ((r = upload_Tv(z, zz))) return r;
+    {
+        const bos::RangeTasks& T = P.tasks;
+        std::vector<double> bz(T.be_pose.size()), bw;
+        for (size_t i = 0; i < bz.size(); ++i) bz[i] = pb->bearing_z[T.be_obs[i]];
+        if ((rc = upload(&s->task_q, T.task_q)) || (rc = upload(&s->task_be, T.task_be)) ||
+            (rc = upload(&s->task_oe, T.task_oe)) || (rc = upload(&s->task_flags, T.task_flags)) ||
+            (rc = upload(&s->be_pose, T.be_pose)) || (rc = upload(&s->be_lm, T.be_lm)) ||
+            (rc = upload(&s->be_meta, T.be_meta)) || (rc = upload(&s->oe_edge, T.oe_edge)) ||
+            (rc = upload(&s->oe_meta, T.oe_meta)) || (rc = upload(&s->cl_ptr, T.cl_ptr)) || (rc = upload(&s->cl, T.cl)) ||
+            (rc = upload(&s->pos_node, P.pos_node)) || (rc = upload(&s->pos_row0, P.pos_row0)) ||
+            (rc = upload(&s->pos_base, P.pos_base)) || (rc = upload(&s->pos_dof, P.pos_dof)) ||
+            (rc = upload(&s->node_base, P.node_base)) || (rc = upload_Tv(&s->be_z, bz)))
+            return bail(rc);
         if (s->has_w) {
-            ww.assign(ni, 1.0);
-            for (size_t i = 0; i < ni; ++i) {
-                const bool bearing = !pose_side || W.item_other[i] >= 0;
-                if (bearing) ww[i] = pb->bearing_omega[W.item_obs[i]];
-            }
-            if ((r = upload_Tv(w, ww))) return r;
+            bw.resize(T.be_pose.size());
+            for (size_t i = 0; i < bw.size(); ++i) bw[i] = pb->bearing_omega[T.be_obs[i]];
+            if ((rc = upload_Tv(&s->be_w, bw))) return bail(rc);
         }
-        return BOS_OK;
-    };
-    if ((rc = up_list(P.pose_list, true, &s->a_task, &s->a_seg_item, &s->a_seg_node, &s->a_other, &s->a_slot, &s->a_grp,
-                      &s->a_z, &s->a_w)))
-        return bail(rc);
-    if ((rc = up_list(P.lm_list, false, &s->b_task, &s->b_seg_item, &s->b_seg_node, &s->b_other, &s->b_slot, &s->b_grp,
-                      &s->b_z, &s->b_w)))
-        return bail(rc);
-    if (s->has_groups) {   // kernels read grp for both lists when either has groups
-        if (!s->a_grp && (rc = upload(&s->a_grp, P.pose_list.item_grp))) return bail(rc);
-        if (!s->b_grp && (rc = upload(&s->b_grp, P.lm_list.item_grp))) return bail(rc);
+        if (s->has_dups && ((rc = upload_Tv(&s->be_woff, T.be_woff)) || (rc = upload_Tv(&s->oe_omoff, T.oe_omoff))))
+            return bail(rc);
     }
     {
         std::vector<int32_t> os(pb->odom_src, pb->odom_src + s->Mo), od(pb->odom_dst, pb->odom_dst + s->Mo);
@@ -514,15 +497,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             (rc = upload_Tv(&s->o_om, om)))
             return bail(rc);
     }
-    {
-        std::vector<int32_t> pr0(NP), pba(NP), pbp(NP), lr0(NL), lba(NL), lbp(NL);
-        for (int i = 0; i < NP; ++i) { pr0[i] = P.node_row0[i]; pba[i] = P.node_base[i]; pbp[i] = P.node_dof[i]; }
-        for (int j = 0; j < NL; ++j) { lr0[j] = P.node_row0[NP + j]; lba[j] = P.node_base[NP + j]; lbp[j] = P.node_dof[NP + j]; }
-        if ((rc = upload(&s->p_row0, pr0)) || (rc = upload(&s->p_base, pba)) || (rc = upload(&s->p_bpos, pbp)) ||
-            (rc = upload(&s->l_row0, lr0)) || (rc = upload(&s->l_base, lba)) || (rc = upload(&s->l_bpos, lbp)) ||
-            (rc = upload(&s->node_dof, P.node_dof)))
-            return bail(rc);
-    }
+    if ((rc = upload(&s->node_dof, P.node_dof))) return bail(rc);
     if ((rc = alloc_T(&s->d_val, std::max<int64_t>(P.nnzA(), 1))) || (rc = alloc_T(&s->d_b, P.n + 3)) ||
         (rc = dalloc(&s->d_rhs, std::max<int64_t>(P.n, 1))))
         return bail(rc);
@@ -543,7 +518,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     } else {
         if ((rc = dalloc(&s->d_dense, (size_t)P.n * P.n))) return bail(rc);
     }
-    const int nt = std::max(1, P.pose_list.ntask());
+    const int nt = std::max(1, P.tasks.ntask());
     if ((rc = dalloc(&s->d_info, 1)) || (rc = dalloc(&s->d_chi_part, nt)) || (rc = dalloc(&s->d_nrob_part, nt)) ||
         (rc = dalloc(&s->d_chi, 1)) || (rc = dalloc(&s->d_nrob, 1)) || (rc = dalloc(&s->d_maxdx, 1)))
         return bail(rc);
@@ -633,8 +608,8 @@ int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
     // compulsory reads of inputs + state, one write of every output block
     info->algorithmic_bytes = s->precision == BOS_FP32 ? 36 * Mb + 80 * Mo + 60 * NP + 32 * NL
                                                        : 64 * Mb + 152 * Mo + 120 * NP + 64 * NL;
-    info->num_items_pose = P.pose_list.nitem();
-    info->num_items_landmark = P.lm_list.nitem();
+    info->num_items_pose = P.tasks.ntask();
+    info->num_items_landmark = P.tasks.nentries();
     info->owned_first_row = P.row_begin;
     info->owned_last_row = P.row_end;
     return BOS_OK;

@@ -177,6 +177,7 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
     pi.NP = pb->num_poses; pi.NL = pb->num_landmarks; pi.Mb = pb->num_bearings; pi.Mo = pb->num_odometry;
     pi.fixed = pb->fixed_pose;
     pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
+    pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
     bos::Plan P;
     std::string err;
     const int rc = bos::build_plan(pi, rank, world, bos::kFactorMultifrontal, P, err);
@@ -193,8 +194,8 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
         info->n = P.n;
         info->nnz_lower = P.nnzA();
         info->nnz_factor = P.mf.L_size;
-        info->num_tasks_pose = P.pose_list.ntask();
-        info->num_tasks_landmark = P.lm_list.ntask();
+        info->num_tasks_pose = P.tasks.ntask();
+        info->num_tasks_landmark = P.tasks.nentries();
         info->flops_temporal = P.ordering.flops_temporal;
         info->flops_nested_dissection = P.ordering.flops_nd;
         info->mf_supernodes = P.mf.nsuper;
@@ -233,6 +234,7 @@ int bos_plan_mf_selftest(const bos_problem* pb, const double* vals, const double
     pi.NP = pb->num_poses; pi.NL = pb->num_landmarks; pi.Mb = pb->num_bearings; pi.Mo = pb->num_odometry;
     pi.fixed = pb->fixed_pose;
     pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
+    pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
     bos::Plan P;
     std::string err;
     const int rc = bos::build_plan(pi, 0, 1, bos::kFactorMultifrontal, P, err);

@@ -11,9 +11,9 @@ namespace bos {
 namespace {
 
 constexpr int kWave = 64;             // wavefront width on CDNA4
-constexpr int kMaxPoseSegs = 7;       // 7 poses x 9 reduced values <= 64 lanes (one pass)
-constexpr int kMaxLmSegs = 12;        // 12 landmarks x 5 reduced values <= 64 lanes
-constexpr int kMfLeaf = 12;           // nested-dissection leaf size (nodes) for the multifrontal solver
+constexpr int kMfLeaf = 12;
+constexpr int kStageCap = 1024;       // largest CSR span (values) a task assembles in LDS
+constexpr int kMaxTaskNodes = 48;     // nodes of one multi-node J+H task (hip/kernels.hpp kMaxTaskNodes)
 
 inline int node_size(int u, int NP) { return u < NP ? 3 : 2; }
 
@@ -317,6 +317,12 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err);
 int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
                        const std::vector<std::pair<int32_t, int32_t>>& blocks, std::string& err);
 
+template <typename BlockOffset>
+int build_tasks(const ProblemIndex& pi, Plan& P, int q_begin, int q_end, const std::vector<int32_t>& pb_ptr,
+                const std::vector<int32_t>& pb, const std::vector<int32_t>& lb_ptr, const std::vector<int32_t>& lb,
+                const std::vector<int32_t>& po_ptr, const std::vector<int32_t>& po, BlockOffset&& block_offset,
+                std::string& err);
+
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& P, std::string& err) {
     const bool want_factor = factor_mode == kFactorScalar;
     const int NP = pi.NP, NL = pi.NL, n_nodes = NP + NL;
@@ -480,106 +486,236 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     P.val_begin = P.rowptr[P.row_begin];
     P.val_end = P.rowptr[P.row_end];
 
-    // work lists
-    auto build_list = [&](bool pose_side, WorkList& W) -> int {
-        W = WorkList();
-        W.task_seg.push_back(0);
-        W.seg_item.push_back(0);
-        const int max_segs = pose_side ? kMaxPoseSegs : kMaxLmSegs;
-        int task_items = 0, task_segs = 0;
-        struct It { int32_t other, obs, slot, key; };
-        std::vector<It> its;
-        auto slot_of = [&](int owner, int other) -> int32_t {
-            const int32_t off = block_offset(owner, other);
-            return off < 0 ? -2 : P.node_row0[owner] + off;
-        };
-        auto add_node = [&](int u) -> int {
-            its.clear();
-            const bool write_ok = u != pi.fixed;
-            if (pose_side) {
-                for (int32_t e = pb_ptr[u]; e < pb_ptr[u + 1]; ++e) {
-                    const int k = pb[e];
-                    const int v = NP + pi.b_lm[k];
-                    int32_t slot = -1;
-                    if (write_ok && P.node_pos[u] > P.node_pos[v]) slot = slot_of(u, v);
-                    its.push_back({pi.b_lm[k], k, slot, P.node_pos[v]});
-                }
-                for (int32_t e = po_ptr[u]; e < po_ptr[u + 1]; ++e) {
-                    const int k = po[e] >> 1, side = po[e] & 1;
-                    const int v = side ? pi.o_src[k] : pi.o_dst[k];
-                    int32_t slot = -1;
-                    if (write_ok && v != pi.fixed && P.node_pos[u] > P.node_pos[v])
-                        slot = slot_of(u, v);
-                    its.push_back({-(2 * k + side) - 1, k, slot, v == pi.fixed ? INT32_MAX : P.node_pos[v]});
-                }
-            } else {
-                const int l = u - NP;
-                for (int32_t e = lb_ptr[l]; e < lb_ptr[l + 1]; ++e) {
-                    const int k = lb[e];
-                    const int v = pi.b_pose[k];
-                    int32_t slot = -1;
-                    if (v != pi.fixed && P.node_pos[u] > P.node_pos[v]) slot = slot_of(u, v);
-                    its.push_back({v, k, slot, v == pi.fixed ? INT32_MAX : P.node_pos[v]});
-                }
-            }
-            std::stable_sort(its.begin(), its.end(), [](const It& a, const It& b) { return a.key < b.key; });
-            for (const It& it : its)
-                if (it.slot < -1) return -3;   // block missing from the pattern (internal error)
-            const int cnt = (int)its.size();
-            // close the current task if this node does not fit
-            if (task_segs > 0 && (task_items + cnt > kWave || task_segs + 1 > max_segs)) {
-                W.task_seg.push_back((int32_t)W.seg_node.size());
-                W.max_items_per_task = std::max(W.max_items_per_task, task_items);
-                task_items = 0;
-                task_segs = 0;
-            }
-            const int32_t base = (int32_t)W.item_other.size();
-            for (int i = 0; i < cnt; ++i) {
-                W.item_other.push_back(its[i].other);
-                W.item_obs.push_back(its[i].obs);
-                W.item_slot.push_back(its[i].slot);
-                W.item_grp.push_back(base + i);
-            }
-            // off-diagonal groups: consecutive writing items with the same block
-            for (int i = 1; i < cnt; ++i) {
-                if (its[i].slot >= 0 && its[i].slot == its[i - 1].slot) {
-                    W.item_grp[base + i] = W.item_grp[base + i - 1];
-                    W.item_slot[base + i - 1] = -1;   // only the group's last item writes
-                    W.has_groups = true;
-                    // a group must not straddle a 64-item chunk boundary of its task
-                    const int first_in_task = W.item_grp[base + i] - W.seg_item[W.task_seg.back()];
-                    const int me_in_task = base + i - W.seg_item[W.task_seg.back()];
-                    if (first_in_task / kWave != me_in_task / kWave) return -2;
-                }
-            }
-            W.seg_node.push_back(pose_side ? u : u - NP);
-            W.seg_item.push_back((int32_t)W.item_other.size());
-            task_items += cnt;
-            task_segs += 1;
-            return 0;
-        };
-        for (int i = cut[rank]; i < cut[rank + 1]; ++i) {
-            const int u = inv[i];
-            if ((u < NP) != pose_side) continue;
-            const int a = add_node(u);
-            if (a == -2) { err = "duplicate observations straddle a 64-item chunk"; return BOS_ERR_UNSUPPORTED; }
-            if (a) { err = "internal error: off-diagonal block missing from the pattern"; return BOS_ERR_INVALID; }
-        }
-        if (pose_side && rank == world - 1) {   // the fixed pose: only its b entries (export)
-            if (add_node(pi.fixed)) { err = "duplicate observations straddle a 64-item chunk"; return BOS_ERR_UNSUPPORTED; }
-        }
-        if (task_segs > 0) {
-            W.task_seg.push_back((int32_t)W.seg_node.size());
-            W.max_items_per_task = std::max(W.max_items_per_task, task_items);
-        }
-        return BOS_OK;
-    };
-    rc = build_list(true, P.pose_list);
-    if (rc) return rc;
-    rc = build_list(false, P.lm_list);
+    // per-position node layout (the J+H kernel walks positions)
+    P.pos_node.assign(m, 0); P.pos_row0.assign(m + 1, 0); P.pos_base.assign(m, 0); P.pos_dof.assign(m + 1, 0);
+    for (int q = 0; q < m; ++q) {
+        const int u = inv[q];
+        P.pos_node[q] = u; P.pos_row0[q] = P.node_row0[u]; P.pos_base[q] = P.node_base[u]; P.pos_dof[q] = P.node_dof[u];
+    }
+    P.pos_row0[m] = (int32_t)P.nnzA();
+    P.pos_dof[m] = (int32_t)P.n;
+    rc = build_tasks(pi, P, cut[rank], cut[rank + 1], pb_ptr, pb, lb_ptr, lb, po_ptr, po, block_offset, err);
     if (rc) return rc;
     if (factor_mode == kFactorMultifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, err))) return rc;
     return validate_plan(pi, P, err);
+}
+
+// Node-range tasks of the J+H kernel (see RangeTasks in plan.hpp).
+template <typename BlockOffset>
+int build_tasks(const ProblemIndex& pi, Plan& P, int q_begin, int q_end, const std::vector<int32_t>& pb_ptr,
+                const std::vector<int32_t>& pb, const std::vector<int32_t>& lb_ptr, const std::vector<int32_t>& lb,
+                const std::vector<int32_t>& po_ptr, const std::vector<int32_t>& po, BlockOffset&& block_offset,
+                std::string& err) {
+    const int NP = pi.NP;
+    RangeTasks& T = P.tasks;
+    T = RangeTasks();
+    const int m = (int)P.pos_node.size();
+    T.cl_ptr.assign(m + 1, 0);
+    std::vector<int32_t> stamp_b(pi.Mb, -1), stamp_o(pi.Mo, -1);
+    auto pos_of = [&](int node) { return node == pi.fixed ? -1 : P.node_pos[node]; };
+    auto count_entries = [&](int q, int tid) {   // new entries node at q would add to task tid
+        const int u = P.pos_node[q];
+        int c = 0;
+        if (u < NP) {
+            for (int32_t e = pb_ptr[u]; e < pb_ptr[u + 1]; ++e) c += stamp_b[pb[e]] != tid;
+            for (int32_t e = po_ptr[u]; e < po_ptr[u + 1]; ++e) c += stamp_o[po[e] >> 1] != tid;
+        } else {
+            const int l = u - NP;
+            for (int32_t e = lb_ptr[l]; e < lb_ptr[l + 1]; ++e) c += stamp_b[lb[e]] != tid;
+        }
+        return c;
+    };
+    auto mark = [&](int q, int tid) {
+        const int u = P.pos_node[q];
+        if (u < NP) {
+            for (int32_t e = pb_ptr[u]; e < pb_ptr[u + 1]; ++e) stamp_b[pb[e]] = tid;
+            for (int32_t e = po_ptr[u]; e < po_ptr[u + 1]; ++e) stamp_o[po[e] >> 1] = tid;
+        } else {
+            for (int32_t e = lb_ptr[u - NP]; e < lb_ptr[u - NP + 1]; ++e) stamp_b[lb[e]] = tid;
+        }
+    };
+    // 1. cut the position range into tasks
+    T.task_q.push_back(q_begin);
+    int tid = 0;
+    for (int q = q_begin; q < q_end;) {
+        int entries = count_entries(q, tid);
+        mark(q, tid);
+        int q1 = q + 1;
+        if (entries <= kWave && P.pos_row0[q1] - P.pos_row0[q] <= kStageCap) {
+            while (q1 < q_end && q1 - q < kMaxTaskNodes) {
+                const int add = count_entries(q1, tid);
+                if (entries + add > kWave || P.pos_row0[q1 + 1] - P.pos_row0[q] > kStageCap) break;
+                entries += add;
+                mark(q1, tid);
+                ++q1;
+            }
+        }
+        T.task_q.push_back(q1);
+        q = q1;
+        ++tid;
+    }
+    // 2. entries, flags, contribution lists
+    std::fill(stamp_b.begin(), stamp_b.end(), -1);
+    std::fill(stamp_o.begin(), stamp_o.end(), -1);
+    T.task_be.push_back(0);
+    T.task_oe.push_back(0);
+    std::vector<std::vector<uint16_t>> node_slots;
+    for (int t = 0; t < (int)T.task_q.size() - 1; ++t) {
+        const int q0 = T.task_q[t], q1 = T.task_q[t + 1];
+        const int v0 = P.pos_row0[q0];
+        const bool single = q1 - q0 == 1;
+        const bool staged = P.pos_row0[q1] - v0 <= kStageCap;
+        T.task_flags.push_back((uint8_t)((staged ? 1 : 0) | (single ? 2 : 0)));
+        auto inside = [&](int node) { const int q = pos_of(node); return q >= q0 && q < q1; };
+        auto owner_and_slot = [&](int a, int b, int& meta) {
+            // the block (a, b) lives in the rows of the later of the two (the fixed pose has no rows)
+            if (a == pi.fixed || b == pi.fixed) return;
+            const bool b_owner = P.node_pos[b] > P.node_pos[a];
+            const int own = b_owner ? b : a, oth = b_owner ? a : b;
+            if (!inside(own)) return;
+            const int32_t off = block_offset(own, oth);
+            if (off < 0) { meta = -1; return; }
+            meta |= 8 | (b_owner ? 16 : 0) | ((P.node_row0[own] + off - v0) << 8);
+        };
+        auto counts_here = [&](int a, int b) {
+            // chi^2 of an observation is counted in the task of its owner (or of its non-fixed end)
+            int own;
+            if (a == pi.fixed) own = b;
+            else if (b == pi.fixed) own = a;
+            else own = P.node_pos[b] > P.node_pos[a] ? b : a;
+            return inside(own);
+        };
+        const int be_first = (int)T.be_pose.size(), oe_first = (int)T.oe_edge.size();
+        for (int q = q0; q < q1; ++q) {
+            const int u = P.pos_node[q];
+            if (u < NP) {
+                for (int32_t e = pb_ptr[u]; e < pb_ptr[u + 1]; ++e) {
+                    const int k = pb[e];
+                    if (stamp_b[k] == t) continue;
+                    stamp_b[k] = t;
+                    const int p = pi.b_pose[k], l = NP + pi.b_lm[k];
+                    int meta = (inside(p) ? 1 : 0) | (inside(l) ? 2 : 0) | (counts_here(p, l) ? 4 : 0);
+                    owner_and_slot(p, l, meta);
+                    if (meta < 0) { err = "internal error: bearing block missing"; return BOS_ERR_INVALID; }
+                    T.be_pose.push_back(pi.b_pose[k]); T.be_lm.push_back(pi.b_lm[k]);
+                    T.be_meta.push_back(meta); T.be_obs.push_back(k);
+                }
+                for (int32_t e = po_ptr[u]; e < po_ptr[u + 1]; ++e) {
+                    const int k = po[e] >> 1;
+                    if (stamp_o[k] == t) continue;
+                    stamp_o[k] = t;
+                    const int s = pi.o_src[k], d = pi.o_dst[k];
+                    int meta = (inside(s) ? 1 : 0) | (inside(d) ? 2 : 0) | (counts_here(s, d) ? 4 : 0);
+                    owner_and_slot(s, d, meta);
+                    if (meta < 0) { err = "internal error: odometry block missing"; return BOS_ERR_INVALID; }
+                    T.oe_edge.push_back(k); T.oe_meta.push_back(meta);
+                }
+            } else {
+                for (int32_t e = lb_ptr[u - NP]; e < lb_ptr[u - NP + 1]; ++e) {
+                    const int k = lb[e];
+                    if (stamp_b[k] == t) continue;
+                    stamp_b[k] = t;
+                    const int p = pi.b_pose[k], l = NP + pi.b_lm[k];
+                    int meta = (inside(p) ? 1 : 0) | (inside(l) ? 2 : 0) | (counts_here(p, l) ? 4 : 0);
+                    owner_and_slot(p, l, meta);
+                    if (meta < 0) { err = "internal error: bearing block missing"; return BOS_ERR_INVALID; }
+                    T.be_pose.push_back(pi.b_pose[k]); T.be_lm.push_back(pi.b_lm[k]);
+                    T.be_meta.push_back(meta); T.be_obs.push_back(k);
+                }
+            }
+        }
+        const int nb = (int)T.be_pose.size() - be_first, no = (int)T.oe_edge.size() - oe_first;
+        T.max_entries = std::max(T.max_entries, nb + no);
+        if (!single && nb + no > kWave) { err = "internal error: task too large"; return BOS_ERR_INVALID; }
+        // contribution slots per node (entry order = fixed reduction order)
+        for (int q = q0; q < q1; ++q) {
+            const int u = P.pos_node[q];
+            std::vector<uint16_t> sl;
+            for (int i = 0; i < nb; ++i) {
+                const int bi = be_first + i;
+                if (u < NP ? (T.be_pose[bi] == u) : (T.be_lm[bi] == u - NP)) sl.push_back((uint16_t)(2 * i + (u < NP ? 0 : 1)));
+            }
+            for (int j = 0; j < no; ++j) {
+                const int k = T.oe_edge[oe_first + j];
+                if (u < NP && pi.o_src[k] == u) sl.push_back((uint16_t)(2 * (nb + j)));
+                if (u < NP && pi.o_dst[k] == u) sl.push_back((uint16_t)(2 * (nb + j) + 1));
+            }
+            T.cl_ptr[q + 1] = (int32_t)sl.size();
+            if (!single) T.cl.insert(T.cl.end(), sl.begin(), sl.end());
+            else T.cl_ptr[q + 1] = 0;   // single-node tasks reduce every entry
+        }
+        T.task_be.push_back((int32_t)T.be_pose.size());
+        T.task_oe.push_back((int32_t)T.oe_edge.size());
+    }
+    for (int q = 0; q < m; ++q) T.cl_ptr[q + 1] += T.cl_ptr[q];
+    // 3. duplicate off-diagonal blocks: the first entry of a group writes, with the group's summed
+    //    information; the others do not write
+    T.be_woff.clear();
+    T.oe_omoff.clear();
+    {
+        std::vector<std::pair<int64_t, int>> key;   // (absolute slot, entry)
+        for (int t = 0; t < T.ntask(); ++t) {
+            const int v0 = P.pos_row0[T.task_q[t]];
+            for (int i = T.task_be[t]; i < T.task_be[t + 1]; ++i)
+                if (T.be_meta[i] & 8) key.push_back({(int64_t)v0 + (T.be_meta[i] >> 8), i});
+            for (int j = T.task_oe[t]; j < T.task_oe[t + 1]; ++j)
+                if (T.oe_meta[j] & 8) key.push_back({(int64_t)v0 + (T.oe_meta[j] >> 8), -1 - j});
+        }
+        std::sort(key.begin(), key.end());
+        for (size_t a = 0; a < key.size();) {
+            size_t b = a + 1;
+            while (b < key.size() && key[b].first == key[a].first) ++b;
+            if (b - a > 1) {
+                if (!T.has_dups) {
+                    T.has_dups = true;
+                    T.be_woff.assign(T.be_pose.size(), 0.0);
+                    T.oe_omoff.assign(6 * T.oe_edge.size(), 0.0);
+                    for (size_t i = 0; i < T.be_pose.size(); ++i) T.be_woff[i] = (T.be_meta[i] & 8) ? 1.0 : 0.0;
+                }
+                const bool bearing = key[a].second >= 0;
+                for (size_t c = a; c < b; ++c)
+                    if ((key[c].second >= 0) != bearing) { err = "bearing and odometry share a block"; return BOS_ERR_INVALID; }
+                if (bearing) {
+                    double wsum = 0;
+                    for (size_t c = a; c < b; ++c) {
+                        const int i = key[c].second;
+                        wsum += pi.b_omega ? pi.b_omega[T.be_obs[i]] : 1.0;
+                        if (c > a) { T.be_meta[i] &= ~8; T.be_woff[i] = 0.0; }
+                    }
+                    T.be_woff[key[a].second] = wsum;
+                } else {
+                    const int j0 = -1 - key[a].second;
+                    const int s0 = pi.o_src[T.oe_edge[j0]];
+                    double om[6] = {0, 0, 0, 0, 0, 0};
+                    for (size_t c = a; c < b; ++c) {
+                        const int j = -1 - key[c].second;
+                        if (pi.o_src[T.oe_edge[j]] != s0) {
+                            err = "odometry edges in both directions between the same poses (not supported)";
+                            return BOS_ERR_UNSUPPORTED;
+                        }
+                        const double* M = pi.o_omega + 9 * (size_t)T.oe_edge[j];
+                        const double u6[6] = {M[0], M[1], M[2], M[4], M[5], M[8]};
+                        for (int z = 0; z < 6; ++z) om[z] += u6[z];
+                        if (c > a) T.oe_meta[j] &= ~8;
+                    }
+                    for (int z = 0; z < 6; ++z) T.oe_omoff[6 * (size_t)j0 + z] = om[z];
+                }
+            }
+            a = b;
+        }
+        if (T.has_dups) {   // entries of singleton blocks use their own information
+            for (size_t j = 0; j < T.oe_edge.size(); ++j) {
+                bool zero = true;
+                for (int z = 0; z < 6; ++z) zero = zero && T.oe_omoff[6 * j + z] == 0.0;
+                if (zero && (T.oe_meta[j] & 8)) {
+                    const double* M = pi.o_omega + 9 * (size_t)T.oe_edge[j];
+                    const double u6[6] = {M[0], M[1], M[2], M[4], M[5], M[8]};
+                    for (int z = 0; z < 6; ++z) T.oe_omoff[6 * j + z] = u6[z];
+                }
+            }
+        }
+    }
+    return BOS_OK;
 }
 
 int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
@@ -729,6 +865,7 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
 int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
     const int NP = pi.NP;
     const int64_t nnz = P.nnzA();
+    const RangeTasks& T = P.tasks;
     auto check_entry = [&](int owner, int r, int64_t pos, int32_t want_col) -> bool {
         const int64_t row = (int64_t)P.node_dof[owner] + r;
         if (row < 0 || row >= P.n) return false;
@@ -737,73 +874,53 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
     };
     auto pos_off = [](int64_t slot, int base, int r, int c) { return slot + (int64_t)r * base + r * (r + 1) / 2 + c; };
     auto pos_diag = [](int64_t row0, int base, int r, int c) { return row0 + (int64_t)r * base + r * (r + 1) / 2 + base + c; };
-    for (int u = 0; u < NP + pi.NL; ++u) {
-        if (u == pi.fixed) {
-            if (P.node_row0[u] != -1) { err = "fixed pose has rows"; return BOS_ERR_INVALID; }
-            continue;
-        }
-        const int su = node_size(u, NP);
-        for (int r = 0; r < su; ++r)
-            for (int c = 0; c <= r; ++c)
-                if (!check_entry(u, r, pos_diag(P.node_row0[u], P.node_base[u], r, c), P.node_dof[u] + c)) {
-                    err = "diagonal block of node " + std::to_string(u) + " misplaced";
-                    return BOS_ERR_INVALID;
-                }
-    }
-    auto check_list = [&](const WorkList& W, bool pose_side) -> bool {
-        for (int s = 0; s + 1 < (int)W.seg_item.size(); ++s) {
-            const int node = pose_side ? W.seg_node[s] : NP + W.seg_node[s];
-            for (int i = W.seg_item[s]; i < W.seg_item[s + 1]; ++i) {
-                if (W.item_grp[i] > i || W.item_grp[i] < W.seg_item[s]) return false;
-                const int slot = W.item_slot[i];
-                if (slot < 0) continue;
-                int other;
-                if (!pose_side) other = W.item_other[i];
-                else if (W.item_other[i] >= 0) other = NP + W.item_other[i];
-                else {
-                    const int code = -W.item_other[i] - 1, k = code >> 1, side = code & 1;
-                    other = side ? pi.o_src[k] : pi.o_dst[k];
-                }
-                const int su = node_size(node, NP), so = node_size(other, NP);
-                for (int r = 0; r < su; ++r)
-                    for (int c = 0; c < so; ++c)
-                        if (!check_entry(node, r, pos_off(slot, P.node_base[node], r, c), P.node_dof[other] + c))
-                            return false;
-            }
-        }
-        return true;
-    };
-    if (!check_list(P.pose_list, true) || !check_list(P.lm_list, false)) {
-        err = "off-diagonal write slot misplaced";
-        return BOS_ERR_INVALID;
-    }
-    // every stored entry of the rows this rank owns is written exactly once per iteration (no
-    // stale values survive), and nothing outside them is written
     std::vector<uint8_t> hit(nnz, 0);
-    auto mark_list = [&](const WorkList& W, bool pose_side) {
-        for (int s = 0; s + 1 < (int)W.seg_item.size(); ++s) {
-            const int node = pose_side ? W.seg_node[s] : NP + W.seg_node[s];
-            if (node == pi.fixed) continue;
-            const int su = node_size(node, NP);
-            for (int r = 0; r < su; ++r)
-                for (int c = 0; c <= r; ++c) ++hit[pos_diag(P.node_row0[node], P.node_base[node], r, c)];
-            for (int i = W.seg_item[s]; i < W.seg_item[s + 1]; ++i) {
-                const int slot = W.item_slot[i];
-                if (slot < 0) continue;
-                int other;
-                if (!pose_side) other = W.item_other[i];
-                else if (W.item_other[i] >= 0) other = NP + W.item_other[i];
-                else {
-                    const int code = -W.item_other[i] - 1, k = code >> 1, side = code & 1;
-                    other = side ? pi.o_src[k] : pi.o_dst[k];
+    std::vector<int32_t> bcount(P.n, 0);
+    std::vector<int32_t> chi(pi.Mb + pi.Mo, 0);
+    for (int t = 0; t < T.ntask(); ++t) {
+        const int q0 = T.task_q[t], q1 = T.task_q[t + 1];
+        if (q1 <= q0) { err = "empty task"; return BOS_ERR_INVALID; }
+        const int64_t v0 = P.pos_row0[q0];
+        for (int q = q0; q < q1; ++q) {
+            const int u = P.pos_node[q];
+            const int su = node_size(u, NP);
+            for (int r = 0; r < su; ++r) {
+                ++bcount[P.node_dof[u] + r];
+                for (int c = 0; c <= r; ++c) {
+                    const int64_t pd = pos_diag(P.node_row0[u], P.node_base[u], r, c);
+                    if (!check_entry(u, r, pd, P.node_dof[u] + c)) { err = "diagonal block misplaced"; return BOS_ERR_INVALID; }
+                    ++hit[pd];
                 }
-                for (int r = 0; r < su; ++r)
-                    for (int c = 0; c < node_size(other, NP); ++c) ++hit[pos_off(slot, P.node_base[node], r, c)];
             }
         }
-    };
-    mark_list(P.pose_list, true);
-    mark_list(P.lm_list, false);
+        auto check_off = [&](int a, int b, int meta) -> bool {
+            if (!(meta & 8)) return true;
+            const int own = (meta & 16) ? b : a, oth = (meta & 16) ? a : b;
+            const int qo = P.node_pos[own];
+            if (qo < q0 || qo >= q1) return false;
+            const int64_t slot = v0 + (meta >> 8);
+            for (int r = 0; r < node_size(own, NP); ++r)
+                for (int c = 0; c < node_size(oth, NP); ++c) {
+                    const int64_t p = pos_off(slot, P.node_base[own], r, c);
+                    if (!check_entry(own, r, p, P.node_dof[oth] + c)) return false;
+                    ++hit[p];
+                }
+            return true;
+        };
+        for (int i = T.task_be[t]; i < T.task_be[t + 1]; ++i) {
+            if (!check_off(T.be_pose[i], NP + T.be_lm[i], T.be_meta[i])) { err = "bearing block misplaced"; return BOS_ERR_INVALID; }
+            if (T.be_meta[i] & 4) ++chi[T.be_obs[i]];
+        }
+        for (int j = T.task_oe[t]; j < T.task_oe[t + 1]; ++j) {
+            const int k = T.oe_edge[j];
+            if (!check_off(pi.o_src[k], pi.o_dst[k], T.oe_meta[j])) { err = "odometry block misplaced"; return BOS_ERR_INVALID; }
+            if (T.oe_meta[j] & 4) ++chi[pi.Mb + k];
+        }
+        if (!(T.task_flags[t] & 2) && T.task_be[t + 1] - T.task_be[t] + T.task_oe[t + 1] - T.task_oe[t] > 64) {
+            err = "multi-node task exceeds one wavefront";
+            return BOS_ERR_INVALID;
+        }
+    }
     for (int64_t e = 0; e < nnz; ++e) {
         const bool owned = e >= P.val_begin && e < P.val_end;
         if (hit[e] != (owned ? 1 : 0)) {
@@ -811,6 +928,11 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
             return BOS_ERR_INVALID;
         }
     }
+    for (int64_t i = 0; i < P.n; ++i)
+        if (bcount[i] != ((i >= P.row_begin && i < P.row_end) ? 1 : 0)) { err = "b entry coverage"; return BOS_ERR_INVALID; }
+    if (P.rank_row_begin.size() == 2)   // single shard: every observation's chi^2 counted once
+        for (size_t k = 0; k < chi.size(); ++k)
+            if (chi[k] != 1) { err = "chi^2 of observation " + std::to_string(k) + " counted " + std::to_string(chi[k]) + " times"; return BOS_ERR_INVALID; }
     return BOS_OK;
 }
 

@@ -22,23 +22,34 @@ struct ProblemIndex {
     const int32_t* b_lm = nullptr;
     const int32_t* o_src = nullptr;
     const int32_t* o_dst = nullptr;
+    const double* b_omega = nullptr;   // [Mb] or null (= 1)
+    const double* o_omega = nullptr;   // [Mo * 9]
 };
 
-struct WorkList {
-    // task -> segments -> items. A task is processed by one wavefront; a segment is one node
-    // (pose for the pose-centric list, landmark for the landmark-centric list); an item is one
-    // observation (or one side of an odometry edge) incident to that node.
-    std::vector<int32_t> task_seg;     // [ntask + 1]
-    std::vector<int32_t> seg_item;     // [nseg + 1]
-    std::vector<int32_t> seg_node;     // [nseg]  pose stix / landmark stix
-    std::vector<int32_t> item_other;   // pose list: lm stix (>= 0) or -(2*edge + side) - 1; lm list: pose stix
-    std::vector<int32_t> item_obs;     // bearing index (or edge index for odometry items)
-    std::vector<int32_t> item_slot;    // CSR position (row 0 of the owner) of the off-diagonal block, -1 none
-    std::vector<int32_t> item_grp;     // first item of this item's off-diagonal group (== own index if alone)
-    bool has_groups = false;           // some off-diagonal block has > 1 contributing item
-    int max_items_per_task = 0;
-    int ntask() const { return task_seg.empty() ? 0 : (int)task_seg.size() - 1; }
-    int nitem() const { return seg_item.empty() ? 0 : seg_item.back(); }
+// Work of the J+H kernel (hip/kernels.hip). A task is one wavefront and owns a contiguous
+// range of elimination positions [task_q[t], task_q[t + 1]): its CSR rows are the contiguous
+// value range [pos_row0[q0], pos_row0[q1]) and its b entries [pos_dof[q0], pos_dof[q1]), which
+// the wavefront assembles in LDS and stores with coalesced writes. Entries are the observations
+// incident to the task's nodes (an observation whose two endpoints lie in different tasks
+// appears in both). meta bits: 0 = first endpoint (pose / src) inside, 1 = second endpoint
+// (landmark / dst) inside, 2 = count this observation in chi^2, 3 = write the off-diagonal
+// block, 4 = the owner (row side) of that block is the second endpoint; bits 8.. = offset of
+// the block's first entry relative to the task's first value.
+struct RangeTasks {
+    std::vector<int32_t> task_q;        // [ntask + 1] position ranges
+    std::vector<int32_t> task_be;       // [ntask + 1] bearing-entry ranges
+    std::vector<int32_t> task_oe;       // [ntask + 1] odometry-entry ranges
+    std::vector<uint8_t> task_flags;    // bit 0: rows staged in LDS; bit 1: single node (chunked)
+    std::vector<int32_t> be_pose, be_lm, be_meta, be_obs;
+    std::vector<double> be_woff;        // off-block weight (sum over duplicate group; 0 = no write)
+    std::vector<int32_t> oe_edge, oe_meta;
+    std::vector<double> oe_omoff;       // [6 per entry] off-block information (duplicate groups)
+    std::vector<int32_t> cl_ptr;        // [m + 1] per position: range into cl
+    std::vector<uint16_t> cl;           // contribution slots (2 * entry + side, entry local to the task)
+    bool has_dups = false;
+    int max_entries = 0;
+    int ntask() const { return task_q.empty() ? 0 : (int)task_q.size() - 1; }
+    int nentries() const { return (int)be_pose.size() + (int)oe_edge.size(); }
 };
 
 struct OrderingReport {
@@ -80,7 +91,8 @@ struct Plan {
     std::vector<int32_t> rowptr, colind;   // lower triangle of P^T H_nf P, n rows
     std::vector<int32_t> Lptr, Lind;       // symbolic Cholesky factor (lower, with diagonal)
     Multifrontal mf;                       // built when factor_mode == kFactorMultifrontal
-    WorkList pose_list, lm_list;
+    RangeTasks tasks;
+    std::vector<int32_t> pos_node, pos_row0, pos_base, pos_dof;   // per elimination position
     OrderingReport ordering;
     // ownership for observation sharding: this rank writes rows [row_begin, row_end)
     int32_t row_begin = 0, row_end = 0;
