@@ -101,10 +101,12 @@ typedef struct bos_system_info {
     int64_t nnz_lower;              /* stored entries of the lower triangle of H_nf              */
     int64_t nnz_factor;             /* entries of the Cholesky factor (sparse solver)            */
     int64_t algorithmic_bytes;      /* SURVEY §8(d) J+H bytes for this problem and precision      */
-    int64_t num_items_pose;         /* pose-centric work items (bearings + 2 x odometry)         */
-    int64_t num_items_landmark;     /* landmark-centric work items (bearings)                    */
-    int32_t owned_first_row;        /* this shard's rows of H_nf [first, last)                   */
-    int32_t owned_last_row;
+    int64_t num_block_values;       /* size of the block array of H the J+H kernel writes        */
+    int32_t lanes_per_pose;         /* J+H work split: lanes per pose (1, 2 or 4)                */
+    int32_t owned_first_pose;       /* this shard's poses [first, last) and landmarks            */
+    int32_t owned_last_pose;
+    int32_t owned_first_landmark;
+    int32_t owned_last_landmark;
 } bos_system_info;
 
 void bos_default_options(bos_options* opt);

@@ -42,8 +42,8 @@ typedef struct bos_plan_info {
     int64_t n;
     int64_t nnz_lower;
     int64_t nnz_factor;
-    int64_t num_tasks_pose;
-    int64_t num_tasks_landmark;
+    int64_t num_block_values;       /* block array of H (J+H kernel layout)                      */
+    int64_t lanes_per_pose;
     double flops_temporal;
     double flops_nested_dissection;
     char ordering[32];

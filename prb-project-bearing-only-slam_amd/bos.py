@@ -74,14 +74,15 @@ class bos_step_stats(ctypes.Structure):
 
 class bos_system_info(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("nnz_lower", ctypes.c_int64), ("nnz_factor", ctypes.c_int64),
-                ("algorithmic_bytes", ctypes.c_int64), ("num_items_pose", ctypes.c_int64),
-                ("num_items_landmark", ctypes.c_int64), ("owned_first_row", ctypes.c_int32),
-                ("owned_last_row", ctypes.c_int32)]
+                ("algorithmic_bytes", ctypes.c_int64), ("num_block_values", ctypes.c_int64),
+                ("lanes_per_pose", ctypes.c_int32), ("owned_first_pose", ctypes.c_int32),
+                ("owned_last_pose", ctypes.c_int32), ("owned_first_landmark", ctypes.c_int32),
+                ("owned_last_landmark", ctypes.c_int32)]
 
 
 class bos_plan_info(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("nnz_lower", ctypes.c_int64), ("nnz_factor", ctypes.c_int64),
-                ("num_tasks_pose", ctypes.c_int64), ("num_tasks_landmark", ctypes.c_int64),
+                ("num_block_values", ctypes.c_int64), ("lanes_per_pose", ctypes.c_int64),
                 ("flops_temporal", ctypes.c_double), ("flops_nested_dissection", ctypes.c_double),
                 ("ordering", ctypes.c_char * 32), ("mf_supernodes", ctypes.c_int64),
                 ("mf_levels", ctypes.c_int64), ("mf_max_front", ctypes.c_int64), ("mf_flops", ctypes.c_double),
@@ -281,7 +282,7 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
     _check(L.bos_plan_inspect(ctypes.byref(cs), rank, world, 0, None, None, None, None, None, ctypes.byref(info)),
            "plan_inspect")
     out = {"n": info.n, "nnz_lower": info.nnz_lower, "nnz_factor": info.nnz_factor,
-           "num_tasks_pose": info.num_tasks_pose, "num_tasks_landmark": info.num_tasks_landmark,
+           "num_block_values": info.num_block_values, "lanes_per_pose": info.lanes_per_pose,
            "flops_temporal": info.flops_temporal, "flops_nested_dissection": info.flops_nested_dissection,
            "ordering": info.ordering.decode(), "mf_supernodes": info.mf_supernodes,
            "mf_levels": info.mf_levels, "mf_max_front": info.mf_max_front, "mf_flops": info.mf_flops,

@@ -1,17 +1,17 @@
 // HIP kernels of one Gauss-Newton iteration for 2-D bearing-only SLAM on MI355X (gfx950).
 //
 // J+H build (the hot path, reference slam/solver.cpp:28-69 + solver_jacobians.cpp:9-168), one
-// launch. A wavefront owns a task = a contiguous range of nodes in elimination order (host/plan.cpp
-// build_tasks), so the CSR rows it produces are ONE contiguous span of the value array:
-//   1. lane = one observation incident to the task's nodes: error, Jacobian, robust kernel
-//      (scales e only, solver.cpp:37-41/54-58); its per-side contributions (diagonal block + b)
-//      go to LDS slots and its off-diagonal block, when the block's row lives in this task, goes
-//      straight into the LDS image of the rows;
-//   2. lanes (node, value) reduce the slots in a fixed order (deterministic, no atomics) into the
-//      diagonal blocks (+ damping, solver.cpp:64-69) and b;
-//   3. the row image and b are stored with coalesced writes.
-// An observation whose endpoints lie in two tasks is evaluated in both; no workgroup reads what
-// another writes, so the launch has no inter-workgroup communication.
+// launch, no LDS and no atomics. H is written block-sparse in observation order (host/plan.hpp
+// BlockLayout), every value exactly once:
+//   * pose lanes (lpp per pose): each lane walks a segment of its pose's bearings (sorted by
+//     landmark) — error, Jacobian, robust kernel (scales e only, solver.cpp:37-41) — accumulating
+//     the pose's diagonal block and b in registers and storing each pose-landmark block H_pl as it
+//     goes; lane 0 of the group also walks the pose's odometry edges (both sides accumulate
+//     H_ss = H_dd, the source side stores H_sd = -H_ss and counts chi^2). The group's partial sums
+//     are combined with a fixed butterfly (deterministic) and stored with the damping (:64-69).
+//   * landmark lanes: one per landmark, walking its bearings for H_ll and b_l (+ damping).
+// A bearing is evaluated twice (pose side, landmark side): the arithmetic is cheap next to the
+// memory traffic, and no lane ever reads what another writes.
 #include "kernels.hpp"
 
 #include "../host/bos_math.hpp"
@@ -21,10 +21,17 @@ namespace dev {
 
 namespace {
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+template <typename T> struct alignas(4 * sizeof(T)) V4 { T x, y, z, w; };
+template <typename T> struct alignas(2 * sizeof(T)) V2 { T x, y; };
+
+template <typename T> __device__ __forceinline__ V4<T> load4(const T* p) { return *(const V4<T>*)p; }
+template <typename T> __device__ __forceinline__ V2<T> load2(const T* p) { return *(const V2<T>*)p; }
+// six values at an even offset of the block array (8-byte aligned for fp32, 16 for fp64)
+template <typename T> __device__ __forceinline__ void store6(T* p, T a, T b, T c, T d, T e, T f) {
+    V2<T>* q = (V2<T>*)p;
+    q[0] = V2<T>{a, b};
+    q[1] = V2<T>{c, d};
+    q[2] = V2<T>{e, f};
 }
 
 template <typename T> __device__ __forceinline__ T wave_sum(T v) {
@@ -33,87 +40,18 @@ template <typename T> __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
-// lower-triangle index rv (0..5) -> (r, c)
-__device__ __forceinline__ void tri_rc(int rv, int& r, int& c) {
-    r = (rv >= 1) + (rv >= 3);
-    c = rv - ((r * (r + 1)) >> 1);
-}
-
-// Contributions of one side of an observation go to slots[v][2 * entry + side]: pose side 9
-// values (H 00,10,11,20,21,22, b 0..2), landmark side 5 values (H 00,10,11, b 0,1).
-
-template <typename T, bool HAS_W, bool HAS_DUPS>
-__device__ __forceinline__ void eval_bearing(const LinParams<T>& P, int i, int ll, T* rows, T (*slots)[kSlots],
-                                             double& chi, int& nrob) {
-    const int meta = P.be_meta[i];
-    const int p = P.be_pose[i], l = P.be_lm[i];
-    const T px = P.pc[4 * p], py = P.pc[4 * p + 1], c = P.pc[4 * p + 2], sn = P.pc[4 * p + 3];
-    const T lx = P.lc[2 * l], ly = P.lc[2 * l + 1];
-    T J[5];
-    T e = bos::bearing_error_jacobian<T>(px, py, c, sn, lx, ly, P.be_z[i], J);   // solver_jacobians.cpp:9-95
-    const T w = HAS_W ? P.be_w[i] : (T)1;
-    const T rho = e * w * e;                                                        // solver.cpp:37
-    if (meta & 4) chi += (double)rho;
-    if (rho > P.kt) {                                                               // solver.cpp:38-40
-        e *= sqrt(P.kt / rho);
-        if (meta & 4) ++nrob;
-    }
-    // H += (J^T w) J, b += (J^T w) e  (solver.cpp:44-45)
-    const T wJ0 = J[0] * w, wJ1 = J[1] * w, wJ2 = J[2] * w, wJ3 = J[3] * w, wJ4 = J[4] * w;
-    if (meta & 1) {
-        slots[0][2 * ll] = wJ0 * J[0];
-        slots[1][2 * ll] = wJ1 * J[0];
-        slots[2][2 * ll] = wJ1 * J[1];
-        slots[3][2 * ll] = wJ2 * J[0];
-        slots[4][2 * ll] = wJ2 * J[1];
-        slots[5][2 * ll] = wJ2 * J[2];
-        slots[6][2 * ll] = wJ0 * e;
-        slots[7][2 * ll] = wJ1 * e;
-        slots[8][2 * ll] = wJ2 * e;
-    }
-    if (meta & 2) {
-        slots[0][2 * ll + 1] = wJ3 * J[3];
-        slots[1][2 * ll + 1] = wJ4 * J[3];
-        slots[2][2 * ll + 1] = wJ4 * J[4];
-        slots[3][2 * ll + 1] = wJ3 * e;
-        slots[4][2 * ll + 1] = wJ4 * e;
-    }
-    if (meta & 8) {
-        const T wo = HAS_DUPS ? P.be_woff[i] : w;
-        T* blk = rows + (meta >> 8);
-        if (meta & 16) {   // landmark rows (2) x pose cols (3)
-            const int base = P.node_base[P.NP + l];
-            const T a0 = J[3] * wo, a1 = J[4] * wo;
-            blk[0] = a0 * J[0]; blk[1] = a0 * J[1]; blk[2] = a0 * J[2];
-            blk += base + 1;
-            blk[0] = a1 * J[0]; blk[1] = a1 * J[1]; blk[2] = a1 * J[2];
-        } else {           // pose rows (3) x landmark cols (2)
-            const int base = P.node_base[p];
-            const T a0 = J[0] * wo, a1 = J[1] * wo, a2 = J[2] * wo;
-            blk[0] = a0 * J[3]; blk[1] = a0 * J[4];
-            blk += base + 1;
-            blk[0] = a1 * J[3]; blk[1] = a1 * J[4];
-            blk += base + 2;
-            blk[0] = a2 * J[3]; blk[1] = a2 * J[4];
-        }
-    }
-}
-
-// Odometry edge (solver_jacobians.cpp:97-168). J_dst = -J_src exactly in the reference's
-// Jacobian (:137-146: (DR' R_s)^T = -R_s^T DR' since DR' is antisymmetric), so
-// H_ss = H_dd = J_s^T Omega J_s, H_sd = -H_ss, b_d = -b_s.
-template <typename T, bool HAS_DUPS>
-__device__ __forceinline__ void eval_odometry(const LinParams<T>& P, int j, int ll, T* rows, T (*slots)[kSlots],
-                                              double& chi, int& nrob) {
-    const int meta = P.oe_meta[j];
-    const int k = P.oe_edge[j];
-    const int ps = P.o_src[k], pd = P.o_dst[k];
-    const T xs = P.pc[4 * ps], ys = P.pc[4 * ps + 1], cs = P.pc[4 * ps + 2], ss = P.pc[4 * ps + 3];
-    const T xd = P.pc[4 * pd], yd = P.pc[4 * pd + 1];
+// Odometry edge (solver_jacobians.cpp:97-168) seen from one endpoint. J_dst = -J_src exactly in
+// the reference's Jacobian (:137-146: (DR' R_s)^T = -R_s^T DR', DR' antisymmetric), so
+// H_ss = H_dd = J_s^T Omega J_s, H_sd = -H_ss, b_d = -b_s. Returns rho = e^T Omega e; h = H_ss
+// (00, 10, 11, 20, 21, 22), g = b_s.
+template <typename T>
+__device__ __forceinline__ T odometry_hb(const LinParams<T>& P, int k, const V4<T>& S, T ths, const V4<T>& D, T thd,
+                                         T h[6], T g[3]) {
+    const T xs = S.x, ys = S.y, cs = S.z, ss = S.w, xd = D.x, yd = D.y;
     const T tx = xd - xs, ty = yd - ys;
     const T e0 = (cs * tx + ss * ty) - P.o_z[3 * k];                                // :106, :319
     const T e1 = (-ss * tx + cs * ty) - P.o_z[3 * k + 1];
-    const T e2 = bos::normalized_angle<T>(bos::normalized_angle<T>(P.pth[pd] - P.pth[ps]) - P.o_z[3 * k + 2]);
+    const T e2 = bos::normalized_angle<T>(bos::normalized_angle<T>(thd - ths) - P.o_z[3 * k + 2]);
     const T t0 = -ss * xd + cs * yd, t1 = -cs * xd - ss * yd;                       // :139
     // J_s = [[-cs, -ss, t0], [ss, -cs, t1], [0, 0, -1]]
     const T* u = P.o_om + 6 * k;
@@ -122,176 +60,180 @@ __device__ __forceinline__ void eval_odometry(const LinParams<T>& P, int j, int 
     T Oe1 = o01 * e0 + o11 * e1 + o12 * e2;
     T Oe2 = o02 * e0 + o12 * e1 + o22 * e2;
     const T rho = e0 * Oe0 + e1 * Oe1 + e2 * Oe2;                                   // solver.cpp:54
-    if (meta & 4) chi += (double)rho;
     if (rho > P.kt) {                                                               // :55-57
         const T sc = sqrt(P.kt / rho);
         Oe0 *= sc; Oe1 *= sc; Oe2 *= sc;
-        if (meta & 4) ++nrob;
     }
     // Omega J_s, column by column
     const T a00 = -o00 * cs + o01 * ss, a01 = -o00 * ss - o01 * cs, a02 = o00 * t0 + o01 * t1 - o02;
     const T a10 = -o01 * cs + o11 * ss, a11 = -o01 * ss - o11 * cs, a12 = o01 * t0 + o11 * t1 - o12;
     const T a20 = -o02 * cs + o12 * ss, a21 = -o02 * ss - o12 * cs, a22 = o02 * t0 + o12 * t1 - o22;
-    // H_ss = J_s^T (Omega J_s): J_s^T row r = column r of J_s
-    const T h00 = -cs * a00 + ss * a10;
-    const T h10 = -ss * a00 - cs * a10;
-    const T h11 = -ss * a01 - cs * a11;
-    const T h20 = t0 * a00 + t1 * a10 - a20;
-    const T h21 = t0 * a01 + t1 * a11 - a21;
-    const T h22 = t0 * a02 + t1 * a12 - a22;
-    const T b0 = -cs * Oe0 + ss * Oe1, b1 = -ss * Oe0 - cs * Oe1, b2 = t0 * Oe0 + t1 * Oe1 - Oe2;
-    if (meta & 1) {
-        slots[0][2 * ll] = h00; slots[1][2 * ll] = h10; slots[2][2 * ll] = h11;
-        slots[3][2 * ll] = h20; slots[4][2 * ll] = h21; slots[5][2 * ll] = h22;
-        slots[6][2 * ll] = b0; slots[7][2 * ll] = b1; slots[8][2 * ll] = b2;
-    }
-    if (meta & 2) {
-        slots[0][2 * ll + 1] = h00; slots[1][2 * ll + 1] = h10; slots[2][2 * ll + 1] = h11;
-        slots[3][2 * ll + 1] = h20; slots[4][2 * ll + 1] = h21; slots[5][2 * ll + 1] = h22;
-        slots[6][2 * ll + 1] = -b0; slots[7][2 * ll + 1] = -b1; slots[8][2 * ll + 1] = -b2;
-    }
-    if (meta & 8) {
-        T g00 = h00, g10 = h10, g11 = h11, g20 = h20, g21 = h21, g22 = h22;
-        if (HAS_DUPS) {   // summed information of a duplicate group
-            const T* v = P.oe_omoff + 6 * j;
-            const T q00 = -v[0] * cs + v[1] * ss, q01 = -v[0] * ss - v[1] * cs, q02 = v[0] * t0 + v[1] * t1 - v[2];
-            const T q10 = -v[1] * cs + v[3] * ss, q11 = -v[1] * ss - v[3] * cs, q12 = v[1] * t0 + v[3] * t1 - v[4];
-            const T q20 = -v[2] * cs + v[4] * ss, q21 = -v[2] * ss - v[4] * cs, q22 = v[2] * t0 + v[4] * t1 - v[5];
-            g00 = -cs * q00 + ss * q10; g10 = -ss * q00 - cs * q10; g11 = -ss * q01 - cs * q11;
-            g20 = t0 * q00 + t1 * q10 - q20; g21 = t0 * q01 + t1 * q11 - q21; g22 = t0 * q02 + t1 * q12 - q22;
+    // H_ss = J_s^T (Omega J_s)
+    h[0] = -cs * a00 + ss * a10;
+    h[1] = -ss * a00 - cs * a10;
+    h[2] = -ss * a01 - cs * a11;
+    h[3] = t0 * a00 + t1 * a10 - a20;
+    h[4] = t0 * a01 + t1 * a11 - a21;
+    h[5] = t0 * a02 + t1 * a12 - a22;
+    g[0] = -cs * Oe0 + ss * Oe1;
+    g[1] = -ss * Oe0 - cs * Oe1;
+    g[2] = t0 * Oe0 + t1 * Oe1 - Oe2;
+    return rho;
+}
+
+template <typename T, bool HAS_W, bool HAS_DUPS, int LPP>
+__device__ __forceinline__ void pose_lanes(const LinParams<T>& P, double& chi, int& nrob) {
+    const int gid = blockIdx.x * kBlock + threadIdx.x;
+    const int p = P.p_begin + gid / LPP, sub = gid % LPP;
+    const bool active = p < P.p_end;
+    T h[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    if (active) {
+        const V4<T> X = load4(P.pc + 4 * p);
+        const int sg = p * LPP + sub;
+        int i = P.seg_ptr[sg];
+        const int i1 = P.seg_ptr[sg + 1];
+        T* blk = P.hval + P.off_pl + 6 * P.seg_blk[sg];
+        T acc[6] = {0, 0, 0, 0, 0, 0};
+        BRec<T> nxt;
+        if (i < i1) nxt = P.pb[i];
+        for (; i < i1; ++i) {
+            const BRec<T> cur = nxt;
+            if (i + 1 < i1) nxt = P.pb[i + 1];
+            const V2<T> Lm = load2(P.lc + 2 * cur.idx);
+            T J[5];
+            T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, cur.z, J);   // :9-95
+            const T w = HAS_W ? P.pb_w[i] : (T)1;
+            const T rho = e * w * e;                                                       // solver.cpp:37
+            chi += (double)rho;
+            if (rho > P.kt) {                                                              // :38-40
+                e *= sqrt(P.kt / rho);
+                ++nrob;
+            }
+            // H += (J^T w) J, b += (J^T w) e (:44-45)
+            const T w0 = J[0] * w, w1 = J[1] * w, w2 = J[2] * w;
+            h[0] += w0 * J[0]; h[1] += w1 * J[0]; h[2] += w1 * J[1];
+            h[3] += w2 * J[0]; h[4] += w2 * J[1]; h[5] += w2 * J[2];
+            g[0] += w0 * e; g[1] += w1 * e; g[2] += w2 * e;
+            const T o0 = w0 * J[3], o1 = w0 * J[4], o2 = w1 * J[3], o3 = w1 * J[4], o4 = w2 * J[3], o5 = w2 * J[4];
+            if (HAS_DUPS) {   // observations of one pair are adjacent: sum, store once
+                acc[0] += o0; acc[1] += o1; acc[2] += o2; acc[3] += o3; acc[4] += o4; acc[5] += o5;
+                if (i + 1 == i1 || nxt.idx != cur.idx) {
+                    store6(blk, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5]);
+                    blk += 6;
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) acc[q] = (T)0;
+                }
+            } else {
+                store6(blk, o0, o1, o2, o3, o4, o5);
+                blk += 6;
+            }
         }
-        // H_sd = -H_ss (symmetric), rows of the owner x cols of the other pose
-        const int base = P.node_base[(meta & 16) ? pd : ps];
-        T* blk = rows + (meta >> 8);
-        blk[0] = -g00; blk[1] = -g10; blk[2] = -g20;
-        blk += base + 1;
-        blk[0] = -g10; blk[1] = -g11; blk[2] = -g21;
-        blk += base + 2;
-        blk[0] = -g20; blk[1] = -g21; blk[2] = -g22;
+        if (sub == 0) {
+            const T th = P.pth[p];
+            T acc6[6] = {0, 0, 0, 0, 0, 0};
+            const int x1 = P.po_ptr[p + 1];
+            for (int x = P.po_ptr[p]; x < x1; ++x) {
+                const int ent = P.po_ent[x], k = ent >> 1;
+                const bool dst_side = ent & 1;
+                const int q = dst_side ? P.o_src[k] : P.o_dst[k];
+                const V4<T> Q = load4(P.pc + 4 * q);
+                const T thq = P.pth[q];
+                T he[6], ge[3];
+                const T rho = dst_side ? odometry_hb<T>(P, k, Q, thq, X, th, he, ge)
+                                       : odometry_hb<T>(P, k, X, th, Q, thq, he, ge);
+#pragma unroll
+                for (int v = 0; v < 6; ++v) h[v] += he[v];
+                if (dst_side) {
+                    g[0] -= ge[0]; g[1] -= ge[1]; g[2] -= ge[2];
+                    continue;
+                }
+                g[0] += ge[0]; g[1] += ge[1]; g[2] += ge[2];
+                chi += (double)rho;
+                if (rho > P.kt) ++nrob;
+                const int ub = P.po_blk[x];
+                T* ob = P.hval + P.off_pp + 6 * ub;
+                if (HAS_DUPS) {
+#pragma unroll
+                    for (int v = 0; v < 6; ++v) acc6[v] -= he[v];
+                    if (x + 1 == x1 || P.po_blk[x + 1] != ub) {
+                        store6(ob, acc6[0], acc6[1], acc6[2], acc6[3], acc6[4], acc6[5]);
+#pragma unroll
+                        for (int v = 0; v < 6; ++v) acc6[v] = (T)0;
+                    }
+                } else {
+                    store6(ob, -he[0], -he[1], -he[2], -he[3], -he[4], -he[5]);
+                }
+            }
+        }
+    }
+    // combine the lane group's partial sums (fixed butterfly: deterministic)
+#pragma unroll
+    for (int o = 1; o < LPP; o <<= 1) {
+#pragma unroll
+        for (int v = 0; v < 6; ++v) h[v] += __shfl_xor(h[v], o);
+#pragma unroll
+        for (int v = 0; v < 3; ++v) g[v] += __shfl_xor(g[v], o);
+    }
+    if (active && sub == 0) {
+        const T lam = P.lambda;
+        store6(P.hval + 6 * p, h[0] + lam, h[1], h[2] + lam, h[3], h[4], h[5] + lam);
+        T* bp = P.b + 3 * p;
+        bp[0] = g[0]; bp[1] = g[1]; bp[2] = g[2];
     }
 }
 
-// per-wave LDS tables of a task (kMaxTaskNodes nodes, <= 2 x 64 contribution slots)
-struct TaskTables {
-    int32_t node_base[kMaxTaskNodes];
-    int16_t node_rel[kMaxTaskNodes];    // row start relative to the task's first value (< kStageCap)
-    int16_t node_dof[kMaxTaskNodes];    // relative to the task's first dof
-    int16_t node_cl[kMaxTaskNodes + 1]; // contribution-list range, relative to the task's first
-    uint8_t node_pose[kMaxTaskNodes];
-    uint8_t pair_node[9 * kMaxTaskNodes];
-    uint8_t pair_val[9 * kMaxTaskNodes];
-    uint16_t cl[kSlots];
-};
+template <typename T, bool HAS_W>
+__device__ __forceinline__ void landmark_lane(const LinParams<T>& P) {
+    const int l = P.l_begin + (blockIdx.x - P.pose_blocks) * kBlock + threadIdx.x;
+    if (l >= P.l_end) return;
+    const V2<T> Lm = load2(P.lc + 2 * l);
+    T h00 = 0, h10 = 0, h11 = 0, g0 = 0, g1 = 0;
+    int x = P.lb_ptr[l];
+    const int x1 = P.lb_ptr[l + 1];
+    BRec<T> nxt;
+    if (x < x1) nxt = P.lb[x];
+    for (; x < x1; ++x) {
+        const BRec<T> cur = nxt;
+        if (x + 1 < x1) nxt = P.lb[x + 1];
+        const V4<T> X = load4(P.pc + 4 * cur.idx);
+        T J[5];
+        T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, cur.z, J);
+        const T w = HAS_W ? P.lb_w[x] : (T)1;
+        const T rho = e * w * e;
+        if (rho > P.kt) e *= sqrt(P.kt / rho);
+        const T w3 = J[3] * w, w4 = J[4] * w;
+        h00 += w3 * J[3]; h10 += w4 * J[3]; h11 += w4 * J[4];
+        g0 += w3 * e; g1 += w4 * e;
+    }
+    T* hl = P.hval + P.off_ldiag + 3 * l;
+    hl[0] = h00 + P.lambda; hl[1] = h10; hl[2] = h11 + P.lambda;
+    T* bl = P.b + 3 * P.NP + 2 * l;
+    bl[0] = g0; bl[1] = g1;
+}
 
-template <typename T, bool HAS_W, bool HAS_DUPS>
-__device__ __forceinline__ void range_task(const LinParams<T>& P, int t, int lane, T* rowimg, T (*slots)[kSlots],
-                                           T* bimg, TaskTables& tb) {
-    const int q0 = P.task_q[t], q1 = P.task_q[t + 1];
-    const int flags = P.task_flags[t];
-    const bool staged = flags & 1, single = flags & 2;
-    const int v0 = P.pos_row0[q0], v1 = P.pos_row0[q1];
-    const int d0 = P.pos_dof[q0], d1 = P.pos_dof[q1];
-    T* rows = staged ? rowimg : P.val + v0;
-    T* bb = staged ? bimg : P.b + d0;
-    const int be0 = P.task_be[t], nb = P.task_be[t + 1] - be0;
-    const int oe0 = P.task_oe[t], ne = nb + P.task_oe[t + 1] - oe0;
-    const int nn = q1 - q0;
-    // prologue: node table and contribution lists into LDS (independent of the entry loads)
-    int npairs = 0;
-    if (!single) {
-        const int cl0 = P.cl_ptr[q0], ncl = P.cl_ptr[q1] - cl0;
-        int nv = 0;
-        if (lane < nn) {
-            const int q = q0 + lane;
-            const bool pose = P.pos_node[q] < P.NP;
-            nv = pose ? 9 : 5;
-            tb.node_rel[lane] = (int16_t)(P.pos_row0[q] - v0);
-            tb.node_base[lane] = P.pos_base[q];
-            tb.node_dof[lane] = (int16_t)(P.pos_dof[q] - d0);
-            tb.node_cl[lane] = (int16_t)(P.cl_ptr[q] - cl0);
-            tb.node_pose[lane] = pose;
-        }
-        if (lane == 0) tb.node_cl[nn] = (int16_t)ncl;
-        for (int x = lane; x < ncl; x += 64) tb.cl[x] = P.cl[cl0 + x];
-        // exclusive prefix sum of the value counts -> pair table
-        int incl = nv;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-        npairs = __shfl(incl, 63);
-        for (int v = 0; v < nv; ++v) {
-            tb.pair_node[incl - nv + v] = (uint8_t)lane;
-            tb.pair_val[incl - nv + v] = (uint8_t)v;
-        }
+template <typename T, bool HAS_W, bool HAS_DUPS, int LPP>
+__global__ __launch_bounds__(kBlock) void linearize_kernel(const LinParams<T> P) {
+    if ((int)blockIdx.x >= P.pose_blocks) {   // block-uniform branch
+        landmark_lane<T, HAS_W>(P);
+        return;
     }
     double chi = 0.0;
     int nrob = 0;
-    T acc = (T)0;   // single-node tasks: lane v < size accumulates value v over all chunks
-    for (int c0 = 0; c0 < ne; c0 += 64) {
-        const int e = c0 + lane;
-#pragma unroll
-        for (int v = 0; v < 9; ++v) { slots[v][2 * lane] = (T)0; slots[v][2 * lane + 1] = (T)0; }
-        if (e < nb) eval_bearing<T, HAS_W, HAS_DUPS>(P, be0 + e, lane, rows, slots, chi, nrob);
-        else if (e < ne) eval_odometry<T, HAS_DUPS>(P, oe0 + (e - nb), lane, rows, slots, chi, nrob);
-        wave_lds_sync();
-        if (single) {
-            const int cnt = min(64, ne - c0);
-            if (lane < 9)
-                for (int j = 0; j < cnt; ++j) acc += slots[lane][2 * j] + slots[lane][2 * j + 1];
-            wave_lds_sync();
-        }
-    }
-    // reduce per node in a fixed order and write the diagonal blocks (+ damping) and b
-    if (single) {
-        const bool pose = P.pos_node[q0] < P.NP;
-        const int base = P.pos_base[q0];
-        if (lane < (pose ? 9 : 5)) {
-            const int nh = pose ? 6 : 3;
-            if (lane < nh) {
-                int r, c;
-                tri_rc(lane, r, c);
-                rows[r * base + ((r * (r + 1)) >> 1) + base + c] = acc + (r == c ? P.lambda : (T)0);
-            } else {
-                bb[lane - nh] = acc;
-            }
-        }
-    } else {
-        for (int pj = lane; pj < npairs; pj += 64) {
-            const int j = tb.pair_node[pj], v = tb.pair_val[pj];
-            T sum = (T)0;
-            for (int x = tb.node_cl[j]; x < tb.node_cl[j + 1]; ++x) sum += slots[v][tb.cl[x]];
-            const int base = tb.node_base[j], rel = tb.node_rel[j];
-            const int nh = tb.node_pose[j] ? 6 : 3;
-            if (v < nh) {
-                int r, c;
-                tri_rc(v, r, c);
-                rows[rel + r * base + ((r * (r + 1)) >> 1) + base + c] = sum + (r == c ? P.lambda : (T)0);
-            } else {
-                bb[tb.node_dof[j] + v - nh] = sum;
-            }
-        }
-    }
-    wave_lds_sync();
-    if (staged) {
-        for (int x = lane; x < v1 - v0; x += 64) P.val[v0 + x] = rowimg[x];
-        for (int x = lane; x < d1 - d0; x += 64) P.b[d0 + x] = bimg[x];
-    }
+    pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, chi, nrob);
+    // per-block chi^2 / robust count in a fixed order
+    __shared__ double sc[kBlock / 64];
+    __shared__ int sr[kBlock / 64];
     chi = wave_sum(chi);
-    const int nr = (int)wave_sum((double)nrob);
-    if (lane == 0) { P.chi2_part[t] = chi; P.nrob_part[t] = nr; }
-}
-
-template <typename T, bool HAS_W, bool HAS_DUPS>
-__global__ __launch_bounds__(kBlock) void linearize_kernel(const LinParams<T> P) {
-    __shared__ T rowimg[kWavesPerBlock][kStageCap];
-    __shared__ T slots[kWavesPerBlock][9][kSlots];
-    __shared__ T bimg[kWavesPerBlock][kBCap];
-    __shared__ TaskTables tables[kWavesPerBlock];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int t = blockIdx.x * kWavesPerBlock + wave;
-    if (t < P.ntask) range_task<T, HAS_W, HAS_DUPS>(P, t, lane, rowimg[wave], slots[wave], bimg[wave], tables[wave]);
+    nrob = (int)wave_sum((double)nrob);
+    if ((threadIdx.x & 63) == 0) { sc[threadIdx.x >> 6] = chi; sr[threadIdx.x >> 6] = nrob; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double c = 0.0;
+        int r = 0;
+        for (int w = 0; w < kBlock / 64; ++w) { c += sc[w]; r += sr[w]; }
+        P.chi2_part[blockIdx.x] = c;
+        P.nrob_part[blockIdx.x] = r;
+    }
 }
 
 template <typename T> __global__ void refresh_cache_kernel(const UpdateParams<T> U) {
@@ -370,6 +312,11 @@ template <typename T> __global__ void to_f64_kernel(const T* in, double* out, in
         out[i] = (double)in[i];
 }
 
+template <typename T> __global__ void gather_f64_kernel(const T* in, const int32_t* idx, double* out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (double)in[idx[i]];
+}
+
 __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colind, const double* val, int n,
                                      double* dense) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -379,18 +326,23 @@ __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colin
 
 }  // namespace
 
-template <typename T>
-hipError_t launch_linearize(const LinParams<T>& p, bool has_w, bool has_dups, hipStream_t s) {
-    const int grid = (p.ntask + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (grid == 0) return hipSuccess;
-    if (has_w) {
-        if (has_dups) hipLaunchKernelGGL((linearize_kernel<T, true, true>), dim3(grid), dim3(kBlock), 0, s, p);
-        else hipLaunchKernelGGL((linearize_kernel<T, true, false>), dim3(grid), dim3(kBlock), 0, s, p);
-    } else {
-        if (has_dups) hipLaunchKernelGGL((linearize_kernel<T, false, true>), dim3(grid), dim3(kBlock), 0, s, p);
-        else hipLaunchKernelGGL((linearize_kernel<T, false, false>), dim3(grid), dim3(kBlock), 0, s, p);
+template <typename T, bool W, bool D>
+hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, int grid, hipStream_t s) {
+    switch (lpp) {
+        case 1: hipLaunchKernelGGL((linearize_kernel<T, W, D, 1>), dim3(grid), dim3(kBlock), 0, s, p); break;
+        case 2: hipLaunchKernelGGL((linearize_kernel<T, W, D, 2>), dim3(grid), dim3(kBlock), 0, s, p); break;
+        case 4: hipLaunchKernelGGL((linearize_kernel<T, W, D, 4>), dim3(grid), dim3(kBlock), 0, s, p); break;
+        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s) {
+    const int grid = p.pose_blocks + (p.l_end - p.l_begin + kBlock - 1) / kBlock;
+    if (grid == 0) return hipSuccess;
+    if (has_w) return has_dups ? launch_lin_lpp<T, true, true>(p, lpp, grid, s) : launch_lin_lpp<T, true, false>(p, lpp, grid, s);
+    return has_dups ? launch_lin_lpp<T, false, true>(p, lpp, grid, s) : launch_lin_lpp<T, false, false>(p, lpp, grid, s);
 }
 
 template <typename T> hipError_t launch_refresh_cache(const UpdateParams<T>& p, hipStream_t s) {
@@ -420,6 +372,14 @@ template <typename T> hipError_t launch_to_f64(const T* in, double* out, int64_t
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL((gather_f64_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter_dense(const int32_t* rowptr, const int32_t* colind, const double* val, int n, double* dense,
                                 hipStream_t s) {
     if (n == 0) return hipSuccess;
@@ -427,14 +387,16 @@ hipError_t launch_scatter_dense(const int32_t* rowptr, const int32_t* colind, co
     return hipGetLastError();
 }
 
-template hipError_t launch_linearize<double>(const LinParams<double>&, bool, bool, hipStream_t);
-template hipError_t launch_linearize<float>(const LinParams<float>&, bool, bool, hipStream_t);
+template hipError_t launch_linearize<double>(const LinParams<double>&, int, bool, bool, hipStream_t);
+template hipError_t launch_linearize<float>(const LinParams<float>&, int, bool, bool, hipStream_t);
 template hipError_t launch_refresh_cache<double>(const UpdateParams<double>&, hipStream_t);
 template hipError_t launch_refresh_cache<float>(const UpdateParams<float>&, hipStream_t);
 template hipError_t launch_boxplus<double>(const UpdateParams<double>&, hipStream_t);
 template hipError_t launch_boxplus<float>(const UpdateParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);
+template hipError_t launch_gather_f64<double>(const double*, const int32_t*, double*, int64_t, hipStream_t);
+template hipError_t launch_gather_f64<float>(const float*, const int32_t*, double*, int64_t, hipStream_t);
 
 }  // namespace dev
 }  // namespace bos

@@ -2,10 +2,11 @@
 // (host/plan.hpp), the rocSOLVER refactorization state and the RCCL communicator.
 //
 // One GN iteration (reference Solver::step, slam/solver.cpp:27-97):
-//   1. linearize_kernel          J+H build straight into the CSR of P^T H_nf P (+ damping)
-//   2. [world > 1] RCCL broadcasts of every rank's owned rows of H and b (the exchange step)
-//   3. sparse Cholesky refactorization + solve (rocSOLVER csrrf; pattern analysed once, like
-//      SimplicialLDLT::analyzePattern at solver.cpp:77-80) or dense potrf/potrs
+//   1. linearize_kernel          J+H build into the block array of H and b (+ damping)
+//   2. [world > 1] RCCL broadcasts of every rank's owned blocks and b entries (the exchange step)
+//   3. sparse Cholesky factorization + solve: the GPU supernodal multifrontal solver (default;
+//      structure analysed once, like SimplicialLDLT::analyzePattern at solver.cpp:77-80), or
+//      rocSOLVER csrrf / dense potrf-potrs on a gathered CSR copy
 //   4. boxplus_kernel            left-multiplicative box-plus with dx = -x (state.cpp:69-80)
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -78,23 +79,22 @@ struct bos_solver {
     void* d_pc = nullptr;
     void* d_pth = nullptr;
     void* d_lc = nullptr;
-    // node-range tasks
-    int32_t *task_q = nullptr, *task_be = nullptr, *task_oe = nullptr, *be_pose = nullptr, *be_lm = nullptr,
-            *be_meta = nullptr, *oe_edge = nullptr, *oe_meta = nullptr, *pos_node = nullptr, *pos_row0 = nullptr,
-            *pos_base = nullptr, *pos_dof = nullptr, *node_base = nullptr, *cl_ptr = nullptr;
-    uint8_t* task_flags = nullptr;
-    uint16_t* cl = nullptr;
-    void *be_z = nullptr, *be_w = nullptr, *be_woff = nullptr, *oe_omoff = nullptr;
+    // J+H work lists (host/plan.hpp BlockLayout)
+    int32_t *seg_ptr = nullptr, *seg_blk = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_blk = nullptr,
+            *lb_ptr = nullptr, *csr_src = nullptr, *elim_ref = nullptr;
+    void *pb = nullptr, *pb_w = nullptr, *lb = nullptr, *lb_w = nullptr;
+    int pose_blocks = 0;
     // odometry
     int32_t *o_src = nullptr, *o_dst = nullptr;
     void *o_z = nullptr, *o_om = nullptr;
     // node layout
     int32_t* node_dof = nullptr;
     // system
-    void* d_val = nullptr;      // T
-    void* d_b = nullptr;        // T, n + 3
-    double* d_val64 = nullptr;  // fp32 build: fp64 copy for the solver
-    double* d_rhs = nullptr;    // n, solution in place
+    void* d_val = nullptr;      // T, block array of H (BlockLayout)
+    void* d_b = nullptr;        // T, 3 NP + 2 NL, reference dof numbering
+    double* d_val64 = nullptr;  // fp32 build: fp64 copy of the block array for the solver
+    double* d_csr64 = nullptr;  // dense / csrrf solvers: CSR values of P^T H_nf P (fp64)
+    double* d_rhs = nullptr;    // n, permuted order; solution in place
     int32_t *d_rowptr = nullptr, *d_colind = nullptr;
     int32_t *d_Lptr = nullptr, *d_Lind = nullptr, *d_pivQ = nullptr;
     double* d_Lval = nullptr;
@@ -122,17 +122,18 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.pc = (const T*)s->d_pc;
     p.pth = (const T*)s->d_pth;
     p.lc = (const T*)s->d_lc;
+    const bos::Plan& P = s->plan;
     p.NP = s->NP;
-    p.ntask = s->plan.tasks.ntask();
-    p.task_q = s->task_q; p.task_be = s->task_be; p.task_oe = s->task_oe; p.task_flags = s->task_flags;
-    p.be_pose = s->be_pose; p.be_lm = s->be_lm; p.be_meta = s->be_meta;
-    p.be_z = (const T*)s->be_z; p.be_w = (const T*)s->be_w; p.be_woff = (const T*)s->be_woff;
-    p.oe_edge = s->oe_edge; p.oe_meta = s->oe_meta; p.oe_omoff = (const T*)s->oe_omoff;
+    p.p_begin = P.p_begin; p.p_end = P.p_end; p.l_begin = P.l_begin; p.l_end = P.l_end;
+    p.pose_blocks = s->pose_blocks;
+    p.seg_ptr = s->seg_ptr; p.seg_blk = s->seg_blk;
+    p.pb = (const bos::dev::BRec<T>*)s->pb; p.pb_w = (const T*)s->pb_w;
+    p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_blk = s->po_blk;
     p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
-    p.pos_node = s->pos_node; p.pos_row0 = s->pos_row0; p.pos_base = s->pos_base; p.pos_dof = s->pos_dof;
-    p.node_base = s->node_base; p.cl_ptr = s->cl_ptr; p.cl = s->cl;
-    p.val = (T*)s->d_val;
+    p.lb_ptr = s->lb_ptr; p.lb = (const bos::dev::BRec<T>*)s->lb; p.lb_w = (const T*)s->lb_w;
+    p.hval = (T*)s->d_val;
     p.b = (T*)s->d_b;
+    p.off_ldiag = (int)P.blk.off_ldiag; p.off_pl = (int)P.blk.off_pl; p.off_pp = (int)P.blk.off_pp;
     p.chi2_part = s->d_chi_part;
     p.nrob_part = s->d_nrob_part;
     p.kt = (T)s->kt;
@@ -161,33 +162,40 @@ template <typename T> int upload_T(void** p, const std::vector<double>& v) {
 
 int enqueue_linearize(bos_solver* s) {
     hipError_t e;
-    if (s->precision == BOS_FP32) e = bos::dev::launch_linearize<float>(lin_params<float>(s), s->has_w, s->has_dups, s->stream);
-    else e = bos::dev::launch_linearize<double>(lin_params<double>(s), s->has_w, s->has_dups, s->stream);
+    const int lpp = s->plan.blk.lpp;
+    if (s->precision == BOS_FP32) e = bos::dev::launch_linearize<float>(lin_params<float>(s), lpp, s->has_w, s->has_dups, s->stream);
+    else e = bos::dev::launch_linearize<double>(lin_params<double>(s), lpp, s->has_w, s->has_dups, s->stream);
     if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("linearize launch: ") + hipGetErrorString(e));
     return BOS_OK;
 }
 
-// RCCL exchange: every rank owns a contiguous range of rows of P^T H_nf P (and of b); broadcast
-// each range from its owner so every rank holds the full system for the replicated solve.
+// RCCL exchange: every rank owns contiguous pieces of the block array (its poses' diagonal and
+// off-diagonal blocks, its landmarks' diagonal blocks) and of b; broadcast each piece from its
+// owner so every rank holds the full system for the replicated solve.
 int enqueue_exchange(bos_solver* s) {
     if (s->world <= 1) return BOS_OK;
     const ncclDataType_t ty = s->precision == BOS_FP32 ? ncclFloat : ncclDouble;
-    const std::vector<int32_t>& rr = s->plan.rank_row_begin;
+    const bos::Plan& P = s->plan;
     NC_TRY(ncclGroupStart());
     for (int r = 0; r < s->world; ++r) {
-        const int64_t v0 = s->plan.rowptr[rr[r]], v1 = s->plan.rowptr[rr[r + 1]];
-        char* vb = (char*)s->d_val + v0 * s->tsize;
-        if (v1 > v0) NC_TRY(ncclBroadcast(vb, vb, (size_t)(v1 - v0), ty, r, s->comm, s->stream));
-        char* bb = (char*)s->d_b + (int64_t)rr[r] * s->tsize;
-        if (rr[r + 1] > rr[r]) NC_TRY(ncclBroadcast(bb, bb, (size_t)(rr[r + 1] - rr[r]), ty, r, s->comm, s->stream));
+        for (int q = 0; q < 4; ++q) {
+            const bos::Range& g = P.rank_val_ranges[4 * (size_t)r + q];
+            char* vb = (char*)s->d_val + g.begin * s->tsize;
+            if (g.end > g.begin) NC_TRY(ncclBroadcast(vb, vb, (size_t)(g.end - g.begin), ty, r, s->comm, s->stream));
+        }
+        for (int q = 0; q < 2; ++q) {
+            const bos::Range& g = P.rank_b_ranges[2 * (size_t)r + q];
+            char* bb = (char*)s->d_b + g.begin * s->tsize;
+            if (g.end > g.begin) NC_TRY(ncclBroadcast(bb, bb, (size_t)(g.end - g.begin), ty, r, s->comm, s->stream));
+        }
     }
     NC_TRY(ncclGroupEnd());
     return BOS_OK;
 }
 
 int enqueue_stats(bos_solver* s) {
-    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->plan.tasks.ntask(), s->d_chi,
-                                          s->d_nrob, s->stream));
+    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->pose_blocks, s->d_chi, s->d_nrob,
+                                          s->stream));
     if (s->world > 1) {
         NC_TRY(ncclGroupStart());
         NC_TRY(ncclAllReduce(s->d_chi, s->d_chi, 1, ncclDouble, ncclSum, s->comm, s->stream));
@@ -201,21 +209,24 @@ int enqueue_solve(bos_solver* s, bool& ran_analysis) {
     const int64_t n = s->plan.n;
     ran_analysis = false;
     if (n == 0) return BOS_OK;
-    double* A = nullptr;
-    if (s->precision == BOS_FP32) {
-        HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.nnzA(), s->stream));
-        HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_b, s->d_rhs, n, s->stream));
-        A = s->d_val64;
-    } else {
-        HIP_TRY(hipMemcpyAsync(s->d_rhs, s->d_b, n * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
-        A = (double*)s->d_val;
-    }
+    const bool f32 = s->precision == BOS_FP32;
+    // right-hand side in elimination order
+    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream)
+                : bos::dev::launch_gather_f64<double>((const double*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream));
     const rocblas_int nn = (rocblas_int)n;
-    if (s->solver_kind == BOS_SOLVER_SUPERNODAL) {
+    if (s->solver_kind == BOS_SOLVER_SUPERNODAL) {   // reads the block array through its assembly map
+        const double* A = (const double*)s->d_val;
+        if (f32) {
+            HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.blk.size, s->stream));
+            A = s->d_val64;
+        }
         HIP_TRY(bos::dev::mf_factor(s->mf, A, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, s->d_rhs, s->stream));
         return BOS_OK;
     }
+    double* A = s->d_csr64;
+    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_val, s->csr_src, A, s->plan.nnzA(), s->stream)
+                : bos::dev::launch_gather_f64<double>((const double*)s->d_val, s->csr_src, A, s->plan.nnzA(), s->stream));
     if (s->solver_kind == BOS_SOLVER_DENSE_CHOL) {
         HIP_TRY(hipMemsetAsync(s->d_dense, 0, (size_t)n * n * sizeof(double), s->stream));
         HIP_TRY(bos::dev::launch_scatter_dense(s->d_rowptr, s->d_colind, A, nn, s->d_dense, s->stream));
@@ -343,11 +354,10 @@ int bos_destroy(bos_solver* s) {
     if (!s) return BOS_OK;
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->task_q, s->task_be, s->task_oe,
-                    s->be_pose, s->be_lm, s->be_meta, s->oe_edge, s->oe_meta, s->pos_node, s->pos_row0, s->pos_base,
-                    s->pos_dof, s->node_base, s->cl_ptr, s->task_flags, s->cl, s->be_z, s->be_w, s->be_woff,
-                    s->oe_omoff, s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val,
-                    s->d_b, s->d_val64, s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
+    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->seg_ptr, s->seg_blk, s->po_ptr, s->po_ent,
+                    s->po_blk, s->lb_ptr, s->csr_src, s->elim_ref, s->pb, s->pb_w, s->lb, s->lb_w,
+                    s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
+                    s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_chi, s->d_nrob,
                     s->d_maxdx};
     for (void* b : bufs)
@@ -416,7 +426,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     const bos::Plan& P = s->plan;
     if (s->solver_kind == BOS_SOLVER_DENSE_CHOL && P.n > 40000)
         return bail(fail(BOS_ERR_UNSUPPORTED, "dense solver limited to n <= 40000"));
-    s->has_dups = P.tasks.has_dups;
+    s->has_dups = P.blk.has_dups;
     s->has_w = false;
     if (pb->bearing_omega)
         for (int k = 0; k < s->Mb; ++k)
@@ -465,25 +475,41 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         return bail(rc);
 
     {
-        const bos::RangeTasks& T = P.tasks;
-        std::vector<double> bz(T.be_pose.size()), bw;
-        for (size_t i = 0; i < bz.size(); ++i) bz[i] = pb->bearing_z[T.be_obs[i]];
-        if ((rc = upload(&s->task_q, T.task_q)) || (rc = upload(&s->task_be, T.task_be)) ||
-            (rc = upload(&s->task_oe, T.task_oe)) || (rc = upload(&s->task_flags, T.task_flags)) ||
-            (rc = upload(&s->be_pose, T.be_pose)) || (rc = upload(&s->be_lm, T.be_lm)) ||
-            (rc = upload(&s->be_meta, T.be_meta)) || (rc = upload(&s->oe_edge, T.oe_edge)) ||
-            (rc = upload(&s->oe_meta, T.oe_meta)) || (rc = upload(&s->cl_ptr, T.cl_ptr)) || (rc = upload(&s->cl, T.cl)) ||
-            (rc = upload(&s->pos_node, P.pos_node)) || (rc = upload(&s->pos_row0, P.pos_row0)) ||
-            (rc = upload(&s->pos_base, P.pos_base)) || (rc = upload(&s->pos_dof, P.pos_dof)) ||
-            (rc = upload(&s->node_base, P.node_base)) || (rc = upload_Tv(&s->be_z, bz)))
+        const bos::BlockLayout& B = P.blk;
+        const int Mb = s->Mb;
+        std::vector<double> pbz(Mb), lbz(Mb), pbw, lbw;
+        std::vector<int32_t> pbi(Mb), lbi(Mb);
+        for (int i = 0; i < Mb; ++i) {
+            pbi[i] = pb->bearing_landmark[B.pb_obs[i]]; pbz[i] = pb->bearing_z[B.pb_obs[i]];
+            lbi[i] = pb->bearing_pose[B.lb_obs[i]]; lbz[i] = pb->bearing_z[B.lb_obs[i]];
+        }
+        auto upload_recs = [&](void** dst, const std::vector<int32_t>& idx, const std::vector<double>& z) -> int {
+            if (f32) {
+                std::vector<bos::dev::BRec<float>> r(idx.size());
+                for (size_t i = 0; i < r.size(); ++i) { r[i].idx = idx[i]; r[i].z = (float)z[i]; }
+                bos::dev::BRec<float>* d = nullptr;
+                const int e = upload(&d, r);
+                *dst = d;
+                return e;
+            }
+            std::vector<bos::dev::BRec<double>> r(idx.size());
+            for (size_t i = 0; i < r.size(); ++i) { r[i].idx = idx[i]; r[i].pad = 0; r[i].z = z[i]; }
+            bos::dev::BRec<double>* d = nullptr;
+            const int e = upload(&d, r);
+            *dst = d;
+            return e;
+        };
+        if ((rc = upload(&s->seg_ptr, B.seg_ptr)) || (rc = upload(&s->seg_blk, B.seg_blk)) ||
+            (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, B.po_ent)) ||
+            (rc = upload(&s->po_blk, B.po_blk)) || (rc = upload(&s->lb_ptr, B.lb_ptr)) ||
+            (rc = upload_recs(&s->pb, pbi, pbz)) || (rc = upload_recs(&s->lb, lbi, lbz)))
             return bail(rc);
         if (s->has_w) {
-            bw.resize(T.be_pose.size());
-            for (size_t i = 0; i < bw.size(); ++i) bw[i] = pb->bearing_omega[T.be_obs[i]];
-            if ((rc = upload_Tv(&s->be_w, bw))) return bail(rc);
+            pbw.resize(Mb); lbw.resize(Mb);
+            for (int i = 0; i < Mb; ++i) { pbw[i] = pb->bearing_omega[B.pb_obs[i]]; lbw[i] = pb->bearing_omega[B.lb_obs[i]]; }
+            if ((rc = upload_Tv(&s->pb_w, pbw)) || (rc = upload_Tv(&s->lb_w, lbw))) return bail(rc);
         }
-        if (s->has_dups && ((rc = upload_Tv(&s->be_woff, T.be_woff)) || (rc = upload_Tv(&s->oe_omoff, T.oe_omoff))))
-            return bail(rc);
+        s->pose_blocks = (int)(((int64_t)(P.p_end - P.p_begin) * B.lpp + bos::dev::kBlock - 1) / bos::dev::kBlock);
     }
     {
         std::vector<int32_t> os(pb->odom_src, pb->odom_src + s->Mo), od(pb->odom_dst, pb->odom_dst + s->Mo);
@@ -497,14 +523,28 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             (rc = upload_Tv(&s->o_om, om)))
             return bail(rc);
     }
+    // permuted dof -> reference dof
+    s->ref_dof.assign(P.n + 3, 0);
+    for (int u = 0; u < NP + NL; ++u) {
+        const int sz = u < NP ? 3 : 2;
+        const int ref0 = u < NP ? 3 * u : 3 * NP + 2 * (u - NP);
+        for (int d = 0; d < sz; ++d) s->ref_dof[P.node_dof[u] + d] = ref0 + d;
+    }
+    const int64_t nval = std::max<int64_t>(P.blk.size, 1), nb = 3 * (int64_t)NP + 2 * (int64_t)NL;
     if ((rc = upload(&s->node_dof, P.node_dof))) return bail(rc);
-    if ((rc = alloc_T(&s->d_val, std::max<int64_t>(P.nnzA(), 1))) || (rc = alloc_T(&s->d_b, P.n + 3)) ||
-        (rc = dalloc(&s->d_rhs, std::max<int64_t>(P.n, 1))))
+    if ((rc = alloc_T(&s->d_val, nval)) || (rc = alloc_T(&s->d_b, nb)) || (rc = dalloc(&s->d_rhs, std::max<int64_t>(P.n, 1))))
         return bail(rc);
-    if (f32 && (rc = dalloc(&s->d_val64, std::max<int64_t>(P.nnzA(), 1)))) return bail(rc);
-    HIP_TRY(hipMemset(s->d_val, 0, std::max<int64_t>(P.nnzA(), 1) * s->tsize));
-    HIP_TRY(hipMemset(s->d_b, 0, (P.n + 3) * s->tsize));
-    if ((rc = upload(&s->d_rowptr, P.rowptr)) || (rc = upload(&s->d_colind, P.colind))) return bail(rc);
+    if (f32 && s->solver_kind == BOS_SOLVER_SUPERNODAL && (rc = dalloc(&s->d_val64, nval))) return bail(rc);
+    HIP_TRY(hipMemset(s->d_val, 0, nval * s->tsize));
+    HIP_TRY(hipMemset(s->d_b, 0, nb * s->tsize));
+    {
+        std::vector<int32_t> er(s->ref_dof.begin(), s->ref_dof.begin() + P.n);
+        if ((rc = upload(&s->elim_ref, er))) return bail(rc);
+    }
+    if (s->solver_kind != BOS_SOLVER_SUPERNODAL &&
+        ((rc = upload(&s->d_rowptr, P.rowptr)) || (rc = upload(&s->d_colind, P.colind)) ||
+         (rc = upload(&s->csr_src, P.blk.csr_src)) || (rc = dalloc(&s->d_csr64, std::max<int64_t>(P.nnzA(), 1)))))
+        return bail(rc);
     if (s->solver_kind == BOS_SOLVER_SUPERNODAL) {
         std::string merr;
         if (bos::dev::mf_create(P.mf, &s->mf, merr)) return bail(fail(BOS_ERR_DEVICE, merr));
@@ -518,20 +558,13 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     } else {
         if ((rc = dalloc(&s->d_dense, (size_t)P.n * P.n))) return bail(rc);
     }
-    const int nt = std::max(1, P.tasks.ntask());
+    const int nt = std::max(1, s->pose_blocks);
     if ((rc = dalloc(&s->d_info, 1)) || (rc = dalloc(&s->d_chi_part, nt)) || (rc = dalloc(&s->d_nrob_part, nt)) ||
         (rc = dalloc(&s->d_chi, 1)) || (rc = dalloc(&s->d_nrob, 1)) || (rc = dalloc(&s->d_maxdx, 1)))
         return bail(rc);
     HIP_TRY(hipMemset(s->d_chi_part, 0, nt * sizeof(double)));
     HIP_TRY(hipMemset(s->d_nrob_part, 0, nt * sizeof(int32_t)));
     HIP_TRY(hipMemset(s->d_info, 0, sizeof(int32_t)));
-    // permuted dof -> reference dof
-    s->ref_dof.assign(P.n + 3, 0);
-    for (int u = 0; u < NP + NL; ++u) {
-        const int sz = u < NP ? 3 : 2;
-        const int ref0 = u < NP ? 3 * u : 3 * NP + 2 * (u - NP);
-        for (int d = 0; d < sz; ++d) s->ref_dof[P.node_dof[u] + d] = ref0 + d;
-    }
     if ((rc = refresh_cache(s))) return bail(rc);
     HIP_TRY(hipStreamSynchronize(s->stream));
     *out = s;
@@ -608,10 +641,12 @@ int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
     // compulsory reads of inputs + state, one write of every output block
     info->algorithmic_bytes = s->precision == BOS_FP32 ? 36 * Mb + 80 * Mo + 60 * NP + 32 * NL
                                                        : 64 * Mb + 152 * Mo + 120 * NP + 64 * NL;
-    info->num_items_pose = P.tasks.ntask();
-    info->num_items_landmark = P.tasks.nentries();
-    info->owned_first_row = P.row_begin;
-    info->owned_last_row = P.row_end;
+    info->num_block_values = P.blk.size;
+    info->lanes_per_pose = P.blk.lpp;
+    info->owned_first_pose = P.p_begin;
+    info->owned_last_pose = P.p_end;
+    info->owned_first_landmark = P.l_begin;
+    info->owned_last_landmark = P.l_end;
     return BOS_OK;
 }
 
@@ -623,13 +658,16 @@ int bos_export_system(const bos_solver* s, int64_t capacity, int32_t* rows, int3
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
     if (vals) {
+        const int64_t nv = P.blk.size;
+        std::vector<double> v(nv);
         if (s->precision == BOS_FP32) {
-            std::vector<float> v(nnz);
-            if (nnz) HIP_TRY(hipMemcpy(v.data(), s->d_val, nnz * sizeof(float), hipMemcpyDeviceToHost));
-            for (int64_t i = 0; i < nnz; ++i) vals[i] = v[i];
-        } else if (nnz) {
-            HIP_TRY(hipMemcpy(vals, s->d_val, nnz * sizeof(double), hipMemcpyDeviceToHost));
+            std::vector<float> f(nv);
+            if (nv) HIP_TRY(hipMemcpy(f.data(), s->d_val, nv * sizeof(float), hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < nv; ++i) v[i] = f[i];
+        } else if (nv) {
+            HIP_TRY(hipMemcpy(v.data(), s->d_val, nv * sizeof(double), hipMemcpyDeviceToHost));
         }
+        for (int64_t e = 0; e < nnz; ++e) vals[e] = v[P.blk.csr_src[e]];
     }
     if (rows || cols) {
         for (int64_t r = 0; r < P.n; ++r)
@@ -639,17 +677,16 @@ int bos_export_system(const bos_solver* s, int64_t capacity, int32_t* rows, int3
                 if (cols) cols[e] = std::min(a, c);
             }
     }
-    if (b) {
-        const int64_t nb = P.n + 3;
-        std::vector<double> bb(nb);
+    if (b) {   // b is kept in the reference numbering; the fixed pose's entries are not part of H_nf
+        const int64_t nb = 3 * (int64_t)s->NP + 2 * (int64_t)s->NL;
         if (s->precision == BOS_FP32) {
             std::vector<float> v(nb);
             HIP_TRY(hipMemcpy(v.data(), s->d_b, nb * sizeof(float), hipMemcpyDeviceToHost));
-            for (int64_t i = 0; i < nb; ++i) bb[i] = v[i];
+            for (int64_t i = 0; i < nb; ++i) b[i] = v[i];
         } else {
-            HIP_TRY(hipMemcpy(bb.data(), s->d_b, nb * sizeof(double), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(b, s->d_b, nb * sizeof(double), hipMemcpyDeviceToHost));
         }
-        for (int64_t i = 0; i < nb; ++i) b[s->ref_dof[i]] = bb[i];
+        for (int d = 0; d < 3; ++d) b[3 * (int64_t)P.fixed + d] = 0.0;
     }
     return BOS_OK;
 }

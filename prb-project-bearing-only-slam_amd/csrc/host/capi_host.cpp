@@ -194,8 +194,8 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
         info->n = P.n;
         info->nnz_lower = P.nnzA();
         info->nnz_factor = P.mf.L_size;
-        info->num_tasks_pose = P.tasks.ntask();
-        info->num_tasks_landmark = P.tasks.nentries();
+        info->num_block_values = P.blk.size;
+        info->lanes_per_pose = P.blk.lpp;
         info->flops_temporal = P.ordering.flops_temporal;
         info->flops_nested_dissection = P.ordering.flops_nd;
         info->mf_supernodes = P.mf.nsuper;
@@ -212,22 +212,36 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
                 const int32_t a = ref[r], c = ref[P.colind[e]];
                 if (ref_rows) ref_rows[e] = std::max(a, c);
                 if (ref_cols) ref_cols[e] = std::min(a, c);
-                if (owned) owned[e] = (r >= P.row_begin && r < P.row_end) ? 1 : 0;
+                if (owned) {
+                    const int64_t v = P.blk.csr_src[e];
+                    bool mine = false;
+                    for (int q = 0; q < 4; ++q) {
+                        const bos::Range& g = P.rank_val_ranges[4 * (size_t)rank + q];
+                        mine = mine || (v >= g.begin && v < g.end);
+                    }
+                    owned[e] = mine ? 1 : 0;
+                }
             }
     }
     if (perm_to_ref)
         for (int64_t i = 0; i < P.n + 3; ++i) perm_to_ref[i] = ref[i];
     if (b_owned) {
-        for (int64_t i = 0; i < P.n + 3; ++i)
-            b_owned[ref[i]] = (i >= P.row_begin && i < P.row_end) || (i >= P.n && rank == world - 1) ? 1 : 0;
+        for (int64_t i = 0; i < P.n + 3; ++i) {   // b lives in the reference numbering
+            bool mine = false;
+            for (int q = 0; q < 2; ++q) {
+                const bos::Range& g = P.rank_b_ranges[2 * (size_t)rank + q];
+                mine = mine || (i >= g.begin && i < g.end);
+            }
+            b_owned[i] = mine ? 1 : 0;
+        }
     }
     return BOS_OK;
 }
 
 // Test hook: runs the multifrontal algorithm of hip/multifrontal.hip on the host with the plan's
-// tree and maps (validates the symbolic structure without a GPU). vals: CSR values of the plan's
-// H layout (as ordered by bos_plan_inspect), rhs / x: permuted order of length n. Not used by
-// any solve path.
+// tree and maps (validates the symbolic structure without a GPU). vals: values of the stored
+// entries of H_nf in bos_plan_inspect's order (scattered into the block array here), rhs / x:
+// permuted order of length n. Not used by any solve path.
 int bos_plan_mf_selftest(const bos_problem* pb, const double* vals, const double* rhs, double* x) {
     if (!pb || !vals || !rhs || !x) return hfail(BOS_ERR_INVALID, "null argument");
     bos::ProblemIndex pi;
@@ -240,13 +254,15 @@ int bos_plan_mf_selftest(const bos_problem* pb, const double* vals, const double
     const int rc = bos::build_plan(pi, 0, 1, bos::kFactorMultifrontal, P, err);
     if (rc) return hfail(rc, err);
     const bos::Multifrontal& F = P.mf;
+    std::vector<double> hval(P.blk.size, 0.0);   // the block array the GPU solver reads
+    for (int64_t e = 0; e < P.nnzA(); ++e) hval[P.blk.csr_src[e]] = vals[e];
     std::vector<double> L(F.L_size), U(F.U_size), u(F.u_size);
     for (int64_t i = 0; i < P.n; ++i) x[i] = rhs[i];
     for (int lv = 0; lv < F.nlevels; ++lv)
         for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
             const int s = F.level[q], k = F.k[s], r = F.r[s], m = k + r;
             std::vector<double> W((size_t)m * m, 0.0);
-            for (int a = F.amap_ptr[s]; a < F.amap_ptr[s + 1]; ++a) W[F.amap_dst[a]] = vals[F.amap_src[a]];
+            for (int a = F.amap_ptr[s]; a < F.amap_ptr[s + 1]; ++a) W[F.amap_dst[a]] = hval[F.amap_src[a]];
             for (int ci = F.child_ptr[s]; ci < F.child_ptr[s + 1]; ++ci) {
                 const int c = F.child[ci], rc2 = F.r[c];
                 const int32_t* map = F.rmap.data() + F.rmap_off[c];

@@ -10,10 +10,7 @@ namespace bos {
 
 namespace {
 
-constexpr int kWave = 64;             // wavefront width on CDNA4
-constexpr int kMfLeaf = 12;
-constexpr int kStageCap = 1024;       // largest CSR span (values) a task assembles in LDS
-constexpr int kMaxTaskNodes = 48;     // nodes of one multi-node J+H task (hip/kernels.hpp kMaxTaskNodes)
+constexpr int kMfLeaf = 12;          // nested-dissection leaf size (nodes) for the multifrontal solver
 
 inline int node_size(int u, int NP) { return u < NP ? 3 : 2; }
 
@@ -313,15 +310,12 @@ int order_nodes(const ProblemIndex& pi, bool nd_only, std::vector<int32_t>& node
 }
 
 int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err);
+int build_layout(const ProblemIndex& pi, Plan& P, std::string& err);
+void build_ownership(const ProblemIndex& pi, Plan& P, int rank, int world);
+int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& inv, std::string& err);
 
 int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
                        const std::vector<std::pair<int32_t, int32_t>>& blocks, std::string& err);
-
-template <typename BlockOffset>
-int build_tasks(const ProblemIndex& pi, Plan& P, int q_begin, int q_end, const std::vector<int32_t>& pb_ptr,
-                const std::vector<int32_t>& pb, const std::vector<int32_t>& lb_ptr, const std::vector<int32_t>& lb,
-                const std::vector<int32_t>& po_ptr, const std::vector<int32_t>& po, BlockOffset&& block_offset,
-                std::string& err);
 
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& P, std::string& err) {
     const bool want_factor = factor_mode == kFactorScalar;
@@ -362,13 +356,10 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     P.node_dof[pi.fixed] = (int32_t)dof;
     if (dof + 3 > INT32_MAX) { err = "system too large for 32-bit indices"; return BOS_ERR_UNSUPPORTED; }
 
-    // lower neighbours (by position) of every node, with their offsets inside the node's rows
+    // lower neighbours (by position) of every node -> CSR rows of the lower triangle
     std::vector<int64_t> lptr(n_nodes + 1, 0);
     std::vector<int32_t> lnb;              // neighbour node ids, sorted by position
-    std::vector<int32_t> loff;             // entry offset of that neighbour's block in each row
     lnb.reserve(g.adj.size() / 2 + 1);
-    P.node_base.assign(n_nodes, -1);
-    P.node_row0.assign(n_nodes, -1);
     P.rowptr.assign(P.n + 1, 0);
     for (int i = 0; i < m; ++i) {
         const int u = inv[i];
@@ -378,8 +369,7 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
         std::sort(nb.begin(), nb.end(), [&](int a, int b) { return P.node_pos[a] < P.node_pos[b]; });
         lptr[u] = (int64_t)lnb.size();
         int32_t off = 0;
-        for (int v : nb) { lnb.push_back(v); loff.push_back(off); off += node_size(v, NP); }
-        P.node_base[u] = off;
+        for (int v : nb) { lnb.push_back(v); off += node_size(v, NP); }
         const int su = node_size(u, NP);
         const int64_t r0 = P.node_dof[u];
         for (int d = 0; d < su; ++d) P.rowptr[r0 + d + 1] = off + d + 1;   // row lengths for now
@@ -397,7 +387,6 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
         const int u = inv[i];
         const int su = node_size(u, NP);
         const int64_t r0 = P.node_dof[u];
-        P.node_row0[u] = P.rowptr[r0];
         for (int d = 0; d < su; ++d) {
             int64_t w = P.rowptr[r0 + d];
             for (int64_t e = lptr[u]; e < lend[u]; ++e) {
@@ -407,17 +396,6 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
             for (int c = 0; c <= d; ++c) P.colind[w++] = (int32_t)(r0 + c);
         }
     }
-    auto block_offset = [&](int owner, int other) -> int32_t {
-        // offset of other's block inside owner's rows (binary search by position)
-        int64_t lo = lptr[owner], hi = lend[owner];
-        const int key = P.node_pos[other];
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) / 2;
-            if (P.node_pos[lnb[mid]] < key) lo = mid + 1; else hi = mid;
-        }
-        return (lo < lend[owner] && lnb[lo] == other) ? loff[lo] : -1;
-    };
-
     // symbolic Cholesky factor, scalar CSR (lower incl. diagonal)
     if (want_factor) {
         std::vector<int64_t> rptr;
@@ -446,273 +424,201 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
         }
     }
 
-    // incidence lists
-    std::vector<int32_t> pb_ptr(NP + 1, 0), lb_ptr(NL + 1, 0), po_ptr(NP + 1, 0);
-    for (int k = 0; k < pi.Mb; ++k) { ++pb_ptr[pi.b_pose[k] + 1]; ++lb_ptr[pi.b_lm[k] + 1]; }
-    for (int k = 0; k < pi.Mo; ++k) { ++po_ptr[pi.o_src[k] + 1]; ++po_ptr[pi.o_dst[k] + 1]; }
-    for (int i = 0; i < NP; ++i) { pb_ptr[i + 1] += pb_ptr[i]; po_ptr[i + 1] += po_ptr[i]; }
-    for (int j = 0; j < NL; ++j) lb_ptr[j + 1] += lb_ptr[j];
-    std::vector<int32_t> pb(pi.Mb), lb(pi.Mb), po(2 * (size_t)pi.Mo);
-    {
-        std::vector<int32_t> a(pb_ptr.begin(), pb_ptr.end() - 1), b(lb_ptr.begin(), lb_ptr.end() - 1),
-            c(po_ptr.begin(), po_ptr.end() - 1);
-        for (int k = 0; k < pi.Mb; ++k) { pb[a[pi.b_pose[k]]++] = k; lb[b[pi.b_lm[k]]++] = k; }
-        for (int k = 0; k < pi.Mo; ++k) { po[c[pi.o_src[k]]++] = 2 * k; po[c[pi.o_dst[k]]++] = 2 * k + 1; }
-    }
-
-    // ownership: contiguous position ranges balanced by work (incident items)
-    std::vector<int64_t> work(m);
-    int64_t total = 0;
-    for (int i = 0; i < m; ++i) {
-        const int u = inv[i];
-        work[i] = 1 + (u < NP ? (pb_ptr[u + 1] - pb_ptr[u]) + (po_ptr[u + 1] - po_ptr[u]) : (lb_ptr[u - NP + 1] - lb_ptr[u - NP]));
-        total += work[i];
-    }
-    std::vector<int32_t> cut(world + 1, 0);
-    {
-        int64_t acc = 0;
-        int r = 1;
-        for (int i = 0; i < m && r < world; ++i) {
-            acc += work[i];
-            while (r < world && acc * world >= total * r) cut[r++] = i + 1;
-        }
-        while (r < world) cut[r++] = m;
-        cut[world] = m;
-    }
-    P.rank_row_begin.assign(world + 1, 0);
-    for (int r = 0; r <= world; ++r) P.rank_row_begin[r] = cut[r] < m ? P.node_dof[inv[cut[r]]] : (int32_t)P.n;
-    P.row_begin = P.rank_row_begin[rank];
-    P.row_end = P.rank_row_begin[rank + 1];
-    P.val_begin = P.rowptr[P.row_begin];
-    P.val_end = P.rowptr[P.row_end];
-
-    // per-position node layout (the J+H kernel walks positions)
-    P.pos_node.assign(m, 0); P.pos_row0.assign(m + 1, 0); P.pos_base.assign(m, 0); P.pos_dof.assign(m + 1, 0);
-    for (int q = 0; q < m; ++q) {
-        const int u = inv[q];
-        P.pos_node[q] = u; P.pos_row0[q] = P.node_row0[u]; P.pos_base[q] = P.node_base[u]; P.pos_dof[q] = P.node_dof[u];
-    }
-    P.pos_row0[m] = (int32_t)P.nnzA();
-    P.pos_dof[m] = (int32_t)P.n;
-    rc = build_tasks(pi, P, cut[rank], cut[rank + 1], pb_ptr, pb, lb_ptr, lb, po_ptr, po, block_offset, err);
-    if (rc) return rc;
+    if ((rc = build_layout(pi, P, err))) return rc;
+    build_ownership(pi, P, rank, world);
+    if ((rc = build_csr_src(pi, P, inv, err))) return rc;
     if (factor_mode == kFactorMultifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, err))) return rc;
     return validate_plan(pi, P, err);
 }
 
-// Node-range tasks of the J+H kernel (see RangeTasks in plan.hpp).
-template <typename BlockOffset>
-int build_tasks(const ProblemIndex& pi, Plan& P, int q_begin, int q_end, const std::vector<int32_t>& pb_ptr,
-                const std::vector<int32_t>& pb, const std::vector<int32_t>& lb_ptr, const std::vector<int32_t>& lb,
-                const std::vector<int32_t>& po_ptr, const std::vector<int32_t>& po, BlockOffset&& block_offset,
-                std::string& err) {
-    const int NP = pi.NP;
-    RangeTasks& T = P.tasks;
-    T = RangeTasks();
-    const int m = (int)P.pos_node.size();
-    T.cl_ptr.assign(m + 1, 0);
-    std::vector<int32_t> stamp_b(pi.Mb, -1), stamp_o(pi.Mo, -1);
-    auto pos_of = [&](int node) { return node == pi.fixed ? -1 : P.node_pos[node]; };
-    auto count_entries = [&](int q, int tid) {   // new entries node at q would add to task tid
-        const int u = P.pos_node[q];
-        int c = 0;
-        if (u < NP) {
-            for (int32_t e = pb_ptr[u]; e < pb_ptr[u + 1]; ++e) c += stamp_b[pb[e]] != tid;
-            for (int32_t e = po_ptr[u]; e < po_ptr[u + 1]; ++e) c += stamp_o[po[e] >> 1] != tid;
-        } else {
-            const int l = u - NP;
-            for (int32_t e = lb_ptr[l]; e < lb_ptr[l + 1]; ++e) c += stamp_b[lb[e]] != tid;
+// Block layout of H and the J+H work split (see BlockLayout in plan.hpp).
+int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
+    const int NP = pi.NP, NL = pi.NL, Mb = pi.Mb, Mo = pi.Mo;
+    BlockLayout& B = P.blk;
+    B = BlockLayout();
+    // bearings by (pose, landmark, index) and by (landmark, pose, index)
+    B.pb_ptr.assign(NP + 1, 0);
+    B.lb_ptr.assign(NL + 1, 0);
+    for (int k = 0; k < Mb; ++k) { ++B.pb_ptr[pi.b_pose[k] + 1]; ++B.lb_ptr[pi.b_lm[k] + 1]; }
+    for (int p = 0; p < NP; ++p) B.pb_ptr[p + 1] += B.pb_ptr[p];
+    for (int l = 0; l < NL; ++l) B.lb_ptr[l + 1] += B.lb_ptr[l];
+    B.pb_obs.resize(Mb);
+    B.lb_obs.resize(Mb);
+    {
+        std::vector<int32_t> wp(B.pb_ptr.begin(), B.pb_ptr.end() - 1), wl(B.lb_ptr.begin(), B.lb_ptr.end() - 1);
+        for (int k = 0; k < Mb; ++k) { B.pb_obs[wp[pi.b_pose[k]]++] = k; B.lb_obs[wl[pi.b_lm[k]]++] = k; }
+    }
+    for (int p = 0; p < NP; ++p)
+        std::stable_sort(B.pb_obs.begin() + B.pb_ptr[p], B.pb_obs.begin() + B.pb_ptr[p + 1],
+                         [&](int a, int b) { return pi.b_lm[a] < pi.b_lm[b]; });
+    for (int l = 0; l < NL; ++l)
+        std::stable_sort(B.lb_obs.begin() + B.lb_ptr[l], B.lb_obs.begin() + B.lb_ptr[l + 1],
+                         [&](int a, int b) { return pi.b_pose[a] < pi.b_pose[b]; });
+    // unique pose-landmark pairs = pose-landmark blocks
+    B.ub_ptr.assign(NP + 1, 0);
+    for (int p = 0; p < NP; ++p) {
+        for (int i = B.pb_ptr[p]; i < B.pb_ptr[p + 1]; ++i) {
+            const int l = pi.b_lm[B.pb_obs[i]];
+            if (i > B.pb_ptr[p] && l == pi.b_lm[B.pb_obs[i - 1]]) { B.has_dups = true; continue; }
+            B.ub_lm.push_back(l);
+        }
+        B.ub_ptr[p + 1] = (int32_t)B.ub_lm.size();
+    }
+    // odometry entries of each pose: source side sorted by (dst, edge), then destination side by (src, edge)
+    B.po_ptr.assign(NP + 1, 0);
+    for (int k = 0; k < Mo; ++k) { ++B.po_ptr[pi.o_src[k] + 1]; ++B.po_ptr[pi.o_dst[k] + 1]; }
+    for (int p = 0; p < NP; ++p) B.po_ptr[p + 1] += B.po_ptr[p];
+    B.po_ent.resize(2 * (size_t)Mo);
+    {
+        std::vector<int32_t> w(B.po_ptr.begin(), B.po_ptr.end() - 1);
+        for (int k = 0; k < Mo; ++k) { B.po_ent[w[pi.o_src[k]]++] = 2 * k; B.po_ent[w[pi.o_dst[k]]++] = 2 * k + 1; }
+    }
+    auto other = [&](int32_t ent) { return (ent & 1) ? pi.o_src[ent >> 1] : pi.o_dst[ent >> 1]; };
+    for (int p = 0; p < NP; ++p)
+        std::sort(B.po_ent.begin() + B.po_ptr[p], B.po_ent.begin() + B.po_ptr[p + 1], [&](int32_t a, int32_t b) {
+            if ((a & 1) != (b & 1)) return (a & 1) < (b & 1);
+            if (other(a) != other(b)) return other(a) < other(b);
+            return a < b;
+        });
+    B.po_blk.assign(B.po_ent.size(), -1);
+    B.uo_ptr.assign(NP + 1, 0);
+    for (int p = 0; p < NP; ++p) {
+        for (int x = B.po_ptr[p]; x < B.po_ptr[p + 1]; ++x) {
+            const int32_t e = B.po_ent[x];
+            if (e & 1) continue;
+            if (x > B.po_ptr[p] && !(B.po_ent[x - 1] & 1) && other(B.po_ent[x - 1]) == other(e)) {
+                B.has_dups = true;
+                B.po_blk[x] = B.po_blk[x - 1];
+                continue;
+            }
+            B.po_blk[x] = (int32_t)B.uo_dst.size();
+            B.uo_dst.push_back(other(e));
+        }
+        B.uo_ptr[p + 1] = (int32_t)B.uo_dst.size();
+    }
+    for (int s = 0; s < NP; ++s)
+        for (int u = B.uo_ptr[s]; u < B.uo_ptr[s + 1]; ++u) {
+            const int d = B.uo_dst[u];
+            if (std::binary_search(B.uo_dst.begin() + B.uo_ptr[d], B.uo_dst.begin() + B.uo_ptr[d + 1], s)) {
+                err = "odometry edges in both directions between the same poses (not supported)";
+                return BOS_ERR_UNSUPPORTED;
+            }
+        }
+    // lanes per pose and their bearing segments (lane 0 also takes the odometry entries; a run of
+    // duplicate observations of one pair never straddles two lanes)
+    const double avg = NP ? (double)Mb / NP : 0.0;
+    B.lpp = avg >= 24 ? 4 : avg >= 8 ? 2 : 1;
+    const int L = B.lpp;
+    B.seg_ptr.assign((size_t)NP * L + 1, 0);
+    B.seg_blk.assign((size_t)NP * L, 0);
+    for (int p = 0; p < NP; ++p) {
+        const int b0 = B.pb_ptr[p], b1 = B.pb_ptr[p + 1], nb = b1 - b0;
+        const int no = B.po_ptr[p + 1] - B.po_ptr[p];
+        const int share = (nb + no + L - 1) / L;
+        const int q0 = std::min(nb, std::max(0, share - no));
+        std::vector<int> cut(L + 1);
+        cut[0] = b0;
+        cut[L] = b1;
+        for (int j = 1; j < L; ++j) {
+            int c = b0 + q0 + (int)((int64_t)(nb - q0) * (j - 1) / std::max(1, L - 1));
+            c = std::max(c, cut[j - 1]);
+            while (c > b0 && c < b1 && pi.b_lm[B.pb_obs[c]] == pi.b_lm[B.pb_obs[c - 1]]) ++c;
+            cut[j] = c;
+        }
+        int blk = B.ub_ptr[p];
+        for (int j = 0; j < L; ++j) {
+            B.seg_ptr[(size_t)p * L + j] = cut[j];
+            B.seg_blk[(size_t)p * L + j] = blk;
+            for (int i = cut[j]; i < cut[j + 1]; ++i)
+                if (i + 1 == cut[j + 1] || pi.b_lm[B.pb_obs[i + 1]] != pi.b_lm[B.pb_obs[i]]) ++blk;
+        }
+    }
+    B.seg_ptr[(size_t)NP * L] = Mb;
+    B.off_ldiag = 6 * (int64_t)NP;
+    B.off_pl = (B.off_ldiag + 3 * (int64_t)NL + 1) & ~(int64_t)1;   // even: 2-value vector stores stay aligned
+    B.off_pp = B.off_pl + 6 * (int64_t)B.nub();
+    B.size = B.off_pp + 6 * (int64_t)B.nuo();
+    if (B.size > INT32_MAX) { err = "block array exceeds 32-bit indices"; return BOS_ERR_UNSUPPORTED; }
+    return BOS_OK;
+}
+
+// Ownership cuts for observation sharding: contiguous pose and landmark ranges balanced by the
+// observations each lane group evaluates.
+void build_ownership(const ProblemIndex& pi, Plan& P, int rank, int world) {
+    const BlockLayout& B = P.blk;
+    auto cuts = [&](int n, auto&& work) {
+        std::vector<int32_t> c(world + 1, n);
+        c[0] = 0;
+        int64_t total = 0;
+        for (int i = 0; i < n; ++i) total += work(i);
+        int64_t acc = 0;
+        int r = 1;
+        for (int i = 0; i < n && r < world; ++i) {
+            acc += work(i);
+            while (r < world && acc * world >= total * r) c[r++] = i + 1;
         }
         return c;
     };
-    auto mark = [&](int q, int tid) {
-        const int u = P.pos_node[q];
-        if (u < NP) {
-            for (int32_t e = pb_ptr[u]; e < pb_ptr[u + 1]; ++e) stamp_b[pb[e]] = tid;
-            for (int32_t e = po_ptr[u]; e < po_ptr[u + 1]; ++e) stamp_o[po[e] >> 1] = tid;
-        } else {
-            for (int32_t e = lb_ptr[u - NP]; e < lb_ptr[u - NP + 1]; ++e) stamp_b[lb[e]] = tid;
-        }
+    P.rank_pose = cuts(pi.NP, [&](int p) { return (int64_t)1 + B.pb_ptr[p + 1] - B.pb_ptr[p] + B.po_ptr[p + 1] - B.po_ptr[p]; });
+    P.rank_lm = cuts(pi.NL, [&](int l) { return (int64_t)1 + B.lb_ptr[l + 1] - B.lb_ptr[l]; });
+    P.rank = rank;
+    P.world = world;
+    P.p_begin = P.rank_pose[rank]; P.p_end = P.rank_pose[rank + 1];
+    P.l_begin = P.rank_lm[rank]; P.l_end = P.rank_lm[rank + 1];
+    P.rank_val_ranges.resize(4 * (size_t)world);
+    P.rank_b_ranges.resize(2 * (size_t)world);
+    for (int r = 0; r < world; ++r) {
+        const int p0 = P.rank_pose[r], p1 = P.rank_pose[r + 1], l0 = P.rank_lm[r], l1 = P.rank_lm[r + 1];
+        Range* v = &P.rank_val_ranges[4 * (size_t)r];
+        v[0] = {6 * (int64_t)p0, 6 * (int64_t)p1};
+        v[1] = {B.off_ldiag + 3 * (int64_t)l0, B.off_ldiag + 3 * (int64_t)l1};
+        v[2] = {B.off_pl + 6 * (int64_t)B.ub_ptr[p0], B.off_pl + 6 * (int64_t)B.ub_ptr[p1]};
+        v[3] = {B.off_pp + 6 * (int64_t)B.uo_ptr[p0], B.off_pp + 6 * (int64_t)B.uo_ptr[p1]};
+        Range* bb = &P.rank_b_ranges[2 * (size_t)r];
+        bb[0] = {3 * (int64_t)p0, 3 * (int64_t)p1};
+        bb[1] = {3 * (int64_t)pi.NP + 2 * (int64_t)l0, 3 * (int64_t)pi.NP + 2 * (int64_t)l1};
+    }
+}
+
+// Block value feeding every stored entry (row >= col) of the lower triangle of P^T H_nf P.
+int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& inv, std::string& err) {
+    const int NP = pi.NP;
+    const BlockLayout& B = P.blk;
+    std::vector<int32_t> dof_node(P.n), dof_loc(P.n);
+    for (int u : inv)
+        for (int d = 0; d < node_size(u, NP); ++d) { dof_node[P.node_dof[u] + d] = u; dof_loc[P.node_dof[u] + d] = d; }
+    auto tri = [](int r, int c) { return r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r; };
+    auto pl_block = [&](int p, int l) -> int64_t {
+        const auto b = B.ub_lm.begin() + B.ub_ptr[p], e = B.ub_lm.begin() + B.ub_ptr[p + 1];
+        const auto it = std::lower_bound(b, e, l);
+        return (it != e && *it == l) ? (int64_t)(it - B.ub_lm.begin()) : -1;
     };
-    // 1. cut the position range into tasks
-    T.task_q.push_back(q_begin);
-    int tid = 0;
-    for (int q = q_begin; q < q_end;) {
-        int entries = count_entries(q, tid);
-        mark(q, tid);
-        int q1 = q + 1;
-        if (entries <= kWave && P.pos_row0[q1] - P.pos_row0[q] <= kStageCap) {
-            while (q1 < q_end && q1 - q < kMaxTaskNodes) {
-                const int add = count_entries(q1, tid);
-                if (entries + add > kWave || P.pos_row0[q1 + 1] - P.pos_row0[q] > kStageCap) break;
-                entries += add;
-                mark(q1, tid);
-                ++q1;
+    auto pp_block = [&](int s, int d) -> int64_t {
+        const auto b = B.uo_dst.begin() + B.uo_ptr[s], e = B.uo_dst.begin() + B.uo_ptr[s + 1];
+        const auto it = std::lower_bound(b, e, d);
+        return (it != e && *it == d) ? (int64_t)(it - B.uo_dst.begin()) : -1;
+    };
+    P.blk.csr_src.resize(P.nnzA());
+    for (int64_t row = 0; row < P.n; ++row) {
+        const int U = dof_node[row], a = dof_loc[row];
+        for (int64_t e = P.rowptr[row]; e < P.rowptr[row + 1]; ++e) {
+            const int V = dof_node[P.colind[e]], c = dof_loc[P.colind[e]];
+            int64_t v = -1;
+            if (U == V) {
+                v = U < NP ? 6 * (int64_t)U + tri(a, c) : B.off_ldiag + 3 * (int64_t)(U - NP) + tri(a, c);
+            } else if (U < NP && V >= NP) {
+                const int64_t k = pl_block(U, V - NP);
+                if (k >= 0) v = B.off_pl + 6 * k + 2 * a + c;
+            } else if (U >= NP && V < NP) {
+                const int64_t k = pl_block(V, U - NP);
+                if (k >= 0) v = B.off_pl + 6 * k + 2 * c + a;
+            } else if (U < NP && V < NP) {
+                int64_t k = pp_block(U, V);
+                if (k < 0) k = pp_block(V, U);
+                if (k >= 0) v = B.off_pp + 6 * k + tri(a, c);
             }
-        }
-        T.task_q.push_back(q1);
-        q = q1;
-        ++tid;
-    }
-    // 2. entries, flags, contribution lists
-    std::fill(stamp_b.begin(), stamp_b.end(), -1);
-    std::fill(stamp_o.begin(), stamp_o.end(), -1);
-    T.task_be.push_back(0);
-    T.task_oe.push_back(0);
-    std::vector<std::vector<uint16_t>> node_slots;
-    for (int t = 0; t < (int)T.task_q.size() - 1; ++t) {
-        const int q0 = T.task_q[t], q1 = T.task_q[t + 1];
-        const int v0 = P.pos_row0[q0];
-        const bool single = q1 - q0 == 1;
-        const bool staged = P.pos_row0[q1] - v0 <= kStageCap;
-        T.task_flags.push_back((uint8_t)((staged ? 1 : 0) | (single ? 2 : 0)));
-        auto inside = [&](int node) { const int q = pos_of(node); return q >= q0 && q < q1; };
-        auto owner_and_slot = [&](int a, int b, int& meta) {
-            // the block (a, b) lives in the rows of the later of the two (the fixed pose has no rows)
-            if (a == pi.fixed || b == pi.fixed) return;
-            const bool b_owner = P.node_pos[b] > P.node_pos[a];
-            const int own = b_owner ? b : a, oth = b_owner ? a : b;
-            if (!inside(own)) return;
-            const int32_t off = block_offset(own, oth);
-            if (off < 0) { meta = -1; return; }
-            meta |= 8 | (b_owner ? 16 : 0) | ((P.node_row0[own] + off - v0) << 8);
-        };
-        auto counts_here = [&](int a, int b) {
-            // chi^2 of an observation is counted in the task of its owner (or of its non-fixed end)
-            int own;
-            if (a == pi.fixed) own = b;
-            else if (b == pi.fixed) own = a;
-            else own = P.node_pos[b] > P.node_pos[a] ? b : a;
-            return inside(own);
-        };
-        const int be_first = (int)T.be_pose.size(), oe_first = (int)T.oe_edge.size();
-        for (int q = q0; q < q1; ++q) {
-            const int u = P.pos_node[q];
-            if (u < NP) {
-                for (int32_t e = pb_ptr[u]; e < pb_ptr[u + 1]; ++e) {
-                    const int k = pb[e];
-                    if (stamp_b[k] == t) continue;
-                    stamp_b[k] = t;
-                    const int p = pi.b_pose[k], l = NP + pi.b_lm[k];
-                    int meta = (inside(p) ? 1 : 0) | (inside(l) ? 2 : 0) | (counts_here(p, l) ? 4 : 0);
-                    owner_and_slot(p, l, meta);
-                    if (meta < 0) { err = "internal error: bearing block missing"; return BOS_ERR_INVALID; }
-                    T.be_pose.push_back(pi.b_pose[k]); T.be_lm.push_back(pi.b_lm[k]);
-                    T.be_meta.push_back(meta); T.be_obs.push_back(k);
-                }
-                for (int32_t e = po_ptr[u]; e < po_ptr[u + 1]; ++e) {
-                    const int k = po[e] >> 1;
-                    if (stamp_o[k] == t) continue;
-                    stamp_o[k] = t;
-                    const int s = pi.o_src[k], d = pi.o_dst[k];
-                    int meta = (inside(s) ? 1 : 0) | (inside(d) ? 2 : 0) | (counts_here(s, d) ? 4 : 0);
-                    owner_and_slot(s, d, meta);
-                    if (meta < 0) { err = "internal error: odometry block missing"; return BOS_ERR_INVALID; }
-                    T.oe_edge.push_back(k); T.oe_meta.push_back(meta);
-                }
-            } else {
-                for (int32_t e = lb_ptr[u - NP]; e < lb_ptr[u - NP + 1]; ++e) {
-                    const int k = lb[e];
-                    if (stamp_b[k] == t) continue;
-                    stamp_b[k] = t;
-                    const int p = pi.b_pose[k], l = NP + pi.b_lm[k];
-                    int meta = (inside(p) ? 1 : 0) | (inside(l) ? 2 : 0) | (counts_here(p, l) ? 4 : 0);
-                    owner_and_slot(p, l, meta);
-                    if (meta < 0) { err = "internal error: bearing block missing"; return BOS_ERR_INVALID; }
-                    T.be_pose.push_back(pi.b_pose[k]); T.be_lm.push_back(pi.b_lm[k]);
-                    T.be_meta.push_back(meta); T.be_obs.push_back(k);
-                }
-            }
-        }
-        const int nb = (int)T.be_pose.size() - be_first, no = (int)T.oe_edge.size() - oe_first;
-        T.max_entries = std::max(T.max_entries, nb + no);
-        if (!single && nb + no > kWave) { err = "internal error: task too large"; return BOS_ERR_INVALID; }
-        // contribution slots per node (entry order = fixed reduction order)
-        for (int q = q0; q < q1; ++q) {
-            const int u = P.pos_node[q];
-            std::vector<uint16_t> sl;
-            for (int i = 0; i < nb; ++i) {
-                const int bi = be_first + i;
-                if (u < NP ? (T.be_pose[bi] == u) : (T.be_lm[bi] == u - NP)) sl.push_back((uint16_t)(2 * i + (u < NP ? 0 : 1)));
-            }
-            for (int j = 0; j < no; ++j) {
-                const int k = T.oe_edge[oe_first + j];
-                if (u < NP && pi.o_src[k] == u) sl.push_back((uint16_t)(2 * (nb + j)));
-                if (u < NP && pi.o_dst[k] == u) sl.push_back((uint16_t)(2 * (nb + j) + 1));
-            }
-            T.cl_ptr[q + 1] = (int32_t)sl.size();
-            if (!single) T.cl.insert(T.cl.end(), sl.begin(), sl.end());
-            else T.cl_ptr[q + 1] = 0;   // single-node tasks reduce every entry
-        }
-        T.task_be.push_back((int32_t)T.be_pose.size());
-        T.task_oe.push_back((int32_t)T.oe_edge.size());
-    }
-    for (int q = 0; q < m; ++q) T.cl_ptr[q + 1] += T.cl_ptr[q];
-    // 3. duplicate off-diagonal blocks: the first entry of a group writes, with the group's summed
-    //    information; the others do not write
-    T.be_woff.clear();
-    T.oe_omoff.clear();
-    {
-        std::vector<std::pair<int64_t, int>> key;   // (absolute slot, entry)
-        for (int t = 0; t < T.ntask(); ++t) {
-            const int v0 = P.pos_row0[T.task_q[t]];
-            for (int i = T.task_be[t]; i < T.task_be[t + 1]; ++i)
-                if (T.be_meta[i] & 8) key.push_back({(int64_t)v0 + (T.be_meta[i] >> 8), i});
-            for (int j = T.task_oe[t]; j < T.task_oe[t + 1]; ++j)
-                if (T.oe_meta[j] & 8) key.push_back({(int64_t)v0 + (T.oe_meta[j] >> 8), -1 - j});
-        }
-        std::sort(key.begin(), key.end());
-        for (size_t a = 0; a < key.size();) {
-            size_t b = a + 1;
-            while (b < key.size() && key[b].first == key[a].first) ++b;
-            if (b - a > 1) {
-                if (!T.has_dups) {
-                    T.has_dups = true;
-                    T.be_woff.assign(T.be_pose.size(), 0.0);
-                    T.oe_omoff.assign(6 * T.oe_edge.size(), 0.0);
-                    for (size_t i = 0; i < T.be_pose.size(); ++i) T.be_woff[i] = (T.be_meta[i] & 8) ? 1.0 : 0.0;
-                }
-                const bool bearing = key[a].second >= 0;
-                for (size_t c = a; c < b; ++c)
-                    if ((key[c].second >= 0) != bearing) { err = "bearing and odometry share a block"; return BOS_ERR_INVALID; }
-                if (bearing) {
-                    double wsum = 0;
-                    for (size_t c = a; c < b; ++c) {
-                        const int i = key[c].second;
-                        wsum += pi.b_omega ? pi.b_omega[T.be_obs[i]] : 1.0;
-                        if (c > a) { T.be_meta[i] &= ~8; T.be_woff[i] = 0.0; }
-                    }
-                    T.be_woff[key[a].second] = wsum;
-                } else {
-                    const int j0 = -1 - key[a].second;
-                    const int s0 = pi.o_src[T.oe_edge[j0]];
-                    double om[6] = {0, 0, 0, 0, 0, 0};
-                    for (size_t c = a; c < b; ++c) {
-                        const int j = -1 - key[c].second;
-                        if (pi.o_src[T.oe_edge[j]] != s0) {
-                            err = "odometry edges in both directions between the same poses (not supported)";
-                            return BOS_ERR_UNSUPPORTED;
-                        }
-                        const double* M = pi.o_omega + 9 * (size_t)T.oe_edge[j];
-                        const double u6[6] = {M[0], M[1], M[2], M[4], M[5], M[8]};
-                        for (int z = 0; z < 6; ++z) om[z] += u6[z];
-                        if (c > a) T.oe_meta[j] &= ~8;
-                    }
-                    for (int z = 0; z < 6; ++z) T.oe_omoff[6 * (size_t)j0 + z] = om[z];
-                }
-            }
-            a = b;
-        }
-        if (T.has_dups) {   // entries of singleton blocks use their own information
-            for (size_t j = 0; j < T.oe_edge.size(); ++j) {
-                bool zero = true;
-                for (int z = 0; z < 6; ++z) zero = zero && T.oe_omoff[6 * j + z] == 0.0;
-                if (zero && (T.oe_meta[j] & 8)) {
-                    const double* M = pi.o_omega + 9 * (size_t)T.oe_edge[j];
-                    const double u6[6] = {M[0], M[1], M[2], M[4], M[5], M[8]};
-                    for (int z = 0; z < 6; ++z) T.oe_omoff[6 * j + z] = u6[z];
-                }
-            }
+            if (v < 0) { err = "internal error: stored entry without a block"; return BOS_ERR_INVALID; }
+            P.blk.csr_src[e] = (int32_t)v;
         }
     }
     return BOS_OK;
@@ -828,7 +734,8 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
         std::vector<int32_t> w(F.level_ptr.begin(), F.level_ptr.end() - 1);
         for (int s = 0; s < ns; ++s) F.level[w[lev[s]]++] = s;
     }
-    // assembly map: every stored entry of H (row i >= col j) goes to the front of col j's supernode
+    // assembly map: every stored entry of H (row i >= col j) goes to the front of col j's supernode,
+    // read from its block value
     std::vector<int32_t> sn_of_dof(P.n);
     for (int s = 0; s < ns; ++s)
         for (int d = 0; d < F.k[s]; ++d) sn_of_dof[F.col0[s] + d] = s;
@@ -852,87 +759,96 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
         std::vector<int32_t> w(F.amap_ptr.begin(), F.amap_ptr.end() - 1);
         for (int64_t e = 0; e < nnz; ++e) {
             const int32_t q = w[tgt[e]]++;
-            F.amap_src[q] = (int32_t)e;
+            F.amap_src[q] = P.blk.csr_src[e];
             F.amap_dst[q] = dst[e];
         }
     }
     return BOS_OK;
 }
 
-// Proves, on the host, that every address the J+H kernel writes (hip/kernels.hip diag_pos /
-// off_pos) lies inside the intended CSR row at the intended column, so a kernel launch can
-// never write out of bounds. O(items).
+// Proves, on the host, that the J+H kernel's writes (simulated here exactly as hip/kernels.hip
+// issues them) stay inside the block array, cover this rank's ranges exactly once and nothing
+// else, that chi^2 counts every observation once, and that every stored entry of H_nf reads a
+// block value its kernel writes. O(observations + nnz).
 int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
-    const int NP = pi.NP;
-    const int64_t nnz = P.nnzA();
-    const RangeTasks& T = P.tasks;
-    auto check_entry = [&](int owner, int r, int64_t pos, int32_t want_col) -> bool {
-        const int64_t row = (int64_t)P.node_dof[owner] + r;
-        if (row < 0 || row >= P.n) return false;
-        if (pos < P.rowptr[row] || pos >= P.rowptr[row + 1] || pos >= nnz) return false;
-        return P.colind[pos] == want_col;
-    };
-    auto pos_off = [](int64_t slot, int base, int r, int c) { return slot + (int64_t)r * base + r * (r + 1) / 2 + c; };
-    auto pos_diag = [](int64_t row0, int base, int r, int c) { return row0 + (int64_t)r * base + r * (r + 1) / 2 + base + c; };
-    std::vector<uint8_t> hit(nnz, 0);
-    std::vector<int32_t> bcount(P.n, 0);
+    const int NP = pi.NP, NL = pi.NL;
+    const BlockLayout& B = P.blk;
+    const int L = B.lpp;
+    std::vector<uint8_t> hit(B.size, 0), bhit(3 * (size_t)NP + 2 * (size_t)NL, 0);
     std::vector<int32_t> chi(pi.Mb + pi.Mo, 0);
-    for (int t = 0; t < T.ntask(); ++t) {
-        const int q0 = T.task_q[t], q1 = T.task_q[t + 1];
-        if (q1 <= q0) { err = "empty task"; return BOS_ERR_INVALID; }
-        const int64_t v0 = P.pos_row0[q0];
-        for (int q = q0; q < q1; ++q) {
-            const int u = P.pos_node[q];
-            const int su = node_size(u, NP);
-            for (int r = 0; r < su; ++r) {
-                ++bcount[P.node_dof[u] + r];
-                for (int c = 0; c <= r; ++c) {
-                    const int64_t pd = pos_diag(P.node_row0[u], P.node_base[u], r, c);
-                    if (!check_entry(u, r, pd, P.node_dof[u] + c)) { err = "diagonal block misplaced"; return BOS_ERR_INVALID; }
-                    ++hit[pd];
+    auto mark = [&](int64_t v0, int cnt) -> bool {
+        if (v0 < 0 || v0 + cnt > B.size) return false;
+        for (int i = 0; i < cnt; ++i) ++hit[v0 + i];
+        return true;
+    };
+    for (int p = P.p_begin; p < P.p_end; ++p) {
+        if (!mark(6 * (int64_t)p, 6)) { err = "pose diagonal out of range"; return BOS_ERR_INVALID; }
+        for (int d = 0; d < 3; ++d) ++bhit[3 * (size_t)p + d];
+        for (int j = 0; j < L; ++j) {
+            const size_t sg = (size_t)p * L + j;
+            int blk = B.seg_blk[sg];
+            const int i0 = B.seg_ptr[sg], i1 = B.seg_ptr[sg + 1];
+            if (i0 < B.pb_ptr[p] || i1 > B.pb_ptr[p + 1] || i0 > i1) { err = "lane segment outside its pose"; return BOS_ERR_INVALID; }
+            for (int i = i0; i < i1; ++i) {
+                const int k = B.pb_obs[i];
+                ++chi[k];
+                if (i + 1 == i1 || pi.b_lm[B.pb_obs[i + 1]] != pi.b_lm[k]) {
+                    if (blk < B.ub_ptr[p] || blk >= B.ub_ptr[p + 1] || B.ub_lm[blk] != pi.b_lm[k] ||
+                        !mark(B.off_pl + 6 * (int64_t)blk, 6)) {
+                        err = "pose-landmark block misplaced";
+                        return BOS_ERR_INVALID;
+                    }
+                    ++blk;
                 }
             }
         }
-        auto check_off = [&](int a, int b, int meta) -> bool {
-            if (!(meta & 8)) return true;
-            const int own = (meta & 16) ? b : a, oth = (meta & 16) ? a : b;
-            const int qo = P.node_pos[own];
-            if (qo < q0 || qo >= q1) return false;
-            const int64_t slot = v0 + (meta >> 8);
-            for (int r = 0; r < node_size(own, NP); ++r)
-                for (int c = 0; c < node_size(oth, NP); ++c) {
-                    const int64_t p = pos_off(slot, P.node_base[own], r, c);
-                    if (!check_entry(own, r, p, P.node_dof[oth] + c)) return false;
-                    ++hit[p];
+        for (int x = B.po_ptr[p]; x < B.po_ptr[p + 1]; ++x) {
+            const int32_t e = B.po_ent[x];
+            const int k = e >> 1;
+            if ((e & 1) ? pi.o_dst[k] != p : pi.o_src[k] != p) { err = "odometry entry of the wrong pose"; return BOS_ERR_INVALID; }
+            if (e & 1) continue;
+            ++chi[pi.Mb + k];
+            const int u = B.po_blk[x];
+            if (x + 1 == B.po_ptr[p + 1] || B.po_blk[x + 1] != u) {
+                if (u < B.uo_ptr[p] || u >= B.uo_ptr[p + 1] || B.uo_dst[u] != pi.o_dst[k] ||
+                    !mark(B.off_pp + 6 * (int64_t)u, 6)) {
+                    err = "pose-pose block misplaced";
+                    return BOS_ERR_INVALID;
                 }
-            return true;
-        };
-        for (int i = T.task_be[t]; i < T.task_be[t + 1]; ++i) {
-            if (!check_off(T.be_pose[i], NP + T.be_lm[i], T.be_meta[i])) { err = "bearing block misplaced"; return BOS_ERR_INVALID; }
-            if (T.be_meta[i] & 4) ++chi[T.be_obs[i]];
-        }
-        for (int j = T.task_oe[t]; j < T.task_oe[t + 1]; ++j) {
-            const int k = T.oe_edge[j];
-            if (!check_off(pi.o_src[k], pi.o_dst[k], T.oe_meta[j])) { err = "odometry block misplaced"; return BOS_ERR_INVALID; }
-            if (T.oe_meta[j] & 4) ++chi[pi.Mb + k];
-        }
-        if (!(T.task_flags[t] & 2) && T.task_be[t + 1] - T.task_be[t] + T.task_oe[t + 1] - T.task_oe[t] > 64) {
-            err = "multi-node task exceeds one wavefront";
-            return BOS_ERR_INVALID;
+            }
         }
     }
-    for (int64_t e = 0; e < nnz; ++e) {
-        const bool owned = e >= P.val_begin && e < P.val_end;
-        if (hit[e] != (owned ? 1 : 0)) {
-            err = "CSR entry " + std::to_string(e) + " written " + std::to_string((int)hit[e]) + " times";
+    for (int l = P.l_begin; l < P.l_end; ++l) {
+        if (!mark(B.off_ldiag + 3 * (int64_t)l, 3)) { err = "landmark diagonal out of range"; return BOS_ERR_INVALID; }
+        for (int d = 0; d < 2; ++d) ++bhit[3 * (size_t)NP + 2 * (size_t)l + d];
+    }
+    // written exactly once inside this rank's ranges, never outside
+    std::vector<uint8_t> own(B.size, 0), bown(bhit.size(), 0);
+    for (int q = 0; q < 4; ++q) {
+        const Range& g = P.rank_val_ranges[4 * (size_t)P.rank + q];
+        for (int64_t v = g.begin; v < g.end; ++v) own[v] = 1;
+    }
+    for (int q = 0; q < 2; ++q) {
+        const Range& g = P.rank_b_ranges[2 * (size_t)P.rank + q];
+        for (int64_t v = g.begin; v < g.end; ++v) bown[v] = 1;
+    }
+    for (int64_t v = 0; v < B.size; ++v)
+        if (hit[v] != own[v]) {
+            err = "block value " + std::to_string(v) + " written " + std::to_string((int)hit[v]) + " times";
             return BOS_ERR_INVALID;
         }
-    }
-    for (int64_t i = 0; i < P.n; ++i)
-        if (bcount[i] != ((i >= P.row_begin && i < P.row_end) ? 1 : 0)) { err = "b entry coverage"; return BOS_ERR_INVALID; }
-    if (P.rank_row_begin.size() == 2)   // single shard: every observation's chi^2 counted once
+    for (size_t v = 0; v < bhit.size(); ++v)
+        if (bhit[v] != bown[v]) { err = "b entry coverage"; return BOS_ERR_INVALID; }
+    if (P.world == 1)   // single shard: every observation's chi^2 counted once
         for (size_t k = 0; k < chi.size(); ++k)
             if (chi[k] != 1) { err = "chi^2 of observation " + std::to_string(k) + " counted " + std::to_string(chi[k]) + " times"; return BOS_ERR_INVALID; }
+    // every stored entry reads a block value; pose-pose blocks are symmetric (off-diagonal values
+    // read twice), every other value at most once
+    std::vector<uint8_t> refs(B.size, 0);
+    for (int32_t v : B.csr_src) {
+        if (v < 0 || v >= B.size) { err = "stored entry reads outside the block array"; return BOS_ERR_INVALID; }
+        if (++refs[v] > (v >= B.off_pp ? 2 : 1)) { err = "block value read by two stored entries"; return BOS_ERR_INVALID; }
+    }
     return BOS_OK;
 }
 

@@ -2,10 +2,10 @@
 //
 // The reference rebuilds H from scratch every iteration with Eigen sparse additions
 // (slam/solver.cpp:28-69) and runs SimplicialLDLT::analyzePattern once (:77-80). Here the
-// pattern is fixed up front: H_nf (the fixed pose's rows/cols removed, solver.cpp:71-73) is laid
-// out as the lower triangle of P^T H_nf P in CSR, where P is a fill-reducing node ordering, so
-// the J+H kernels scatter straight into the array the sparse Cholesky consumes (no per-step
-// permutation pass), and every observation knows its destination slots in advance.
+// structure is fixed up front: the J+H kernel writes H block-sparse in observation order
+// (BlockLayout), every value exactly once; the solver sees H_nf (the fixed pose's rows/cols
+// removed, solver.cpp:71-73) as the lower triangle of P^T H_nf P, P a fill-reducing node ordering,
+// through index maps into the block array (no per-step assembly or permutation pass).
 //
 // Nodes: pose stix u in [0, NP) (3 dofs), landmark stix l as node NP + l (2 dofs).
 #pragma once
@@ -26,31 +26,46 @@ struct ProblemIndex {
     const double* o_omega = nullptr;   // [Mo * 9]
 };
 
-// Work of the J+H kernel (hip/kernels.hip). A task is one wavefront and owns a contiguous
-// range of elimination positions [task_q[t], task_q[t + 1]): its CSR rows are the contiguous
-// value range [pos_row0[q0], pos_row0[q1]) and its b entries [pos_dof[q0], pos_dof[q1]), which
-// the wavefront assembles in LDS and stores with coalesced writes. Entries are the observations
-// incident to the task's nodes (an observation whose two endpoints lie in different tasks
-// appears in both). meta bits: 0 = first endpoint (pose / src) inside, 1 = second endpoint
-// (landmark / dst) inside, 2 = count this observation in chi^2, 3 = write the off-diagonal
-// block, 4 = the owner (row side) of that block is the second endpoint; bits 8.. = offset of
-// the block's first entry relative to the task's first value.
-struct RangeTasks {
-    std::vector<int32_t> task_q;        // [ntask + 1] position ranges
-    std::vector<int32_t> task_be;       // [ntask + 1] bearing-entry ranges
-    std::vector<int32_t> task_oe;       // [ntask + 1] odometry-entry ranges
-    std::vector<uint8_t> task_flags;    // bit 0: rows staged in LDS; bit 1: single node (chunked)
-    std::vector<int32_t> be_pose, be_lm, be_meta, be_obs;
-    std::vector<double> be_woff;        // off-block weight (sum over duplicate group; 0 = no write)
-    std::vector<int32_t> oe_edge, oe_meta;
-    std::vector<double> oe_omoff;       // [6 per entry] off-block information (duplicate groups)
-    std::vector<int32_t> cl_ptr;        // [m + 1] per position: range into cl
-    std::vector<uint16_t> cl;           // contribution slots (2 * entry + side, entry local to the task)
-    bool has_dups = false;
-    int max_entries = 0;
-    int ntask() const { return task_q.empty() ? 0 : (int)task_q.size() - 1; }
-    int nentries() const { return (int)be_pose.size() + (int)oe_edge.size(); }
+// Block-sparse storage of H that the J+H kernel (hip/kernels.hip) writes, in observation order
+// rather than in the solver's order (the solver reads it through index maps: Multifrontal::amap_src
+// and csr_src). One array of T:
+//   [0, off_ldiag)        pose diagonal blocks, 6 per pose, lower triangle (00, 10, 11, 20, 21, 22)
+//   [off_ldiag, off_pl)   landmark diagonal blocks, 3 per landmark (00, 10, 11)
+//   [off_pl, off_pp)      pose-landmark blocks H_pl (3 x 2 row-major), one per unique (pose,
+//                         landmark) pair, ordered by pose then landmark
+//   [off_pp, size)        pose-pose blocks H_sd, one per unique odometry (src, dst) pair, ordered by
+//                         src then dst; H_sd = -J_s^T Omega J_s is symmetric (J_d = -J_s), so 6
+//                         values like a diagonal block
+// b stays in the reference dof numbering (3 per pose, then 2 per landmark; the fixed pose's entries
+// are computed but not used). Diagonal blocks and b include all nodes, the fixed pose too.
+//
+// Work: lane groups of lpp lanes per pose, each lane a segment of the pose's bearings (sorted by
+// landmark, so duplicate observations of one pair are adjacent and merged by one lane); lane 0 of
+// the group also takes the pose's odometry entries. One lane per landmark for its diagonal block.
+struct BlockLayout {
+    int64_t off_ldiag = 0, off_pl = 0, off_pp = 0, size = 0;
+    int lpp = 1;                        // lanes per pose: 1, 2 or 4
+    bool has_dups = false;              // some (pose, landmark) or (src, dst) pair repeats
+    std::vector<int32_t> pb_obs;        // [Mb] bearings sorted by (pose, landmark, index)
+    std::vector<int32_t> pb_ptr;        // [NP + 1] bearings of each pose (into pb_obs)
+    std::vector<int32_t> seg_ptr;       // [NP * lpp + 1] lane segments (into pb_obs)
+    std::vector<int32_t> seg_blk;       // [NP * lpp] first pose-landmark block of each segment
+    std::vector<int32_t> ub_ptr;        // [NP + 1] pose-landmark blocks of each pose
+    std::vector<int32_t> ub_lm;         // [nub] landmark of each pose-landmark block
+    std::vector<int32_t> po_ptr;        // [NP + 1] odometry entries of each pose
+    std::vector<int32_t> po_ent;        // edge << 1 | 1 when the pose is the destination
+    std::vector<int32_t> po_blk;        // pose-pose block of a source-side entry, -1 on the destination side
+    std::vector<int32_t> uo_ptr;        // [NP + 1] pose-pose blocks of each pose (as source)
+    std::vector<int32_t> uo_dst;        // [nuo] destination pose of each pose-pose block
+    std::vector<int32_t> lb_ptr;        // [NL + 1] bearings of each landmark (into lb_obs)
+    std::vector<int32_t> lb_obs;        // [Mb] bearings sorted by (landmark, pose, index)
+    std::vector<int32_t> csr_src;       // [nnzA] block value of each stored entry of P^T H_nf P
+    int nub() const { return ub_ptr.empty() ? 0 : ub_ptr.back(); }
+    int nuo() const { return uo_ptr.empty() ? 0 : uo_ptr.back(); }
 };
+
+// A contiguous piece of the block array / b that one rank writes (and broadcasts).
+struct Range { int64_t begin = 0, end = 0; };
 
 struct OrderingReport {
     std::string chosen;                // "temporal" or "nested-dissection"
@@ -75,7 +90,7 @@ struct Multifrontal {
     std::vector<int64_t> rmap_off;          // per supernode: r positions of its rows in the parent's front
     std::vector<int32_t> rmap;
     std::vector<int32_t> amap_ptr;          // per supernode: range into amap_src / amap_dst
-    std::vector<int32_t> amap_src, amap_dst;// value index in the CSR of H -> column-major front position
+    std::vector<int32_t> amap_src, amap_dst;// block-array value (BlockLayout) -> column-major front position
     std::vector<int32_t> level_ptr, level;  // supernodes grouped by tree level (leaves first)
     int64_t L_size = 0, U_size = 0, u_size = 0;
     double flops = 0;
@@ -86,18 +101,20 @@ struct Plan {
     int64_t n = 0;                         // system size N - 3
     std::vector<int32_t> node_pos;         // elimination position; -1 for the fixed pose
     std::vector<int32_t> node_dof;         // first dof in the permuted system; fixed pose -> n
-    std::vector<int32_t> node_row0;        // CSR position of the node's first row start; -1 fixed
-    std::vector<int32_t> node_base;        // entries before the diagonal block in each of its rows
     std::vector<int32_t> rowptr, colind;   // lower triangle of P^T H_nf P, n rows
     std::vector<int32_t> Lptr, Lind;       // symbolic Cholesky factor (lower, with diagonal)
     Multifrontal mf;                       // built when factor_mode == kFactorMultifrontal
-    RangeTasks tasks;
-    std::vector<int32_t> pos_node, pos_row0, pos_base, pos_dof;   // per elimination position
+    BlockLayout blk;
     OrderingReport ordering;
-    // ownership for observation sharding: this rank writes rows [row_begin, row_end)
-    int32_t row_begin = 0, row_end = 0;
-    int64_t val_begin = 0, val_end = 0;
-    std::vector<int32_t> rank_row_begin;   // [world + 1] row split of every rank
+    // observation sharding: rank r owns poses [rank_pose[r], rank_pose[r + 1]) and landmarks
+    // [rank_lm[r], rank_lm[r + 1]), i.e. their diagonal blocks, b entries and the off-diagonal
+    // blocks of the observations its poses own
+    int rank = 0, world = 1;
+    std::vector<int32_t> rank_pose, rank_lm;     // [world + 1]
+    int32_t p_begin = 0, p_end = 0, l_begin = 0, l_end = 0;
+    // per rank: 4 block-array ranges (pose diag, landmark diag, pose-landmark, pose-pose) and 2 b
+    // ranges (poses, landmarks)
+    std::vector<Range> rank_val_ranges, rank_b_ranges;   // [world * 4], [world * 2]
     int64_t nnzA() const { return rowptr.empty() ? 0 : rowptr.back(); }
     int64_t nnzL() const { return Lptr.empty() ? 0 : Lptr.back(); }
 };
