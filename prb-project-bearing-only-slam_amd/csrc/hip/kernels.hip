@@ -6,7 +6,8 @@
 //   * pose lanes (lpp per pose): each lane walks a segment of its pose's bearings (sorted by
 //     landmark) — error, Jacobian, robust kernel (scales e only, solver.cpp:37-41) — accumulating
 //     the pose's diagonal block and b in registers and storing each pose-landmark block H_pl as it
-//     goes; lane 0 of the group also walks the pose's odometry edges (both sides accumulate
+//     goes (lists are wave-interleaved, so every step of a wave reads 64 consecutive records and
+//     writes 64 consecutive blocks); lane 0 of the group also walks the pose's odometry edges (both sides accumulate
 //     H_ss = H_dd, the source side stores H_sd = -H_ss and counts chi^2). The group's partial sums
 //     are combined with a fixed butterfly (deterministic) and stored with the damping (:64-69).
 //   * landmark lanes: one per landmark, walking its bearings for H_ll and b_l (+ damping).
@@ -83,26 +84,24 @@ __device__ __forceinline__ T odometry_hb(const LinParams<T>& P, int k, const V4<
 
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP>
 __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, double& chi, int& nrob) {
-    const int gid = blockIdx.x * kBlock + threadIdx.x;
-    const int p = P.p_begin + gid / LPP, sub = gid % LPP;
+    const int g = P.p_begin * LPP + blockIdx.x * kBlock + threadIdx.x;   // lane; shards start at a wave
+    const int p = g / LPP, sub = g % LPP, t = g & 63;
     const bool active = p < P.p_end;
-    T h[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    T h[6] = {0, 0, 0, 0, 0, 0}, gb[3] = {0, 0, 0};
     if (active) {
         const V4<T> X = load4(P.pc + 4 * p);
-        const int sg = p * LPP + sub;
-        int i = P.seg_ptr[sg];
-        const int i1 = P.seg_ptr[sg + 1];
-        T* blk = P.hval + P.off_pl + 6 * P.seg_blk[sg];
+        const int n = P.pl_cnt[g];
+        int sl = P.pw_base[g >> 6] + t;   // slot of item j: + 64 j
         T acc[6] = {0, 0, 0, 0, 0, 0};
         BRec<T> nxt;
-        if (i < i1) nxt = P.pb[i];
-        for (; i < i1; ++i) {
+        if (n > 0) nxt = P.pb[sl];
+        for (int j = 0; j < n; ++j, sl += 64) {
             const BRec<T> cur = nxt;
-            if (i + 1 < i1) nxt = P.pb[i + 1];
+            if (j + 1 < n) nxt = P.pb[sl + 64];
             const V2<T> Lm = load2(P.lc + 2 * cur.idx);
             T J[5];
             T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, cur.z, J);   // :9-95
-            const T w = HAS_W ? P.pb_w[i] : (T)1;
+            const T w = HAS_W ? P.pb_w[sl] : (T)1;
             const T rho = e * w * e;                                                       // solver.cpp:37
             chi += (double)rho;
             if (rho > P.kt) {                                                              // :38-40
@@ -113,19 +112,18 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, double& chi, i
             const T w0 = J[0] * w, w1 = J[1] * w, w2 = J[2] * w;
             h[0] += w0 * J[0]; h[1] += w1 * J[0]; h[2] += w1 * J[1];
             h[3] += w2 * J[0]; h[4] += w2 * J[1]; h[5] += w2 * J[2];
-            g[0] += w0 * e; g[1] += w1 * e; g[2] += w2 * e;
+            gb[0] += w0 * e; gb[1] += w1 * e; gb[2] += w2 * e;
             const T o0 = w0 * J[3], o1 = w0 * J[4], o2 = w1 * J[3], o3 = w1 * J[4], o4 = w2 * J[3], o5 = w2 * J[4];
-            if (HAS_DUPS) {   // observations of one pair are adjacent: sum, store once
+            T* blk = P.hval + P.off_pl + 6 * sl;
+            if (HAS_DUPS) {   // observations of one pair are adjacent: sum, store at the last one
                 acc[0] += o0; acc[1] += o1; acc[2] += o2; acc[3] += o3; acc[4] += o4; acc[5] += o5;
-                if (i + 1 == i1 || nxt.idx != cur.idx) {
+                if (j + 1 == n || nxt.idx != cur.idx) {
                     store6(blk, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5]);
-                    blk += 6;
 #pragma unroll
                     for (int q = 0; q < 6; ++q) acc[q] = (T)0;
                 }
             } else {
                 store6(blk, o0, o1, o2, o3, o4, o5);
-                blk += 6;
             }
         }
         if (sub == 0) {
@@ -144,10 +142,10 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, double& chi, i
 #pragma unroll
                 for (int v = 0; v < 6; ++v) h[v] += he[v];
                 if (dst_side) {
-                    g[0] -= ge[0]; g[1] -= ge[1]; g[2] -= ge[2];
+                    gb[0] -= ge[0]; gb[1] -= ge[1]; gb[2] -= ge[2];
                     continue;
                 }
-                g[0] += ge[0]; g[1] += ge[1]; g[2] += ge[2];
+                gb[0] += ge[0]; gb[1] += ge[1]; gb[2] += ge[2];
                 chi += (double)rho;
                 if (rho > P.kt) ++nrob;
                 const int ub = P.po_blk[x];
@@ -172,33 +170,33 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, double& chi, i
 #pragma unroll
         for (int v = 0; v < 6; ++v) h[v] += __shfl_xor(h[v], o);
 #pragma unroll
-        for (int v = 0; v < 3; ++v) g[v] += __shfl_xor(g[v], o);
+        for (int v = 0; v < 3; ++v) gb[v] += __shfl_xor(gb[v], o);
     }
     if (active && sub == 0) {
         const T lam = P.lambda;
         store6(P.hval + 6 * p, h[0] + lam, h[1], h[2] + lam, h[3], h[4], h[5] + lam);
         T* bp = P.b + 3 * p;
-        bp[0] = g[0]; bp[1] = g[1]; bp[2] = g[2];
+        bp[0] = gb[0]; bp[1] = gb[1]; bp[2] = gb[2];
     }
 }
 
 template <typename T, bool HAS_W>
 __device__ __forceinline__ void landmark_lane(const LinParams<T>& P) {
-    const int l = P.l_begin + (blockIdx.x - P.pose_blocks) * kBlock + threadIdx.x;
+    const int l = P.l_begin + (blockIdx.x - P.pose_blocks) * kBlock + threadIdx.x;   // shards start at a wave
     if (l >= P.l_end) return;
     const V2<T> Lm = load2(P.lc + 2 * l);
     T h00 = 0, h10 = 0, h11 = 0, g0 = 0, g1 = 0;
-    int x = P.lb_ptr[l];
-    const int x1 = P.lb_ptr[l + 1];
+    const int n = P.ll_cnt[l];
+    int sl = P.lw_base[l >> 6] + (l & 63);
     BRec<T> nxt;
-    if (x < x1) nxt = P.lb[x];
-    for (; x < x1; ++x) {
+    if (n > 0) nxt = P.lb[sl];
+    for (int j = 0; j < n; ++j, sl += 64) {
         const BRec<T> cur = nxt;
-        if (x + 1 < x1) nxt = P.lb[x + 1];
+        if (j + 1 < n) nxt = P.lb[sl + 64];
         const V4<T> X = load4(P.pc + 4 * cur.idx);
         T J[5];
         T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, cur.z, J);
-        const T w = HAS_W ? P.lb_w[x] : (T)1;
+        const T w = HAS_W ? P.lb_w[sl] : (T)1;
         const T rho = e * w * e;
         if (rho > P.kt) e *= sqrt(P.kt / rho);
         const T w3 = J[3] * w, w4 = J[4] * w;

@@ -16,7 +16,8 @@ template <> struct alignas(8) BRec<float> { int32_t idx; float z; };
 template <> struct alignas(16) BRec<double> { int32_t idx; int32_t pad; double z; };
 
 // J+H build (host/plan.hpp BlockLayout). Blocks [0, pose_blocks) run lane groups of lpp lanes
-// per owned pose, the rest one lane per owned landmark.
+// per owned pose, the rest one lane per owned landmark. Lane lists are wave-interleaved: item j of
+// lane t of wave w is slot w_base[w] + 64 j + t.
 template <typename T> struct LinParams {
     // state caches (T precision), refreshed by the box-plus kernel
     const T* pc;          // [NP][4] x, y, cos(theta), sin(theta)
@@ -25,10 +26,10 @@ template <typename T> struct LinParams {
     int NP;
     int p_begin, p_end, l_begin, l_end, pose_blocks;
     // pose lanes
-    const int32_t* seg_ptr;   // [NP * lpp + 1] bearing segment of each lane
-    const int32_t* seg_blk;   // [NP * lpp] first pose-landmark block of each lane
-    const BRec<T>* pb;        // [Mb] (landmark, z), bearings sorted by (pose, landmark)
-    const T* pb_w;            // [Mb] information, null => 1
+    const int32_t* pw_base;   // [waves + 1]
+    const int32_t* pl_cnt;    // [NP * lpp]
+    const BRec<T>* pb;        // [slots] (landmark, z); the pose-landmark block of a slot is at off_pl + 6 slot
+    const T* pb_w;            // [slots] information, null => 1
     const int32_t* po_ptr;    // [NP + 1]
     const int32_t* po_ent;    // edge << 1 | destination side
     const int32_t* po_blk;    // pose-pose block of a source-side entry
@@ -37,8 +38,9 @@ template <typename T> struct LinParams {
     const T* o_z;             // [M_o][3]
     const T* o_om;            // [M_o][6] upper triangle (00, 01, 02, 11, 12, 22)
     // landmark lanes
-    const int32_t* lb_ptr;    // [NL + 1]
-    const BRec<T>* lb;        // [Mb] (pose, z), bearings sorted by (landmark, pose)
+    const int32_t* lw_base;   // [waves + 1]
+    const int32_t* ll_cnt;    // [NL]
+    const BRec<T>* lb;        // [slots] (pose, z)
     const T* lb_w;
     // outputs
     T* hval;                  // block array (BlockLayout)

@@ -80,8 +80,8 @@ struct bos_solver {
     void* d_pth = nullptr;
     void* d_lc = nullptr;
     // J+H work lists (host/plan.hpp BlockLayout)
-    int32_t *seg_ptr = nullptr, *seg_blk = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_blk = nullptr,
-            *lb_ptr = nullptr, *csr_src = nullptr, *elim_ref = nullptr;
+    int32_t *pw_base = nullptr, *pl_cnt = nullptr, *lw_base = nullptr, *ll_cnt = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_blk = nullptr, *csr_src = nullptr,
+            *elim_ref = nullptr;
     void *pb = nullptr, *pb_w = nullptr, *lb = nullptr, *lb_w = nullptr;
     int pose_blocks = 0;
     // odometry
@@ -126,11 +126,12 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.NP = s->NP;
     p.p_begin = P.p_begin; p.p_end = P.p_end; p.l_begin = P.l_begin; p.l_end = P.l_end;
     p.pose_blocks = s->pose_blocks;
-    p.seg_ptr = s->seg_ptr; p.seg_blk = s->seg_blk;
+    p.pw_base = s->pw_base; p.pl_cnt = s->pl_cnt;
     p.pb = (const bos::dev::BRec<T>*)s->pb; p.pb_w = (const T*)s->pb_w;
     p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_blk = s->po_blk;
     p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
-    p.lb_ptr = s->lb_ptr; p.lb = (const bos::dev::BRec<T>*)s->lb; p.lb_w = (const T*)s->lb_w;
+    p.lw_base = s->lw_base; p.ll_cnt = s->ll_cnt;
+    p.lb = (const bos::dev::BRec<T>*)s->lb; p.lb_w = (const T*)s->lb_w;
     p.hval = (T*)s->d_val;
     p.b = (T*)s->d_b;
     p.off_ldiag = (int)P.blk.off_ldiag; p.off_pl = (int)P.blk.off_pl; p.off_pp = (int)P.blk.off_pp;
@@ -354,8 +355,8 @@ int bos_destroy(bos_solver* s) {
     if (!s) return BOS_OK;
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->seg_ptr, s->seg_blk, s->po_ptr, s->po_ent,
-                    s->po_blk, s->lb_ptr, s->csr_src, s->elim_ref, s->pb, s->pb_w, s->lb, s->lb_w,
+    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pl_cnt, s->lw_base, s->ll_cnt,
+                    s->po_ptr, s->po_ent, s->po_blk, s->csr_src, s->elim_ref, s->pb, s->pb_w, s->lb, s->lb_w,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_chi, s->d_nrob,
@@ -476,13 +477,15 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
 
     {
         const bos::BlockLayout& B = P.blk;
-        const int Mb = s->Mb;
-        std::vector<double> pbz(Mb), lbz(Mb), pbw, lbw;
-        std::vector<int32_t> pbi(Mb), lbi(Mb);
-        for (int i = 0; i < Mb; ++i) {
-            pbi[i] = pb->bearing_landmark[B.pb_obs[i]]; pbz[i] = pb->bearing_z[B.pb_obs[i]];
-            lbi[i] = pb->bearing_pose[B.lb_obs[i]]; lbz[i] = pb->bearing_z[B.lb_obs[i]];
-        }
+        // slot records (padding slots: index 0, z 0, never read)
+        const std::vector<int32_t>& po = B.pose_lanes.obs;
+        const std::vector<int32_t>& lo = B.lm_lanes.obs;
+        std::vector<double> pbz(po.size(), 0.0), lbz(lo.size(), 0.0), pbw, lbw;
+        std::vector<int32_t> pbi(po.size(), 0), lbi(lo.size(), 0);
+        for (size_t i = 0; i < po.size(); ++i)
+            if (po[i] >= 0) { pbi[i] = pb->bearing_landmark[po[i]]; pbz[i] = pb->bearing_z[po[i]]; }
+        for (size_t i = 0; i < lo.size(); ++i)
+            if (lo[i] >= 0) { lbi[i] = pb->bearing_pose[lo[i]]; lbz[i] = pb->bearing_z[lo[i]]; }
         auto upload_recs = [&](void** dst, const std::vector<int32_t>& idx, const std::vector<double>& z) -> int {
             if (f32) {
                 std::vector<bos::dev::BRec<float>> r(idx.size());
@@ -499,14 +502,16 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             *dst = d;
             return e;
         };
-        if ((rc = upload(&s->seg_ptr, B.seg_ptr)) || (rc = upload(&s->seg_blk, B.seg_blk)) ||
+        if ((rc = upload(&s->pw_base, B.pose_lanes.w_base)) || (rc = upload(&s->pl_cnt, B.pose_lanes.cnt)) ||
+            (rc = upload(&s->lw_base, B.lm_lanes.w_base)) || (rc = upload(&s->ll_cnt, B.lm_lanes.cnt)) ||
             (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, B.po_ent)) ||
-            (rc = upload(&s->po_blk, B.po_blk)) || (rc = upload(&s->lb_ptr, B.lb_ptr)) ||
-            (rc = upload_recs(&s->pb, pbi, pbz)) || (rc = upload_recs(&s->lb, lbi, lbz)))
+            (rc = upload(&s->po_blk, B.po_blk)) || (rc = upload_recs(&s->pb, pbi, pbz)) ||
+            (rc = upload_recs(&s->lb, lbi, lbz)))
             return bail(rc);
         if (s->has_w) {
-            pbw.resize(Mb); lbw.resize(Mb);
-            for (int i = 0; i < Mb; ++i) { pbw[i] = pb->bearing_omega[B.pb_obs[i]]; lbw[i] = pb->bearing_omega[B.lb_obs[i]]; }
+            pbw.assign(po.size(), 0.0); lbw.assign(lo.size(), 0.0);
+            for (size_t i = 0; i < po.size(); ++i) if (po[i] >= 0) pbw[i] = pb->bearing_omega[po[i]];
+            for (size_t i = 0; i < lo.size(); ++i) if (lo[i] >= 0) lbw[i] = pb->bearing_omega[lo[i]];
             if ((rc = upload_Tv(&s->pb_w, pbw)) || (rc = upload_Tv(&s->lb_w, lbw))) return bail(rc);
         }
         s->pose_blocks = (int)(((int64_t)(P.p_end - P.p_begin) * B.lpp + bos::dev::kBlock - 1) / bos::dev::kBlock);

@@ -431,39 +431,44 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     return validate_plan(pi, P, err);
 }
 
+// Wave-interleaved lane lists (LaneLists in plan.hpp) from per-lane item ranges.
+void make_lane_lists(int lanes, const std::vector<int32_t>& lane_ptr, const std::vector<int32_t>& items, LaneLists& L) {
+    const int waves = (lanes + 63) / 64;
+    L.w_base.assign(waves + 1, 0);
+    L.w_len.assign(waves, 0);
+    L.cnt.assign(lanes, 0);
+    for (int g = 0; g < lanes; ++g) {
+        L.cnt[g] = lane_ptr[g + 1] - lane_ptr[g];
+        L.w_len[g / 64] = std::max(L.w_len[g / 64], L.cnt[g]);
+    }
+    for (int w = 0; w < waves; ++w) L.w_base[w + 1] = L.w_base[w] + 64 * L.w_len[w];
+    L.obs.assign(L.slots(), -1);
+    for (int g = 0; g < lanes; ++g)
+        for (int j = 0; j < L.cnt[g]; ++j) L.obs[L.w_base[g / 64] + 64 * j + (g & 63)] = items[lane_ptr[g] + j];
+}
+
+inline int32_t lane_slot(const LaneLists& L, int g, int j) { return L.w_base[g / 64] + 64 * j + (g & 63); }
+
 // Block layout of H and the J+H work split (see BlockLayout in plan.hpp).
 int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     const int NP = pi.NP, NL = pi.NL, Mb = pi.Mb, Mo = pi.Mo;
     BlockLayout& B = P.blk;
     B = BlockLayout();
     // bearings by (pose, landmark, index) and by (landmark, pose, index)
-    B.pb_ptr.assign(NP + 1, 0);
-    B.lb_ptr.assign(NL + 1, 0);
-    for (int k = 0; k < Mb; ++k) { ++B.pb_ptr[pi.b_pose[k] + 1]; ++B.lb_ptr[pi.b_lm[k] + 1]; }
-    for (int p = 0; p < NP; ++p) B.pb_ptr[p + 1] += B.pb_ptr[p];
-    for (int l = 0; l < NL; ++l) B.lb_ptr[l + 1] += B.lb_ptr[l];
-    B.pb_obs.resize(Mb);
-    B.lb_obs.resize(Mb);
+    std::vector<int32_t> pb_ptr(NP + 1, 0), lb_ptr(NL + 1, 0), pb_obs(Mb), lb_obs(Mb);
+    for (int k = 0; k < Mb; ++k) { ++pb_ptr[pi.b_pose[k] + 1]; ++lb_ptr[pi.b_lm[k] + 1]; }
+    for (int p = 0; p < NP; ++p) pb_ptr[p + 1] += pb_ptr[p];
+    for (int l = 0; l < NL; ++l) lb_ptr[l + 1] += lb_ptr[l];
     {
-        std::vector<int32_t> wp(B.pb_ptr.begin(), B.pb_ptr.end() - 1), wl(B.lb_ptr.begin(), B.lb_ptr.end() - 1);
-        for (int k = 0; k < Mb; ++k) { B.pb_obs[wp[pi.b_pose[k]]++] = k; B.lb_obs[wl[pi.b_lm[k]]++] = k; }
+        std::vector<int32_t> wp(pb_ptr.begin(), pb_ptr.end() - 1), wl(lb_ptr.begin(), lb_ptr.end() - 1);
+        for (int k = 0; k < Mb; ++k) { pb_obs[wp[pi.b_pose[k]]++] = k; lb_obs[wl[pi.b_lm[k]]++] = k; }
     }
     for (int p = 0; p < NP; ++p)
-        std::stable_sort(B.pb_obs.begin() + B.pb_ptr[p], B.pb_obs.begin() + B.pb_ptr[p + 1],
+        std::stable_sort(pb_obs.begin() + pb_ptr[p], pb_obs.begin() + pb_ptr[p + 1],
                          [&](int a, int b) { return pi.b_lm[a] < pi.b_lm[b]; });
     for (int l = 0; l < NL; ++l)
-        std::stable_sort(B.lb_obs.begin() + B.lb_ptr[l], B.lb_obs.begin() + B.lb_ptr[l + 1],
+        std::stable_sort(lb_obs.begin() + lb_ptr[l], lb_obs.begin() + lb_ptr[l + 1],
                          [&](int a, int b) { return pi.b_pose[a] < pi.b_pose[b]; });
-    // unique pose-landmark pairs = pose-landmark blocks
-    B.ub_ptr.assign(NP + 1, 0);
-    for (int p = 0; p < NP; ++p) {
-        for (int i = B.pb_ptr[p]; i < B.pb_ptr[p + 1]; ++i) {
-            const int l = pi.b_lm[B.pb_obs[i]];
-            if (i > B.pb_ptr[p] && l == pi.b_lm[B.pb_obs[i - 1]]) { B.has_dups = true; continue; }
-            B.ub_lm.push_back(l);
-        }
-        B.ub_ptr[p + 1] = (int32_t)B.ub_lm.size();
-    }
     // odometry entries of each pose: source side sorted by (dst, edge), then destination side by (src, edge)
     B.po_ptr.assign(NP + 1, 0);
     for (int k = 0; k < Mo; ++k) { ++B.po_ptr[pi.o_src[k] + 1]; ++B.po_ptr[pi.o_dst[k] + 1]; }
@@ -509,70 +514,93 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     const double avg = NP ? (double)Mb / NP : 0.0;
     B.lpp = avg >= 24 ? 4 : avg >= 8 ? 2 : 1;
     const int L = B.lpp;
-    B.seg_ptr.assign((size_t)NP * L + 1, 0);
-    B.seg_blk.assign((size_t)NP * L, 0);
+    auto same_lm = [&](int i, int j) { return pi.b_lm[pb_obs[i]] == pi.b_lm[pb_obs[j]]; };
+    std::vector<int32_t> lane_ptr((size_t)NP * L + 1, 0);
     for (int p = 0; p < NP; ++p) {
-        const int b0 = B.pb_ptr[p], b1 = B.pb_ptr[p + 1], nb = b1 - b0;
+        const int b0 = pb_ptr[p], b1 = pb_ptr[p + 1], nb = b1 - b0;
         const int no = B.po_ptr[p + 1] - B.po_ptr[p];
         const int share = (nb + no + L - 1) / L;
         const int q0 = std::min(nb, std::max(0, share - no));
-        std::vector<int> cut(L + 1);
-        cut[0] = b0;
-        cut[L] = b1;
-        for (int j = 1; j < L; ++j) {
-            int c = b0 + q0 + (int)((int64_t)(nb - q0) * (j - 1) / std::max(1, L - 1));
-            c = std::max(c, cut[j - 1]);
-            while (c > b0 && c < b1 && pi.b_lm[B.pb_obs[c]] == pi.b_lm[B.pb_obs[c - 1]]) ++c;
-            cut[j] = c;
-        }
-        int blk = B.ub_ptr[p];
+        int prev = b0;
         for (int j = 0; j < L; ++j) {
-            B.seg_ptr[(size_t)p * L + j] = cut[j];
-            B.seg_blk[(size_t)p * L + j] = blk;
-            for (int i = cut[j]; i < cut[j + 1]; ++i)
-                if (i + 1 == cut[j + 1] || pi.b_lm[B.pb_obs[i + 1]] != pi.b_lm[B.pb_obs[i]]) ++blk;
+            lane_ptr[(size_t)p * L + j] = prev;
+            if (j + 1 < L) {
+                int c = b0 + q0 + (int)((int64_t)(nb - q0) * j / std::max(1, L - 1));
+                c = std::max(c, prev);
+                while (c > b0 && c < b1 && same_lm(c, c - 1)) ++c;
+                prev = c;
+            }
         }
     }
-    B.seg_ptr[(size_t)NP * L] = Mb;
+    lane_ptr[(size_t)NP * L] = Mb;
+    for (int p = 0; p < NP; ++p)
+        for (int i = pb_ptr[p] + 1; i < pb_ptr[p + 1]; ++i)
+            if (same_lm(i, i - 1)) B.has_dups = true;
+    make_lane_lists(NP * L, lane_ptr, pb_obs, B.pose_lanes);
+    make_lane_lists(NL, lb_ptr, lb_obs, B.lm_lanes);
+    // pose-landmark blocks: the slot of the last bearing of each (pose, landmark) run
+    B.ub_ptr.assign(NP + 1, 0);
+    for (int p = 0; p < NP; ++p) {
+        for (int sub = 0; sub < L; ++sub) {
+            const int g = p * L + sub;
+            const int n = B.pose_lanes.cnt[g], i0 = lane_ptr[g];
+            for (int j = 0; j < n; ++j)
+                if (j + 1 == n || !same_lm(i0 + j + 1, i0 + j)) {
+                    B.ub_lm.push_back(pi.b_lm[pb_obs[i0 + j]]);
+                    B.ub_slot.push_back(lane_slot(B.pose_lanes, g, j));
+                }
+        }
+        B.ub_ptr[p + 1] = (int32_t)B.ub_lm.size();
+    }
     B.off_ldiag = 6 * (int64_t)NP;
     B.off_pl = (B.off_ldiag + 3 * (int64_t)NL + 1) & ~(int64_t)1;   // even: 2-value vector stores stay aligned
-    B.off_pp = B.off_pl + 6 * (int64_t)B.nub();
+    B.off_pp = B.off_pl + 6 * B.pose_lanes.slots();
     B.size = B.off_pp + 6 * (int64_t)B.nuo();
     if (B.size > INT32_MAX) { err = "block array exceeds 32-bit indices"; return BOS_ERR_UNSUPPORTED; }
     return BOS_OK;
 }
 
-// Ownership cuts for observation sharding: contiguous pose and landmark ranges balanced by the
-// observations each lane group evaluates.
+// Ownership cuts for observation sharding: contiguous ranges of whole waves of pose lanes and of
+// landmark lanes, balanced by the observations they evaluate.
 void build_ownership(const ProblemIndex& pi, Plan& P, int rank, int world) {
     const BlockLayout& B = P.blk;
-    auto cuts = [&](int n, auto&& work) {
+    const int ppw = B.poses_per_wave();
+    auto cuts = [&](int n, int unit, auto&& work) {   // cut [0, n) at multiples of unit
+        const int nu = (n + unit - 1) / unit;
+        std::vector<int64_t> wu(nu, 0);
+        int64_t total = 0;
+        for (int i = 0; i < n; ++i) { wu[i / unit] += work(i); total += work(i); }
         std::vector<int32_t> c(world + 1, n);
         c[0] = 0;
-        int64_t total = 0;
-        for (int i = 0; i < n; ++i) total += work(i);
         int64_t acc = 0;
         int r = 1;
-        for (int i = 0; i < n && r < world; ++i) {
-            acc += work(i);
-            while (r < world && acc * world >= total * r) c[r++] = i + 1;
+        for (int u = 0; u < nu && r < world; ++u) {
+            acc += wu[u];
+            while (r < world && acc * world >= total * r) c[r++] = std::min(n, (u + 1) * unit);
         }
         return c;
     };
-    P.rank_pose = cuts(pi.NP, [&](int p) { return (int64_t)1 + B.pb_ptr[p + 1] - B.pb_ptr[p] + B.po_ptr[p + 1] - B.po_ptr[p]; });
-    P.rank_lm = cuts(pi.NL, [&](int l) { return (int64_t)1 + B.lb_ptr[l + 1] - B.lb_ptr[l]; });
+    auto npose_items = [&](int p) {
+        int64_t c = 1 + B.po_ptr[p + 1] - B.po_ptr[p];
+        for (int s = 0; s < B.lpp; ++s) c += B.pose_lanes.cnt[(size_t)p * B.lpp + s];
+        return c;
+    };
+    P.rank_pose = cuts(pi.NP, ppw, npose_items);
+    P.rank_lm = cuts(pi.NL, 64, [&](int l) { return (int64_t)1 + B.lm_lanes.cnt[l]; });
     P.rank = rank;
     P.world = world;
     P.p_begin = P.rank_pose[rank]; P.p_end = P.rank_pose[rank + 1];
     P.l_begin = P.rank_lm[rank]; P.l_end = P.rank_lm[rank + 1];
     P.rank_val_ranges.resize(4 * (size_t)world);
     P.rank_b_ranges.resize(2 * (size_t)world);
+    const std::vector<int32_t>& wb = B.pose_lanes.w_base;
+    auto wave_of = [&](int p) { return (int)(((int64_t)p * B.lpp + 63) / 64); };   // p is wave aligned or NP
     for (int r = 0; r < world; ++r) {
         const int p0 = P.rank_pose[r], p1 = P.rank_pose[r + 1], l0 = P.rank_lm[r], l1 = P.rank_lm[r + 1];
         Range* v = &P.rank_val_ranges[4 * (size_t)r];
         v[0] = {6 * (int64_t)p0, 6 * (int64_t)p1};
         v[1] = {B.off_ldiag + 3 * (int64_t)l0, B.off_ldiag + 3 * (int64_t)l1};
-        v[2] = {B.off_pl + 6 * (int64_t)B.ub_ptr[p0], B.off_pl + 6 * (int64_t)B.ub_ptr[p1]};
+        v[2] = {B.off_pl + 6 * (int64_t)wb[wave_of(p0)], B.off_pl + 6 * (int64_t)wb[wave_of(p1)]};
         v[3] = {B.off_pp + 6 * (int64_t)B.uo_ptr[p0], B.off_pp + 6 * (int64_t)B.uo_ptr[p1]};
         Range* bb = &P.rank_b_ranges[2 * (size_t)r];
         bb[0] = {3 * (int64_t)p0, 3 * (int64_t)p1};
@@ -588,10 +616,10 @@ int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& i
     for (int u : inv)
         for (int d = 0; d < node_size(u, NP); ++d) { dof_node[P.node_dof[u] + d] = u; dof_loc[P.node_dof[u] + d] = d; }
     auto tri = [](int r, int c) { return r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r; };
-    auto pl_block = [&](int p, int l) -> int64_t {
+    auto pl_slot = [&](int p, int l) -> int64_t {
         const auto b = B.ub_lm.begin() + B.ub_ptr[p], e = B.ub_lm.begin() + B.ub_ptr[p + 1];
         const auto it = std::lower_bound(b, e, l);
-        return (it != e && *it == l) ? (int64_t)(it - B.ub_lm.begin()) : -1;
+        return (it != e && *it == l) ? (int64_t)B.ub_slot[it - B.ub_lm.begin()] : -1;
     };
     auto pp_block = [&](int s, int d) -> int64_t {
         const auto b = B.uo_dst.begin() + B.uo_ptr[s], e = B.uo_dst.begin() + B.uo_ptr[s + 1];
@@ -607,10 +635,10 @@ int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& i
             if (U == V) {
                 v = U < NP ? 6 * (int64_t)U + tri(a, c) : B.off_ldiag + 3 * (int64_t)(U - NP) + tri(a, c);
             } else if (U < NP && V >= NP) {
-                const int64_t k = pl_block(U, V - NP);
+                const int64_t k = pl_slot(U, V - NP);
                 if (k >= 0) v = B.off_pl + 6 * k + 2 * a + c;
             } else if (U >= NP && V < NP) {
-                const int64_t k = pl_block(V, U - NP);
+                const int64_t k = pl_slot(V, U - NP);
                 if (k >= 0) v = B.off_pl + 6 * k + 2 * c + a;
             } else if (U < NP && V < NP) {
                 int64_t k = pp_block(U, V);
@@ -767,13 +795,15 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
 }
 
 // Proves, on the host, that the J+H kernel's writes (simulated here exactly as hip/kernels.hip
-// issues them) stay inside the block array, cover this rank's ranges exactly once and nothing
-// else, that chi^2 counts every observation once, and that every stored entry of H_nf reads a
-// block value its kernel writes. O(observations + nnz).
+// issues them) stay inside this rank's ranges of the block array, write every value at most once
+// and every value the solver reads exactly once, cover b exactly, and that chi^2 counts every
+// observation once. O(slots + nnz).
 int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
     const int NP = pi.NP, NL = pi.NL;
     const BlockLayout& B = P.blk;
     const int L = B.lpp;
+    const LaneLists& PL = B.pose_lanes;
+    const LaneLists& LL = B.lm_lanes;
     std::vector<uint8_t> hit(B.size, 0), bhit(3 * (size_t)NP + 2 * (size_t)NL, 0);
     std::vector<int32_t> chi(pi.Mb + pi.Mo, 0);
     auto mark = [&](int64_t v0, int cnt) -> bool {
@@ -781,24 +811,25 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
         for (int i = 0; i < cnt; ++i) ++hit[v0 + i];
         return true;
     };
+    if ((P.p_begin * (int64_t)L) % 64 || P.l_begin % 64) { err = "shard does not start at a wave"; return BOS_ERR_INVALID; }
+    std::vector<int32_t> slot_block(PL.slots(), -1);   // landmark whose block lives in the slot
+    for (int p = 0; p < NP; ++p)
+        for (int u = B.ub_ptr[p]; u < B.ub_ptr[p + 1]; ++u) slot_block[B.ub_slot[u]] = B.ub_lm[u];
     for (int p = P.p_begin; p < P.p_end; ++p) {
         if (!mark(6 * (int64_t)p, 6)) { err = "pose diagonal out of range"; return BOS_ERR_INVALID; }
         for (int d = 0; d < 3; ++d) ++bhit[3 * (size_t)p + d];
-        for (int j = 0; j < L; ++j) {
-            const size_t sg = (size_t)p * L + j;
-            int blk = B.seg_blk[sg];
-            const int i0 = B.seg_ptr[sg], i1 = B.seg_ptr[sg + 1];
-            if (i0 < B.pb_ptr[p] || i1 > B.pb_ptr[p + 1] || i0 > i1) { err = "lane segment outside its pose"; return BOS_ERR_INVALID; }
-            for (int i = i0; i < i1; ++i) {
-                const int k = B.pb_obs[i];
+        for (int sub = 0; sub < L; ++sub) {
+            const int g = p * L + sub, n = PL.cnt[g];
+            if (n > PL.w_len[g / 64]) { err = "lane longer than its wave"; return BOS_ERR_INVALID; }
+            for (int j = 0; j < n; ++j) {
+                const int32_t sl = lane_slot(PL, g, j), k = PL.obs[sl];
+                if (k < 0 || pi.b_pose[k] != p) { err = "bearing slot of the wrong pose"; return BOS_ERR_INVALID; }
                 ++chi[k];
-                if (i + 1 == i1 || pi.b_lm[B.pb_obs[i + 1]] != pi.b_lm[k]) {
-                    if (blk < B.ub_ptr[p] || blk >= B.ub_ptr[p + 1] || B.ub_lm[blk] != pi.b_lm[k] ||
-                        !mark(B.off_pl + 6 * (int64_t)blk, 6)) {
+                if (j + 1 == n || pi.b_lm[PL.obs[lane_slot(PL, g, j + 1)]] != pi.b_lm[k]) {
+                    if (slot_block[sl] != pi.b_lm[k] || !mark(B.off_pl + 6 * (int64_t)sl, 6)) {
                         err = "pose-landmark block misplaced";
                         return BOS_ERR_INVALID;
                     }
-                    ++blk;
                 }
             }
         }
@@ -819,10 +850,15 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
         }
     }
     for (int l = P.l_begin; l < P.l_end; ++l) {
+        if (LL.cnt[l] > LL.w_len[l / 64]) { err = "lane longer than its wave"; return BOS_ERR_INVALID; }
+        for (int j = 0; j < LL.cnt[l]; ++j) {
+            const int32_t k = LL.obs[lane_slot(LL, l, j)];
+            if (k < 0 || pi.b_lm[k] != l) { err = "bearing slot of the wrong landmark"; return BOS_ERR_INVALID; }
+        }
         if (!mark(B.off_ldiag + 3 * (int64_t)l, 3)) { err = "landmark diagonal out of range"; return BOS_ERR_INVALID; }
         for (int d = 0; d < 2; ++d) ++bhit[3 * (size_t)NP + 2 * (size_t)l + d];
     }
-    // written exactly once inside this rank's ranges, never outside
+    // at most once, only inside this rank's ranges; everything the solver reads there exactly once
     std::vector<uint8_t> own(B.size, 0), bown(bhit.size(), 0);
     for (int q = 0; q < 4; ++q) {
         const Range& g = P.rank_val_ranges[4 * (size_t)P.rank + q];
@@ -833,7 +869,7 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
         for (int64_t v = g.begin; v < g.end; ++v) bown[v] = 1;
     }
     for (int64_t v = 0; v < B.size; ++v)
-        if (hit[v] != own[v]) {
+        if (hit[v] > own[v]) {
             err = "block value " + std::to_string(v) + " written " + std::to_string((int)hit[v]) + " times";
             return BOS_ERR_INVALID;
         }
@@ -842,12 +878,13 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
     if (P.world == 1)   // single shard: every observation's chi^2 counted once
         for (size_t k = 0; k < chi.size(); ++k)
             if (chi[k] != 1) { err = "chi^2 of observation " + std::to_string(k) + " counted " + std::to_string(chi[k]) + " times"; return BOS_ERR_INVALID; }
-    // every stored entry reads a block value; pose-pose blocks are symmetric (off-diagonal values
-    // read twice), every other value at most once
+    // every stored entry reads a block value written by its owner; pose-pose blocks are symmetric
+    // (off-diagonal values read twice), every other value at most once
     std::vector<uint8_t> refs(B.size, 0);
     for (int32_t v : B.csr_src) {
         if (v < 0 || v >= B.size) { err = "stored entry reads outside the block array"; return BOS_ERR_INVALID; }
         if (++refs[v] > (v >= B.off_pp ? 2 : 1)) { err = "block value read by two stored entries"; return BOS_ERR_INVALID; }
+        if (own[v] && hit[v] != 1) { err = "block value read by the solver is never written"; return BOS_ERR_INVALID; }
     }
     return BOS_OK;
 }

@@ -31,37 +31,46 @@ struct ProblemIndex {
 // and csr_src). One array of T:
 //   [0, off_ldiag)        pose diagonal blocks, 6 per pose, lower triangle (00, 10, 11, 20, 21, 22)
 //   [off_ldiag, off_pl)   landmark diagonal blocks, 3 per landmark (00, 10, 11)
-//   [off_pl, off_pp)      pose-landmark blocks H_pl (3 x 2 row-major), one per unique (pose,
-//                         landmark) pair, ordered by pose then landmark
+//   [off_pl, off_pp)      pose-landmark blocks H_pl (3 x 2 row-major), 6 values per bearing slot
+//                         (below); a pair observed more than once uses the slot of its last bearing
 //   [off_pp, size)        pose-pose blocks H_sd, one per unique odometry (src, dst) pair, ordered by
 //                         src then dst; H_sd = -J_s^T Omega J_s is symmetric (J_d = -J_s), so 6
 //                         values like a diagonal block
 // b stays in the reference dof numbering (3 per pose, then 2 per landmark; the fixed pose's entries
 // are computed but not used). Diagonal blocks and b include all nodes, the fixed pose too.
 //
-// Work: lane groups of lpp lanes per pose, each lane a segment of the pose's bearings (sorted by
-// landmark, so duplicate observations of one pair are adjacent and merged by one lane); lane 0 of
-// the group also takes the pose's odometry entries. One lane per landmark for its diagonal block.
+// Work: lpp lanes per pose (lane g = pose * lpp + sub), one lane per landmark; lanes form waves of
+// 64. A lane walks a list of bearings (pose lanes: a segment of the pose's bearings sorted by
+// landmark, so duplicates of one pair are adjacent and merged by one lane; lane 0 of a pose also
+// walks its odometry entries). The lists are stored wave-interleaved (ELL per wave): item j of
+// lane t of wave w sits in slot w_base[w] + 64 j + t, so each step of a wave reads 64 consecutive
+// records and writes 64 consecutive blocks — whole cache lines, no re-fetch between steps.
+struct LaneLists {
+    std::vector<int32_t> w_base;    // [waves + 1] first slot of each wave (64 * w_len slots)
+    std::vector<int32_t> w_len;     // [waves] items per lane in the wave (max over its lanes)
+    std::vector<int32_t> cnt;       // [lanes] items of each lane
+    std::vector<int32_t> obs;       // [slots] bearing in each slot, -1 = padding
+    int64_t slots() const { return w_base.empty() ? 0 : w_base.back(); }
+};
+
 struct BlockLayout {
     int64_t off_ldiag = 0, off_pl = 0, off_pp = 0, size = 0;
     int lpp = 1;                        // lanes per pose: 1, 2 or 4
     bool has_dups = false;              // some (pose, landmark) or (src, dst) pair repeats
-    std::vector<int32_t> pb_obs;        // [Mb] bearings sorted by (pose, landmark, index)
-    std::vector<int32_t> pb_ptr;        // [NP + 1] bearings of each pose (into pb_obs)
-    std::vector<int32_t> seg_ptr;       // [NP * lpp + 1] lane segments (into pb_obs)
-    std::vector<int32_t> seg_blk;       // [NP * lpp] first pose-landmark block of each segment
+    LaneLists pose_lanes;               // lanes = NP * lpp
+    LaneLists lm_lanes;                 // lanes = NL
     std::vector<int32_t> ub_ptr;        // [NP + 1] pose-landmark blocks of each pose
-    std::vector<int32_t> ub_lm;         // [nub] landmark of each pose-landmark block
+    std::vector<int32_t> ub_lm;         // [nub] landmark of each pose-landmark block (ascending per pose)
+    std::vector<int32_t> ub_slot;       // [nub] bearing slot holding the block
     std::vector<int32_t> po_ptr;        // [NP + 1] odometry entries of each pose
     std::vector<int32_t> po_ent;        // edge << 1 | 1 when the pose is the destination
     std::vector<int32_t> po_blk;        // pose-pose block of a source-side entry, -1 on the destination side
     std::vector<int32_t> uo_ptr;        // [NP + 1] pose-pose blocks of each pose (as source)
     std::vector<int32_t> uo_dst;        // [nuo] destination pose of each pose-pose block
-    std::vector<int32_t> lb_ptr;        // [NL + 1] bearings of each landmark (into lb_obs)
-    std::vector<int32_t> lb_obs;        // [Mb] bearings sorted by (landmark, pose, index)
     std::vector<int32_t> csr_src;       // [nnzA] block value of each stored entry of P^T H_nf P
     int nub() const { return ub_ptr.empty() ? 0 : ub_ptr.back(); }
     int nuo() const { return uo_ptr.empty() ? 0 : uo_ptr.back(); }
+    int poses_per_wave() const { return 64 / lpp; }
 };
 
 // A contiguous piece of the block array / b that one rank writes (and broadcasts).
