@@ -80,9 +80,13 @@ def cpu_gn_baseline(P, budget_s=10.0):
             "sample": f"{n} GN iterations of config 3 (oracle J+H fp64 + scipy spsolve + box-plus)"}
 
 
+PROFILE_TAG = "r01"   # profiles/<tag>_pmc_linearize_<prec>.json, written by tools/pmc_summary.py
+
+
 def traffic_from_profile(precision):
-    """HBM bytes per launch of the J+H kernel from the committed rocprofv3 PMC summary."""
-    name = "r01_pmc_linearize_fp32.json" if precision == bos.BOS_FP32 else "r01_pmc_linearize_fp64.json"
+    """HBM bytes per launch of the J+H kernel from the committed rocprofv3 PMC summary
+    (L2<->fabric requests by size, tools/gpu_profile.sh)."""
+    name = f"{PROFILE_TAG}_pmc_linearize_" + ("fp32" if precision == bos.BOS_FP32 else "fp64") + ".json"
     path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None
