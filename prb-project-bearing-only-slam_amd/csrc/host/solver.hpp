@@ -1,5 +1,5 @@
 // proj02::Solver — C++ façade with the reference's API (slam/solver.hpp:21-92) over the C ABI
-// (include/bos.h). step() runs on the GPU (HIP kernels + rocSOLVER); there is no CPU path.
+// (include/bos.h). step() runs on the GPU (HIP kernels + GPU sparse Cholesky); there is no CPU path.
 //
 // Differences to the reference, all documented in INTEGRATION.md:
 //  - SparseMatrixXf Jacobians (Eigen) become small dense blocks with their column indices
