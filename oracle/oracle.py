@@ -66,6 +66,10 @@ def lib():
         L.oracle_smallest_angle_f64.argtypes = [ctypes.c_double]
         L.oracle_smallest_angle_f32.restype = ctypes.c_float
         L.oracle_smallest_angle_f32.argtypes = [ctypes.c_float]
+        L.oracle_atan2_f64.restype = ctypes.c_double
+        L.oracle_atan2_f64.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.oracle_atan2_f32.restype = ctypes.c_float
+        L.oracle_atan2_f32.argtypes = [ctypes.c_float, ctypes.c_float]
         L.oracle_predict_bearing_f64.restype = ctypes.c_double
         L.oracle_predict_bearing_f64.argtypes = [dp, ctypes.c_double, ctypes.c_double]
         L.oracle_predict_bearing_f32.restype = ctypes.c_float
@@ -90,7 +94,7 @@ def lib():
         L.oracle_triangulate.restype = ctypes.c_int
         L.oracle_triangulate.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, dp,
                                          ctypes.c_int, ip, dp]
-        assert L.oracle_version() == 3
+        assert L.oracle_version() == 4
         _lib = L
     return _lib
 
@@ -120,6 +124,12 @@ def smallest_angle(a: float, precision: int = 64) -> float:
     if precision == 32:
         return lib().oracle_smallest_angle_f32(a)
     return lib().oracle_smallest_angle_f64(a)
+
+
+def atan2(y: float, x: float, precision: int = 64) -> float:
+    """The portable atan2 shared by the oracle and the GPU path (det_atan2.hpp)."""
+    L = lib()
+    return L.oracle_atan2_f64(y, x) if precision == 64 else L.oracle_atan2_f32(y, x)
 
 
 def predict_bearing(pose, lm, precision: int = 64) -> float:

@@ -93,12 +93,17 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, double& chi, i
         const int n = P.pl_cnt[g];
         int sl = P.pw_base[g >> 6] + t;   // slot of item j: + 64 j
         T acc[6] = {0, 0, 0, 0, 0, 0};
-        BRec<T> nxt;
-        if (n > 0) nxt = P.pb[sl];
+        // two-stage software pipeline: record j+2 and the landmark of item j+1 are in flight while
+        // item j is evaluated
+        BRec<T> nxt, nxt2;
+        V2<T> Lnxt;
+        if (n > 0) { nxt = P.pb[sl]; Lnxt = load2(P.lc + 2 * nxt.idx); }
+        if (n > 1) nxt2 = P.pb[sl + 64];
         for (int j = 0; j < n; ++j, sl += 64) {
             const BRec<T> cur = nxt;
-            if (j + 1 < n) nxt = P.pb[sl + 64];
-            const V2<T> Lm = load2(P.lc + 2 * cur.idx);
+            const V2<T> Lm = Lnxt;
+            if (j + 1 < n) { nxt = nxt2; Lnxt = load2(P.lc + 2 * nxt.idx); }
+            if (j + 2 < n) nxt2 = P.pb[sl + 128];
             T J[5];
             T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, cur.z, J);   // :9-95
             const T w = HAS_W ? P.pb_w[sl] : (T)1;
@@ -188,12 +193,15 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P) {
     T h00 = 0, h10 = 0, h11 = 0, g0 = 0, g1 = 0;
     const int n = P.ll_cnt[l];
     int sl = P.lw_base[l >> 6] + (l & 63);
-    BRec<T> nxt;
-    if (n > 0) nxt = P.lb[sl];
+    BRec<T> nxt, nxt2;
+    V4<T> Xnxt;
+    if (n > 0) { nxt = P.lb[sl]; Xnxt = load4(P.pc + 4 * nxt.idx); }
+    if (n > 1) nxt2 = P.lb[sl + 64];
     for (int j = 0; j < n; ++j, sl += 64) {
         const BRec<T> cur = nxt;
-        if (j + 1 < n) nxt = P.lb[sl + 64];
-        const V4<T> X = load4(P.pc + 4 * cur.idx);
+        const V4<T> X = Xnxt;
+        if (j + 1 < n) { nxt = nxt2; Xnxt = load4(P.pc + 4 * nxt.idx); }
+        if (j + 2 < n) nxt2 = P.lb[sl + 128];
         T J[5];
         T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, cur.z, J);
         const T w = HAS_W ? P.lb_w[sl] : (T)1;
@@ -231,22 +239,6 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(const LinParams<T> P)
         for (int w = 0; w < kBlock / 64; ++w) { c += sc[w]; r += sr[w]; }
         P.chi2_part[blockIdx.x] = c;
         P.nrob_part[blockIdx.x] = r;
-    }
-}
-
-template <typename T> __global__ void refresh_cache_kernel(const UpdateParams<T> U) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < U.NP) {
-        const double x = U.pose[3 * i], y = U.pose[3 * i + 1], th = U.pose[3 * i + 2];
-        U.pc[4 * i] = (T)x;
-        U.pc[4 * i + 1] = (T)y;
-        U.pc[4 * i + 2] = cos((T)th);
-        U.pc[4 * i + 3] = sin((T)th);
-        U.pth[i] = (T)th;
-    } else if (i < U.NP + U.NL) {
-        const int j = i - U.NP;
-        U.lc[2 * j] = (T)U.lm[2 * j];
-        U.lc[2 * j + 1] = (T)U.lm[2 * j + 1];
     }
 }
 
@@ -343,13 +335,6 @@ hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has
     return has_dups ? launch_lin_lpp<T, false, true>(p, lpp, grid, s) : launch_lin_lpp<T, false, false>(p, lpp, grid, s);
 }
 
-template <typename T> hipError_t launch_refresh_cache(const UpdateParams<T>& p, hipStream_t s) {
-    const int n = p.NP + p.NL;
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL((refresh_cache_kernel<T>), dim3((n + 255) / 256), dim3(256), 0, s, p);
-    return hipGetLastError();
-}
-
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s) {
     const int n = p.NP + p.NL;
     if (n == 0) return hipSuccess;
@@ -387,8 +372,6 @@ hipError_t launch_scatter_dense(const int32_t* rowptr, const int32_t* colind, co
 
 template hipError_t launch_linearize<double>(const LinParams<double>&, int, bool, bool, hipStream_t);
 template hipError_t launch_linearize<float>(const LinParams<float>&, int, bool, bool, hipStream_t);
-template hipError_t launch_refresh_cache<double>(const UpdateParams<double>&, hipStream_t);
-template hipError_t launch_refresh_cache<float>(const UpdateParams<float>&, hipStream_t);
 template hipError_t launch_boxplus<double>(const UpdateParams<double>&, hipStream_t);
 template hipError_t launch_boxplus<float>(const UpdateParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);

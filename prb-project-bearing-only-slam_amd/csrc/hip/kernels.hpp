@@ -19,7 +19,7 @@ template <> struct alignas(16) BRec<double> { int32_t idx; int32_t pad; double z
 // per owned pose, the rest one lane per owned landmark. Lane lists are wave-interleaved: item j of
 // lane t of wave w is slot w_base[w] + 64 j + t.
 template <typename T> struct LinParams {
-    // state caches (T precision), refreshed by the box-plus kernel
+    // state caches (T precision): host-computed at create / set_state, then kept by the box-plus kernel
     const T* pc;          // [NP][4] x, y, cos(theta), sin(theta)
     const T* pth;         // [NP] theta
     const T* lc;          // [NL][2]
@@ -66,7 +66,6 @@ template <typename T> struct UpdateParams {
 
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);
-template <typename T> hipError_t launch_refresh_cache(const UpdateParams<T>& p, hipStream_t s);
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s);
 hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double* chi_out,
                                int32_t* nrob_out, hipStream_t s);

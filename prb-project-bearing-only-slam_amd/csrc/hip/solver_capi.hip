@@ -257,12 +257,32 @@ int enqueue_update(bos_solver* s) {
     return BOS_OK;
 }
 
-int refresh_cache(bos_solver* s) {
-    hipError_t e = s->precision == BOS_FP32 ? bos::dev::launch_refresh_cache<float>(upd_params<float>(s), s->stream)
-                                            : bos::dev::launch_refresh_cache<double>(upd_params<double>(s), s->stream);
-    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("cache launch: ") + hipGetErrorString(e));
+// State caches in T precision (x, y, cos, sin per pose; theta; landmark x, y) computed on the host
+// from the master state with the host libm, exactly as the CPU oracle evaluates them, so that
+// iteration 0 is bit-reproducible against it (see host/det_atan2.hpp); the box-plus kernel keeps
+// them current afterwards.
+template <typename T> int upload_cache_T(bos_solver* s) {
+    const int NP = s->NP, NL = s->NL;
+    std::vector<double> pose(3 * (size_t)NP), lm(2 * (size_t)NL);
+    HIP_TRY(hipMemcpy(pose.data(), s->d_pose, pose.size() * sizeof(double), hipMemcpyDeviceToHost));
+    if (NL) HIP_TRY(hipMemcpy(lm.data(), s->d_lm, lm.size() * sizeof(double), hipMemcpyDeviceToHost));
+    std::vector<T> pc(4 * (size_t)NP), pth(NP), lc(2 * (size_t)NL);
+    for (int i = 0; i < NP; ++i) {
+        const T th = (T)pose[3 * (size_t)i + 2];
+        pc[4 * (size_t)i] = (T)pose[3 * (size_t)i];
+        pc[4 * (size_t)i + 1] = (T)pose[3 * (size_t)i + 1];
+        pc[4 * (size_t)i + 2] = std::cos(th);
+        pc[4 * (size_t)i + 3] = std::sin(th);
+        pth[i] = th;
+    }
+    for (size_t j = 0; j < lc.size(); ++j) lc[j] = (T)lm[j];
+    HIP_TRY(hipMemcpy(s->d_pc, pc.data(), pc.size() * sizeof(T), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->d_pth, pth.data(), pth.size() * sizeof(T), hipMemcpyHostToDevice));
+    if (NL) HIP_TRY(hipMemcpy(s->d_lc, lc.data(), lc.size() * sizeof(T), hipMemcpyHostToDevice));
     return BOS_OK;
 }
+
+int upload_cache(bos_solver* s) { return s->precision == BOS_FP32 ? upload_cache_T<float>(s) : upload_cache_T<double>(s); }
 
 float elapsed(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
@@ -570,7 +590,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     HIP_TRY(hipMemset(s->d_chi_part, 0, nt * sizeof(double)));
     HIP_TRY(hipMemset(s->d_nrob_part, 0, nt * sizeof(int32_t)));
     HIP_TRY(hipMemset(s->d_info, 0, sizeof(int32_t)));
-    if ((rc = refresh_cache(s))) return bail(rc);
+    if ((rc = upload_cache(s))) return bail(rc);
     HIP_TRY(hipStreamSynchronize(s->stream));
     *out = s;
     return BOS_OK;
@@ -717,7 +737,7 @@ int bos_set_state(bos_solver* s, const double* pose_xyt, const double* landmark_
     }
     if (landmark_xy && s->NL)
         HIP_TRY(hipMemcpy(s->d_lm, landmark_xy, 2 * (size_t)s->NL * sizeof(double), hipMemcpyHostToDevice));
-    int rc = refresh_cache(s);
+    int rc = upload_cache(s);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     return BOS_OK;

@@ -9,6 +9,8 @@
 
 #include <cmath>
 
+#include "det_atan2.hpp"
+
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define BOS_HD __host__ __device__ __forceinline__
@@ -38,10 +40,23 @@ template <typename T> BOS_HD T smallest_angle(T a) {
     return t;
 }
 
-template <typename T> BOS_HD T bos_atan2(T y, T x) { return atan2(y, x); }
-#if defined(__HIPCC__) || defined(__HIP__)
-template <> BOS_HD float bos_atan2<float>(float y, float x) { return atan2f(y, x); }
+// Bearing error only (slam/solver_jacobians.cpp:15-18, :301-305), with g = X^-1 l. Evaluated with
+// plain IEEE operations (no FP contraction) and the portable atan2, so that the GPU lanes and the
+// CPU oracle round identically: an error on the +-pi wrap flips sign on a last-ulp difference
+// (det_atan2.hpp).
+template <typename T> BOS_HD T bearing_error(T px, T py, T c, T s, T lx, T ly, T z, T& gx, T& gy) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
 #endif
+    // g = X^-1 l = R^T l + (-R^T t), Isometry inverse (R^T, -R^T t) (:32, :302); explicit fma
+    // (correctly rounded on both targets), the oracle evaluates the same expressions
+    using std::fma;
+    const T itx = -fma(c, px, s * py);
+    const T ity = -fma(-s, px, c * py);
+    gx = fma(c, lx, s * ly) + itx;
+    gy = fma(-s, lx, c * ly) + ity;
+    return normalized_angle<T>(det_atan2<T>(gy, gx) - z);                // :15, :18
+}
 
 // Bearing error and analytic Jacobian (slam/solver_jacobians.cpp:9-95).
 // Inputs: pose translation (px, py), cached c = cos(theta), s = sin(theta); landmark (lx, ly);
@@ -49,12 +64,8 @@ template <> BOS_HD float bos_atan2<float>(float y, float x) { return atan2f(y, x
 // J = [dJ/dt_x, dJ/dt_y, dJ/dtheta, dJ/dl_x, dJ/dl_y]. Returns e.
 template <typename T>
 BOS_HD T bearing_error_jacobian(T px, T py, T c, T s, T lx, T ly, T z, T J[5]) {
-    // g = X^-1 l, Isometry inverse (R^T, -R^T t) (:32, :302)
-    const T itx = -(c * px + s * py);
-    const T ity = -(-s * px + c * py);
-    const T gx = (c * lx + s * ly) + itx;
-    const T gy = (-s * lx + c * ly) + ity;
-    const T e = normalized_angle<T>(bos_atan2<T>(gy, gx) - z);          // :15, :18
+    T gx, gy;
+    const T e = bearing_error<T>(px, py, c, s, lx, ly, z, gx, gy);
     const T f = (T)1 / (gx * gx + gy * gy);                              // :35
     const T a0 = f * (-gy), a1 = f * gx;                                 // :47-48
     const T gth_x = c * ly + s * (-lx);                                  // R^T [[0,1],[-1,0]] l (:60)

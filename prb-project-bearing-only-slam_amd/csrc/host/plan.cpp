@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <numeric>
 
 #include "../../../include/bos.h"
@@ -512,7 +513,11 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     // lanes per pose and their bearing segments (lane 0 also takes the odometry entries; a run of
     // duplicate observations of one pair never straddles two lanes)
     const double avg = NP ? (double)Mb / NP : 0.0;
-    B.lpp = avg >= 24 ? 4 : avg >= 8 ? 2 : 1;
+    B.lpp = avg >= 32 ? 2 : 1;   // measured on config 3 (K = 10): 1 lane per pose beats 2 and 4
+    if (const char* e = std::getenv("BOS_LANES_PER_POSE")) {   // tuning override: 1, 2 or 4
+        const int v = std::atoi(e);
+        if (v == 1 || v == 2 || v == 4) B.lpp = v;
+    }
     const int L = B.lpp;
     auto same_lm = [&](int i, int j) { return pi.b_lm[pb_obs[i]] == pi.b_lm[pb_obs[j]]; };
     std::vector<int32_t> lane_ptr((size_t)NP * L + 1, 0);

@@ -39,7 +39,7 @@ def c1():
     return bos.load_g2o(C1)
 
 
-def _lin_parity(P, precision=bos.BOS_FP64, kt=1.0, damping=0.01, tol=1e-12, p999=None):
+def _lin_parity(P, precision=bos.BOS_FP64, kt=1.0, damping=0.01, tol=1e-12, p999=None, btol=None):
     Q = to_oracle(P)
     S = bos.Solver(P, precision=precision, kernel_threshold=kt, damping=damping)
     st = S.linearize()
@@ -54,7 +54,7 @@ def _lin_parity(P, precision=bos.BOS_FP64, kt=1.0, damping=0.01, tol=1e-12, p999
     assert np.all(b[~keep] == 0.0)
     eb = np.abs(b - lin.b)[keep].max() / max(np.abs(lin.b[keep]).max(), 1e-300)
     assert eh <= tol, f"H rel err {eh}"
-    assert eb <= 10 * tol, f"b rel err {eb}"
+    assert eb <= (10 * tol if btol is None else btol), f"b rel err {eb}"
     if p999 is not None:
         # scale-invariant per-entry error |dH_ij| / sqrt(H_ii H_jj) (bounded by 1 for SPD H)
         d = (Hg - Ho).tocoo()
@@ -81,8 +81,10 @@ def test_linearize_mini_fp64():
 @pytest.mark.parametrize("kt", [1e-8, 1e12])
 def test_robust_branch_forced(c1, kt):
     # kt tiny: every observation is rescaled (the rare branch, solver.cpp:38-40 / :55-57);
-    # kt huge: none is.
-    _lin_parity(c1, kt=kt)
+    # kt huge: none is. With every residual rescaled to |e| = sqrt(kt), b shrinks to max 0.066
+    # while its terms do not, so the relative b metric is ill-conditioned: the CPU oracle built
+    # with and without FMA contraction already differs by 1.16e-11 here (2.4e-14 at kt = 1).
+    _lin_parity(c1, kt=kt, btol=1e-10 if kt < 1e-4 else None)
 
 
 @pytest.mark.parametrize("damping", [0.0, 1.0])

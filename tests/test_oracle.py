@@ -205,3 +205,42 @@ def test_accuracy_vs_ground_truth(c1):
     e1 = np.linalg.norm(X[:, :2] - pose_gt[:, :2], axis=1)
     assert np.median(e1) < 0.5 * np.median(e0)
     assert e1.max() < e0.max()
+
+
+def _ulps(a, b, dtype):
+    ia = np.asarray(a, dtype=dtype).view(np.int64 if dtype == np.float64 else np.int32).astype(np.int64)
+    ib = np.asarray(b, dtype=dtype).view(np.int64 if dtype == np.float64 else np.int32).astype(np.int64)
+    lim = np.int64(-(2 ** 63)) if dtype == np.float64 else np.int64(-(2 ** 31))
+    ia = np.where(ia < 0, lim - ia, ia)
+    ib = np.where(ib < 0, lim - ib, ib)
+    return np.abs(ia - ib)
+
+
+def test_portable_atan2_within_one_ulp():
+    """det_atan2.hpp (shared by the oracle and the GPU path so both round identically on the +-pi
+    wrap) against libm atan2 through NumPy: <= 1 ulp in double, and in float against the rounded
+    double result."""
+    rng = np.random.default_rng(5)
+    n = 20000
+    y = rng.uniform(-1, 1, n) * 10.0 ** rng.uniform(-3, 3, n)
+    x = rng.uniform(-1, 1, n) * 10.0 ** rng.uniform(-3, 3, n)
+    y[::7] = x[::7] * (1 + 1e-3 * rng.uniform(-1, 1, len(x[::7])))
+    edges = [(0.0, -1.0), (-0.0, -1.0), (1.0, 0.0), (-1.0, 0.0), (0.0, 1.0), (1e-300, -1.0), (3.0, -3.0)]
+    y = np.concatenate([y, [e[0] for e in edges]])
+    x = np.concatenate([x, [e[1] for e in edges]])
+    d = np.array([O.atan2(a, b) for a, b in zip(y, x)])
+    assert _ulps(d, np.arctan2(y, x), np.float64).max() <= 1
+    yf, xf = y.astype(np.float32), x.astype(np.float32)
+    f = np.array([O.atan2(float(a), float(b), 32) for a, b in zip(yf, xf)], dtype=np.float32)
+    ref = np.arctan2(yf.astype(np.float64), xf.astype(np.float64)).astype(np.float32)
+    assert _ulps(f, ref, np.float32).max() <= 1
+
+
+def test_wrap_knife_edge_is_reproducible(c1):
+    """Landmark 112 (one observation, rank-1 basic solution) sits exactly behind its observer:
+    atan2(g) - z is within an ulp of pi, so the sign of e is decided by rounding. The oracle
+    evaluates it with the portable atan2, bit for bit like the GPU kernels."""
+    j = int(np.nonzero(c1.lm_ids == 112)[0][0])
+    k = int(np.nonzero(c1.b_lm == j)[0][0])
+    e, _ = O.bearing_error_and_jacobian(c1.pose_xyt[c1.b_pose[k]], c1.lm_xy[j], c1.b_z[k])
+    assert abs(abs(e) - PI) < 1e-12
