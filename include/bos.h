@@ -77,7 +77,9 @@ typedef struct bos_options {
     int32_t device;                 /* HIP device ordinal, -1 = current                          */
     int32_t rank;                   /* shard index (0 for one GPU)                               */
     int32_t world_size;             /* number of shards (1 for one GPU)                          */
-    const void* nccl_unique_id;     /* 128-byte ncclUniqueId when world_size > 1, else NULL      */
+    const void* nccl_unique_id;     /* 128-byte ncclUniqueId; required when world_size > 1. Given
+                                       with world_size 1 it still creates the communicator and runs
+                                       the exchange collectives (single-GPU test of that path)     */
     double kernel_threshold;        /* robust kernel threshold, reference default 1.0 (:16)      */
     double damping;                 /* damping factor, reference default 0.01 (:17)              */
     void* stream;                   /* hipStream_t to launch on, NULL = the handle's own stream  */

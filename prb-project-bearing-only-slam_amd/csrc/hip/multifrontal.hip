@@ -2,14 +2,18 @@
 // Eigen SimplicialLDLT, slam/solver.cpp:75-85; pattern analysed once like analyzePattern at
 // :77-80 — here the symbolic analysis is host/plan.cpp build_multifrontal).
 //
-// H_nf (already in nested-dissection order, lower CSR) = L L^T. The assembly tree is processed
-// level by level (leaves first): one launch per level, one workgroup per supernode. A workgroup
-//   1. zeroes its dense front F (m x m, column-major, in LDS when it fits, else global scratch),
-//   2. scatters its entries of H (precomputed map) and extend-adds its children's update
-//      matrices (children sequentially, entries in parallel: deterministic),
-//   3. runs a right-looking partial Cholesky of its k own columns,
-//   4. writes the m x k panel of L and the r x r update matrix for its parent.
-// Forward (bottom-up) and backward (top-down) substitutions use the same tree and levels.
+// P^T H_nf P = L L^T, H read from the J+H kernel's block array through the assembly map. The
+// assembly tree is processed level by level (leaves first). Each level has two launches:
+//  * fronts with m = k + r <= kMfWaveMaxM (the many small ones near the leaves): one wavefront per
+//    front, the front packed lower-triangular in LDS, wave-level synchronisation only;
+//  * larger fronts: one 256-thread workgroup, full m x m front in LDS (m <= 90) or global scratch.
+// A front is
+//   1. zeroed, then receives its entries of H (precomputed map) and the extend-add of its
+//      children's update matrices (children sequentially, entries in parallel: deterministic),
+//   2. partially factored (right-looking Cholesky of its k own columns),
+//   3. written out: the m x k panel of L and the packed r x r update matrix for its parent.
+// Forward (bottom-up) and backward (top-down) substitutions use the same tree and levels; the
+// wave variants stage the L panel in LDS so no global load sits on the sequential dependency chain.
 // Everything is fp64 and deterministic (no atomics on values).
 #include <hip/hip_runtime.h>
 
@@ -27,7 +31,15 @@ namespace dev {
 namespace {
 
 constexpr int kMfBlock = 256;
-constexpr int kLdsCapM = 90;   // fronts up to 90 x 90 doubles (64.8 KB) are factored in LDS
+constexpr int kLdsCapM = 90;   // larger fronts up to 90 x 90 doubles (64.8 KB) are factored in LDS
+
+__device__ __forceinline__ int64_t pk(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 struct MfArgs {
     const int32_t* level;        // supernode ids of this level
@@ -76,10 +88,10 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_level(const MfArgs a) {
         const int rc = a.r[c];
         const int32_t* map = a.rmap + a.rmap_off[c];
         const double* Uc = a.U + a.U_off[c];
-        const int64_t n2 = (int64_t)rc * rc;
-        for (int64_t e = tid; e < n2; e += kMfBlock) {
-            const int i = (int)(e % rc), j = (int)(e / rc);
-            if (i >= j) F[map[i] + (int64_t)map[j] * m] += Uc[e];
+        for (int j = tid >> 6; j < rc; j += kMfBlock / 64) {
+            const int64_t pj = (int64_t)map[j] * m;
+            const double* uj = Uc + pk(j, j, rc) - j;
+            for (int i = j + (tid & 63); i < rc; i += 64) F[map[i] + pj] += uj[i];
         }
         __syncthreads();
     }
@@ -110,10 +122,72 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_level(const MfArgs a) {
     const int64_t nL = (int64_t)m * k;
     for (int64_t e = tid; e < nL; e += kMfBlock) Ls[e] = F[e];
     double* Us = a.U + a.U_off[s];
-    const int64_t nU = (int64_t)r * r;
-    for (int64_t e = tid; e < nU; e += kMfBlock) {
-        const int i = (int)(e % r), j = (int)(e / r);
-        Us[e] = F[(k + i) + (int64_t)(k + j) * m];
+    for (int j = wave; j < r; j += kMfBlock / 64) {
+        double* uj = Us + pk(j, j, r) - j;
+        const double* fj = F + (k + (int64_t)(k + j) * m);
+        for (int i = j + lane; i < r; i += 64) uj[i] = fj[i];
+    }
+}
+
+// One wavefront per front (m <= kMfWaveMaxM), front packed lower-triangular in LDS.
+__global__ __launch_bounds__(64) void mf_factor_wave(const MfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double F[];
+    const int s = a.level[blockIdx.x];
+    const int k = a.k[s], r = a.r[s], m = k + r;
+    const int lane = threadIdx.x;
+    const int np = m * (m + 1) / 2;
+    for (int e = lane; e < np; e += 64) F[e] = 0.0;
+    wave_sync();
+    for (int q = a.amap_ptr[s] + lane; q < a.amap_ptr[s + 1]; q += 64) F[a.amap_dst[q]] = a.A[a.amap_src[q]];
+    wave_sync();
+    for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {   // positions of one child are distinct
+        const int c = a.child[ci];
+        const int rc = a.r[c];
+        const int32_t* map = a.rmap + a.rmap_off[c];
+        const double* Uc = a.U + a.U_off[c];
+        for (int j = 0; j < rc; ++j) {
+            const int pj = map[j];
+            const double* uj = Uc + pk(j, j, rc) - j;
+            for (int i = j + lane; i < rc; i += 64) F[pk(map[i], pj, m)] += uj[i];
+        }
+        wave_sync();
+    }
+    for (int j = 0; j < k; ++j) {
+        const int cj = (int)pk(j, j, m);   // column j: F[cj + (i - j)], i >= j
+        double d = F[cj];
+        if (!(d > 0.0)) {
+            if (lane == 0) atomicAdd(a.info, 1);
+            d = 1e-300;
+        }
+        const double ljj = sqrt(d), inv = 1.0 / ljj;
+        wave_sync();
+        if (lane == 0) F[cj] = ljj;
+        for (int i = j + 1 + lane; i < m; i += 64) F[cj + i - j] *= inv;
+        wave_sync();
+        // trailing triangle (columns j+1.., rows >= column) is contiguous in packed storage:
+        // lanes take every 64th entry, decoding (row, column) incrementally
+        int l = j + 1, len = m - l, o = lane;
+        while (len > 0 && o >= len) { o -= len; ++l; --len; }
+        int p = (int)pk(l, l, m) + o;
+        while (len > 0) {
+            F[p] -= F[cj + (l + o) - j] * F[cj + l - j];
+            o += 64;
+            p += 64;
+            while (len > 0 && o >= len) { o -= len; ++l; --len; }
+        }
+        wave_sync();
+    }
+    double* Ls = a.L + a.L_off[s];
+    for (int j = 0; j < k; ++j) {
+        const double* fj = F + pk(j, j, m) - j;
+        double* lj = Ls + (int64_t)j * m;
+        for (int i = j + lane; i < m; i += 64) lj[i] = fj[i];
+    }
+    double* Us = a.U + a.U_off[s];
+    for (int j = 0; j < r; ++j) {
+        const double* fj = F + pk(k + j, k + j, m) - j;
+        double* uj = Us + pk(j, j, r) - j;
+        for (int i = j + lane; i < r; i += 64) uj[i] = fj[i];
     }
 }
 
@@ -181,6 +255,73 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
     for (int j = tid; j < k; j += kMfBlock) a.x[c0 + j] = w[j];
 }
 
+// forward substitution, one wavefront per front (m <= kMfWaveMaxM); LDS: w[m] | L panel (lower, m x k)
+__global__ __launch_bounds__(64) void mf_forward_wave(const MfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double w[];
+    const int s = a.level[blockIdx.x];
+    const int k = a.k[s], r = a.r[s], m = k + r;
+    const int lane = threadIdx.x;
+    const int c0 = a.col0[s];
+    double* Lw = w + m;
+    const double* Ls = a.L + a.L_off[s];
+    for (int e = lane; e < m * k; e += 64) Lw[e] = Ls[e];
+    for (int i = lane; i < m; i += 64) w[i] = i < k ? a.x[c0 + i] : 0.0;
+    wave_sync();
+    for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {
+        const int c = a.child[ci];
+        const int rc = a.r[c];
+        const int32_t* map = a.rmap + a.rmap_off[c];
+        const double* uc = a.u + a.u_off[c];
+        for (int t = lane; t < rc; t += 64) w[map[t]] += uc[t];
+        wave_sync();
+    }
+    for (int j = 0; j < k; ++j) {
+        const double yj = w[j] / Lw[j + j * m];
+        wave_sync();
+        if (lane == 0) w[j] = yj;
+        for (int i = j + 1 + lane; i < m; i += 64) w[i] -= Lw[i + j * m] * yj;
+        wave_sync();
+    }
+    for (int i = lane; i < m; i += 64) {
+        if (i < k) a.x[c0 + i] = w[i];
+        else a.u[a.u_off[s] + (i - k)] = w[i];
+    }
+}
+
+// backward substitution, one wavefront per front; LDS: x_own[k] | t[k] | L panel (m x k)
+__global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double w[];
+    const int s = a.level[blockIdx.x];
+    const int k = a.k[s], r = a.r[s], m = k + r;
+    const int lane = threadIdx.x;
+    const int c0 = a.col0[s];
+    const double* Ls = a.L + a.L_off[s];
+    const int32_t* fi = a.findex + a.findex_off[s];
+    double* t = w + k;
+    double* Lw = w + 2 * k;
+    for (int e = lane; e < m * k; e += 64) Lw[e] = Ls[e];
+    // the rows below the supernode are ancestors' dofs, final in x: xr in the lane of the row
+    const double xr = lane < r ? a.x[fi[k + lane]] : 0.0;
+    for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
+    wave_sync();
+    // t_j = sum_i L[k + i, j] x[fi[k + i]]: fixed-order wave reduction per column
+    for (int j = 0; j < k; ++j) {
+        double v = lane < r ? Lw[k + lane + j * m] * xr : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) t[j] = v;
+    }
+    wave_sync();
+    for (int j = k - 1; j >= 0; --j) {
+        const double xj = (w[j] - t[j]) / Lw[j + j * m];
+        wave_sync();
+        if (lane == 0) w[j] = xj;
+        for (int i = lane; i < j; i += 64) t[i] += Lw[j + i * m] * xj;
+        wave_sync();
+    }
+    for (int j = lane; j < k; j += 64) a.x[c0 + j] = w[j];
+}
+
 template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
     *p = nullptr;
     if (v.empty()) return 0;
@@ -196,19 +337,22 @@ template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
 
 struct MfDevice {
     int nlevels = 0;
-    std::vector<int32_t> level_ptr;
-    std::vector<int> level_lds_factor, level_lds_fwd, level_lds_bwd;
-    int32_t *level = nullptr, *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
+    // per level: supernodes factored by one wavefront (m <= kMfWaveMaxM) and by a workgroup
+    std::vector<int32_t> wave_ptr, large_ptr;
+    std::vector<int> lds_factor_w, lds_fwd_w, lds_bwd_w, lds_factor_l, lds_fwd_l, lds_bwd_l;
+    int32_t *wave_list = nullptr, *large_list = nullptr;
+    int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
             *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
             *info = nullptr;
     int64_t *L_off = nullptr, *U_off = nullptr, *u_off = nullptr, *scratch_off = nullptr, *rmap_off = nullptr,
             *findex_off = nullptr;
     double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
 
-    MfArgs args(int lev, const double* A, double* x) const {
+    MfArgs args(bool wave, int lev, const double* A, double* x) const {
         MfArgs g;
-        g.level = level + level_ptr[lev];
-        g.count = level_ptr[lev + 1] - level_ptr[lev];
+        const std::vector<int32_t>& ptr = wave ? wave_ptr : large_ptr;
+        g.level = (wave ? wave_list : large_list) + ptr[lev];
+        g.count = ptr[lev + 1] - ptr[lev];
         g.col0 = col0; g.k = k; g.r = r; g.L_off = L_off; g.U_off = U_off; g.u_off = u_off;
         g.scratch_off = scratch_off; g.child_ptr = child_ptr; g.child = child; g.rmap_off = rmap_off; g.rmap = rmap;
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
@@ -221,26 +365,38 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
     MfDevice* d = new MfDevice();
     *out = d;
     d->nlevels = F.nlevels;
-    d->level_ptr = F.level_ptr;
     std::vector<int64_t> scr(F.nsuper, -1);
     int64_t scratch_size = 0;
     for (int s = 0; s < F.nsuper; ++s) {
         const int m = F.k[s] + F.r[s];
         if (m > kLdsCapM) { scr[s] = scratch_size; scratch_size += (int64_t)m * m; }
     }
-    d->level_lds_factor.assign(F.nlevels, 0);
-    d->level_lds_fwd.assign(F.nlevels, 0);
-    d->level_lds_bwd.assign(F.nlevels, 0);
-    for (int l = 0; l < F.nlevels; ++l)
+    const int L = F.nlevels;
+    d->lds_factor_w.assign(L, 0); d->lds_fwd_w.assign(L, 0); d->lds_bwd_w.assign(L, 0);
+    d->lds_factor_l.assign(L, 0); d->lds_fwd_l.assign(L, 0); d->lds_bwd_l.assign(L, 0);
+    d->wave_ptr.assign(L + 1, 0);
+    d->large_ptr.assign(L + 1, 0);
+    std::vector<int32_t> wl, ll;
+    for (int l = 0; l < L; ++l) {
         for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
-            const int s = F.level[q];
-            const int m = F.k[s] + F.r[s];
-            if (m <= kLdsCapM) d->level_lds_factor[l] = std::max(d->level_lds_factor[l], m * m * 8);
-            d->level_lds_fwd[l] = std::max(d->level_lds_fwd[l], m * 8);
-            d->level_lds_bwd[l] = std::max(d->level_lds_bwd[l], 2 * F.k[s] * 8);
+            const int s = F.level[q], k = F.k[s], m = k + F.r[s];
+            if (m <= kMfWaveMaxM) {
+                wl.push_back(s);
+                d->lds_factor_w[l] = std::max(d->lds_factor_w[l], m * (m + 1) / 2 * 8);
+                d->lds_fwd_w[l] = std::max(d->lds_fwd_w[l], (m + m * k) * 8);
+                d->lds_bwd_w[l] = std::max(d->lds_bwd_w[l], (2 * k + m * k) * 8);
+            } else {
+                ll.push_back(s);
+                if (m <= kLdsCapM) d->lds_factor_l[l] = std::max(d->lds_factor_l[l], m * m * 8);
+                d->lds_fwd_l[l] = std::max(d->lds_fwd_l[l], m * 8);
+                d->lds_bwd_l[l] = std::max(d->lds_bwd_l[l], 2 * k * 8);
+            }
         }
+        d->wave_ptr[l + 1] = (int32_t)wl.size();
+        d->large_ptr[l + 1] = (int32_t)ll.size();
+    }
     int rc = 0;
-    if ((rc = up(&d->level, F.level, err)) || (rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
+    if ((rc = up(&d->wave_list, wl, err)) || (rc = up(&d->large_list, ll, err)) || (rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
         (rc = up(&d->r, F.r, err)) || (rc = up(&d->child_ptr, F.child_ptr, err)) || (rc = up(&d->child, F.child, err)) ||
         (rc = up(&d->rmap, F.rmap, err)) || (rc = up(&d->amap_ptr, F.amap_ptr, err)) ||
         (rc = up(&d->amap_src, F.amap_src, err)) || (rc = up(&d->amap_dst, F.amap_dst, err)) ||
@@ -263,7 +419,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
 
 void mf_destroy(MfDevice* d) {
     if (!d) return;
-    void* bufs[] = {d->level, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
+    void* bufs[] = {d->wave_list, d->large_list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
     for (void* b : bufs)
@@ -275,9 +431,9 @@ hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s) {
     hipError_t e = hipMemsetAsync(d->info, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return e;
     for (int l = 0; l < d->nlevels; ++l) {
-        const int n = d->level_ptr[l + 1] - d->level_ptr[l];
-        if (!n) continue;
-        hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), d->level_lds_factor[l], s, d->args(l, A, nullptr));
+        const int nw = d->wave_ptr[l + 1] - d->wave_ptr[l], nl = d->large_ptr[l + 1] - d->large_ptr[l];
+        if (nw) hipLaunchKernelGGL(mf_factor_wave, dim3(nw), dim3(64), d->lds_factor_w[l], s, d->args(true, l, A, nullptr));
+        if (nl) hipLaunchKernelGGL(mf_factor_level, dim3(nl), dim3(kMfBlock), d->lds_factor_l[l], s, d->args(false, l, A, nullptr));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -286,15 +442,15 @@ hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s) {
 hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
     hipError_t e;
     for (int l = 0; l < d->nlevels; ++l) {
-        const int n = d->level_ptr[l + 1] - d->level_ptr[l];
-        if (!n) continue;
-        hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), d->level_lds_fwd[l], s, d->args(l, nullptr, x));
+        const int nw = d->wave_ptr[l + 1] - d->wave_ptr[l], nl = d->large_ptr[l + 1] - d->large_ptr[l];
+        if (nw) hipLaunchKernelGGL(mf_forward_wave, dim3(nw), dim3(64), d->lds_fwd_w[l], s, d->args(true, l, nullptr, x));
+        if (nl) hipLaunchKernelGGL(mf_forward_level, dim3(nl), dim3(kMfBlock), d->lds_fwd_l[l], s, d->args(false, l, nullptr, x));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     for (int l = d->nlevels - 1; l >= 0; --l) {
-        const int n = d->level_ptr[l + 1] - d->level_ptr[l];
-        if (!n) continue;
-        hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), d->level_lds_bwd[l], s, d->args(l, nullptr, x));
+        const int nw = d->wave_ptr[l + 1] - d->wave_ptr[l], nl = d->large_ptr[l + 1] - d->large_ptr[l];
+        if (nw) hipLaunchKernelGGL(mf_backward_wave, dim3(nw), dim3(64), d->lds_bwd_w[l], s, d->args(true, l, nullptr, x));
+        if (nl) hipLaunchKernelGGL(mf_backward_level, dim3(nl), dim3(kMfBlock), d->lds_bwd_l[l], s, d->args(false, l, nullptr, x));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;

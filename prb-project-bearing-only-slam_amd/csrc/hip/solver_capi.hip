@@ -174,7 +174,7 @@ int enqueue_linearize(bos_solver* s) {
 // off-diagonal blocks, its landmarks' diagonal blocks) and of b; broadcast each piece from its
 // owner so every rank holds the full system for the replicated solve.
 int enqueue_exchange(bos_solver* s) {
-    if (s->world <= 1) return BOS_OK;
+    if (!s->comm) return BOS_OK;
     const ncclDataType_t ty = s->precision == BOS_FP32 ? ncclFloat : ncclDouble;
     const bos::Plan& P = s->plan;
     NC_TRY(ncclGroupStart());
@@ -197,7 +197,7 @@ int enqueue_exchange(bos_solver* s) {
 int enqueue_stats(bos_solver* s) {
     HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->pose_blocks, s->d_chi, s->d_nrob,
                                           s->stream));
-    if (s->world > 1) {
+    if (s->comm) {
         NC_TRY(ncclGroupStart());
         NC_TRY(ncclAllReduce(s->d_chi, s->d_chi, 1, ncclDouble, ncclSum, s->comm, s->stream));
         NC_TRY(ncclAllReduce(s->d_nrob, s->d_nrob, 1, ncclInt32, ncclSum, s->comm, s->stream));
@@ -470,7 +470,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         if (rocsolver_set_rfinfo_mode(s->rf, rocsolver_rfinfo_mode_cholesky) != rocblas_status_success)
             return bail(fail(BOS_ERR_SOLVER, "set_rfinfo_mode"));
     }
-    if (s->world > 1) {
+    if (opt.nccl_unique_id) {   // world_size 1 with an id runs the exchange path on one GPU (tests)
         ncclUniqueId id;
         std::memcpy(&id, opt.nccl_unique_id, sizeof(id));
         ncclResult_t r = ncclCommInitRank(&s->comm, s->world, id, s->rank);

@@ -262,12 +262,20 @@ int bos_plan_mf_selftest(const bos_problem* pb, const double* vals, const double
         for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
             const int s = F.level[q], k = F.k[s], r = F.r[s], m = k + r;
             std::vector<double> W((size_t)m * m, 0.0);
-            for (int a = F.amap_ptr[s]; a < F.amap_ptr[s + 1]; ++a) W[F.amap_dst[a]] = hval[F.amap_src[a]];
+            for (int a = F.amap_ptr[s]; a < F.amap_ptr[s + 1]; ++a) {
+                int64_t d = F.amap_dst[a];
+                if (m <= bos::kMfWaveMaxM) {   // packed lower column-major -> (i, j)
+                    int64_t j = 0;
+                    while (d >= m - j) { d -= m - j; ++j; }
+                    d = (j + d) + j * m;
+                }
+                W[d] = hval[F.amap_src[a]];
+            }
             for (int ci = F.child_ptr[s]; ci < F.child_ptr[s + 1]; ++ci) {
                 const int c = F.child[ci], rc2 = F.r[c];
                 const int32_t* map = F.rmap.data() + F.rmap_off[c];
                 for (int j = 0; j < rc2; ++j)
-                    for (int i = j; i < rc2; ++i) W[map[i] + (size_t)map[j] * m] += U[F.U_off[c] + i + (size_t)j * rc2];
+                    for (int i = j; i < rc2; ++i) W[map[i] + (size_t)map[j] * m] += U[F.U_off[c] + bos::mf_packed(i, j, rc2)];
             }
             for (int j = 0; j < k; ++j) {
                 const double d = std::sqrt(std::max(W[j + (size_t)j * m], 1e-300));
@@ -279,7 +287,7 @@ int bos_plan_mf_selftest(const bos_problem* pb, const double* vals, const double
             for (int j = 0; j < k; ++j)
                 for (int i = 0; i < m; ++i) L[F.L_off[s] + i + (size_t)j * m] = W[i + (size_t)j * m];
             for (int j = 0; j < r; ++j)
-                for (int i = 0; i < r; ++i) U[F.U_off[s] + i + (size_t)j * r] = W[(k + i) + (size_t)(k + j) * m];
+                for (int i = j; i < r; ++i) U[F.U_off[s] + bos::mf_packed(i, j, r)] = W[(k + i) + (size_t)(k + j) * m];
         }
     for (int lv = 0; lv < F.nlevels; ++lv)
         for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {

@@ -738,7 +738,7 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
         const int k = F.k[s], r = F.r[s], mm = k + r;
         F.max_m = std::max(F.max_m, mm);
         F.L_off[s] = F.L_size; F.L_size += (int64_t)mm * k;
-        F.U_off[s] = F.U_size; F.U_size += (int64_t)r * r;
+        F.U_off[s] = F.U_size; F.U_size += (int64_t)r * (r + 1) / 2;
         F.u_off[s] = F.u_size; F.u_size += r;
         F.flops += (double)k * k * k / 3.0 + (double)k * k * r + (double)k * r * r;
         F.rmap_off[s] = (int64_t)F.rmap.size();
@@ -782,7 +782,8 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
             const int32_t li = front_pos(s, (int32_t)row);
             if (li < 0) { err = "multifrontal: H entry outside its front"; return BOS_ERR_INVALID; }
             tgt[e] = s;
-            dst[e] = li + (j - F.col0[s]) * (F.k[s] + F.r[s]);
+            const int fm = F.k[s] + F.r[s];
+            dst[e] = fm <= kMfWaveMaxM ? (int32_t)mf_packed(li, j - F.col0[s], fm) : li + (j - F.col0[s]) * fm;
             ++F.amap_ptr[s + 1];
         }
     for (int s = 0; s < ns; ++s) F.amap_ptr[s + 1] += F.amap_ptr[s];

@@ -85,21 +85,29 @@ struct OrderingReport {
 // Supernodal multifrontal Cholesky structure (GPU solver, hip/multifrontal.hip). Supernodes are
 // the blocks of the nested-dissection ordering (contiguous position ranges); the assembly tree
 // links each supernode to the one holding the first row of its update matrix. Fronts are dense,
-// column-major, index list = [k own dofs | r update rows].
+// index list = [k own dofs | r update rows]. Storage conventions:
+//  - fronts with m = k + r <= kMfWaveMaxM are factored by one wavefront, packed lower-triangular
+//    column-major (mf_packed); their amap_dst are packed indices. Larger fronts are full m x m
+//    column-major and their amap_dst are i + j m.
+//  - update matrices U are packed lower-triangular column-major (r (r + 1) / 2 values) for all.
+//  - L panels are m x k column-major (entries above the diagonal unused).
+constexpr int kMfWaveMaxM = 64;
+inline int64_t mf_packed(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }   // i >= j
+
 struct Multifrontal {
     int nsuper = 0, nlevels = 0, max_m = 0;
     std::vector<int32_t> col0, k, r;        // per supernode: first dof, #own dofs, #update rows
     std::vector<int64_t> findex_off;        // into findex (m = k + r entries; first k = col0..col0+k-1)
     std::vector<int32_t> findex;
     std::vector<int64_t> L_off;             // dense m x k panel (col-major) in the factor buffer
-    std::vector<int64_t> U_off;             // dense r x r update matrix (col-major)
+    std::vector<int64_t> U_off;             // packed lower r x r update matrix
     std::vector<int64_t> u_off;             // r-vector (forward solve update)
     std::vector<int32_t> parent;            // -1 for roots
     std::vector<int32_t> child_ptr, child;  // children CSR
     std::vector<int64_t> rmap_off;          // per supernode: r positions of its rows in the parent's front
     std::vector<int32_t> rmap;
     std::vector<int32_t> amap_ptr;          // per supernode: range into amap_src / amap_dst
-    std::vector<int32_t> amap_src, amap_dst;// block-array value (BlockLayout) -> column-major front position
+    std::vector<int32_t> amap_src, amap_dst;// block-array value (BlockLayout) -> front position (see above)
     std::vector<int32_t> level_ptr, level;  // supernodes grouped by tree level (leaves first)
     int64_t L_size = 0, U_size = 0, u_size = 0;
     double flops = 0;

@@ -243,3 +243,22 @@ def test_c3_step_properties(c3):
     B.step_n(3)
     pb, lb = B.get_state()
     assert np.array_equal(pa, pb) and np.array_equal(la, lb)
+
+
+def test_exchange_path_single_rank(c1):
+    """The RCCL exchange (grouped ncclBroadcast of every rank's block ranges and b ranges, and
+    the chi^2 all-reduce) run with a one-rank communicator: results equal the plain path. The
+    multi-rank partition itself is covered by tests/test_sharding.py (gloo) and the plan tests."""
+    S0 = bos.Solver(c1)
+    S1 = bos.Solver(c1, rank=0, world_size=1, nccl_id=bos.nccl_unique_id())
+    a, b = S0.linearize(), S1.linearize()
+    assert a["chi2"] == b["chi2"] and a["n_robust"] == b["n_robust"]
+    r0, c0, v0, b0 = S0.export_system()
+    r1, c1_, v1, b1 = S1.export_system()
+    assert np.array_equal(v0, v1) and np.array_equal(b0, b1)
+    for _ in range(3):
+        S0.step()
+        S1.step()
+    p0, l0 = S0.get_state()
+    p1, l1 = S1.get_state()
+    assert np.array_equal(p0, p1) and np.array_equal(l0, l1)
