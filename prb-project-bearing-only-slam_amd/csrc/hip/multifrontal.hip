@@ -4,8 +4,9 @@
 //
 // P^T H_nf P = L L^T, H read from the J+H kernel's block array through the assembly map. The
 // assembly tree is processed level by level (leaves first). Each level has two launches:
-//  * fronts with m = k + r <= kMfWaveMaxM (the many small ones near the leaves): one wavefront per
-//    front, the front packed lower-triangular in LDS, wave-level synchronisation only;
+//  * fronts with m = k + r <= kMfWaveMaxM (the many small ones near the leaves), binned by m into
+//    classes 16 / 32 / 48 / 64: one wavefront per front, assembled packed in LDS, then factored in
+//    registers (lane i holds row i; each pivot column broadcast through a 2 x MAXM LDS buffer);
 //  * larger fronts: one 256-thread workgroup, full m x m front in LDS (m <= 90) or global scratch.
 // A front is
 //   1. zeroed, then receives its entries of H (precomputed map) and the extend-add of its
@@ -34,6 +35,23 @@ constexpr int kMfBlock = 256;
 constexpr int kLdsCapM = 90;   // larger fronts up to 90 x 90 doubles (64.8 KB) are factored in LDS
 
 __device__ __forceinline__ int64_t pk(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }
+
+// Copy n doubles global -> LDS by one wavefront, 8 independent loads in flight per lane.
+__device__ __forceinline__ void stage_lds(double* dst, const double* src, int n, int lane) {
+    for (int e0 = 0; e0 < n; e0 += 512) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + 64 * u + lane;
+            v[u] = e < n ? src[e] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + 64 * u + lane;
+            if (e < n) dst[e] = v[u];
+        }
+    }
+}
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -68,6 +86,27 @@ struct MfArgs {
     double* x;                   // rhs in, solution out (permuted order)
     int32_t* info;               // count of non-positive pivots
 };
+
+// Assembly of H entries into a front by one wavefront (F[dst] = A[src]), 4 entries per lane in
+// flight: index loads, then value gathers, then LDS stores.
+__device__ __forceinline__ void assemble_wave(const MfArgs& a, int s, double* F, int lane) {
+    const int q1 = a.amap_ptr[s + 1];
+    for (int q0 = a.amap_ptr[s]; q0 < q1; q0 += 256) {
+        int src[4], dst[4];
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = q0 + 64 * u + lane;
+            src[u] = q < q1 ? a.amap_src[q] : 0;
+            dst[u] = q < q1 ? a.amap_dst[q] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = q0 + 64 * u + lane < q1 ? a.A[src[u]] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (q0 + 64 * u + lane < q1) F[dst[u]] = v[u];
+    }
+}
 
 __global__ __launch_bounds__(kMfBlock) void mf_factor_level(const MfArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -125,68 +164,6 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_level(const MfArgs a) {
     for (int j = wave; j < r; j += kMfBlock / 64) {
         double* uj = Us + pk(j, j, r) - j;
         const double* fj = F + (k + (int64_t)(k + j) * m);
-        for (int i = j + lane; i < r; i += 64) uj[i] = fj[i];
-    }
-}
-
-// One wavefront per front (m <= kMfWaveMaxM), front packed lower-triangular in LDS.
-__global__ __launch_bounds__(64) void mf_factor_wave(const MfArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double F[];
-    const int s = a.level[blockIdx.x];
-    const int k = a.k[s], r = a.r[s], m = k + r;
-    const int lane = threadIdx.x;
-    const int np = m * (m + 1) / 2;
-    for (int e = lane; e < np; e += 64) F[e] = 0.0;
-    wave_sync();
-    for (int q = a.amap_ptr[s] + lane; q < a.amap_ptr[s + 1]; q += 64) F[a.amap_dst[q]] = a.A[a.amap_src[q]];
-    wave_sync();
-    for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {   // positions of one child are distinct
-        const int c = a.child[ci];
-        const int rc = a.r[c];
-        const int32_t* map = a.rmap + a.rmap_off[c];
-        const double* Uc = a.U + a.U_off[c];
-        for (int j = 0; j < rc; ++j) {
-            const int pj = map[j];
-            const double* uj = Uc + pk(j, j, rc) - j;
-            for (int i = j + lane; i < rc; i += 64) F[pk(map[i], pj, m)] += uj[i];
-        }
-        wave_sync();
-    }
-    for (int j = 0; j < k; ++j) {
-        const int cj = (int)pk(j, j, m);   // column j: F[cj + (i - j)], i >= j
-        double d = F[cj];
-        if (!(d > 0.0)) {
-            if (lane == 0) atomicAdd(a.info, 1);
-            d = 1e-300;
-        }
-        const double ljj = sqrt(d), inv = 1.0 / ljj;
-        wave_sync();
-        if (lane == 0) F[cj] = ljj;
-        for (int i = j + 1 + lane; i < m; i += 64) F[cj + i - j] *= inv;
-        wave_sync();
-        // trailing triangle (columns j+1.., rows >= column) is contiguous in packed storage:
-        // lanes take every 64th entry, decoding (row, column) incrementally
-        int l = j + 1, len = m - l, o = lane;
-        while (len > 0 && o >= len) { o -= len; ++l; --len; }
-        int p = (int)pk(l, l, m) + o;
-        while (len > 0) {
-            F[p] -= F[cj + (l + o) - j] * F[cj + l - j];
-            o += 64;
-            p += 64;
-            while (len > 0 && o >= len) { o -= len; ++l; --len; }
-        }
-        wave_sync();
-    }
-    double* Ls = a.L + a.L_off[s];
-    for (int j = 0; j < k; ++j) {
-        const double* fj = F + pk(j, j, m) - j;
-        double* lj = Ls + (int64_t)j * m;
-        for (int i = j + lane; i < m; i += 64) lj[i] = fj[i];
-    }
-    double* Us = a.U + a.U_off[s];
-    for (int j = 0; j < r; ++j) {
-        const double* fj = F + pk(k + j, k + j, m) - j;
-        double* uj = Us + pk(j, j, r) - j;
         for (int i = j + lane; i < r; i += 64) uj[i] = fj[i];
     }
 }
@@ -255,6 +232,87 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
     for (int j = tid; j < k; j += kMfBlock) a.x[c0 + j] = w[j];
 }
 
+// One wavefront per front with m <= MAXM, the factorization in registers: lane i holds row i of
+// the (lower) front in a compile-time-indexed array; each column step broadcasts the pivot column
+// through a small LDS buffer (one store per lane, broadcast reads). LDS otherwise only stages the
+// assembly.
+template <int MAXM>
+__global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
+    __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
+    __shared__ int smap[kMfWaveMaxM];
+    const int s = a.level[blockIdx.x];
+    const int k = a.k[s], r = a.r[s], m = k + r;
+    const int lane = threadIdx.x;
+    const int np = m * (m + 1) / 2;
+    for (int e = lane; e < np; e += 64) F[e] = 0.0;
+    wave_sync();
+    assemble_wave(a, s, F, lane);
+    wave_sync();
+    // extend-add: the child's row map staged in LDS, its packed update matrix swept by all lanes
+    // (contiguous loads, 4 in flight; (row, column) decoded incrementally). Positions of one
+    // child are distinct.
+    for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {
+        const int c = a.child[ci];
+        const int rc = a.r[c];   // rc < m <= MAXM
+        if (lane < rc) smap[lane] = a.rmap[a.rmap_off[c] + lane];
+        const double* Uc = a.U + a.U_off[c];
+        wave_sync();
+        const int ne = rc * (rc + 1) / 2;
+        int j = 0, len = rc, o = lane;
+        while (len > 0 && o >= len) { o -= len; ++j; --len; }
+        for (int e0 = 0; e0 < ne; e0 += 256) {
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = e0 + 64 * u + lane < ne ? Uc[e0 + 64 * u + lane] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (len > 0) {
+                    F[pk(smap[j + o], smap[j], m)] += v[u];
+                    o += 64;
+                    while (len > 0 && o >= len) { o -= len; ++j; --len; }
+                }
+            }
+        }
+        wave_sync();
+    }
+    const bool live = lane < m;
+    double row[MAXM];
+#pragma unroll
+    for (int c = 0; c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk(lane, c, m)] : 0.0;
+    // Right-looking: step j broadcasts column j through a double-buffered LDS column (one store
+    // per lane, same-address reads). Entries above the diagonal (c > lane) and rows >= m are
+    // scratch, so the updates need no predicates.
+    __shared__ __attribute__((aligned(16))) double colbuf[2][MAXM];
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) {
+        if (j < k) {
+            double* col = colbuf[j & 1];
+            if (lane < MAXM) col[lane] = row[j];
+            wave_sync();
+            double d = col[j];
+            if (!(d > 0.0)) {
+                if (lane == 0) atomicAdd(a.info, 1);
+                d = 1e-300;
+            }
+            const double ljj = sqrt(d), inv = 1.0 / ljj;
+            const double lij = lane == j ? ljj : row[j] * inv;   // L[i, j]
+            row[j] = lij;
+            const double g = lij * inv;                          // L[i, j] / L[j, j]
+#pragma unroll
+            for (int l = j + 1; l < MAXM; ++l) row[l] = fma(-g, col[l], row[l]);   // -= L[i,j] L[l,j]
+        }
+    }
+    double* Ls = a.L + a.L_off[s];
+    double* Us = a.U + a.U_off[s];
+#pragma unroll
+    for (int c = 0; c < MAXM; ++c) {
+        if (live && c <= lane) {
+            if (c < k) Ls[lane + (int64_t)c * m] = row[c];
+            else Us[pk(lane - k, c - k, r)] = row[c];
+        }
+    }
+}
+
 // forward substitution, one wavefront per front (m <= kMfWaveMaxM); LDS: w[m] | L panel (lower, m x k)
 __global__ __launch_bounds__(64) void mf_forward_wave(const MfArgs a) {
     extern __shared__ __attribute__((aligned(16))) double w[];
@@ -263,8 +321,7 @@ __global__ __launch_bounds__(64) void mf_forward_wave(const MfArgs a) {
     const int lane = threadIdx.x;
     const int c0 = a.col0[s];
     double* Lw = w + m;
-    const double* Ls = a.L + a.L_off[s];
-    for (int e = lane; e < m * k; e += 64) Lw[e] = Ls[e];
+    stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
     for (int i = lane; i < m; i += 64) w[i] = i < k ? a.x[c0 + i] : 0.0;
     wave_sync();
     for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {
@@ -299,7 +356,7 @@ __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
     const int32_t* fi = a.findex + a.findex_off[s];
     double* t = w + k;
     double* Lw = w + 2 * k;
-    for (int e = lane; e < m * k; e += 64) Lw[e] = Ls[e];
+    stage_lds(Lw, Ls, m * k, lane);
     // the rows below the supernode are ancestors' dofs, final in x: xr in the lane of the row
     const double xr = lane < r ? a.x[fi[k + lane]] : 0.0;
     for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
@@ -335,12 +392,16 @@ template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
 
 }  // namespace
 
+// front size classes: m <= 16, 32, 48, 64 (one wavefront, registers / LDS) and larger (workgroup)
+constexpr int kClasses = 5;
+inline int front_class(int m) { return m <= kMfWaveMaxM ? (m - 1) / 16 : 4; }
+
 struct MfDevice {
     int nlevels = 0;
-    // per level: supernodes factored by one wavefront (m <= kMfWaveMaxM) and by a workgroup
-    std::vector<int32_t> wave_ptr, large_ptr;
-    std::vector<int> lds_factor_w, lds_fwd_w, lds_bwd_w, lds_factor_l, lds_fwd_l, lds_bwd_l;
-    int32_t *wave_list = nullptr, *large_list = nullptr;
+    // supernodes of (level l, class c) = list[ptr[l * kClasses + c], ptr[l * kClasses + c + 1])
+    std::vector<int32_t> ptr;
+    std::vector<int> lds_factor, lds_fwd, lds_bwd;   // per (level, class): dynamic LDS bytes
+    int32_t* list = nullptr;
     int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
             *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
             *info = nullptr;
@@ -348,11 +409,11 @@ struct MfDevice {
             *findex_off = nullptr;
     double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
 
-    MfArgs args(bool wave, int lev, const double* A, double* x) const {
+    int count(int lev, int c) const { return ptr[lev * kClasses + c + 1] - ptr[lev * kClasses + c]; }
+    MfArgs args(int lev, int c, const double* A, double* x) const {
         MfArgs g;
-        const std::vector<int32_t>& ptr = wave ? wave_ptr : large_ptr;
-        g.level = (wave ? wave_list : large_list) + ptr[lev];
-        g.count = ptr[lev + 1] - ptr[lev];
+        g.level = list + ptr[lev * kClasses + c];
+        g.count = count(lev, c);
         g.col0 = col0; g.k = k; g.r = r; g.L_off = L_off; g.U_off = U_off; g.u_off = u_off;
         g.scratch_off = scratch_off; g.child_ptr = child_ptr; g.child = child; g.rmap_off = rmap_off; g.rmap = rmap;
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
@@ -372,31 +433,29 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         if (m > kLdsCapM) { scr[s] = scratch_size; scratch_size += (int64_t)m * m; }
     }
     const int L = F.nlevels;
-    d->lds_factor_w.assign(L, 0); d->lds_fwd_w.assign(L, 0); d->lds_bwd_w.assign(L, 0);
-    d->lds_factor_l.assign(L, 0); d->lds_fwd_l.assign(L, 0); d->lds_bwd_l.assign(L, 0);
-    d->wave_ptr.assign(L + 1, 0);
-    d->large_ptr.assign(L + 1, 0);
-    std::vector<int32_t> wl, ll;
-    for (int l = 0; l < L; ++l) {
-        for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
-            const int s = F.level[q], k = F.k[s], m = k + F.r[s];
-            if (m <= kMfWaveMaxM) {
-                wl.push_back(s);
-                d->lds_factor_w[l] = std::max(d->lds_factor_w[l], m * (m + 1) / 2 * 8);
-                d->lds_fwd_w[l] = std::max(d->lds_fwd_w[l], (m + m * k) * 8);
-                d->lds_bwd_w[l] = std::max(d->lds_bwd_w[l], (2 * k + m * k) * 8);
-            } else {
-                ll.push_back(s);
-                if (m <= kLdsCapM) d->lds_factor_l[l] = std::max(d->lds_factor_l[l], m * m * 8);
-                d->lds_fwd_l[l] = std::max(d->lds_fwd_l[l], m * 8);
-                d->lds_bwd_l[l] = std::max(d->lds_bwd_l[l], 2 * k * 8);
+    d->lds_factor.assign(L * kClasses, 0); d->lds_fwd.assign(L * kClasses, 0); d->lds_bwd.assign(L * kClasses, 0);
+    d->ptr.assign(L * kClasses + 1, 0);
+    std::vector<int32_t> lst;
+    for (int l = 0; l < L; ++l)
+        for (int c = 0; c < kClasses; ++c) {
+            const int lc = l * kClasses + c;
+            for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
+                const int s = F.level[q], k = F.k[s], m = k + F.r[s];
+                if (front_class(m) != c) continue;
+                lst.push_back(s);
+                if (c < 4) {
+                    d->lds_fwd[lc] = std::max(d->lds_fwd[lc], (m + m * k) * 8);
+                    d->lds_bwd[lc] = std::max(d->lds_bwd[lc], (2 * k + m * k) * 8);
+                } else {
+                    if (m <= kLdsCapM) d->lds_factor[lc] = std::max(d->lds_factor[lc], m * m * 8);
+                    d->lds_fwd[lc] = std::max(d->lds_fwd[lc], m * 8);
+                    d->lds_bwd[lc] = std::max(d->lds_bwd[lc], 2 * k * 8);
+                }
             }
+            d->ptr[lc + 1] = (int32_t)lst.size();
         }
-        d->wave_ptr[l + 1] = (int32_t)wl.size();
-        d->large_ptr[l + 1] = (int32_t)ll.size();
-    }
     int rc = 0;
-    if ((rc = up(&d->wave_list, wl, err)) || (rc = up(&d->large_list, ll, err)) || (rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
+    if ((rc = up(&d->list, lst, err)) || (rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
         (rc = up(&d->r, F.r, err)) || (rc = up(&d->child_ptr, F.child_ptr, err)) || (rc = up(&d->child, F.child, err)) ||
         (rc = up(&d->rmap, F.rmap, err)) || (rc = up(&d->amap_ptr, F.amap_ptr, err)) ||
         (rc = up(&d->amap_src, F.amap_src, err)) || (rc = up(&d->amap_dst, F.amap_dst, err)) ||
@@ -419,7 +478,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
 
 void mf_destroy(MfDevice* d) {
     if (!d) return;
-    void* bufs[] = {d->wave_list, d->large_list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
+    void* bufs[] = {d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
     for (void* b : bufs)
@@ -431,9 +490,14 @@ hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s) {
     hipError_t e = hipMemsetAsync(d->info, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return e;
     for (int l = 0; l < d->nlevels; ++l) {
-        const int nw = d->wave_ptr[l + 1] - d->wave_ptr[l], nl = d->large_ptr[l + 1] - d->large_ptr[l];
-        if (nw) hipLaunchKernelGGL(mf_factor_wave, dim3(nw), dim3(64), d->lds_factor_w[l], s, d->args(true, l, A, nullptr));
-        if (nl) hipLaunchKernelGGL(mf_factor_level, dim3(nl), dim3(kMfBlock), d->lds_factor_l[l], s, d->args(false, l, A, nullptr));
+        int n;
+        if ((n = d->count(l, 0))) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(l, 0, A, nullptr));
+        if ((n = d->count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(l, 1, A, nullptr));
+        if ((n = d->count(l, 2))) hipLaunchKernelGGL(mf_factor_reg<48>, dim3(n), dim3(64), 0, s, d->args(l, 2, A, nullptr));
+        if ((n = d->count(l, 3))) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(l, 3, A, nullptr));
+        if ((n = d->count(l, 4)))
+            hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), d->lds_factor[l * kClasses + 4], s,
+                               d->args(l, 4, A, nullptr));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -441,18 +505,22 @@ hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s) {
 
 hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
     hipError_t e;
-    for (int l = 0; l < d->nlevels; ++l) {
-        const int nw = d->wave_ptr[l + 1] - d->wave_ptr[l], nl = d->large_ptr[l + 1] - d->large_ptr[l];
-        if (nw) hipLaunchKernelGGL(mf_forward_wave, dim3(nw), dim3(64), d->lds_fwd_w[l], s, d->args(true, l, nullptr, x));
-        if (nl) hipLaunchKernelGGL(mf_forward_level, dim3(nl), dim3(kMfBlock), d->lds_fwd_l[l], s, d->args(false, l, nullptr, x));
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    for (int l = d->nlevels - 1; l >= 0; --l) {
-        const int nw = d->wave_ptr[l + 1] - d->wave_ptr[l], nl = d->large_ptr[l + 1] - d->large_ptr[l];
-        if (nw) hipLaunchKernelGGL(mf_backward_wave, dim3(nw), dim3(64), d->lds_bwd_w[l], s, d->args(true, l, nullptr, x));
-        if (nl) hipLaunchKernelGGL(mf_backward_level, dim3(nl), dim3(kMfBlock), d->lds_bwd_l[l], s, d->args(false, l, nullptr, x));
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    for (int l = 0; l < d->nlevels; ++l)
+        for (int c = 0; c < kClasses; ++c) {
+            const int n = d->count(l, c);
+            if (!n) continue;
+            if (c < 4) hipLaunchKernelGGL(mf_forward_wave, dim3(n), dim3(64), d->lds_fwd[l * kClasses + c], s, d->args(l, c, nullptr, x));
+            else hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), d->lds_fwd[l * kClasses + c], s, d->args(l, c, nullptr, x));
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+    for (int l = d->nlevels - 1; l >= 0; --l)
+        for (int c = 0; c < kClasses; ++c) {
+            const int n = d->count(l, c);
+            if (!n) continue;
+            if (c < 4) hipLaunchKernelGGL(mf_backward_wave, dim3(n), dim3(64), d->lds_bwd[l * kClasses + c], s, d->args(l, c, nullptr, x));
+            else hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), d->lds_bwd[l * kClasses + c], s, d->args(l, c, nullptr, x));
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
     return hipSuccess;
 }
 

@@ -758,6 +758,7 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
     }
     F.rmap_off[ns] = (int64_t)F.rmap.size();
     F.nlevels = 0;
+    const bool stats = std::getenv("BOS_MF_STATS") != nullptr;   // diagnostics: per-level front sizes
     for (int s = 0; s < ns; ++s) F.nlevels = std::max(F.nlevels, lev[s] + 1);
     F.level_ptr.assign(F.nlevels + 1, 0);
     for (int s = 0; s < ns; ++s) ++F.level_ptr[lev[s] + 1];
@@ -767,6 +768,25 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
         std::vector<int32_t> w(F.level_ptr.begin(), F.level_ptr.end() - 1);
         for (int s = 0; s < ns; ++s) F.level[w[lev[s]]++] = s;
     }
+    if (stats)
+        for (int l = 0; l < F.nlevels; ++l) {
+            double sk = 0, sr = 0, fl = 0;
+            int mk = 0, mr = 0, mm = 0, n = F.level_ptr[l + 1] - F.level_ptr[l];
+            for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
+                const int s = F.level[q];
+                sk += F.k[s]; sr += F.r[s];
+                mk = std::max(mk, F.k[s]); mr = std::max(mr, F.r[s]); mm = std::max(mm, F.k[s] + F.r[s]);
+                fl += (double)F.k[s] * F.k[s] * F.k[s] / 3 + (double)F.k[s] * F.k[s] * F.r[s] + (double)F.k[s] * F.r[s] * F.r[s];
+            }
+            int h[4] = {0, 0, 0, 0};   // m <= 16, 32, 48, 64
+            for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
+                const int m = F.k[F.level[q]] + F.r[F.level[q]];
+                if (m <= 64) ++h[(m - 1) / 16];
+            }
+            std::fprintf(stderr, "mf level %2d: %6d fronts, k mean %5.1f max %3d, r mean %5.1f max %3d, m max %3d, "
+                         "m<=16/32/48/64: %d %d %d %d, flops %.3g\n", l, n, sk / n, mk, sr / n, mr, mm, h[0], h[1], h[2],
+                         h[3], fl);
+        }
     // assembly map: every stored entry of H (row i >= col j) goes to the front of col j's supernode,
     // read from its block value
     std::vector<int32_t> sn_of_dof(P.n);
