@@ -409,7 +409,14 @@ struct MfDevice {
             *findex_off = nullptr;
     double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
 
-    int count(int lev, int c) const { return ptr[lev * kClasses + c + 1] - ptr[lev * kClasses + c]; }
+    // classes [c0, c1) of level lev are contiguous in the list
+    int count(int lev, int c0, int c1) const { return ptr[lev * kClasses + c1] - ptr[lev * kClasses + c0]; }
+    int count(int lev, int c) const { return count(lev, c, c + 1); }
+    int lds_max(const std::vector<int>& v, int lev, int c0, int c1) const {
+        int b = 0;
+        for (int c = c0; c < c1; ++c) b = std::max(b, v[lev * kClasses + c]);
+        return b;
+    }
     MfArgs args(int lev, int c, const double* A, double* x) const {
         MfArgs g;
         g.level = list + ptr[lev * kClasses + c];
@@ -505,22 +512,23 @@ hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s) {
 
 hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
     hipError_t e;
-    for (int l = 0; l < d->nlevels; ++l)
-        for (int c = 0; c < kClasses; ++c) {
-            const int n = d->count(l, c);
-            if (!n) continue;
-            if (c < 4) hipLaunchKernelGGL(mf_forward_wave, dim3(n), dim3(64), d->lds_fwd[l * kClasses + c], s, d->args(l, c, nullptr, x));
-            else hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), d->lds_fwd[l * kClasses + c], s, d->args(l, c, nullptr, x));
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
-    for (int l = d->nlevels - 1; l >= 0; --l)
-        for (int c = 0; c < kClasses; ++c) {
-            const int n = d->count(l, c);
-            if (!n) continue;
-            if (c < 4) hipLaunchKernelGGL(mf_backward_wave, dim3(n), dim3(64), d->lds_bwd[l * kClasses + c], s, d->args(l, c, nullptr, x));
-            else hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), d->lds_bwd[l * kClasses + c], s, d->args(l, c, nullptr, x));
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
+    // the solve kernels do not depend on the size class: one wave launch per level for classes 0-3
+    for (int l = 0; l < d->nlevels; ++l) {
+        int n;
+        if ((n = d->count(l, 0, 4)))
+            hipLaunchKernelGGL(mf_forward_wave, dim3(n), dim3(64), d->lds_max(d->lds_fwd, l, 0, 4), s, d->args(l, 0, nullptr, x));
+        if ((n = d->count(l, 4)))
+            hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), d->lds_fwd[l * kClasses + 4], s, d->args(l, 4, nullptr, x));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    for (int l = d->nlevels - 1; l >= 0; --l) {
+        int n;
+        if ((n = d->count(l, 0, 4)))
+            hipLaunchKernelGGL(mf_backward_wave, dim3(n), dim3(64), d->lds_max(d->lds_bwd, l, 0, 4), s, d->args(l, 0, nullptr, x));
+        if ((n = d->count(l, 4)))
+            hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), d->lds_bwd[l * kClasses + 4], s, d->args(l, 4, nullptr, x));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 
