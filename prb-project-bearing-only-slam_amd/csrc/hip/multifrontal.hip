@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -57,6 +58,18 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Hand-off data between fronts processed in one dataflow launch (update matrices, forward
+// u-vectors, backward x rows) is written and read with relaxed agent-scope atomics (coherent sc1
+// accesses) so no L2-wide release/acquire fence is needed per front; COH = false is plain access.
+template <bool COH> __device__ __forceinline__ double ldc(const double* p) {
+    if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool COH> __device__ __forceinline__ void stc(double* p, double v) {
+    if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
 }
 
 struct MfArgs {
@@ -235,14 +248,11 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
 // One wavefront per front with m <= MAXM, the factorization in registers: lane i holds row i of
 // the (lower) front in a compile-time-indexed array; each column step broadcasts the pivot column
 // through a small LDS buffer (one store per lane, broadcast reads). LDS otherwise only stages the
-// assembly.
-template <int MAXM>
-__global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
-    __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
-    __shared__ int smap[kMfWaveMaxM];
-    const int s = a.level[blockIdx.x];
+// assembly. F: packed front (MAXM (MAXM + 1) / 2), colbuf: 2 MAXM, smap: 64 ints.
+template <int MAXM, bool COH>
+__device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf, int* smap,
+                                                 int lane) {
     const int k = a.k[s], r = a.r[s], m = k + r;
-    const int lane = threadIdx.x;
     const int np = m * (m + 1) / 2;
     for (int e = lane; e < np; e += 64) F[e] = 0.0;
     wave_sync();
@@ -263,7 +273,7 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
         for (int e0 = 0; e0 < ne; e0 += 256) {
             double v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = e0 + 64 * u + lane < ne ? Uc[e0 + 64 * u + lane] : 0.0;
+            for (int u = 0; u < 4; ++u) v[u] = e0 + 64 * u + lane < ne ? ldc<COH>(Uc + e0 + 64 * u + lane) : 0.0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 if (len > 0) {
@@ -282,11 +292,10 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
     // Right-looking: step j broadcasts column j through a double-buffered LDS column (one store
     // per lane, same-address reads). Entries above the diagonal (c > lane) and rows >= m are
     // scratch, so the updates need no predicates.
-    __shared__ __attribute__((aligned(16))) double colbuf[2][MAXM];
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
         if (j < k) {
-            double* col = colbuf[j & 1];
+            double* col = colbuf + (j & 1) * MAXM;
             if (lane < MAXM) col[lane] = row[j];
             wave_sync();
             double d = col[j];
@@ -308,17 +317,23 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
     for (int c = 0; c < MAXM; ++c) {
         if (live && c <= lane) {
             if (c < k) Ls[lane + (int64_t)c * m] = row[c];
-            else Us[pk(lane - k, c - k, r)] = row[c];
+            else stc<COH>(Us + pk(lane - k, c - k, r), row[c]);
         }
     }
+    wave_sync();
 }
 
-// forward substitution, one wavefront per front (m <= kMfWaveMaxM); LDS: w[m] | L panel (lower, m x k)
-__global__ __launch_bounds__(64) void mf_forward_wave(const MfArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double w[];
-    const int s = a.level[blockIdx.x];
+template <int MAXM>
+__global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
+    __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * MAXM];
+    __shared__ int smap[64];
+    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, smap, threadIdx.x);
+}
+
+// Forward substitution of one front by one wavefront (any m); LDS: w[m] | L panel (m x k).
+template <bool COH> __device__ __forceinline__ void forward_front(const MfArgs& a, int s, double* w, int lane) {
     const int k = a.k[s], r = a.r[s], m = k + r;
-    const int lane = threadIdx.x;
     const int c0 = a.col0[s];
     double* Lw = w + m;
     stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
@@ -329,7 +344,7 @@ __global__ __launch_bounds__(64) void mf_forward_wave(const MfArgs a) {
         const int rc = a.r[c];
         const int32_t* map = a.rmap + a.rmap_off[c];
         const double* uc = a.u + a.u_off[c];
-        for (int t = lane; t < rc; t += 64) w[map[t]] += uc[t];
+        for (int t = lane; t < rc; t += 64) w[map[t]] += ldc<COH>(uc + t);
         wave_sync();
     }
     for (int j = 0; j < k; ++j) {
@@ -341,29 +356,28 @@ __global__ __launch_bounds__(64) void mf_forward_wave(const MfArgs a) {
     }
     for (int i = lane; i < m; i += 64) {
         if (i < k) a.x[c0 + i] = w[i];
-        else a.u[a.u_off[s] + (i - k)] = w[i];
+        else stc<COH>(a.u + a.u_off[s] + (i - k), w[i]);
     }
+    wave_sync();
 }
 
-// backward substitution, one wavefront per front; LDS: x_own[k] | t[k] | L panel (m x k)
-__global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double w[];
-    const int s = a.level[blockIdx.x];
+// Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
+// L panel (m x k). The rows below the supernode are ancestors' dofs, already final in x.
+template <bool COH> __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w, int lane) {
     const int k = a.k[s], r = a.r[s], m = k + r;
-    const int lane = threadIdx.x;
     const int c0 = a.col0[s];
-    const double* Ls = a.L + a.L_off[s];
     const int32_t* fi = a.findex + a.findex_off[s];
     double* t = w + k;
-    double* Lw = w + 2 * k;
-    stage_lds(Lw, Ls, m * k, lane);
-    // the rows below the supernode are ancestors' dofs, final in x: xr in the lane of the row
-    const double xr = lane < r ? a.x[fi[k + lane]] : 0.0;
+    double* xs = w + 2 * k;
+    double* Lw = w + 2 * k + r;
+    stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
+    for (int i = lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
     wave_sync();
     // t_j = sum_i L[k + i, j] x[fi[k + i]]: fixed-order wave reduction per column
     for (int j = 0; j < k; ++j) {
-        double v = lane < r ? Lw[k + lane + j * m] * xr : 0.0;
+        double v = 0.0;
+        for (int i = lane; i < r; i += 64) v += Lw[k + i + j * m] * xs[i];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         if (lane == 0) t[j] = v;
@@ -376,7 +390,112 @@ __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
         for (int i = lane; i < j; i += 64) t[i] += Lw[j + i * m] * xj;
         wave_sync();
     }
-    for (int j = lane; j < k; j += 64) a.x[c0 + j] = w[j];
+    for (int j = lane; j < k; j += 64) stc<COH>(a.x + c0 + j, w[j]);
+    wave_sync();
+}
+
+__global__ __launch_bounds__(64) void mf_forward_wave(const MfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double w[];
+    forward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x);
+}
+
+__global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double w[];
+    backward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x);
+}
+
+// ---- dataflow (work-queue) kernels: one launch walks a whole tree range. A wavefront takes the
+// next front from an atomic ticket (fronts listed in topological order), waits for the fronts it
+// depends on (children bottom-up, the parent top-down) through per-supernode completion flags,
+// processes the front and publishes its flag. Hand-off data goes through coherent (sc1) accesses
+// (ldc / stc), drained by s_waitcnt before the flag store: no L2 writeback / invalidate per front.
+// A wave only ever waits for tickets already taken by running waves, so any grid size is
+// deadlock-free; every wait is bounded (a stall is reported through info, never a hang).
+struct Flow {
+    const int32_t* order;   // fronts in processing order
+    int n;
+    int* ticket;            // zeroed before the launch
+    uint32_t* done;         // per supernode: epoch of its last completion
+    uint32_t epoch;
+    const int32_t* slev;    // level of every supernode
+    int lev0;               // factor: children below this level were finished by earlier launches
+};
+
+constexpr int kStall = 1 << 20;   // added to info when a dependency wait times out
+
+__device__ __forceinline__ int next_ticket(int* ticket) {
+    int t = 0;
+    if (threadIdx.x == 0) t = atomicAdd(ticket, 1);
+    return __builtin_amdgcn_readfirstlane(t);
+}
+
+__device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
+    if (threadIdx.x == 0) {
+        int it = 0;
+        while (__hip_atomic_load(f.done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != f.epoch) {
+            if (++it > (1 << 22)) {
+                atomicAdd(info, kStall);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+}
+
+__device__ __forceinline__ void publish_done(const Flow& f, int s) {
+    // drain this wave's sc1 stores before the flag (a workgroup-scope fence emits no vmcnt wait)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64) void mf_factor_flow(const MfArgs a, const Flow f) {
+    __shared__ __attribute__((aligned(16))) double F[kMfWaveMaxM * (kMfWaveMaxM + 1) / 2];
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * kMfWaveMaxM];
+    __shared__ int smap[64];
+    const int lane = threadIdx.x;
+    // a wave takes at most n + 1 tickets: the loop is bounded (an unbounded for (;;) version of
+    // this kernel never terminated on gfx950 / ROCm 7.2)
+    for (int it = 0; it <= f.n; ++it) {
+        const int t = next_ticket(f.ticket);
+        if (t >= f.n) break;
+        const int s = f.order[t];
+        for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci)
+            if (f.slev[a.child[ci]] >= f.lev0) wait_done(f, a.child[ci], a.info);
+        const int m = a.k[s] + a.r[s];   // <= kMfWaveMaxM for every front of the flow range
+        if (m <= 16) factor_front_reg<16, true>(a, s, F, colbuf, smap, lane);
+        else if (m <= 32) factor_front_reg<32, true>(a, s, F, colbuf, smap, lane);
+        else if (m <= 48) factor_front_reg<48, true>(a, s, F, colbuf, smap, lane);
+        else factor_front_reg<64, true>(a, s, F, colbuf, smap, lane);
+        publish_done(f, s);
+    }
+}
+
+__global__ __launch_bounds__(64) void mf_forward_flow(const MfArgs a, const Flow f) {
+    extern __shared__ __attribute__((aligned(16))) double w[];
+    for (int it = 0; it <= f.n; ++it) {
+        const int t = next_ticket(f.ticket);
+        if (t >= f.n) break;
+        const int s = f.order[t];
+        for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci)
+            if (f.slev[a.child[ci]] >= f.lev0) wait_done(f, a.child[ci], a.info);
+        forward_front<true>(a, s, w, threadIdx.x);
+        publish_done(f, s);
+    }
+}
+
+__global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flow f, const int32_t* parent) {
+    extern __shared__ __attribute__((aligned(16))) double w[];
+    for (int it = 0; it <= f.n; ++it) {
+        const int t = next_ticket(f.ticket);
+        if (t >= f.n) break;
+        const int s = f.order[t];
+        if (parent[s] >= 0) wait_done(f, parent[s], a.info);
+        backward_front<true>(a, s, w, threadIdx.x);
+        publish_done(f, s);
+    }
 }
 
 template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
@@ -402,6 +521,16 @@ struct MfDevice {
     std::vector<int32_t> ptr;
     std::vector<int> lds_factor, lds_fwd, lds_bwd;   // per (level, class): dynamic LDS bytes
     int32_t* list = nullptr;
+    // dataflow launches: the factorization of levels >= flow_lev0 (all fronts there <= 64) and both
+    // solves over the whole tree (when their LDS fits), each as one work-queue launch
+    int flow_lev0 = 0, n_flow_factor = 0, nsuper = 0, ncu = 256;
+    bool flow_solve = false;
+    int solve_lev0 = 0, n_flow_solve = 0;   // solves: levels < solve_lev0 per level, the rest one flow each
+    int lds_fwd_flow = 0, lds_bwd_flow = 0;
+    int32_t *order_factor = nullptr, *order_fwd = nullptr, *order_bwd = nullptr, *slev = nullptr, *parent = nullptr;
+    uint32_t* done = nullptr;   // [3][nsuper]: factor, forward, backward
+    int* tickets = nullptr;     // [3]
+    uint32_t epoch = 0;
     int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
             *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
             *info = nullptr;
@@ -452,7 +581,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
                 lst.push_back(s);
                 if (c < 4) {
                     d->lds_fwd[lc] = std::max(d->lds_fwd[lc], (m + m * k) * 8);
-                    d->lds_bwd[lc] = std::max(d->lds_bwd[lc], (2 * k + m * k) * 8);
+                    d->lds_bwd[lc] = std::max(d->lds_bwd[lc], (2 * k + (m - k) + m * k) * 8);
                 } else {
                     if (m <= kLdsCapM) d->lds_factor[lc] = std::max(d->lds_factor[lc], m * m * 8);
                     d->lds_fwd[lc] = std::max(d->lds_fwd[lc], m * 8);
@@ -461,7 +590,53 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
             }
             d->ptr[lc + 1] = (int32_t)lst.size();
         }
+    // dataflow set-up
+    d->nsuper = F.nsuper;
+    {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+            d->ncu = ncu;
+    }
+    std::vector<int32_t> slev(F.nsuper, 0), ofac, ofwd, obwd;
+    for (int l = 0; l < L; ++l)
+        for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) slev[F.level[q]] = l;
+    d->flow_lev0 = L;   // lowest level from which every front is <= kMfWaveMaxM (and >= 2)
+    while (d->flow_lev0 > 2) {
+        bool small = true;
+        for (int q = F.level_ptr[d->flow_lev0 - 1]; q < F.level_ptr[d->flow_lev0] && small; ++q)
+            small = F.k[F.level[q]] + F.r[F.level[q]] <= kMfWaveMaxM;
+        if (!small) break;
+        --d->flow_lev0;
+    }
+    for (int q = F.level_ptr[d->flow_lev0]; q < F.level_ptr[L]; ++q) ofac.push_back(F.level[q]);
+    d->n_flow_factor = (int)ofac.size();
+    // solves: the two lowest levels (many independent fronts) stay per-level launches
+    d->solve_lev0 = std::min(2, L);
+    for (int q = F.level_ptr[d->solve_lev0]; q < F.level_ptr[L]; ++q) {
+        const int s = F.level[q], k = F.k[s], m = k + F.r[s];
+        ofwd.push_back(s);
+        d->lds_fwd_flow = std::max(d->lds_fwd_flow, (m + m * k) * 8);
+        d->lds_bwd_flow = std::max(d->lds_bwd_flow, (2 * k + (m - k) + m * k) * 8);
+    }
+    obwd.assign(ofwd.rbegin(), ofwd.rend());
+    d->n_flow_solve = (int)ofwd.size();
+    d->flow_solve = d->n_flow_solve > 0 && d->lds_fwd_flow <= 48 * 1024 && d->lds_bwd_flow <= 48 * 1024;
+    if (!d->flow_solve) d->solve_lev0 = L;
+    if (const char* e = std::getenv("BOS_MF_FLOW")) {   // diagnostics: bit 0 factor flow, bit 1 solve flows
+        const int v = std::atoi(e);
+        if (!(v & 1)) { d->flow_lev0 = L; ofac.clear(); d->n_flow_factor = 0; }
+        if (!(v & 2)) { d->flow_solve = false; d->solve_lev0 = L; }
+    }
     int rc = 0;
+    if ((rc = up(&d->order_factor, ofac, err)) || (rc = up(&d->order_fwd, ofwd, err)) || (rc = up(&d->order_bwd, obwd, err)) ||
+        (rc = up(&d->slev, slev, err)) || (rc = up(&d->parent, F.parent, err)))
+        return rc;
+    if (hipMalloc((void**)&d->done, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(d->done, 0, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void**)&d->tickets, 3 * sizeof(int)) != hipSuccess) {
+        err = "hipMalloc failed (multifrontal flow)";
+        return -2;
+    }
     if ((rc = up(&d->list, lst, err)) || (rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
         (rc = up(&d->r, F.r, err)) || (rc = up(&d->child_ptr, F.child_ptr, err)) || (rc = up(&d->child, F.child, err)) ||
         (rc = up(&d->rmap, F.rmap, err)) || (rc = up(&d->amap_ptr, F.amap_ptr, err)) ||
@@ -485,7 +660,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
 
 void mf_destroy(MfDevice* d) {
     if (!d) return;
-    void* bufs[] = {d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
+    void* bufs[] = {d->order_factor, d->order_fwd, d->order_bwd, d->slev, d->parent, d->done, d->tickets, d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
     for (void* b : bufs)
@@ -496,7 +671,8 @@ void mf_destroy(MfDevice* d) {
 hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s) {
     hipError_t e = hipMemsetAsync(d->info, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return e;
-    for (int l = 0; l < d->nlevels; ++l) {
+    const uint32_t epoch = ++d->epoch;
+    for (int l = 0; l < d->flow_lev0; ++l) {
         int n;
         if ((n = d->count(l, 0))) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(l, 0, A, nullptr));
         if ((n = d->count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(l, 1, A, nullptr));
@@ -507,13 +683,24 @@ hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s) {
                                d->args(l, 4, A, nullptr));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    if (d->n_flow_factor > 0) {
+        if ((e = hipMemsetAsync(d->tickets, 0, sizeof(int), s)) != hipSuccess) return e;
+        const Flow f{d->order_factor, d->n_flow_factor, d->tickets, d->done, epoch, d->slev, d->flow_lev0};
+        const int grid = std::min(d->n_flow_factor, d->ncu * 12);
+        hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(0, 0, A, nullptr), f);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 
 hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
     hipError_t e;
-    // the solve kernels do not depend on the size class: one wave launch per level for classes 0-3
-    for (int l = 0; l < d->nlevels; ++l) {
+    const uint32_t epoch = ++d->epoch;
+    const int grid = std::min(d->n_flow_solve, d->ncu * 8);
+    if (d->flow_solve && (e = hipMemsetAsync(d->tickets + 1, 0, 2 * sizeof(int), s)) != hipSuccess) return e;
+    // forward: per-level launches below solve_lev0 (the solve kernels do not depend on the size
+    // class: one wave launch per level for classes 0-3), then one flow over the rest of the tree
+    for (int l = 0; l < d->solve_lev0; ++l) {
         int n;
         if ((n = d->count(l, 0, 4)))
             hipLaunchKernelGGL(mf_forward_wave, dim3(n), dim3(64), d->lds_max(d->lds_fwd, l, 0, 4), s, d->args(l, 0, nullptr, x));
@@ -521,7 +708,17 @@ hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
             hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), d->lds_fwd[l * kClasses + 4], s, d->args(l, 4, nullptr, x));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    for (int l = d->nlevels - 1; l >= 0; --l) {
+    if (d->flow_solve) {
+        const Flow ff{d->order_fwd, d->n_flow_solve, d->tickets + 1, d->done + d->nsuper, epoch, d->slev, d->solve_lev0};
+        hipLaunchKernelGGL(mf_forward_flow, dim3(grid), dim3(64), d->lds_fwd_flow, s, d->args(0, 0, nullptr, x), ff);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        const Flow fb{d->order_bwd, d->n_flow_solve, d->tickets + 2, d->done + 2 * (size_t)d->nsuper, epoch, d->slev,
+                      d->solve_lev0};
+        hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), d->lds_bwd_flow, s, d->args(0, 0, nullptr, x), fb,
+                           (const int32_t*)d->parent);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    for (int l = std::min(d->solve_lev0, d->nlevels) - 1; l >= 0; --l) {
         int n;
         if ((n = d->count(l, 0, 4)))
             hipLaunchKernelGGL(mf_backward_wave, dim3(n), dim3(64), d->lds_max(d->lds_bwd, l, 0, 4), s, d->args(l, 0, nullptr, x));
