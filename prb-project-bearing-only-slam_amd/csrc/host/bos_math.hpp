@@ -25,7 +25,10 @@ constexpr double kPi = 3.1415926535897932384626433832795;
 constexpr double k2Pi = 6.283185307179586476925286766559;
 
 // Solver::normalized_angle (slam/solver_jacobians.cpp:325-333): [-pi, pi), compared in double.
+// For a float, (double)a < -pi <=> a <= -(float)pi and (double)a >= pi <=> a >= (float)pi
+// ((float)pi > pi), so the common in-range case skips the double arithmetic exactly.
 template <typename T> BOS_HD T normalized_angle(T a) {
+    if (sizeof(T) == 4 && a > -(T)3.14159274101257324 && a < (T)3.14159274101257324) return a;
     while ((double)a < -kPi) a = (T)((double)a + k2Pi);
     while ((double)a >= kPi) a = (T)((double)a - k2Pi);
     return a;
