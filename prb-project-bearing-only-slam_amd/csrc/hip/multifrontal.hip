@@ -249,12 +249,27 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
 // the (lower) front in a compile-time-indexed array; each column step broadcasts the pivot column
 // through a small LDS buffer (one store per lane, broadcast reads). LDS otherwise only stages the
 // assembly. F: packed front (MAXM (MAXM + 1) / 2), colbuf: 2 MAXM, smap: 64 ints.
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Factorization of one front fused with its forward elimination: w (LDS, m doubles) receives the
+// front's right-hand side (x of its own dofs) plus the children's u-vectors, extend-added with
+// their update matrices; after the partial Cholesky, lane i eliminates with its row of L (still in
+// registers): y_j = w_j / L_jj, w_i -= L_ij y_j. y goes to x, the remaining w (rows >= k) to the
+// front's u-vector for its parent.
 template <int MAXM, bool COH>
 __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf, int* smap,
-                                                 int lane) {
+                                                 double* wv, int lane) {
     const int k = a.k[s], r = a.r[s], m = k + r;
+    const int c0 = a.col0[s];
     const int np = m * (m + 1) / 2;
+    const double xo = lane < k ? a.x[c0 + lane] : 0.0;   // right-hand side of the own dofs (k < 64)
     for (int e = lane; e < np; e += 64) F[e] = 0.0;
+    for (int i = lane; i < m; i += 64) wv[i] = 0.0;    // children's u-vectors accumulate here
     wave_sync();
     assemble_wave(a, s, F, lane);
     wave_sync();
@@ -267,6 +282,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         if (lane < rc) smap[lane] = a.rmap[a.rmap_off[c] + lane];
         const double* Uc = a.U + a.U_off[c];
         wave_sync();
+        const double uval = lane < rc ? ldc<COH>(a.u + a.u_off[c] + lane) : 0.0;   // the child's u-vector
         const int ne = rc * (rc + 1) / 2;
         int j = 0, len = rc, o = lane;
         while (len > 0 && o >= len) { o -= len; ++j; --len; }
@@ -283,10 +299,12 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
                 }
             }
         }
+        if (lane < rc) wv[smap[lane]] += uval;
         wave_sync();
     }
     const bool live = lane < m;
     double row[MAXM];
+    double myinv = 0.0;
 #pragma unroll
     for (int c = 0; c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk(lane, c, m)] : 0.0;
     // Right-looking: step j broadcasts column j through a double-buffered LDS column (one store
@@ -306,6 +324,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             const double ljj = sqrt(d), inv = 1.0 / ljj;
             const double lij = lane == j ? ljj : row[j] * inv;   // L[i, j]
             row[j] = lij;
+            if (lane == j) myinv = inv;                          // 1 / L_jj, kept by the pivot lane
             const double g = lij * inv;                          // L[i, j] / L[j, j]
 #pragma unroll
             for (int l = j + 1; l < MAXM; ++l) row[l] = fma(-g, col[l], row[l]);   // -= L[i,j] L[l,j]
@@ -320,6 +339,20 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             else stc<COH>(Us + pk(lane - k, c - k, r), row[c]);
         }
     }
+    // fused forward elimination with the rows of L held in registers
+    double wi = live ? wv[lane] + xo : 0.0;
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) {
+        if (j < k) {
+            const double yj = readlane_d(wi * myinv, j);   // lane j: w_j / L_jj
+            if (lane == j) wi = yj;
+            else if (lane > j) wi -= row[j] * yj;
+        }
+    }
+    if (live) {
+        if (lane < k) a.x[c0 + lane] = wi;
+        else stc<COH>(a.u + a.u_off[s] + (lane - k), wi);
+    }
     wave_sync();
 }
 
@@ -327,38 +360,9 @@ template <int MAXM>
 __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * MAXM];
+    __shared__ __attribute__((aligned(16))) double wv[MAXM];
     __shared__ int smap[64];
-    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, smap, threadIdx.x);
-}
-
-// Forward substitution of one front by one wavefront (any m); LDS: w[m] | L panel (m x k).
-template <bool COH> __device__ __forceinline__ void forward_front(const MfArgs& a, int s, double* w, int lane) {
-    const int k = a.k[s], r = a.r[s], m = k + r;
-    const int c0 = a.col0[s];
-    double* Lw = w + m;
-    stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
-    for (int i = lane; i < m; i += 64) w[i] = i < k ? a.x[c0 + i] : 0.0;
-    wave_sync();
-    for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {
-        const int c = a.child[ci];
-        const int rc = a.r[c];
-        const int32_t* map = a.rmap + a.rmap_off[c];
-        const double* uc = a.u + a.u_off[c];
-        for (int t = lane; t < rc; t += 64) w[map[t]] += ldc<COH>(uc + t);
-        wave_sync();
-    }
-    for (int j = 0; j < k; ++j) {
-        const double yj = w[j] / Lw[j + j * m];
-        wave_sync();
-        if (lane == 0) w[j] = yj;
-        for (int i = j + 1 + lane; i < m; i += 64) w[i] -= Lw[i + j * m] * yj;
-        wave_sync();
-    }
-    for (int i = lane; i < m; i += 64) {
-        if (i < k) a.x[c0 + i] = w[i];
-        else stc<COH>(a.u + a.u_off[s] + (i - k), w[i]);
-    }
-    wave_sync();
+    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, smap, wv, threadIdx.x);
 }
 
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
@@ -392,11 +396,6 @@ template <bool COH> __device__ __forceinline__ void backward_front(const MfArgs&
     }
     for (int j = lane; j < k; j += 64) stc<COH>(a.x + c0 + j, w[j]);
     wave_sync();
-}
-
-__global__ __launch_bounds__(64) void mf_forward_wave(const MfArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double w[];
-    forward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x);
 }
 
 __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
@@ -451,9 +450,16 @@ __device__ __forceinline__ void publish_done(const Flow& f, int s) {
     if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(64) void mf_factor_flow(const MfArgs a, const Flow f) {
-    __shared__ __attribute__((aligned(16))) double F[kMfWaveMaxM * (kMfWaveMaxM + 1) / 2];
-    __shared__ __attribute__((aligned(16))) double colbuf[2 * kMfWaveMaxM];
+// The flow kernel instantiates one register class only: inlining all four merged their register
+// demands (256 VGPRs + AGPRs, 1 wave per SIMD), out-of-line calls spilled, and forcing 4 waves per
+// SIMD spilled too (all measured slower). Fronts of the flow range are <= kFlowMaxM (mf_create
+// picks the range accordingly).
+constexpr int kFlowMaxM = 48;
+
+__device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f) {
+    __shared__ __attribute__((aligned(16))) double F[kFlowMaxM * (kFlowMaxM + 1) / 2];
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * kFlowMaxM];
+    __shared__ __attribute__((aligned(16))) double wv[kFlowMaxM];
     __shared__ int smap[64];
     const int lane = threadIdx.x;
     // a wave takes at most n + 1 tickets: the loop is bounded (an unbounded for (;;) version of
@@ -464,27 +470,12 @@ __global__ __launch_bounds__(64) void mf_factor_flow(const MfArgs a, const Flow 
         const int s = f.order[t];
         for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci)
             if (f.slev[a.child[ci]] >= f.lev0) wait_done(f, a.child[ci], a.info);
-        const int m = a.k[s] + a.r[s];   // <= kMfWaveMaxM for every front of the flow range
-        if (m <= 16) factor_front_reg<16, true>(a, s, F, colbuf, smap, lane);
-        else if (m <= 32) factor_front_reg<32, true>(a, s, F, colbuf, smap, lane);
-        else if (m <= 48) factor_front_reg<48, true>(a, s, F, colbuf, smap, lane);
-        else factor_front_reg<64, true>(a, s, F, colbuf, smap, lane);
+        factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, smap, wv, lane);   // m <= kFlowMaxM
         publish_done(f, s);
     }
 }
 
-__global__ __launch_bounds__(64) void mf_forward_flow(const MfArgs a, const Flow f) {
-    extern __shared__ __attribute__((aligned(16))) double w[];
-    for (int it = 0; it <= f.n; ++it) {
-        const int t = next_ticket(f.ticket);
-        if (t >= f.n) break;
-        const int s = f.order[t];
-        for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci)
-            if (f.slev[a.child[ci]] >= f.lev0) wait_done(f, a.child[ci], a.info);
-        forward_front<true>(a, s, w, threadIdx.x);
-        publish_done(f, s);
-    }
-}
+__global__ __launch_bounds__(64) void mf_factor_flow(const MfArgs a, const Flow f) { factor_flow_body(a, f); }
 
 __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flow f, const int32_t* parent) {
     extern __shared__ __attribute__((aligned(16))) double w[];
@@ -526,8 +517,8 @@ struct MfDevice {
     int flow_lev0 = 0, n_flow_factor = 0, nsuper = 0, ncu = 256;
     bool flow_solve = false;
     int solve_lev0 = 0, n_flow_solve = 0;   // solves: levels < solve_lev0 per level, the rest one flow each
-    int lds_fwd_flow = 0, lds_bwd_flow = 0;
-    int32_t *order_factor = nullptr, *order_fwd = nullptr, *order_bwd = nullptr, *slev = nullptr, *parent = nullptr;
+    int lds_bwd_flow = 0;
+    int32_t *order_factor = nullptr, *order_bwd = nullptr, *slev = nullptr, *parent = nullptr;
     uint32_t* done = nullptr;   // [3][nsuper]: factor, forward, backward
     int* tickets = nullptr;     // [3]
     uint32_t epoch = 0;
@@ -597,14 +588,14 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
             d->ncu = ncu;
     }
-    std::vector<int32_t> slev(F.nsuper, 0), ofac, ofwd, obwd;
+    std::vector<int32_t> slev(F.nsuper, 0), ofac, ofwd, obwd;   // ofwd: the solve flow range, bottom-up
     for (int l = 0; l < L; ++l)
         for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) slev[F.level[q]] = l;
-    d->flow_lev0 = L;   // lowest level from which every front is <= kMfWaveMaxM (and >= 2)
+    d->flow_lev0 = L;   // lowest level from which every front is <= kFlowMaxM (and >= 2)
     while (d->flow_lev0 > 2) {
         bool small = true;
         for (int q = F.level_ptr[d->flow_lev0 - 1]; q < F.level_ptr[d->flow_lev0] && small; ++q)
-            small = F.k[F.level[q]] + F.r[F.level[q]] <= kMfWaveMaxM;
+            small = F.k[F.level[q]] + F.r[F.level[q]] <= kFlowMaxM;
         if (!small) break;
         --d->flow_lev0;
     }
@@ -615,12 +606,11 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
     for (int q = F.level_ptr[d->solve_lev0]; q < F.level_ptr[L]; ++q) {
         const int s = F.level[q], k = F.k[s], m = k + F.r[s];
         ofwd.push_back(s);
-        d->lds_fwd_flow = std::max(d->lds_fwd_flow, (m + m * k) * 8);
         d->lds_bwd_flow = std::max(d->lds_bwd_flow, (2 * k + (m - k) + m * k) * 8);
     }
     obwd.assign(ofwd.rbegin(), ofwd.rend());
     d->n_flow_solve = (int)ofwd.size();
-    d->flow_solve = d->n_flow_solve > 0 && d->lds_fwd_flow <= 48 * 1024 && d->lds_bwd_flow <= 48 * 1024;
+    d->flow_solve = d->n_flow_solve > 0 && d->lds_bwd_flow <= 48 * 1024;
     if (!d->flow_solve) d->solve_lev0 = L;
     if (const char* e = std::getenv("BOS_MF_FLOW")) {   // diagnostics: bit 0 factor flow, bit 1 solve flows
         const int v = std::atoi(e);
@@ -628,7 +618,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         if (!(v & 2)) { d->flow_solve = false; d->solve_lev0 = L; }
     }
     int rc = 0;
-    if ((rc = up(&d->order_factor, ofac, err)) || (rc = up(&d->order_fwd, ofwd, err)) || (rc = up(&d->order_bwd, obwd, err)) ||
+    if ((rc = up(&d->order_factor, ofac, err)) || (rc = up(&d->order_bwd, obwd, err)) ||
         (rc = up(&d->slev, slev, err)) || (rc = up(&d->parent, F.parent, err)))
         return rc;
     if (hipMalloc((void**)&d->done, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
@@ -660,7 +650,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
 
 void mf_destroy(MfDevice* d) {
     if (!d) return;
-    void* bufs[] = {d->order_factor, d->order_fwd, d->order_bwd, d->slev, d->parent, d->done, d->tickets, d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
+    void* bufs[] = {d->order_factor, d->order_bwd, d->slev, d->parent, d->done, d->tickets, d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
     for (void* b : bufs)
@@ -668,52 +658,43 @@ void mf_destroy(MfDevice* d) {
     delete d;
 }
 
-hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s) {
+hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
     hipError_t e = hipMemsetAsync(d->info, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return e;
     const uint32_t epoch = ++d->epoch;
     for (int l = 0; l < d->flow_lev0; ++l) {
         int n;
-        if ((n = d->count(l, 0))) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(l, 0, A, nullptr));
-        if ((n = d->count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(l, 1, A, nullptr));
-        if ((n = d->count(l, 2))) hipLaunchKernelGGL(mf_factor_reg<48>, dim3(n), dim3(64), 0, s, d->args(l, 2, A, nullptr));
-        if ((n = d->count(l, 3))) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(l, 3, A, nullptr));
-        if ((n = d->count(l, 4)))
+        if ((n = d->count(l, 0))) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(l, 0, A, x));
+        if ((n = d->count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(l, 1, A, x));
+        if ((n = d->count(l, 2))) hipLaunchKernelGGL(mf_factor_reg<48>, dim3(n), dim3(64), 0, s, d->args(l, 2, A, x));
+        if ((n = d->count(l, 3))) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(l, 3, A, x));
+        if ((n = d->count(l, 4))) {   // large fronts: workgroup factorization, then their forward step
             hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), d->lds_factor[l * kClasses + 4], s,
-                               d->args(l, 4, A, nullptr));
+                               d->args(l, 4, A, x));
+            hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), d->lds_fwd[l * kClasses + 4], s,
+                               d->args(l, 4, A, x));
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (d->n_flow_factor > 0) {
         if ((e = hipMemsetAsync(d->tickets, 0, sizeof(int), s)) != hipSuccess) return e;
         const Flow f{d->order_factor, d->n_flow_factor, d->tickets, d->done, epoch, d->slev, d->flow_lev0};
         const int grid = std::min(d->n_flow_factor, d->ncu * 12);
-        hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(0, 0, A, nullptr), f);
+        hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
 }
 
 hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
+    // backward substitution (the forward one ran inside mf_factor): one flow launch over the levels
+    // >= solve_lev0 (top-down), then per-level launches below it
     hipError_t e;
     const uint32_t epoch = ++d->epoch;
-    const int grid = std::min(d->n_flow_solve, d->ncu * 8);
-    if (d->flow_solve && (e = hipMemsetAsync(d->tickets + 1, 0, 2 * sizeof(int), s)) != hipSuccess) return e;
-    // forward: per-level launches below solve_lev0 (the solve kernels do not depend on the size
-    // class: one wave launch per level for classes 0-3), then one flow over the rest of the tree
-    for (int l = 0; l < d->solve_lev0; ++l) {
-        int n;
-        if ((n = d->count(l, 0, 4)))
-            hipLaunchKernelGGL(mf_forward_wave, dim3(n), dim3(64), d->lds_max(d->lds_fwd, l, 0, 4), s, d->args(l, 0, nullptr, x));
-        if ((n = d->count(l, 4)))
-            hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), d->lds_fwd[l * kClasses + 4], s, d->args(l, 4, nullptr, x));
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     if (d->flow_solve) {
-        const Flow ff{d->order_fwd, d->n_flow_solve, d->tickets + 1, d->done + d->nsuper, epoch, d->slev, d->solve_lev0};
-        hipLaunchKernelGGL(mf_forward_flow, dim3(grid), dim3(64), d->lds_fwd_flow, s, d->args(0, 0, nullptr, x), ff);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        const Flow fb{d->order_bwd, d->n_flow_solve, d->tickets + 2, d->done + 2 * (size_t)d->nsuper, epoch, d->slev,
-                      d->solve_lev0};
+        if ((e = hipMemsetAsync(d->tickets + 1, 0, sizeof(int), s)) != hipSuccess) return e;
+        const Flow fb{d->order_bwd, d->n_flow_solve, d->tickets + 1, d->done + d->nsuper, epoch, d->slev, d->solve_lev0};
+        const int grid = std::min(d->n_flow_solve, d->ncu * 8);
         hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), d->lds_bwd_flow, s, d->args(0, 0, nullptr, x), fb,
                            (const int32_t*)d->parent);
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -14,9 +14,10 @@ struct MfDevice;
 // Upload the static tree / maps and allocate factor buffers. Returns 0 or < 0 with err.
 int mf_create(const Multifrontal& F, MfDevice** out, std::string& err);
 void mf_destroy(MfDevice* d);
-// Numeric factorization of H (CSR values in nested-dissection order, fp64).
-hipError_t mf_factor(MfDevice* d, const double* A, hipStream_t s);
-// x <- H^{-1} x (x in the same permuted order) using the last factorization.
+// Numeric factorization of H (read from the block array A through the assembly map, fp64), fused
+// with the forward substitution: x (permuted order) holds b on entry and L^{-1} b on exit.
+hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s);
+// Backward substitution: x <- L^{-T} x, completing x = H^{-1} b.
 hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s);
 // device counter of non-positive pivots met by the last factorization
 const int32_t* mf_info_ptr(const MfDevice* d);

@@ -221,7 +221,7 @@ int enqueue_solve(bos_solver* s, bool& ran_analysis) {
             HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.blk.size, s->stream));
             A = s->d_val64;
         }
-        HIP_TRY(bos::dev::mf_factor(s->mf, A, s->stream));
+        HIP_TRY(bos::dev::mf_factor(s->mf, A, s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, s->d_rhs, s->stream));
         return BOS_OK;
     }
