@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--gn-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--solver", choices=["supernodal", "schur"], default="supernodal",
+                    help="GN linear solver: nested-dissection multifrontal or landmarks-first Schur (config 5)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,7 +137,8 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     t_create = time.perf_counter()
-    S = bos.Solver(P, precision=precision, device=local_rank, stream=stream.cuda_stream, rank=rank,
+    solver = bos.BOS_SOLVER_SCHUR if args.solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
+    S = bos.Solver(P, precision=precision, solver=solver, device=local_rank, stream=stream.cuda_stream, rank=rank,
                    world_size=world, nccl_id=nccl_id)
     info = S.system_info()
     log(f"rank {rank}: bos_create {time.perf_counter() - t_create:.1f} s, n={info['n']} "
@@ -210,7 +213,7 @@ def main():
             "config": {
                 "workload": "config 3: synthetic 100k poses / 200k landmarks / 1M bearings / 99999 odometry "
                             "edges; J+H build " + ("fp32" if precision == bos.BOS_FP32 else "fp64") +
-                            " (solve fp64)",
+                            " (solve fp64, " + args.solver + ")",
                 "poses": P.NP, "landmarks": P.NL, "bearings": int(len(P.b_z)), "odometry": int(len(P.o_z)),
                 "parallelism": f"observation-sharded x{world}" if world > 1 else "single GPU",
             },

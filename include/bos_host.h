@@ -54,18 +54,20 @@ typedef struct bos_plan_info {
     int64_t mf_update_bytes;
 } bos_plan_info;
 
-/* Build the static plan on the host (what bos_create does before touching the GPU).
+/* Build the static plan on the host (what bos_create does before touching the GPU) for solver
+ * `solver` (BOS_SOLVER_*: it selects the ordering).
  * If ref_rows/ref_cols/owned are given (capacity >= nnz_lower) they receive, for every stored
  * entry of the lower triangle of H_nf, its (row, col) in the reference dof numbering
  * (row >= col) and whether rank `rank` of `world` writes it; b_owned (n + 3 entries, reference
  * order of the N dofs minus nothing: indexed by reference dof) marks the b entries it writes;
  * perm_to_ref (n + 3 entries) maps the permuted dof order used on the device to reference dofs. */
-int bos_plan_inspect(const bos_problem* problem, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
+int bos_plan_inspect(const bos_problem* problem, int32_t solver, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
                      int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref, bos_plan_info* info);
 
 /* Test hook: the GPU multifrontal algorithm re-run on the host with the plan's tree and maps
- * (vals in the plan's CSR order, rhs/x in its permuted dof order). Not used by any solve. */
-int bos_plan_mf_selftest(const bos_problem* problem, const double* vals, const double* rhs, double* x);
+ * (solver BOS_SOLVER_SUPERNODAL or _SCHUR; vals in the plan's CSR order, rhs/x in its permuted
+ * dof order). Not used by any solve. */
+int bos_plan_mf_selftest(const bos_problem* problem, int32_t solver, const double* vals, const double* rhs, double* x);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,7 @@ BOS_FP32 = 32
 BOS_SOLVER_SUPERNODAL = 0
 BOS_SOLVER_DENSE_CHOL = 1
 BOS_SOLVER_ROCSOLVER_RF = 2
+BOS_SOLVER_SCHUR = 3
 BOS_SOLVER_SPARSE_CHOL = BOS_SOLVER_SUPERNODAL
 
 # every symbol declared in include/bos.h and include/bos_host.h
@@ -132,10 +133,10 @@ def lib():
         "bos_dataset_ground_truth": (ctypes.c_int, [vp, ctypes.POINTER(_dp), ctypes.POINTER(_dp)]),
         "bos_dataset_write_g2o": (ctypes.c_int, [vp, ctypes.c_char_p, _dp, _dp, ctypes.c_int]),
         "bos_dataset_free": (None, [vp]),
-        "bos_plan_inspect": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32,
+        "bos_plan_inspect": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_int64, _ip, _ip, ctypes.POINTER(ctypes.c_uint8),
                                             ctypes.POINTER(ctypes.c_uint8), _ip, ctypes.POINTER(bos_plan_info)]),
-        "bos_plan_mf_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), _dp, _dp, _dp]),
+        "bos_plan_mf_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, _dp, _dp, _dp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -274,12 +275,13 @@ def write_g2o(P: Problem, path: str, pose_xyt=None, lm_xy=None, with_landmarks=T
         L.bos_dataset_free(h)
 
 
-def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = False):
+def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = False,
+                 solver: int = BOS_SOLVER_SUPERNODAL):
     """Host-only plan build (ordering, CSR layout, shard ownership) — no GPU needed."""
     L = lib()
     cs = P.c_struct()
     info = bos_plan_info()
-    _check(L.bos_plan_inspect(ctypes.byref(cs), rank, world, 0, None, None, None, None, None, ctypes.byref(info)),
+    _check(L.bos_plan_inspect(ctypes.byref(cs), solver, rank, world, 0, None, None, None, None, None, ctypes.byref(info)),
            "plan_inspect")
     out = {"n": info.n, "nnz_lower": info.nnz_lower, "nnz_factor": info.nnz_factor,
            "num_block_values": info.num_block_values, "lanes_per_pose": info.lanes_per_pose,
@@ -294,20 +296,20 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
         owned = np.zeros(nnz, dtype=np.uint8)
         b_owned = np.zeros(P.N, dtype=np.uint8)
         perm = np.zeros(P.N, dtype=np.int32)
-        _check(L.bos_plan_inspect(ctypes.byref(cs), rank, world, nnz, _ptr(rows, ctypes.c_int32),
+        _check(L.bos_plan_inspect(ctypes.byref(cs), solver, rank, world, nnz, _ptr(rows, ctypes.c_int32),
                                   _ptr(cols, ctypes.c_int32), _ptr(owned, ctypes.c_uint8),
                                   _ptr(b_owned, ctypes.c_uint8), _ptr(perm, ctypes.c_int32), None), "plan_inspect")
         out.update(rows=rows, cols=cols, owned=owned.astype(bool), b_owned=b_owned.astype(bool), perm_to_ref=perm)
     return out
 
 
-def plan_mf_selftest(P: Problem, vals, rhs):
+def plan_mf_selftest(P: Problem, vals, rhs, solver: int = BOS_SOLVER_SUPERNODAL):
     """Host re-run of the GPU multifrontal algorithm on the plan's tree (test hook)."""
     cs = P.c_struct()
     v = np.ascontiguousarray(vals, dtype=np.float64)
     b = np.ascontiguousarray(rhs, dtype=np.float64)
     x = np.zeros_like(b)
-    _check(lib().bos_plan_mf_selftest(ctypes.byref(cs), _ptr(v, ctypes.c_double), _ptr(b, ctypes.c_double),
+    _check(lib().bos_plan_mf_selftest(ctypes.byref(cs), solver, _ptr(v, ctypes.c_double), _ptr(b, ctypes.c_double),
                                       _ptr(x, ctypes.c_double)), "plan_mf_selftest")
     return x
 

@@ -1,5 +1,5 @@
 // Headless drop-in for executables/bearing_only_slam.cpp (reference :40-116).
-// Usage: bearing_only_slam <dataset_fname> [--iters N] [--fp32] [--dense] [--dump out.g2o] [--quiet]
+// Usage: bearing_only_slam <dataset_fname> [--iters N] [--fp32] [--dense|--schur] [--dump out.g2o] [--quiet]
 // Same flow as the reference's main: parse_g2o, default the fixed pose, triangulate the
 // landmarks, construct the Solver, then iterate (the reference's Tab press = 50 iterations,
 // :93-99). The OpenCV window is replaced by a per-iteration chi^2 line and an optional g2o dump.
@@ -17,7 +17,7 @@ using namespace proj02;
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::cout << "usage: bearing_only_slam <dataset_fname> [--iters N] [--fp32] [--dense] [--dump out.g2o] [--quiet]"
+        std::cout << "usage: bearing_only_slam <dataset_fname> [--iters N] [--fp32] [--dense|--schur] [--dump out.g2o] [--quiet]"
                   << std::endl;
         return 1;
     }
@@ -30,6 +30,7 @@ int main(int argc, char** argv) {
         if (!std::strcmp(argv[i], "--iters") && i + 1 < argc) iters = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--fp32")) opt.precision = BOS_FP32;
         else if (!std::strcmp(argv[i], "--dense")) opt.solver = BOS_SOLVER_DENSE_CHOL;
+        else if (!std::strcmp(argv[i], "--schur")) opt.solver = BOS_SOLVER_SCHUR;
         else if (!std::strcmp(argv[i], "--dump") && i + 1 < argc) dump = argv[++i];
         else if (!std::strcmp(argv[i], "--quiet")) quiet = true;
         else { std::cerr << "unknown argument " << argv[i] << std::endl; return 1; }

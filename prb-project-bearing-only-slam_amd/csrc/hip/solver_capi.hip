@@ -116,6 +116,13 @@ struct bos_solver {
 };
 
 namespace {
+// both multifrontal orderings (nested dissection / landmarks-first Schur) share the GPU engine
+bool uses_mf(const bos_solver* s) {
+    return s->solver_kind == BOS_SOLVER_SUPERNODAL || s->solver_kind == BOS_SOLVER_SCHUR;
+}
+}  // namespace
+
+namespace {
 
 template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     bos::dev::LinParams<T> p;
@@ -215,7 +222,7 @@ int enqueue_solve(bos_solver* s, bool& ran_analysis) {
     HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream)
                 : bos::dev::launch_gather_f64<double>((const double*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream));
     const rocblas_int nn = (rocblas_int)n;
-    if (s->solver_kind == BOS_SOLVER_SUPERNODAL) {   // reads the block array through its assembly map
+    if (uses_mf(s)) {   // reads the block array through its assembly map
         const double* A = (const double*)s->d_val;
         if (f32) {
             HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.blk.size, s->stream));
@@ -299,7 +306,7 @@ int read_stats(bos_solver* s, bos_step_stats* st, bool with_update, bool with_so
     if (with_update) HIP_TRY(hipMemcpyAsync(&mdx, s->d_maxdx, sizeof(mdx), hipMemcpyDeviceToHost, s->stream));
     if (with_solve && s->solver_kind == BOS_SOLVER_DENSE_CHOL)
         HIP_TRY(hipMemcpyAsync(&info, s->d_info, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
-    if (with_solve && s->solver_kind == BOS_SOLVER_SUPERNODAL)
+    if (with_solve && uses_mf(s))
         HIP_TRY(hipMemcpyAsync(&info, bos::dev::mf_info_ptr(s->mf), sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     if (st) {
@@ -402,7 +409,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     if (opt_in) opt = *opt_in;
     if (opt.precision != BOS_FP64 && opt.precision != BOS_FP32) return fail(BOS_ERR_INVALID, "precision must be 32 or 64");
     if (opt.solver != BOS_SOLVER_SUPERNODAL && opt.solver != BOS_SOLVER_DENSE_CHOL &&
-        opt.solver != BOS_SOLVER_ROCSOLVER_RF)
+        opt.solver != BOS_SOLVER_ROCSOLVER_RF && opt.solver != BOS_SOLVER_SCHUR)
         return fail(BOS_ERR_INVALID, "unknown solver");
     if (pb->num_poses <= 0 || pb->num_landmarks < 0 || pb->num_bearings < 0 || pb->num_odometry < 0)
         return fail(BOS_ERR_INVALID, "bad problem sizes");
@@ -440,6 +447,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
     std::string err;
     const int fmode = s->solver_kind == BOS_SOLVER_SUPERNODAL    ? bos::kFactorMultifrontal
+                      : s->solver_kind == BOS_SOLVER_SCHUR        ? bos::kFactorSchur
                       : s->solver_kind == BOS_SOLVER_ROCSOLVER_RF ? bos::kFactorScalar
                                                                   : bos::kFactorNone;
     int rc = bos::build_plan(pi, s->rank, s->world, fmode, s->plan, err);
@@ -559,18 +567,18 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     if ((rc = upload(&s->node_dof, P.node_dof))) return bail(rc);
     if ((rc = alloc_T(&s->d_val, nval)) || (rc = alloc_T(&s->d_b, nb)) || (rc = dalloc(&s->d_rhs, std::max<int64_t>(P.n, 1))))
         return bail(rc);
-    if (f32 && s->solver_kind == BOS_SOLVER_SUPERNODAL && (rc = dalloc(&s->d_val64, nval))) return bail(rc);
+    if (f32 && uses_mf(s) && (rc = dalloc(&s->d_val64, nval))) return bail(rc);
     HIP_TRY(hipMemset(s->d_val, 0, nval * s->tsize));
     HIP_TRY(hipMemset(s->d_b, 0, nb * s->tsize));
     {
         std::vector<int32_t> er(s->ref_dof.begin(), s->ref_dof.begin() + P.n);
         if ((rc = upload(&s->elim_ref, er))) return bail(rc);
     }
-    if (s->solver_kind != BOS_SOLVER_SUPERNODAL &&
+    if (!uses_mf(s) &&
         ((rc = upload(&s->d_rowptr, P.rowptr)) || (rc = upload(&s->d_colind, P.colind)) ||
          (rc = upload(&s->csr_src, P.blk.csr_src)) || (rc = dalloc(&s->d_csr64, std::max<int64_t>(P.nnzA(), 1)))))
         return bail(rc);
-    if (s->solver_kind == BOS_SOLVER_SUPERNODAL) {
+    if (uses_mf(s)) {
         std::string merr;
         if (bos::dev::mf_create(P.mf, &s->mf, merr)) return bail(fail(BOS_ERR_DEVICE, merr));
     } else if (s->solver_kind == BOS_SOLVER_ROCSOLVER_RF) {
@@ -661,7 +669,7 @@ int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
     const bos::Plan& P = s->plan;
     info->n = P.n;
     info->nnz_lower = P.nnzA();
-    info->nnz_factor = s->solver_kind == BOS_SOLVER_SUPERNODAL ? P.mf.L_size : P.nnzL();
+    info->nnz_factor = uses_mf(s) ? P.mf.L_size : P.nnzL();
     const int64_t Mb = s->Mb, Mo = s->Mo, NP = s->NP, NL = s->NL;
     // compulsory reads of inputs + state, one write of every output block
     info->algorithmic_bytes = s->precision == BOS_FP32 ? 36 * Mb + 80 * Mo + 60 * NP + 32 * NL

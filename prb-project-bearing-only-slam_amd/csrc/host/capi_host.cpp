@@ -169,10 +169,24 @@ int bos_dataset_write_g2o(const bos_dataset* d, const char* path, const double* 
 
 void bos_dataset_free(bos_dataset* d) { delete d; }
 
-int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
+namespace {
+int factor_mode_of(int32_t solver) {
+    switch (solver) {
+        case BOS_SOLVER_SUPERNODAL: return bos::kFactorMultifrontal;
+        case BOS_SOLVER_SCHUR: return bos::kFactorSchur;
+        case BOS_SOLVER_ROCSOLVER_RF: return bos::kFactorScalar;
+        case BOS_SOLVER_DENSE_CHOL: return bos::kFactorNone;
+        default: return -1;
+    }
+}
+}  // namespace
+
+int bos_plan_inspect(const bos_problem* pb, int32_t solver, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
                      int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref,
                      bos_plan_info* info) {
     if (!pb) return hfail(BOS_ERR_INVALID, "null problem");
+    const int fmode = factor_mode_of(solver);
+    if (fmode < 0) return hfail(BOS_ERR_INVALID, "unknown solver");
     bos::ProblemIndex pi;
     pi.NP = pb->num_poses; pi.NL = pb->num_landmarks; pi.Mb = pb->num_bearings; pi.Mo = pb->num_odometry;
     pi.fixed = pb->fixed_pose;
@@ -180,7 +194,7 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
     pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
     bos::Plan P;
     std::string err;
-    const int rc = bos::build_plan(pi, rank, world, bos::kFactorMultifrontal, P, err);
+    const int rc = bos::build_plan(pi, rank, world, fmode, P, err);
     if (rc) return hfail(rc, err);
     const int NP = pi.NP;
     std::vector<int32_t> ref(P.n + 3);
@@ -193,7 +207,7 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
         std::memset(info, 0, sizeof(*info));
         info->n = P.n;
         info->nnz_lower = P.nnzA();
-        info->nnz_factor = P.mf.L_size;
+        info->nnz_factor = P.mf.nsuper ? P.mf.L_size : P.nnzL();
         info->num_block_values = P.blk.size;
         info->lanes_per_pose = P.blk.lpp;
         info->flops_temporal = P.ordering.flops_temporal;
@@ -242,8 +256,10 @@ int bos_plan_inspect(const bos_problem* pb, int32_t rank, int32_t world, int64_t
 // tree and maps (validates the symbolic structure without a GPU). vals: values of the stored
 // entries of H_nf in bos_plan_inspect's order (scattered into the block array here), rhs / x:
 // permuted order of length n. Not used by any solve path.
-int bos_plan_mf_selftest(const bos_problem* pb, const double* vals, const double* rhs, double* x) {
+int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* vals, const double* rhs, double* x) {
     if (!pb || !vals || !rhs || !x) return hfail(BOS_ERR_INVALID, "null argument");
+    if (solver != BOS_SOLVER_SUPERNODAL && solver != BOS_SOLVER_SCHUR)
+        return hfail(BOS_ERR_INVALID, "selftest needs a multifrontal solver");
     bos::ProblemIndex pi;
     pi.NP = pb->num_poses; pi.NL = pb->num_landmarks; pi.Mb = pb->num_bearings; pi.Mo = pb->num_odometry;
     pi.fixed = pb->fixed_pose;
@@ -251,7 +267,7 @@ int bos_plan_mf_selftest(const bos_problem* pb, const double* vals, const double
     pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
     bos::Plan P;
     std::string err;
-    const int rc = bos::build_plan(pi, 0, 1, bos::kFactorMultifrontal, P, err);
+    const int rc = bos::build_plan(pi, 0, 1, factor_mode_of(solver), P, err);
     if (rc) return hfail(rc, err);
     const bos::Multifrontal& F = P.mf;
     std::vector<double> hval(P.blk.size, 0.0);   // the block array the GPU solver reads

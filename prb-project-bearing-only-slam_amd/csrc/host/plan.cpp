@@ -250,10 +250,70 @@ void nested_dissection(const Graph& g, const std::vector<char>& active, std::vec
 
 }  // namespace
 
-int order_nodes(const ProblemIndex& pi, bool nd_only, std::vector<int32_t>& node_pos,
+// Pose graph of the Schur complement: odometry edges and every pair of poses observing a common
+// landmark (the fill of eliminating that landmark). The fixed pose has no edges.
+Graph build_schur_graph(const ProblemIndex& pi) {
+    Graph g;
+    g.n = pi.NP + pi.NL;   // landmark nodes stay isolated
+    std::vector<std::vector<int32_t>> obs(pi.NL);
+    for (int k = 0; k < pi.Mb; ++k)
+        if (pi.b_pose[k] != pi.fixed) obs[pi.b_lm[k]].push_back(pi.b_pose[k]);
+    std::vector<std::vector<int32_t>> adj(pi.NP);
+    for (int l = 0; l < pi.NL; ++l) {
+        std::vector<int32_t>& o = obs[l];
+        std::sort(o.begin(), o.end());
+        o.erase(std::unique(o.begin(), o.end()), o.end());
+        for (size_t a = 0; a < o.size(); ++a)
+            for (size_t b = a + 1; b < o.size(); ++b) { adj[o[a]].push_back(o[b]); adj[o[b]].push_back(o[a]); }
+    }
+    for (int k = 0; k < pi.Mo; ++k) {
+        const int s = pi.o_src[k], d = pi.o_dst[k];
+        if (s == d || s == pi.fixed || d == pi.fixed) continue;
+        adj[s].push_back(d);
+        adj[d].push_back(s);
+    }
+    g.ptr.assign(g.n + 1, 0);
+    for (int u = 0; u < pi.NP; ++u) {
+        std::sort(adj[u].begin(), adj[u].end());
+        adj[u].erase(std::unique(adj[u].begin(), adj[u].end()), adj[u].end());
+        g.ptr[u + 1] = g.ptr[u] + (int64_t)adj[u].size();
+    }
+    for (int u = pi.NP; u < g.n; ++u) g.ptr[u + 1] = g.ptr[u];
+    g.adj.reserve(g.ptr[g.n]);
+    for (int u = 0; u < pi.NP; ++u) g.adj.insert(g.adj.end(), adj[u].begin(), adj[u].end());
+    return g;
+}
+
+int order_nodes(const ProblemIndex& pi, int mode, std::vector<int32_t>& node_pos,
                 std::vector<std::pair<int32_t, int32_t>>* blocks, OrderingReport& rep, std::string& err) {
     const int NP = pi.NP, NL = pi.NL, n = NP + NL;
+    const bool nd_only = mode == kFactorMultifrontal;
     const Graph g = build_graph(pi);
+    if (mode == kFactorSchur) {
+        // landmarks first, each its own supernode (ascending stix), then ND of the poses on S's graph
+        std::vector<int32_t> order;
+        order.reserve(n);
+        for (int l = 0; l < NL; ++l) {
+            order.push_back(NP + l);
+            if (blocks) blocks->push_back({l, l + 1});
+        }
+        std::vector<char> active(n, 0);
+        for (int u = 0; u < NP; ++u) active[u] = u != pi.fixed;
+        std::vector<int32_t> ord_p;
+        std::vector<std::pair<int32_t, int32_t>> pblocks;
+        nested_dissection(build_schur_graph(pi), active, ord_p, kMfLeaf, &pblocks);
+        if ((int)ord_p.size() != NP - 1) { err = "nested dissection of the pose graph lost nodes"; return BOS_ERR_INVALID; }
+        order.insert(order.end(), ord_p.begin(), ord_p.end());
+        if (blocks)
+            for (const auto& b : pblocks) blocks->push_back({b.first + NL, b.second + NL});
+        node_pos.assign(n, -1);
+        for (size_t i = 0; i < order.size(); ++i) node_pos[order[i]] = (int32_t)i;
+        const SymbCost c = symbolic(g, NP, node_pos, order, nullptr, nullptr);
+        rep.flops_nd = c.flops;
+        rep.nnz_nd = c.nnz;
+        rep.chosen = "schur-landmarks-first";
+        return BOS_OK;
+    }
     // last pose observing each landmark (temporal key)
     std::vector<int32_t> last_obs(NL, -1);
     for (int k = 0; k < pi.Mb; ++k) last_obs[pi.b_lm[k]] = std::max(last_obs[pi.b_lm[k]], pi.b_pose[k]);
@@ -342,7 +402,8 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     P = Plan();
     P.NP = NP; P.NL = NL; P.Mb = pi.Mb; P.Mo = pi.Mo; P.fixed = pi.fixed;
     std::vector<std::pair<int32_t, int32_t>> blocks;
-    int rc = order_nodes(pi, factor_mode == kFactorMultifrontal, P.node_pos, &blocks, P.ordering, err);
+    const bool multifrontal = factor_mode == kFactorMultifrontal || factor_mode == kFactorSchur;
+    int rc = order_nodes(pi, factor_mode, P.node_pos, &blocks, P.ordering, err);
     if (rc) return rc;
     const Graph g = build_graph(pi);
     const int m = n_nodes - 1;
@@ -428,7 +489,7 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     if ((rc = build_layout(pi, P, err))) return rc;
     build_ownership(pi, P, rank, world);
     if ((rc = build_csr_src(pi, P, inv, err))) return rc;
-    if (factor_mode == kFactorMultifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, err))) return rc;
+    if (multifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, err))) return rc;
     return validate_plan(pi, P, err);
 }
 

@@ -140,14 +140,19 @@ enum FactorMode {
     kFactorNone = 0,          // dense solver: pattern only
     kFactorScalar = 1,        // scalar CSR Cholesky pattern (rocSOLVER csrrf), cheapest-flops ordering
     kFactorMultifrontal = 2,  // nested dissection + supernodal multifrontal structure (GPU solver)
+    kFactorSchur = 3,         // multifrontal with every landmark eliminated first (its own leaf
+                              // supernode), then nested dissection of the poses on the graph of the
+                              // Schur complement S = H_pp - H_pl H_ll^-1 H_lp
 };
 
 // Builds the plan. Returns 0 or a negative BOS_ERR_* code with a message in err.
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& out, std::string& err);
 
-// Node ordering only (positions) and its symbolic cost. nd_only: force nested dissection and
-// return its blocks (contiguous position ranges: leaves and separators) in `blocks`.
-int order_nodes(const ProblemIndex& pi, bool nd_only, std::vector<int32_t>& node_pos,
+// Node ordering only (positions) and its symbolic cost. mode kFactorScalar / kFactorNone: the
+// cheapest of temporal, landmarks-first and nested dissection; kFactorMultifrontal: nested
+// dissection; kFactorSchur: landmarks first, then nested dissection of the poses on the graph of S.
+// The multifrontal modes return their supernode blocks (contiguous position ranges) in `blocks`.
+int order_nodes(const ProblemIndex& pi, int mode, std::vector<int32_t>& node_pos,
                 std::vector<std::pair<int32_t, int32_t>>* blocks, OrderingReport& rep, std::string& err);
 
 }  // namespace bos

@@ -131,10 +131,10 @@ def test_step_dx_matches_oracle(c1):
     assert np.abs(dxg - dxo).max() <= 1e-8 * np.abs(dxo).max()
 
 
-@pytest.mark.parametrize("other", [bos.BOS_SOLVER_DENSE_CHOL, bos.BOS_SOLVER_ROCSOLVER_RF])
+@pytest.mark.parametrize("other", [bos.BOS_SOLVER_DENSE_CHOL, bos.BOS_SOLVER_ROCSOLVER_RF, bos.BOS_SOLVER_SCHUR])
 def test_solvers_agree(c1, other):
-    """The supernodal multifrontal solver (default) against rocSOLVER dense potrf and
-    rocSOLVER csrrf on the same iterations."""
+    """The supernodal multifrontal solver (default) against rocSOLVER dense potrf, rocSOLVER
+    csrrf and the landmarks-first Schur-complement ordering on the same iterations."""
     A = bos.Solver(c1, solver=bos.BOS_SOLVER_SUPERNODAL)
     B = bos.Solver(c1, solver=other)
     A.step_n(5)

@@ -145,19 +145,21 @@ def test_plan_pattern_matches_oracle(which):
     assert set(perm[info["n"]:].tolist()) == {3 * P.fixed, 3 * P.fixed + 1, 3 * P.fixed + 2}
 
 
+@pytest.mark.parametrize("solver", ["supernodal", "schur"])
 @pytest.mark.parametrize("which", ["c1", "c2"])
-def test_multifrontal_structure_solves_like_scipy(which):
+def test_multifrontal_structure_solves_like_scipy(which, solver):
     """The supernodal tree and its maps (host/plan.cpp build_multifrontal) re-run on the host
     reproduce a SciPy solve of H_nf x = b."""
     P = bos.load_g2o(C1) if which == "c1" else bos.synthetic(1000, 2000, 20)
+    kind = bos.BOS_SOLVER_SCHUR if solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
     Q = to_oracle(P)
     lin = O.linearize(Q)
     Hl = oracle_lower_nf(Q, lin).tocsr()
-    info = bos.plan_inspect(P, entries=True)
+    info = bos.plan_inspect(P, entries=True, solver=kind)
     vals = np.asarray(Hl[info["rows"], info["cols"]]).ravel()
     n = info["n"]
     perm = info["perm_to_ref"][:n]
-    x = bos.plan_mf_selftest(P, vals, lin.b[perm])
+    x = bos.plan_mf_selftest(P, vals, lin.b[perm], solver=kind)
     Hf = (Hl + sp.tril(Hl, -1).T).tocsc()
     keep = np.ones(P.N, dtype=bool)
     keep[3 * P.fixed:3 * P.fixed + 3] = False
@@ -166,6 +168,9 @@ def test_multifrontal_structure_solves_like_scipy(which):
     xr[idx] = spla.spsolve(Hf[idx][:, idx], lin.b[idx])
     assert np.abs(x - xr[perm]).max() <= 1e-8 * np.abs(xr).max()
     assert info["mf_levels"] >= 1 and info["mf_max_front"] >= 3
+    if solver == "schur":   # every landmark is its own 2-column supernode, eliminated before any pose
+        assert info["ordering"] == "schur-landmarks-first"
+        assert info["mf_supernodes"] > P.NL and set(perm[:2 * P.NL].tolist()) == set(range(3 * P.NP, P.N))
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
