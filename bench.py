@@ -105,8 +105,9 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--gn-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--solver", choices=["supernodal", "schur"], default="supernodal",
-                    help="GN linear solver: nested-dissection multifrontal or landmarks-first Schur (config 5)")
+    ap.add_argument("--solver", choices=["supernodal", "schur"], default="schur",
+                    help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
+                         "nested-dissection multifrontal; the other one is timed too (gn_other)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -174,24 +175,32 @@ def main():
     value = nobs * args.steps / wall
 
     # ---- full GN iterations (J+H + exchange + solve + update)
-    gn_it_s, phase = None, None
-    if args.gn_steps > 0:
-        S.step()   # first iteration includes the one-time factorization analysis
+    def time_gn(solver_handle):
+        solver_handle.step()   # first iteration includes the one-time factorization analysis
         barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        gn_stats = []
-        for _ in range(args.gn_steps):
-            gn_stats.append(S.step())
+        stats = [solver_handle.step() for _ in range(args.gn_steps)]
         barrier()
         gn_wall = time.perf_counter() - tg
         if world > 1:
             t = torch.tensor([gn_wall], device="cuda", dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             gn_wall = float(t.item())
-        gn_it_s = args.gn_steps / gn_wall
-        phase = {k: float(np.median([g[k] for g in gn_stats])) for k in
-                 ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
+        ph = {k: float(np.median([g[k] for g in stats])) for k in
+              ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
+        return args.gn_steps / gn_wall, ph
+
+    gn_it_s, phase, gn_other = None, None, None
+    if args.gn_steps > 0:
+        gn_it_s, phase = time_gn(S)
+        if world == 1:   # the other multifrontal ordering on the same problem, for comparison
+            other = "supernodal" if args.solver == "schur" else "schur"
+            S2 = bos.Solver(P, precision=precision, device=local_rank, stream=stream.cuda_stream,
+                            solver=bos.BOS_SOLVER_SUPERNODAL if other == "supernodal" else bos.BOS_SOLVER_SCHUR)
+            it2, ph2 = time_gn(S2)
+            gn_other = {"solver": other, "gn_iters_per_s": it2, "t_solve_ms": ph2["t_solve_ms"]}
+            S2.close()
 
     if rank == 0:
         algo = info["algorithmic_bytes"]
@@ -219,6 +228,8 @@ def main():
             },
             "gn_iters_per_s": gn_it_s,
             "gn_phase_ms": phase,
+            "gn_solver": args.solver,
+            "gn_other": gn_other,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,

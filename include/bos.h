@@ -41,12 +41,12 @@ extern "C" {
 #define BOS_FP32 32
 
 /* linear solver for H_nf dx = -b_nf (the reference: Eigen SimplicialLDLT, slam/solver.hpp:71-72) */
-#define BOS_SOLVER_SUPERNODAL 0   /* GPU multifrontal supernodal Cholesky, nested dissection (default) */
+#define BOS_SOLVER_SUPERNODAL 0   /* GPU multifrontal supernodal Cholesky, nested dissection          */
 #define BOS_SOLVER_DENSE_CHOL 1   /* rocSOLVER potrf/potrs on a dense copy (small problems)          */
 #define BOS_SOLVER_ROCSOLVER_RF 2 /* rocSOLVER csrrf analysis/refactchol/solve (level-scheduled)      */
-#define BOS_SOLVER_SCHUR 3         /* same GPU engine, landmarks eliminated first: the pose fronts factor the
-                                      Schur complement S = H_pp - H_pl H_ll^-1 H_lp (config 5)          */
-#define BOS_SOLVER_SPARSE_CHOL BOS_SOLVER_SUPERNODAL
+#define BOS_SOLVER_SCHUR 3        /* same GPU engine, landmarks eliminated first (default): the pose fronts
+                                     factor the Schur complement S = H_pp - H_pl H_ll^-1 H_lp (config 5) */
+#define BOS_SOLVER_SPARSE_CHOL BOS_SOLVER_SCHUR
 
 /*
  * Problem in stix order (framework/state.hpp:47-53): poses in file order, landmarks in
@@ -75,7 +75,7 @@ typedef struct bos_problem {
 
 typedef struct bos_options {
     int32_t precision;              /* BOS_FP64 (default) or BOS_FP32                            */
-    int32_t solver;                 /* BOS_SOLVER_SUPERNODAL (default) / _DENSE_CHOL / _ROCSOLVER_RF / _SCHUR */
+    int32_t solver;                 /* BOS_SOLVER_SCHUR (default) / _SUPERNODAL / _DENSE_CHOL / _ROCSOLVER_RF */
     int32_t device;                 /* HIP device ordinal, -1 = current                          */
     int32_t rank;                   /* shard index (0 for one GPU)                               */
     int32_t world_size;             /* number of shards (1 for one GPU)                          */

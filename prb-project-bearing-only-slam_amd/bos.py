@@ -29,7 +29,7 @@ BOS_SOLVER_SUPERNODAL = 0
 BOS_SOLVER_DENSE_CHOL = 1
 BOS_SOLVER_ROCSOLVER_RF = 2
 BOS_SOLVER_SCHUR = 3
-BOS_SOLVER_SPARSE_CHOL = BOS_SOLVER_SUPERNODAL
+BOS_SOLVER_SPARSE_CHOL = BOS_SOLVER_SCHUR
 
 # every symbol declared in include/bos.h and include/bos_host.h
 EXPORTED_SYMBOLS = [

@@ -36,6 +36,7 @@ constexpr int kMfBlock = 256;
 constexpr int kLdsCapM = 90;   // larger fronts up to 90 x 90 doubles (64.8 KB) are factored in LDS
 
 __device__ __forceinline__ int64_t pk(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }
+__device__ __forceinline__ int pk32(int i, int j, int m) { return j * m - j * (j - 1) / 2 + (i - j); }   // LDS fronts
 
 // Copy n doubles global -> LDS by one wavefront, 8 independent loads in flight per lane.
 __device__ __forceinline__ void stage_lds(double* dst, const double* src, int n, int lane) {
@@ -98,6 +99,20 @@ struct MfArgs {
     double* scratch;
     double* x;                   // rhs in, solution out (permuted order)
     int32_t* info;               // count of non-positive pivots
+    const int32_t* fold_cnt;     // folded landmark children (Schur ordering, see plan.hpp)
+    const int32_t* fold_cptr;
+    const int32_t* fold_chunk;
+    const int32_t* fold_rec;
+};
+
+// LDS of one wave's folded rows: L[t, 0..1] of the landmark, the row's u entry, its position p in
+// the parent front with the packed column base cb(p) (packed index of (i, p) = cb(p) + i), and the
+// landmark's r
+struct FoldBuf {
+    double2 l[kFoldChunk];
+    double u[kFoldChunk];
+    int2 pc[kFoldChunk];
+    int rc[kFoldChunk];
 };
 
 // Assembly of H entries into a front by one wavefront (F[dst] = A[src]), 4 entries per lane in
@@ -256,6 +271,91 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Folded landmark children (Schur ordering) of front s, eliminated by its wave: per chunk (whole
+// children, <= 64 rows) lane q takes row t of landmark c (one 32-byte record: sources of its two
+// entries, of the landmark's 2 x 2 block, the landmark's col0 / r / L offset and the row's position
+// in this front), factors the 2 x 2 block, forms L[t, 0..1], the landmark's forward step y and the
+// row's u entry, and writes the landmark's L panel and y. The landmarks' update matrices
+// -L21 L21^T and u-vectors are then extend-added into this front one landmark at a time (pairs of
+// rows across lanes; positions of one landmark are distinct): deterministic, and nothing goes
+// through global memory. Same arithmetic as the generic path up to rounding.
+__device__ __forceinline__ int4 fold_rec_load(const MfArgs& a, int q, int half) {
+    return reinterpret_cast<const int4*>(a.fold_rec + (int64_t)kFoldRec * q)[half];
+}
+
+__device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F, double* wv, FoldBuf* fb, int m,
+                                              int lane) {
+    const int ch0 = a.fold_cptr[s], ch1 = a.fold_cptr[s + 1];
+    int q0 = a.fold_chunk[ch0], n = a.fold_chunk[ch0 + 1] - q0;
+    int4 r0 = make_int4(-1, -1, -1, -1), r1 = make_int4(0, 0, 0, 0);
+    if (lane < n) { r0 = fold_rec_load(a, q0 + lane, 0); r1 = fold_rec_load(a, q0 + lane, 1); }
+    for (int ch = ch0; ch < ch1; ++ch) {
+        // this chunk's values, then the next chunk's records (in flight during this chunk's work)
+        const double ht0 = r0.x >= 0 ? a.A[r0.x] : 0.0, ht1 = r0.y >= 0 ? a.A[r0.y] : 0.0;
+        const double a00 = r0.z >= 0 ? a.A[r0.z] : 0.0, a10 = r0.w >= 0 ? a.A[r0.w] : 0.0;
+        const double a11 = r1.x >= 0 ? a.A[r1.x] : 0.0;
+        const int col0 = r1.y, t = r1.z & 63, rc = (r1.z >> 6) & 63, pos = r1.z >> 12;
+        const bool mine = lane < n;
+        const double x0 = mine ? a.x[col0] : 0.0, x1 = mine ? a.x[col0 + 1] : 0.0;
+        const int64_t loff = r1.w;
+        const int nn = ch + 1 < ch1 ? a.fold_chunk[ch + 2] - a.fold_chunk[ch + 1] : 0;
+        if (lane < nn) {
+            r0 = fold_rec_load(a, a.fold_chunk[ch + 1] + lane, 0);
+            r1 = fold_rec_load(a, a.fold_chunk[ch + 1] + lane, 1);
+        }
+        if (mine) {
+            double d0 = a00;
+            int bad = 0;
+            if (!(d0 > 0.0)) { d0 = 1e-300; ++bad; }
+            const double l00 = sqrt(d0), i0 = 1.0 / l00;
+            const double l10 = a10 * i0;
+            double d1 = a11 - l10 * l10;
+            if (!(d1 > 0.0)) { d1 = 1e-300; ++bad; }
+            const double l11 = sqrt(d1), i1 = 1.0 / l11;
+            const double lt0 = ht0 * i0, lt1 = (ht1 - lt0 * l10) * i1;
+            const double y0 = x0 * i0, y1 = (x1 - l10 * y0) * i1;
+            const int mc = 2 + rc;
+            double* Lc = a.L + loff;
+            Lc[2 + t] = lt0;
+            Lc[mc + 2 + t] = lt1;
+            if (t == 0) {
+                Lc[0] = l00;
+                Lc[1] = l10;
+                Lc[mc + 1] = l11;
+                a.x[col0] = y0;
+                a.x[col0 + 1] = y1;
+                if (bad) atomicAdd(a.info, bad);
+            }
+            fb->l[lane] = make_double2(lt0, lt1);
+            fb->u[lane] = -(lt0 * y0 + lt1 * y1);
+            fb->pc[lane] = make_int2(pos, pos * m - pos * (pos - 1) / 2 - pos);
+            fb->rc[lane] = rc;
+        }
+        wave_sync();
+        // one landmark at a time: its packed r x r pairs across lanes, (row, column) in closed form
+        for (int c0 = 0; c0 < n;) {
+            const int rcc = fb->rc[c0];
+            const int ne = rcc * (rcc + 1) / 2;
+            const float b = 2.0f * rcc + 1.0f;
+            for (int e = lane; e < ne; e += 64) {
+                int j = (int)((b - sqrtf(b * b - 8.0f * e)) * 0.5f);
+                int sj = j * rcc - j * (j - 1) / 2;
+                if (sj > e) { --j; sj = j * rcc - j * (j - 1) / 2; }
+                else if (sj + (rcc - j) <= e) { sj += rcc - j; ++j; }
+                const int i = j + (e - sj);
+                const double2 li = fb->l[c0 + i], lj = fb->l[c0 + j];
+                const int pi = fb->pc[c0 + i].x, cbj = fb->pc[c0 + j].y;
+                F[cbj + pi] -= li.x * lj.x + li.y * lj.y;
+            }
+            if (lane < rcc) wv[fb->pc[c0 + lane].x] += fb->u[c0 + lane];
+            wave_sync();
+            c0 += rcc;
+        }
+        q0 = ch + 1 < ch1 ? a.fold_chunk[ch + 1] : 0;
+        n = nn;
+    }
+}
+
 // Factorization of one front fused with its forward elimination: w (LDS, m doubles) receives the
 // front's right-hand side (x of its own dofs) plus the children's u-vectors, extend-added with
 // their update matrices; after the partial Cholesky, lane i eliminates with its row of L (still in
@@ -263,8 +363,9 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
 // front's u-vector for its parent.
 template <int MAXM, bool COH>
 __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf, int* smap,
-                                                 double* wv, int lane) {
+                                                 double* wv, FoldBuf* fb, int lane) {
     const int k = a.k[s], r = a.r[s], m = k + r;
+    const int nfold = a.fold_cnt[s];
     const int c0 = a.col0[s];
     const int np = m * (m + 1) / 2;
     const double xo = lane < k ? a.x[c0 + lane] : 0.0;   // right-hand side of the own dofs (k < 64)
@@ -273,10 +374,11 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     wave_sync();
     assemble_wave(a, s, F, lane);
     wave_sync();
+    if (nfold > 0) fold_children(a, s, F, wv, fb, m, lane);
     // extend-add: the child's row map staged in LDS, its packed update matrix swept by all lanes
     // (contiguous loads, 4 in flight; (row, column) decoded incrementally). Positions of one
     // child are distinct.
-    for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {
+    for (int ci = a.child_ptr[s] + nfold; ci < a.child_ptr[s + 1]; ++ci) {
         const int c = a.child[ci];
         const int rc = a.r[c];   // rc < m <= MAXM
         if (lane < rc) smap[lane] = a.rmap[a.rmap_off[c] + lane];
@@ -293,7 +395,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 if (len > 0) {
-                    F[pk(smap[j + o], smap[j], m)] += v[u];
+                    F[pk32(smap[j + o], smap[j], m)] += v[u];
                     o += 64;
                     while (len > 0 && o >= len) { o -= len; ++j; --len; }
                 }
@@ -306,7 +408,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     double row[MAXM];
     double myinv = 0.0;
 #pragma unroll
-    for (int c = 0; c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk(lane, c, m)] : 0.0;
+    for (int c = 0; c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk32(lane, c, m)] : 0.0;
     // Right-looking: step j broadcasts column j through a double-buffered LDS column (one store
     // per lane, same-address reads). Entries above the diagonal (c > lane) and rows >= m are
     // scratch, so the updates need no predicates.
@@ -362,7 +464,8 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double colbuf[2 * MAXM];
     __shared__ __attribute__((aligned(16))) double wv[MAXM];
     __shared__ int smap[64];
-    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, smap, wv, threadIdx.x);
+    __shared__ FoldBuf fb;
+    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, smap, wv, &fb, threadIdx.x);
 }
 
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
@@ -401,6 +504,28 @@ template <bool COH> __device__ __forceinline__ void backward_front(const MfArgs&
 __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
     extern __shared__ __attribute__((aligned(16))) double w[];
     backward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x);
+}
+
+// Backward substitution of the folded landmarks (k = 2), one thread each: t = L21^T x_rows, then
+// x1 = (y1 - t1) / L11, x0 = (y0 - t0 - L10 x1) / L00.
+__global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
+    const int i = blockIdx.x * kMfBlock + threadIdx.x;
+    if (i >= a.count) return;
+    const int s = a.level[i];
+    const int r = a.r[s], m = 2 + r, c0 = a.col0[s];
+    const double* Ls = a.L + a.L_off[s];
+    const int32_t* fi = a.findex + a.findex_off[s] + 2;
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll 4
+    for (int q = 0; q < r; ++q) {
+        const double xv = a.x[fi[q]];
+        t0 += Ls[2 + q] * xv;
+        t1 += Ls[m + 2 + q] * xv;
+    }
+    const double x1 = (a.x[c0 + 1] - t1) / Ls[m + 1];
+    t0 += Ls[1] * x1;
+    a.x[c0] = (a.x[c0] - t0) / Ls[0];
+    a.x[c0 + 1] = x1;
 }
 
 // ---- dataflow (work-queue) kernels: one launch walks a whole tree range. A wavefront takes the
@@ -461,6 +586,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
     __shared__ __attribute__((aligned(16))) double colbuf[2 * kFlowMaxM];
     __shared__ __attribute__((aligned(16))) double wv[kFlowMaxM];
     __shared__ int smap[64];
+    __shared__ FoldBuf fb;
     const int lane = threadIdx.x;
     // a wave takes at most n + 1 tickets: the loop is bounded (an unbounded for (;;) version of
     // this kernel never terminated on gfx950 / ROCm 7.2)
@@ -470,7 +596,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
         const int s = f.order[t];
         for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci)
             if (f.slev[a.child[ci]] >= f.lev0) wait_done(f, a.child[ci], a.info);
-        factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, smap, wv, lane);   // m <= kFlowMaxM
+        factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, smap, wv, &fb, lane);   // m <= kFlowMaxM
         publish_done(f, s);
     }
 }
@@ -522,6 +648,9 @@ struct MfDevice {
     uint32_t* done = nullptr;   // [3][nsuper]: factor, forward, backward
     int* tickets = nullptr;     // [3]
     uint32_t epoch = 0;
+    int32_t *fold_cnt = nullptr, *fold_cptr = nullptr, *fold_chunk = nullptr, *fold_rec = nullptr,
+            *fold_list = nullptr;
+    int n_fold = 0;
     int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
             *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
             *info = nullptr;
@@ -545,6 +674,7 @@ struct MfDevice {
         g.scratch_off = scratch_off; g.child_ptr = child_ptr; g.child = child; g.rmap_off = rmap_off; g.rmap = rmap;
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
         g.findex = findex; g.A = A; g.L = L; g.U = U; g.u = u; g.scratch = scratch; g.x = x; g.info = info;
+        g.fold_cnt = fold_cnt; g.fold_cptr = fold_cptr; g.fold_chunk = fold_chunk; g.fold_rec = fold_rec;
         return g;
     }
 };
@@ -633,8 +763,12 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         (rc = up(&d->amap_src, F.amap_src, err)) || (rc = up(&d->amap_dst, F.amap_dst, err)) ||
         (rc = up(&d->findex, F.findex, err)) || (rc = up(&d->L_off, F.L_off, err)) || (rc = up(&d->U_off, F.U_off, err)) ||
         (rc = up(&d->u_off, F.u_off, err)) || (rc = up(&d->scratch_off, scr, err)) ||
-        (rc = up(&d->rmap_off, F.rmap_off, err)) || (rc = up(&d->findex_off, F.findex_off, err)))
+        (rc = up(&d->rmap_off, F.rmap_off, err)) || (rc = up(&d->findex_off, F.findex_off, err)) ||
+        (rc = up(&d->fold_cnt, F.fold_cnt, err)) || (rc = up(&d->fold_cptr, F.fold_cptr, err)) ||
+        (rc = up(&d->fold_chunk, F.fold_chunk, err)) || (rc = up(&d->fold_rec, F.fold_rec, err)) ||
+        (rc = up(&d->fold_list, F.fold_list, err)))
         return rc;
+    d->n_fold = (int)F.fold_list.size();
     auto alloc = [&](double** p, int64_t n) -> int {
         if (n <= 0) n = 1;
         if (hipMalloc((void**)p, n * sizeof(double)) != hipSuccess) { err = "hipMalloc failed (multifrontal buffers)"; return -2; }
@@ -650,7 +784,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
 
 void mf_destroy(MfDevice* d) {
     if (!d) return;
-    void* bufs[] = {d->order_factor, d->order_bwd, d->slev, d->parent, d->done, d->tickets, d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
+    void* bufs[] = {d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->fold_list, d->order_factor, d->order_bwd, d->slev, d->parent, d->done, d->tickets, d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
     for (void* b : bufs)
@@ -705,6 +839,13 @@ hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
             hipLaunchKernelGGL(mf_backward_wave, dim3(n), dim3(64), d->lds_max(d->lds_bwd, l, 0, 4), s, d->args(l, 0, nullptr, x));
         if ((n = d->count(l, 4)))
             hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), d->lds_bwd[l * kClasses + 4], s, d->args(l, 4, nullptr, x));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (d->n_fold > 0) {   // folded landmarks last: their rows are poses, final by now
+        MfArgs g = d->args(0, 0, nullptr, x);
+        g.level = d->fold_list;
+        g.count = d->n_fold;
+        hipLaunchKernelGGL(mf_backward_fold, dim3((d->n_fold + kMfBlock - 1) / kMfBlock), dim3(kMfBlock), 0, s, g);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;

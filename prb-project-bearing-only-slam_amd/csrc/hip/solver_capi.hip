@@ -474,7 +474,13 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     if (rocblas_create_handle(&s->rb) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "rocblas_create_handle"));
     if (rocblas_set_stream(s->rb, s->stream) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "rocblas_set_stream"));
     if (s->solver_kind == BOS_SOLVER_ROCSOLVER_RF) {
-        if (rocsolver_create_rfinfo(&s->rf, s->rb) != rocblas_status_success) return bail(fail(BOS_ERR_SOLVER, "create_rfinfo"));
+        const rocblas_status st = rocsolver_create_rfinfo(&s->rf, s->rb);
+        if (st != rocblas_status_success) {
+            size_t fr = 0, tot = 0;
+            (void)hipMemGetInfo(&fr, &tot);
+            return bail(fail(BOS_ERR_SOLVER, "rocsolver_create_rfinfo: status " + std::to_string((int)st) +
+                                                 ", device memory free " + std::to_string(fr >> 20) + " MiB"));
+        }
         if (rocsolver_set_rfinfo_mode(s->rf, rocsolver_rfinfo_mode_cholesky) != rocblas_status_success)
             return bail(fail(BOS_ERR_SOLVER, "set_rfinfo_mode"));
     }

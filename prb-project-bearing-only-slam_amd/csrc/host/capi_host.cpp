@@ -274,6 +274,39 @@ int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* va
     for (int64_t e = 0; e < P.nnzA(); ++e) hval[P.blk.csr_src[e]] = vals[e];
     std::vector<double> L(F.L_size), U(F.U_size), u(F.u_size);
     for (int64_t i = 0; i < P.n; ++i) x[i] = rhs[i];
+    // folded landmark children (Schur ordering): the fold records, as hip/multifrontal.hip
+    // fold_children reads them; their u entries accumulate per parent in fwv
+    std::vector<std::vector<double>> fwv(F.nsuper);
+    auto fold = [&](int s, std::vector<double>& W, int m) {
+        fwv[s].assign(m, 0.0);
+        for (int ch = F.fold_cptr[s]; ch < F.fold_cptr[s + 1]; ++ch) {
+            const int q0 = F.fold_chunk[ch], n = F.fold_chunk[ch + 1] - q0;
+            std::vector<double> l0(n), l1(n);
+            std::vector<int> pos(n), rcs(n);
+            for (int q = 0; q < n; ++q) {
+                const int32_t* rec = F.fold_rec.data() + (size_t)bos::kFoldRec * (q0 + q);
+                auto v = [&](int32_t src) { return src >= 0 ? hval[src] : 0.0; };
+                const int col0 = rec[5], t = rec[6] & 63, rc = (rec[6] >> 6) & 63;
+                const double l00 = std::sqrt(std::max(v(rec[2]), 1e-300)), l10 = v(rec[3]) / l00;
+                const double l11 = std::sqrt(std::max(v(rec[4]) - l10 * l10, 1e-300));
+                l0[q] = v(rec[0]) / l00;
+                l1[q] = (v(rec[1]) - l0[q] * l10) / l11;
+                const double y0 = rhs[col0] / l00, y1 = (rhs[col0 + 1] - l10 * y0) / l11;
+                double* Lc = L.data() + rec[7];
+                const int mc = 2 + rc;
+                Lc[2 + t] = l0[q];
+                Lc[mc + 2 + t] = l1[q];
+                if (t == 0) { Lc[0] = l00; Lc[1] = l10; Lc[mc + 1] = l11; x[col0] = y0; x[col0 + 1] = y1; }
+                pos[q] = rec[6] >> 12;
+                rcs[q] = rc;
+                fwv[s][pos[q]] -= l0[q] * y0 + l1[q] * y1;
+            }
+            for (int c0 = 0; c0 < n; c0 += rcs[c0])
+                for (int j = c0; j < c0 + rcs[c0]; ++j)
+                    for (int i = j; i < c0 + rcs[c0]; ++i)
+                        W[pos[i] + (size_t)pos[j] * m] -= l0[i] * l0[j] + l1[i] * l1[j];
+        }
+    };
     for (int lv = 0; lv < F.nlevels; ++lv)
         for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
             const int s = F.level[q], k = F.k[s], r = F.r[s], m = k + r;
@@ -287,7 +320,8 @@ int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* va
                 }
                 W[d] = hval[F.amap_src[a]];
             }
-            for (int ci = F.child_ptr[s]; ci < F.child_ptr[s + 1]; ++ci) {
+            fold(s, W, m);
+            for (int ci = F.child_ptr[s] + F.fold_cnt[s]; ci < F.child_ptr[s + 1]; ++ci) {
                 const int c = F.child[ci], rc2 = F.r[c];
                 const int32_t* map = F.rmap.data() + F.rmap_off[c];
                 for (int j = 0; j < rc2; ++j)
@@ -310,7 +344,8 @@ int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* va
             const int s = F.level[q], k = F.k[s], r = F.r[s], m = k + r;
             std::vector<double> w(m, 0.0);
             for (int i = 0; i < k; ++i) w[i] = x[F.col0[s] + i];
-            for (int ci = F.child_ptr[s]; ci < F.child_ptr[s + 1]; ++ci) {
+            for (size_t i = 0; i < fwv[s].size(); ++i) w[i] += fwv[s][i];
+            for (int ci = F.child_ptr[s] + F.fold_cnt[s]; ci < F.child_ptr[s + 1]; ++ci) {
                 const int c = F.child[ci];
                 for (int t = 0; t < F.r[c]; ++t) w[F.rmap[F.rmap_off[c] + t]] += u[F.u_off[c] + t];
             }
@@ -322,17 +357,18 @@ int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* va
             for (int i = 0; i < k; ++i) x[F.col0[s] + i] = w[i];
             for (int t = 0; t < r; ++t) u[F.u_off[s] + t] = w[k + t];
         }
-    for (int lv = F.nlevels - 1; lv >= 0; --lv)
-        for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
-            const int s = F.level[q], k = F.k[s], m = k + F.r[s];
-            const double* Ls = L.data() + F.L_off[s];
-            const int32_t* fi = F.findex.data() + F.findex_off[s];
-            for (int j = k - 1; j >= 0; --j) {
-                double acc = x[F.col0[s] + j];
-                for (int i = j + 1; i < m; ++i) acc -= Ls[i + (size_t)j * m] * x[fi[i]];
-                x[F.col0[s] + j] = acc / Ls[j + (size_t)j * m];
-            }
+    std::vector<int32_t> bwd(F.level.rbegin(), F.level.rend());   // top-down, folded landmarks last
+    bwd.insert(bwd.end(), F.fold_list.begin(), F.fold_list.end());
+    for (int s : bwd) {
+        const int k = F.k[s], m = k + F.r[s];
+        const double* Ls = L.data() + F.L_off[s];
+        const int32_t* fi = F.findex.data() + F.findex_off[s];
+        for (int j = k - 1; j >= 0; --j) {
+            double acc = x[F.col0[s] + j];
+            for (int i = j + 1; i < m; ++i) acc -= Ls[i + (size_t)j * m] * x[fi[i]];
+            x[F.col0[s] + j] = acc / Ls[j + (size_t)j * m];
         }
+    }
     return BOS_OK;
 }
 

@@ -12,6 +12,9 @@ namespace bos {
 namespace {
 
 constexpr int kMfLeaf = 12;          // nested-dissection leaf size (nodes) for the multifrontal solver
+// pose leaves of the Schur ordering: 10 keeps the leaf fronts (poses + their landmarks' rows) within
+// one wavefront (m <= 64, so every landmark folds) at config 3; 6 / 8 / 12 measured slower
+constexpr int kSchurLeaf = 10;
 
 inline int node_size(int u, int NP) { return u < NP ? 3 : 2; }
 
@@ -301,7 +304,7 @@ int order_nodes(const ProblemIndex& pi, int mode, std::vector<int32_t>& node_pos
         for (int u = 0; u < NP; ++u) active[u] = u != pi.fixed;
         std::vector<int32_t> ord_p;
         std::vector<std::pair<int32_t, int32_t>> pblocks;
-        nested_dissection(build_schur_graph(pi), active, ord_p, kMfLeaf, &pblocks);
+        nested_dissection(build_schur_graph(pi), active, ord_p, kSchurLeaf, &pblocks);
         if ((int)ord_p.size() != NP - 1) { err = "nested dissection of the pose graph lost nodes"; return BOS_ERR_INVALID; }
         order.insert(order.end(), ord_p.begin(), ord_p.end());
         if (blocks)
@@ -376,7 +379,7 @@ void build_ownership(const ProblemIndex& pi, Plan& P, int rank, int world);
 int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& inv, std::string& err);
 
 int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
-                       const std::vector<std::pair<int32_t, int32_t>>& blocks, std::string& err);
+                       const std::vector<std::pair<int32_t, int32_t>>& blocks, int n_fold_cand, std::string& err);
 
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& P, std::string& err) {
     const bool want_factor = factor_mode == kFactorScalar;
@@ -489,7 +492,9 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     if ((rc = build_layout(pi, P, err))) return rc;
     build_ownership(pi, P, rank, world);
     if ((rc = build_csr_src(pi, P, inv, err))) return rc;
-    if (multifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, err))) return rc;
+    // Schur: the first NL blocks are the landmarks, candidates for folding into their parents
+    const int n_fold_cand = factor_mode == kFactorSchur ? NL : 0;
+    if (multifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, n_fold_cand, err))) return rc;
     return validate_plan(pi, P, err);
 }
 
@@ -719,7 +724,7 @@ int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& i
 }
 
 int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
-                       const std::vector<std::pair<int32_t, int32_t>>& blocks, std::string& err) {
+                       const std::vector<std::pair<int32_t, int32_t>>& blocks, int n_fold_cand, std::string& err) {
     const int m = (int)inv.size();
     Multifrontal& F = P.mf;
     F = Multifrontal();
@@ -792,6 +797,26 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
         std::vector<int32_t> w(F.child_ptr.begin(), F.child_ptr.end() - 1);
         for (int s = 0; s < ns; ++s) if (F.parent[s] >= 0) F.child[w[F.parent[s]]++] = s;
     }
+    // folding (Schur ordering): a parent factored by one wavefront takes all its landmark children
+    // (2-column leaves with m <= kMfWaveMaxM) into its own front; children lists are ascending, so
+    // the landmark supernodes (ids < n_fold_cand) come first
+    F.fold_cnt.assign(ns, 0);
+    std::vector<char> folded(ns, 0);
+    for (int p = 0; p < ns && n_fold_cand > 0; ++p) {
+        if (F.k[p] + F.r[p] > kMfWaveMaxM) continue;
+        int nf = 0;
+        bool ok = true;
+        for (int ci = F.child_ptr[p]; ci < F.child_ptr[p + 1]; ++ci) {
+            const int c = F.child[ci];
+            if (c >= n_fold_cand) break;
+            ok = ok && F.k[c] == 2 && F.k[c] + F.r[c] <= kMfWaveMaxM && F.r[c] <= kFoldChunk &&
+                 F.child_ptr[c] == F.child_ptr[c + 1];
+            ++nf;
+        }
+        if (!ok || nf == 0) continue;
+        F.fold_cnt[p] = nf;
+        for (int ci = F.child_ptr[p]; ci < F.child_ptr[p] + nf; ++ci) folded[F.child[ci]] = 1;
+    }
     F.rmap_off.resize(ns + 1);
     F.L_off.resize(ns); F.U_off.resize(ns); F.u_off.resize(ns);
     std::vector<int32_t> lev(ns, 0);
@@ -811,7 +836,7 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
                 if (fp < 0) { err = "multifrontal: update row missing from the parent front"; return BOS_ERR_INVALID; }
                 F.rmap.push_back(fp);
             }
-            lev[p] = std::max(lev[p], lev[s] + 1);
+            if (!folded[s]) lev[p] = std::max(lev[p], lev[s] + 1);
         } else if (r != 0) {
             err = "multifrontal: root with update rows";
             return BOS_ERR_INVALID;
@@ -822,13 +847,15 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
     const bool stats = std::getenv("BOS_MF_STATS") != nullptr;   // diagnostics: per-level front sizes
     for (int s = 0; s < ns; ++s) F.nlevels = std::max(F.nlevels, lev[s] + 1);
     F.level_ptr.assign(F.nlevels + 1, 0);
-    for (int s = 0; s < ns; ++s) ++F.level_ptr[lev[s] + 1];
+    for (int s = 0; s < ns; ++s) if (!folded[s]) ++F.level_ptr[lev[s] + 1];
     for (int l = 0; l < F.nlevels; ++l) F.level_ptr[l + 1] += F.level_ptr[l];
-    F.level.resize(ns);
+    F.level.resize(F.level_ptr[F.nlevels]);
     {
         std::vector<int32_t> w(F.level_ptr.begin(), F.level_ptr.end() - 1);
-        for (int s = 0; s < ns; ++s) F.level[w[lev[s]]++] = s;
+        for (int s = 0; s < ns; ++s) if (!folded[s]) F.level[w[lev[s]]++] = s;
     }
+    F.fold_list.clear();
+    for (int s = 0; s < ns; ++s) if (folded[s]) F.fold_list.push_back(s);
     if (stats)
         for (int l = 0; l < F.nlevels; ++l) {
             double sk = 0, sr = 0, fl = 0;
@@ -878,6 +905,38 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
             F.amap_dst[q] = dst[e];
         }
     }
+    // fold records, one per row t of a folded child c (parents in id order, their folded children
+    // in child-list order): {src (t, 0), src (t, 1), src (0, 0), src (1, 0), src (1, 1), col0[c],
+    // t | r[c] << 6 | (row t's position in the parent front) << 12, L_off[c]}; src = block-array
+    // index of the front entry (-1: structurally zero)
+    F.fold_cptr.assign(ns + 1, 0);
+    F.fold_chunk.clear();
+    F.fold_rec.clear();
+    if (!F.fold_list.empty() && F.L_size > INT32_MAX) { err = "multifrontal: factor too large for folding"; return BOS_ERR_UNSUPPORTED; }
+    int32_t nrows = 0;
+    for (int p = 0; p < ns; ++p) {
+        F.fold_cptr[p] = (int32_t)F.fold_chunk.size();
+        int32_t chunk_rows = kFoldChunk;   // forces a new chunk at the parent's first child
+        for (int ci = F.child_ptr[p]; ci < F.child_ptr[p] + F.fold_cnt[p]; ++ci) {
+            const int c = F.child[ci], rc = F.r[c], mc = 2 + rc;
+            if (chunk_rows + rc > kFoldChunk) { F.fold_chunk.push_back(nrows); chunk_rows = 0; }
+            std::vector<int32_t> src((size_t)mc * 2, -1);   // (i, j) -> i + j * mc
+            for (int q = F.amap_ptr[c]; q < F.amap_ptr[c + 1]; ++q) {
+                int64_t d = F.amap_dst[q], j = 0;
+                while (d >= mc - j) { d -= mc - j; ++j; }
+                src[(j + d) + j * mc] = F.amap_src[q];
+            }
+            for (int t = 0; t < rc; ++t) {
+                const int32_t rec[kFoldRec] = {src[2 + t], src[2 + t + mc], src[0], src[1], src[1 + mc], F.col0[c],
+                                               t | rc << 6 | F.rmap[F.rmap_off[c] + t] << 12, (int32_t)F.L_off[c]};
+                F.fold_rec.insert(F.fold_rec.end(), rec, rec + kFoldRec);
+            }
+            chunk_rows += rc;
+            nrows += rc;
+        }
+    }
+    F.fold_cptr[ns] = (int32_t)F.fold_chunk.size();
+    F.fold_chunk.push_back(nrows);
     return BOS_OK;
 }
 

@@ -92,6 +92,8 @@ struct OrderingReport {
 //  - update matrices U are packed lower-triangular column-major (r (r + 1) / 2 values) for all.
 //  - L panels are m x k column-major (entries above the diagonal unused).
 constexpr int kMfWaveMaxM = 64;
+constexpr int kFoldChunk = 64;   // folded rows per chunk (one per lane)
+constexpr int kFoldRec = 8;      // ints per folded row
 inline int64_t mf_packed(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }   // i >= j
 
 struct Multifrontal {
@@ -109,6 +111,16 @@ struct Multifrontal {
     std::vector<int32_t> amap_ptr;          // per supernode: range into amap_src / amap_dst
     std::vector<int32_t> amap_src, amap_dst;// block-array value (BlockLayout) -> front position (see above)
     std::vector<int32_t> level_ptr, level;  // supernodes grouped by tree level (leaves first)
+    // Schur ordering: landmark supernodes (k = 2, leaves) are folded into their parent's front when
+    // the parent is factored by one wavefront (m <= kMfWaveMaxM): the parent's wave eliminates them
+    // itself (no launch, no update matrix). Folded supernodes are in no level list (the parent's
+    // level ignores them); fold_list holds them for the backward substitution.
+    std::vector<int32_t> fold_cnt;          // per supernode: #folded children (the first of its child list)
+    std::vector<int32_t> fold_cptr;         // per supernode: its chunks [fold_cptr[s], fold_cptr[s + 1])
+    std::vector<int32_t> fold_chunk;        // chunk c = folded rows [fold_chunk[c], fold_chunk[c + 1]):
+                                            // whole children, <= kFoldChunk rows
+    std::vector<int32_t> fold_rec;          // kFoldRec ints per folded row (layout: build_multifrontal)
+    std::vector<int32_t> fold_list;         // folded supernodes
     int64_t L_size = 0, U_size = 0, u_size = 0;
     double flops = 0;
 };

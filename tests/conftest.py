@@ -10,6 +10,14 @@ for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# Load the product library (and the ROCm 7.2 libraries it links) before any test module imports
+# torch: torch bundles its own ROCm runtime under the same sonames, and whichever loads first serves
+# the whole process. The tests exercise the library as shipped (system ROCm); bench.py, which needs
+# torch first, documents that it runs on torch's bundled runtime.
+import bos  # noqa: E402
+
+bos.lib()
+
 DATA = os.path.join(ROOT, "tests", "golden", "data")
 C1 = os.path.join(DATA, "slam2D_bearing_only_initial_guess.g2o")
 C1_GT = os.path.join(DATA, "slam2D_bearing_only_ground_truth.g2o")

@@ -6,7 +6,7 @@ import sys
 path = glob.glob(sys.argv[1] + "/**/run_kernel_trace.csv", recursive=True)[0]
 rows = list(csv.DictReader(open(path)))
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
-names = ["mf_factor_flow", "mf_backward_flow", "mf_factor_reg", "mf_factor_wave", "mf_factor_level", "mf_forward_wave", "mf_forward_level", "mf_backward_wave",
+names = ["mf_factor_flow", "mf_backward_flow", "mf_factor_reg", "mf_factor_wave", "mf_factor_level", "mf_forward_wave", "mf_forward_level", "mf_backward_wave", "mf_backward_fold",
          "mf_backward_level", "linearize_kernel", "gather_f64", "to_f64", "boxplus", "reduce_stats"]
 # the last GN step: from the last linearize launch followed by a factor launch
 idx = [i for i, r in enumerate(rows) if "linearize_kernel" in r["Kernel_Name"]]
