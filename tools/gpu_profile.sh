@@ -1,19 +1,27 @@
-# Profiles of the J+H kernel on config 3, run on the GPU box from the repo root:
-#   1. rocprofv3 --kernel-trace --stats of the default bench command (fp32) and of the fp64 bench
-#   2. PMC passes, one counter group each (never together with tracing domains):
-#      L2<->fabric read requests by size | write requests by size | SQ wave/issue counters
-# Usage: bash tools/gpu_profile.sh TAG      (outputs under gpurun_out/prof_TAG_*)
+# Profile set for the committed numbers ($1 = tag, e.g. r01): for fp32 and fp64 J+H builds
+#   * the bench command under rocprofv3 --kernel-trace --stats (bench JSON + kernel stats)
+#   * three separate --pmc passes on the J+H kernel (read requests by size | writes | SQ)
+# Results land in gpurun_out/prof_<tag>/; copy the summaries into profiles/ afterwards.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-r01}
-for PREC in fp32 fp64; do
-  O=gpurun_out/prof_${TAG}_${PREC}
-  mkdir -p $O
-  if [ $PREC = fp32 ]; then B="python3 bench.py"; else B="python3 bench.py --precision fp64"; fi
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B > $O/bench.json 2> $O/trace.err || exit 1
-  P="python3 bench.py --steps 20 --warmup 2 --gn-steps 0 --no-cpu-baseline --precision $PREC"
-  timeout -k 10 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --kernel-include-regex linearize -d $O/rd -o run --output-format csv -- $P > $O/rd.out 2>&1 || exit 1
-  timeout -k 10 240 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-include-regex linearize -d $O/wr -o run --output-format csv -- $P > $O/wr.out 2>&1 || exit 1
-  timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-include-regex linearize -d $O/sq -o run --output-format csv -- $P > $O/sq.out 2>&1 || exit 1
+O=gpurun_out/prof_$TAG
+mkdir -p $O
+for P in fp32 fp64; do
+  CPU=""
+  [ $P = fp64 ] && CPU="--no-cpu-baseline"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace_$P -o run --output-format csv -- \
+    python3 bench.py --steps 200 --warmup 20 --gn-steps 10 --precision $P $CPU > $O/bench_$P.json 2> $O/bench_$P.err || exit 1
+  i=0
+  for C in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum" \
+           "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" \
+           "SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
+    timeout -s KILL 90 rocprofv3 --pmc $C --kernel-include-regex linearize -d $O/pmc_${P}_$i -o run --output-format csv -- \
+      python3 bench.py --steps 20 --warmup 2 --gn-steps 0 --no-cpu-baseline --precision $P > $O/pmc_${P}_$i.json 2> $O/pmc_${P}_$i.err || exit 1
+    i=$((i+1))
+  done
+  ALGO=$(python3 -c "import json,sys; print(json.load(open('$O/bench_$P.json'))['roofline']['algorithmic_bytes_per_launch'])")
+  python3 tools/pmc_summary.py $O/pmc_linearize_$P.json $ALGO \
+    "config 3 synthetic, 100k poses / 200k landmarks / 1M bearings, J+H build $P" $O/pmc_${P}_0 $O/pmc_${P}_1 $O/pmc_${P}_2 || exit 1
 done
