@@ -69,6 +69,12 @@ int bos_plan_inspect(const bos_problem* problem, int32_t solver, int32_t rank, i
  * dof order). Not used by any solve. */
 int bos_plan_mf_selftest(const bos_problem* problem, int32_t solver, const double* vals, const double* rhs, double* x);
 
+/* Diagnostics: one J+H launch with per-wave timeline stamps, 8 x uint64 per wave: block, wave in
+ * block, kind (0 pose lanes / 1 landmark lanes), t_start, t_loop, t_loop_end, t_end (realtime clock,
+ * 100 MHz ticks), hw_id | xcc_id << 32. capacity in waves; *n_waves = waves of the launch. Not part
+ * of the drop-in boundary; the product launches never carry stamps. */
+int bos_debug_linearize_timeline(struct bos_solver* s, int64_t capacity, uint64_t* stamps, int64_t* n_waves);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = [
     "bos_dataset_load_g2o", "bos_dataset_synthetic", "bos_dataset_problem", "bos_dataset_pose_ids",
     "bos_dataset_landmark_ids", "bos_dataset_fixed_pose_id", "bos_dataset_bound", "bos_dataset_ground_truth",
     "bos_dataset_write_g2o", "bos_dataset_free", "bos_plan_inspect", "bos_plan_mf_selftest",
+    "bos_debug_linearize_timeline",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -117,6 +118,8 @@ def lib():
         "bos_linearize": (ctypes.c_int, [vp, ctypes.POINTER(bos_step_stats)]),
         "bos_linearize_async": (ctypes.c_int, [vp]),
         "bos_synchronize": (ctypes.c_int, [vp]),
+        "bos_debug_linearize_timeline": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64),
+                                                        ctypes.POINTER(ctypes.c_int64)]),
         "bos_system_info_get": (ctypes.c_int, [vp, ctypes.POINTER(bos_system_info)]),
         "bos_export_system": (ctypes.c_int, [vp, ctypes.c_int64, _ip, _ip, _dp, _dp]),
         "bos_get_state": (ctypes.c_int, [vp, _dp, _dp]),
@@ -379,6 +382,16 @@ class Solver:
 
     def linearize_async(self):
         _check(lib().bos_linearize_async(self._h), "bos_linearize_async")
+
+    def debug_timeline(self) -> np.ndarray:
+        """One J+H launch with per-wave stamps (diagnostics): rows of [block, wave, kind, t_start,
+        t_loop, t_loop_end, t_end, hw_id | xcc << 32], times in 100 MHz ticks."""
+        n = ctypes.c_int64(0)
+        _check(lib().bos_debug_linearize_timeline(self._h, 0, None, ctypes.byref(n)), "timeline")
+        out = np.zeros((n.value, 8), dtype=np.uint64)
+        _check(lib().bos_debug_linearize_timeline(self._h, n.value, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                                  ctypes.byref(n)), "timeline")
+        return out
 
     def synchronize(self):
         _check(lib().bos_synchronize(self._h), "bos_synchronize")

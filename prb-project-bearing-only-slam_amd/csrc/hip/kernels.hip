@@ -15,6 +15,9 @@
 // memory traffic, and no lane ever reads what another writes.
 #include "kernels.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "../host/bos_math.hpp"
 
 namespace bos {
@@ -41,28 +44,42 @@ template <typename T> __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// Timeline diagnostics (bos_debug_linearize_timeline only; null in every product launch): per wave,
+// [block, wave, kind, t_start, t_loop, t_loop_end, t_end, hw_id | xcc << 32], realtime clock (100 MHz).
+__device__ __forceinline__ void stamp(const unsigned long long* base, unsigned long long* st, int k) {
+    if (base) st[k] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void stamp_flush(unsigned long long* diag, const unsigned long long* st, int kind) {
+    if (!diag || (threadIdx.x & 63)) return;
+    unsigned long long* d = diag + 8 * ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    d[0] = blockIdx.x; d[1] = threadIdx.x >> 6; d[2] = kind;
+    d[3] = st[0]; d[4] = st[1]; d[5] = st[2]; d[6] = __builtin_amdgcn_s_memrealtime();
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);           // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);         // HW_REG_XCC_ID
+    d[7] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+}
+
 // Odometry edge (solver_jacobians.cpp:97-168) seen from one endpoint. J_dst = -J_src exactly in
 // the reference's Jacobian (:137-146: (DR' R_s)^T = -R_s^T DR', DR' antisymmetric), so
 // H_ss = H_dd = J_s^T Omega J_s, H_sd = -H_ss, b_d = -b_s. Returns rho = e^T Omega e; h = H_ss
-// (00, 10, 11, 20, 21, 22), g = b_s.
+// (00, 10, 11, 20, 21, 22), g = b_s. z = measurement, u = upper triangle of Omega.
 template <typename T>
-__device__ __forceinline__ T odometry_hb(const LinParams<T>& P, int k, const V4<T>& S, T ths, const V4<T>& D, T thd,
-                                         T h[6], T g[3]) {
+__device__ __forceinline__ T odometry_hb(T kt, const T z[3], const T u[6], const V4<T>& S, T ths, const V4<T>& D,
+                                         T thd, T h[6], T g[3]) {
     const T xs = S.x, ys = S.y, cs = S.z, ss = S.w, xd = D.x, yd = D.y;
     const T tx = xd - xs, ty = yd - ys;
-    const T e0 = (cs * tx + ss * ty) - P.o_z[3 * k];                                // :106, :319
-    const T e1 = (-ss * tx + cs * ty) - P.o_z[3 * k + 1];
-    const T e2 = bos::normalized_angle<T>(bos::normalized_angle<T>(thd - ths) - P.o_z[3 * k + 2]);
+    const T e0 = (cs * tx + ss * ty) - z[0];                                        // :106, :319
+    const T e1 = (-ss * tx + cs * ty) - z[1];
+    const T e2 = bos::normalized_angle<T>(bos::normalized_angle<T>(thd - ths) - z[2]);
     const T t0 = -ss * xd + cs * yd, t1 = -cs * xd - ss * yd;                       // :139
     // J_s = [[-cs, -ss, t0], [ss, -cs, t1], [0, 0, -1]]
-    const T* u = P.o_om + 6 * k;
     const T o00 = u[0], o01 = u[1], o02 = u[2], o11 = u[3], o12 = u[4], o22 = u[5];
     T Oe0 = o00 * e0 + o01 * e1 + o02 * e2;
     T Oe1 = o01 * e0 + o11 * e1 + o12 * e2;
     T Oe2 = o02 * e0 + o12 * e1 + o22 * e2;
     const T rho = e0 * Oe0 + e1 * Oe1 + e2 * Oe2;                                   // solver.cpp:54
-    if (rho > P.kt) {                                                               // :55-57
-        const T sc = sqrt(P.kt / rho);
+    if (rho > kt) {                                                                 // :55-57
+        const T sc = sqrt(kt / rho);
         Oe0 *= sc; Oe1 *= sc; Oe2 *= sc;
     }
     // Omega J_s, column by column
@@ -82,92 +99,182 @@ __device__ __forceinline__ T odometry_hb(const LinParams<T>& P, int k, const V4<
     return rho;
 }
 
+// Inputs of one odometry entry of a pose, gathered before any of them is used.
+template <typename T> struct OdoIn {
+    int ent, blk;     // edge << 1 | destination side; pose-pose block (source side)
+    V4<T> Q;          // the other pose: x, y, cos, sin
+    T thq;
+    T z[3], u[6];
+};
+
+template <typename T> __device__ __forceinline__ void odo_fetch_ids(const LinParams<T>& P, int x, OdoIn<T>& o, int& oth) {
+    o.ent = P.po_ent[x];
+    o.blk = P.po_blk[x];
+    oth = P.po_oth[x];
+}
+
+template <typename T> __device__ __forceinline__ void odo_fetch_data(const LinParams<T>& P, int oth, OdoIn<T>& o) {
+    o.Q = load4(P.pc + 4 * oth);
+    o.thq = P.pth[oth];
+    const int k = o.ent >> 1;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) o.z[v] = P.o_z[3 * k + v];
+    const V2<T>* u = (const V2<T>*)(P.o_om + 6 * k);
+#pragma unroll
+    for (int v = 0; v < 3; ++v) { const V2<T> q = u[v]; o.u[2 * v] = q.x; o.u[2 * v + 1] = q.y; }
+}
+
+// One odometry entry of pose p (pose state X, th): the entry's edge seen from p's side. Both sides
+// add H_ss = H_dd to the pose's diagonal block; b gets +b_s (source) or -b_s (destination); the
+// source side counts chi^2 and stores H_sd = -H_ss. Source and destination are chosen by selects,
+// so lanes on different sides of their edges run one instruction stream.
+template <typename T, bool HAS_DUPS>
+__device__ __forceinline__ void odometry_entry(const LinParams<T>& P, int x, int x1, const OdoIn<T>& o, const V4<T>& X,
+                                               T th, T h[6], T gb[3], T acc6[6], double& chi, int& nrob) {
+    const bool dst_side = o.ent & 1;
+    const V4<T> S = dst_side ? o.Q : X, D = dst_side ? X : o.Q;
+    const T ths = dst_side ? o.thq : th, thd = dst_side ? th : o.thq;
+    T he[6], ge[3];
+    const T rho = odometry_hb<T>(P.kt, o.z, o.u, S, ths, D, thd, he, ge);
+#pragma unroll
+    for (int v = 0; v < 6; ++v) h[v] += he[v];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) gb[v] += dst_side ? -ge[v] : ge[v];   // a + (-b) == a - b exactly
+    if (dst_side) return;
+    chi += (double)rho;
+    if (rho > P.kt) ++nrob;
+    T* ob = P.hval + P.off_pp + 6 * o.blk;
+    if (HAS_DUPS) {
+#pragma unroll
+        for (int v = 0; v < 6; ++v) acc6[v] -= he[v];
+        if (x + 1 == x1 || P.po_blk[x + 1] != o.blk) {
+            store6(ob, acc6[0], acc6[1], acc6[2], acc6[3], acc6[4], acc6[5]);
+#pragma unroll
+            for (int v = 0; v < 6; ++v) acc6[v] = (T)0;
+        }
+    } else {
+        store6(ob, -he[0], -he[1], -he[2], -he[3], -he[4], -he[5]);
+    }
+}
+
+// One bearing seen from its pose (solver_jacobians.cpp:9-95, solver.cpp:37-45): accumulates the
+// pose's diagonal block h and b, returns the pose-landmark block o (J_p^T w J_l).
+template <typename T>
+__device__ __forceinline__ void pose_bearing(const LinParams<T>& P, const V4<T>& X, const V2<T>& Lm, T z, T w,
+                                             T h[6], T gb[3], T o[6], double& chi, int& nrob) {
+    T J[5];
+    T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, z, J);   // :9-95
+    const T rho = e * w * e;                                                       // solver.cpp:37
+    chi += (double)rho;
+    if (rho > P.kt) {                                                              // :38-40
+        e *= sqrt(P.kt / rho);
+        ++nrob;
+    }
+    // H += (J^T w) J, b += (J^T w) e (:44-45)
+    const T w0 = J[0] * w, w1 = J[1] * w, w2 = J[2] * w;
+    h[0] += w0 * J[0]; h[1] += w1 * J[0]; h[2] += w1 * J[1];
+    h[3] += w2 * J[0]; h[4] += w2 * J[1]; h[5] += w2 * J[2];
+    gb[0] += w0 * e; gb[1] += w1 * e; gb[2] += w2 * e;
+    o[0] = w0 * J[3]; o[1] = w0 * J[4]; o[2] = w1 * J[3]; o[3] = w1 * J[4]; o[4] = w2 * J[3]; o[5] = w2 * J[4];
+}
+
+// The pose-landmark block of a bearing: stored at its slot, or (duplicate pairs) summed over the
+// run of equal landmarks and stored at the run's last slot (records of earlier slots of a run carry
+// kRunCont in their index).
+template <typename T, bool HAS_DUPS>
+__device__ __forceinline__ void put_pl(T* blkp, const T o[6], T acc[6], bool last) {
+    if (HAS_DUPS) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) acc[q] += o[q];
+        if (last) {
+            store6(blkp, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5]);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) acc[q] = (T)0;
+        }
+    } else {
+        store6(blkp, o[0], o[1], o[2], o[3], o[4], o[5]);
+    }
+}
+
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP>
-__device__ __forceinline__ void pose_lanes(const LinParams<T>& P, double& chi, int& nrob) {
-    const int g = P.p_begin * LPP + blockIdx.x * kBlock + threadIdx.x;   // lane; shards start at a wave
+__device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, double& chi, int& nrob,
+                                           unsigned long long* st) {
+    const int g = P.p_begin * LPP + blk * kBlock + threadIdx.x;   // lane; shards start at a wave
     const int p = g / LPP, sub = g % LPP, t = g & 63;
     const bool active = p < P.p_end;
     T h[6] = {0, 0, 0, 0, 0, 0}, gb[3] = {0, 0, 0};
     if (active) {
+        // Dependent load stages, the bearing chain (count/base -> records -> landmarks) and the
+        // odometry chain (entry range -> entry ids -> other pose + edge data) issued side by side.
         const V4<T> X = load4(P.pc + 4 * p);
         const int n = P.pl_cnt[g];
-        int sl = P.pw_base[g >> 6] + t;   // slot of item j: + 64 j
-        T acc[6] = {0, 0, 0, 0, 0, 0};
-        // two-stage software pipeline: record j+2 and the landmark of item j+1 are in flight while
-        // item j is evaluated
-        BRec<T> nxt, nxt2;
-        V2<T> Lnxt;
-        if (n > 0) { nxt = P.pb[sl]; Lnxt = load2(P.lc + 2 * nxt.idx); }
-        if (n > 1) nxt2 = P.pb[sl + 64];
-        for (int j = 0; j < n; ++j, sl += 64) {
-            const BRec<T> cur = nxt;
-            const V2<T> Lm = Lnxt;
-            if (j + 1 < n) { nxt = nxt2; Lnxt = load2(P.lc + 2 * nxt.idx); }
-            if (j + 2 < n) nxt2 = P.pb[sl + 128];
-            T J[5];
-            T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, cur.z, J);   // :9-95
-            const T w = HAS_W ? P.pb_w[sl] : (T)1;
-            const T rho = e * w * e;                                                       // solver.cpp:37
-            chi += (double)rho;
-            if (rho > P.kt) {                                                              // :38-40
-                e *= sqrt(P.kt / rho);
-                ++nrob;
+        const int sl = P.pw_base[g >> 6] + t;   // slot of item j: + 64 j
+        const bool odo = sub == 0 && !(P.diag_skip & 4);
+        int x0 = 0, x1 = 0;
+        T th = (T)0;
+        if (odo) { x0 = P.po_ptr[p]; x1 = P.po_ptr[p + 1]; th = P.pth[p]; }
+        // Bearing items run in pairs with two register sets (A: even items, B: odd items). Per set,
+        // the record index is loaded two pairs ahead, the full record and the landmark gather one
+        // pair ahead; every register is refilled by a load right after its last use, so no loaded
+        // value is ever copied (a copy waits for its load) and each gather has a whole pair of items
+        // to land. All unguarded: the record arrays carry kRecPad padding records (landmark 0).
+        const BRec<T>* rp = P.pb + sl;
+        int iA = rp[0].idx & kIdxMask, iB = rp[64].idx & kIdxMask;
+        OdoIn<T> oa, ob;
+        int otha = 0, othb = 0;
+        if (x0 < x1) odo_fetch_ids(P, x0, oa, otha);
+        if (x0 + 1 < x1) odo_fetch_ids(P, x0 + 1, ob, othb);
+        BRec<T> rA = rp[0], rB = rp[64];
+        V2<T> LA = load2(P.lc + 2 * iA), LB = load2(P.lc + 2 * iB);
+        T wA = HAS_W ? P.pb_w[sl] : (T)1, wB = HAS_W ? P.pb_w[sl + 64] : (T)1;
+        iA = rp[128].idx & kIdxMask;
+        iB = rp[192].idx & kIdxMask;
+        // odometry first (fp32): its arithmetic covers the landmark gathers of items 0 and 1; the
+        // fp64 variant runs it after the bearings, which keeps it within 128 VGPRs
+        constexpr bool kOdoFirst = true;
+        T acc6[6] = {0, 0, 0, 0, 0, 0};
+        auto odometry = [&]() {
+            if (x0 < x1) odo_fetch_data(P, otha, oa);
+            if (x0 + 1 < x1) odo_fetch_data(P, othb, ob);
+            if (x0 < x1) odometry_entry<T, HAS_DUPS>(P, x0, x1, oa, X, th, h, gb, acc6, chi, nrob);
+            if (x0 + 1 < x1) odometry_entry<T, HAS_DUPS>(P, x0 + 1, x1, ob, X, th, h, gb, acc6, chi, nrob);
+            for (int x = x0 + 2; x < x1; ++x) {
+                OdoIn<T> oc;
+                int othc;
+                odo_fetch_ids(P, x, oc, othc);
+                odo_fetch_data(P, othc, oc);
+                odometry_entry<T, HAS_DUPS>(P, x, x1, oc, X, th, h, gb, acc6, chi, nrob);
             }
-            // H += (J^T w) J, b += (J^T w) e (:44-45)
-            const T w0 = J[0] * w, w1 = J[1] * w, w2 = J[2] * w;
-            h[0] += w0 * J[0]; h[1] += w1 * J[0]; h[2] += w1 * J[1];
-            h[3] += w2 * J[0]; h[4] += w2 * J[1]; h[5] += w2 * J[2];
-            gb[0] += w0 * e; gb[1] += w1 * e; gb[2] += w2 * e;
-            const T o0 = w0 * J[3], o1 = w0 * J[4], o2 = w1 * J[3], o3 = w1 * J[4], o4 = w2 * J[3], o5 = w2 * J[4];
-            T* blk = P.hval + P.off_pl + 6 * sl;
-            if (HAS_DUPS) {   // observations of one pair are adjacent: sum, store at the last one
-                acc[0] += o0; acc[1] += o1; acc[2] += o2; acc[3] += o3; acc[4] += o4; acc[5] += o5;
-                if (j + 1 == n || nxt.idx != cur.idx) {
-                    store6(blk, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5]);
-#pragma unroll
-                    for (int q = 0; q < 6; ++q) acc[q] = (T)0;
-                }
+        };
+        if (kOdoFirst) odometry();
+        T acc[6] = {0, 0, 0, 0, 0, 0}, o[6];
+        T* blkp = P.hval + P.off_pl + 6 * sl;
+        stamp(P.diag_stamps, st, 1);
+        for (int j = 0; j < n; j += 2, rp += 128, blkp += 6 * 128) {
+            // item j (set A), then refill A with item j + 2 (record, gather) and j + 4 (index)
+            pose_bearing<T>(P, X, LA, rA.z, wA, h, gb, o, chi, nrob);
+            put_pl<T, HAS_DUPS>(blkp, o, acc, !(rA.idx & kRunCont));
+            rA = rp[128];
+            LA = load2(P.lc + 2 * iA);
+            if (HAS_W) wA = P.pb_w[sl + 64 * (j + 2)];
+            iA = rp[256].idx & kIdxMask;
+            // item j + 1 (set B). Its block is stored even past the lane's last item (a padding slot
+            // of the lane's wave: pose-lane waves have an even number of slots per lane), so both
+            // paths issue the same memory operations and the loop's waits stay exact.
+            if (j + 1 < n) {
+                pose_bearing<T>(P, X, LB, rB.z, wB, h, gb, o, chi, nrob);
             } else {
-                store6(blk, o0, o1, o2, o3, o4, o5);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) o[q] = (T)0;
             }
+            put_pl<T, HAS_DUPS>(blkp + 6 * 64, o, acc, !(rB.idx & kRunCont));
+            rB = rp[192];
+            LB = load2(P.lc + 2 * iB);
+            if (HAS_W) wB = P.pb_w[sl + 64 * (j + 3)];
+            iB = rp[320].idx & kIdxMask;
         }
-        if (sub == 0) {
-            const T th = P.pth[p];
-            T acc6[6] = {0, 0, 0, 0, 0, 0};
-            const int x1 = P.po_ptr[p + 1];
-            for (int x = P.po_ptr[p]; x < x1; ++x) {
-                const int ent = P.po_ent[x], k = ent >> 1;
-                const bool dst_side = ent & 1;
-                const int q = dst_side ? P.o_src[k] : P.o_dst[k];
-                const V4<T> Q = load4(P.pc + 4 * q);
-                const T thq = P.pth[q];
-                T he[6], ge[3];
-                const T rho = dst_side ? odometry_hb<T>(P, k, Q, thq, X, th, he, ge)
-                                       : odometry_hb<T>(P, k, X, th, Q, thq, he, ge);
-#pragma unroll
-                for (int v = 0; v < 6; ++v) h[v] += he[v];
-                if (dst_side) {
-                    gb[0] -= ge[0]; gb[1] -= ge[1]; gb[2] -= ge[2];
-                    continue;
-                }
-                gb[0] += ge[0]; gb[1] += ge[1]; gb[2] += ge[2];
-                chi += (double)rho;
-                if (rho > P.kt) ++nrob;
-                const int ub = P.po_blk[x];
-                T* ob = P.hval + P.off_pp + 6 * ub;
-                if (HAS_DUPS) {
-#pragma unroll
-                    for (int v = 0; v < 6; ++v) acc6[v] -= he[v];
-                    if (x + 1 == x1 || P.po_blk[x + 1] != ub) {
-                        store6(ob, acc6[0], acc6[1], acc6[2], acc6[3], acc6[4], acc6[5]);
-#pragma unroll
-                        for (int v = 0; v < 6; ++v) acc6[v] = (T)0;
-                    }
-                } else {
-                    store6(ob, -he[0], -he[1], -he[2], -he[3], -he[4], -he[5]);
-                }
-            }
-        }
+        stamp(P.diag_stamps, st, 2);
+        if (!kOdoFirst) odometry();
     }
     // combine the lane group's partial sums (fixed butterfly: deterministic)
 #pragma unroll
@@ -185,47 +292,85 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, double& chi, i
     }
 }
 
-template <typename T, bool HAS_W>
-__device__ __forceinline__ void landmark_lane(const LinParams<T>& P) {
-    const int l = P.l_begin + (blockIdx.x - P.pose_blocks) * kBlock + threadIdx.x;   // shards start at a wave
-    if (l >= P.l_end) return;
-    const V2<T> Lm = load2(P.lc + 2 * l);
-    T h00 = 0, h10 = 0, h11 = 0, g0 = 0, g1 = 0;
-    const int n = P.ll_cnt[l];
-    int sl = P.lw_base[l >> 6] + (l & 63);
-    BRec<T> nxt, nxt2;
-    V4<T> Xnxt;
-    if (n > 0) { nxt = P.lb[sl]; Xnxt = load4(P.pc + 4 * nxt.idx); }
-    if (n > 1) nxt2 = P.lb[sl + 64];
-    for (int j = 0; j < n; ++j, sl += 64) {
-        const BRec<T> cur = nxt;
-        const V4<T> X = Xnxt;
-        if (j + 1 < n) { nxt = nxt2; Xnxt = load4(P.pc + 4 * nxt.idx); }
-        if (j + 2 < n) nxt2 = P.lb[sl + 128];
-        T J[5];
-        T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, cur.z, J);
-        const T w = HAS_W ? P.lb_w[sl] : (T)1;
-        const T rho = e * w * e;
-        if (rho > P.kt) e *= sqrt(P.kt / rho);
-        const T w3 = J[3] * w, w4 = J[4] * w;
-        h00 += w3 * J[3]; h10 += w4 * J[3]; h11 += w4 * J[4];
-        g0 += w3 * e; g1 += w4 * e;
-    }
-    T* hl = P.hval + P.off_ldiag + 3 * l;
-    hl[0] = h00 + P.lambda; hl[1] = h10; hl[2] = h11 + P.lambda;
-    T* bl = P.b + 3 * P.NP + 2 * l;
-    bl[0] = g0; bl[1] = g1;
+// One bearing seen from its landmark: the landmark's diagonal block and b.
+template <typename T>
+__device__ __forceinline__ void landmark_bearing(const LinParams<T>& P, const V4<T>& X, const V2<T>& Lm, T z, T w,
+                                                 T hl[3], T gl[2]) {
+    T J[5];
+    T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, z, J);
+    const T rho = e * w * e;
+    if (rho > P.kt) e *= sqrt(P.kt / rho);
+    const T w3 = J[3] * w, w4 = J[4] * w;
+    hl[0] += w3 * J[3]; hl[1] += w4 * J[3]; hl[2] += w4 * J[4];
+    gl[0] += w3 * e; gl[1] += w4 * e;
 }
 
-template <typename T, bool HAS_W, bool HAS_DUPS, int LPP>
-__global__ __launch_bounds__(kBlock) void linearize_kernel(const LinParams<T> P) {
-    if ((int)blockIdx.x >= P.pose_blocks) {   // block-uniform branch
-        landmark_lane<T, HAS_W>(P);
+template <typename T, bool HAS_W>
+__device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int blk, unsigned long long* st) {
+    const int g = P.l_begin + blk * kBlock + threadIdx.x;   // lane; shards start at a lane window
+    if (g >= P.l_end) return;
+    const int l = P.ll_lm[g];
+    const int n = P.ll_cnt[g];
+    const int sl = P.lw_base[g >> 6] + (g & 63);
+    const V2<T> Lm = load2(P.lc + 2 * l);
+    T hl[3] = {0, 0, 0}, gl[2] = {0, 0};
+    // paired register sets as in pose_lanes (padding records point at pose 0)
+    const BRec<T>* rp = P.lb + sl;
+    int iA = rp[0].idx, iB = rp[64].idx;
+    T zA = rp[0].z, zB = rp[64].z;
+    V4<T> XA = load4(P.pc + 4 * iA), XB = load4(P.pc + 4 * iB);
+    T wA = HAS_W ? P.lb_w[sl] : (T)1, wB = HAS_W ? P.lb_w[sl + 64] : (T)1;
+    iA = rp[128].idx;
+    iB = rp[192].idx;
+    stamp(P.diag_stamps, st, 1);
+    for (int j = 0; j < n; j += 2, rp += 128) {
+        landmark_bearing<T>(P, XA, Lm, zA, wA, hl, gl);
+        zA = rp[128].z;
+        XA = load4(P.pc + 4 * iA);
+        if (HAS_W) wA = P.lb_w[sl + 64 * (j + 2)];
+        iA = rp[256].idx;
+        if (j + 1 < n) landmark_bearing<T>(P, XB, Lm, zB, wB, hl, gl);
+        zB = rp[192].z;
+        XB = load4(P.pc + 4 * iB);
+        if (HAS_W) wB = P.lb_w[sl + 64 * (j + 3)];
+        iB = rp[320].idx;
+    }
+    stamp(P.diag_stamps, st, 2);
+    T* hp = P.hval + P.off_ldiag + 3 * l;
+    hp[0] = hl[0] + P.lambda; hp[1] = hl[1]; hp[2] = hl[2] + P.lambda;
+    T* bl = P.b + 3 * P.NP + 2 * l;
+    bl[0] = gl[0]; bl[1] = gl[1];
+}
+
+// Pose and landmark blocks interleaved in proportion over the grid (pose block i sits at the
+// b with floor(b Pb / T) == i < floor((b + 1) Pb / T)), so every CU gets its share of the longer
+// pose lists.
+template <typename T, bool HAS_W, bool HAS_DUPS, int LPP, int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams<T> P) {
+    const int64_t nb = gridDim.x, b = blockIdx.x;
+    int pb0, pb1;
+    if (P.interleave) {
+        pb0 = (int)(b * P.pose_blocks / nb);
+        pb1 = (int)((b + 1) * P.pose_blocks / nb);
+    } else {   // pose blocks first
+        pb0 = (int)min(b, (int64_t)P.pose_blocks);
+        pb1 = (int)min(b + 1, (int64_t)P.pose_blocks);
+    }
+    unsigned long long st[3] = {0, 0, 0};
+    stamp(P.diag_stamps, st, 0);
+    if (pb1 == pb0) {   // block-uniform branch
+        // lm_rep landmark-lane blocks per block (so the launch fits the resident wave slots)
+        const int lb0 = ((int)b - pb0) * P.lm_rep;
+        if (!(P.diag_skip & 1))
+            for (int r = 0; r < P.lm_rep; ++r) landmark_lane<T, HAS_W>(P, lb0 + r, st);
+        stamp_flush(P.diag_stamps, st, 1);
         return;
     }
+    if (P.diag_skip & 2) return;
     double chi = 0.0;
     int nrob = 0;
-    pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, chi, nrob);
+    pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, pb0, chi, nrob, st);
+    stamp_flush(P.diag_stamps, st, 0);
     // per-block chi^2 / robust count in a fixed order
     __shared__ double sc[kBlock / 64];
     __shared__ int sr[kBlock / 64];
@@ -237,8 +382,8 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(const LinParams<T> P)
         double c = 0.0;
         int r = 0;
         for (int w = 0; w < kBlock / 64; ++w) { c += sc[w]; r += sr[w]; }
-        P.chi2_part[blockIdx.x] = c;
-        P.nrob_part[blockIdx.x] = r;
+        P.chi2_part[pb0] = c;
+        P.nrob_part[pb0] = r;
     }
 }
 
@@ -316,23 +461,45 @@ __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colin
 
 }  // namespace
 
-template <typename T, bool W, bool D>
-hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, int grid, hipStream_t s) {
+// Landmark-lane blocks per launched block (BOS_JH_LM_REP, default 1). Folding two into one block
+// lets the fp64 grid fit the resident wave slots (4 waves per SIMD), but measured slower on config 3
+// (35 vs 31 us): the kernel is bound by the memory pipeline, not by the second wave generation.
+inline int lm_rep() {
+    static const int r = [] { const char* e = std::getenv("BOS_JH_LM_REP"); return e ? std::max(1, std::atoi(e)) : 1; }();
+    return r;
+}
+
+template <typename T, bool W, bool D, int LPP, int MINW>
+hipError_t launch_lin_k(LinParams<T> p, hipStream_t s) {
+    const int lm_blocks = (p.l_end - p.l_begin + kBlock - 1) / kBlock;
+    p.lm_rep = lm_rep();
+    const int grid = p.pose_blocks + (lm_blocks + p.lm_rep - 1) / p.lm_rep;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL((linearize_kernel<T, W, D, LPP, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+}
+
+template <typename T, bool W, bool D, int MINW>
+hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, hipStream_t s) {
     switch (lpp) {
-        case 1: hipLaunchKernelGGL((linearize_kernel<T, W, D, 1>), dim3(grid), dim3(kBlock), 0, s, p); break;
-        case 2: hipLaunchKernelGGL((linearize_kernel<T, W, D, 2>), dim3(grid), dim3(kBlock), 0, s, p); break;
-        case 4: hipLaunchKernelGGL((linearize_kernel<T, W, D, 4>), dim3(grid), dim3(kBlock), 0, s, p); break;
+        case 1: return launch_lin_k<T, W, D, 1, MINW>(p, s);
+        case 2: return launch_lin_k<T, W, D, 2, MINW>(p, s);
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+}
+
+// Minimum waves per SIMD the kernel is compiled for (register budget): 4 (<= 128 VGPRs); 5 (<= 102)
+// makes the fp64 variant spill, measured slower (36 vs 31 us on config 3), BOS_JH_MINWAVES=5.
+template <typename T, bool W, bool D>
+hipError_t launch_lin_w(const LinParams<T>& p, int lpp, hipStream_t s) {
+    static const int minw = [] { const char* e = std::getenv("BOS_JH_MINWAVES"); return e ? std::atoi(e) : 4; }();
+    return minw == 5 ? launch_lin_lpp<T, W, D, 5>(p, lpp, s) : launch_lin_lpp<T, W, D, 4>(p, lpp, s);
 }
 
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s) {
-    const int grid = p.pose_blocks + (p.l_end - p.l_begin + kBlock - 1) / kBlock;
-    if (grid == 0) return hipSuccess;
-    if (has_w) return has_dups ? launch_lin_lpp<T, true, true>(p, lpp, grid, s) : launch_lin_lpp<T, true, false>(p, lpp, grid, s);
-    return has_dups ? launch_lin_lpp<T, false, true>(p, lpp, grid, s) : launch_lin_lpp<T, false, false>(p, lpp, grid, s);
+    if (has_w) return has_dups ? launch_lin_w<T, true, true>(p, lpp, s) : launch_lin_w<T, true, false>(p, lpp, s);
+    return has_dups ? launch_lin_w<T, false, true>(p, lpp, s) : launch_lin_w<T, false, false>(p, lpp, s);
 }
 
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s) {

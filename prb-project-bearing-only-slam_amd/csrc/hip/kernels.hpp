@@ -8,6 +8,14 @@ namespace bos {
 namespace dev {
 
 constexpr int kBlock = 256;
+// padding records after each lane-list array: the J+H kernel reads records up to five items past a
+// lane's last one, unguarded
+constexpr int kRecPad = 512;
+
+// Pose-list records whose next item observes the same landmark (a run of duplicate observations,
+// summed into the run's last slot) carry kRunCont in their index.
+constexpr int32_t kRunCont = (int32_t)0x80000000u;
+constexpr int32_t kIdxMask = 0x7fffffff;
 
 // One observation in a lane's list: the other endpoint (landmark for the pose lists, pose for the
 // landmark lists) and the measured bearing; one vector load.
@@ -32,6 +40,7 @@ template <typename T> struct LinParams {
     const T* pb_w;            // [slots] information, null => 1
     const int32_t* po_ptr;    // [NP + 1]
     const int32_t* po_ent;    // edge << 1 | destination side
+    const int32_t* po_oth;    // the other pose of the entry's edge
     const int32_t* po_blk;    // pose-pose block of a source-side entry
     const int32_t* o_src;
     const int32_t* o_dst;
@@ -39,7 +48,8 @@ template <typename T> struct LinParams {
     const T* o_om;            // [M_o][6] upper triangle (00, 01, 02, 11, 12, 22)
     // landmark lanes
     const int32_t* lw_base;   // [waves + 1]
-    const int32_t* ll_cnt;    // [NL]
+    const int32_t* ll_cnt;    // [NL] per lane
+    const int32_t* ll_lm;     // [NL] landmark of each lane (degree-sorted inside 256-lane windows)
     const BRec<T>* lb;        // [slots] (pose, z)
     const T* lb_w;
     // outputs
@@ -50,6 +60,10 @@ template <typename T> struct LinParams {
     int32_t* nrob_part;       // [pose_blocks]
     T kt;                     // robust kernel threshold
     T lambda;                 // damping
+    int lm_rep;               // landmark-lane blocks handled per launched block (set by the launcher)
+    int interleave;           // pose and landmark blocks interleaved over the grid (else pose blocks first)
+    int diag_skip;            // timing diagnostics only (BOS_JH_DIAG_SKIP): 1 landmark lanes, 2 pose lanes, 4 odometry
+    unsigned long long* diag_stamps;   // timeline diagnostics only (8 x u64 per wave), null otherwise
 };
 
 template <typename T> struct UpdateParams {

@@ -80,7 +80,7 @@ struct bos_solver {
     void* d_pth = nullptr;
     void* d_lc = nullptr;
     // J+H work lists (host/plan.hpp BlockLayout)
-    int32_t *pw_base = nullptr, *pl_cnt = nullptr, *lw_base = nullptr, *ll_cnt = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_blk = nullptr, *csr_src = nullptr,
+    int32_t *pw_base = nullptr, *pl_cnt = nullptr, *lw_base = nullptr, *ll_cnt = nullptr, *ll_lm = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_oth = nullptr, *po_blk = nullptr, *csr_src = nullptr,
             *elim_ref = nullptr;
     void *pb = nullptr, *pb_w = nullptr, *lb = nullptr, *lb_w = nullptr;
     int pose_blocks = 0;
@@ -135,9 +135,9 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.pose_blocks = s->pose_blocks;
     p.pw_base = s->pw_base; p.pl_cnt = s->pl_cnt;
     p.pb = (const bos::dev::BRec<T>*)s->pb; p.pb_w = (const T*)s->pb_w;
-    p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_blk = s->po_blk;
+    p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_oth = s->po_oth; p.po_blk = s->po_blk;
     p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
-    p.lw_base = s->lw_base; p.ll_cnt = s->ll_cnt;
+    p.lw_base = s->lw_base; p.ll_cnt = s->ll_cnt; p.ll_lm = s->ll_lm;
     p.lb = (const bos::dev::BRec<T>*)s->lb; p.lb_w = (const T*)s->lb_w;
     p.hval = (T*)s->d_val;
     p.b = (T*)s->d_b;
@@ -146,6 +146,12 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.nrob_part = s->d_nrob_part;
     p.kt = (T)s->kt;
     p.lambda = (T)s->damping;
+    static const int interleave = [] { const char* e = std::getenv("BOS_JH_INTERLEAVE"); return e ? std::atoi(e) : 0; }();
+    static const int diag_skip = [] { const char* e = std::getenv("BOS_JH_DIAG_SKIP"); return e ? std::atoi(e) : 0; }();
+    p.interleave = interleave;
+    p.diag_skip = diag_skip;
+    p.diag_stamps = nullptr;
+    p.lm_rep = 1;
     return p;
 }
 
@@ -382,8 +388,8 @@ int bos_destroy(bos_solver* s) {
     if (!s) return BOS_OK;
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pl_cnt, s->lw_base, s->ll_cnt,
-                    s->po_ptr, s->po_ent, s->po_blk, s->csr_src, s->elim_ref, s->pb, s->pb_w, s->lb, s->lb_w,
+    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pl_cnt, s->lw_base, s->ll_cnt, s->ll_lm,
+                    s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb, s->pb_w, s->lb, s->lb_w,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_chi, s->d_nrob,
@@ -511,15 +517,31 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
 
     {
         const bos::BlockLayout& B = P.blk;
-        // slot records (padding slots: index 0, z 0, never read)
+        // slot records (padding slots: index 0, z 0). The arrays carry kRecPad extra padding records
+        // so the kernel's two-ahead prefetch never leaves them; a prefetched padding record is
+        // never evaluated.
         const std::vector<int32_t>& po = B.pose_lanes.obs;
         const std::vector<int32_t>& lo = B.lm_lanes.obs;
-        std::vector<double> pbz(po.size(), 0.0), lbz(lo.size(), 0.0), pbw, lbw;
-        std::vector<int32_t> pbi(po.size(), 0), lbi(lo.size(), 0);
+        const size_t pad = bos::dev::kRecPad;
+        std::vector<double> pbz(po.size() + pad, 0.0), lbz(lo.size() + pad, 0.0), pbw, lbw;
+        std::vector<int32_t> pbi(po.size() + pad, 0), lbi(lo.size() + pad, 0);
         for (size_t i = 0; i < po.size(); ++i)
             if (po[i] >= 0) { pbi[i] = pb->bearing_landmark[po[i]]; pbz[i] = pb->bearing_z[po[i]]; }
         for (size_t i = 0; i < lo.size(); ++i)
             if (lo[i] >= 0) { lbi[i] = pb->bearing_pose[lo[i]]; lbz[i] = pb->bearing_z[lo[i]]; }
+        {   // runs of duplicate (pose, landmark) observations: every record but the run's last is flagged
+            const bos::LaneLists& PLn = B.pose_lanes;
+            for (size_t g = 0; g < PLn.cnt.size(); ++g)
+                for (int j = 0; j + 1 < PLn.cnt[g]; ++j) {
+                    const int64_t sl = PLn.w_base[g / 64] + 64 * (int64_t)j + (int64_t)(g & 63);
+                    if (pbi[sl] == pbi[sl + 64]) pbi[sl] |= bos::dev::kRunCont;
+                }
+        }
+        std::vector<int32_t> po_oth(B.po_ent.size());
+        for (size_t x = 0; x < po_oth.size(); ++x) {
+            const int32_t e = B.po_ent[x];
+            po_oth[x] = (e & 1) ? pb->odom_src[e >> 1] : pb->odom_dst[e >> 1];
+        }
         auto upload_recs = [&](void** dst, const std::vector<int32_t>& idx, const std::vector<double>& z) -> int {
             if (f32) {
                 std::vector<bos::dev::BRec<float>> r(idx.size());
@@ -538,12 +560,14 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         };
         if ((rc = upload(&s->pw_base, B.pose_lanes.w_base)) || (rc = upload(&s->pl_cnt, B.pose_lanes.cnt)) ||
             (rc = upload(&s->lw_base, B.lm_lanes.w_base)) || (rc = upload(&s->ll_cnt, B.lm_lanes.cnt)) ||
+            (rc = upload(&s->ll_lm, B.lm_lane_lm)) ||
             (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, B.po_ent)) ||
+            (rc = upload(&s->po_oth, po_oth)) ||
             (rc = upload(&s->po_blk, B.po_blk)) || (rc = upload_recs(&s->pb, pbi, pbz)) ||
             (rc = upload_recs(&s->lb, lbi, lbz)))
             return bail(rc);
         if (s->has_w) {
-            pbw.assign(po.size(), 0.0); lbw.assign(lo.size(), 0.0);
+            pbw.assign(po.size() + pad, 0.0); lbw.assign(lo.size() + pad, 0.0);
             for (size_t i = 0; i < po.size(); ++i) if (po[i] >= 0) pbw[i] = pb->bearing_omega[po[i]];
             for (size_t i = 0; i < lo.size(); ++i) if (lo[i] >= 0) lbw[i] = pb->bearing_omega[lo[i]];
             if ((rc = upload_Tv(&s->pb_w, pbw)) || (rc = upload_Tv(&s->lb_w, lbw))) return bail(rc);
@@ -643,6 +667,36 @@ int bos_linearize_async(bos_solver* s) {
     int rc = enqueue_linearize(s);
     if (rc) return rc;
     return enqueue_exchange(s);
+}
+
+int bos_debug_linearize_timeline(bos_solver* s, int64_t capacity, uint64_t* stamps, int64_t* n_waves) {
+    if (!s || !n_waves) return fail(BOS_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(s->device));
+    const bos::Plan& P = s->plan;
+    const int64_t grid = s->pose_blocks + (P.l_end - P.l_begin + bos::dev::kBlock - 1) / bos::dev::kBlock;
+    const int64_t waves = grid * (bos::dev::kBlock / 64);
+    *n_waves = waves;
+    if (!stamps || capacity < waves) return BOS_OK;
+    unsigned long long* d = nullptr;
+    int rc = dalloc(&d, 8 * (size_t)waves);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(d, 0, 8 * (size_t)waves * sizeof(unsigned long long), s->stream));
+    hipError_t e;
+    const int lpp = P.blk.lpp;
+    if (s->precision == BOS_FP32) {
+        bos::dev::LinParams<float> p = lin_params<float>(s);
+        p.diag_stamps = d;
+        e = bos::dev::launch_linearize<float>(p, lpp, s->has_w, s->has_dups, s->stream);
+    } else {
+        bos::dev::LinParams<double> p = lin_params<double>(s);
+        p.diag_stamps = d;
+        e = bos::dev::launch_linearize<double>(p, lpp, s->has_w, s->has_dups, s->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) e = hipMemcpy(stamps, d, 8 * (size_t)waves * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("timeline: ") + hipGetErrorString(e));
+    return BOS_OK;
 }
 
 int bos_synchronize(bos_solver* s) {

@@ -61,6 +61,23 @@ template <typename T> BOS_HD T bearing_error(T px, T py, T c, T s, T lx, T ly, T
     return normalized_angle<T>(det_atan2<T>(gy, gx) - z);                // :15, :18
 }
 
+// 1/x for the Jacobian's 1/|g|^2 (slam/solver_jacobians.cpp:35). Host: IEEE division. Device: the
+// hardware reciprocal (fp32: v_rcp_f32, 1 ulp) or its Newton-refined fp64 form. The Jacobian
+// tolerates an ulp; the error's atan2 (det_atan2.hpp) keeps its correctly rounded division.
+template <typename T> BOS_HD T jac_recip(T x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_amdgcn_rcpf(x);
+    } else {
+        T r = __builtin_amdgcn_rcp(x);
+        r = fma(fma(-x, r, (T)1), r, r);
+        return fma(fma(-x, r, (T)1), r, r);
+    }
+#else
+    return (T)1 / x;
+#endif
+}
+
 // Bearing error and analytic Jacobian (slam/solver_jacobians.cpp:9-95).
 // Inputs: pose translation (px, py), cached c = cos(theta), s = sin(theta); landmark (lx, ly);
 // measured z (smallestAngle-wrapped). Outputs: e = normalized(atan2(g) - z) and
@@ -69,7 +86,7 @@ template <typename T>
 BOS_HD T bearing_error_jacobian(T px, T py, T c, T s, T lx, T ly, T z, T J[5]) {
     T gx, gy;
     const T e = bearing_error<T>(px, py, c, s, lx, ly, z, gx, gy);
-    const T f = (T)1 / (gx * gx + gy * gy);                              // :35
+    const T f = jac_recip<T>(gx * gx + gy * gy);                         // :35
     const T a0 = f * (-gy), a1 = f * gx;                                 // :47-48
     const T gth_x = c * ly + s * (-lx);                                  // R^T [[0,1],[-1,0]] l (:60)
     const T gth_y = -s * ly + c * (-lx);

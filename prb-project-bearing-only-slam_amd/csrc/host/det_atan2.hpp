@@ -61,19 +61,22 @@ template <typename T> BOS_DET_HD T det_atan_ratio(T ay, T ax) {
 #pragma clang fp contract(off)
 #endif
     using C = AtanConsts<T>;
-    // reduction interval: 0: t < 7/16, 1: < 11/16, 2: < 19/16, 3: < 39/16, 4: beyond
-    const int id = (ay >= (T)0.4375 * ax) + (ay >= (T)0.6875 * ax) + (ay >= (T)1.1875 * ax) + (ay >= (T)2.4375 * ax);
-    const T c = id == 1 ? (T)0.5 : id == 2 ? (T)1 : id == 3 ? (T)1.5 : (T)0;
-    const T num = id == 4 ? -ax : ay - c * ax;
-    const T den = id == 4 ? ay : ax + c * ay;
+    // reduction interval: 0: t < 7/16, 1: < 11/16, 2: < 19/16, 3: < 39/16, 4: beyond. The tests
+    // are nested (k ax is monotone in k), so the interval is the last one that holds; written as
+    // selects (no branches on the GPU)
+    const bool b1 = ay >= (T)0.4375 * ax, b2 = ay >= (T)0.6875 * ax, b3 = ay >= (T)1.1875 * ax,
+               b4 = ay >= (T)2.4375 * ax;
+    const T c = b3 ? (T)1.5 : b2 ? (T)1 : b1 ? (T)0.5 : (T)0;
+    const T num = b4 ? -ax : ay - c * ax;
+    const T den = b4 ? ay : ax + c * ay;
     const T u = num / den;
     const T z = u * u, w = z * z;
     using std::fma;
     const T s1 = z * fma(w, fma(w, fma(w, fma(w, fma(w, C::aT[10], C::aT[8]), C::aT[6]), C::aT[4]), C::aT[2]), C::aT[0]);
     const T s2 = w * fma(w, fma(w, fma(w, fma(w, C::aT[9], C::aT[7]), C::aT[5]), C::aT[3]), C::aT[1]);
     // atan(c) = hi + lo, selected without memory indexing
-    const T hi = id == 1 ? C::hi[1] : id == 2 ? C::hi[2] : id == 3 ? C::hi[3] : id == 4 ? C::hi[4] : (T)0;
-    const T lo = id == 1 ? C::lo[1] : id == 2 ? C::lo[2] : id == 3 ? C::lo[3] : id == 4 ? C::lo[4] : (T)0;
+    const T hi = b4 ? C::hi[4] : b3 ? C::hi[3] : b2 ? C::hi[2] : b1 ? C::hi[1] : (T)0;
+    const T lo = b4 ? C::lo[4] : b3 ? C::lo[3] : b2 ? C::lo[2] : b1 ? C::lo[1] : (T)0;
     return hi - (fma(u, s1 + s2, -lo) - u);
 }
 
@@ -83,15 +86,11 @@ template <typename T> BOS_DET_HD T det_atan2(T y, T x) {
 #endif
     using C = AtanConsts<T>;
     const T ax = std::fabs(x), ay = std::fabs(y);
-    T r;
-    if (ay == (T)0) {
-        r = std::signbit(x) ? C::pi : (T)0;
-    } else if (ax == (T)0) {
-        r = C::pi_o_2;
-    } else {
-        const T a = det_atan_ratio<T>(ay, ax);
-        r = std::signbit(x) ? C::pi - (a - C::pi_lo) : a;
-    }
+    // the ratio is evaluated unconditionally and discarded on the axes (0/0 there), so the GPU
+    // runs this as selects
+    const T a = det_atan_ratio<T>(ay, ax);
+    const bool neg_x = std::signbit(x);
+    const T r = ay == (T)0 ? (neg_x ? C::pi : (T)0) : ax == (T)0 ? C::pi_o_2 : neg_x ? C::pi - (a - C::pi_lo) : a;
     return std::signbit(y) ? -r : r;
 }
 

@@ -499,7 +499,8 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
 }
 
 // Wave-interleaved lane lists (LaneLists in plan.hpp) from per-lane item ranges.
-void make_lane_lists(int lanes, const std::vector<int32_t>& lane_ptr, const std::vector<int32_t>& items, LaneLists& L) {
+void make_lane_lists(int lanes, const std::vector<int32_t>& lane_ptr, const std::vector<int32_t>& items, LaneLists& L,
+                     bool even) {
     const int waves = (lanes + 63) / 64;
     L.w_base.assign(waves + 1, 0);
     L.w_len.assign(waves, 0);
@@ -508,6 +509,8 @@ void make_lane_lists(int lanes, const std::vector<int32_t>& lane_ptr, const std:
         L.cnt[g] = lane_ptr[g + 1] - lane_ptr[g];
         L.w_len[g / 64] = std::max(L.w_len[g / 64], L.cnt[g]);
     }
+    if (even)   // the J+H kernel walks pose lists in pairs and stores the second item of the last pair
+        for (int w = 0; w < waves; ++w) L.w_len[w] += L.w_len[w] & 1;
     for (int w = 0; w < waves; ++w) L.w_base[w + 1] = L.w_base[w] + 64 * L.w_len[w];
     L.obs.assign(L.slots(), -1);
     for (int g = 0; g < lanes; ++g)
@@ -580,9 +583,9 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     // duplicate observations of one pair never straddles two lanes)
     const double avg = NP ? (double)Mb / NP : 0.0;
     B.lpp = avg >= 32 ? 2 : 1;   // measured on config 3 (K = 10): 1 lane per pose beats 2 and 4
-    if (const char* e = std::getenv("BOS_LANES_PER_POSE")) {   // tuning override: 1, 2 or 4
+    if (const char* e = std::getenv("BOS_LANES_PER_POSE")) {   // tuning override: 1 or 2
         const int v = std::atoi(e);
-        if (v == 1 || v == 2 || v == 4) B.lpp = v;
+        if (v == 1 || v == 2) B.lpp = v;
     }
     const int L = B.lpp;
     auto same_lm = [&](int i, int j) { return pi.b_lm[pb_obs[i]] == pi.b_lm[pb_obs[j]]; };
@@ -607,8 +610,24 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     for (int p = 0; p < NP; ++p)
         for (int i = pb_ptr[p] + 1; i < pb_ptr[p + 1]; ++i)
             if (same_lm(i, i - 1)) B.has_dups = true;
-    make_lane_lists(NP * L, lane_ptr, pb_obs, B.pose_lanes);
-    make_lane_lists(NL, lb_ptr, lb_obs, B.lm_lanes);
+    make_lane_lists(NP * L, lane_ptr, pb_obs, B.pose_lanes, true);
+    {   // landmark lanes, degree-sorted inside each window (ties by id: deterministic)
+        B.lm_lane_lm.resize(NL);
+        for (int l = 0; l < NL; ++l) B.lm_lane_lm[l] = l;
+        auto deg = [&](int l) { return lb_ptr[l + 1] - lb_ptr[l]; };
+        const char* no_sort = std::getenv("BOS_LM_SORT");   // tuning override: 0 = landmark order
+        if (!no_sort || std::atoi(no_sort) != 0)
+            for (int w0 = 0; w0 < NL; w0 += kLmWindow)
+                std::stable_sort(B.lm_lane_lm.begin() + w0, B.lm_lane_lm.begin() + std::min(NL, w0 + kLmWindow),
+                                 [&](int a, int b) { return deg(a) > deg(b); });
+        std::vector<int32_t> lptr(NL + 1, 0), litems(Mb);
+        for (int g = 0; g < NL; ++g) {
+            const int l = B.lm_lane_lm[g];
+            std::copy(lb_obs.begin() + lb_ptr[l], lb_obs.begin() + lb_ptr[l + 1], litems.begin() + lptr[g]);
+            lptr[g + 1] = lptr[g] + deg(l);
+        }
+        make_lane_lists(NL, lptr, litems, B.lm_lanes, false);
+    }
     // pose-landmark blocks: the slot of the last bearing of each (pose, landmark) run
     B.ub_ptr.assign(NP + 1, 0);
     for (int p = 0; p < NP; ++p) {
@@ -657,7 +676,8 @@ void build_ownership(const ProblemIndex& pi, Plan& P, int rank, int world) {
         return c;
     };
     P.rank_pose = cuts(pi.NP, ppw, npose_items);
-    P.rank_lm = cuts(pi.NL, 64, [&](int l) { return (int64_t)1 + B.lm_lanes.cnt[l]; });
+    // landmark lanes cut at window boundaries: each rank owns a contiguous landmark range
+    P.rank_lm = cuts(pi.NL, kLmWindow, [&](int g) { return (int64_t)1 + B.lm_lanes.cnt[g]; });
     P.rank = rank;
     P.world = world;
     P.p_begin = P.rank_pose[rank]; P.p_end = P.rank_pose[rank + 1];
@@ -957,7 +977,10 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
         for (int i = 0; i < cnt; ++i) ++hit[v0 + i];
         return true;
     };
-    if ((P.p_begin * (int64_t)L) % 64 || P.l_begin % 64) { err = "shard does not start at a wave"; return BOS_ERR_INVALID; }
+    if (((P.p_begin * (int64_t)L) % 64 && P.p_begin != NP) || (P.l_begin % 64 && P.l_begin != NL)) {
+        err = "shard does not start at a wave";
+        return BOS_ERR_INVALID;
+    }
     std::vector<int32_t> slot_block(PL.slots(), -1);   // landmark whose block lives in the slot
     for (int p = 0; p < NP; ++p)
         for (int u = B.ub_ptr[p]; u < B.ub_ptr[p + 1]; ++u) slot_block[B.ub_slot[u]] = B.ub_lm[u];
@@ -995,10 +1018,16 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
             }
         }
     }
-    for (int l = P.l_begin; l < P.l_end; ++l) {
-        if (LL.cnt[l] > LL.w_len[l / 64]) { err = "lane longer than its wave"; return BOS_ERR_INVALID; }
-        for (int j = 0; j < LL.cnt[l]; ++j) {
-            const int32_t k = LL.obs[lane_slot(LL, l, j)];
+    if ((P.l_begin % kLmWindow && P.l_begin != NL) || (P.l_end % kLmWindow && P.l_end != NL)) {
+        err = "landmark shard not aligned to a lane window";
+        return BOS_ERR_INVALID;
+    }
+    for (int g = P.l_begin; g < P.l_end; ++g) {
+        const int l = B.lm_lane_lm[g];
+        if (l / kLmWindow != g / kLmWindow) { err = "landmark lane outside its window"; return BOS_ERR_INVALID; }
+        if (LL.cnt[g] > LL.w_len[g / 64]) { err = "lane longer than its wave"; return BOS_ERR_INVALID; }
+        for (int j = 0; j < LL.cnt[g]; ++j) {
+            const int32_t k = LL.obs[lane_slot(LL, g, j)];
             if (k < 0 || pi.b_lm[k] != l) { err = "bearing slot of the wrong landmark"; return BOS_ERR_INVALID; }
         }
         if (!mark(B.off_ldiag + 3 * (int64_t)l, 3)) { err = "landmark diagonal out of range"; return BOS_ERR_INVALID; }

@@ -53,12 +53,17 @@ struct LaneLists {
     int64_t slots() const { return w_base.empty() ? 0 : w_base.back(); }
 };
 
+constexpr int kLmWindow = 256;   // landmark lanes are permuted only inside aligned windows of this size
+
 struct BlockLayout {
     int64_t off_ldiag = 0, off_pl = 0, off_pp = 0, size = 0;
-    int lpp = 1;                        // lanes per pose: 1, 2 or 4
+    int lpp = 1;                        // lanes per pose: 1 or 2
     bool has_dups = false;              // some (pose, landmark) or (src, dst) pair repeats
     LaneLists pose_lanes;               // lanes = NP * lpp
-    LaneLists lm_lanes;                 // lanes = NL
+    LaneLists lm_lanes;                 // lanes = NL, lane g -> landmark lm_lane_lm[g]
+    // landmark of each landmark lane: inside each window of kLmWindow lanes the window's landmarks
+    // sorted by degree (descending), so the lanes of a wave walk lists of similar length
+    std::vector<int32_t> lm_lane_lm;
     std::vector<int32_t> ub_ptr;        // [NP + 1] pose-landmark blocks of each pose
     std::vector<int32_t> ub_lm;         // [nub] landmark of each pose-landmark block (ascending per pose)
     std::vector<int32_t> ub_slot;       // [nub] bearing slot holding the block
