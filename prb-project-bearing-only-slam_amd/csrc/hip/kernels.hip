@@ -218,17 +218,19 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
         // pair ahead; every register is refilled by a load right after its last use, so no loaded
         // value is ever copied (a copy waits for its load) and each gather has a whole pair of items
         // to land. All unguarded: the record arrays carry kRecPad padding records (landmark 0).
-        const BRec<T>* rp = P.pb + sl;
-        int iA = rp[0].idx & kIdxMask, iB = rp[64].idx & kIdxMask;
+        const int32_t* ip = P.pb_idx + sl;
+        const T* zp = P.pb_z + sl;
+        int iA = ip[0], iB = ip[64];
         OdoIn<T> oa, ob;
         int otha = 0, othb = 0;
         if (x0 < x1) odo_fetch_ids(P, x0, oa, otha);
         if (x0 + 1 < x1) odo_fetch_ids(P, x0 + 1, ob, othb);
-        BRec<T> rA = rp[0], rB = rp[64];
-        V2<T> LA = load2(P.lc + 2 * iA), LB = load2(P.lc + 2 * iB);
+        V2<T> LA = load2(P.lc + 2 * (iA & kIdxMask)), LB = load2(P.lc + 2 * (iB & kIdxMask));
+        T zA = zp[0], zB = zp[64];
+        bool lastA = !(iA & kRunCont), lastB = !(iB & kRunCont);
         T wA = HAS_W ? P.pb_w[sl] : (T)1, wB = HAS_W ? P.pb_w[sl + 64] : (T)1;
-        iA = rp[128].idx & kIdxMask;
-        iB = rp[192].idx & kIdxMask;
+        iA = ip[128];
+        iB = ip[192];
         // odometry first (fp32): its arithmetic covers the landmark gathers of items 0 and 1; the
         // fp64 variant runs it after the bearings, which keeps it within 128 VGPRs
         constexpr bool kOdoFirst = true;
@@ -250,28 +252,30 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
         T acc[6] = {0, 0, 0, 0, 0, 0}, o[6];
         T* blkp = P.hval + P.off_pl + 6 * sl;
         stamp(P.diag_stamps, st, 1);
-        for (int j = 0; j < n; j += 2, rp += 128, blkp += 6 * 128) {
-            // item j (set A), then refill A with item j + 2 (record, gather) and j + 4 (index)
-            pose_bearing<T>(P, X, LA, rA.z, wA, h, gb, o, chi, nrob);
-            put_pl<T, HAS_DUPS>(blkp, o, acc, !(rA.idx & kRunCont));
-            rA = rp[128];
-            LA = load2(P.lc + 2 * iA);
+        for (int j = 0; j < n; j += 2, ip += 128, zp += 128, blkp += 6 * 128) {
+            // item j (set A), then refill A: item j + 2's gather and z, item j + 4's index
+            pose_bearing<T>(P, X, LA, zA, wA, h, gb, o, chi, nrob);
+            put_pl<T, HAS_DUPS>(blkp, o, acc, lastA);
+            lastA = !(iA & kRunCont);
+            LA = load2(P.lc + 2 * (iA & kIdxMask));
+            zA = zp[128];
             if (HAS_W) wA = P.pb_w[sl + 64 * (j + 2)];
-            iA = rp[256].idx & kIdxMask;
+            iA = ip[256];
             // item j + 1 (set B). Its block is stored even past the lane's last item (a padding slot
             // of the lane's wave: pose-lane waves have an even number of slots per lane), so both
             // paths issue the same memory operations and the loop's waits stay exact.
             if (j + 1 < n) {
-                pose_bearing<T>(P, X, LB, rB.z, wB, h, gb, o, chi, nrob);
+                pose_bearing<T>(P, X, LB, zB, wB, h, gb, o, chi, nrob);
             } else {
 #pragma unroll
                 for (int q = 0; q < 6; ++q) o[q] = (T)0;
             }
-            put_pl<T, HAS_DUPS>(blkp + 6 * 64, o, acc, !(rB.idx & kRunCont));
-            rB = rp[192];
-            LB = load2(P.lc + 2 * iB);
+            put_pl<T, HAS_DUPS>(blkp + 6 * 64, o, acc, lastB);
+            lastB = !(iB & kRunCont);
+            LB = load2(P.lc + 2 * (iB & kIdxMask));
+            zB = zp[192];
             if (HAS_W) wB = P.pb_w[sl + 64 * (j + 3)];
-            iB = rp[320].idx & kIdxMask;
+            iB = ip[320];
         }
         stamp(P.diag_stamps, st, 2);
         if (!kOdoFirst) odometry();
@@ -315,25 +319,26 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int blk, un
     const V2<T> Lm = load2(P.lc + 2 * l);
     T hl[3] = {0, 0, 0}, gl[2] = {0, 0};
     // paired register sets as in pose_lanes (padding records point at pose 0)
-    const BRec<T>* rp = P.lb + sl;
-    int iA = rp[0].idx, iB = rp[64].idx;
-    T zA = rp[0].z, zB = rp[64].z;
+    const int32_t* ip = P.lb_idx + sl;
+    const T* zp = P.lb_z + sl;
+    int iA = ip[0], iB = ip[64];
     V4<T> XA = load4(P.pc + 4 * iA), XB = load4(P.pc + 4 * iB);
+    T zA = zp[0], zB = zp[64];
     T wA = HAS_W ? P.lb_w[sl] : (T)1, wB = HAS_W ? P.lb_w[sl + 64] : (T)1;
-    iA = rp[128].idx;
-    iB = rp[192].idx;
+    iA = ip[128];
+    iB = ip[192];
     stamp(P.diag_stamps, st, 1);
-    for (int j = 0; j < n; j += 2, rp += 128) {
+    for (int j = 0; j < n; j += 2, ip += 128, zp += 128) {
         landmark_bearing<T>(P, XA, Lm, zA, wA, hl, gl);
-        zA = rp[128].z;
         XA = load4(P.pc + 4 * iA);
+        zA = zp[128];
         if (HAS_W) wA = P.lb_w[sl + 64 * (j + 2)];
-        iA = rp[256].idx;
+        iA = ip[256];
         if (j + 1 < n) landmark_bearing<T>(P, XB, Lm, zB, wB, hl, gl);
-        zB = rp[192].z;
         XB = load4(P.pc + 4 * iB);
+        zB = zp[192];
         if (HAS_W) wB = P.lb_w[sl + 64 * (j + 3)];
-        iB = rp[320].idx;
+        iB = ip[320];
     }
     stamp(P.diag_stamps, st, 2);
     T* hp = P.hval + P.off_ldiag + 3 * l;

@@ -17,11 +17,8 @@ constexpr int kRecPad = 512;
 constexpr int32_t kRunCont = (int32_t)0x80000000u;
 constexpr int32_t kIdxMask = 0x7fffffff;
 
-// One observation in a lane's list: the other endpoint (landmark for the pose lists, pose for the
-// landmark lists) and the measured bearing; one vector load.
-template <typename T> struct BRec;
-template <> struct alignas(8) BRec<float> { int32_t idx; float z; };
-template <> struct alignas(16) BRec<double> { int32_t idx; int32_t pad; double z; };
+// A lane list item is the other endpoint (landmark for the pose lists, pose for the landmark lists)
+// and the measured bearing, stored as two arrays (index, z) so each is read exactly once.
 
 // J+H build (host/plan.hpp BlockLayout). Blocks [0, pose_blocks) run lane groups of lpp lanes
 // per owned pose, the rest one lane per owned landmark. Lane lists are wave-interleaved: item j of
@@ -36,7 +33,8 @@ template <typename T> struct LinParams {
     // pose lanes
     const int32_t* pw_base;   // [waves + 1]
     const int32_t* pl_cnt;    // [NP * lpp]
-    const BRec<T>* pb;        // [slots] (landmark, z); the pose-landmark block of a slot is at off_pl + 6 slot
+    const int32_t* pb_idx;    // [slots] landmark (| kRunCont); the pose-landmark block of a slot is at off_pl + 6 slot
+    const T* pb_z;            // [slots] measured bearing
     const T* pb_w;            // [slots] information, null => 1
     const int32_t* po_ptr;    // [NP + 1]
     const int32_t* po_ent;    // edge << 1 | destination side
@@ -50,7 +48,8 @@ template <typename T> struct LinParams {
     const int32_t* lw_base;   // [waves + 1]
     const int32_t* ll_cnt;    // [NL] per lane
     const int32_t* ll_lm;     // [NL] landmark of each lane (degree-sorted inside 256-lane windows)
-    const BRec<T>* lb;        // [slots] (pose, z)
+    const int32_t* lb_idx;    // [slots] pose
+    const T* lb_z;            // [slots] measured bearing
     const T* lb_w;
     // outputs
     T* hval;                  // block array (BlockLayout)

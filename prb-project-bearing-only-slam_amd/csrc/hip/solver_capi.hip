@@ -82,7 +82,8 @@ struct bos_solver {
     // J+H work lists (host/plan.hpp BlockLayout)
     int32_t *pw_base = nullptr, *pl_cnt = nullptr, *lw_base = nullptr, *ll_cnt = nullptr, *ll_lm = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_oth = nullptr, *po_blk = nullptr, *csr_src = nullptr,
             *elim_ref = nullptr;
-    void *pb = nullptr, *pb_w = nullptr, *lb = nullptr, *lb_w = nullptr;
+    int32_t *pb_idx = nullptr, *lb_idx = nullptr;
+    void *pb_z = nullptr, *pb_w = nullptr, *lb_z = nullptr, *lb_w = nullptr;
     int pose_blocks = 0;
     // odometry
     int32_t *o_src = nullptr, *o_dst = nullptr;
@@ -134,11 +135,11 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.p_begin = P.p_begin; p.p_end = P.p_end; p.l_begin = P.l_begin; p.l_end = P.l_end;
     p.pose_blocks = s->pose_blocks;
     p.pw_base = s->pw_base; p.pl_cnt = s->pl_cnt;
-    p.pb = (const bos::dev::BRec<T>*)s->pb; p.pb_w = (const T*)s->pb_w;
+    p.pb_idx = s->pb_idx; p.pb_z = (const T*)s->pb_z; p.pb_w = (const T*)s->pb_w;
     p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_oth = s->po_oth; p.po_blk = s->po_blk;
     p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
     p.lw_base = s->lw_base; p.ll_cnt = s->ll_cnt; p.ll_lm = s->ll_lm;
-    p.lb = (const bos::dev::BRec<T>*)s->lb; p.lb_w = (const T*)s->lb_w;
+    p.lb_idx = s->lb_idx; p.lb_z = (const T*)s->lb_z; p.lb_w = (const T*)s->lb_w;
     p.hval = (T*)s->d_val;
     p.b = (T*)s->d_b;
     p.off_ldiag = (int)P.blk.off_ldiag; p.off_pl = (int)P.blk.off_pl; p.off_pp = (int)P.blk.off_pp;
@@ -389,7 +390,7 @@ int bos_destroy(bos_solver* s) {
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pl_cnt, s->lw_base, s->ll_cnt, s->ll_lm,
-                    s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb, s->pb_w, s->lb, s->lb_w,
+                    s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_chi, s->d_nrob,
@@ -542,29 +543,13 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             const int32_t e = B.po_ent[x];
             po_oth[x] = (e & 1) ? pb->odom_src[e >> 1] : pb->odom_dst[e >> 1];
         }
-        auto upload_recs = [&](void** dst, const std::vector<int32_t>& idx, const std::vector<double>& z) -> int {
-            if (f32) {
-                std::vector<bos::dev::BRec<float>> r(idx.size());
-                for (size_t i = 0; i < r.size(); ++i) { r[i].idx = idx[i]; r[i].z = (float)z[i]; }
-                bos::dev::BRec<float>* d = nullptr;
-                const int e = upload(&d, r);
-                *dst = d;
-                return e;
-            }
-            std::vector<bos::dev::BRec<double>> r(idx.size());
-            for (size_t i = 0; i < r.size(); ++i) { r[i].idx = idx[i]; r[i].pad = 0; r[i].z = z[i]; }
-            bos::dev::BRec<double>* d = nullptr;
-            const int e = upload(&d, r);
-            *dst = d;
-            return e;
-        };
         if ((rc = upload(&s->pw_base, B.pose_lanes.w_base)) || (rc = upload(&s->pl_cnt, B.pose_lanes.cnt)) ||
             (rc = upload(&s->lw_base, B.lm_lanes.w_base)) || (rc = upload(&s->ll_cnt, B.lm_lanes.cnt)) ||
             (rc = upload(&s->ll_lm, B.lm_lane_lm)) ||
             (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, B.po_ent)) ||
             (rc = upload(&s->po_oth, po_oth)) ||
-            (rc = upload(&s->po_blk, B.po_blk)) || (rc = upload_recs(&s->pb, pbi, pbz)) ||
-            (rc = upload_recs(&s->lb, lbi, lbz)))
+            (rc = upload(&s->po_blk, B.po_blk)) || (rc = upload(&s->pb_idx, pbi)) || (rc = upload_Tv(&s->pb_z, pbz)) ||
+            (rc = upload(&s->lb_idx, lbi)) || (rc = upload_Tv(&s->lb_z, lbz)))
             return bail(rc);
         if (s->has_w) {
             pbw.assign(po.size() + pad, 0.0); lbw.assign(lo.size() + pad, 0.0);
