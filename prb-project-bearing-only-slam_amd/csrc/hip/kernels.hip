@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams
 }
 
 // State::apply_boxplus (framework/state.cpp:69-80): dx = -x (the solve ran on +b)
-template <typename T> __global__ void boxplus_kernel(const UpdateParams<T> U) {
+template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_kernel(const UpdateParams<T> U) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     double m = 0.0;
     if (i < U.NP) {
@@ -423,28 +423,54 @@ template <typename T> __global__ void boxplus_kernel(const UpdateParams<T> U) {
         U.lc[2 * j + 1] = (T)y;
         m = fmax(fabs(dx), fabs(dy));
     }
-    // max is order independent: deterministic
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0 && m > 0.0)
-        atomicMax(U.max_dx_bits, (unsigned long long)__double_as_longlong(m));
+    // block max into its partial slot (max is order independent: deterministic; no atomics, which
+    // would serialize on one address)
+    m = fmax(m, __shfl_xor(m, 32));
+    m = fmax(m, __shfl_xor(m, 16));
+    m = fmax(m, __shfl_xor(m, 8));
+    m = fmax(m, __shfl_xor(m, 4));
+    m = fmax(m, __shfl_xor(m, 2));
+    m = fmax(m, __shfl_xor(m, 1));
+    __shared__ double sm[kUpdateBlock / 64];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double b = sm[0];
+        for (int w = 1; w < kUpdateBlock / 64; ++w) b = fmax(b, sm[w]);
+        U.max_part[blockIdx.x] = b;
+    }
 }
 
-__global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_part, int n, double* chi_out,
-                                    int32_t* nrob_out) {
+__global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_part, int n, const double* max_part,
+                                    int n_max, int32_t* info, int32_t* reset, int n_reset, StepStatus* out) {
     __shared__ double sc[256];
+    __shared__ double sm[256];
     __shared__ long long sr[256];
-    double c = 0.0;
+    double c = 0.0, m = 0.0;
     long long r = 0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) { c += chi_part[i]; r += nrob_part[i]; }
+    if (max_part)
+        for (int i = threadIdx.x; i < n_max; i += blockDim.x) m = fmax(m, max_part[i]);
     sc[threadIdx.x] = c;
+    sm[threadIdx.x] = m;
     sr[threadIdx.x] = r;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) { sc[threadIdx.x] += sc[threadIdx.x + o]; sr[threadIdx.x] += sr[threadIdx.x + o]; }
+        if ((int)threadIdx.x < o) {
+            sc[threadIdx.x] += sc[threadIdx.x + o];
+            sr[threadIdx.x] += sr[threadIdx.x + o];
+            sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + o]);
+        }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { *chi_out = sc[0]; *nrob_out = (int32_t)sr[0]; }
+    if ((int)threadIdx.x < n_reset) reset[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        out->chi2 = sc[0];
+        out->n_robust = (int32_t)sr[0];
+        out->max_dx = sm[0];
+        out->info = info ? *info : 0;
+        if (info) *info = 0;
+    }
 }
 
 template <typename T> __global__ void to_f64_kernel(const T* in, double* out, int64_t n) {
@@ -510,13 +536,15 @@ hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s) {
     const int n = p.NP + p.NL;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL((boxplus_kernel<T>), dim3((n + 255) / 256), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((boxplus_kernel<T>), dim3((n + kUpdateBlock - 1) / kUpdateBlock), dim3(kUpdateBlock), 0, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double* chi_out,
-                               int32_t* nrob_out, hipStream_t s) {
-    hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n, chi_out, nrob_out);
+hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, const double* max_part,
+                               int n_max, int32_t* info, int32_t* reset, int n_reset, StepStatus* out, hipStream_t s) {
+    if (n_reset > 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n, max_part, n_max, info,
+                       reset, n_reset, out);
     return hipGetLastError();
 }
 

@@ -74,14 +74,28 @@ template <typename T> struct UpdateParams {
     T* pc;
     T* pth;
     T* lc;
-    unsigned long long* max_dx_bits;   // max |dx| as ordered bits of a non-negative double
+    double* max_part;         // [update blocks] max |dx| of each block (reduced by reduce_stats)
 };
+
+// End-of-iteration summary, read back by the host in one copy.
+struct StepStatus {
+    double chi2;
+    double max_dx;
+    int32_t n_robust;
+    int32_t info;     // solver status (multifrontal: first non-positive pivot + 1, 0 = ok)
+};
+
+constexpr int kUpdateBlock = 256;
 
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s);
-hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double* chi_out,
-                               int32_t* nrob_out, hipStream_t s);
+// Reduces the J+H kernel's chi^2 / robust-count partials (and the box-plus max |dx| partials when
+// max_part is set) into *out, moves *info into out->info, then zeroes *info and reset[0, n_reset)
+// (the solver's work-queue tickets) for the next iteration: one launch replaces the per-step
+// memsets and read-backs.
+hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, const double* max_part,
+                               int n_max, int32_t* info, int32_t* reset, int n_reset, StepStatus* out, hipStream_t s);
 template <typename T> hipError_t launch_to_f64(const T* in, double* out, int64_t n, hipStream_t s);
 // out[i] = (double)in[idx[i]]
 template <typename T> hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s);

@@ -753,7 +753,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         return rc;
     if (hipMalloc((void**)&d->done, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(d->done, 0, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void**)&d->tickets, 3 * sizeof(int)) != hipSuccess) {
+        hipMalloc((void**)&d->tickets, 3 * sizeof(int)) != hipSuccess || hipMemset(d->tickets, 0, 3 * sizeof(int)) != hipSuccess) {
         err = "hipMalloc failed (multifrontal flow)";
         return -2;
     }
@@ -792,9 +792,10 @@ void mf_destroy(MfDevice* d) {
     delete d;
 }
 
+// info and the work-queue tickets are zero on entry: zeroed at creation and, after every
+// iteration, by the end-of-step reduce_stats launch (mf_info_ptr / mf_tickets_ptr).
 hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(d->info, 0, sizeof(int32_t), s);
-    if (e != hipSuccess) return e;
+    hipError_t e;
     const uint32_t epoch = ++d->epoch;
     for (int l = 0; l < d->flow_lev0; ++l) {
         int n;
@@ -811,7 +812,6 @@ hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (d->n_flow_factor > 0) {
-        if ((e = hipMemsetAsync(d->tickets, 0, sizeof(int), s)) != hipSuccess) return e;
         const Flow f{d->order_factor, d->n_flow_factor, d->tickets, d->done, epoch, d->slev, d->flow_lev0};
         const int grid = std::min(d->n_flow_factor, d->ncu * 12);
         hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(0, 0, A, x), f);
@@ -826,7 +826,6 @@ hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
     hipError_t e;
     const uint32_t epoch = ++d->epoch;
     if (d->flow_solve) {
-        if ((e = hipMemsetAsync(d->tickets + 1, 0, sizeof(int), s)) != hipSuccess) return e;
         const Flow fb{d->order_bwd, d->n_flow_solve, d->tickets + 1, d->done + d->nsuper, epoch, d->slev, d->solve_lev0};
         const int grid = std::min(d->n_flow_solve, d->ncu * 8);
         hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), d->lds_bwd_flow, s, d->args(0, 0, nullptr, x), fb,
@@ -851,7 +850,8 @@ hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
     return hipSuccess;
 }
 
-const int32_t* mf_info_ptr(const MfDevice* d) { return d->info; }
+int32_t* mf_info_ptr(const MfDevice* d) { return d->info; }
+int32_t* mf_tickets_ptr(const MfDevice* d) { return d->tickets; }
 
 }  // namespace dev
 }  // namespace bos

@@ -20,7 +20,10 @@ hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s);
 // Backward substitution: x <- L^{-T} x, completing x = H^{-1} b.
 hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s);
 // device counter of non-positive pivots met by the last factorization
-const int32_t* mf_info_ptr(const MfDevice* d);
+int32_t* mf_info_ptr(const MfDevice* d);
+// work-queue tickets (kMfTickets ints), zero between iterations
+int32_t* mf_tickets_ptr(const MfDevice* d);
+constexpr int kMfTickets = 3;
 
 }  // namespace dev
 }  // namespace bos

@@ -103,9 +103,8 @@ struct bos_solver {
     int32_t* d_info = nullptr;
     double* d_chi_part = nullptr;
     int32_t* d_nrob_part = nullptr;
-    double* d_chi = nullptr;
-    int32_t* d_nrob = nullptr;
-    unsigned long long* d_maxdx = nullptr;
+    bos::dev::StepStatus* d_status = nullptr;   // end-of-iteration summary (one read-back)
+    double* d_maxpart = nullptr;                 // box-plus max |dx| per update block
     rocblas_handle rb = nullptr;
     rocsolver_rfinfo rf = nullptr;
     bos::dev::MfDevice* mf = nullptr;
@@ -163,7 +162,7 @@ template <typename T> bos::dev::UpdateParams<T> upd_params(const bos_solver* s) 
     u.x = s->d_rhs;
     u.pose = s->d_pose; u.lm = s->d_lm;
     u.pc = (T*)s->d_pc; u.pth = (T*)s->d_pth; u.lc = (T*)s->d_lc;
-    u.max_dx_bits = s->d_maxdx;
+    u.max_part = s->d_maxpart;
     return u;
 }
 
@@ -208,13 +207,17 @@ int enqueue_exchange(bos_solver* s) {
     return BOS_OK;
 }
 
-int enqueue_stats(bos_solver* s) {
-    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->pose_blocks, s->d_chi, s->d_nrob,
+int enqueue_stats(bos_solver* s, bool with_update) {
+    int32_t* info = uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : (s->solver_kind == BOS_SOLVER_DENSE_CHOL ? s->d_info : nullptr);
+    int32_t* tickets = uses_mf(s) ? bos::dev::mf_tickets_ptr(s->mf) : nullptr;
+    const int nupd = (s->NP + s->NL + bos::dev::kUpdateBlock - 1) / bos::dev::kUpdateBlock;
+    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->pose_blocks, with_update ? s->d_maxpart : nullptr,
+                                          nupd, info, tickets, tickets ? bos::dev::kMfTickets : 0, s->d_status,
                                           s->stream));
     if (s->comm) {
         NC_TRY(ncclGroupStart());
-        NC_TRY(ncclAllReduce(s->d_chi, s->d_chi, 1, ncclDouble, ncclSum, s->comm, s->stream));
-        NC_TRY(ncclAllReduce(s->d_nrob, s->d_nrob, 1, ncclInt32, ncclSum, s->comm, s->stream));
+        NC_TRY(ncclAllReduce(&s->d_status->chi2, &s->d_status->chi2, 1, ncclDouble, ncclSum, s->comm, s->stream));
+        NC_TRY(ncclAllReduce(&s->d_status->n_robust, &s->d_status->n_robust, 1, ncclInt32, ncclSum, s->comm, s->stream));
         NC_TRY(ncclGroupEnd());
     }
     return BOS_OK;
@@ -264,7 +267,6 @@ int enqueue_solve(bos_solver* s, bool& ran_analysis) {
 }
 
 int enqueue_update(bos_solver* s) {
-    HIP_TRY(hipMemsetAsync(s->d_maxdx, 0, sizeof(unsigned long long), s->stream));
     hipError_t e = s->precision == BOS_FP32 ? bos::dev::launch_boxplus<float>(upd_params<float>(s), s->stream)
                                             : bos::dev::launch_boxplus<double>(upd_params<double>(s), s->stream);
     if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("boxplus launch: ") + hipGetErrorString(e));
@@ -304,26 +306,16 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
-int read_stats(bos_solver* s, bos_step_stats* st, bool with_update, bool with_solve) {
-    double chi = 0;
-    int32_t nrob = 0, info = 0;
-    unsigned long long mdx = 0;
-    HIP_TRY(hipMemcpyAsync(&chi, s->d_chi, sizeof(double), hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipMemcpyAsync(&nrob, s->d_nrob, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
-    if (with_update) HIP_TRY(hipMemcpyAsync(&mdx, s->d_maxdx, sizeof(mdx), hipMemcpyDeviceToHost, s->stream));
-    if (with_solve && s->solver_kind == BOS_SOLVER_DENSE_CHOL)
-        HIP_TRY(hipMemcpyAsync(&info, s->d_info, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
-    if (with_solve && uses_mf(s))
-        HIP_TRY(hipMemcpyAsync(&info, bos::dev::mf_info_ptr(s->mf), sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+int read_stats(bos_solver* s, bos_step_stats* st) {
+    bos::dev::StepStatus h;
+    HIP_TRY(hipMemcpyAsync(&h, s->d_status, sizeof(h), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     if (st) {
         std::memset(st, 0, sizeof(*st));
-        st->chi2 = chi;
-        st->n_robust = nrob;
-        st->solver_info = info;
-        double m = 0;
-        std::memcpy(&m, &mdx, sizeof(m));
-        st->max_abs_dx = m;
+        st->chi2 = h.chi2;
+        st->n_robust = h.n_robust;
+        st->solver_info = h.info;
+        st->max_abs_dx = h.max_dx;
     }
     return BOS_OK;
 }
@@ -339,11 +331,11 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     if ((rc = enqueue_solve(s, analysed_now))) return rc;
     HIP_TRY(hipEventRecord(s->ev[3], s->stream));
     if ((rc = enqueue_update(s))) return rc;
-    if ((rc = enqueue_stats(s))) return rc;
+    if ((rc = enqueue_stats(s, true))) return rc;
     HIP_TRY(hipEventRecord(s->ev[4], s->stream));
     s->have_dx = true;
     if (!sync) return BOS_OK;
-    if ((rc = read_stats(s, st, true, true))) return rc;
+    if ((rc = read_stats(s, st))) return rc;
     if (st) {
         st->t_linearize_ms = elapsed(s->ev[0], s->ev[2]);
         st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
@@ -393,8 +385,8 @@ int bos_destroy(bos_solver* s) {
                     s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
-                    s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_chi, s->d_nrob,
-                    s->d_maxdx};
+                    s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_status,
+                    s->d_maxpart};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (s->rf) rocsolver_destroy_rfinfo(s->rf);
@@ -608,7 +600,8 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     }
     const int nt = std::max(1, s->pose_blocks);
     if ((rc = dalloc(&s->d_info, 1)) || (rc = dalloc(&s->d_chi_part, nt)) || (rc = dalloc(&s->d_nrob_part, nt)) ||
-        (rc = dalloc(&s->d_chi, 1)) || (rc = dalloc(&s->d_nrob, 1)) || (rc = dalloc(&s->d_maxdx, 1)))
+        (rc = dalloc(&s->d_status, 1)) ||
+        (rc = dalloc(&s->d_maxpart, (size_t)std::max(1, (s->NP + s->NL + bos::dev::kUpdateBlock - 1) / bos::dev::kUpdateBlock))))
         return bail(rc);
     HIP_TRY(hipMemset(s->d_chi_part, 0, nt * sizeof(double)));
     HIP_TRY(hipMemset(s->d_nrob_part, 0, nt * sizeof(int32_t)));
@@ -699,8 +692,8 @@ int bos_linearize(bos_solver* s, bos_step_stats* st) {
     HIP_TRY(hipEventRecord(s->ev[1], s->stream));
     if ((rc = enqueue_exchange(s))) return rc;
     HIP_TRY(hipEventRecord(s->ev[2], s->stream));
-    if ((rc = enqueue_stats(s))) return rc;
-    if ((rc = read_stats(s, st, false, false))) return rc;
+    if ((rc = enqueue_stats(s, false))) return rc;
+    if ((rc = read_stats(s, st))) return rc;
     if (st) {
         st->t_linearize_ms = elapsed(s->ev[0], s->ev[2]);
         st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
