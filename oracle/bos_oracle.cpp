@@ -298,6 +298,112 @@ int linearize(const ProblemView<T>& P, double kernel_threshold, double damping, 
     return 0;
 }
 
+// The same accumulation, parallel without per-thread copies of H and b ("owner computes", the
+// CPU baseline of bench.py): each pose owns its diagonal block, its b entries and the pose-landmark
+// blocks of its bearings; each landmark owns its diagonal block and b entries. A bearing is
+// evaluated twice (once by its pose, once by its landmark), an odometry edge by both endpoints
+// (the source also writes the off-diagonal block and counts chi^2). Only the summation order of
+// the diagonal blocks and b differs from linearize() (rounding-level differences).
+//   pb_ptr/pb_obs: bearings grouped by pose; lb_ptr/lb_obs: by landmark;
+//   po_ptr/po_ent: odometry entries of each pose, edge << 1 | (pose is the destination).
+template <typename T>
+int linearize_owner(const ProblemView<T>& P, const int32_t* pb_ptr, const int32_t* pb_obs, const int32_t* lb_ptr,
+                    const int32_t* lb_obs, const int32_t* po_ptr, const int32_t* po_ent, double kernel_threshold,
+                    double damping, double* pose_diag, double* lm_diag, double* hpl, double* hoff, double* b,
+                    double* chi2_out, int* nrobust_out, int threads) {
+    const int NP = P.NP, NL = P.NL;
+    const T kt = (T)kernel_threshold, lam = (T)damping;
+    const int nt = num_threads_or(threads);
+    double chi2 = 0.0;
+    long long nr = 0;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nt) schedule(dynamic, 256) reduction(+ : chi2, nr)
+#endif
+    for (int ip = 0; ip < NP; ++ip) {
+        const PoseT<T> p = load_pose<T>(P.pose_xyt, ip);
+        T H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, B[3] = {0, 0, 0};
+        for (int x = pb_ptr[ip]; x < pb_ptr[ip + 1]; ++x) {
+            const int k = pb_obs[x], il = P.b_lm[k];
+            T J[5];
+            T e = bearing_error_and_jacobian<T>(p, (T)P.lm_xy[2 * il], (T)P.lm_xy[2 * il + 1], (T)P.b_z[k], J);
+            const T w = P.b_omega ? (T)P.b_omega[k] : (T)1;
+            const T rho = e * w * e;
+            chi2 += (double)rho;
+            if (rho > kt) { e *= std::sqrt(kt / rho); ++nr; }
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) H[3 * i + j] += J[i] * w * J[j];
+            double* hk = hpl + 6 * (size_t)k;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 2; ++j) hk[2 * i + j] = (double)(J[i] * w * J[3 + j]);
+            for (int i = 0; i < 3; ++i) B[i] += J[i] * w * e;
+        }
+        for (int x = po_ptr[ip]; x < po_ptr[ip + 1]; ++x) {
+            const int k = po_ent[x] >> 1;
+            const bool dst = po_ent[x] & 1;
+            const int is = P.o_src[k], id = P.o_dst[k];
+            const PoseT<T> s = load_pose<T>(P.pose_xyt, is), d = load_pose<T>(P.pose_xyt, id);
+            T z[3] = {(T)P.o_z[3 * k], (T)P.o_z[3 * k + 1], (T)P.o_z[3 * k + 2]};
+            T Om[9];
+            for (int i = 0; i < 9; ++i) Om[i] = (T)P.o_omega[9 * k + i];
+            T e[3], J[18];
+            odometry_error_and_jacobian<T>(s, d, z, e, J);
+            T Oe[3];
+            for (int i = 0; i < 3; ++i) Oe[i] = Om[3 * i] * e[0] + Om[3 * i + 1] * e[1] + Om[3 * i + 2] * e[2];
+            const T rho = e[0] * Oe[0] + e[1] * Oe[1] + e[2] * Oe[2];
+            if (rho > kt) {
+                const T sc = std::sqrt(kt / rho);
+                for (int i = 0; i < 3; ++i) Oe[i] *= sc;
+            }
+            const int c0 = dst ? 3 : 0;   // this pose's columns of J
+            T OJ[18];
+            for (int i = 0; i < 3; ++i)
+                for (int c = 0; c < 6; ++c)
+                    OJ[6 * i + c] = Om[3 * i] * J[c] + Om[3 * i + 1] * J[6 + c] + Om[3 * i + 2] * J[12 + c];
+            for (int r = 0; r < 3; ++r) {
+                for (int c = 0; c < 3; ++c)
+                    H[3 * r + c] += J[c0 + r] * OJ[c0 + c] + J[6 + c0 + r] * OJ[6 + c0 + c] + J[12 + c0 + r] * OJ[12 + c0 + c];
+                B[r] += J[c0 + r] * Oe[0] + J[6 + c0 + r] * Oe[1] + J[12 + c0 + r] * Oe[2];
+            }
+            if (!dst) {
+                chi2 += (double)rho;
+                if (rho > kt) ++nr;
+                double* hk = hoff + 9 * (size_t)k;
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c)
+                        hk[3 * r + c] = (double)(J[r] * OJ[3 + c] + J[6 + r] * OJ[9 + c] + J[12 + r] * OJ[15 + c]);
+            }
+        }
+        for (int d = 0; d < 3; ++d) H[4 * d] += lam;
+        for (int i = 0; i < 9; ++i) pose_diag[9 * (size_t)ip + i] = (double)H[i];
+        for (int i = 0; i < 3; ++i) b[3 * (size_t)ip + i] = (double)B[i];
+    }
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nt) schedule(dynamic, 512)
+#endif
+    for (int il = 0; il < NL; ++il) {
+        const T lx = (T)P.lm_xy[2 * il], ly = (T)P.lm_xy[2 * il + 1];
+        T H[4] = {0, 0, 0, 0}, B[2] = {0, 0};
+        for (int x = lb_ptr[il]; x < lb_ptr[il + 1]; ++x) {
+            const int k = lb_obs[x];
+            T J[5];
+            T e = bearing_error_and_jacobian<T>(load_pose<T>(P.pose_xyt, P.b_pose[k]), lx, ly, (T)P.b_z[k], J);
+            const T w = P.b_omega ? (T)P.b_omega[k] : (T)1;
+            const T rho = e * w * e;
+            if (rho > kt) e *= std::sqrt(kt / rho);
+            for (int i = 0; i < 2; ++i)
+                for (int j = 0; j < 2; ++j) H[2 * i + j] += J[3 + i] * w * J[3 + j];
+            for (int i = 0; i < 2; ++i) B[i] += J[3 + i] * w * e;
+        }
+        H[0] += lam;
+        H[3] += lam;
+        for (int i = 0; i < 4; ++i) lm_diag[4 * (size_t)il + i] = (double)H[i];
+        for (int i = 0; i < 2; ++i) b[3 * (size_t)NP + 2 * (size_t)il + i] = (double)B[i];
+    }
+    if (chi2_out) *chi2_out = chi2;
+    if (nrobust_out) *nrobust_out = (int)nr;
+    return 0;
+}
+
 // State::apply_boxplus — framework/state.cpp:69-80 with boxplus = v2t(dx) * X
 // (framework/state.hpp:11-13, definitions.hpp:45-53): R <- dR R, t <- dR t + dt.
 // theta is stored explicitly and kept wrapped by normalized_angle (t2v(X) then equals it).
@@ -428,6 +534,23 @@ int oracle_linearize(int precision, int NP, int NL, int Mb, int Mo, const double
     }
     ProblemView<double> P{NP, NL, Mb, Mo, -1, pose_xyt, lm_xy, b_pose, b_lm, b_z, b_omega, o_src, o_dst, o_z, o_omega};
     return linearize<double>(P, kernel_threshold, damping, pose_diag, lm_diag, hpl, hoff, b, chi2, nrobust, threads);
+}
+
+int oracle_linearize_owner(int precision, int NP, int NL, int Mb, int Mo, const double* pose_xyt, const double* lm_xy,
+                           const int32_t* b_pose, const int32_t* b_lm, const double* b_z, const double* b_omega,
+                           const int32_t* o_src, const int32_t* o_dst, const double* o_z, const double* o_omega,
+                           const int32_t* pb_ptr, const int32_t* pb_obs, const int32_t* lb_ptr, const int32_t* lb_obs,
+                           const int32_t* po_ptr, const int32_t* po_ent, double kernel_threshold, double damping,
+                           double* pose_diag, double* lm_diag, double* hpl, double* hoff, double* b, double* chi2,
+                           int* nrobust, int threads) {
+    if (precision == 32) {
+        ProblemView<float> P{NP, NL, Mb, Mo, -1, pose_xyt, lm_xy, b_pose, b_lm, b_z, b_omega, o_src, o_dst, o_z, o_omega};
+        return linearize_owner<float>(P, pb_ptr, pb_obs, lb_ptr, lb_obs, po_ptr, po_ent, kernel_threshold, damping,
+                                      pose_diag, lm_diag, hpl, hoff, b, chi2, nrobust, threads);
+    }
+    ProblemView<double> P{NP, NL, Mb, Mo, -1, pose_xyt, lm_xy, b_pose, b_lm, b_z, b_omega, o_src, o_dst, o_z, o_omega};
+    return linearize_owner<double>(P, pb_ptr, pb_obs, lb_ptr, lb_obs, po_ptr, po_ent, kernel_threshold, damping,
+                                   pose_diag, lm_diag, hpl, hoff, b, chi2, nrobust, threads);
 }
 
 void oracle_apply_boxplus(int precision, int NP, int NL, double* pose_xyt, double* lm_xy, const double* dx) {

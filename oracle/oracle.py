@@ -89,6 +89,12 @@ def lib():
                                                             ctypes.c_double, ctypes.c_double,
                                                             dp, dp, dp, dp, dp, dp,
                                                             ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        L.oracle_linearize_owner.restype = ctypes.c_int
+        L.oracle_linearize_owner.argtypes = [ctypes.c_int] * 5 + [dp, dp, ip, ip, dp, dp, ip, ip, dp, dp,
+                                                                  ip, ip, ip, ip, ip, ip,
+                                                                  ctypes.c_double, ctypes.c_double,
+                                                                  dp, dp, dp, dp, dp, dp,
+                                                                  ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.oracle_apply_boxplus.restype = None
         L.oracle_apply_boxplus.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp]
         L.oracle_triangulate.restype = ctypes.c_int
@@ -333,8 +339,35 @@ class Linearization:
     n_robust: int
 
 
+def owner_index(P: Problem):
+    """Bearings grouped by pose and by landmark, odometry entries grouped by pose (CSR), for
+    linearize(..., owner=True). Built once per problem and cached on it."""
+    idx = getattr(P, "_owner_index", None)
+    if idx is not None:
+        return idx
+    NP, NL = P.NP, P.NL
+    bp = np.asarray(P.b_pose, dtype=np.int64)
+    bl = np.asarray(P.b_lm, dtype=np.int64)
+    pb_obs = np.argsort(bp, kind="stable").astype(np.int32)
+    lb_obs = np.argsort(bl, kind="stable").astype(np.int32)
+    pb_ptr = np.concatenate([[0], np.cumsum(np.bincount(bp, minlength=NP))]).astype(np.int32)
+    lb_ptr = np.concatenate([[0], np.cumsum(np.bincount(bl, minlength=NL))]).astype(np.int32)
+    Mo = len(P.o_z)
+    ends = np.concatenate([np.asarray(P.o_src, dtype=np.int64), np.asarray(P.o_dst, dtype=np.int64)])
+    ent = np.concatenate([2 * np.arange(Mo), 2 * np.arange(Mo) + 1]).astype(np.int32)
+    order = np.argsort(ends, kind="stable")
+    po_ent = ent[order].astype(np.int32)
+    po_ptr = np.concatenate([[0], np.cumsum(np.bincount(ends, minlength=NP))]).astype(np.int32)
+    idx = (pb_ptr, pb_obs, lb_ptr, lb_obs, po_ptr, po_ent)
+    P._owner_index = idx
+    return idx
+
+
 def linearize(P: Problem, pose_xyt=None, lm_xy=None, kernel_threshold=1.0, damping=0.01,
-              precision: int = 64, threads: int = 1) -> Linearization:
+              precision: int = 64, threads: int = 1, owner: bool = False) -> Linearization:
+    """One J+H build. owner=False: the reference's accumulation order (bearings in file order,
+    then odometry; per-thread partials when threads > 1). owner=True: the owner-computes parallel
+    form (no per-thread copies; the CPU baseline of bench.py)."""
     pose_xyt = np.ascontiguousarray(P.pose_xyt if pose_xyt is None else pose_xyt, dtype=np.float64)
     lm_xy = np.ascontiguousarray(P.lm_xy if lm_xy is None else lm_xy, dtype=np.float64)
     NP, NL, Mb, Mo = P.NP, P.NL, len(P.b_z), len(P.o_z)
@@ -348,6 +381,17 @@ def linearize(P: Problem, pose_xyt=None, lm_xy=None, kernel_threshold=1.0, dampi
     bom = None if P.b_omega is None else np.ascontiguousarray(P.b_omega, dtype=np.float64)
     o_z = np.ascontiguousarray(P.o_z, dtype=np.float64)
     o_om = np.ascontiguousarray(P.o_omega, dtype=np.float64)
+    if owner:
+        pb_ptr, pb_obs, lb_ptr, lb_obs, po_ptr, po_ent = owner_index(P)
+        rc = lib().oracle_linearize_owner(precision, NP, NL, Mb, Mo, _pd(pose_xyt), _pd(lm_xy), _pi(P.b_pose),
+                                          _pi(P.b_lm), _pd(np.ascontiguousarray(P.b_z)), _pd(bom), _pi(P.o_src),
+                                          _pi(P.o_dst), _pd(o_z), _pd(o_om), _pi(pb_ptr), _pi(pb_obs), _pi(lb_ptr),
+                                          _pi(lb_obs), _pi(po_ptr), _pi(po_ent), float(kernel_threshold),
+                                          float(damping), _pd(pd), _pd(ld), _pd(hpl), _pd(hoff), _pd(b),
+                                          ctypes.byref(chi2), ctypes.byref(nrob), int(threads))
+        if rc != 0:
+            raise RuntimeError(f"oracle_linearize_owner failed: {rc}")
+        return Linearization(pd[:NP], ld[:NL], hpl[:Mb], hoff[:Mo], b[:P.N], chi2.value, nrob.value)
     rc = lib().oracle_linearize(precision, NP, NL, Mb, Mo, _pd(pose_xyt), _pd(lm_xy), _pi(P.b_pose),
                                 _pi(P.b_lm), _pd(np.ascontiguousarray(P.b_z)), _pd(bom), _pi(P.o_src),
                                 _pi(P.o_dst), _pd(o_z), _pd(o_om), float(kernel_threshold),

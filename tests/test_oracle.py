@@ -244,3 +244,19 @@ def test_wrap_knife_edge_is_reproducible(c1):
     k = int(np.nonzero(c1.b_lm == j)[0][0])
     e, _ = O.bearing_error_and_jacobian(c1.pose_xyt[c1.b_pose[k]], c1.lm_xy[j], c1.b_z[k])
     assert abs(abs(e) - PI) < 1e-12
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_owner_computes_equals_reference_order(c1, precision):
+    """The parallel owner-computes J+H (bench.py's CPU baseline) equals the reference-order
+    accumulation up to summation order: per-observation blocks bit-equal, diagonal blocks and b
+    within rounding, chi^2 and the robust count equal."""
+    a = O.linearize(c1, precision=precision)
+    for threads in (1, 4):
+        b = O.linearize(c1, precision=precision, threads=threads, owner=True)
+        tol = 1e-12 if precision == 64 else 2e-5
+        assert np.array_equal(a.hpl, b.hpl) and np.array_equal(a.hoff, b.hoff)
+        for x, y in ((a.pose_diag, b.pose_diag), (a.lm_diag, b.lm_diag), (a.b, b.b)):
+            assert np.abs(x - y).max() <= tol * max(1.0, np.abs(x).max())
+        assert a.n_robust == b.n_robust
+        assert abs(a.chi2 - b.chi2) <= tol * a.chi2
