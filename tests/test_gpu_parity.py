@@ -21,53 +21,14 @@ import pytest
 import bos
 import oracle as O
 from conftest import C1, MINI
-from helpers import gpu_lower, oracle_lower_nf, rel_err, to_oracle
+from helpers import close_state as _close_state, gpu_lower, lin_parity as _lin_parity, oracle_lower_nf, rel_err, to_oracle
 
 pytestmark = pytest.mark.gpu
-
-
-def _close_state(pa, la, pb, lb, rtol=1e-6, atol=1e-9):
-    dp = pa - pb
-    dp[:, 2] = (dp[:, 2] + np.pi) % (2 * np.pi) - np.pi
-    ok_p = np.all(np.abs(dp) <= rtol * np.abs(pb) + atol)
-    ok_l = np.all(np.abs(la - lb) <= rtol * np.abs(lb) + atol)
-    return ok_p and ok_l, float(np.abs(dp).max()), float(np.abs(la - lb).max() if len(lb) else 0.0)
 
 
 @pytest.fixture(scope="module")
 def c1():
     return bos.load_g2o(C1)
-
-
-def _lin_parity(P, precision=bos.BOS_FP64, kt=1.0, damping=0.01, tol=1e-12, p999=None, btol=None):
-    Q = to_oracle(P)
-    S = bos.Solver(P, precision=precision, kernel_threshold=kt, damping=damping)
-    st = S.linearize()
-    rows, cols, vals, b = S.export_system()
-    lin = O.linearize(Q, kernel_threshold=kt, damping=damping, precision=32 if precision == bos.BOS_FP32 else 64)
-    Hg = gpu_lower(rows, cols, vals, P.N)
-    Ho = oracle_lower_nf(Q, lin)
-    eh = rel_err(Hg, Ho)
-    # b of the fixed pose is discarded by the reference (solver.cpp:73) and not produced here
-    keep = np.ones(P.N, dtype=bool)
-    keep[3 * P.fixed:3 * P.fixed + 3] = False
-    assert np.all(b[~keep] == 0.0)
-    eb = np.abs(b - lin.b)[keep].max() / max(np.abs(lin.b[keep]).max(), 1e-300)
-    assert eh <= tol, f"H rel err {eh}"
-    assert eb <= (10 * tol if btol is None else btol), f"b rel err {eb}"
-    if p999 is not None:
-        # scale-invariant per-entry error |dH_ij| / sqrt(H_ii H_jj) (bounded by 1 for SPD H)
-        d = (Hg - Ho).tocoo()
-        dg = np.abs(Ho.diagonal())
-        per = np.abs(d.data) / np.sqrt(np.maximum(dg[d.row] * dg[d.col], 1e-300))
-        assert np.quantile(per, 0.999) <= p999, np.quantile(per, 0.999)
-    if precision == bos.BOS_FP64:
-        assert abs(st["chi2"] - lin.chi2) <= 1e-9 * max(lin.chi2, 1.0)
-        assert st["n_robust"] == lin.n_robust
-    else:
-        assert abs(st["chi2"] - lin.chi2) <= 1e-3 * max(lin.chi2, 1.0)
-    S.close()
-    return eh, eb
 
 
 def test_linearize_c1_fp64(c1):
