@@ -110,6 +110,7 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--gn-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gn-other", action="store_true", help="skip timing the other solver ordering")
     ap.add_argument("--solver", choices=["supernodal", "schur"], default="schur",
                     help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
                          "nested-dissection multifrontal; the other one is timed too (gn_other)")
@@ -199,7 +200,7 @@ def main():
     gn_it_s, phase, gn_other = None, None, None
     if args.gn_steps > 0:
         gn_it_s, phase = time_gn(S)
-        if world == 1:   # the other multifrontal ordering on the same problem, for comparison
+        if world == 1 and not args.no_gn_other:   # the other multifrontal ordering, for comparison
             other = "supernodal" if args.solver == "schur" else "schur"
             S2 = bos.Solver(P, precision=precision, device=local_rank, stream=stream.cuda_stream,
                             solver=bos.BOS_SOLVER_SUPERNODAL if other == "supernodal" else bos.BOS_SOLVER_SCHUR)

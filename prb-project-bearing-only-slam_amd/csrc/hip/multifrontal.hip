@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstdint>
+#include <cstdio>
 #include <string>
 #include <vector>
 
@@ -103,6 +104,9 @@ struct MfArgs {
     const int32_t* fold_cptr;
     const int32_t* fold_chunk;
     const int32_t* fold_rec;
+    unsigned long long* stamps;  // timing diagnostics only (BOS_MF_STAMPS): 8 per supernode, null otherwise
+    int diag_skip;               // timing diagnostics only (BOS_MF_DIAG_SKIP): 1 assembly, 2 fold, 4 extend-add,
+                                 // 8 factor loop, 16 panel writes (results are then wrong)
 };
 
 // LDS of one wave's folded rows: L[t, 0..1] of the landmark, the row's u entry, its position p in
@@ -271,6 +275,20 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+__device__ __forceinline__ void mf_stamp(const MfArgs& a, int s, int k, int lane) {
+    if (a.stamps && lane == 0) a.stamps[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// 1 / sqrt(d) for d > 0 in the normal range: hardware estimate refined by two Newton steps
+// (quadratic convergence: full double precision, within an ulp or two of 1.0 / sqrt(d)).
+__device__ __forceinline__ double rsqrt_nr(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
 // Folded landmark children (Schur ordering) of front s, eliminated by its wave: per chunk (whole
 // children, <= 64 rows) lane q takes row t of landmark c (one 32-byte record: sources of its two
 // entries, of the landmark's 2 x 2 block, the landmark's col0 / r / L offset and the row's position
@@ -283,35 +301,59 @@ __device__ __forceinline__ int4 fold_rec_load(const MfArgs& a, int q, int half) 
     return reinterpret_cast<const int4*>(a.fold_rec + (int64_t)kFoldRec * q)[half];
 }
 
+// The values one chunk's rows need (H entries of the row and of its landmark's 2 x 2 block, the
+// landmark's right-hand side), gathered for chunk c + 1 while chunk c is processed.
+struct FoldVals {
+    double ht0, ht1, a00, a10, a11, x0, x1;
+};
+
+__device__ __forceinline__ FoldVals fold_vals(const MfArgs& a, const int4& r0, const int4& r1, bool mine) {
+    FoldVals v;
+    v.ht0 = r0.x >= 0 ? a.A[r0.x] : 0.0;
+    v.ht1 = r0.y >= 0 ? a.A[r0.y] : 0.0;
+    v.a00 = r0.z >= 0 ? a.A[r0.z] : 0.0;
+    v.a10 = r0.w >= 0 ? a.A[r0.w] : 0.0;
+    v.a11 = r1.x >= 0 ? a.A[r1.x] : 0.0;
+    v.x0 = mine ? a.x[r1.y] : 0.0;
+    v.x1 = mine ? a.x[r1.y + 1] : 0.0;
+    return v;
+}
+
 __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F, double* wv, FoldBuf* fb, int m,
                                               int lane) {
     const int ch0 = a.fold_cptr[s], ch1 = a.fold_cptr[s + 1];
-    int q0 = a.fold_chunk[ch0], n = a.fold_chunk[ch0 + 1] - q0;
+    int n = a.fold_chunk[ch0 + 1] - a.fold_chunk[ch0];
     int4 r0 = make_int4(-1, -1, -1, -1), r1 = make_int4(0, 0, 0, 0);
-    if (lane < n) { r0 = fold_rec_load(a, q0 + lane, 0); r1 = fold_rec_load(a, q0 + lane, 1); }
+    if (lane < n) { r0 = fold_rec_load(a, a.fold_chunk[ch0] + lane, 0); r1 = fold_rec_load(a, a.fold_chunk[ch0] + lane, 1); }
+    FoldVals v = fold_vals(a, r0, r1, lane < n);
+    // next chunk's records, then (inside the loop) its values, both one chunk ahead
+    int nn = ch0 + 1 < ch1 ? a.fold_chunk[ch0 + 2] - a.fold_chunk[ch0 + 1] : 0;
+    int4 n0 = make_int4(-1, -1, -1, -1), n1 = make_int4(0, 0, 0, 0);
+    if (lane < nn) { n0 = fold_rec_load(a, a.fold_chunk[ch0 + 1] + lane, 0); n1 = fold_rec_load(a, a.fold_chunk[ch0 + 1] + lane, 1); }
+    unsigned long long t_rows = 0, t_ext = 0;   // diagnostics (stamps 6, 7): per-row phase, extend-add phase
     for (int ch = ch0; ch < ch1; ++ch) {
-        // this chunk's values, then the next chunk's records (in flight during this chunk's work)
-        const double ht0 = r0.x >= 0 ? a.A[r0.x] : 0.0, ht1 = r0.y >= 0 ? a.A[r0.y] : 0.0;
-        const double a00 = r0.z >= 0 ? a.A[r0.z] : 0.0, a10 = r0.w >= 0 ? a.A[r0.w] : 0.0;
-        const double a11 = r1.x >= 0 ? a.A[r1.x] : 0.0;
-        const int col0 = r1.y, t = r1.z & 63, rc = (r1.z >> 6) & 63, pos = r1.z >> 12;
+        const unsigned long long tc0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+        const double ht0 = v.ht0, ht1 = v.ht1, a00 = v.a00, a10 = v.a10, a11 = v.a11;
+        const int t = r1.z & 63, rc = (r1.z >> 6) & 63, pos = r1.z >> 12;
         const bool mine = lane < n;
-        const double x0 = mine ? a.x[col0] : 0.0, x1 = mine ? a.x[col0 + 1] : 0.0;
+        const double x0 = v.x0, x1 = v.x1;
+        const int col0 = r1.y;
         const int64_t loff = r1.w;
-        const int nn = ch + 1 < ch1 ? a.fold_chunk[ch + 2] - a.fold_chunk[ch + 1] : 0;
-        if (lane < nn) {
-            r0 = fold_rec_load(a, a.fold_chunk[ch + 1] + lane, 0);
-            r1 = fold_rec_load(a, a.fold_chunk[ch + 1] + lane, 1);
-        }
+        // chunk ch + 1: values now (its records arrived during chunk ch - 1), records of ch + 2
+        v = fold_vals(a, n0, n1, lane < nn);
+        r0 = n0;
+        r1 = n1;
+        const int n2 = ch + 2 < ch1 ? a.fold_chunk[ch + 3] - a.fold_chunk[ch + 2] : 0;
+        if (lane < n2) { n0 = fold_rec_load(a, a.fold_chunk[ch + 2] + lane, 0); n1 = fold_rec_load(a, a.fold_chunk[ch + 2] + lane, 1); }
         if (mine) {
             double d0 = a00;
             int bad = 0;
             if (!(d0 > 0.0)) { d0 = 1e-300; ++bad; }
-            const double l00 = sqrt(d0), i0 = 1.0 / l00;
+            const double i0 = rsqrt_nr(d0), l00 = d0 * i0;
             const double l10 = a10 * i0;
             double d1 = a11 - l10 * l10;
             if (!(d1 > 0.0)) { d1 = 1e-300; ++bad; }
-            const double l11 = sqrt(d1), i1 = 1.0 / l11;
+            const double i1 = rsqrt_nr(d1), l11 = d1 * i1;
             const double lt0 = ht0 * i0, lt1 = (ht1 - lt0 * l10) * i1;
             const double y0 = x0 * i0, y1 = (x1 - l10 * y0) * i1;
             const int mc = 2 + rc;
@@ -332,6 +374,7 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F,
             fb->rc[lane] = rc;
         }
         wave_sync();
+        const unsigned long long tc1 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
         // one landmark at a time: its packed r x r pairs across lanes, (row, column) in closed form
         for (int c0 = 0; c0 < n;) {
             const int rcc = fb->rc[c0];
@@ -351,9 +394,65 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F,
             wave_sync();
             c0 += rcc;
         }
-        q0 = ch + 1 < ch1 ? a.fold_chunk[ch + 1] : 0;
         n = nn;
+        nn = n2;
+        if (a.stamps) {
+            const unsigned long long tc2 = __builtin_amdgcn_s_memrealtime();
+            t_rows += tc1 - tc0;
+            t_ext += tc2 - tc1;
+        }
     }
+    if (a.stamps && lane == 0) { a.stamps[8 * (int64_t)s + 6] = t_rows; a.stamps[8 * (int64_t)s + 7] = t_ext; }
+}
+
+// A child's extend-add inputs: its row map entry and u-vector entry for this lane (lane < rc), the
+// first 256 entries of its packed update matrix (4 per lane), and where the rest starts.
+struct ChildPre {
+    int rc, smap_v;
+    double uval;
+    double v[4];
+    const double* Uc;
+};
+
+template <bool COH>
+__device__ __forceinline__ void child_prefetch(const MfArgs& a, int c, int lane, ChildPre& p) {
+    const int rc = a.r[c];   // rc < m <= MAXM
+    p.rc = rc;
+    p.smap_v = lane < rc ? a.rmap[a.rmap_off[c] + lane] : 0;
+    p.uval = lane < rc ? ldc<COH>(a.u + a.u_off[c] + lane) : 0.0;
+    p.Uc = a.U + a.U_off[c];
+    const int ne = rc * (rc + 1) / 2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p.v[u] = 64 * u + lane < ne ? ldc<COH>(p.Uc + 64 * u + lane) : 0.0;
+}
+
+// Extend-add of one child: its row map staged in LDS, its packed update matrix swept by all lanes
+// ((row, column) decoded incrementally). Positions of one child are distinct.
+template <bool COH>
+__device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p, double* F, double* wv, int* smap,
+                                             int m, int lane) {
+    const int rc = p.rc;
+    if (lane < rc) smap[lane] = p.smap_v;
+    wave_sync();
+    const int ne = rc * (rc + 1) / 2;
+    int j = 0, len = rc, o = lane;
+    while (len > 0 && o >= len) { o -= len; ++j; --len; }
+    for (int e0 = 0; e0 < ne; e0 += 256) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            v[u] = e0 == 0 ? p.v[u] : (e0 + 64 * u + lane < ne ? ldc<COH>(p.Uc + e0 + 64 * u + lane) : 0.0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (len > 0) {
+                F[pk32(smap[j + o], smap[j], m)] += v[u];
+                o += 64;
+                while (len > 0 && o >= len) { o -= len; ++j; --len; }
+            }
+        }
+    }
+    if (lane < rc) wv[smap[lane]] += p.uval;
+    wave_sync();
 }
 
 // Factorization of one front fused with its forward elimination: w (LDS, m doubles) receives the
@@ -364,46 +463,36 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F,
 template <int MAXM, bool COH>
 __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf, int* smap,
                                                  double* wv, FoldBuf* fb, int lane) {
+    mf_stamp(a, s, 0, lane);
     const int k = a.k[s], r = a.r[s], m = k + r;
     const int nfold = a.fold_cnt[s];
     const int c0 = a.col0[s];
     const int np = m * (m + 1) / 2;
     const double xo = lane < k ? a.x[c0 + lane] : 0.0;   // right-hand side of the own dofs (k < 64)
+    // The first two (non-folded) children's row maps, u-vectors and first 256 update-matrix
+    // entries are loaded up front, in flight during the assembly and the fold (a child's data
+    // was published before this front started: the flow kernel waited for its flag).
+    const int cb = (a.diag_skip & 4) ? a.child_ptr[s + 1] : a.child_ptr[s] + nfold, ce = a.child_ptr[s + 1];
+    ChildPre p0, p1;
+    if (cb < ce) child_prefetch<COH>(a, a.child[cb], lane, p0);
+    if (cb + 1 < ce) child_prefetch<COH>(a, a.child[cb + 1], lane, p1);
     for (int e = lane; e < np; e += 64) F[e] = 0.0;
     for (int i = lane; i < m; i += 64) wv[i] = 0.0;    // children's u-vectors accumulate here
     wave_sync();
-    assemble_wave(a, s, F, lane);
+    if (!(a.diag_skip & 1)) assemble_wave(a, s, F, lane);
     wave_sync();
-    if (nfold > 0) fold_children(a, s, F, wv, fb, m, lane);
-    // extend-add: the child's row map staged in LDS, its packed update matrix swept by all lanes
-    // (contiguous loads, 4 in flight; (row, column) decoded incrementally). Positions of one
-    // child are distinct.
-    for (int ci = a.child_ptr[s] + nfold; ci < a.child_ptr[s + 1]; ++ci) {
-        const int c = a.child[ci];
-        const int rc = a.r[c];   // rc < m <= MAXM
-        if (lane < rc) smap[lane] = a.rmap[a.rmap_off[c] + lane];
-        const double* Uc = a.U + a.U_off[c];
-        wave_sync();
-        const double uval = lane < rc ? ldc<COH>(a.u + a.u_off[c] + lane) : 0.0;   // the child's u-vector
-        const int ne = rc * (rc + 1) / 2;
-        int j = 0, len = rc, o = lane;
-        while (len > 0 && o >= len) { o -= len; ++j; --len; }
-        for (int e0 = 0; e0 < ne; e0 += 256) {
-            double v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = e0 + 64 * u + lane < ne ? ldc<COH>(Uc + e0 + 64 * u + lane) : 0.0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (len > 0) {
-                    F[pk32(smap[j + o], smap[j], m)] += v[u];
-                    o += 64;
-                    while (len > 0 && o >= len) { o -= len; ++j; --len; }
-                }
-            }
-        }
-        if (lane < rc) wv[smap[lane]] += uval;
-        wave_sync();
+    mf_stamp(a, s, 1, lane);
+    if (nfold > 0 && !(a.diag_skip & 2)) fold_children(a, s, F, wv, fb, m, lane);
+    mf_stamp(a, s, 2, lane);
+    // extend-add, children in list order (deterministic)
+    if (cb < ce) extend_child<COH>(a, p0, F, wv, smap, m, lane);
+    if (cb + 1 < ce) extend_child<COH>(a, p1, F, wv, smap, m, lane);
+    for (int ci = cb + 2; ci < ce; ++ci) {
+        ChildPre pq;
+        child_prefetch<COH>(a, a.child[ci], lane, pq);
+        extend_child<COH>(a, pq, F, wv, smap, m, lane);
     }
+    mf_stamp(a, s, 3, lane);
     const bool live = lane < m;
     double row[MAXM];
     double myinv = 0.0;
@@ -412,31 +501,45 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     // Right-looking: step j broadcasts column j through a double-buffered LDS column (one store
     // per lane, same-address reads). Entries above the diagonal (c > lane) and rows >= m are
     // scratch, so the updates need no predicates.
+    const int kf = (a.diag_skip & 8) ? 0 : k;
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
-        if (j < k) {
+        if (j < kf) {
             double* col = colbuf + (j & 1) * MAXM;
             if (lane < MAXM) col[lane] = row[j];
+            // the pivot straight from lane j's register (no LDS round trip on the critical path; the
+            // column's LDS broadcast lands meanwhile), 1 / sqrt(d) by v_rsq_f64 + two Newton steps
+            double d = readlane_d(row[j], j);
             wave_sync();
-            double d = col[j];
             if (!(d > 0.0)) {
                 if (lane == 0) atomicAdd(a.info, 1);
                 d = 1e-300;
             }
-            const double ljj = sqrt(d), inv = 1.0 / ljj;
+            const double inv = rsqrt_nr(d), ljj = d * inv;
             const double lij = lane == j ? ljj : row[j] * inv;   // L[i, j]
             row[j] = lij;
             if (lane == j) myinv = inv;                          // 1 / L_jj, kept by the pivot lane
             const double g = lij * inv;                          // L[i, j] / L[j, j]
+            // columns l < m only (m is wave-uniform: whole groups of 8 are skipped by a scalar branch)
+            // (loops with compile-time trip counts only, so row[] stays in registers)
 #pragma unroll
-            for (int l = j + 1; l < MAXM; ++l) row[l] = fma(-g, col[l], row[l]);   // -= L[i,j] L[l,j]
+            for (int l0 = 0; l0 < MAXM; l0 += 8) {
+                if (l0 + 8 > j + 1 && l0 < m) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int l = l0 + u;
+                        if (l > j && l < MAXM) row[l] = fma(-g, col[l], row[l]);   // -= L[i,j] L[l,j]
+                    }
+                }
+            }
         }
     }
+    mf_stamp(a, s, 4, lane);
     double* Ls = a.L + a.L_off[s];
     double* Us = a.U + a.U_off[s];
 #pragma unroll
     for (int c = 0; c < MAXM; ++c) {
-        if (live && c <= lane) {
+        if (live && c <= lane && !(a.diag_skip & 16)) {
             if (c < k) Ls[lane + (int64_t)c * m] = row[c];
             else stc<COH>(Us + pk(lane - k, c - k, r), row[c]);
         }
@@ -456,6 +559,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         else stc<COH>(a.u + a.u_off[s] + (lane - k), wi);
     }
     wave_sync();
+    mf_stamp(a, s, 5, lane);
 }
 
 template <int MAXM>
@@ -657,6 +761,10 @@ struct MfDevice {
     int64_t *L_off = nullptr, *U_off = nullptr, *u_off = nullptr, *scratch_off = nullptr, *rmap_off = nullptr,
             *findex_off = nullptr;
     double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
+    // timing diagnostics (BOS_MF_STAMPS=<file>): per-supernode phase stamps, dumped at destroy
+    unsigned long long* stamps = nullptr;
+    std::string stamp_path;
+    std::vector<int32_t> h_meta;   // per supernode: level (-1 folded), k, r, nfold
 
     // classes [c0, c1) of level lev are contiguous in the list
     int count(int lev, int c0, int c1) const { return ptr[lev * kClasses + c1] - ptr[lev * kClasses + c0]; }
@@ -675,6 +783,9 @@ struct MfDevice {
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
         g.findex = findex; g.A = A; g.L = L; g.U = U; g.u = u; g.scratch = scratch; g.x = x; g.info = info;
         g.fold_cnt = fold_cnt; g.fold_cptr = fold_cptr; g.fold_chunk = fold_chunk; g.fold_rec = fold_rec;
+        static const int skip = [] { const char* e = std::getenv("BOS_MF_DIAG_SKIP"); return e ? std::atoi(e) : 0; }();
+        g.diag_skip = skip;
+        g.stamps = stamps;
         return g;
     }
 };
@@ -683,6 +794,22 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
     MfDevice* d = new MfDevice();
     *out = d;
     d->nlevels = F.nlevels;
+    if (const char* sp = std::getenv("BOS_MF_STAMPS")) {
+        d->stamp_path = sp;
+        if (hipMalloc((void**)&d->stamps, 8 * (size_t)std::max(1, F.nsuper) * sizeof(unsigned long long)) != hipSuccess ||
+            hipMemset(d->stamps, 0, 8 * (size_t)std::max(1, F.nsuper) * sizeof(unsigned long long)) != hipSuccess) {
+            err = "hipMalloc failed (stamps)";
+            return -2;
+        }
+        d->h_meta.assign(4 * (size_t)F.nsuper, -1);
+        for (int l = 0; l < F.nlevels; ++l)
+            for (int i = F.level_ptr[l]; i < F.level_ptr[l + 1]; ++i) d->h_meta[4 * (size_t)F.level[i]] = l;
+        for (int s2 = 0; s2 < F.nsuper; ++s2) {
+            d->h_meta[4 * (size_t)s2 + 1] = F.k[s2];
+            d->h_meta[4 * (size_t)s2 + 2] = F.r[s2];
+            d->h_meta[4 * (size_t)s2 + 3] = F.fold_cnt.empty() ? 0 : F.fold_cnt[s2];
+        }
+    }
     std::vector<int64_t> scr(F.nsuper, -1);
     int64_t scratch_size = 0;
     for (int s = 0; s < F.nsuper; ++s) {
@@ -784,6 +911,21 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
 
 void mf_destroy(MfDevice* d) {
     if (!d) return;
+    if (d->stamps && !d->stamp_path.empty()) {   // diagnostics: [nsuper] then per supernode meta[4] + stamps[8]
+        const size_t ns = d->h_meta.size() / 4;
+        std::vector<unsigned long long> st(8 * ns);
+        if (hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(st.data(), d->stamps, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
+            if (FILE* f = std::fopen(d->stamp_path.c_str(), "wb")) {
+                const int64_t n = (int64_t)ns;
+                std::fwrite(&n, sizeof(n), 1, f);
+                std::fwrite(d->h_meta.data(), sizeof(int32_t), d->h_meta.size(), f);
+                std::fwrite(st.data(), sizeof(unsigned long long), st.size(), f);
+                std::fclose(f);
+            }
+        }
+        (void)hipFree(d->stamps);
+    }
     void* bufs[] = {d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->fold_list, d->order_factor, d->order_bwd, d->slev, d->parent, d->done, d->tickets, d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
