@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--gn-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gn-other", action="store_true", help="skip timing the other solver ordering")
+    ap.add_argument("--tri-steps", type=int, default=20, help="device triangulations timed (0: skip)")
     ap.add_argument("--solver", choices=["supernodal", "schur"], default="schur",
                     help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
                          "nested-dissection multifrontal; the other one is timed too (gn_other)")
@@ -208,6 +209,31 @@ def main():
             gn_other = {"solver": other, "gn_iters_per_s": it2, "t_solve_ms": ph2["t_solve_ms"]}
             S2.close()
 
+    # ---- landmark triangulation on the device (slam/triangulation.cpp:65-74), config 3 (run last:
+    # it re-estimates the landmarks of S)
+    tri = None
+    if world == 1 and args.tri_steps > 0:
+        S.triangulate()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.tri_steps):
+            S.triangulate_async()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        tri_ms = e0.elapsed_time(e1) / args.tri_steps
+        tri = {"landmarks": P.NL, "bearings": int(len(P.b_z)), "ms": tri_ms, "landmarks_per_s": P.NL / (tri_ms * 1e-3)}
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            pose, _ = S.get_state()
+            t0 = time.perf_counter()
+            O.triangulate(pose, P.b_pose, P.b_lm, P.b_z)
+            cpu_ms = (time.perf_counter() - t0) * 1e3
+            tri["cpu_baseline"] = {"ms": cpu_ms, "landmarks_per_s": P.NL / (cpu_ms * 1e-3), "cores": 1,
+                                   "kind": "port", "sample": "one triangulation of config 3 by the C++ oracle"}
+
     if rank == 0:
         algo = info["algorithmic_bytes"]
         achieved = algo / (kernel_ms * 1e-3) / 1e9
@@ -236,6 +262,7 @@ def main():
             "gn_phase_ms": phase,
             "gn_solver": args.solver,
             "gn_other": gn_other,
+            "triangulation": tri,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,

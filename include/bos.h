@@ -61,7 +61,7 @@ typedef struct bos_problem {
     int32_t num_bearings;           /* M_b                                                       */
     int32_t num_odometry;           /* M_o                                                       */
     const double* pose_xyt;         /* [NP*3] x, y, theta                                        */
-    const double* landmark_xy;      /* [NL*2]                                                    */
+    const double* landmark_xy;      /* [NL*2], or NULL: triangulated on the device (bos_triangulate) */
     const int32_t* bearing_pose;    /* [M_b] pose stix                                           */
     const int32_t* bearing_landmark;/* [M_b] landmark stix                                       */
     const double* bearing_z;        /* [M_b] bearing, already smallestAngle-wrapped              */
@@ -137,6 +137,13 @@ int bos_linearize(struct bos_solver* s, bos_step_stats* stats);
 /* Enqueue the J+H build on the handle's stream without synchronising (benchmarking) */
 int bos_linearize_async(struct bos_solver* s);
 int bos_synchronize(struct bos_solver* s);
+/* triangulate_landmarks (slam/triangulation.cpp:65-74, per landmark triangulate_one_landmark
+ * :21-62): every landmark re-estimated on the device from the current poses and its bearings
+ * (column-pivoted least squares, the basic solution for single-observation landmarks), synchronous.
+ * bos_create does the same when bos_problem.landmark_xy is NULL (the reference triangulates before
+ * constructing the Solver, executables/bearing_only_slam.cpp). The _async form only enqueues it. */
+int bos_triangulate(struct bos_solver* s);
+int bos_triangulate_async(struct bos_solver* s);
 int bos_system_info_get(const struct bos_solver* s, bos_system_info* info);
 /*
  * Export the last linearization in the reference's dof order (poses 3*stix, landmarks

@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = [
     "bos_dataset_load_g2o", "bos_dataset_synthetic", "bos_dataset_problem", "bos_dataset_pose_ids",
     "bos_dataset_landmark_ids", "bos_dataset_fixed_pose_id", "bos_dataset_bound", "bos_dataset_ground_truth",
     "bos_dataset_write_g2o", "bos_dataset_free", "bos_plan_inspect", "bos_plan_mf_selftest",
-    "bos_debug_linearize_timeline",
+    "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -118,6 +118,8 @@ def lib():
         "bos_linearize": (ctypes.c_int, [vp, ctypes.POINTER(bos_step_stats)]),
         "bos_linearize_async": (ctypes.c_int, [vp]),
         "bos_synchronize": (ctypes.c_int, [vp]),
+        "bos_triangulate": (ctypes.c_int, [vp]),
+        "bos_triangulate_async": (ctypes.c_int, [vp]),
         "bos_debug_linearize_timeline": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64),
                                                         ctypes.POINTER(ctypes.c_int64)]),
         "bos_system_info_get": (ctypes.c_int, [vp, ctypes.POINTER(bos_system_info)]),
@@ -328,7 +330,9 @@ class Solver:
 
     def __init__(self, P: Problem, precision: int = BOS_FP64, solver: int = BOS_SOLVER_SPARSE_CHOL,
                  device: int = -1, kernel_threshold: float = 1.0, damping: float = 0.01, stream: int = 0,
-                 rank: int = 0, world_size: int = 1, nccl_id: Optional[bytes] = None):
+                 rank: int = 0, world_size: int = 1, nccl_id: Optional[bytes] = None, triangulate: bool = False):
+        """triangulate=True: ignore P.lm_xy and triangulate the landmarks on the device from the
+        initial poses (bos_problem.landmark_xy = NULL)."""
         L = lib()
         self.P = P
         opt = bos_options()
@@ -343,6 +347,8 @@ class Solver:
             opt.nccl_unique_id = ctypes.cast(self._nid, ctypes.c_void_p)
         self._h = ctypes.c_void_p()
         cs = P.c_struct()
+        if triangulate:
+            cs.landmark_xy = None
         _check(L.bos_create(ctypes.byref(cs), ctypes.byref(opt), ctypes.byref(self._h)), "bos_create")
         self.last_stats = None
 
@@ -392,6 +398,13 @@ class Solver:
         _check(lib().bos_debug_linearize_timeline(self._h, n.value, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                                                   ctypes.byref(n)), "timeline")
         return out
+
+    def triangulate(self):
+        """triangulate_landmarks on the device from the current poses (slam/triangulation.cpp:65-74)."""
+        _check(lib().bos_triangulate(self._h), "bos_triangulate")
+
+    def triangulate_async(self):
+        _check(lib().bos_triangulate_async(self._h), "bos_triangulate_async")
 
     def synchronize(self):
         _check(lib().bos_synchronize(self._h), "bos_synchronize")

@@ -473,6 +473,86 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
     }
 }
 
+// triangulate_one_landmark (slam/triangulation.cpp:21-62): the rows [sin(th + z), -cos(th + z)],
+// rhs sin(th + z) px - cos(th + z) py, solved by the reference with Eigen's column-pivoted
+// Householder QR; here (as in the host build, host/triangulation.cpp) by column-pivoted modified
+// Gram-Schmidt with one re-orthogonalisation and Eigen's nonzeroPivots() rank rule, so a rank-1
+// system (one observation) gets the basic solution. The same operation sequence as the host code,
+// without FP contraction; the rows are computed once and kept in scratch for the later passes.
+template <typename T> __global__ __launch_bounds__(256) void triangulate_kernel(const TriParams<T> P) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= P.NL) return;
+    const int x0 = P.lm_ptr[l], x1 = P.lm_ptr[l + 1], M = x1 - x0;
+    double n0 = 0.0, n1 = 0.0;
+    for (int x = x0; x < x1; ++x) {
+        const int k = P.lm_obs[x];
+        const double* p = P.pose + 3 * (int64_t)P.b_pose[k];
+        const double ang = p[2] + P.b_z[k];
+        const double sn = sin(ang), cs = cos(ang);
+        const double a0 = sn, a1 = -cs, r = sn * p[0] - cs * p[1];
+        double* w = P.scratch + 3 * (int64_t)x;
+        w[0] = a0; w[1] = a1; w[2] = r;
+        n0 += a0 * a0;
+        n1 += a1 * a1;
+    }
+    double ox = 0.0, oy = 0.0;
+    const bool swap = n1 > n0;                     // pivot: the first column of maximal norm
+    const double r00 = sqrt(fmax(n0, n1));
+    if (M > 0 && r00 != 0.0) {
+        auto c0 = [&](const double* w) { return swap ? w[1] : w[0]; };
+        auto c1 = [&](const double* w) { return swap ? w[0] : w[1]; };
+        double qb0 = 0.0;
+        for (int x = x0; x < x1; ++x) { const double* w = P.scratch + 3 * (int64_t)x; qb0 += (c0(w) / r00) * w[2]; }
+        double x_piv, x_oth = 0.0;
+        bool rank2 = false;
+        double r01 = 0.0, r11 = 0.0, qb1 = 0.0;
+        if (M >= 2) {
+            // two MGS passes: d1 = q0 . c1, c1' = c1 - d1 q0; d2 = q0 . c1', c1'' = c1' - d2 q0
+            double d1 = 0.0, d2 = 0.0;
+            for (int x = x0; x < x1; ++x) { const double* w = P.scratch + 3 * (int64_t)x; d1 += (c0(w) / r00) * c1(w); }
+            for (int x = x0; x < x1; ++x) {
+                const double* w = P.scratch + 3 * (int64_t)x;
+                const double q = c0(w) / r00;
+                d2 += q * (c1(w) - d1 * q);
+            }
+            r01 = d1 + d2;
+            double rem = 0.0;
+            for (int x = x0; x < x1; ++x) {
+                const double* w = P.scratch + 3 * (int64_t)x;
+                const double q = c0(w) / r00;
+                const double v = (c1(w) - d1 * q) - d2 * q;
+                rem += v * v;
+            }
+            const double eps = 2.220446049250313e-16;
+            const double thr = (r00 * eps) * (r00 * eps) / (double)M * (double)(M - 1);
+            if (!(rem < thr)) {
+                rank2 = true;
+                r11 = sqrt(rem);
+                for (int x = x0; x < x1; ++x) {
+                    const double* w = P.scratch + 3 * (int64_t)x;
+                    const double q = c0(w) / r00;
+                    qb1 += (((c1(w) - d1 * q) - d2 * q) / r11) * w[2];
+                }
+            }
+        }
+        if (rank2) {
+            x_oth = qb1 / r11;
+            x_piv = (qb0 - r01 * x_oth) / r00;
+        } else {
+            x_piv = qb0 / r00;
+        }
+        ox = swap ? x_oth : x_piv;
+        oy = swap ? x_piv : x_oth;
+    }
+    P.lm[2 * (int64_t)l] = ox;
+    P.lm[2 * (int64_t)l + 1] = oy;
+    P.lc[2 * (int64_t)l] = (T)ox;
+    P.lc[2 * (int64_t)l + 1] = (T)oy;
+}
+
 template <typename T> __global__ void to_f64_kernel(const T* in, double* out, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = (double)in[i];
@@ -540,6 +620,12 @@ template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStr
     return hipGetLastError();
 }
 
+template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s) {
+    if (p.NL == 0) return hipSuccess;
+    hipLaunchKernelGGL((triangulate_kernel<T>), dim3((p.NL + 255) / 256), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, const double* max_part,
                                int n_max, int32_t* info, int32_t* reset, int n_reset, StepStatus* out, hipStream_t s) {
     if (n_reset > 256) return hipErrorInvalidValue;
@@ -574,6 +660,8 @@ template hipError_t launch_linearize<double>(const LinParams<double>&, int, bool
 template hipError_t launch_linearize<float>(const LinParams<float>&, int, bool, bool, hipStream_t);
 template hipError_t launch_boxplus<double>(const UpdateParams<double>&, hipStream_t);
 template hipError_t launch_boxplus<float>(const UpdateParams<float>&, hipStream_t);
+template hipError_t launch_triangulate<double>(const TriParams<double>&, hipStream_t);
+template hipError_t launch_triangulate<float>(const TriParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);
 template hipError_t launch_gather_f64<double>(const double*, const int32_t*, double*, int64_t, hipStream_t);

@@ -87,9 +87,24 @@ struct StepStatus {
 
 constexpr int kUpdateBlock = 256;
 
+// Landmark triangulation (slam/triangulation.cpp:21-74) on the device: one lane per landmark over its
+// bearings (CSR in file order, as the reference groups them by landmark id).
+template <typename T> struct TriParams {
+    int NL;
+    const int32_t* lm_ptr;    // [NL + 1]
+    const int32_t* lm_obs;    // [M_b] bearing indices grouped by landmark
+    const int32_t* b_pose;    // [M_b]
+    const double* b_z;        // [M_b]
+    const double* pose;       // [NP][3] master state
+    double* scratch;          // [M_b][3] the least-squares rows (a0, a1, r) in CSR order
+    double* lm;               // [NL][2] out: master state
+    T* lc;                    // [NL][2] out: T-precision cache
+};
+
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s);
+template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
 // Reduces the J+H kernel's chi^2 / robust-count partials (and the box-plus max |dx| partials when
 // max_part is set) into *out, moves *info into out->info, then zeroes *info and reset[0, n_reset)
 // (the solver's work-queue tickets) for the next iteration: one launch replaces the per-step

@@ -104,6 +104,9 @@ struct bos_solver {
     double* d_chi_part = nullptr;
     int32_t* d_nrob_part = nullptr;
     bos::dev::StepStatus* d_status = nullptr;   // end-of-iteration summary (one read-back)
+    // triangulation inputs: bearings grouped by landmark (file order), their pose and z (fp64)
+    int32_t *tri_ptr = nullptr, *tri_obs = nullptr, *tri_pose = nullptr;
+    double *tri_z = nullptr, *tri_scr = nullptr;
     double* d_maxpart = nullptr;                 // box-plus max |dx| per update block
     rocblas_handle rb = nullptr;
     rocsolver_rfinfo rf = nullptr;
@@ -306,6 +309,21 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
+template <typename T> bos::dev::TriParams<T> tri_params(const bos_solver* s) {
+    bos::dev::TriParams<T> p;
+    p.NL = s->NL;
+    p.lm_ptr = s->tri_ptr; p.lm_obs = s->tri_obs; p.b_pose = s->tri_pose; p.b_z = s->tri_z;
+    p.pose = s->d_pose; p.scratch = s->tri_scr; p.lm = s->d_lm; p.lc = (T*)s->d_lc;
+    return p;
+}
+
+int enqueue_triangulate(bos_solver* s) {
+    const hipError_t e = s->precision == BOS_FP32 ? bos::dev::launch_triangulate<float>(tri_params<float>(s), s->stream)
+                                                  : bos::dev::launch_triangulate<double>(tri_params<double>(s), s->stream);
+    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("triangulate launch: ") + hipGetErrorString(e));
+    return BOS_OK;
+}
+
 int read_stats(bos_solver* s, bos_step_stats* st) {
     bos::dev::StepStatus h;
     HIP_TRY(hipMemcpyAsync(&h, s->d_status, sizeof(h), hipMemcpyDeviceToHost, s->stream));
@@ -386,7 +404,7 @@ int bos_destroy(bos_solver* s) {
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_status,
-                    s->d_maxpart};
+                    s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (s->rf) rocsolver_destroy_rfinfo(s->rf);
@@ -412,7 +430,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         return fail(BOS_ERR_INVALID, "unknown solver");
     if (pb->num_poses <= 0 || pb->num_landmarks < 0 || pb->num_bearings < 0 || pb->num_odometry < 0)
         return fail(BOS_ERR_INVALID, "bad problem sizes");
-    if (!pb->pose_xyt || (pb->num_landmarks && !pb->landmark_xy) ||
+    if (!pb->pose_xyt ||
         (pb->num_bearings && (!pb->bearing_pose || !pb->bearing_landmark || !pb->bearing_z)) ||
         (pb->num_odometry && (!pb->odom_src || !pb->odom_dst || !pb->odom_z || !pb->odom_omega)))
         return fail(BOS_ERR_INVALID, "null problem array");
@@ -494,8 +512,10 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     const int NP = s->NP, NL = s->NL;
     std::vector<double> pose(pb->pose_xyt, pb->pose_xyt + 3 * (size_t)NP);
     for (int i = 0; i < NP; ++i) pose[3 * i + 2] = bos::normalized_angle<double>(bos::smallest_angle<double>(pose[3 * i + 2]));
-    std::vector<double> lm(pb->landmark_xy ? pb->landmark_xy : nullptr,
-                           pb->landmark_xy ? pb->landmark_xy + 2 * (size_t)NL : nullptr);
+    // landmark_xy == NULL: the landmarks are triangulated on the device below (the reference's
+    // triangulate_landmarks before the Solver ctor, bearing_only_slam.cpp / slam/triangulation.cpp)
+    std::vector<double> lm(2 * (size_t)NL, 0.0);
+    if (pb->landmark_xy) lm.assign(pb->landmark_xy, pb->landmark_xy + 2 * (size_t)NL);
     if ((rc = upload(&s->d_pose, pose)) || (rc = upload(&s->d_lm, lm))) return bail(rc);
     const bool f32 = s->precision == BOS_FP32;
     auto alloc_T = [&](void** p, size_t count) -> int {
@@ -606,6 +626,18 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     HIP_TRY(hipMemset(s->d_chi_part, 0, nt * sizeof(double)));
     HIP_TRY(hipMemset(s->d_nrob_part, 0, nt * sizeof(int32_t)));
     HIP_TRY(hipMemset(s->d_info, 0, sizeof(int32_t)));
+    {   // triangulation inputs (kept for bos_triangulate)
+        std::vector<int32_t> tptr(NL + 1, 0), tobs(s->Mb), tpose(pb->bearing_pose, pb->bearing_pose + s->Mb);
+        for (int k = 0; k < s->Mb; ++k) ++tptr[pb->bearing_landmark[k] + 1];
+        for (int l = 0; l < NL; ++l) tptr[l + 1] += tptr[l];
+        std::vector<int32_t> w(tptr.begin(), tptr.end() - 1);
+        for (int k = 0; k < s->Mb; ++k) tobs[w[pb->bearing_landmark[k]]++] = k;
+        std::vector<double> tz(pb->bearing_z, pb->bearing_z + s->Mb);
+        if ((rc = upload(&s->tri_ptr, tptr)) || (rc = upload(&s->tri_obs, tobs)) || (rc = upload(&s->tri_pose, tpose)) ||
+            (rc = upload(&s->tri_z, tz)) || (rc = dalloc(&s->tri_scr, 3 * (size_t)std::max(1, s->Mb))))
+            return bail(rc);
+    }
+    if (!pb->landmark_xy && NL && (rc = enqueue_triangulate(s))) return bail(rc);
     if ((rc = upload_cache(s))) return bail(rc);
     HIP_TRY(hipStreamSynchronize(s->stream));
     *out = s;
@@ -675,6 +707,21 @@ int bos_debug_linearize_timeline(bos_solver* s, int64_t capacity, uint64_t* stam
     (void)hipFree(d);
     if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("timeline: ") + hipGetErrorString(e));
     return BOS_OK;
+}
+
+int bos_triangulate(bos_solver* s) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = enqueue_triangulate(s);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->have_dx = false;
+    return BOS_OK;
+}
+
+int bos_triangulate_async(bos_solver* s) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    return enqueue_triangulate(s);
 }
 
 int bos_synchronize(bos_solver* s) {
