@@ -1,4 +1,7 @@
 // Host-side C ABI (include/bos_host.h): datasets (g2o / synthetic) and plan inspection.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -42,25 +45,54 @@ struct bos_dataset {
         for (size_t j = 0; j < L.size(); ++j) { lm_xy[2 * j] = L[j].x; lm_xy[2 * j + 1] = L[j].y; }
         pose_ids.assign(state.pose_ids().begin(), state.pose_ids().end());
         lm_ids.assign(state.landmark_ids().begin(), state.landmark_ids().end());
+        // id -> stix as flat tables when the ids are dense enough (else the State's maps); a repeated
+        // id maps to its last stix, as the State's map does (state.cpp:23)
+        auto flat = [](const std::vector<int32_t>& ids, std::vector<int32_t>& tab, int32_t& lo) {
+            tab.clear();
+            lo = 0;
+            if (ids.empty()) return false;
+            const auto mm = std::minmax_element(ids.begin(), ids.end());
+            lo = *mm.first;
+            const int64_t span = (int64_t)*mm.second - lo + 1;
+            if (span > 4 * (int64_t)ids.size() + 1024) return false;
+            tab.assign((size_t)span, -1);
+            for (size_t i = 0; i < ids.size(); ++i) tab[(size_t)(ids[i] - lo)] = (int32_t)i;
+            return true;
+        };
+        std::vector<int32_t> ptab, ltab;
+        int32_t plo = 0, llo = 0;
+        const bool pf = flat(pose_ids, ptab, plo), lf = flat(lm_ids, ltab, llo);
+        auto pstix = [&](int id) -> int32_t {
+            if (!pf) return state.pose_stix(id);
+            const int64_t q = (int64_t)id - plo;
+            if (q < 0 || q >= (int64_t)ptab.size() || ptab[(size_t)q] < 0) throw std::out_of_range("pose id");
+            return ptab[(size_t)q];
+        };
+        auto lstix = [&](int id) -> int32_t {
+            if (!lf) return state.landmark_stix(id);
+            const int64_t q = (int64_t)id - llo;
+            if (q < 0 || q >= (int64_t)ltab.size() || ltab[(size_t)q] < 0) throw std::out_of_range("landmark id");
+            return ltab[(size_t)q];
+        };
         try {
             b_pose.resize(bearings.size()); b_lm.resize(bearings.size()); b_z.resize(bearings.size());
             for (size_t k = 0; k < bearings.size(); ++k) {
-                b_pose[k] = state.pose_stix(bearings[k].get_pose_id());
-                b_lm[k] = state.landmark_stix(bearings[k].get_lm_id());
+                b_pose[k] = pstix(bearings[k].get_pose_id());
+                b_lm[k] = lstix(bearings[k].get_lm_id());
                 b_z[k] = bearings[k].get_bearing_angle();
             }
             o_src.resize(odometry.size()); o_dst.resize(odometry.size());
             o_z.resize(3 * odometry.size()); o_om.resize(9 * odometry.size());
             for (size_t k = 0; k < odometry.size(); ++k) {
-                o_src[k] = state.pose_stix(odometry[k].get_source_id());
-                o_dst[k] = state.pose_stix(odometry[k].get_dest_id());
+                o_src[k] = pstix(odometry[k].get_source_id());
+                o_dst[k] = pstix(odometry[k].get_dest_id());
                 const proj02::EPose z = odometry[k].get_transformation();
                 o_z[3 * k] = z.x; o_z[3 * k + 1] = z.y; o_z[3 * k + 2] = z.z;
                 const proj02::Mat3 m = odometry[k].get_omega();
                 for (int r = 0; r < 3; ++r)
                     for (int c = 0; c < 3; ++c) o_om[9 * k + 3 * r + c] = m(r, c);
             }
-            fixed_stix = state.pose_stix(fixed_pose_id);
+            fixed_stix = pstix(fixed_pose_id);
         } catch (const std::out_of_range&) {
             return hfail(BOS_ERR_INVALID, "an observation or FIX references an unknown id");
         }
@@ -74,13 +106,23 @@ int bos_dataset_load_g2o(const char* path, int triangulate, int verbose, bos_dat
     if (!path || !out) return hfail(BOS_ERR_INVALID, "null argument");
     *out = nullptr;
     bos_dataset* d = new bos_dataset();
+    const bool timing = std::getenv("BOS_LOAD_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = now();
     const int rc = proj02::parse_g2o(path, d->state, d->bearings, d->odometry, d->fixed_pose_id, d->bound);
+    const auto t1 = now();
     if (rc) { delete d; return hfail(BOS_ERR_IO, rc == -1 ? "cannot open g2o file" : "malformed g2o line"); }
     if (d->state.number_of_poses() == 0) { delete d; return hfail(BOS_ERR_INVALID, "no poses"); }
     if (d->fixed_pose_id < 0) d->fixed_pose_id = d->state.default_pose_id();   // bearing_only_slam.cpp:63-65
     if (triangulate) proj02::triangulate_landmarks(d->state, d->bearings, verbose != 0);
+    const auto t2 = now();
     const int r2 = d->finalize();
     if (r2) { delete d; return r2; }
+    if (timing) {
+        const auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "load_g2o: parse %.1f ms, triangulate %.1f ms, finalize %.1f ms\n", ms(t0, t1), ms(t1, t2),
+                     ms(t2, now()));
+    }
     *out = d;
     return BOS_OK;
 }

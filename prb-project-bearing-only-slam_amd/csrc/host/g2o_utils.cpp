@@ -1,11 +1,15 @@
 #include "g2o_utils.hpp"
 
+#include <algorithm>
+#include <array>
 #include <cerrno>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
+#include <thread>
 #include <vector>
 
 namespace proj02 {
@@ -46,8 +50,8 @@ struct Line {
 
 }  // namespace
 
-int parse_g2o(const std::string& fname, State& state, BearingObservationVector& bearings,
-              OdometryObservationVector& odometries, int& fixed_pose_id, float& bound) {
+int parse_g2o_simple(const std::string& fname, State& state, BearingObservationVector& bearings,
+                     OdometryObservationVector& odometries, int& fixed_pose_id, float& bound) {
     bound = 0;
     fixed_pose_id = -1;
     FILE* f = std::fopen(fname.c_str(), "r");
@@ -94,6 +98,155 @@ int parse_g2o(const std::string& fname, State& state, BearingObservationVector& 
     }
     std::fclose(f);
     if (rc) return rc;
+    bound = (float)fb + 3.0f;                                           // :124
+    if (state.number_of_poses() == 0) std::cout << "Warning: no poses found. Stuff is likely to break." << std::endl;
+    if (bearings.empty()) std::cout << "Warning: no bearing observations found. Stuff is likely to break." << std::endl;
+    return 0;
+}
+
+namespace {
+
+// ---- parallel parser: the file is read at once, cut into chunks at line starts, each chunk parsed
+// by its own thread into per-chunk vectors (std::from_chars: correctly rounded like strtod), and
+// the chunks merged in file order, so the result equals the line-by-line parser's.
+struct Tok {
+    const char* p;
+    const char* e;
+    bool next(const char*& b, const char*& t) {
+        while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) ++p;
+        if (p >= e) return false;
+        b = p;
+        while (p < e && *p != ' ' && *p != '\t' && *p != '\r') ++p;
+        t = p;
+        return true;
+    }
+    // a token parsed like strtol / strtod on it (leading '+' allowed, trailing junk ignored)
+    bool integer(int& v) {
+        const char *b, *t;
+        if (!next(b, t)) return false;
+        if (*b == '+') ++b;
+        long x = 0;
+        const auto r = std::from_chars(b, t, x);
+        if (r.ec != std::errc() || x < INT32_MIN || x > INT32_MAX) return false;
+        v = (int)x;
+        return true;
+    }
+    bool real(double& v) {
+        const char *b, *t;
+        if (!next(b, t)) return false;
+        if (*b == '+') ++b;
+        const auto r = std::from_chars(b, t, v);
+        if (r.ec == std::errc::result_out_of_range) v = std::strtod(std::string(b, t).c_str(), nullptr);   // +-inf / 0
+        return r.ec == std::errc() || r.ec == std::errc::result_out_of_range;
+    }
+};
+
+struct ChunkOut {
+    std::vector<std::pair<int, std::array<double, 3>>> poses;
+    std::vector<std::pair<int, std::array<double, 2>>> landmarks;
+    OdometryObservationVector odometries;
+    BearingObservationVector bearings;
+    std::vector<std::string> unknown;
+    int fix = -1;
+    double fb = 0;
+    bool bad = false;
+};
+
+bool tok_is(const char* b, const char* t, const char* w) {
+    const size_t n = std::strlen(w);
+    return (size_t)(t - b) == n && std::memcmp(b, w, n) == 0;
+}
+
+void parse_chunk(const char* p, const char* e, ChunkOut& o) {
+    while (p < e && !o.bad) {
+        const char* le = (const char*)std::memchr(p, '\n', (size_t)(e - p));
+        if (!le) le = e;
+        Tok ln{p, le};
+        p = le + 1;
+        const char *b, *t;
+        if (!ln.next(b, t)) continue;                                   // empty line (:113-116)
+        if (tok_is(b, t, "VERTEX_SE2")) {                               // :19-37
+            int id; double x, y, th;
+            if (!(ln.integer(id) && ln.real(x) && ln.real(y) && ln.real(th))) { o.bad = true; break; }
+            o.fb = std::max(o.fb, std::max(std::fabs(x), std::fabs(y)));
+            o.poses.push_back({id, {x, y, th}});
+        } else if (tok_is(b, t, "VERTEX_XY")) {                         // :40-56
+            int id; double x, y;
+            if (!(ln.integer(id) && ln.real(x) && ln.real(y))) { o.bad = true; break; }
+            o.fb = std::max(o.fb, std::max(std::fabs(x), std::fabs(y)));
+            o.landmarks.push_back({id, {x, y}});
+        } else if (tok_is(b, t, "FIX")) {                               // :59-65 (last one wins)
+            int id;
+            if (!ln.integer(id)) { o.bad = true; break; }
+            o.fix = id;
+        } else if (tok_is(b, t, "EDGE_SE2")) {                          // :68-98
+            int s, d; double x, y, th, u[6];
+            if (!(ln.integer(s) && ln.integer(d) && ln.real(x) && ln.real(y) && ln.real(th))) { o.bad = true; break; }
+            bool ok = true;
+            for (int k = 0; k < 6; ++k) ok = ok && ln.real(u[k]);
+            if (!ok) { o.bad = true; break; }
+            Mat3 om;
+            om(0, 0) = u[0]; om(0, 1) = u[1]; om(0, 2) = u[2];
+            om(1, 0) = u[1]; om(1, 1) = u[3]; om(1, 2) = u[4];
+            om(2, 0) = u[2]; om(2, 1) = u[4]; om(2, 2) = u[5];
+            o.odometries.emplace_back(s, d, x, y, th, om);
+        } else if (tok_is(b, t, "EDGE_BEARING_SE2_XY")) {               // :101-110, omega = 1
+            int ps, l; double z;
+            if (!(ln.integer(ps) && ln.integer(l) && ln.real(z))) { o.bad = true; break; }
+            o.bearings.emplace_back(ps, l, z);
+        } else {
+            o.unknown.emplace_back(b, t);                               // :118-120
+        }
+    }
+}
+
+}  // namespace
+
+int parse_g2o(const std::string& fname, State& state, BearingObservationVector& bearings,
+              OdometryObservationVector& odometries, int& fixed_pose_id, float& bound) {
+    if (const char* e = std::getenv("BOS_G2O_SIMPLE"))   // the line-by-line parser (tests compare the two)
+        if (std::atoi(e) == 1) return parse_g2o_simple(fname, state, bearings, odometries, fixed_pose_id, bound);
+    bound = 0;
+    fixed_pose_id = -1;
+    FILE* f = std::fopen(fname.c_str(), "rb");
+    if (!f) return -1;
+    std::vector<char> buf;
+    {
+        std::fseek(f, 0, SEEK_END);
+        const long n = std::ftell(f);
+        std::fseek(f, 0, SEEK_SET);
+        if (n < 0) { std::fclose(f); return -1; }
+        buf.resize((size_t)n);
+        if (n > 0 && std::fread(buf.data(), 1, (size_t)n, f) != (size_t)n) { std::fclose(f); return -1; }
+    }
+    std::fclose(f);
+    const char* base = buf.data();
+    const size_t n = buf.size();
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int nt = (int)std::min<size_t>(std::min(16u, hw), std::max<size_t>(1, n >> 20));   // >= 1 MiB per chunk
+    std::vector<size_t> cut(nt + 1, n);
+    cut[0] = 0;
+    for (int c = 1; c < nt; ++c) {
+        size_t q = std::max(cut[c - 1], n * c / nt);
+        while (q < n && q > 0 && base[q - 1] != '\n') ++q;   // chunks start at line starts
+        cut[c] = q;
+    }
+    std::vector<ChunkOut> out(nt);
+    std::vector<std::thread> th;
+    for (int c = 1; c < nt; ++c) th.emplace_back(parse_chunk, base + cut[c], base + cut[c + 1], std::ref(out[c]));
+    parse_chunk(base + cut[0], base + cut[1], out[0]);
+    for (std::thread& t : th) t.join();
+    double fb = 0;
+    for (const ChunkOut& o : out) {
+        if (o.bad) return -2;
+        for (const auto& q : o.poses) state.add_pose(q.second[0], q.second[1], q.second[2], q.first);
+        for (const auto& q : o.landmarks) state.add_landmark(q.second[0], q.second[1], q.first);
+        odometries.insert(odometries.end(), o.odometries.begin(), o.odometries.end());
+        bearings.insert(bearings.end(), o.bearings.begin(), o.bearings.end());
+        for (const std::string& u : o.unknown) std::cout << "Unrecognized " << u << std::endl;
+        if (o.fix >= 0) fixed_pose_id = o.fix;
+        fb = std::max(fb, o.fb);
+    }
     bound = (float)fb + 3.0f;                                           // :124
     if (state.number_of_poses() == 0) std::cout << "Warning: no poses found. Stuff is likely to break." << std::endl;
     if (bearings.empty()) std::cout << "Warning: no bearing observations found. Stuff is likely to break." << std::endl;

@@ -22,6 +22,11 @@ namespace proj02 {
 int parse_g2o(const std::string& fname, State& state, BearingObservationVector& bearings,
               OdometryObservationVector& odometries, int& fixed_pose_id, float& bound);
 
+// The line-by-line form of parse_g2o (parse_g2o reads the file at once and parses chunks in
+// parallel, merged in file order; BOS_G2O_SIMPLE=1 selects this one instead).
+int parse_g2o_simple(const std::string& fname, State& state, BearingObservationVector& bearings,
+                     OdometryObservationVector& odometries, int& fixed_pose_id, float& bound);
+
 // utils/g2o_utils.cpp:5-8 (legacy overload without odometry)
 int parse_g2o(const std::string& fname, State& state, BearingObservationVector& bearings, int& fixed_pose_id,
               float& bound);

@@ -4,6 +4,8 @@
 #include <cmath>
 #include <iostream>
 #include <limits>
+#include <thread>
+#include <vector>
 
 namespace proj02 {
 
@@ -74,9 +76,34 @@ LMPos triangulate_one_landmark(const State& state, const BearingObservationVecto
     return swap ? LMPos(x_oth, x_piv) : LMPos(x_piv, x_oth);
 }
 
+// Groups in ascending id order with the bearings of a group in file order (the std::map of
+// subdivide_bearings_by_landmark_id), solved in parallel, added to the state in id order.
 void triangulate_landmarks(State& state, const BearingObservationVector& observations, bool verbose) {
-    const BearingObservationsByLandmarkId by_lm = subdivide_bearings_by_landmark_id(observations);
-    for (const auto& kv : by_lm) state.add_landmark(triangulate_one_landmark(state, kv.second, verbose), kv.first);
+    std::vector<int32_t> order(observations.size());
+    for (size_t k = 0; k < order.size(); ++k) order[k] = (int32_t)k;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int32_t a, int32_t b) { return observations[a].get_lm_id() < observations[b].get_lm_id(); });
+    std::vector<size_t> gptr;
+    for (size_t i = 0; i < order.size(); ++i)
+        if (i == 0 || observations[order[i]].get_lm_id() != observations[order[i - 1]].get_lm_id()) gptr.push_back(i);
+    gptr.push_back(order.size());
+    const size_t ng = gptr.size() - 1;
+    std::vector<LMPos> out(ng);
+    auto solve = [&](size_t g0, size_t g1) {
+        BearingObservationVector grp;
+        for (size_t g = g0; g < g1; ++g) {
+            grp.clear();
+            for (size_t i = gptr[g]; i < gptr[g + 1]; ++i) grp.push_back(observations[order[i]]);
+            out[g] = triangulate_one_landmark(state, grp, verbose);
+        }
+    };
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = verbose ? 1 : std::min<size_t>(std::min(16u, hw), std::max<size_t>(1, ng / 4096));
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) th.emplace_back(solve, ng * t / nt, ng * (t + 1) / nt);
+    solve(0, ng / nt);
+    for (std::thread& t : th) t.join();
+    for (size_t g = 0; g < ng; ++g) state.add_landmark(out[g], observations[order[gptr[g]]].get_lm_id());
 }
 
 }  // namespace proj02

@@ -186,3 +186,26 @@ def test_plan_shards_partition_rows(world):
     keep = np.ones(P.N, dtype=bool)
     keep[3 * P.fixed:3 * P.fixed + 3] = False
     assert np.all(b_owned[keep] == 1)
+
+
+def test_parallel_g2o_parser_equals_line_parser(tmp_path, monkeypatch):
+    """The chunked parallel g2o parser (default) and the line-by-line one give identical problems,
+    on the reference dataset and on a written synthetic world large enough to use several chunks."""
+    import ctypes
+    L = bos.lib()
+    h = ctypes.c_void_p()
+    assert L.bos_dataset_synthetic(3000, 6000, 10, 7, ctypes.byref(h)) == 0
+    path = str(tmp_path / "w.g2o")
+    assert L.bos_dataset_write_g2o(h, path.encode(), None, None, 1) == 0
+    L.bos_dataset_free(h)
+    with open(path, "a") as f:   # pad past 1 MiB so the parser cuts several chunks
+        f.write("\n" * (3 << 20))
+    keys = ("pose_xyt", "lm_xy", "b_pose", "b_lm", "b_z", "o_src", "o_dst", "o_z", "o_omega", "pose_ids", "lm_ids")
+    for p in (C1, path):
+        monkeypatch.setenv("BOS_G2O_SIMPLE", "1")
+        A = bos.load_g2o(p)
+        monkeypatch.delenv("BOS_G2O_SIMPLE")
+        B = bos.load_g2o(p)
+        assert A.fixed == B.fixed
+        for k in keys:
+            assert np.array_equal(getattr(A, k), getattr(B, k)), k
