@@ -553,6 +553,17 @@ template <typename T> __global__ __launch_bounds__(256) void triangulate_kernel(
     P.lc[2 * (int64_t)l + 1] = (T)oy;
 }
 
+// one segment per blockIdx.y, its elements grid-strided over blockIdx.x
+template <typename T>
+__global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* segs) {
+    const ExSeg g = segs[blockIdx.y];
+    T* const base[4] = {val, b, send, recv};
+    const T* src = base[g.src_kind] + g.src;
+    T* dst = base[g.dst_kind] + g.dst;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < g.len; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 template <typename T> __global__ void to_f64_kernel(const T* in, double* out, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = (double)in[i];
@@ -620,6 +631,14 @@ template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStr
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s) {
+    if (nseg == 0 || max_len == 0) return hipSuccess;
+    const int64_t bx = std::min<int64_t>((max_len + 255) / 256, 256);
+    hipLaunchKernelGGL((seg_copy_kernel<T>), dim3((unsigned)bx, (unsigned)nseg), dim3(256), 0, s, val, b, send, recv, segs);
+    return hipGetLastError();
+}
+
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s) {
     if (p.NL == 0) return hipSuccess;
     hipLaunchKernelGGL((triangulate_kernel<T>), dim3((p.NL + 255) / 256), dim3(256), 0, s, p);
@@ -661,6 +680,8 @@ template hipError_t launch_linearize<float>(const LinParams<float>&, int, bool, 
 template hipError_t launch_boxplus<double>(const UpdateParams<double>&, hipStream_t);
 template hipError_t launch_boxplus<float>(const UpdateParams<float>&, hipStream_t);
 template hipError_t launch_triangulate<double>(const TriParams<double>&, hipStream_t);
+template hipError_t launch_seg_copy<double>(double*, double*, double*, double*, const ExSeg*, int, int64_t, hipStream_t);
+template hipError_t launch_seg_copy<float>(float*, float*, float*, float*, const ExSeg*, int, int64_t, hipStream_t);
 template hipError_t launch_triangulate<float>(const TriParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);

@@ -101,6 +101,17 @@ template <typename T> struct TriParams {
     T* lc;                    // [NL][2] out: T-precision cache
 };
 
+// Exchange of the sharded J+H results (hip/solver_capi.hip enqueue_exchange): copies of contiguous
+// segments between the block array (kind 0), b (1), the packed send buffer (2) and the all-gather
+// receive buffer (3).
+struct ExSeg {
+    int64_t src, dst, len;   // element offsets and count
+    int32_t src_kind, dst_kind;
+};
+
+template <typename T>
+hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s);
+
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s);

@@ -104,6 +104,11 @@ struct bos_solver {
     double* d_chi_part = nullptr;
     int32_t* d_nrob_part = nullptr;
     bos::dev::StepStatus* d_status = nullptr;   // end-of-iteration summary (one read-back)
+    // exchange (world > 1): own ranges packed into ex_send, all-gathered into ex_recv, unpacked
+    void *ex_send = nullptr, *ex_recv = nullptr;
+    bos::dev::ExSeg *ex_pack = nullptr, *ex_unpack = nullptr;
+    int ex_npack = 0, ex_nunpack = 0;
+    int64_t ex_count = 0, ex_maxlen_pack = 0, ex_maxlen_unpack = 0;
     // triangulation inputs: bearings grouped by landmark (file order), their pose and z (fp64)
     int32_t *tri_ptr = nullptr, *tri_obs = nullptr, *tri_pose = nullptr;
     double *tri_z = nullptr, *tri_scr = nullptr;
@@ -187,26 +192,78 @@ int enqueue_linearize(bos_solver* s) {
 }
 
 // RCCL exchange: every rank owns contiguous pieces of the block array (its poses' diagonal and
-// off-diagonal blocks, its landmarks' diagonal blocks) and of b; broadcast each piece from its
-// owner so every rank holds the full system for the replicated solve.
+// off-diagonal blocks, its landmarks' diagonal blocks) and of b. Each rank packs its pieces into one
+// buffer, one ncclAllGather of equal-size (padded) buffers moves them to every rank, and the
+// received pieces are copied to their places: every rank then holds the full system for the
+// replicated solve. (One collective instead of one broadcast per piece and rank.)
 int enqueue_exchange(bos_solver* s) {
     if (!s->comm) return BOS_OK;
     const ncclDataType_t ty = s->precision == BOS_FP32 ? ncclFloat : ncclDouble;
+    hipError_t e;
+    if (s->precision == BOS_FP32) {
+        e = bos::dev::launch_seg_copy<float>((float*)s->d_val, (float*)s->d_b, (float*)s->ex_send, (float*)s->ex_recv,
+                                            s->ex_pack, s->ex_npack, s->ex_maxlen_pack, s->stream);
+    } else {
+        e = bos::dev::launch_seg_copy<double>((double*)s->d_val, (double*)s->d_b, (double*)s->ex_send,
+                                             (double*)s->ex_recv, s->ex_pack, s->ex_npack, s->ex_maxlen_pack, s->stream);
+    }
+    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("exchange pack: ") + hipGetErrorString(e));
+    NC_TRY(ncclAllGather(s->ex_send, s->ex_recv, (size_t)s->ex_count, ty, s->comm, s->stream));
+    if (s->precision == BOS_FP32) {
+        e = bos::dev::launch_seg_copy<float>((float*)s->d_val, (float*)s->d_b, (float*)s->ex_send, (float*)s->ex_recv,
+                                            s->ex_unpack, s->ex_nunpack, s->ex_maxlen_unpack, s->stream);
+    } else {
+        e = bos::dev::launch_seg_copy<double>((double*)s->d_val, (double*)s->d_b, (double*)s->ex_send,
+                                             (double*)s->ex_recv, s->ex_unpack, s->ex_nunpack, s->ex_maxlen_unpack,
+                                             s->stream);
+    }
+    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("exchange unpack: ") + hipGetErrorString(e));
+    return BOS_OK;
+}
+
+// Segment tables of the exchange (world > 1, or a one-rank communicator in tests): rank r's pieces
+// in a fixed order [4 block-array ranges | 2 b ranges] at packed offsets, padded to the largest
+// rank's total.
+int setup_exchange(bos_solver* s) {
     const bos::Plan& P = s->plan;
-    NC_TRY(ncclGroupStart());
-    for (int r = 0; r < s->world; ++r) {
-        for (int q = 0; q < 4; ++q) {
-            const bos::Range& g = P.rank_val_ranges[4 * (size_t)r + q];
-            char* vb = (char*)s->d_val + g.begin * s->tsize;
-            if (g.end > g.begin) NC_TRY(ncclBroadcast(vb, vb, (size_t)(g.end - g.begin), ty, r, s->comm, s->stream));
-        }
-        for (int q = 0; q < 2; ++q) {
-            const bos::Range& g = P.rank_b_ranges[2 * (size_t)r + q];
-            char* bb = (char*)s->d_b + g.begin * s->tsize;
-            if (g.end > g.begin) NC_TRY(ncclBroadcast(bb, bb, (size_t)(g.end - g.begin), ty, r, s->comm, s->stream));
+    const int W = s->world;
+    std::vector<int64_t> total(W, 0);
+    for (int r = 0; r < W; ++r) {
+        for (int q = 0; q < 4; ++q) total[r] += P.rank_val_ranges[4 * (size_t)r + q].end - P.rank_val_ranges[4 * (size_t)r + q].begin;
+        for (int q = 0; q < 2; ++q) total[r] += P.rank_b_ranges[2 * (size_t)r + q].end - P.rank_b_ranges[2 * (size_t)r + q].begin;
+    }
+    s->ex_count = std::max<int64_t>(1, *std::max_element(total.begin(), total.end()));
+    std::vector<bos::dev::ExSeg> pack, unpack;
+    for (int r = 0; r < W; ++r) {
+        int64_t off = 0;
+        for (int q = 0; q < 6; ++q) {
+            const bos::Range& g = q < 4 ? P.rank_val_ranges[4 * (size_t)r + q] : P.rank_b_ranges[2 * (size_t)r + (q - 4)];
+            const int64_t len = g.end - g.begin;
+            if (len <= 0) continue;
+            const int32_t kind = q < 4 ? 0 : 1;
+            if (r == s->rank) {
+                pack.push_back({g.begin, off, len, kind, 2});
+                s->ex_maxlen_pack = std::max(s->ex_maxlen_pack, len);
+            } else {
+                unpack.push_back({(int64_t)r * s->ex_count + off, g.begin, len, 3, kind});
+                s->ex_maxlen_unpack = std::max(s->ex_maxlen_unpack, len);
+            }
+            off += len;
         }
     }
-    NC_TRY(ncclGroupEnd());
+    s->ex_npack = (int)pack.size();
+    s->ex_nunpack = (int)unpack.size();
+    int rc;
+    if ((rc = upload(&s->ex_pack, pack)) || (rc = upload(&s->ex_unpack, unpack))) return rc;
+    if (s->precision == BOS_FP32) {
+        float *a = nullptr, *b = nullptr;
+        if ((rc = dalloc(&a, (size_t)s->ex_count)) || (rc = dalloc(&b, (size_t)s->ex_count * W))) return rc;
+        s->ex_send = a; s->ex_recv = b;
+    } else {
+        double *a = nullptr, *b = nullptr;
+        if ((rc = dalloc(&a, (size_t)s->ex_count)) || (rc = dalloc(&b, (size_t)s->ex_count * W))) return rc;
+        s->ex_send = a; s->ex_recv = b;
+    }
     return BOS_OK;
 }
 
@@ -404,7 +461,8 @@ int bos_destroy(bos_solver* s) {
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_status,
-                    s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr};
+                    s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr,
+                    s->ex_send, s->ex_recv, s->ex_pack, s->ex_unpack};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (s->rf) rocsolver_destroy_rfinfo(s->rf);
@@ -506,6 +564,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         std::memcpy(&id, opt.nccl_unique_id, sizeof(id));
         ncclResult_t r = ncclCommInitRank(&s->comm, s->world, id, s->rank);
         if (r != ncclSuccess) return bail(fail(BOS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
+        if ((rc = setup_exchange(s))) return bail(rc);
     }
 
     // ---- upload
@@ -637,7 +696,10 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             (rc = upload(&s->tri_z, tz)) || (rc = dalloc(&s->tri_scr, 3 * (size_t)std::max(1, s->Mb))))
             return bail(rc);
     }
-    if (!pb->landmark_xy && NL && (rc = enqueue_triangulate(s))) return bail(rc);
+    if (!pb->landmark_xy && NL) {
+        if ((rc = enqueue_triangulate(s))) return bail(rc);
+        HIP_TRY(hipStreamSynchronize(s->stream));   // upload_cache reads the landmarks back
+    }
     if ((rc = upload_cache(s))) return bail(rc);
     HIP_TRY(hipStreamSynchronize(s->stream));
     *out = s;
