@@ -69,6 +69,11 @@ int bos_plan_inspect(const bos_problem* problem, int32_t solver, int32_t rank, i
  * dof order). Not used by any solve. */
 int bos_plan_mf_selftest(const bos_problem* problem, int32_t solver, const double* vals, const double* rhs, double* x);
 
+/* Test hook: the sharded exchange (pack / all-gather / unpack of every rank's pieces of H and b)
+ * simulated on the host for all `world` ranks; BOS_OK when every rank ends with every value the
+ * solver reads and every b entry but the fixed pose's. */
+int bos_plan_exchange_selftest(const bos_problem* problem, int32_t world);
+
 /* Diagnostics: one J+H launch with per-wave timeline stamps, 8 x uint64 per wave: block, wave in
  * block, kind (0 pose lanes / 1 landmark lanes), t_start, t_loop, t_loop_end, t_end (realtime clock,
  * 100 MHz ticks), hw_id | xcc_id << 32. capacity in waves; *n_waves = waves of the launch. Not part

@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = [
     "bos_dataset_load_g2o", "bos_dataset_synthetic", "bos_dataset_problem", "bos_dataset_pose_ids",
     "bos_dataset_landmark_ids", "bos_dataset_fixed_pose_id", "bos_dataset_bound", "bos_dataset_ground_truth",
     "bos_dataset_write_g2o", "bos_dataset_free", "bos_plan_inspect", "bos_plan_mf_selftest",
-    "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async",
+    "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async", "bos_plan_exchange_selftest",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -142,6 +142,7 @@ def lib():
                                             ctypes.c_int64, _ip, _ip, ctypes.POINTER(ctypes.c_uint8),
                                             ctypes.POINTER(ctypes.c_uint8), _ip, ctypes.POINTER(bos_plan_info)]),
         "bos_plan_mf_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, _dp, _dp, _dp]),
+        "bos_plan_exchange_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -317,6 +318,13 @@ def plan_mf_selftest(P: Problem, vals, rhs, solver: int = BOS_SOLVER_SUPERNODAL)
     _check(lib().bos_plan_mf_selftest(ctypes.byref(cs), solver, _ptr(v, ctypes.c_double), _ptr(b, ctypes.c_double),
                                       _ptr(x, ctypes.c_double)), "plan_mf_selftest")
     return x
+
+
+def plan_exchange_selftest(P: Problem, world: int) -> None:
+    """Host simulation of the sharded exchange for all `world` ranks (test hook); raises if a rank
+    would miss a value of H or b after the all-gather."""
+    cs = P.c_struct()
+    _check(lib().bos_plan_exchange_selftest(ctypes.byref(cs), world), "plan_exchange_selftest")
 
 
 def nccl_unique_id() -> bytes:

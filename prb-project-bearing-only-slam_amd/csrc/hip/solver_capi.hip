@@ -221,38 +221,22 @@ int enqueue_exchange(bos_solver* s) {
     return BOS_OK;
 }
 
-// Segment tables of the exchange (world > 1, or a one-rank communicator in tests): rank r's pieces
-// in a fixed order [4 block-array ranges | 2 b ranges] at packed offsets, padded to the largest
-// rank's total.
+// Segment tables of the exchange (host/plan.cpp exchange_segments) and its buffers.
 int setup_exchange(bos_solver* s) {
-    const bos::Plan& P = s->plan;
-    const int W = s->world;
-    std::vector<int64_t> total(W, 0);
-    for (int r = 0; r < W; ++r) {
-        for (int q = 0; q < 4; ++q) total[r] += P.rank_val_ranges[4 * (size_t)r + q].end - P.rank_val_ranges[4 * (size_t)r + q].begin;
-        for (int q = 0; q < 2; ++q) total[r] += P.rank_b_ranges[2 * (size_t)r + q].end - P.rank_b_ranges[2 * (size_t)r + q].begin;
-    }
-    s->ex_count = std::max<int64_t>(1, *std::max_element(total.begin(), total.end()));
-    std::vector<bos::dev::ExSeg> pack, unpack;
-    for (int r = 0; r < W; ++r) {
-        int64_t off = 0;
-        for (int q = 0; q < 6; ++q) {
-            const bos::Range& g = q < 4 ? P.rank_val_ranges[4 * (size_t)r + q] : P.rank_b_ranges[2 * (size_t)r + (q - 4)];
-            const int64_t len = g.end - g.begin;
-            if (len <= 0) continue;
-            const int32_t kind = q < 4 ? 0 : 1;
-            if (r == s->rank) {
-                pack.push_back({g.begin, off, len, kind, 2});
-                s->ex_maxlen_pack = std::max(s->ex_maxlen_pack, len);
-            } else {
-                unpack.push_back({(int64_t)r * s->ex_count + off, g.begin, len, 3, kind});
-                s->ex_maxlen_unpack = std::max(s->ex_maxlen_unpack, len);
-            }
-            off += len;
+    std::vector<bos::ExchangeSeg> hp, hu;
+    bos::exchange_segments(s->plan, s->rank, hp, hu, s->ex_count);
+    auto conv = [](const std::vector<bos::ExchangeSeg>& v, int64_t& maxlen) {
+        std::vector<bos::dev::ExSeg> o(v.size());
+        for (size_t i = 0; i < v.size(); ++i) {
+            o[i] = {v[i].src, v[i].dst, v[i].len, v[i].src_kind, v[i].dst_kind};
+            maxlen = std::max(maxlen, v[i].len);
         }
-    }
+        return o;
+    };
+    const std::vector<bos::dev::ExSeg> pack = conv(hp, s->ex_maxlen_pack), unpack = conv(hu, s->ex_maxlen_unpack);
     s->ex_npack = (int)pack.size();
     s->ex_nunpack = (int)unpack.size();
+    const int W = s->world;
     int rc;
     if ((rc = upload(&s->ex_pack, pack)) || (rc = upload(&s->ex_unpack, unpack))) return rc;
     if (s->precision == BOS_FP32) {

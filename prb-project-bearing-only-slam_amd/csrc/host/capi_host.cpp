@@ -223,6 +223,67 @@ int factor_mode_of(int32_t solver) {
 }
 }  // namespace
 
+// The sharded exchange simulated on the host for all `world` ranks (the RCCL all-gather becomes a
+// concatenation): every rank writes only its own pieces of the block array and b (value = index),
+// packs, the send buffers are concatenated, every rank unpacks; afterwards every rank must hold
+// every value the solver reads and every b entry but the fixed pose's.
+int bos_plan_exchange_selftest(const bos_problem* pb, int32_t world) {
+    if (!pb || world < 1) return hfail(BOS_ERR_INVALID, "bad argument");
+    bos::ProblemIndex pi;
+    pi.NP = pb->num_poses; pi.NL = pb->num_landmarks; pi.Mb = pb->num_bearings; pi.Mo = pb->num_odometry;
+    pi.fixed = pb->fixed_pose;
+    pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
+    pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
+    std::vector<bos::Plan> plans(world);
+    for (int r = 0; r < world; ++r) {
+        std::string err;
+        const int rc = bos::build_plan(pi, r, world, 0, plans[r], err);
+        if (rc) return hfail(rc, err);
+    }
+    const int64_t nval = plans[0].blk.size, nb = 3 * (int64_t)pi.NP + 2 * (int64_t)pi.NL;
+    const double junk = -1.0;
+    std::vector<std::vector<double>> val(world, std::vector<double>(nval, junk)), b(world, std::vector<double>(nb, junk));
+    std::vector<std::vector<bos::ExchangeSeg>> pack(world), unpack(world);
+    int64_t count = 0;
+    for (int r = 0; r < world; ++r) {
+        int64_t c = 0;
+        bos::exchange_segments(plans[r], r, pack[r], unpack[r], c);
+        if (r && c != count) return hfail(BOS_ERR_INVALID, "ranks disagree on the exchange size");
+        count = c;
+        for (int q = 0; q < 4; ++q)   // the J+H kernel of rank r writes its own pieces
+            for (int64_t i = plans[r].rank_val_ranges[4 * (size_t)r + q].begin; i < plans[r].rank_val_ranges[4 * (size_t)r + q].end; ++i) val[r][i] = (double)i;
+        for (int q = 0; q < 2; ++q)
+            for (int64_t i = plans[r].rank_b_ranges[2 * (size_t)r + q].begin; i < plans[r].rank_b_ranges[2 * (size_t)r + q].end; ++i) b[r][i] = (double)i;
+    }
+    std::vector<double> recv((size_t)count * world, junk);
+    for (int r = 0; r < world; ++r) {
+        std::vector<double> send((size_t)count, junk);
+        for (const bos::ExchangeSeg& g : pack[r]) {
+            const std::vector<double>& src = g.src_kind == 0 ? val[r] : b[r];
+            if (g.dst_kind != 2 || g.src + g.len > (int64_t)src.size() || g.dst + g.len > count)
+                return hfail(BOS_ERR_INVALID, "pack segment out of range");
+            std::copy(src.begin() + g.src, src.begin() + g.src + g.len, send.begin() + g.dst);
+        }
+        std::copy(send.begin(), send.end(), recv.begin() + (int64_t)r * count);   // the all-gather
+    }
+    for (int r = 0; r < world; ++r)
+        for (const bos::ExchangeSeg& g : unpack[r]) {
+            std::vector<double>& dst = g.dst_kind == 0 ? val[r] : b[r];
+            if (g.src_kind != 3 || g.src + g.len > (int64_t)recv.size() || g.dst + g.len > (int64_t)dst.size())
+                return hfail(BOS_ERR_INVALID, "unpack segment out of range");
+            std::copy(recv.begin() + g.src, recv.begin() + g.src + g.len, dst.begin() + g.dst);
+        }
+    for (int r = 0; r < world; ++r) {
+        for (int32_t v : plans[r].blk.csr_src)
+            if (val[r][v] != (double)v) return hfail(BOS_ERR_INVALID, "a block value the solver reads is missing on a rank");
+        for (int64_t i = 0; i < nb; ++i) {
+            const bool fixed = i < 3 * (int64_t)pi.NP && i / 3 == pi.fixed;
+            if (!fixed && b[r][i] != (double)i) return hfail(BOS_ERR_INVALID, "a b entry is missing on a rank");
+        }
+    }
+    return BOS_OK;
+}
+
 int bos_plan_inspect(const bos_problem* pb, int32_t solver, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
                      int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref,
                      bos_plan_info* info) {

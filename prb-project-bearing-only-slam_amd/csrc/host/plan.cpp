@@ -498,6 +498,34 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     return validate_plan(pi, P, err);
 }
 
+void exchange_segments(const Plan& P, int rank, std::vector<ExchangeSeg>& pack, std::vector<ExchangeSeg>& unpack,
+                       int64_t& count) {
+    const int W = P.world;
+    pack.clear();
+    unpack.clear();
+    auto piece = [&](int r, int q) -> const Range& {
+        return q < 4 ? P.rank_val_ranges[4 * (size_t)r + q] : P.rank_b_ranges[2 * (size_t)r + (q - 4)];
+    };
+    count = 1;
+    for (int r = 0; r < W; ++r) {
+        int64_t t = 0;
+        for (int q = 0; q < 6; ++q) t += std::max<int64_t>(0, piece(r, q).end - piece(r, q).begin);
+        count = std::max(count, t);
+    }
+    for (int r = 0; r < W; ++r) {
+        int64_t off = 0;
+        for (int q = 0; q < 6; ++q) {
+            const Range& g = piece(r, q);
+            const int64_t len = g.end - g.begin;
+            if (len <= 0) continue;
+            const int32_t kind = q < 4 ? 0 : 1;
+            if (r == rank) pack.push_back({g.begin, off, len, kind, 2});
+            else unpack.push_back({(int64_t)r * count + off, g.begin, len, 3, kind});
+            off += len;
+        }
+    }
+}
+
 // Wave-interleaved lane lists (LaneLists in plan.hpp) from per-lane item ranges.
 void make_lane_lists(int lanes, const std::vector<int32_t>& lane_ptr, const std::vector<int32_t>& items, LaneLists& L,
                      bool even) {

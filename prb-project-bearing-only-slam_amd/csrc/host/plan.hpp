@@ -165,6 +165,18 @@ enum FactorMode {
 // Builds the plan. Returns 0 or a negative BOS_ERR_* code with a message in err.
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& out, std::string& err);
 
+// The sharded J+H exchange (hip/solver_capi.hip enqueue_exchange): rank r packs its pieces of the
+// block array (kind 0) and of b (kind 1) — rank_val_ranges then rank_b_ranges, in order — into a
+// send buffer (kind 2) of `count` elements (the largest rank's total), one all-gather concatenates
+// the W send buffers into the receive buffer (kind 3), and every other rank's pieces are copied
+// back to their places.
+struct ExchangeSeg {
+    int64_t src, dst, len;      // element offsets and count
+    int32_t src_kind, dst_kind;
+};
+void exchange_segments(const Plan& P, int rank, std::vector<ExchangeSeg>& pack, std::vector<ExchangeSeg>& unpack,
+                       int64_t& count);
+
 // Node ordering only (positions) and its symbolic cost. mode kFactorScalar / kFactorNone: the
 // cheapest of temporal, landmarks-first and nested dissection; kFactorMultifrontal: nested
 // dissection; kFactorSchur: landmarks first, then nested dissection of the poses on the graph of S.

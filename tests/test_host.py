@@ -188,6 +188,16 @@ def test_plan_shards_partition_rows(world):
     assert np.all(b_owned[keep] == 1)
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("which", ["c1", "synthetic"])
+def test_plan_exchange_covers_every_rank(world, which):
+    """The segment tables of the sharded exchange (pack own pieces, all-gather, unpack the others')
+    leave every rank with every value of H the solver reads and every b entry: the N>1 data path
+    checked on the host, since one GPU cannot host two RCCL ranks."""
+    P = bos.load_g2o(C1) if which == "c1" else bos.synthetic(3000, 6000, 10, seed=5)
+    bos.plan_exchange_selftest(P, world)
+
+
 def test_parallel_g2o_parser_equals_line_parser(tmp_path, monkeypatch):
     """The chunked parallel g2o parser (default) and the line-by-line one give identical problems,
     on the reference dataset and on a written synthetic world large enough to use several chunks."""
