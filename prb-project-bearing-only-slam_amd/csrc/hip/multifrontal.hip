@@ -495,64 +495,55 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     mf_stamp(a, s, 3, lane);
     const bool live = lane < m;
     double row[MAXM];
-    double myinv = 0.0;
 #pragma unroll
     for (int c = 0; c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk32(lane, c, m)] : 0.0;
-    // Right-looking: step j broadcasts column j through a double-buffered LDS column (one store
-    // per lane, same-address reads). Entries above the diagonal (c > lane) and rows >= m are
-    // scratch, so the updates need no predicates.
+    double* Ls = a.L + a.L_off[s];
+    double* Us = a.U + a.U_off[s];
+    double wi = live ? wv[lane] + xo : 0.0;   // forward elimination, fused into the pivot loop
+    // Right-looking, with a rotating register window: before step j, row[t] holds column j + t of
+    // this lane's row, so the pivot column is always row[0] and the update of column j + 1 + t is
+    // written to row[t] (the shift costs nothing). The pivot loop is a real loop — one copy of its
+    // body instead of MAXM unrolled ones keeps the kernel inside the instruction cache. Column j
+    // (rows > j) is broadcast through a double-buffered LDS column indexed by t; entries above the
+    // diagonal, rows >= m and columns >= m are scratch, so the updates need no predicates.
     const int kf = (a.diag_skip & 8) ? 0 : k;
+#pragma nounroll
+    for (int j = 0; j < kf; ++j) {
+        double* col = colbuf + (j & 1) * MAXM;
+        if (lane > j && lane < m) col[lane - j - 1] = row[0];
+        // the pivot straight from lane j's register (no LDS round trip on the critical path; the
+        // column's LDS broadcast lands meanwhile), 1 / sqrt(d) by v_rsq_f64 + two Newton steps
+        double d = readlane_d(row[0], j);
+        wave_sync();
+        if (!(d > 0.0)) {
+            if (lane == 0) atomicAdd(a.info, 1);
+            d = 1e-300;
+        }
+        const double inv = rsqrt_nr(d), ljj = d * inv;
+        const double lij = lane == j ? ljj : row[0] * inv;   // L[i, j]
+        if (live && lane >= j && !(a.diag_skip & 16)) Ls[lane + (int64_t)j * m] = lij;
+        // forward step: y_j = w_j / L_jj, w_i -= L_ij y_j
+        const double yj = readlane_d(wi, j) * inv;
+        if (lane == j) wi = yj;
+        else if (lane > j) wi -= lij * yj;
+        const double g = lij * inv;                          // L[i, j] / L[j, j]
+        const int nt = m - j - 1;                            // live columns after this step (uniform)
 #pragma unroll
-    for (int j = 0; j < MAXM; ++j) {
-        if (j < kf) {
-            double* col = colbuf + (j & 1) * MAXM;
-            if (lane < MAXM) col[lane] = row[j];
-            // the pivot straight from lane j's register (no LDS round trip on the critical path; the
-            // column's LDS broadcast lands meanwhile), 1 / sqrt(d) by v_rsq_f64 + two Newton steps
-            double d = readlane_d(row[j], j);
-            wave_sync();
-            if (!(d > 0.0)) {
-                if (lane == 0) atomicAdd(a.info, 1);
-                d = 1e-300;
-            }
-            const double inv = rsqrt_nr(d), ljj = d * inv;
-            const double lij = lane == j ? ljj : row[j] * inv;   // L[i, j]
-            row[j] = lij;
-            if (lane == j) myinv = inv;                          // 1 / L_jj, kept by the pivot lane
-            const double g = lij * inv;                          // L[i, j] / L[j, j]
-            // columns l < m only (m is wave-uniform: whole groups of 8 are skipped by a scalar branch)
-            // (loops with compile-time trip counts only, so row[] stays in registers)
+        for (int t0 = 0; t0 < MAXM - 1; t0 += 8) {
+            if (t0 < nt) {
 #pragma unroll
-            for (int l0 = 0; l0 < MAXM; l0 += 8) {
-                if (l0 + 8 > j + 1 && l0 < m) {
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int l = l0 + u;
-                        if (l > j && l < MAXM) row[l] = fma(-g, col[l], row[l]);   // -= L[i,j] L[l,j]
-                    }
+                for (int u = 0; u < 8; ++u) {
+                    const int t = t0 + u;
+                    if (t < MAXM - 1) row[t] = fma(-g, col[t], row[t + 1]);   // -= L[i,j] L[l,j], l = j + 1 + t
                 }
             }
         }
     }
     mf_stamp(a, s, 4, lane);
-    double* Ls = a.L + a.L_off[s];
-    double* Us = a.U + a.U_off[s];
+    // the update matrix: row[t] holds column k + t
 #pragma unroll
-    for (int c = 0; c < MAXM; ++c) {
-        if (live && c <= lane && !(a.diag_skip & 16)) {
-            if (c < k) Ls[lane + (int64_t)c * m] = row[c];
-            else stc<COH>(Us + pk(lane - k, c - k, r), row[c]);
-        }
-    }
-    // fused forward elimination with the rows of L held in registers
-    double wi = live ? wv[lane] + xo : 0.0;
-#pragma unroll
-    for (int j = 0; j < MAXM; ++j) {
-        if (j < k) {
-            const double yj = readlane_d(wi * myinv, j);   // lane j: w_j / L_jj
-            if (lane == j) wi = yj;
-            else if (lane > j) wi -= row[j] * yj;
-        }
+    for (int t = 0; t < MAXM; ++t) {
+        if (live && lane >= k && t <= lane - k && !(a.diag_skip & 16)) stc<COH>(Us + pk(lane - k, t, r), row[t]);
     }
     if (live) {
         if (lane < k) a.x[c0 + lane] = wi;
