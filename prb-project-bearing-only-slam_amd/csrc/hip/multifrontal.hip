@@ -405,22 +405,76 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F,
     if (a.stamps && lane == 0) { a.stamps[8 * (int64_t)s + 6] = t_rows; a.stamps[8 * (int64_t)s + 7] = t_ext; }
 }
 
-// A child's extend-add inputs: its row map entry and u-vector entry for this lane (lane < rc), the
-// first 256 entries of its packed update matrix (4 per lane), and where the rest starts.
+// ---- dataflow (work-queue) kernels: one launch walks a whole tree range. A wavefront takes the
+// next front from an atomic ticket (fronts listed in topological order), waits for the fronts it
+// depends on (children bottom-up, the parent top-down) through per-supernode completion flags,
+// processes the front and publishes its flag. Hand-off data goes through coherent (sc1) accesses
+// (ldc / stc), drained by s_waitcnt before the flag store: no L2 writeback / invalidate per front.
+// A wave only ever waits for tickets already taken by running waves, so any grid size is
+// deadlock-free; every wait is bounded (a stall is reported through info, never a hang).
+struct Flow {
+    const int32_t* order;   // fronts in processing order
+    int n;
+    int* ticket;            // zeroed before the launch
+    uint32_t* done;         // per supernode: epoch of its last completion
+    uint32_t epoch;
+    const int32_t* slev;    // level of every supernode
+    int lev0;               // factor: children below this level were finished by earlier launches
+};
+
+constexpr int kStall = 1 << 20;   // added to info when a dependency wait times out
+
+__device__ __forceinline__ int next_ticket(int* ticket) {
+    int t = 0;
+    if (threadIdx.x == 0) t = atomicAdd(ticket, 1);
+    return __builtin_amdgcn_readfirstlane(t);
+}
+
+__device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
+    if (threadIdx.x == 0) {
+        int it = 0;
+        while (__hip_atomic_load(f.done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != f.epoch) {
+            if (++it > (1 << 22)) {
+                atomicAdd(info, kStall);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+}
+
+__device__ __forceinline__ void publish_done(const Flow& f, int s) {
+    // drain this wave's sc1 stores before the flag (a workgroup-scope fence emits no vmcnt wait)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A child's extend-add inputs: its r, row map entry (lane < rc) and where its update matrix and
+// u-vector live — static structure, loaded before the child has finished — then its values: the
+// u-vector entry and the first 256 entries of the packed update matrix (4 per lane).
 struct ChildPre {
     int rc, smap_v;
     double uval;
     double v[4];
     const double* Uc;
+    const double* uc;
 };
 
-template <bool COH>
-__device__ __forceinline__ void child_prefetch(const MfArgs& a, int c, int lane, ChildPre& p) {
+__device__ __forceinline__ void child_meta(const MfArgs& a, int c, int lane, ChildPre& p) {
     const int rc = a.r[c];   // rc < m <= MAXM
     p.rc = rc;
     p.smap_v = lane < rc ? a.rmap[a.rmap_off[c] + lane] : 0;
-    p.uval = lane < rc ? ldc<COH>(a.u + a.u_off[c] + lane) : 0.0;
     p.Uc = a.U + a.U_off[c];
+    p.uc = a.u + a.u_off[c];
+}
+
+template <bool COH>
+__device__ __forceinline__ void child_vals(int lane, ChildPre& p) {
+    const int rc = p.rc;
+    p.uval = lane < rc ? ldc<COH>(p.uc + lane) : 0.0;
     const int ne = rc * (rc + 1) / 2;
 #pragma unroll
     for (int u = 0; u < 4; ++u) p.v[u] = 64 * u + lane < ne ? ldc<COH>(p.Uc + 64 * u + lane) : 0.0;
@@ -460,22 +514,24 @@ __device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p,
 // their update matrices; after the partial Cholesky, lane i eliminates with its row of L (still in
 // registers): y_j = w_j / L_jj, w_i -= L_ij y_j. y goes to x, the remaining w (rows >= k) to the
 // front's u-vector for its parent.
-template <int MAXM, bool COH>
+template <int MAXM, bool FLOW>
 __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf, int* smap,
-                                                 double* wv, FoldBuf* fb, int lane) {
+                                                 double* wv, FoldBuf* fb, int lane, const Flow* f) {
+    constexpr bool COH = FLOW;
     mf_stamp(a, s, 0, lane);
     const int k = a.k[s], r = a.r[s], m = k + r;
     const int nfold = a.fold_cnt[s];
     const int c0 = a.col0[s];
     const int np = m * (m + 1) / 2;
     const double xo = lane < k ? a.x[c0 + lane] : 0.0;   // right-hand side of the own dofs (k < 64)
-    // The first two (non-folded) children's row maps, u-vectors and first 256 update-matrix
-    // entries are loaded up front, in flight during the assembly and the fold (a child's data
-    // was published before this front started: the flow kernel waited for its flag).
+    // The first two (non-folded) children's structure is loaded up front, in flight during the
+    // assembly and the fold. Everything up to the extend-add depends on H only, so the flow kernel
+    // waits for the children after it: on the critical path a front's assembly and fold overlap
+    // its children's work.
     const int cb = (a.diag_skip & 4) ? a.child_ptr[s + 1] : a.child_ptr[s] + nfold, ce = a.child_ptr[s + 1];
     ChildPre p0, p1;
-    if (cb < ce) child_prefetch<COH>(a, a.child[cb], lane, p0);
-    if (cb + 1 < ce) child_prefetch<COH>(a, a.child[cb + 1], lane, p1);
+    if (cb < ce) child_meta(a, a.child[cb], lane, p0);
+    if (cb + 1 < ce) child_meta(a, a.child[cb + 1], lane, p1);
     for (int e = lane; e < np; e += 64) F[e] = 0.0;
     for (int i = lane; i < m; i += 64) wv[i] = 0.0;    // children's u-vectors accumulate here
     wave_sync();
@@ -483,13 +539,20 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     wave_sync();
     mf_stamp(a, s, 1, lane);
     if (nfold > 0 && !(a.diag_skip & 2)) fold_children(a, s, F, wv, fb, m, lane);
+    if constexpr (FLOW) {
+        for (int ci = a.child_ptr[s]; ci < ce; ++ci)
+            if (f->slev[a.child[ci]] >= f->lev0) wait_done(*f, a.child[ci], a.info);
+    }
     mf_stamp(a, s, 2, lane);
     // extend-add, children in list order (deterministic)
+    if (cb < ce) child_vals<COH>(lane, p0);
+    if (cb + 1 < ce) child_vals<COH>(lane, p1);
     if (cb < ce) extend_child<COH>(a, p0, F, wv, smap, m, lane);
     if (cb + 1 < ce) extend_child<COH>(a, p1, F, wv, smap, m, lane);
     for (int ci = cb + 2; ci < ce; ++ci) {
         ChildPre pq;
-        child_prefetch<COH>(a, a.child[ci], lane, pq);
+        child_meta(a, a.child[ci], lane, pq);
+        child_vals<COH>(lane, pq);
         extend_child<COH>(a, pq, F, wv, smap, m, lane);
     }
     mf_stamp(a, s, 3, lane);
@@ -560,12 +623,17 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double wv[MAXM];
     __shared__ int smap[64];
     __shared__ FoldBuf fb;
-    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, smap, wv, &fb, threadIdx.x);
+    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, smap, wv, &fb, threadIdx.x, nullptr);
 }
 
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
 // L panel (m x k). The rows below the supernode are ancestors' dofs, already final in x.
-template <bool COH> __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w, int lane) {
+// The L panel and the front's own forward results do not depend on the ancestors, so the flow
+// kernel stages them before it waits for the parent (FLOW: f and parent set).
+template <bool FLOW>
+__device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w, int lane, const Flow* f,
+                                               const int32_t* parent) {
+    constexpr bool COH = FLOW;
     const int k = a.k[s], r = a.r[s], m = k + r;
     const int c0 = a.col0[s];
     const int32_t* fi = a.findex + a.findex_off[s];
@@ -573,8 +641,11 @@ template <bool COH> __device__ __forceinline__ void backward_front(const MfArgs&
     double* xs = w + 2 * k;
     double* Lw = w + 2 * k + r;
     stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
-    for (int i = lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
+    if constexpr (FLOW) {
+        if (parent[s] >= 0) wait_done(*f, parent[s], a.info);
+    }
+    for (int i = lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     wave_sync();
     // t_j = sum_i L[k + i, j] x[fi[k + i]]: fixed-order wave reduction per column
     for (int j = 0; j < k; ++j) {
@@ -598,7 +669,7 @@ template <bool COH> __device__ __forceinline__ void backward_front(const MfArgs&
 
 __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
     extern __shared__ __attribute__((aligned(16))) double w[];
-    backward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x);
+    backward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x, nullptr, nullptr);
 }
 
 // Backward substitution of the folded landmarks (k = 2), one thread each: t = L21^T x_rows, then
@@ -623,53 +694,6 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     a.x[c0 + 1] = x1;
 }
 
-// ---- dataflow (work-queue) kernels: one launch walks a whole tree range. A wavefront takes the
-// next front from an atomic ticket (fronts listed in topological order), waits for the fronts it
-// depends on (children bottom-up, the parent top-down) through per-supernode completion flags,
-// processes the front and publishes its flag. Hand-off data goes through coherent (sc1) accesses
-// (ldc / stc), drained by s_waitcnt before the flag store: no L2 writeback / invalidate per front.
-// A wave only ever waits for tickets already taken by running waves, so any grid size is
-// deadlock-free; every wait is bounded (a stall is reported through info, never a hang).
-struct Flow {
-    const int32_t* order;   // fronts in processing order
-    int n;
-    int* ticket;            // zeroed before the launch
-    uint32_t* done;         // per supernode: epoch of its last completion
-    uint32_t epoch;
-    const int32_t* slev;    // level of every supernode
-    int lev0;               // factor: children below this level were finished by earlier launches
-};
-
-constexpr int kStall = 1 << 20;   // added to info when a dependency wait times out
-
-__device__ __forceinline__ int next_ticket(int* ticket) {
-    int t = 0;
-    if (threadIdx.x == 0) t = atomicAdd(ticket, 1);
-    return __builtin_amdgcn_readfirstlane(t);
-}
-
-__device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
-    if (threadIdx.x == 0) {
-        int it = 0;
-        while (__hip_atomic_load(f.done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != f.epoch) {
-            if (++it > (1 << 22)) {
-                atomicAdd(info, kStall);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    wave_sync();
-}
-
-__device__ __forceinline__ void publish_done(const Flow& f, int s) {
-    // drain this wave's sc1 stores before the flag (a workgroup-scope fence emits no vmcnt wait)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // The flow kernel instantiates one register class only: inlining all four merged their register
 // demands (256 VGPRs + AGPRs, 1 wave per SIMD), out-of-line calls spilled, and forcing 4 waves per
 // SIMD spilled too (all measured slower). Fronts of the flow range are <= kFlowMaxM (mf_create
@@ -689,9 +713,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
         const int t = next_ticket(f.ticket);
         if (t >= f.n) break;
         const int s = f.order[t];
-        for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci)
-            if (f.slev[a.child[ci]] >= f.lev0) wait_done(f, a.child[ci], a.info);
-        factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, smap, wv, &fb, lane);   // m <= kFlowMaxM
+        factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, smap, wv, &fb, lane, &f);   // m <= kFlowMaxM
         publish_done(f, s);
     }
 }
@@ -704,8 +726,7 @@ __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flo
         const int t = next_ticket(f.ticket);
         if (t >= f.n) break;
         const int s = f.order[t];
-        if (parent[s] >= 0) wait_done(f, parent[s], a.info);
-        backward_front<true>(a, s, w, threadIdx.x);
+        backward_front<true>(a, s, w, threadIdx.x, &f, parent);
         publish_done(f, s);
     }
 }
