@@ -647,6 +647,24 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
     }
     for (int i = lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     wave_sync();
+    if (k <= 64) {
+        // lane j < k: t_j = sum_i L[k + i, j] x[fi[k + i]] in row order, then the triangular
+        // solve in registers: x_j = (y_j - t_j) / L_jj broadcast from lane j, t_i += L[j, i] x_j
+        const bool own = lane < k;
+        double tj = 0.0;
+        if (own)
+            for (int i = 0; i < r; ++i) tj += Lw[k + i + lane * m] * xs[i];
+        const double yv = own ? w[lane] : 0.0, djj = own ? Lw[lane + lane * m] : 1.0;
+        double xv = 0.0;
+        for (int j = k - 1; j >= 0; --j) {
+            const double xj = readlane_d((yv - tj) / djj, j);
+            if (lane == j) xv = xj;
+            else if (lane < j) tj += Lw[j + lane * m] * xj;
+        }
+        if (own) stc<COH>(a.x + c0 + lane, xv);
+        wave_sync();
+        return;
+    }
     // t_j = sum_i L[k + i, j] x[fi[k + i]]: fixed-order wave reduction per column
     for (int j = 0; j < k; ++j) {
         double v = 0.0;
