@@ -690,26 +690,36 @@ __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
     backward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x, nullptr, nullptr);
 }
 
-// Backward substitution of the folded landmarks (k = 2), one thread each: t = L21^T x_rows, then
+// Backward substitution of the folded landmarks (k = 2), 16 lanes each (rows of the landmark's
+// two L columns across the lanes, coalesced): t = L21^T x_rows reduced over the 16 lanes, then
 // x1 = (y1 - t1) / L11, x0 = (y0 - t0 - L10 x1) / L00.
+constexpr int kFoldLanes = 16;
 __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
-    const int i = blockIdx.x * kMfBlock + threadIdx.x;
-    if (i >= a.count) return;
-    const int s = a.level[i];
-    const int r = a.r[s], m = 2 + r, c0 = a.col0[s];
-    const double* Ls = a.L + a.L_off[s];
-    const int32_t* fi = a.findex + a.findex_off[s] + 2;
+    const int g = (blockIdx.x * kMfBlock + threadIdx.x) / kFoldLanes;
+    const int q0 = threadIdx.x % kFoldLanes;
+    const bool valid = g < a.count;
+    const int s = valid ? a.level[g] : 0;
+    const int r = valid ? a.r[s] : 0, m = 2 + r;
+    const double* Ls = a.L + (valid ? a.L_off[s] : 0);
+    const int32_t* fi = a.findex + (valid ? a.findex_off[s] : 0) + 2;
     double t0 = 0.0, t1 = 0.0;
-#pragma unroll 4
-    for (int q = 0; q < r; ++q) {
+    for (int q = q0; q < r; q += kFoldLanes) {
         const double xv = a.x[fi[q]];
         t0 += Ls[2 + q] * xv;
         t1 += Ls[m + 2 + q] * xv;
     }
-    const double x1 = (a.x[c0 + 1] - t1) / Ls[m + 1];
-    t0 += Ls[1] * x1;
-    a.x[c0] = (a.x[c0] - t0) / Ls[0];
-    a.x[c0 + 1] = x1;
+#pragma unroll
+    for (int o = kFoldLanes / 2; o > 0; o >>= 1) {
+        t0 += __shfl_xor(t0, o, kFoldLanes);
+        t1 += __shfl_xor(t1, o, kFoldLanes);
+    }
+    if (valid && q0 == 0) {
+        const int c0 = a.col0[s];
+        const double x1 = (a.x[c0 + 1] - t1) / Ls[m + 1];
+        t0 += Ls[1] * x1;
+        a.x[c0] = (a.x[c0] - t0) / Ls[0];
+        a.x[c0 + 1] = x1;
+    }
 }
 
 // The flow kernel instantiates one register class only: inlining all four merged their register
@@ -1016,7 +1026,7 @@ hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
         MfArgs g = d->args(0, 0, nullptr, x);
         g.level = d->fold_list;
         g.count = d->n_fold;
-        hipLaunchKernelGGL(mf_backward_fold, dim3((d->n_fold + kMfBlock - 1) / kMfBlock), dim3(kMfBlock), 0, s, g);
+        hipLaunchKernelGGL(mf_backward_fold, dim3(((int64_t)d->n_fold * kFoldLanes + kMfBlock - 1) / kMfBlock), dim3(kMfBlock), 0, s, g);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
