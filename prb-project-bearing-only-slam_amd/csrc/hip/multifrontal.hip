@@ -876,6 +876,21 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
                     d->lds_bwd[lc] = std::max(d->lds_bwd[lc], 2 * k * 8);
                 }
             }
+            // longest fronts first (estimated by flops plus folded rows): the launch's tail is
+            // then made of short fronts
+            {
+                auto cost = [&](int s2) {
+                    const double k = F.k[s2], r = F.r[s2];
+                    double c = k * k * k / 3 + k * k * r + k * r * r;
+                    if (!F.fold_cnt.empty())
+                        for (int ci = F.child_ptr[s2]; ci < F.child_ptr[s2] + F.fold_cnt[s2]; ++ci)
+                            c += 4.0 * F.r[F.child[ci]] * F.r[F.child[ci]];
+                    return c;
+                };
+                static const bool lpt = [] { const char* e = std::getenv("BOS_MF_LPT"); return !e || std::atoi(e) != 0; }();
+                if (lpt)
+                    std::stable_sort(lst.begin() + d->ptr[lc], lst.end(), [&](int x, int y) { return cost(x) > cost(y); });
+            }
             d->ptr[lc + 1] = (int32_t)lst.size();
         }
     // dataflow set-up
