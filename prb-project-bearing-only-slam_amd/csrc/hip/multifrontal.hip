@@ -109,19 +109,27 @@ struct MfArgs {
                                  // 8 factor loop, 16 panel writes (results are then wrong)
 };
 
-// LDS of one wave's folded rows: L[t, 0..1] of the landmark, the row's u entry, its position p in
-// the parent front with the packed column base cb(p) (packed index of (i, p) = cb(p) + i), and the
-// landmark's r
+// LDS of one wave's fold chunk: the y (forward-step) values of its landmarks, two per landmark
 struct FoldBuf {
-    double2 l[kFoldChunk];
-    double u[kFoldChunk];
-    int2 pc[kFoldChunk];
-    int rc[kFoldChunk];
+    double y[2 * fold_chunk_landmarks(kMfWaveMaxM)];
 };
 
-// Assembly of H entries into a front by one wavefront (F[dst] = A[src]), 4 entries per lane in
-// flight: index loads, then value gathers, then LDS stores.
-__device__ __forceinline__ void assemble_wave(const MfArgs& a, int s, double* F, int lane) {
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// The folded landmarks' contribution to the front, lower 16 x 16 blocks of W W^T (f64 MFMA
+// accumulators: lane l holds rows (l >> 4) + 4 v, column l & 15 of each block) and, per
+// position lane, the u-vector part -W y.
+template <int MAXM>
+struct FoldAcc {
+    static constexpr int NB = MAXM / 16, NP = NB * (NB + 1) / 2;
+    dbl4 d[NP];
+    double w;
+};
+
+// Assembly of H entries into a front by one wavefront (F[dst] = A[src], or += when the front
+// already holds the folded landmarks' part), 4 entries per lane in flight: index loads, then value
+// gathers, then LDS stores.
+__device__ __forceinline__ void assemble_wave(const MfArgs& a, int s, double* F, int lane, bool add) {
     const int q1 = a.amap_ptr[s + 1];
     for (int q0 = a.amap_ptr[s]; q0 < q1; q0 += 256) {
         int src[4], dst[4];
@@ -136,7 +144,7 @@ __device__ __forceinline__ void assemble_wave(const MfArgs& a, int s, double* F,
         for (int u = 0; u < 4; ++u) v[u] = q0 + 64 * u + lane < q1 ? a.A[src[u]] : 0.0;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (q0 + 64 * u + lane < q1) F[dst[u]] = v[u];
+            if (q0 + 64 * u + lane < q1) F[dst[u]] = add ? F[dst[u]] + v[u] : v[u];
     }
 }
 
@@ -290,13 +298,15 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 }
 
 // Folded landmark children (Schur ordering) of front s, eliminated by its wave: per chunk (whole
-// children, <= 64 rows) lane q takes row t of landmark c (one 32-byte record: sources of its two
-// entries, of the landmark's 2 x 2 block, the landmark's col0 / r / L offset and the row's position
-// in this front), factors the 2 x 2 block, forms L[t, 0..1], the landmark's forward step y and the
-// row's u entry, and writes the landmark's L panel and y. The landmarks' update matrices
-// -L21 L21^T and u-vectors are then extend-added into this front one landmark at a time (pairs of
-// rows across lanes; positions of one landmark are distinct): deterministic, and nothing goes
-// through global memory. Same arithmetic as the generic path up to rounding.
+// children, <= 64 rows, <= fold_chunk_landmarks(m) landmarks) lane q takes row t of landmark c
+// (one 32-byte record: sources of its two entries, of the landmark's 2 x 2 block, the landmark's
+// col0 / r / L offset, the row's position in this front and c's index in the chunk), factors the
+// 2 x 2 block, forms L[t, 0..1], the landmark's forward step y, and writes the landmark's L panel
+// and y. The rows also form the chunk's W (front position x 2 columns per landmark, in LDS that
+// the front's F uses later) and its y; W W^T accumulates in f64 MFMA registers (the landmarks'
+// update matrices -L21 L21^T, summed) and -W y in the position lanes (their u-vectors). The
+// caller subtracts both once the front is assembled. Nothing goes through global memory and the
+// result is deterministic.
 __device__ __forceinline__ int4 fold_rec_load(const MfArgs& a, int q, int half) {
     return reinterpret_cast<const int4*>(a.fold_rec + (int64_t)kFoldRec * q)[half];
 }
@@ -319,8 +329,16 @@ __device__ __forceinline__ FoldVals fold_vals(const MfArgs& a, const int4& r0, c
     return v;
 }
 
-__device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F, double* wv, FoldBuf* fb, int m,
-                                              int lane) {
+template <int MAXM>
+__device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W, FoldBuf* fb, int m, int lane,
+                                              FoldAcc<MAXM>& acc) {
+    constexpr int NB = FoldAcc<MAXM>::NB;
+    constexpr int WS = 2 * fold_chunk_landmarks(MAXM) + 1;   // W row stride (odd: no bank conflicts)
+    const int nbm = (m + 15) >> 4;
+#pragma unroll
+    for (int q = 0; q < FoldAcc<MAXM>::NP; ++q) acc.d[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+    acc.w = 0.0;
+    for (int e = lane; e < MAXM * WS; e += 64) W[e] = 0.0;
     const int ch0 = a.fold_cptr[s], ch1 = a.fold_cptr[s + 1];
     int n = a.fold_chunk[ch0 + 1] - a.fold_chunk[ch0];
     int4 r0 = make_int4(-1, -1, -1, -1), r1 = make_int4(0, 0, 0, 0);
@@ -330,12 +348,13 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F,
     int nn = ch0 + 1 < ch1 ? a.fold_chunk[ch0 + 2] - a.fold_chunk[ch0 + 1] : 0;
     int4 n0 = make_int4(-1, -1, -1, -1), n1 = make_int4(0, 0, 0, 0);
     if (lane < nn) { n0 = fold_rec_load(a, a.fold_chunk[ch0 + 1] + lane, 0); n1 = fold_rec_load(a, a.fold_chunk[ch0 + 1] + lane, 1); }
-    unsigned long long t_rows = 0, t_ext = 0;   // diagnostics (stamps 6, 7): per-row phase, extend-add phase
+    unsigned long long t_rows = 0, t_ext = 0;   // diagnostics (stamps 6, 7): per-row phase, W W^T phase
     for (int ch = ch0; ch < ch1; ++ch) {
         const unsigned long long tc0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
         const double ht0 = v.ht0, ht1 = v.ht1, a00 = v.a00, a10 = v.a10, a11 = v.a11;
-        const int t = r1.z & 63, rc = (r1.z >> 6) & 63, pos = r1.z >> 12;
+        const int t = r1.z & 63, rc = (r1.z >> 6) & 63, pos = (r1.z >> 12) & 63, lml = (r1.z >> 18) & 63;
         const bool mine = lane < n;
+        const int nl = __builtin_amdgcn_readlane(lml, n - 1) + 1;   // landmarks of this chunk
         const double x0 = v.x0, x1 = v.x1;
         const int col0 = r1.y;
         const int64_t loff = r1.w;
@@ -367,33 +386,39 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F,
                 a.x[col0] = y0;
                 a.x[col0 + 1] = y1;
                 if (bad) atomicAdd(a.info, bad);
+                fb->y[2 * lml] = y0;
+                fb->y[2 * lml + 1] = y1;
             }
-            fb->l[lane] = make_double2(lt0, lt1);
-            fb->u[lane] = -(lt0 * y0 + lt1 * y1);
-            fb->pc[lane] = make_int2(pos, pos * m - pos * (pos - 1) / 2 - pos);
-            fb->rc[lane] = rc;
+            W[pos * WS + 2 * lml] = lt0;
+            W[pos * WS + 2 * lml + 1] = lt1;
         }
         wave_sync();
         const unsigned long long tc1 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-        // one landmark at a time: its packed r x r pairs across lanes, (row, column) in closed form
-        for (int c0 = 0; c0 < n;) {
-            const int rcc = fb->rc[c0];
-            const int ne = rcc * (rcc + 1) / 2;
-            const float b = 2.0f * rcc + 1.0f;
-            for (int e = lane; e < ne; e += 64) {
-                int j = (int)((b - sqrtf(b * b - 8.0f * e)) * 0.5f);
-                int sj = j * rcc - j * (j - 1) / 2;
-                if (sj > e) { --j; sj = j * rcc - j * (j - 1) / 2; }
-                else if (sj + (rcc - j) <= e) { sj += rcc - j; ++j; }
-                const int i = j + (e - sj);
-                const double2 li = fb->l[c0 + i], lj = fb->l[c0 + j];
-                const int pi = fb->pc[c0 + i].x, cbj = fb->pc[c0 + j].y;
-                F[cbj + pi] -= li.x * lj.x + li.y * lj.y;
-            }
-            if (lane < rcc) wv[fb->pc[c0 + lane].x] += fb->u[c0 + lane];
-            wave_sync();
-            c0 += rcc;
+        const int kc = 2 * nl;
+        if (lane < m) {   // u-vector part: -(W y) at this lane's position
+            double w = 0.0;
+            for (int q = 0; q < kc; ++q) w += W[lane * WS + q] * fb->y[q];
+            acc.w -= w;
         }
+        // W W^T, 4 columns per MFMA step; lane l feeds row 16 b + (l & 15), column 4 st + (l >> 4)
+        // of W to the blocks of row b (as A) and of column b (as B, the same values)
+        for (int st = 0; 4 * st < kc; ++st) {
+            double av[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) av[b] = b < nbm ? W[(16 * b + (lane & 15)) * WS + 4 * st + (lane >> 4)] : 0.0;
+            int q = 0;
+#pragma unroll
+            for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+                for (int bj = 0; bj <= bi; ++bj, ++q)
+                    if (bi < nbm) acc.d[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], av[bj], acc.d[q], 0, 0, 0);
+        }
+        wave_sync();
+        if (mine) {   // clear this chunk's W entries for the next chunk
+            W[pos * WS + 2 * lml] = 0.0;
+            W[pos * WS + 2 * lml + 1] = 0.0;
+        }
+        wave_sync();
         n = nn;
         nn = n2;
         if (a.stamps) {
@@ -403,6 +428,29 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* F,
         }
     }
     if (a.stamps && lane == 0) { a.stamps[8 * (int64_t)s + 6] = t_rows; a.stamps[8 * (int64_t)s + 7] = t_ext; }
+}
+
+// The front before its assembly: every lower entry of F and of wv set to minus the folded
+// landmarks' contribution (each entry once).
+template <int MAXM>
+__device__ __forceinline__ void fold_store(const FoldAcc<MAXM>& acc, double* F, double* wv, int m, int lane) {
+    constexpr int NB = FoldAcc<MAXM>::NB;
+    const int nbm = (m + 15) >> 4;
+    int q = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+        for (int bj = 0; bj <= bi; ++bj, ++q) {
+            if (bi < nbm) {
+                const int j = 16 * bj + (lane & 15);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int i = 16 * bi + (lane >> 4) + 4 * e;
+                    if (i < m && j <= i) F[pk32(i, j, m)] = -acc.d[q][e];
+                }
+            }
+        }
+    if (lane < m) wv[lane] = acc.w;
 }
 
 // ---- dataflow (work-queue) kernels: one launch walks a whole tree range. A wavefront takes the
@@ -532,13 +580,22 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     ChildPre p0, p1;
     if (cb < ce) child_meta(a, a.child[cb], lane, p0);
     if (cb + 1 < ce) child_meta(a, a.child[cb + 1], lane, p1);
-    for (int e = lane; e < np; e += 64) F[e] = 0.0;
-    for (int i = lane; i < m; i += 64) wv[i] = 0.0;    // children's u-vectors accumulate here
-    wave_sync();
-    if (!(a.diag_skip & 1)) assemble_wave(a, s, F, lane);
+    // the folded landmarks first (their W uses F's LDS): F and the u-vector accumulator wv start
+    // from minus their contribution, the assembly then adds H
+    const bool fold = nfold > 0 && !(a.diag_skip & 2);
+    if (fold) {
+        FoldAcc<MAXM> facc;
+        fold_children<MAXM>(a, s, F, fb, m, lane, facc);
+        wave_sync();
+        fold_store<MAXM>(facc, F, wv, m, lane);
+    } else {
+        for (int e = lane; e < np; e += 64) F[e] = 0.0;
+        for (int i = lane; i < m; i += 64) wv[i] = 0.0;    // children's u-vectors accumulate here
+    }
     wave_sync();
     mf_stamp(a, s, 1, lane);
-    if (nfold > 0 && !(a.diag_skip & 2)) fold_children(a, s, F, wv, fb, m, lane);
+    if (!(a.diag_skip & 1)) assemble_wave(a, s, F, lane, fold);
+    wave_sync();
     if constexpr (FLOW) {
         for (int ci = a.child_ptr[s]; ci < ce; ++ci)
             if (f->slev[a.child[ci]] >= f->lev0) wait_done(*f, a.child[ci], a.info);

@@ -400,7 +400,7 @@ int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* va
                 Lc[2 + t] = l0[q];
                 Lc[mc + 2 + t] = l1[q];
                 if (t == 0) { Lc[0] = l00; Lc[1] = l10; Lc[mc + 1] = l11; x[col0] = y0; x[col0 + 1] = y1; }
-                pos[q] = rec[6] >> 12;
+                pos[q] = (rec[6] >> 12) & 63;
                 rcs[q] = rc;
                 fwv[s][pos[q]] -= l0[q] * y0 + l1[q] * y1;
             }

@@ -959,7 +959,8 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
     }
     // fold records, one per row t of a folded child c (parents in id order, their folded children
     // in child-list order): {src (t, 0), src (t, 1), src (0, 0), src (1, 0), src (1, 1), col0[c],
-    // t | r[c] << 6 | (row t's position in the parent front) << 12, L_off[c]}; src = block-array
+    // t | r[c] << 6 | (row t's position in the parent front) << 12 | (c's index in the chunk) << 18,
+    // L_off[c]}; src = block-array
     // index of the front entry (-1: structurally zero)
     F.fold_cptr.assign(ns + 1, 0);
     F.fold_chunk.clear();
@@ -968,10 +969,15 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
     int32_t nrows = 0;
     for (int p = 0; p < ns; ++p) {
         F.fold_cptr[p] = (int32_t)F.fold_chunk.size();
-        int32_t chunk_rows = kFoldChunk;   // forces a new chunk at the parent's first child
+        int32_t chunk_rows = kFoldChunk, chunk_lms = 0;   // forces a new chunk at the parent's first child
+        const int cap = fold_chunk_landmarks(F.k[p] + F.r[p]);
         for (int ci = F.child_ptr[p]; ci < F.child_ptr[p] + F.fold_cnt[p]; ++ci) {
             const int c = F.child[ci], rc = F.r[c], mc = 2 + rc;
-            if (chunk_rows + rc > kFoldChunk) { F.fold_chunk.push_back(nrows); chunk_rows = 0; }
+            if (chunk_rows + rc > kFoldChunk || chunk_lms >= cap) {
+                F.fold_chunk.push_back(nrows);
+                chunk_rows = 0;
+                chunk_lms = 0;
+            }
             std::vector<int32_t> src((size_t)mc * 2, -1);   // (i, j) -> i + j * mc
             for (int q = F.amap_ptr[c]; q < F.amap_ptr[c + 1]; ++q) {
                 int64_t d = F.amap_dst[q], j = 0;
@@ -980,10 +986,12 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
             }
             for (int t = 0; t < rc; ++t) {
                 const int32_t rec[kFoldRec] = {src[2 + t], src[2 + t + mc], src[0], src[1], src[1 + mc], F.col0[c],
-                                               t | rc << 6 | F.rmap[F.rmap_off[c] + t] << 12, (int32_t)F.L_off[c]};
+                                               t | rc << 6 | F.rmap[F.rmap_off[c] + t] << 12 | chunk_lms << 18,
+                                               (int32_t)F.L_off[c]};
                 F.fold_rec.insert(F.fold_rec.end(), rec, rec + kFoldRec);
             }
             chunk_rows += rc;
+            ++chunk_lms;
             nrows += rc;
         }
     }

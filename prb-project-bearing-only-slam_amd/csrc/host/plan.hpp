@@ -99,6 +99,9 @@ struct OrderingReport {
 constexpr int kMfWaveMaxM = 64;
 constexpr int kFoldChunk = 64;   // folded rows per chunk (one per lane)
 constexpr int kFoldRec = 8;      // ints per folded row
+// landmarks per fold chunk for a parent front of size m: the device forms the chunk's
+// W (m x 2 landmarks, aliasing the front's LDS) whose W W^T it accumulates with f64 MFMA
+constexpr int fold_chunk_landmarks(int m) { return m <= 16 ? 2 : m <= 32 ? 4 : 8; }
 inline int64_t mf_packed(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }   // i >= j
 
 struct Multifrontal {
