@@ -803,7 +803,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
     }
 }
 
-__global__ __launch_bounds__(64) void mf_factor_flow(const MfArgs a, const Flow f) { factor_flow_body(a, f); }
+__global__ __launch_bounds__(64, 3) void mf_factor_flow(const MfArgs a, const Flow f) { factor_flow_body(a, f); }
 
 __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flow f, const int32_t* parent) {
     extern __shared__ __attribute__((aligned(16))) double w[];

@@ -308,7 +308,8 @@ int order_nodes(const ProblemIndex& pi, int mode, std::vector<int32_t>& node_pos
         for (int u = 0; u < NP; ++u) active[u] = u != pi.fixed;
         std::vector<int32_t> ord_p;
         std::vector<std::pair<int32_t, int32_t>> pblocks;
-        nested_dissection(build_schur_graph(pi), active, ord_p, kSchurLeaf, &pblocks);
+        static const int leaf = [] { const char* e = std::getenv("BOS_SCHUR_LEAF"); return e ? std::atoi(e) : kSchurLeaf; }();
+        nested_dissection(build_schur_graph(pi), active, ord_p, leaf, &pblocks);
         if ((int)ord_p.size() != NP - 1) { err = "nested dissection of the pose graph lost nodes"; return BOS_ERR_INVALID; }
         order.insert(order.end(), ord_p.begin(), ord_p.end());
         if (blocks)
