@@ -835,6 +835,10 @@ inline int front_class(int m) { return m <= kMfWaveMaxM ? (m - 1) / 16 : 4; }
 
 struct MfDevice {
     int nlevels = 0;
+    // level 0's largest fronts (class 64: one round, latency-bound) run on a side stream beside
+    // the other classes of level 0 (BOS_MF_SIDE=0 disables)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // supernodes of (level l, class c) = list[ptr[l * kClasses + c], ptr[l * kClasses + c + 1])
     std::vector<int32_t> ptr;
     std::vector<int> lds_factor, lds_fwd, lds_bwd;   // per (level, class): dynamic LDS bytes
@@ -1008,6 +1012,16 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         (rc = up(&d->fold_list, F.fold_list, err)))
         return rc;
     d->n_fold = (int)F.fold_list.size();
+    {
+        const char* e = std::getenv("BOS_MF_SIDE");
+        if (!(e && std::atoi(e) == 0) &&
+            (hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking) != hipSuccess ||
+             hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess ||
+             hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess)) {
+            err = "side stream creation failed (multifrontal)";
+            return -2;
+        }
+    }
     auto alloc = [&](double** p, int64_t n) -> int {
         if (n <= 0) n = 1;
         if (hipMalloc((void**)p, n * sizeof(double)) != hipSuccess) { err = "hipMalloc failed (multifrontal buffers)"; return -2; }
@@ -1043,6 +1057,9 @@ void mf_destroy(MfDevice* d) {
                     d->findex_off, d->L, d->U, d->u, d->scratch};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
+    if (d->ev_join) (void)hipEventDestroy(d->ev_join);
+    if (d->side) (void)hipStreamDestroy(d->side);
     delete d;
 }
 
@@ -1053,10 +1070,18 @@ hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
     const uint32_t epoch = ++d->epoch;
     for (int l = 0; l < d->flow_lev0; ++l) {
         int n;
+        const bool fork = l == 0 && d->side && d->count(l, 3) > 0;
+        if (fork) {
+            if ((e = hipEventRecord(d->ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(d->side, d->ev_fork, 0)) != hipSuccess)
+                return e;
+            hipLaunchKernelGGL(mf_factor_reg<64>, dim3(d->count(l, 3)), dim3(64), 0, d->side, d->args(l, 3, A, x));
+            if ((e = hipEventRecord(d->ev_join, d->side)) != hipSuccess) return e;
+        }
         if ((n = d->count(l, 0))) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(l, 0, A, x));
         if ((n = d->count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(l, 1, A, x));
         if ((n = d->count(l, 2))) hipLaunchKernelGGL(mf_factor_reg<48>, dim3(n), dim3(64), 0, s, d->args(l, 2, A, x));
-        if ((n = d->count(l, 3))) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(l, 3, A, x));
+        if ((n = d->count(l, 3)) && !fork) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(l, 3, A, x));
+        if (fork && (e = hipStreamWaitEvent(s, d->ev_join, 0)) != hipSuccess) return e;
         if ((n = d->count(l, 4))) {   // large fronts: workgroup factorization, then their forward step
             hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), d->lds_factor[l * kClasses + 4], s,
                                d->args(l, 4, A, x));
