@@ -835,8 +835,8 @@ inline int front_class(int m) { return m <= kMfWaveMaxM ? (m - 1) / 16 : 4; }
 
 struct MfDevice {
     int nlevels = 0;
-    // level 0's largest fronts (class 64: one round, latency-bound) run on a side stream beside
-    // the other classes of level 0 (BOS_MF_SIDE=0 disables)
+    // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
+    // the level's other classes (BOS_MF_SIDE=0 disables)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // supernodes of (level l, class c) = list[ptr[l * kClasses + c], ptr[l * kClasses + c + 1])
@@ -1070,7 +1070,7 @@ hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
     const uint32_t epoch = ++d->epoch;
     for (int l = 0; l < d->flow_lev0; ++l) {
         int n;
-        const bool fork = l == 0 && d->side && d->count(l, 3) > 0;
+        const bool fork = d->side && d->count(l, 3) > 0;
         if (fork) {
             if ((e = hipEventRecord(d->ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(d->side, d->ev_fork, 0)) != hipSuccess)
                 return e;
