@@ -616,7 +616,15 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     const bool live = lane < m;
     double row[MAXM];
 #pragma unroll
-    for (int c = 0; c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk32(lane, c, m)] : 0.0;
+    for (int c0 = 0; c0 < MAXM; c0 += 8) {   // whole groups of 8 past m skipped by a scalar branch
+        if (c0 < m) {
+#pragma unroll
+            for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk32(lane, c, m)] : 0.0;
+        } else {
+#pragma unroll
+            for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = 0.0;
+        }
+    }
     double* Ls = a.L + a.L_off[s];
     double* Us = a.U + a.U_off[s];
     double wi = live ? wv[lane] + xo : 0.0;   // forward elimination, fused into the pivot loop
@@ -662,8 +670,12 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     mf_stamp(a, s, 4, lane);
     // the update matrix: row[t] holds column k + t
 #pragma unroll
-    for (int t = 0; t < MAXM; ++t) {
-        if (live && lane >= k && t <= lane - k && !(a.diag_skip & 16)) stc<COH>(Us + pk(lane - k, t, r), row[t]);
+    for (int t0 = 0; t0 < MAXM; t0 += 8) {
+        if (t0 < r) {
+#pragma unroll
+            for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
+                if (live && lane >= k && t <= lane - k && !(a.diag_skip & 16)) stc<COH>(Us + pk(lane - k, t, r), row[t]);
+        }
     }
     if (live) {
         if (lane < k) a.x[c0 + lane] = wi;

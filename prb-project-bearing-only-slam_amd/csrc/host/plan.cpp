@@ -924,9 +924,14 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
                 const int m = F.k[F.level[q]] + F.r[F.level[q]];
                 if (m <= 64) ++h[(m - 1) / 16];
             }
+            int single = 0;   // fronts with exactly one (non-folded) child
+            for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
+                const int s2 = F.level[q];
+                single += F.child_ptr[s2 + 1] - F.child_ptr[s2] - F.fold_cnt[s2] == 1;
+            }
             std::fprintf(stderr, "mf level %2d: %6d fronts, k mean %5.1f max %3d, r mean %5.1f max %3d, m max %3d, "
-                         "m<=16/32/48/64: %d %d %d %d, flops %.3g\n", l, n, sk / n, mk, sr / n, mr, mm, h[0], h[1], h[2],
-                         h[3], fl);
+                         "m<=16/32/48/64: %d %d %d %d, flops %.3g, one child %d\n", l, n, sk / n, mk, sr / n, mr, mm, h[0], h[1], h[2],
+                         h[3], fl, single);
         }
     // assembly map: every stored entry of H (row i >= col j) goes to the front of col j's supernode,
     // read from its block value
