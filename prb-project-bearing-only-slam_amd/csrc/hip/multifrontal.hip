@@ -635,6 +635,8 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     // (rows > j) is broadcast through a double-buffered LDS column indexed by t; entries above the
     // diagonal, rows >= m and columns >= m are scratch, so the updates need no predicates.
     const int kf = (a.diag_skip & 8) ? 0 : k;
+    int nbad = 0;   // non-positive pivots (uniform), reported once per front
+    double* Lj = Ls + lane;
 #pragma nounroll
     for (int j = 0; j < kf; ++j) {
         double* col = colbuf + (j & 1) * MAXM;
@@ -643,13 +645,18 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         // column's LDS broadcast lands meanwhile), 1 / sqrt(d) by v_rsq_f64 + two Newton steps
         double d = readlane_d(row[0], j);
         wave_sync();
-        if (!(d > 0.0)) {
-            if (lane == 0) atomicAdd(a.info, 1);
-            d = 1e-300;
-        }
+        // the first 8 column entries are read before the pivot arithmetic (no branch between), so
+        // their LDS latency overlaps it
+        double c0v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c0v[u] = u < MAXM ? col[u] : 0.0;
+        const bool bad = !(d > 0.0);
+        nbad += bad;
+        d = bad ? 1e-300 : d;
         const double inv = rsqrt_nr(d), ljj = d * inv;
         const double lij = lane == j ? ljj : row[0] * inv;   // L[i, j]
-        if (live && lane >= j && !(a.diag_skip & 16)) Ls[lane + (int64_t)j * m] = lij;
+        if (live && lane >= j && !(a.diag_skip & 16)) *Lj = lij;
+        Lj += m;
         // forward step: y_j = w_j / L_jj, w_i -= L_ij y_j
         const double yj = readlane_d(wi, j) * inv;
         if (lane == j) wi = yj;
@@ -657,16 +664,20 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         const double g = lij * inv;                          // L[i, j] / L[j, j]
         const int nt = m - j - 1;                            // live columns after this step (uniform)
 #pragma unroll
-        for (int t0 = 0; t0 < MAXM - 1; t0 += 8) {
+        for (int u = 0; u < 8; ++u)
+            if (u < MAXM - 1) row[u] = fma(-g, c0v[u], row[u + 1]);   // -= L[i,j] L[l,j], l = j + 1 + t
+#pragma unroll
+        for (int t0 = 8; t0 < MAXM - 1; t0 += 8) {
             if (t0 < nt) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int t = t0 + u;
-                    if (t < MAXM - 1) row[t] = fma(-g, col[t], row[t + 1]);   // -= L[i,j] L[l,j], l = j + 1 + t
+                    if (t < MAXM - 1) row[t] = fma(-g, col[t], row[t + 1]);
                 }
             }
         }
     }
+    if (nbad && lane == 0) atomicAdd(a.info, nbad);
     mf_stamp(a, s, 4, lane);
     // the update matrix: row[t] holds column k + t
 #pragma unroll
@@ -793,8 +804,9 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
 
 // The flow kernel instantiates one register class only: inlining all four merged their register
 // demands (256 VGPRs + AGPRs, 1 wave per SIMD), out-of-line calls spilled, and forcing 4 waves per
-// SIMD spilled too (all measured slower). Fronts of the flow range are <= kFlowMaxM (mf_create
-// picks the range accordingly).
+// SIMD spilled too (all measured slower); 2 waves per SIMD (no spills) measured faster than 3 (a
+// few spilled registers). Fronts of the flow range are <= kFlowMaxM (mf_create picks the range
+// accordingly).
 constexpr int kFlowMaxM = 48;
 
 __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f) {
@@ -815,7 +827,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
     }
 }
 
-__global__ __launch_bounds__(64, 3) void mf_factor_flow(const MfArgs a, const Flow f) { factor_flow_body(a, f); }
+__global__ __launch_bounds__(64, 2) void mf_factor_flow(const MfArgs a, const Flow f) { factor_flow_body(a, f); }
 
 __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flow f, const int32_t* parent) {
     extern __shared__ __attribute__((aligned(16))) double w[];
@@ -1104,7 +1116,7 @@ hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
     }
     if (d->n_flow_factor > 0) {
         const Flow f{d->order_factor, d->n_flow_factor, d->tickets, d->done, epoch, d->slev, d->flow_lev0};
-        const int grid = std::min(d->n_flow_factor, d->ncu * 12);
+        const int grid = std::min(d->n_flow_factor, d->ncu * 8);   // 2 waves per SIMD resident
         hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
