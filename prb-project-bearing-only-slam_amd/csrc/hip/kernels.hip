@@ -350,9 +350,21 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int blk, un
 // Pose and landmark blocks interleaved in proportion over the grid (pose block i sits at the
 // b with floor(b Pb / T) == i < floor((b + 1) Pb / T)), so every CU gets its share of the longer
 // pose lists.
+// XCD-aware block order: blocks b and b + 8 share an XCD (and its L2), so a segment [s0, s1) of
+// the grid is renumbered to give each XCD a contiguous run of it; the pose (landmark) blocks an
+// XCD runs then cover a stretch of the trajectory, and the landmark (pose) cache lines their
+// gathers fetch come from that stretch only, instead of every XCD's L2 fetching all of them.
+__device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t s0, int64_t s1) {
+    const int64_t n = s1 - s0, i = b - s0, g = i & 7, q = n >> 3, rmd = n & 7;
+    return s0 + g * q + (g < rmd ? g : rmd) + (i >> 3);
+}
+
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams<T> P) {
-    const int64_t nb = gridDim.x, b = blockIdx.x;
+    const int64_t nb = gridDim.x;
+    int64_t b = blockIdx.x;
+    if (P.xcd_remap && !P.interleave)
+        b = b < P.pose_blocks ? xcd_contiguous(b, 0, P.pose_blocks) : xcd_contiguous(b, P.pose_blocks, nb);
     int pb0, pb1;
     if (P.interleave) {
         pb0 = (int)(b * P.pose_blocks / nb);

@@ -61,6 +61,7 @@ template <typename T> struct LinParams {
     T lambda;                 // damping
     int lm_rep;               // landmark-lane blocks handled per launched block (set by the launcher)
     int interleave;           // pose and landmark blocks interleaved over the grid (else pose blocks first)
+    int xcd_remap;            // each XCD runs a contiguous run of the pose and of the landmark blocks
     int diag_skip;            // timing diagnostics only (BOS_JH_DIAG_SKIP): 1 landmark lanes, 2 pose lanes, 4 odometry
     unsigned long long* diag_stamps;   // timeline diagnostics only (8 x u64 per wave), null otherwise
 };

@@ -157,6 +157,8 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     static const int interleave = [] { const char* e = std::getenv("BOS_JH_INTERLEAVE"); return e ? std::atoi(e) : 0; }();
     static const int diag_skip = [] { const char* e = std::getenv("BOS_JH_DIAG_SKIP"); return e ? std::atoi(e) : 0; }();
     p.interleave = interleave;
+    static const int xcd_remap = [] { const char* e = std::getenv("BOS_JH_XCD"); return e ? std::atoi(e) : 1; }();
+    p.xcd_remap = xcd_remap;
     p.diag_skip = diag_skip;
     p.diag_stamps = nullptr;
     p.lm_rep = 1;
