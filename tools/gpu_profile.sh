@@ -11,8 +11,7 @@ mkdir -p $O
 for P in fp32 fp64; do
   CPU=""
   [ $P = fp64 ] && CPU="--no-cpu-baseline"
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace_$P -o run --output-format csv -- \
-    python3 bench.py --steps 200 --warmup 20 --gn-steps 10 --precision $P $CPU > $O/bench_$P.json 2> $O/bench_$P.err || exit 1
+  # PMC passes first, so the traced bench below reports this build's traffic
   i=0
   for C in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum" \
            "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" \
@@ -21,7 +20,10 @@ for P in fp32 fp64; do
       python3 bench.py --steps 20 --warmup 2 --gn-steps 0 --no-cpu-baseline --precision $P > $O/pmc_${P}_$i.json 2> $O/pmc_${P}_$i.err || exit 1
     i=$((i+1))
   done
-  ALGO=$(python3 -c "import json,sys; print(json.load(open('$O/bench_$P.json'))['roofline']['algorithmic_bytes_per_launch'])")
+  ALGO=$(python3 -c "import json; print(json.loads([l for l in open('$O/pmc_${P}_0.json').read().splitlines() if l.startswith('{')][-1])['roofline']['algorithmic_bytes_per_launch'])")
   python3 tools/pmc_summary.py $O/pmc_linearize_$P.json $ALGO \
     "config 3 synthetic, 100k poses / 200k landmarks / 1M bearings, J+H build $P" $O/pmc_${P}_0 $O/pmc_${P}_1 $O/pmc_${P}_2 || exit 1
+  cp $O/pmc_linearize_$P.json profiles/${TAG}_pmc_linearize_$P.json || exit 1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace_$P -o run --output-format csv -- \
+    python3 bench.py --steps 200 --warmup 20 --gn-steps 10 --precision $P $CPU > $O/bench_$P.json 2> $O/bench_$P.err || exit 1
 done
