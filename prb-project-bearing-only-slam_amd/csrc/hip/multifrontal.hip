@@ -572,6 +572,10 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     const int c0 = a.col0[s];
     const int np = m * (m + 1) / 2;
     const double xo = lane < k ? a.x[c0 + lane] : 0.0;   // right-hand side of the own dofs (k < 64)
+    // output offsets up front: their loads complete during the assembly instead of before the pivots
+    double* Ls = a.L + a.L_off[s];
+    double* Us = a.U + a.U_off[s];
+    double* us = a.u + a.u_off[s];
     // The first two (non-folded) children's structure is loaded up front, in flight during the
     // assembly and the fold. Everything up to the extend-add depends on H only, so the flow kernel
     // waits for the children after it: on the critical path a front's assembly and fold overlap
@@ -625,8 +629,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = 0.0;
         }
     }
-    double* Ls = a.L + a.L_off[s];
-    double* Us = a.U + a.U_off[s];
     double wi = live ? wv[lane] + xo : 0.0;   // forward elimination, fused into the pivot loop
     // Right-looking, with a rotating register window: before step j, row[t] holds column j + t of
     // this lane's row, so the pivot column is always row[0] and the update of column j + 1 + t is
@@ -690,7 +692,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     }
     if (live) {
         if (lane < k) a.x[c0 + lane] = wi;
-        else stc<COH>(a.u + a.u_off[s] + (lane - k), wi);
+        else stc<COH>(us + (lane - k), wi);
     }
     wave_sync();
     mf_stamp(a, s, 5, lane);
