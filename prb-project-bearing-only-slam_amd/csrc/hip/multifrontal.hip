@@ -722,12 +722,14 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
     double* t = w + k;
     double* xs = w + 2 * k;
     double* Lw = w + 2 * k + r;
+    const int xi0 = lane < r ? fi[k + lane] : 0;   // where the first 64 rows' x live (static)
     stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
     for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
     if constexpr (FLOW) {
         if (parent[s] >= 0) wait_done(*f, parent[s], a.info);
     }
-    for (int i = lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
+    if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
+    for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     wave_sync();
     if (k <= 64) {
         // lane j < k: t_j = sum_i L[k + i, j] x[fi[k + i]] in row order, then the triangular
