@@ -867,6 +867,7 @@ struct MfDevice {
     // the level's other classes (BOS_MF_SIDE=0 disables)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int tiny16 = 256;   // class-16 launches of at most this many fronts go to the side stream too (BOS_MF_TINY16)
     // supernodes of (level l, class c) = list[ptr[l * kClasses + c], ptr[l * kClasses + c + 1])
     std::vector<int32_t> ptr;
     std::vector<int> lds_factor, lds_fwd, lds_bwd;   // per (level, class): dynamic LDS bytes
@@ -1040,6 +1041,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         (rc = up(&d->fold_list, F.fold_list, err)))
         return rc;
     d->n_fold = (int)F.fold_list.size();
+    if (const char* e = std::getenv("BOS_MF_TINY16")) d->tiny16 = std::atoi(e);
     {
         const char* e = std::getenv("BOS_MF_SIDE");
         if (!(e && std::atoi(e) == 0) &&
@@ -1099,13 +1101,17 @@ hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
     for (int l = 0; l < d->flow_lev0; ++l) {
         int n;
         const bool fork = d->side && d->count(l, 3) > 0;
+        // a handful of class-16 fronts (one latency-bound round, negligible load) follow them there
+        const bool tiny16 = fork && d->count(l, 0) <= d->tiny16;
         if (fork) {
             if ((e = hipEventRecord(d->ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(d->side, d->ev_fork, 0)) != hipSuccess)
                 return e;
             hipLaunchKernelGGL(mf_factor_reg<64>, dim3(d->count(l, 3)), dim3(64), 0, d->side, d->args(l, 3, A, x));
+            if (tiny16 && (n = d->count(l, 0)))
+                hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, d->side, d->args(l, 0, A, x));
             if ((e = hipEventRecord(d->ev_join, d->side)) != hipSuccess) return e;
         }
-        if ((n = d->count(l, 0))) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(l, 0, A, x));
+        if ((n = d->count(l, 0)) && !tiny16) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(l, 0, A, x));
         if ((n = d->count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(l, 1, A, x));
         if ((n = d->count(l, 2))) hipLaunchKernelGGL(mf_factor_reg<48>, dim3(n), dim3(64), 0, s, d->args(l, 2, A, x));
         if ((n = d->count(l, 3)) && !fork) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(l, 3, A, x));
