@@ -105,6 +105,7 @@ struct MfArgs {
     const int32_t* fold_chunk;
     const int32_t* fold_rec;
     unsigned long long* stamps;  // timing diagnostics only (BOS_MF_STAMPS): 8 per supernode, null otherwise
+    int pair;                    // register fronts: two pivots per step (BOS_MF_PAIR=0: one)
     int diag_skip;               // timing diagnostics only (BOS_MF_DIAG_SKIP): 1 assembly, 2 fold, 4 extend-add,
                                  // 8 factor loop, 16 panel writes (results are then wrong)
 };
@@ -639,8 +640,60 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     const int kf = (a.diag_skip & 8) ? 0 : k;
     int nbad = 0;   // non-positive pivots (uniform), reported once per front
     double* Lj = Ls + lane;
+    int j = 0;
+    // Two pivots per step: column j + 1 is brought up to date in registers (L(j+1, j) by readlane),
+    // both columns go through ONE LDS broadcast as pairs, and the trailing columns take a rank-2
+    // update; the window rotates by two.
+    if (a.pair) {
 #pragma nounroll
-    for (int j = 0; j < kf; ++j) {
+        for (; j + 1 < kf; j += 2) {
+            double d0 = readlane_d(row[0], j);
+            const bool bad0 = !(d0 > 0.0);
+            nbad += bad0;
+            d0 = bad0 ? 1e-300 : d0;
+            const double inv0 = rsqrt_nr(d0), l00 = d0 * inv0;
+            const double l0 = lane == j ? l00 : row[0] * inv0;   // L[i, j]
+            const double lj1 = readlane_d(l0, j + 1);            // L[j+1, j]
+            const double f1 = fma(-l0, lj1, row[1]);             // column j+1 after pivot j
+            double d1 = readlane_d(f1, j + 1);
+            const bool bad1 = !(d1 > 0.0);
+            nbad += bad1;
+            d1 = bad1 ? 1e-300 : d1;
+            const double inv1 = rsqrt_nr(d1), l11 = d1 * inv1;
+            const double l1 = lane == j + 1 ? l11 : f1 * inv1;   // L[i, j+1]
+            double2* cp = reinterpret_cast<double2*>(colbuf);   // (L[l, j], L[l, j+1]), l = j + 2 + t
+            if (lane > j + 1 && lane < m) cp[lane - j - 2] = make_double2(l0, l1);
+            if (live && !(a.diag_skip & 16)) {
+                if (lane >= j) Lj[0] = l0;
+                if (lane >= j + 1) Lj[m] = l1;
+            }
+            Lj += 2 * m;
+            const double y0 = readlane_d(wi, j) * inv0;          // forward steps j, j + 1
+            if (lane == j) wi = y0;
+            else if (lane > j) wi -= l0 * y0;
+            const double y1 = readlane_d(wi, j + 1) * inv1;
+            if (lane == j + 1) wi = y1;
+            else if (lane > j + 1) wi -= l1 * y1;
+            wave_sync();
+            const int nt = m - j - 2;                            // live columns after this step
+#pragma unroll
+            for (int t0 = 0; t0 < MAXM - 2; t0 += 8) {
+                if (t0 < nt) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int t = t0 + u;
+                        if (t < MAXM - 2) {
+                            const double2 c = cp[t];
+                            row[t] = fma(-l1, c.y, fma(-l0, c.x, row[t + 2]));
+                        }
+                    }
+                }
+            }
+            wave_sync();
+        }
+    }
+#pragma nounroll
+    for (; j < kf; ++j) {
         double* col = colbuf + (j & 1) * MAXM;
         if (lane > j && lane < m) col[lane - j - 1] = row[0];
         // the pivot straight from lane j's register (no LDS round trip on the critical path; the
@@ -915,6 +968,8 @@ struct MfDevice {
         g.fold_cnt = fold_cnt; g.fold_cptr = fold_cptr; g.fold_chunk = fold_chunk; g.fold_rec = fold_rec;
         static const int skip = [] { const char* e = std::getenv("BOS_MF_DIAG_SKIP"); return e ? std::atoi(e) : 0; }();
         g.diag_skip = skip;
+        static const int pair = [] { const char* e = std::getenv("BOS_MF_PAIR"); return e ? std::atoi(e) : 1; }();
+        g.pair = pair;
         g.stamps = stamps;
         return g;
     }
