@@ -689,7 +689,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
                     }
                 }
             }
-            wave_sync();
+            __builtin_amdgcn_wave_barrier();   // the next step's pair stores stay after these reads
         }
     }
 #pragma nounroll
