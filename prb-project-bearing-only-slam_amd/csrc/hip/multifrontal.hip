@@ -106,8 +106,8 @@ struct MfArgs {
     const int32_t* fold_rec;
     unsigned long long* stamps;  // timing diagnostics only (BOS_MF_STAMPS): 8 per supernode, null otherwise
     int pair;                    // register fronts: two pivots per step (BOS_MF_PAIR=0: one)
-    int diag_skip;               // timing diagnostics only (BOS_MF_DIAG_SKIP): 1 assembly, 2 fold, 4 extend-add,
-                                 // 8 factor loop, 16 panel writes (results are then wrong)
+    int diag_skip;               // timing diagnostics only (BOS_MF_DIAG_SKIP): 1 assembly, 2 fold, 4 extend-add
+                                 // (results are then wrong)
 };
 
 // LDS of one wave's fold chunk: the y (forward-step) values of its landmarks, two per landmark
@@ -637,7 +637,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     // body instead of MAXM unrolled ones keeps the kernel inside the instruction cache. Column j
     // (rows > j) is broadcast through a double-buffered LDS column indexed by t; entries above the
     // diagonal, rows >= m and columns >= m are scratch, so the updates need no predicates.
-    const int kf = (a.diag_skip & 8) ? 0 : k;
+    const int kf = k;
     int nbad = 0;   // non-positive pivots (uniform), reported once per front
     double* Lj = Ls + lane;
     int j = 0;
@@ -663,7 +663,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             const double l1 = lane == j + 1 ? l11 : f1 * inv1;   // L[i, j+1]
             double2* cp = reinterpret_cast<double2*>(colbuf);   // (L[l, j], L[l, j+1]), l = j + 2 + t
             if (lane > j + 1 && lane < m) cp[lane - j - 2] = make_double2(l0, l1);
-            if (live && !(a.diag_skip & 16)) {
+            if (live) {
                 if (lane >= j) Lj[0] = l0;
                 if (lane >= j + 1) Lj[m] = l1;
             }
@@ -710,7 +710,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         d = bad ? 1e-300 : d;
         const double inv = rsqrt_nr(d), ljj = d * inv;
         const double lij = lane == j ? ljj : row[0] * inv;   // L[i, j]
-        if (live && lane >= j && !(a.diag_skip & 16)) *Lj = lij;
+        if (live && lane >= j) *Lj = lij;
         Lj += m;
         // forward step: y_j = w_j / L_jj, w_i -= L_ij y_j
         const double yj = readlane_d(wi, j) * inv;
@@ -740,7 +740,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         if (t0 < r) {
 #pragma unroll
             for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
-                if (live && lane >= k && t <= lane - k && !(a.diag_skip & 16)) stc<COH>(Us + pk(lane - k, t, r), row[t]);
+                if (live && lane >= k && t <= lane - k) stc<COH>(Us + pk(lane - k, t, r), row[t]);
         }
     }
     if (live) {
