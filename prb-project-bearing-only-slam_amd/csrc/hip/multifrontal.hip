@@ -791,10 +791,11 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         double tj = 0.0;
         if (own)
             for (int i = 0; i < r; ++i) tj += Lw[k + i + lane * m] * xs[i];
-        const double yv = own ? w[lane] : 0.0, djj = own ? Lw[lane + lane * m] : 1.0;
+        // 1 / L_jj by every lane at once, off the sequential chain below
+        const double yv = own ? w[lane] : 0.0, rjj = own ? 1.0 / Lw[lane + lane * m] : 1.0;
         double xv = 0.0;
         for (int j = k - 1; j >= 0; --j) {
-            const double xj = readlane_d((yv - tj) / djj, j);
+            const double xj = readlane_d((yv - tj) * rjj, j);
             if (lane == j) xv = xj;
             else if (lane < j) tj += Lw[j + lane * m] * xj;
         }
