@@ -865,7 +865,7 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
 // SIMD spilled too (all measured slower); 2 waves per SIMD (no spills) measured faster than 3 (a
 // few spilled registers). Fronts of the flow range are <= kFlowMaxM (mf_create picks the range
 // accordingly).
-constexpr int kFlowMaxM = 48;
+constexpr int kFlowMaxM = kMfFlowMaxM;
 
 __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f) {
     __shared__ __attribute__((aligned(16))) double F[kFlowMaxM * (kFlowMaxM + 1) / 2];

@@ -128,6 +128,14 @@ SymbCost symbolic(const Graph& g, int NP, const std::vector<int32_t>& pos, const
     return c;
 }
 
+// Separator balance of nested_dissection (percent of a part's nodes each side must keep): set per
+// plan attempt by build_plan, BOS_ND_MINPCT overrides (diagnostics).
+thread_local int t_nd_minpct = 40;
+int nd_minpct() {
+    static const int env = [] { const char* e = std::getenv("BOS_ND_MINPCT"); return e ? std::atoi(e) : 0; }();
+    return env > 0 ? env : t_nd_minpct;
+}
+
 // Nested dissection with BFS level-structure vertex separators (graph-based, no coordinates).
 void nested_dissection(const Graph& g, const std::vector<char>& active, std::vector<int32_t>& order, int leaf,
                        std::vector<std::pair<int32_t, int32_t>>* blocks) {
@@ -225,7 +233,7 @@ void nested_dissection(const Graph& g, const std::vector<char>& active, std::vec
         // balanced splits keep the assembly tree shallow (its depth is the solver's critical path):
         // each side must hold >= minpct % of the nodes (40: 17 levels at config 3 instead of 27
         // with 20, for 6 % more flops); BOS_ND_MINPCT overrides (diagnostics)
-        static const int minpct = [] { const char* e = std::getenv("BOS_ND_MINPCT"); return e ? std::atoi(e) : 40; }();
+        const int minpct = nd_minpct();
         for (int k = 1; k + 1 < h; ++k) {
             const int64_t below = cum[k - 1], above = tot - cum[k];
             if (below * 100 < tot * minpct || above * 100 < tot * minpct) continue;
@@ -386,7 +394,7 @@ int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& i
 int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
                        const std::vector<std::pair<int32_t, int32_t>>& blocks, int n_fold_cand, std::string& err);
 
-int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& P, std::string& err) {
+int build_plan_once(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& P, std::string& err) {
     const bool want_factor = factor_mode == kFactorScalar;
     const int NP = pi.NP, NL = pi.NL, n_nodes = NP + NL;
     if (NP <= 0) { err = "no poses"; return BOS_ERR_INVALID; }
@@ -501,6 +509,36 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     const int n_fold_cand = factor_mode == kFactorSchur ? NL : 0;
     if (multifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, n_fold_cand, err))) return rc;
     return validate_plan(pi, P, err);
+}
+
+// The Schur ordering's tree is cut at balanced separators (>= 40 % of a part on each side: few
+// levels); some graphs then get a front the fast kernels do not take (m > 64 anywhere, or m > 48
+// from level 2 up, where the dataflow launch starts), which costs far more than the balance buys.
+// Such plans are rebuilt with other balances; the first plan without those fronts is kept (the
+// first attempt's plan if none is).
+bool schur_fronts_fit(const Multifrontal& F) {
+    for (int l = 0; l < F.nlevels; ++l)
+        for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
+            const int m = F.k[F.level[q]] + F.r[F.level[q]];
+            if (m > kMfWaveMaxM || (l >= 2 && m > kMfFlowMaxM)) return false;
+        }
+    return true;
+}
+
+int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& P, std::string& err) {
+    if (factor_mode != kFactorSchur) return build_plan_once(pi, rank, world, factor_mode, P, err);
+    const int tries[] = {40, 35, 45, 30, 20};
+    Plan first;
+    for (int i = 0; i < 5; ++i) {
+        t_nd_minpct = tries[i];
+        const int rc = build_plan_once(pi, rank, world, factor_mode, P, err);
+        if (rc) { t_nd_minpct = 40; return rc; }
+        if (schur_fronts_fit(P.mf) || std::getenv("BOS_ND_MINPCT")) break;
+        if (i == 0) first = P;
+        if (i == 4) P = std::move(first);
+    }
+    t_nd_minpct = 40;
+    return BOS_OK;
 }
 
 void exchange_segments(const Plan& P, int rank, std::vector<ExchangeSeg>& pack, std::vector<ExchangeSeg>& unpack,

@@ -97,6 +97,7 @@ struct OrderingReport {
 //  - update matrices U are packed lower-triangular column-major (r (r + 1) / 2 values) for all.
 //  - L panels are m x k column-major (entries above the diagonal unused).
 constexpr int kMfWaveMaxM = 64;
+constexpr int kMfFlowMaxM = 48;   // fronts of the dataflow factor launch (hip/multifrontal.hip kFlowMaxM)
 constexpr int kFoldChunk = 64;   // folded rows per chunk (one per lane)
 constexpr int kFoldRec = 8;      // ints per folded row
 // landmarks per fold chunk for a parent front of size m: the device forms the chunk's
