@@ -198,6 +198,15 @@ def test_plan_exchange_covers_every_rank(world, which):
     bos.plan_exchange_selftest(P, world)
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_schur_plan_fronts_fit_the_wave_kernels(seed):
+    """The Schur plan retries other separator balances until no front exceeds one wavefront's
+    rows (m <= 64): the default 40 % leaves a 66-row front on some of these worlds."""
+    P = bos.synthetic(30000, 60000, 10, seed=seed)
+    info = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR)
+    assert info["mf_max_front"] <= 64
+
+
 def test_parallel_g2o_parser_equals_line_parser(tmp_path, monkeypatch):
     """The chunked parallel g2o parser (default) and the line-by-line one give identical problems,
     on the reference dataset and on a written synthetic world large enough to use several chunks."""
