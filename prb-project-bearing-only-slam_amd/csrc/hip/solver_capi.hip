@@ -398,7 +398,7 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     if (!sync) return BOS_OK;
     if ((rc = read_stats(s, st))) return rc;
     if (st) {
-        st->t_linearize_ms = elapsed(s->ev[0], s->ev[2]);
+        st->t_linearize_ms = elapsed(s->ev[0], s->ev[1]);
         st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
         st->t_solve_ms = elapsed(s->ev[2], s->ev[3]);
         st->t_update_ms = elapsed(s->ev[3], s->ev[4]);
@@ -790,7 +790,7 @@ int bos_linearize(bos_solver* s, bos_step_stats* st) {
     if ((rc = enqueue_stats(s, false))) return rc;
     if ((rc = read_stats(s, st))) return rc;
     if (st) {
-        st->t_linearize_ms = elapsed(s->ev[0], s->ev[2]);
+        st->t_linearize_ms = elapsed(s->ev[0], s->ev[1]);
         st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
     }
     return BOS_OK;
