@@ -27,6 +27,12 @@ import numpy as np  # noqa: E402
 
 import bos  # noqa: E402
 
+# libbos.so (and the system ROCm 7.2 libraries it links: HIP runtime, rocBLAS/rocSOLVER, RCCL) is
+# loaded before torch, exactly as in the test suite (tests/conftest.py): whichever copy of those
+# sonames loads first serves the process, so the benchmarked binary runs on the runtime the parity
+# tests validated, not on torch's bundled copies.
+bos.lib()
+
 METRIC = "GN iterations/sec + observations/sec (J+H build) at 1/2/4/8 GPUs vs CPU"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, HBM3E peak (spec)
 CONFIG3 = dict(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
@@ -36,10 +42,36 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(P, precision, budget_s=12.0):
+def host_cpus():
+    """CPUs this process may use (affinity mask, capped by a cgroup CPU quota when one is set), the
+    machine's logical CPU count and the CPU model (lscpu), for the CPU baselines' record."""
+    n_aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(n_aff, quota) if quota else n_aff
+    model = ""
+    try:
+        import subprocess
+        for ln in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if ln.startswith("Model name:"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"usable": usable, "nproc": os.cpu_count(), "affinity": n_aff, "cgroup_quota_cpus": quota,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": model}
+
+
+def cpu_baseline(P, precision, cpus, budget_s=12.0):
     """The oracle's J+H build on this host (bounded sample): the reference-order accumulation on one
-    thread and the owner-computes parallel form (oracle linearize(owner=True)) on all threads; the
-    faster one is the baseline."""
+    thread and the owner-computes parallel form (oracle linearize(owner=True)) on every usable CPU;
+    the faster one is the baseline."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
@@ -48,8 +80,9 @@ def cpu_baseline(P, precision, budget_s=12.0):
     prec = 32 if precision == bos.BOS_FP32 else 64
     nobs = len(P.b_z) + len(P.o_z)
     best = None
-    threads_all = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    threads_all = cpus["usable"]
     O.owner_index(Q)   # built once, like the GPU plan
+    forms = {}
     for th, owner in sorted({(1, False), (threads_all, True)}):
         O.linearize(Q, precision=prec, threads=th, owner=owner)   # warm-up
         t0 = time.perf_counter()
@@ -60,16 +93,18 @@ def cpu_baseline(P, precision, budget_s=12.0):
         dt = (time.perf_counter() - t0) / n
         rate = nobs / dt
         form = "owner-computes" if owner else "reference order"
+        forms[f"{form}, {th} threads"] = rate
         log(f"cpu oracle J+H {form} threads={th}: {dt * 1e3:.1f} ms/step, {rate / 1e6:.2f} Mobs/s ({n} steps)")
         if best is None or rate > best[0]:
             best = (rate, th, n, form)
     return {"value": best[0], "unit": "obs/s", "cores": best[1], "kind": "port",
             "sample": f"{best[2]} full J+H builds of config 3 ({nobs} obs each, {prec}-bit) by the C++ oracle "
                       f"({best[3]}), ~{budget_s / 2:.0f} s per form; best of 1 thread (reference order) and "
-                      f"{threads_all} threads (owner-computes)"}
+                      f"{threads_all} threads (owner-computes)",
+            "forms_obs_per_s": forms, "host": cpus}
 
 
-def cpu_gn_baseline(P, budget_s=10.0):
+def cpu_gn_baseline(P, cpus, budget_s=10.0):
     """Full CPU GN steps (oracle J+H + SciPy sparse solve + box-plus), bounded sample."""
     import oracle as O
     from helpers import to_oracle
@@ -78,28 +113,31 @@ def cpu_gn_baseline(P, budget_s=10.0):
     t0 = time.perf_counter()
     n = 0
     while time.perf_counter() - t0 < budget_s or n == 0:
-        O.step(Q, p, l, threads=1)
+        O.step(Q, p, l, threads=cpus["usable"])
         n += 1
     dt = (time.perf_counter() - t0) / n
-    return {"value": 1.0 / dt, "unit": "it/s", "cores": 1, "kind": "port",
-            "sample": f"{n} GN iterations of config 3 (oracle J+H fp64 + scipy spsolve + box-plus)"}
+    return {"value": 1.0 / dt, "unit": "it/s", "cores": cpus["usable"], "kind": "port",
+            "sample": f"{n} GN iterations of config 3 (oracle J+H fp64 on {cpus['usable']} threads + SciPy SuperLU "
+                      f"spsolve, single-threaded + box-plus)", "host": cpus}
 
 
-PROFILE_TAG = "r01"   # profiles/<tag>_pmc_linearize_<prec>.json, written by tools/pmc_summary.py
+PROFILE_TAG = "r02"   # profiles/<tag>_pmc_linearize_<prec>.json, written by tools/pmc_summary.py
 
 
 def traffic_from_profile(precision):
-    """HBM bytes per launch of the J+H kernel from the committed rocprofv3 PMC summary
-    (L2<->fabric requests by size, tools/gpu_profile.sh)."""
-    name = f"{PROFILE_TAG}_pmc_linearize_" + ("fp32" if precision == bos.BOS_FP32 else "fp64") + ".json"
-    path = os.path.join(ROOT, "profiles", name)
-    if not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            return float(json.load(f)["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+    """Fabric bytes per launch of the J+H kernel from the committed rocprofv3 PMC summaries
+    (L2 <-> fabric requests by size, tools/gpu_profile.sh): {"warm": ..., "cold": ...}."""
+    out = {}
+    for label in ("warm", "cold"):
+        name = f"{PROFILE_TAG}_pmc_linearize_" + ("fp32" if precision == bos.BOS_FP32 else "fp64") + \
+            ("_cold" if label == "cold" else "") + ".json"
+        path = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(path) as f:
+                out[label] = float(json.load(f)["hbm_bytes_per_launch"])
+        except (OSError, ValueError, KeyError):
+            out[label] = None
+    return out
 
 
 def main():
@@ -109,6 +147,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--gn-steps", type=int, default=10)
+    ap.add_argument("--cold-steps", type=int, default=20, help="J+H builds timed from cold caches (in-step roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gn-other", action="store_true", help="skip timing the other solver ordering")
     ap.add_argument("--tri-steps", type=int, default=20, help="device triangulations timed (0: skip)")
@@ -122,11 +161,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    import torch
-    import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
+    # torch only for the rendezvous (gloo, host memory): the GPU work and its timing go through
+    # libbos.so (HIP events on the handle's stream), and the exchange runs on RCCL inside it
+    dist = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
     precision = bos.BOS_FP32 if args.precision == "fp32" else bos.BOS_FP64
 
     t_gen = time.perf_counter()
@@ -140,14 +181,10 @@ def main():
         obj = [bos.nccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         nccl_id = obj[0]
-    # a dedicated (non-null) stream: the handle launches every kernel on it, and the timing
-    # events below are recorded on the same stream
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
     t_create = time.perf_counter()
     solver = bos.BOS_SOLVER_SCHUR if args.solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
-    S = bos.Solver(P, precision=precision, solver=solver, device=local_rank, stream=stream.cuda_stream, rank=rank,
-                   world_size=world, nccl_id=nccl_id)
+    S = bos.Solver(P, precision=precision, solver=solver, device=local_rank, rank=rank, world_size=world,
+                   nccl_id=nccl_id)
     info = S.system_info()
     log(f"rank {rank}: bos_create {time.perf_counter() - t_create:.1f} s, n={info['n']} "
         f"nnz(H lower)={info['nnz_lower']} nnz(L)={info['nnz_factor']}")
@@ -156,44 +193,37 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # ---- J+H build throughput
-    for _ in range(args.warmup):
-        S.linearize_async()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        S.linearize_async()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        t = torch.tensor([wall], device="cuda", dtype=torch.float64)
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+        return float(t.item())
+
+    # ---- J+H build throughput: K builds back to back (the timed region), warm caches
+    S.time_linearize(args.warmup)
+    S.synchronize()
+    barrier()
+    S.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = S.time_linearize(args.steps)   # synchronises the handle's stream
+    barrier()
+    wall = max_over_ranks(time.perf_counter() - t0)
     ms_per_step = wall / args.steps * 1e3
     value = nobs * args.steps / wall
+    # ---- the same build from cold caches (1 GiB read before each): what it costs inside a GN
+    # iteration, where the solver's factor streams between two builds
+    cold_ms = S.time_linearize(args.cold_steps, flush_caches=True) if args.cold_steps > 0 else None
 
     # ---- full GN iterations (J+H + exchange + solve + update)
     def time_gn(solver_handle):
         solver_handle.step()   # first iteration includes the one-time factorization analysis
         barrier()
-        torch.cuda.synchronize()
         tg = time.perf_counter()
         stats = [solver_handle.step() for _ in range(args.gn_steps)]
         barrier()
-        gn_wall = time.perf_counter() - tg
-        if world > 1:
-            t = torch.tensor([gn_wall], device="cuda", dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            gn_wall = float(t.item())
+        gn_wall = max_over_ranks(time.perf_counter() - tg)
+        assert all(g["solver_info"] == 0 for g in stats), "non-positive pivot in a benchmarked GN step"
         ph = {k: float(np.median([g[k] for g in stats])) for k in
               ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
         return args.gn_steps / gn_wall, ph
@@ -203,7 +233,7 @@ def main():
         gn_it_s, phase = time_gn(S)
         if world == 1 and not args.no_gn_other:   # the other multifrontal ordering, for comparison
             other = "supernodal" if args.solver == "schur" else "schur"
-            S2 = bos.Solver(P, precision=precision, device=local_rank, stream=stream.cuda_stream,
+            S2 = bos.Solver(P, precision=precision, device=local_rank,
                             solver=bos.BOS_SOLVER_SUPERNODAL if other == "supernodal" else bos.BOS_SOLVER_SCHUR)
             it2, ph2 = time_gn(S2)
             gn_other = {"solver": other, "gn_iters_per_s": it2, "t_solve_ms": ph2["t_solve_ms"]}
@@ -214,15 +244,7 @@ def main():
     tri = None
     if world == 1 and args.tri_steps > 0:
         S.triangulate()
-        torch.cuda.synchronize()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(args.tri_steps):
-            S.triangulate_async()
-        e1.record(stream)
-        torch.cuda.synchronize()
-        tri_ms = e0.elapsed_time(e1) / args.tri_steps
+        tri_ms = S.time_triangulate(args.tri_steps)
         tri = {"landmarks": P.NL, "bearings": int(len(P.b_z)), "ms": tri_ms, "landmarks_per_s": P.NL / (tri_ms * 1e-3)}
         if not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -236,8 +258,13 @@ def main():
 
     if rank == 0:
         algo = info["algorithmic_bytes"]
-        achieved = algo / (kernel_ms * 1e-3) / 1e9
         traffic = traffic_from_profile(precision) if world == 1 else None
+
+        def roof(ms, label):
+            a = algo / (ms * 1e-3) / 1e9
+            return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
+                    "traffic": traffic.get(label) if traffic else None, "algorithmic_bytes_per_launch": algo,
+                    "kernel_ms": ms, "caches": label}
         line = {
             "metric": METRIC,
             "value": value,
@@ -263,20 +290,15 @@ def main():
             "gn_solver": args.solver,
             "gn_other": gn_other,
             "triangulation": tri,
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": algo,
-                "kernel_ms": kernel_ms,
-            },
+            # in-step figure (inputs from HBM, as inside a GN iteration) first; the back-to-back
+            # replay (working set partly served by the Infinity Cache) second
+            "roofline": roof(cold_ms, "cold") if cold_ms else roof(kernel_ms, "warm"),
+            "roofline_warm_replay": roof(kernel_ms, "warm"),
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(P, precision)
-            line["cpu_baseline_gn"] = cpu_gn_baseline(P)
+            cpus = host_cpus()
+            line["cpu_baseline"] = cpu_baseline(P, precision, cpus)
+            line["cpu_baseline_gn"] = cpu_gn_baseline(P, cpus)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
             if gn_it_s:
                 line["gn_speedup_vs_cpu"] = gn_it_s / line["cpu_baseline_gn"]["value"]

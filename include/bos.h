@@ -91,9 +91,11 @@ typedef struct bos_options {
 typedef struct bos_step_stats {
     double chi2;                    /* sum e^T Omega e over all edges before the robust kernel   */
     int32_t n_robust;               /* observations scaled by the robust kernel                  */
-    int32_t solver_info;            /* 0 ok, >0 factorization reported a non-SPD pivot           */
-    double max_abs_dx;              /* max |dx| of the applied update                            */
-    double t_linearize_ms;          /* J+H build (incl. exchange when sharded), hipEvent timed   */
+    int32_t solver_info;            /* 0 ok, >0 number of non-positive pivots the factorization met
+                                       (reported and continued, like the reference's NumericalIssue
+                                       message, slam/solver.cpp:82-84)                            */
+    double max_abs_dx;              /* max |dx| of the applied update (NaN if the update was not finite) */
+    double t_linearize_ms;          /* J+H build only (the exchange is t_exchange_ms), hipEvent timed */
     double t_exchange_ms;           /* RCCL exchange part (0 on one GPU)                         */
     double t_solve_ms;              /* factorization + triangular solves                         */
     double t_update_ms;             /* box-plus                                                  */
@@ -127,7 +129,10 @@ int bos_destroy(struct bos_solver* s);
 /* Solver::set_kernel_threshold / set_damping_factor (slam/solver.hpp:33-34) */
 int bos_set_kernel_threshold(struct bos_solver* s, double kt);
 int bos_set_damping_factor(struct bos_solver* s, double df);
-/* Solver::step (slam/solver.hpp:36, slam/solver.cpp:27-97): one synchronous GN iteration */
+/* Solver::step (slam/solver.hpp:36, slam/solver.cpp:27-97): one synchronous GN iteration.
+ * BOS_ERR_SOLVER (state untouched by the failed iteration) if the GPU factorization could not
+ * complete (a dataflow dependency wait timed out); a non-positive pivot is only reported in
+ * stats->solver_info, as the reference reports and continues. */
 int bos_step(struct bos_solver* s, bos_step_stats* stats);
 /* bos_step repeated n times with one host synchronisation at the end (UI batch of 50,
  * executables/bearing_only_slam.cpp:95-98); stats of the last iteration */

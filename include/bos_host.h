@@ -52,6 +52,9 @@ typedef struct bos_plan_info {
     int64_t mf_max_front;
     double mf_flops;
     int64_t mf_update_bytes;
+    int64_t mf_fits;                /* Schur: every front fits the fast kernels (m <= 64, m <= 48 from level 2 up) */
+    int64_t mf_max_front_upper;     /* Schur: largest front from tree level 2 up                  */
+    int64_t mf_balance_pct;         /* Schur: separator balance of the plan kept (40 = first try)   */
 } bos_plan_info;
 
 /* Build the static plan on the host (what bos_create does before touching the GPU) for solver
@@ -73,6 +76,24 @@ int bos_plan_mf_selftest(const bos_problem* problem, int32_t solver, const doubl
  * simulated on the host for all `world` ranks; BOS_OK when every rank ends with every value the
  * solver reads and every b entry but the fixed pose's. */
 int bos_plan_exchange_selftest(const bos_problem* problem, int32_t world);
+
+/* Benchmark helpers (bench.py; HIP events on the handle's stream, no torch):
+ * bos_time_linearize: n J+H builds (+ the exchange when sharded). flush_caches = 0: back to back,
+ * the average per build; flush_caches = 1: 1 GiB is read before each build so its inputs come from
+ * HBM (as inside a GN step), each build timed alone (J+H only).
+ * bos_time_triangulate: n device triangulations back to back (re-estimates the landmarks). */
+int bos_time_linearize(struct bos_solver* s, int32_t n, int32_t flush_caches, double* ms_per_build);
+int bos_time_triangulate(struct bos_solver* s, int32_t n, double* ms_per_call);
+
+/* Test hooks (process-wide, default 0 = product behaviour; not part of the drop-in boundary):
+ * poses per nested-dissection leaf of the Schur ordering (forces the plan fallback when large),
+ * and the line-by-line g2o parser instead of the chunked one (the tests prove them identical). */
+void bos_debug_set_schur_leaf(int32_t poses);
+void bos_debug_set_g2o_parser(int32_t line_by_line);
+/* Test hook: the next bos_step's factor dataflow launch skips its first front, so a dependency
+ * wait times out — bos_step must then fail with BOS_ERR_SOLVER and leave the state untouched.
+ * BOS_ERR_UNSUPPORTED when the handle's solver has no dataflow launch. */
+int bos_debug_inject_stall(struct bos_solver* s);
 
 /* Diagnostics: one J+H launch with per-wave timeline stamps, 8 x uint64 per wave: block, wave in
  * block, kind (0 pose lanes / 1 landmark lanes), t_start, t_loop, t_loop_end, t_end (realtime clock,

@@ -239,6 +239,13 @@ int linearize(const ProblemView<T>& P, double kernel_threshold, double damping, 
                 for (int i = 0; i < 3; ++i) { e[i] *= sc; Oe[i] *= sc; }
                 ++lrob;
             }
+            if (is == id) {
+                // self-loop: the source and destination triplets share columns and setFromTriplets
+                // sums them (solver_jacobians.cpp:126-165): J = J_s + J_d = 0 exactly (the two blocks
+                // are exact negations), so H and b receive nothing (solver.cpp:60-61)
+                for (int i = 0; i < 9; ++i) hoff[9 * (size_t)k + i] = 0.0;
+                continue;
+            }
             // OJ = Omega * J (3x6)
             T OJ[18];
             for (int i = 0; i < 3; ++i)
@@ -353,6 +360,14 @@ int linearize_owner(const ProblemView<T>& P, const int32_t* pb_ptr, const int32_
             if (rho > kt) {
                 const T sc = std::sqrt(kt / rho);
                 for (int i = 0; i < 3; ++i) Oe[i] *= sc;
+            }
+            if (is == id) {   // self-loop: J = J_s + J_d = 0 (see linearize), chi^2 only
+                if (!dst) {
+                    chi2 += (double)rho;
+                    if (rho > kt) ++nr;
+                    for (int i = 0; i < 9; ++i) hoff[9 * (size_t)k + i] = 0.0;
+                }
+                continue;
             }
             const int c0 = dst ? 3 : 0;   // this pose's columns of J
             T OJ[18];

@@ -41,6 +41,8 @@ EXPORTED_SYMBOLS = [
     "bos_dataset_landmark_ids", "bos_dataset_fixed_pose_id", "bos_dataset_bound", "bos_dataset_ground_truth",
     "bos_dataset_write_g2o", "bos_dataset_free", "bos_plan_inspect", "bos_plan_mf_selftest",
     "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async", "bos_plan_exchange_selftest",
+    "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall",
+    "bos_time_linearize", "bos_time_triangulate",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -88,7 +90,8 @@ class bos_plan_info(ctypes.Structure):
                 ("flops_temporal", ctypes.c_double), ("flops_nested_dissection", ctypes.c_double),
                 ("ordering", ctypes.c_char * 32), ("mf_supernodes", ctypes.c_int64),
                 ("mf_levels", ctypes.c_int64), ("mf_max_front", ctypes.c_int64), ("mf_flops", ctypes.c_double),
-                ("mf_update_bytes", ctypes.c_int64)]
+                ("mf_update_bytes", ctypes.c_int64), ("mf_fits", ctypes.c_int64),
+                ("mf_max_front_upper", ctypes.c_int64), ("mf_balance_pct", ctypes.c_int64)]
 
 
 _lib = None
@@ -143,6 +146,11 @@ def lib():
                                             ctypes.POINTER(ctypes.c_uint8), _ip, ctypes.POINTER(bos_plan_info)]),
         "bos_plan_mf_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, _dp, _dp, _dp]),
         "bos_plan_exchange_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32]),
+        "bos_debug_set_schur_leaf": (None, [ctypes.c_int32]),
+        "bos_debug_set_g2o_parser": (None, [ctypes.c_int32]),
+        "bos_debug_inject_stall": (ctypes.c_int, [vp]),
+        "bos_time_linearize": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, _dp]),
+        "bos_time_triangulate": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -294,7 +302,8 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
            "flops_temporal": info.flops_temporal, "flops_nested_dissection": info.flops_nested_dissection,
            "ordering": info.ordering.decode(), "mf_supernodes": info.mf_supernodes,
            "mf_levels": info.mf_levels, "mf_max_front": info.mf_max_front, "mf_flops": info.mf_flops,
-           "mf_update_bytes": info.mf_update_bytes}
+           "mf_update_bytes": info.mf_update_bytes, "mf_fits": bool(info.mf_fits),
+           "mf_max_front_upper": info.mf_max_front_upper, "mf_balance_pct": info.mf_balance_pct}
     if entries:
         nnz = info.nnz_lower
         rows = np.zeros(nnz, dtype=np.int32)
@@ -406,6 +415,22 @@ class Solver:
         _check(lib().bos_debug_linearize_timeline(self._h, n.value, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                                                   ctypes.byref(n)), "timeline")
         return out
+
+    def debug_inject_stall(self):
+        """Test hook: the next step's factor dataflow launch skips its first front (a stalled
+        dependency); that step must fail with BOS_ERR_SOLVER and leave the state unchanged."""
+        _check(lib().bos_debug_inject_stall(self._h), "bos_debug_inject_stall")
+
+    def time_linearize(self, n: int, flush_caches: bool = False) -> float:
+        """ms per J+H build (HIP events on the handle's stream, see bos_time_linearize)."""
+        ms = ctypes.c_double(0)
+        _check(lib().bos_time_linearize(self._h, n, int(flush_caches), ctypes.byref(ms)), "bos_time_linearize")
+        return ms.value
+
+    def time_triangulate(self, n: int) -> float:
+        ms = ctypes.c_double(0)
+        _check(lib().bos_time_triangulate(self._h, n, ctypes.byref(ms)), "bos_time_triangulate")
+        return ms.value
 
     def triangulate(self):
         """triangulate_landmarks on the device from the current poses (slam/triangulation.cpp:65-74)."""

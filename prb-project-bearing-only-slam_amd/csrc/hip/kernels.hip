@@ -126,7 +126,8 @@ template <typename T> __device__ __forceinline__ void odo_fetch_data(const LinPa
 
 // One odometry entry of pose p (pose state X, th): the entry's edge seen from p's side. Both sides
 // add H_ss = H_dd to the pose's diagonal block; b gets +b_s (source) or -b_s (destination); the
-// source side counts chi^2 and stores H_sd = -H_ss. Source and destination are chosen by selects,
+// source side counts chi^2; the lower pose of the pair adds H_sd = -H_ss to the pair's block (edges
+// in both directions between two poses share it). Source and destination are chosen by selects,
 // so lanes on different sides of their edges run one instruction stream.
 template <typename T, bool HAS_DUPS>
 __device__ __forceinline__ void odometry_entry(const LinParams<T>& P, int x, int x1, const OdoIn<T>& o, const V4<T>& X,
@@ -140,9 +141,11 @@ __device__ __forceinline__ void odometry_entry(const LinParams<T>& P, int x, int
     for (int v = 0; v < 6; ++v) h[v] += he[v];
 #pragma unroll
     for (int v = 0; v < 3; ++v) gb[v] += dst_side ? -ge[v] : ge[v];   // a + (-b) == a - b exactly
-    if (dst_side) return;
-    chi += (double)rho;
-    if (rho > P.kt) ++nrob;
+    if (!dst_side) {
+        chi += (double)rho;
+        if (rho > P.kt) ++nrob;
+    }
+    if (o.blk < 0) return;
     T* ob = P.hval + P.off_pp + 6 * o.blk;
     if (HAS_DUPS) {
 #pragma unroll
@@ -209,7 +212,7 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
         const V4<T> X = load4(P.pc + 4 * p);
         const int n = P.pl_cnt[g];
         const int sl = P.pw_base[g >> 6] + t;   // slot of item j: + 64 j
-        const bool odo = sub == 0 && !(P.diag_skip & 4);
+        const bool odo = sub == 0;
         int x0 = 0, x1 = 0;
         T th = (T)0;
         if (odo) { x0 = P.po_ptr[p]; x1 = P.po_ptr[p + 1]; th = P.pth[p]; }
@@ -347,9 +350,6 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int blk, un
     bl[0] = gl[0]; bl[1] = gl[1];
 }
 
-// Pose and landmark blocks interleaved in proportion over the grid (pose block i sits at the
-// b with floor(b Pb / T) == i < floor((b + 1) Pb / T)), so every CU gets its share of the longer
-// pose lists.
 // XCD-aware block order: blocks b and b + 8 share an XCD (and its L2), so a segment [s0, s1) of
 // the grid is renumbered to give each XCD a contiguous run of it; the pose (landmark) blocks an
 // XCD runs then cover a stretch of the trajectory, and the landmark (pose) cache lines their
@@ -362,28 +362,17 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t s0, int64_t
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams<T> P) {
     const int64_t nb = gridDim.x;
-    int64_t b = blockIdx.x;
-    if (P.xcd_remap && !P.interleave)
-        b = b < P.pose_blocks ? xcd_contiguous(b, 0, P.pose_blocks) : xcd_contiguous(b, P.pose_blocks, nb);
-    int pb0, pb1;
-    if (P.interleave) {
-        pb0 = (int)(b * P.pose_blocks / nb);
-        pb1 = (int)((b + 1) * P.pose_blocks / nb);
-    } else {   // pose blocks first
-        pb0 = (int)min(b, (int64_t)P.pose_blocks);
-        pb1 = (int)min(b + 1, (int64_t)P.pose_blocks);
-    }
+    // pose blocks first, then landmark blocks, each range in XCD-contiguous order
+    const int64_t b = blockIdx.x < P.pose_blocks ? xcd_contiguous(blockIdx.x, 0, P.pose_blocks)
+                                                 : xcd_contiguous(blockIdx.x, P.pose_blocks, nb);
     unsigned long long st[3] = {0, 0, 0};
     stamp(P.diag_stamps, st, 0);
-    if (pb1 == pb0) {   // block-uniform branch
-        // lm_rep landmark-lane blocks per block (so the launch fits the resident wave slots)
-        const int lb0 = ((int)b - pb0) * P.lm_rep;
-        if (!(P.diag_skip & 1))
-            for (int r = 0; r < P.lm_rep; ++r) landmark_lane<T, HAS_W>(P, lb0 + r, st);
+    if (b >= P.pose_blocks) {   // block-uniform branch
+        landmark_lane<T, HAS_W>(P, (int)(b - P.pose_blocks), st);
         stamp_flush(P.diag_stamps, st, 1);
         return;
     }
-    if (P.diag_skip & 2) return;
+    const int pb0 = (int)b;
     double chi = 0.0;
     int nrob = 0;
     pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, pb0, chi, nrob, st);
@@ -404,10 +393,19 @@ __global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams
     }
 }
 
-// State::apply_boxplus (framework/state.cpp:69-80): dx = -x (the solve ran on +b)
+// max that propagates NaN (fmax returns the non-NaN operand): a non-finite update must not read
+// as convergence
+__device__ __forceinline__ double nan_max(double a, double b) { return (a != a || b != b) ? a + b : fmax(a, b); }
+
+// State::apply_boxplus (framework/state.cpp:69-80): dx = -x (the solve ran on +b). Skipped (state
+// untouched) when the solver reports an aborted factorization.
 template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_kernel(const UpdateParams<T> U) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     double m = 0.0;
+    if (U.info && (*U.info & kStepAbort)) {
+        if (threadIdx.x == 0) U.max_part[blockIdx.x] = 0.0;
+        return;
+    }
     if (i < U.NP) {
         if (i != U.fixed) {
             const int d = U.node_dof[i];
@@ -422,7 +420,7 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
             U.pc[4 * i + 2] = cos((T)th);
             U.pc[4 * i + 3] = sin((T)th);
             U.pth[i] = (T)th;
-            m = fmax(fabs(dx), fmax(fabs(dy), fabs(dth)));
+            m = nan_max(fabs(dx), nan_max(fabs(dy), fabs(dth)));
         }
     } else if (i < U.NP + U.NL) {
         const int j = i - U.NP;
@@ -433,28 +431,25 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
         U.lm[2 * j + 1] = y;
         U.lc[2 * j] = (T)x;
         U.lc[2 * j + 1] = (T)y;
-        m = fmax(fabs(dx), fabs(dy));
+        m = nan_max(fabs(dx), fabs(dy));
     }
     // block max into its partial slot (max is order independent: deterministic; no atomics, which
     // would serialize on one address)
-    m = fmax(m, __shfl_xor(m, 32));
-    m = fmax(m, __shfl_xor(m, 16));
-    m = fmax(m, __shfl_xor(m, 8));
-    m = fmax(m, __shfl_xor(m, 4));
-    m = fmax(m, __shfl_xor(m, 2));
-    m = fmax(m, __shfl_xor(m, 1));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o));
     __shared__ double sm[kUpdateBlock / 64];
     if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
         double b = sm[0];
-        for (int w = 1; w < kUpdateBlock / 64; ++w) b = fmax(b, sm[w]);
+        for (int w = 1; w < kUpdateBlock / 64; ++w) b = nan_max(b, sm[w]);
         U.max_part[blockIdx.x] = b;
     }
 }
 
-__global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_part, int n, const double* max_part,
-                                    int n_max, int32_t* info, int32_t* reset, int n_reset, StepStatus* out) {
+__global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
+                                    int32_t nrob_const, const double* max_part, int n_max, int32_t* info,
+                                    int first, StepStatus* out) {
     __shared__ double sc[256];
     __shared__ double sm[256];
     __shared__ long long sr[256];
@@ -462,7 +457,7 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
     long long r = 0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) { c += chi_part[i]; r += nrob_part[i]; }
     if (max_part)
-        for (int i = threadIdx.x; i < n_max; i += blockDim.x) m = fmax(m, max_part[i]);
+        for (int i = threadIdx.x; i < n_max; i += blockDim.x) m = nan_max(m, max_part[i]);
     sc[threadIdx.x] = c;
     sm[threadIdx.x] = m;
     sr[threadIdx.x] = r;
@@ -471,16 +466,17 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
         if ((int)threadIdx.x < o) {
             sc[threadIdx.x] += sc[threadIdx.x + o];
             sr[threadIdx.x] += sr[threadIdx.x + o];
-            sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + o]);
+            sm[threadIdx.x] = nan_max(sm[threadIdx.x], sm[threadIdx.x + o]);
         }
         __syncthreads();
     }
-    if ((int)threadIdx.x < n_reset) reset[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
-        out->chi2 = sc[0];
-        out->n_robust = (int32_t)sr[0];
+        out->chi2 = sc[0] + chi_const;
+        out->n_robust = (int32_t)sr[0] + nrob_const;
         out->max_dx = sm[0];
-        out->info = info ? *info : 0;
+        const int32_t inf = info ? *info : 0;
+        out->info = inf;
+        out->aborted = (first ? 0 : out->aborted) | (inf & kStepAbort);
         if (info) *info = 0;
     }
 }
@@ -576,6 +572,13 @@ __global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* seg
         dst[i] = src[i];
 }
 
+__global__ __launch_bounds__(256) void cache_scrub_kernel(const double* buf, int64_t n, double* sink) {
+    double acc = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        acc += buf[i];
+    if (acc == -1.0) sink[0] = acc;   // never true for the zeroed buffer: keeps the loads alive
+}
+
 template <typename T> __global__ void to_f64_kernel(const T* in, double* out, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = (double)in[i];
@@ -595,19 +598,10 @@ __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colin
 
 }  // namespace
 
-// Landmark-lane blocks per launched block (BOS_JH_LM_REP, default 1). Folding two into one block
-// lets the fp64 grid fit the resident wave slots (4 waves per SIMD), but measured slower on config 3
-// (35 vs 31 us): the kernel is bound by the memory pipeline, not by the second wave generation.
-inline int lm_rep() {
-    static const int r = [] { const char* e = std::getenv("BOS_JH_LM_REP"); return e ? std::max(1, std::atoi(e)) : 1; }();
-    return r;
-}
-
 template <typename T, bool W, bool D, int LPP, int MINW>
 hipError_t launch_lin_k(LinParams<T> p, hipStream_t s) {
     const int lm_blocks = (p.l_end - p.l_begin + kBlock - 1) / kBlock;
-    p.lm_rep = lm_rep();
-    const int grid = p.pose_blocks + (lm_blocks + p.lm_rep - 1) / p.lm_rep;
+    const int grid = p.pose_blocks + lm_blocks;
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((linearize_kernel<T, W, D, LPP, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
     return hipGetLastError();
@@ -623,11 +617,10 @@ hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, hipStream_t s) {
 }
 
 // Minimum waves per SIMD the kernel is compiled for (register budget): 4 (<= 128 VGPRs); 5 (<= 102)
-// makes the fp64 variant spill, measured slower (36 vs 31 us on config 3), BOS_JH_MINWAVES=5.
+// makes the fp64 variant spill, measured slower (36 vs 31 us on config 3).
 template <typename T, bool W, bool D>
 hipError_t launch_lin_w(const LinParams<T>& p, int lpp, hipStream_t s) {
-    static const int minw = [] { const char* e = std::getenv("BOS_JH_MINWAVES"); return e ? std::atoi(e) : 4; }();
-    return minw == 5 ? launch_lin_lpp<T, W, D, 5>(p, lpp, s) : launch_lin_lpp<T, W, D, 4>(p, lpp, s);
+    return launch_lin_lpp<T, W, D, 4>(p, lpp, s);
 }
 
 template <typename T>
@@ -657,11 +650,16 @@ template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipSt
     return hipGetLastError();
 }
 
-hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, const double* max_part,
-                               int n_max, int32_t* info, int32_t* reset, int n_reset, StepStatus* out, hipStream_t s) {
-    if (n_reset > 256) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n, max_part, n_max, info,
-                       reset, n_reset, out);
+hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
+                               int32_t nrob_const, const double* max_part, int n_max, int32_t* info, bool first,
+                               StepStatus* out, hipStream_t s) {
+    hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n, chi_const, nrob_const,
+                       max_part, n_max, info, (int)first, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_cache_scrub(const double* buf, int64_t n, double* sink, hipStream_t s) {
+    hipLaunchKernelGGL(cache_scrub_kernel, dim3(4096), dim3(256), 0, s, buf, n, sink);
     return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ template <typename T> struct LinParams {
     const int32_t* po_ptr;    // [NP + 1]
     const int32_t* po_ent;    // edge << 1 | destination side
     const int32_t* po_oth;    // the other pose of the entry's edge
-    const int32_t* po_blk;    // pose-pose block of a source-side entry
+    const int32_t* po_blk;    // pose-pose block the entry adds to (other pose higher), else -1
     const int32_t* o_src;
     const int32_t* o_dst;
     const T* o_z;             // [M_o][3]
@@ -59,10 +59,6 @@ template <typename T> struct LinParams {
     int32_t* nrob_part;       // [pose_blocks]
     T kt;                     // robust kernel threshold
     T lambda;                 // damping
-    int lm_rep;               // landmark-lane blocks handled per launched block (set by the launcher)
-    int interleave;           // pose and landmark blocks interleaved over the grid (else pose blocks first)
-    int xcd_remap;            // each XCD runs a contiguous run of the pose and of the landmark blocks
-    int diag_skip;            // timing diagnostics only (BOS_JH_DIAG_SKIP): 1 landmark lanes, 2 pose lanes, 4 odometry
     unsigned long long* diag_stamps;   // timeline diagnostics only (8 x u64 per wave), null otherwise
 };
 
@@ -76,14 +72,21 @@ template <typename T> struct UpdateParams {
     T* pth;
     T* lc;
     double* max_part;         // [update blocks] max |dx| of each block (reduced by reduce_stats)
+    const int32_t* info;      // solver status word or null; | kStepAbort => the update is skipped
 };
+
+// Solver status bit: the factorization's results are invalid (a dataflow launch timed out,
+// multifrontal.hpp kMfStall); the box-plus then leaves the state untouched and bos_step fails.
+constexpr int32_t kStepAbort = 1 << 30;
 
 // End-of-iteration summary, read back by the host in one copy.
 struct StepStatus {
     double chi2;
     double max_dx;
     int32_t n_robust;
-    int32_t info;     // solver status (multifrontal: first non-positive pivot + 1, 0 = ok)
+    int32_t info;     // solver status: count of non-positive pivots, | kStepAbort (see above)
+    int32_t aborted;  // kStepAbort if any step since the last reset (first step of a bos_step_n batch) aborted
+    int32_t pad;
 };
 
 constexpr int kUpdateBlock = 256;
@@ -117,12 +120,16 @@ template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s);
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
-// Reduces the J+H kernel's chi^2 / robust-count partials (and the box-plus max |dx| partials when
-// max_part is set) into *out, moves *info into out->info, then zeroes *info and reset[0, n_reset)
-// (the solver's work-queue tickets) for the next iteration: one launch replaces the per-step
-// memsets and read-backs.
-hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, const double* max_part,
-                               int n_max, int32_t* info, int32_t* reset, int n_reset, StepStatus* out, hipStream_t s);
+// Reduces the J+H kernel's chi^2 / robust-count partials (plus the constant terms of odometry
+// self-loops, chi_const / nrob_const) and the box-plus max |dx| partials (when max_part is set; a NaN
+// propagates) into *out, moves *info into out->info and zeroes *info for the next iteration: one
+// launch replaces the per-step memsets and read-backs.
+hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
+                               int32_t nrob_const, const double* max_part, int n_max, int32_t* info, bool first,
+                               StepStatus* out, hipStream_t s);
+// Reads n doubles (all of them: the sum is compared with an impossible value), so L2 and the
+// Infinity Cache hold clean lines of this buffer afterwards (cold-cache timing, bos_time_linearize).
+hipError_t launch_cache_scrub(const double* buf, int64_t n, double* sink, hipStream_t s);
 template <typename T> hipError_t launch_to_f64(const T* in, double* out, int64_t n, hipStream_t s);
 // out[i] = (double)in[idx[i]]
 template <typename T> hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s);

@@ -104,10 +104,6 @@ struct MfArgs {
     const int32_t* fold_cptr;
     const int32_t* fold_chunk;
     const int32_t* fold_rec;
-    unsigned long long* stamps;  // timing diagnostics only (BOS_MF_STAMPS): 8 per supernode, null otherwise
-    int pair;                    // register fronts: two pivots per step (BOS_MF_PAIR=0: one)
-    int diag_skip;               // timing diagnostics only (BOS_MF_DIAG_SKIP): 1 assembly, 2 fold, 4 extend-add
-                                 // (results are then wrong)
 };
 
 // LDS of one wave's fold chunk: the y (forward-step) values of its landmarks, two per landmark
@@ -284,10 +280,6 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-__device__ __forceinline__ void mf_stamp(const MfArgs& a, int s, int k, int lane) {
-    if (a.stamps && lane == 0) a.stamps[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
-}
-
 // 1 / sqrt(d) for d > 0 in the normal range: hardware estimate refined by two Newton steps
 // (quadratic convergence: full double precision, within an ulp or two of 1.0 / sqrt(d)).
 __device__ __forceinline__ double rsqrt_nr(double d) {
@@ -349,9 +341,7 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
     int nn = ch0 + 1 < ch1 ? a.fold_chunk[ch0 + 2] - a.fold_chunk[ch0 + 1] : 0;
     int4 n0 = make_int4(-1, -1, -1, -1), n1 = make_int4(0, 0, 0, 0);
     if (lane < nn) { n0 = fold_rec_load(a, a.fold_chunk[ch0 + 1] + lane, 0); n1 = fold_rec_load(a, a.fold_chunk[ch0 + 1] + lane, 1); }
-    unsigned long long t_rows = 0, t_ext = 0;   // diagnostics (stamps 6, 7): per-row phase, W W^T phase
     for (int ch = ch0; ch < ch1; ++ch) {
-        const unsigned long long tc0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
         const double ht0 = v.ht0, ht1 = v.ht1, a00 = v.a00, a10 = v.a10, a11 = v.a11;
         const int t = r1.z & 63, rc = (r1.z >> 6) & 63, pos = (r1.z >> 12) & 63, lml = (r1.z >> 18) & 63;
         const bool mine = lane < n;
@@ -394,7 +384,6 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
             W[pos * WS + 2 * lml + 1] = lt1;
         }
         wave_sync();
-        const unsigned long long tc1 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
         const int kc = 2 * nl;
         if (lane < m) {   // u-vector part: -(W y) at this lane's position
             double w = 0.0;
@@ -422,13 +411,7 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
         wave_sync();
         n = nn;
         nn = n2;
-        if (a.stamps) {
-            const unsigned long long tc2 = __builtin_amdgcn_s_memrealtime();
-            t_rows += tc1 - tc0;
-            t_ext += tc2 - tc1;
-        }
     }
-    if (a.stamps && lane == 0) { a.stamps[8 * (int64_t)s + 6] = t_rows; a.stamps[8 * (int64_t)s + 7] = t_ext; }
 }
 
 // The front before its assembly: every lower entry of F and of wv set to minus the folded
@@ -460,18 +443,26 @@ __device__ __forceinline__ void fold_store(const FoldAcc<MAXM>& acc, double* F, 
 // processes the front and publishes its flag. Hand-off data goes through coherent (sc1) accesses
 // (ldc / stc), drained by s_waitcnt before the flag store: no L2 writeback / invalidate per front.
 // A wave only ever waits for tickets already taken by running waves, so any grid size is
-// deadlock-free; every wait is bounded (a stall is reported through info, never a hang).
+// deadlock-free. Every wait is bounded in time: a dependency that has not completed within
+// kWaitTicks marks the launch stalled (kStall in info), and from then on every wait of every wave
+// returns at once, so a stalled launch drains in about one timeout and is reported as an error
+// (bos_step returns BOS_ERR_SOLVER and the box-plus is skipped), never a hang.
+// The ticket is reset by the launch itself: the last wave to leave zeroes it (and its exit
+// counter), so no host-side reset is needed between launches and no error path can leave a
+// partly consumed ticket behind (a launch that never started never took one).
 struct Flow {
     const int32_t* order;   // fronts in processing order
     int n;
-    int* ticket;            // zeroed before the launch
+    int* ticket;            // zero at launch; zeroed again by the launch's last wave
+    int* exits;             // waves that have left the launch (same life cycle)
     uint32_t* done;         // per supernode: epoch of its last completion
     uint32_t epoch;
     const int32_t* slev;    // level of every supernode
     int lev0;               // factor: children below this level were finished by earlier launches
 };
 
-constexpr int kStall = 1 << 20;   // added to info when a dependency wait times out
+constexpr int kStall = kMfStall;               // or-ed into info when a dependency wait times out
+constexpr uint64_t kWaitTicks = 5000000;        // 50 ms of the 100 MHz realtime clock
 
 __device__ __forceinline__ int next_ticket(int* ticket) {
     int t = 0;
@@ -481,10 +472,11 @@ __device__ __forceinline__ int next_ticket(int* ticket) {
 
 __device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
     if (threadIdx.x == 0) {
-        int it = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(f.done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != f.epoch) {
-            if (++it > (1 << 22)) {
-                atomicAdd(info, kStall);
+            if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStall) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) {
+                atomicOr(info, kStall);
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -492,6 +484,14 @@ __device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     wave_sync();
+}
+
+// Called by every wave once it has taken its last ticket.
+__device__ __forceinline__ void leave_flow(const Flow& f) {
+    if (threadIdx.x == 0 && atomicAdd(f.exits, 1) == (int)gridDim.x - 1) {
+        __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(f.exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __device__ __forceinline__ void publish_done(const Flow& f, int s) {
@@ -567,7 +567,6 @@ template <int MAXM, bool FLOW>
 __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf, int* smap,
                                                  double* wv, FoldBuf* fb, int lane, const Flow* f) {
     constexpr bool COH = FLOW;
-    mf_stamp(a, s, 0, lane);
     const int k = a.k[s], r = a.r[s], m = k + r;
     const int nfold = a.fold_cnt[s];
     const int c0 = a.col0[s];
@@ -581,13 +580,13 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     // assembly and the fold. Everything up to the extend-add depends on H only, so the flow kernel
     // waits for the children after it: on the critical path a front's assembly and fold overlap
     // its children's work.
-    const int cb = (a.diag_skip & 4) ? a.child_ptr[s + 1] : a.child_ptr[s] + nfold, ce = a.child_ptr[s + 1];
+    const int cb = a.child_ptr[s] + nfold, ce = a.child_ptr[s + 1];
     ChildPre p0, p1;
     if (cb < ce) child_meta(a, a.child[cb], lane, p0);
     if (cb + 1 < ce) child_meta(a, a.child[cb + 1], lane, p1);
     // the folded landmarks first (their W uses F's LDS): F and the u-vector accumulator wv start
     // from minus their contribution, the assembly then adds H
-    const bool fold = nfold > 0 && !(a.diag_skip & 2);
+    const bool fold = nfold > 0;
     if (fold) {
         FoldAcc<MAXM> facc;
         fold_children<MAXM>(a, s, F, fb, m, lane, facc);
@@ -598,14 +597,12 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         for (int i = lane; i < m; i += 64) wv[i] = 0.0;    // children's u-vectors accumulate here
     }
     wave_sync();
-    mf_stamp(a, s, 1, lane);
-    if (!(a.diag_skip & 1)) assemble_wave(a, s, F, lane, fold);
+    assemble_wave(a, s, F, lane, fold);
     wave_sync();
     if constexpr (FLOW) {
         for (int ci = a.child_ptr[s]; ci < ce; ++ci)
             if (f->slev[a.child[ci]] >= f->lev0) wait_done(*f, a.child[ci], a.info);
     }
-    mf_stamp(a, s, 2, lane);
     // extend-add, children in list order (deterministic)
     if (cb < ce) child_vals<COH>(lane, p0);
     if (cb + 1 < ce) child_vals<COH>(lane, p1);
@@ -617,7 +614,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         child_vals<COH>(lane, pq);
         extend_child<COH>(a, pq, F, wv, smap, m, lane);
     }
-    mf_stamp(a, s, 3, lane);
     const bool live = lane < m;
     double row[MAXM];
 #pragma unroll
@@ -644,7 +640,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     // Two pivots per step: column j + 1 is brought up to date in registers (L(j+1, j) by readlane),
     // both columns go through ONE LDS broadcast as pairs, and the trailing columns take a rank-2
     // update; the window rotates by two.
-    if (a.pair) {
+    {
 #pragma nounroll
         for (; j + 1 < kf; j += 2) {
             double d0 = readlane_d(row[0], j);
@@ -733,7 +729,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         }
     }
     if (nbad && lane == 0) atomicAdd(a.info, nbad);
-    mf_stamp(a, s, 4, lane);
     // the update matrix: row[t] holds column k + t
 #pragma unroll
     for (int t0 = 0; t0 < MAXM; t0 += 8) {
@@ -748,7 +743,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         else stc<COH>(us + (lane - k), wi);
     }
     wave_sync();
-    mf_stamp(a, s, 5, lane);
 }
 
 template <int MAXM>
@@ -883,6 +877,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
         factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, smap, wv, &fb, lane, &f);   // m <= kFlowMaxM
         publish_done(f, s);
     }
+    leave_flow(f);
 }
 
 __global__ __launch_bounds__(64, 2) void mf_factor_flow(const MfArgs a, const Flow f) { factor_flow_body(a, f); }
@@ -896,6 +891,7 @@ __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flo
         backward_front<true>(a, s, w, threadIdx.x, &f, parent);
         publish_done(f, s);
     }
+    leave_flow(f);
 }
 
 template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
@@ -918,10 +914,10 @@ inline int front_class(int m) { return m <= kMfWaveMaxM ? (m - 1) / 16 : 4; }
 struct MfDevice {
     int nlevels = 0;
     // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
-    // the level's other classes (BOS_MF_SIDE=0 disables)
+    // the level's other classes
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int tiny16 = 256;   // class-16 launches of at most this many fronts go to the side stream too (BOS_MF_TINY16)
+    static constexpr int tiny16 = 256;   // class-16 launches of at most this many fronts go to the side stream too
     // supernodes of (level l, class c) = list[ptr[l * kClasses + c], ptr[l * kClasses + c + 1])
     std::vector<int32_t> ptr;
     std::vector<int> lds_factor, lds_fwd, lds_bwd;   // per (level, class): dynamic LDS bytes
@@ -934,7 +930,7 @@ struct MfDevice {
     int lds_bwd_flow = 0;
     int32_t *order_factor = nullptr, *order_bwd = nullptr, *slev = nullptr, *parent = nullptr;
     uint32_t* done = nullptr;   // [3][nsuper]: factor, forward, backward
-    int* tickets = nullptr;     // [3]
+    int* tickets = nullptr;     // [2 * kMfTickets]: work-queue tickets, then the launches' exit counters
     uint32_t epoch = 0;
     int32_t *fold_cnt = nullptr, *fold_cptr = nullptr, *fold_chunk = nullptr, *fold_rec = nullptr,
             *fold_list = nullptr;
@@ -945,10 +941,6 @@ struct MfDevice {
     int64_t *L_off = nullptr, *U_off = nullptr, *u_off = nullptr, *scratch_off = nullptr, *rmap_off = nullptr,
             *findex_off = nullptr;
     double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
-    // timing diagnostics (BOS_MF_STAMPS=<file>): per-supernode phase stamps, dumped at destroy
-    unsigned long long* stamps = nullptr;
-    std::string stamp_path;
-    std::vector<int32_t> h_meta;   // per supernode: level (-1 folded), k, r, nfold
 
     // classes [c0, c1) of level lev are contiguous in the list
     int count(int lev, int c0, int c1) const { return ptr[lev * kClasses + c1] - ptr[lev * kClasses + c0]; }
@@ -967,11 +959,6 @@ struct MfDevice {
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
         g.findex = findex; g.A = A; g.L = L; g.U = U; g.u = u; g.scratch = scratch; g.x = x; g.info = info;
         g.fold_cnt = fold_cnt; g.fold_cptr = fold_cptr; g.fold_chunk = fold_chunk; g.fold_rec = fold_rec;
-        static const int skip = [] { const char* e = std::getenv("BOS_MF_DIAG_SKIP"); return e ? std::atoi(e) : 0; }();
-        g.diag_skip = skip;
-        static const int pair = [] { const char* e = std::getenv("BOS_MF_PAIR"); return e ? std::atoi(e) : 1; }();
-        g.pair = pair;
-        g.stamps = stamps;
         return g;
     }
 };
@@ -980,22 +967,6 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
     MfDevice* d = new MfDevice();
     *out = d;
     d->nlevels = F.nlevels;
-    if (const char* sp = std::getenv("BOS_MF_STAMPS")) {
-        d->stamp_path = sp;
-        if (hipMalloc((void**)&d->stamps, 8 * (size_t)std::max(1, F.nsuper) * sizeof(unsigned long long)) != hipSuccess ||
-            hipMemset(d->stamps, 0, 8 * (size_t)std::max(1, F.nsuper) * sizeof(unsigned long long)) != hipSuccess) {
-            err = "hipMalloc failed (stamps)";
-            return -2;
-        }
-        d->h_meta.assign(4 * (size_t)F.nsuper, -1);
-        for (int l = 0; l < F.nlevels; ++l)
-            for (int i = F.level_ptr[l]; i < F.level_ptr[l + 1]; ++i) d->h_meta[4 * (size_t)F.level[i]] = l;
-        for (int s2 = 0; s2 < F.nsuper; ++s2) {
-            d->h_meta[4 * (size_t)s2 + 1] = F.k[s2];
-            d->h_meta[4 * (size_t)s2 + 2] = F.r[s2];
-            d->h_meta[4 * (size_t)s2 + 3] = F.fold_cnt.empty() ? 0 : F.fold_cnt[s2];
-        }
-    }
     std::vector<int64_t> scr(F.nsuper, -1);
     int64_t scratch_size = 0;
     for (int s = 0; s < F.nsuper; ++s) {
@@ -1033,9 +1004,7 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
                             c += 4.0 * F.r[F.child[ci]] * F.r[F.child[ci]];
                     return c;
                 };
-                static const bool lpt = [] { const char* e = std::getenv("BOS_MF_LPT"); return !e || std::atoi(e) != 0; }();
-                if (lpt)
-                    std::stable_sort(lst.begin() + d->ptr[lc], lst.end(), [&](int x, int y) { return cost(x) > cost(y); });
+                std::stable_sort(lst.begin() + d->ptr[lc], lst.end(), [&](int x, int y) { return cost(x) > cost(y); });
             }
             d->ptr[lc + 1] = (int32_t)lst.size();
         }
@@ -1070,18 +1039,14 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
     d->n_flow_solve = (int)ofwd.size();
     d->flow_solve = d->n_flow_solve > 0 && d->lds_bwd_flow <= 48 * 1024;
     if (!d->flow_solve) d->solve_lev0 = L;
-    if (const char* e = std::getenv("BOS_MF_FLOW")) {   // diagnostics: bit 0 factor flow, bit 1 solve flows
-        const int v = std::atoi(e);
-        if (!(v & 1)) { d->flow_lev0 = L; ofac.clear(); d->n_flow_factor = 0; }
-        if (!(v & 2)) { d->flow_solve = false; d->solve_lev0 = L; }
-    }
     int rc = 0;
     if ((rc = up(&d->order_factor, ofac, err)) || (rc = up(&d->order_bwd, obwd, err)) ||
         (rc = up(&d->slev, slev, err)) || (rc = up(&d->parent, F.parent, err)))
         return rc;
     if (hipMalloc((void**)&d->done, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(d->done, 0, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void**)&d->tickets, 3 * sizeof(int)) != hipSuccess || hipMemset(d->tickets, 0, 3 * sizeof(int)) != hipSuccess) {
+        hipMalloc((void**)&d->tickets, 2 * kMfTickets * sizeof(int)) != hipSuccess ||
+        hipMemset(d->tickets, 0, 2 * kMfTickets * sizeof(int)) != hipSuccess) {
         err = "hipMalloc failed (multifrontal flow)";
         return -2;
     }
@@ -1097,16 +1062,11 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         (rc = up(&d->fold_list, F.fold_list, err)))
         return rc;
     d->n_fold = (int)F.fold_list.size();
-    if (const char* e = std::getenv("BOS_MF_TINY16")) d->tiny16 = std::atoi(e);
-    {
-        const char* e = std::getenv("BOS_MF_SIDE");
-        if (!(e && std::atoi(e) == 0) &&
-            (hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking) != hipSuccess ||
-             hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess ||
-             hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess)) {
-            err = "side stream creation failed (multifrontal)";
-            return -2;
-        }
+    if (hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) {
+        err = "side stream creation failed (multifrontal)";
+        return -2;
     }
     auto alloc = [&](double** p, int64_t n) -> int {
         if (n <= 0) n = 1;
@@ -1123,21 +1083,6 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
 
 void mf_destroy(MfDevice* d) {
     if (!d) return;
-    if (d->stamps && !d->stamp_path.empty()) {   // diagnostics: [nsuper] then per supernode meta[4] + stamps[8]
-        const size_t ns = d->h_meta.size() / 4;
-        std::vector<unsigned long long> st(8 * ns);
-        if (hipDeviceSynchronize() == hipSuccess &&
-            hipMemcpy(st.data(), d->stamps, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
-            if (FILE* f = std::fopen(d->stamp_path.c_str(), "wb")) {
-                const int64_t n = (int64_t)ns;
-                std::fwrite(&n, sizeof(n), 1, f);
-                std::fwrite(d->h_meta.data(), sizeof(int32_t), d->h_meta.size(), f);
-                std::fwrite(st.data(), sizeof(unsigned long long), st.size(), f);
-                std::fclose(f);
-            }
-        }
-        (void)hipFree(d->stamps);
-    }
     void* bufs[] = {d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->fold_list, d->order_factor, d->order_bwd, d->slev, d->parent, d->done, d->tickets, d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
@@ -1149,8 +1094,8 @@ void mf_destroy(MfDevice* d) {
     delete d;
 }
 
-// info and the work-queue tickets are zero on entry: zeroed at creation and, after every
-// iteration, by the end-of-step reduce_stats launch (mf_info_ptr / mf_tickets_ptr).
+// info is zero on entry: zeroed at creation and, after every iteration, by the end-of-step
+// reduce_stats launch (mf_info_ptr). The work-queue tickets reset themselves (leave_flow).
 hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
     hipError_t e;
     const uint32_t epoch = ++d->epoch;
@@ -1181,7 +1126,8 @@ hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (d->n_flow_factor > 0) {
-        const Flow f{d->order_factor, d->n_flow_factor, d->tickets, d->done, epoch, d->slev, d->flow_lev0};
+        const Flow f{d->order_factor, d->n_flow_factor, d->tickets, d->tickets + kMfTickets, d->done, epoch, d->slev,
+                     d->flow_lev0};
         const int grid = std::min(d->n_flow_factor, d->ncu * 8);   // 2 waves per SIMD resident
         hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1195,7 +1141,8 @@ hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
     hipError_t e;
     const uint32_t epoch = ++d->epoch;
     if (d->flow_solve) {
-        const Flow fb{d->order_bwd, d->n_flow_solve, d->tickets + 1, d->done + d->nsuper, epoch, d->slev, d->solve_lev0};
+        const Flow fb{d->order_bwd, d->n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1, d->done + d->nsuper,
+                      epoch, d->slev, d->solve_lev0};
         const int grid = std::min(d->n_flow_solve, d->ncu * 8);
         hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), d->lds_bwd_flow, s, d->args(0, 0, nullptr, x), fb,
                            (const int32_t*)d->parent);
@@ -1221,6 +1168,12 @@ hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
 
 int32_t* mf_info_ptr(const MfDevice* d) { return d->info; }
 int32_t* mf_tickets_ptr(const MfDevice* d) { return d->tickets; }
+
+hipError_t mf_debug_skip_next_front(MfDevice* d, hipStream_t s) {
+    if (d->n_flow_factor == 0) return hipErrorInvalidValue;
+    static const int one = 1;
+    return hipMemcpyAsync(d->tickets, &one, sizeof(int), hipMemcpyHostToDevice, s);
+}
 
 }  // namespace dev
 }  // namespace bos

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../../include/bos.h"
+#include "../../../include/bos_host.h"
 #include "../host/bos_math.hpp"
 #include "../host/error.hpp"
 #include "../host/plan.hpp"
@@ -121,7 +122,12 @@ struct bos_solver {
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     std::vector<int32_t> ref_dof;   // permuted dof -> reference dof (size n + 3)
     bool have_dx = false;
+    // odometry self-loops: z[3] and Omega upper triangle [6] each (constant chi^2 terms)
+    std::vector<double> loop_z, loop_om;
+    double* scrub = nullptr;   // bos_time_linearize(flush_caches): 1 GiB read between launches
 };
+
+static_assert(bos::dev::kStepAbort == bos::dev::kMfStall, "solver abort bit");
 
 namespace {
 // both multifrontal orderings (nested dissection / landmarks-first Schur) share the GPU engine
@@ -154,14 +160,7 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.nrob_part = s->d_nrob_part;
     p.kt = (T)s->kt;
     p.lambda = (T)s->damping;
-    static const int interleave = [] { const char* e = std::getenv("BOS_JH_INTERLEAVE"); return e ? std::atoi(e) : 0; }();
-    static const int diag_skip = [] { const char* e = std::getenv("BOS_JH_DIAG_SKIP"); return e ? std::atoi(e) : 0; }();
-    p.interleave = interleave;
-    static const int xcd_remap = [] { const char* e = std::getenv("BOS_JH_XCD"); return e ? std::atoi(e) : 1; }();
-    p.xcd_remap = xcd_remap;
-    p.diag_skip = diag_skip;
     p.diag_stamps = nullptr;
-    p.lm_rep = 1;
     return p;
 }
 
@@ -173,6 +172,7 @@ template <typename T> bos::dev::UpdateParams<T> upd_params(const bos_solver* s) 
     u.pose = s->d_pose; u.lm = s->d_lm;
     u.pc = (T*)s->d_pc; u.pth = (T*)s->d_pth; u.lc = (T*)s->d_lc;
     u.max_part = s->d_maxpart;
+    u.info = uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : nullptr;
     return u;
 }
 
@@ -253,12 +253,39 @@ int setup_exchange(bos_solver* s) {
     return BOS_OK;
 }
 
-int enqueue_stats(bos_solver* s, bool with_update) {
+// chi^2 and robust count of the odometry self-loops: constant (e = -z whatever the state, their
+// Jacobian is zero, see host/plan.cpp build_layout), evaluated in T like the kernel; rank 0 adds them
+template <typename T> void self_loop_terms(const bos_solver* s, double& chi, int32_t& nrob) {
+    chi = 0.0;
+    nrob = 0;
+    if (s->rank != 0) return;
+    const T kt = (T)s->kt;
+    for (size_t i = 0; i < s->loop_z.size() / 3; ++i) {
+        const T* z = nullptr;
+        T zz[3], u[6];
+        for (int v = 0; v < 3; ++v) zz[v] = (T)s->loop_z[3 * i + v];
+        for (int v = 0; v < 6; ++v) u[v] = (T)s->loop_om[6 * i + v];
+        z = zz;
+        const T e0 = (T)0 - z[0], e1 = (T)0 - z[1];
+        const T e2 = bos::normalized_angle<T>(bos::normalized_angle<T>((T)0) - z[2]);
+        const T Oe0 = u[0] * e0 + u[1] * e1 + u[2] * e2;
+        const T Oe1 = u[1] * e0 + u[3] * e1 + u[4] * e2;
+        const T Oe2 = u[2] * e0 + u[4] * e1 + u[5] * e2;
+        const T rho = e0 * Oe0 + e1 * Oe1 + e2 * Oe2;
+        chi += (double)rho;
+        if (rho > kt) ++nrob;
+    }
+}
+
+int enqueue_stats(bos_solver* s, bool with_update, bool first = true) {
     int32_t* info = uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : (s->solver_kind == BOS_SOLVER_DENSE_CHOL ? s->d_info : nullptr);
-    int32_t* tickets = uses_mf(s) ? bos::dev::mf_tickets_ptr(s->mf) : nullptr;
     const int nupd = (s->NP + s->NL + bos::dev::kUpdateBlock - 1) / bos::dev::kUpdateBlock;
-    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->pose_blocks, with_update ? s->d_maxpart : nullptr,
-                                          nupd, info, tickets, tickets ? bos::dev::kMfTickets : 0, s->d_status,
+    double chi_c = 0.0;
+    int32_t nrob_c = 0;
+    if (s->precision == BOS_FP32) self_loop_terms<float>(s, chi_c, nrob_c);
+    else self_loop_terms<double>(s, chi_c, nrob_c);
+    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->pose_blocks, chi_c, nrob_c,
+                                          with_update ? s->d_maxpart : nullptr, nupd, info, first, s->d_status,
                                           s->stream));
     if (s->comm) {
         NC_TRY(ncclGroupStart());
@@ -367,7 +394,7 @@ int enqueue_triangulate(bos_solver* s) {
     return BOS_OK;
 }
 
-int read_stats(bos_solver* s, bos_step_stats* st) {
+int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr) {
     bos::dev::StepStatus h;
     HIP_TRY(hipMemcpyAsync(&h, s->d_status, sizeof(h), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -375,13 +402,17 @@ int read_stats(bos_solver* s, bos_step_stats* st) {
         std::memset(st, 0, sizeof(*st));
         st->chi2 = h.chi2;
         st->n_robust = h.n_robust;
-        st->solver_info = h.info;
+        st->solver_info = h.info & ~bos::dev::kStepAbort;
         st->max_abs_dx = h.max_dx;
     }
+    if (aborted) *aborted = h.aborted;
     return BOS_OK;
 }
 
-int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
+// One GN iteration. first: the first of a bos_step_n batch (resets the sticky abort flag); sync:
+// the last one (reads the status back). A factorization whose dataflow launch timed out leaves the
+// state untouched (the box-plus kernel checks the solver word) and fails the call.
+int do_step(bos_solver* s, bos_step_stats* st, bool first, bool sync) {
     int rc;
     HIP_TRY(hipEventRecord(s->ev[0], s->stream));
     if ((rc = enqueue_linearize(s))) return rc;
@@ -392,11 +423,17 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     if ((rc = enqueue_solve(s, analysed_now))) return rc;
     HIP_TRY(hipEventRecord(s->ev[3], s->stream));
     if ((rc = enqueue_update(s))) return rc;
-    if ((rc = enqueue_stats(s, true))) return rc;
+    if ((rc = enqueue_stats(s, true, first))) return rc;
     HIP_TRY(hipEventRecord(s->ev[4], s->stream));
     s->have_dx = true;
     if (!sync) return BOS_OK;
-    if ((rc = read_stats(s, st))) return rc;
+    int32_t aborted = 0;
+    if ((rc = read_stats(s, st, &aborted))) return rc;
+    if (aborted) {
+        s->have_dx = false;
+        return fail(BOS_ERR_SOLVER, "sparse factorization aborted: a dataflow dependency wait timed out (state "
+                                    "left unchanged by the failed iteration)");
+    }
     if (st) {
         st->t_linearize_ms = elapsed(s->ev[0], s->ev[1]);
         st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
@@ -448,7 +485,7 @@ int bos_destroy(bos_solver* s) {
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_status,
                     s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr,
-                    s->ex_send, s->ex_recv, s->ex_pack, s->ex_unpack};
+                    s->ex_send, s->ex_recv, s->ex_pack, s->ex_unpack, s->scrub};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (s->rf) rocsolver_destroy_rfinfo(s->rf);
@@ -616,6 +653,12 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         }
         s->pose_blocks = (int)(((int64_t)(P.p_end - P.p_begin) * B.lpp + bos::dev::kBlock - 1) / bos::dev::kBlock);
     }
+    for (int k = 0; k < s->Mo; ++k)
+        if (pb->odom_src[k] == pb->odom_dst[k]) {
+            const double* m = pb->odom_omega + 9 * (size_t)k;
+            for (int v = 0; v < 3; ++v) s->loop_z.push_back(pb->odom_z[3 * (size_t)k + v]);
+            for (double v : {m[0], m[1], m[2], m[4], m[5], m[8]}) s->loop_om.push_back(v);
+        }
     {
         std::vector<int32_t> os(pb->odom_src, pb->odom_src + s->Mo), od(pb->odom_dst, pb->odom_dst + s->Mo);
         std::vector<double> oz(pb->odom_z, pb->odom_z + 3 * (size_t)s->Mo), om(6 * (size_t)s->Mo);
@@ -707,14 +750,14 @@ int bos_set_damping_factor(bos_solver* s, double df) {
 int bos_step(bos_solver* s, bos_step_stats* st) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
     HIP_TRY(hipSetDevice(s->device));
-    return do_step(s, st, true);
+    return do_step(s, st, true, true);
 }
 
 int bos_step_n(bos_solver* s, int n, bos_step_stats* last) {
     if (!s || n < 0) return fail(BOS_ERR_INVALID, "bad argument");
     HIP_TRY(hipSetDevice(s->device));
     for (int i = 0; i < n; ++i) {
-        int rc = do_step(s, last, i + 1 == n);
+        int rc = do_step(s, last, i == 0, i + 1 == n);
         if (rc) return rc;
     }
     return BOS_OK;
@@ -754,6 +797,64 @@ int bos_debug_linearize_timeline(bos_solver* s, int64_t capacity, uint64_t* stam
     if (e == hipSuccess) e = hipMemcpy(stamps, d, 8 * (size_t)waves * sizeof(uint64_t), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("timeline: ") + hipGetErrorString(e));
+    return BOS_OK;
+}
+
+int bos_time_linearize(bos_solver* s, int32_t n, int32_t flush_caches, double* ms_per_build) {
+    if (!s || n <= 0 || !ms_per_build) return fail(BOS_ERR_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(s->device));
+    int rc;
+    if (!flush_caches) {   // back to back: the block array and lists stay in L2 / Infinity Cache
+        HIP_TRY(hipEventRecord(s->ev[0], s->stream));
+        for (int i = 0; i < n; ++i)
+            if ((rc = enqueue_linearize(s))) return rc;
+        HIP_TRY(hipEventRecord(s->ev[1], s->stream));
+        HIP_TRY(hipEventSynchronize(s->ev[1]));
+        *ms_per_build = elapsed(s->ev[0], s->ev[1]) / n;
+        return BOS_OK;
+    }
+    // cold: before every build, 1 GiB is read (4x the Infinity Cache) so the build's inputs come
+    // from HBM, as inside a GN step where the solver streams its factor between two builds; each
+    // build is timed alone
+    constexpr int64_t kScrub = (int64_t)1 << 27;   // doubles
+    if (!s->scrub) {
+        if ((rc = dalloc(&s->scrub, kScrub + 1))) return rc;
+        HIP_TRY(hipMemset(s->scrub, 0, (kScrub + 1) * sizeof(double)));
+    }
+    double total = 0.0;
+    for (int i = 0; i < n; ++i) {
+        HIP_TRY(bos::dev::launch_cache_scrub(s->scrub, kScrub, s->scrub + kScrub, s->stream));
+        HIP_TRY(hipEventRecord(s->ev[0], s->stream));
+        if ((rc = enqueue_linearize(s))) return rc;
+        HIP_TRY(hipEventRecord(s->ev[1], s->stream));
+        HIP_TRY(hipEventSynchronize(s->ev[1]));
+        total += elapsed(s->ev[0], s->ev[1]);
+    }
+    *ms_per_build = total / n;
+    return BOS_OK;
+}
+
+int bos_time_triangulate(bos_solver* s, int32_t n, double* ms_per_call) {
+    if (!s || n <= 0 || !ms_per_call) return fail(BOS_ERR_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(s->device));
+    int rc;
+    HIP_TRY(hipEventRecord(s->ev[0], s->stream));
+    for (int i = 0; i < n; ++i)
+        if ((rc = enqueue_triangulate(s))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[1], s->stream));
+    HIP_TRY(hipEventSynchronize(s->ev[1]));
+    *ms_per_call = elapsed(s->ev[0], s->ev[1]) / n;
+    s->have_dx = false;
+    return BOS_OK;
+}
+
+int bos_debug_inject_stall(bos_solver* s) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    if (!uses_mf(s)) return fail(BOS_ERR_UNSUPPORTED, "no dataflow launch in this solver");
+    HIP_TRY(hipSetDevice(s->device));
+    const hipError_t e = bos::dev::mf_debug_skip_next_front(s->mf, s->stream);
+    if (e == hipErrorInvalidValue) return fail(BOS_ERR_UNSUPPORTED, "no dataflow launch in this plan");
+    HIP_TRY(e);
     return BOS_OK;
 }
 

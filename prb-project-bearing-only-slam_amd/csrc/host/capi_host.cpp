@@ -106,23 +106,13 @@ int bos_dataset_load_g2o(const char* path, int triangulate, int verbose, bos_dat
     if (!path || !out) return hfail(BOS_ERR_INVALID, "null argument");
     *out = nullptr;
     bos_dataset* d = new bos_dataset();
-    const bool timing = std::getenv("BOS_LOAD_TIMING") != nullptr;
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    const auto t0 = now();
     const int rc = proj02::parse_g2o(path, d->state, d->bearings, d->odometry, d->fixed_pose_id, d->bound);
-    const auto t1 = now();
     if (rc) { delete d; return hfail(BOS_ERR_IO, rc == -1 ? "cannot open g2o file" : "malformed g2o line"); }
     if (d->state.number_of_poses() == 0) { delete d; return hfail(BOS_ERR_INVALID, "no poses"); }
     if (d->fixed_pose_id < 0) d->fixed_pose_id = d->state.default_pose_id();   // bearing_only_slam.cpp:63-65
     if (triangulate) proj02::triangulate_landmarks(d->state, d->bearings, verbose != 0);
-    const auto t2 = now();
     const int r2 = d->finalize();
     if (r2) { delete d; return r2; }
-    if (timing) {
-        const auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "load_g2o: parse %.1f ms, triangulate %.1f ms, finalize %.1f ms\n", ms(t0, t1), ms(t1, t2),
-                     ms(t2, now()));
-    }
     *out = d;
     return BOS_OK;
 }
@@ -284,6 +274,9 @@ int bos_plan_exchange_selftest(const bos_problem* pb, int32_t world) {
     return BOS_OK;
 }
 
+void bos_debug_set_schur_leaf(int32_t poses) { bos::g_schur_leaf = poses > 0 ? poses : 0; }
+void bos_debug_set_g2o_parser(int32_t line_by_line) { proj02::g_g2o_line_parser = line_by_line != 0; }
+
 int bos_plan_inspect(const bos_problem* pb, int32_t solver, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
                      int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref,
                      bos_plan_info* info) {
@@ -320,6 +313,9 @@ int bos_plan_inspect(const bos_problem* pb, int32_t solver, int32_t rank, int32_
         info->mf_max_front = P.mf.max_m;
         info->mf_flops = P.mf.flops;
         info->mf_update_bytes = P.mf.U_size * 8;
+        info->mf_fits = P.mf.fits;
+        info->mf_max_front_upper = P.mf.max_m_upper;
+        info->mf_balance_pct = P.mf.balance_pct;
         std::strncpy(info->ordering, P.ordering.chosen.c_str(), sizeof(info->ordering) - 1);
     }
     if (ref_rows || ref_cols || owned) {

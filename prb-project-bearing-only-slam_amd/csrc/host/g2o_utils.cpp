@@ -202,10 +202,11 @@ void parse_chunk(const char* p, const char* e, ChunkOut& o) {
 
 }  // namespace
 
+int g_g2o_line_parser = 0;
+
 int parse_g2o(const std::string& fname, State& state, BearingObservationVector& bearings,
               OdometryObservationVector& odometries, int& fixed_pose_id, float& bound) {
-    if (const char* e = std::getenv("BOS_G2O_SIMPLE"))   // the line-by-line parser (tests compare the two)
-        if (std::atoi(e) == 1) return parse_g2o_simple(fname, state, bearings, odometries, fixed_pose_id, bound);
+    if (g_g2o_line_parser) return parse_g2o_simple(fname, state, bearings, odometries, fixed_pose_id, bound);
     bound = 0;
     fixed_pose_id = -1;
     FILE* f = std::fopen(fname.c_str(), "rb");

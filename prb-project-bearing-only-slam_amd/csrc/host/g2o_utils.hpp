@@ -24,6 +24,8 @@ int parse_g2o(const std::string& fname, State& state, BearingObservationVector& 
 
 // The line-by-line form of parse_g2o (parse_g2o reads the file at once and parses chunks in
 // parallel, merged in file order; BOS_G2O_SIMPLE=1 selects this one instead).
+// Test hook (bos_debug_set_g2o_parser): nonzero makes parse_g2o use the line-by-line form.
+extern int g_g2o_line_parser;
 int parse_g2o_simple(const std::string& fname, State& state, BearingObservationVector& bearings,
                      OdometryObservationVector& odometries, int& fixed_pose_id, float& bound);
 

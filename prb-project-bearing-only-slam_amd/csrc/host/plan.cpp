@@ -15,6 +15,11 @@ constexpr int kMfLeaf = 12;          // nested-dissection leaf size (nodes) for 
 // pose leaves of the Schur ordering: 10 keeps the leaf fronts (poses + their landmarks' rows) within
 // one wavefront (m <= 64, so every landmark folds) at config 3; 6 / 8 / 12 measured slower
 constexpr int kSchurLeaf = 10;
+}  // namespace
+
+int g_schur_leaf = 0;   // test hook (bos_debug_set_schur_leaf); 0 = kSchurLeaf
+
+namespace {
 
 inline int node_size(int u, int NP) { return u < NP ? 3 : 2; }
 
@@ -129,12 +134,9 @@ SymbCost symbolic(const Graph& g, int NP, const std::vector<int32_t>& pos, const
 }
 
 // Separator balance of nested_dissection (percent of a part's nodes each side must keep): set per
-// plan attempt by build_plan, BOS_ND_MINPCT overrides (diagnostics).
+// plan attempt by build_plan.
 thread_local int t_nd_minpct = 40;
-int nd_minpct() {
-    static const int env = [] { const char* e = std::getenv("BOS_ND_MINPCT"); return e ? std::atoi(e) : 0; }();
-    return env > 0 ? env : t_nd_minpct;
-}
+int nd_minpct() { return t_nd_minpct; }
 
 // Nested dissection with BFS level-structure vertex separators (graph-based, no coordinates).
 void nested_dissection(const Graph& g, const std::vector<char>& active, std::vector<int32_t>& order, int leaf,
@@ -316,7 +318,7 @@ int order_nodes(const ProblemIndex& pi, int mode, std::vector<int32_t>& node_pos
         for (int u = 0; u < NP; ++u) active[u] = u != pi.fixed;
         std::vector<int32_t> ord_p;
         std::vector<std::pair<int32_t, int32_t>> pblocks;
-        static const int leaf = [] { const char* e = std::getenv("BOS_SCHUR_LEAF"); return e ? std::atoi(e) : kSchurLeaf; }();
+        const int leaf = g_schur_leaf > 0 ? g_schur_leaf : kSchurLeaf;
         nested_dissection(build_schur_graph(pi), active, ord_p, leaf, &pblocks);
         if ((int)ord_p.size() != NP - 1) { err = "nested dissection of the pose graph lost nodes"; return BOS_ERR_INVALID; }
         order.insert(order.end(), ord_p.begin(), ord_p.end());
@@ -409,10 +411,6 @@ int build_plan_once(const ProblemIndex& pi, int rank, int world, int factor_mode
         if (pi.o_src[k] < 0 || pi.o_src[k] >= NP || pi.o_dst[k] < 0 || pi.o_dst[k] >= NP) {
             err = "odometry edge " + std::to_string(k) + " references an unknown pose stix";
             return BOS_ERR_INVALID;
-        }
-        if (pi.o_src[k] == pi.o_dst[k]) {
-            err = "odometry edge " + std::to_string(k) + " is a self loop (not supported)";
-            return BOS_ERR_UNSUPPORTED;
         }
     }
     P = Plan();
@@ -516,28 +514,40 @@ int build_plan_once(const ProblemIndex& pi, int rank, int world, int factor_mode
 // from level 2 up, where the dataflow launch starts), which costs far more than the balance buys.
 // Such plans are rebuilt with other balances; the first plan without those fronts is kept (the
 // first attempt's plan if none is).
-bool schur_fronts_fit(const Multifrontal& F) {
+void schur_front_report(Multifrontal& F) {
+    F.max_m_upper = 0;
+    F.fits = true;
     for (int l = 0; l < F.nlevels; ++l)
         for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
             const int m = F.k[F.level[q]] + F.r[F.level[q]];
-            if (m > kMfWaveMaxM || (l >= 2 && m > kMfFlowMaxM)) return false;
+            if (l >= 2) F.max_m_upper = std::max(F.max_m_upper, m);
+            if (m > kMfWaveMaxM || (l >= 2 && m > kMfFlowMaxM)) F.fits = false;
         }
-    return true;
 }
 
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& P, std::string& err) {
     if (factor_mode != kFactorSchur) return build_plan_once(pi, rank, world, factor_mode, P, err);
+    // The first attempt (40 %) decides success: a later, less balanced attempt has more fill, so an
+    // error there (e.g. a 32-bit size limit) only means "does not fit" and the first plan is kept.
     const int tries[] = {40, 35, 45, 30, 20};
     Plan first;
     for (int i = 0; i < 5; ++i) {
         t_nd_minpct = tries[i];
-        const int rc = build_plan_once(pi, rank, world, factor_mode, P, err);
-        if (rc) { t_nd_minpct = 40; return rc; }
-        if (schur_fronts_fit(P.mf) || std::getenv("BOS_ND_MINPCT")) break;
-        if (i == 0) first = P;
-        if (i == 4) P = std::move(first);
+        Plan attempt;
+        std::string aerr;
+        const int rc = build_plan_once(pi, rank, world, factor_mode, attempt, aerr);
+        t_nd_minpct = 40;
+        if (rc) {
+            if (i == 0) { err = aerr; return rc; }
+            continue;
+        }
+        schur_front_report(attempt.mf);
+        attempt.mf.balance_pct = tries[i];
+        if (attempt.mf.fits) { P = std::move(attempt); return BOS_OK; }
+        if (i == 0) first = std::move(attempt);
     }
-    t_nd_minpct = 40;
+    P = std::move(first);   // no balance fits: the default plan (fronts the fast kernels do not take run
+                            // on the general workgroup path)
     return BOS_OK;
 }
 
@@ -610,19 +620,25 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     for (int l = 0; l < NL; ++l)
         std::stable_sort(lb_obs.begin() + lb_ptr[l], lb_obs.begin() + lb_ptr[l + 1],
                          [&](int a, int b) { return pi.b_pose[a] < pi.b_pose[b]; });
-    // odometry entries of each pose: source side sorted by (dst, edge), then destination side by (src, edge)
+    // Odometry entries of each pose, sorted by (other pose, edge). An odometry self-loop has a zero
+    // Jacobian in the reference (its source and destination triplets land on the same columns and
+    // cancel exactly, solver_jacobians.cpp:126-146 with setFromTriplets summing duplicates), so it
+    // adds nothing to H or b: it gets no entries (its constant chi^2 is added by the step's stats).
+    // The pose-pose block of an unordered pair {p, q} is stored by the lower pose's lane: every edge
+    // between the two, in either direction, adds -H_ss (symmetric) to it.
     B.po_ptr.assign(NP + 1, 0);
-    for (int k = 0; k < Mo; ++k) { ++B.po_ptr[pi.o_src[k] + 1]; ++B.po_ptr[pi.o_dst[k] + 1]; }
+    for (int k = 0; k < Mo; ++k)
+        if (pi.o_src[k] != pi.o_dst[k]) { ++B.po_ptr[pi.o_src[k] + 1]; ++B.po_ptr[pi.o_dst[k] + 1]; }
     for (int p = 0; p < NP; ++p) B.po_ptr[p + 1] += B.po_ptr[p];
-    B.po_ent.resize(2 * (size_t)Mo);
+    B.po_ent.resize(B.po_ptr[NP]);
     {
         std::vector<int32_t> w(B.po_ptr.begin(), B.po_ptr.end() - 1);
-        for (int k = 0; k < Mo; ++k) { B.po_ent[w[pi.o_src[k]]++] = 2 * k; B.po_ent[w[pi.o_dst[k]]++] = 2 * k + 1; }
+        for (int k = 0; k < Mo; ++k)
+            if (pi.o_src[k] != pi.o_dst[k]) { B.po_ent[w[pi.o_src[k]]++] = 2 * k; B.po_ent[w[pi.o_dst[k]]++] = 2 * k + 1; }
     }
     auto other = [&](int32_t ent) { return (ent & 1) ? pi.o_src[ent >> 1] : pi.o_dst[ent >> 1]; };
     for (int p = 0; p < NP; ++p)
         std::sort(B.po_ent.begin() + B.po_ptr[p], B.po_ent.begin() + B.po_ptr[p + 1], [&](int32_t a, int32_t b) {
-            if ((a & 1) != (b & 1)) return (a & 1) < (b & 1);
             if (other(a) != other(b)) return other(a) < other(b);
             return a < b;
         });
@@ -631,8 +647,8 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     for (int p = 0; p < NP; ++p) {
         for (int x = B.po_ptr[p]; x < B.po_ptr[p + 1]; ++x) {
             const int32_t e = B.po_ent[x];
-            if (e & 1) continue;
-            if (x > B.po_ptr[p] && !(B.po_ent[x - 1] & 1) && other(B.po_ent[x - 1]) == other(e)) {
+            if (other(e) < p) continue;
+            if (x > B.po_ptr[p] && other(B.po_ent[x - 1]) == other(e)) {
                 B.has_dups = true;
                 B.po_blk[x] = B.po_blk[x - 1];
                 continue;
@@ -642,22 +658,10 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
         }
         B.uo_ptr[p + 1] = (int32_t)B.uo_dst.size();
     }
-    for (int s = 0; s < NP; ++s)
-        for (int u = B.uo_ptr[s]; u < B.uo_ptr[s + 1]; ++u) {
-            const int d = B.uo_dst[u];
-            if (std::binary_search(B.uo_dst.begin() + B.uo_ptr[d], B.uo_dst.begin() + B.uo_ptr[d + 1], s)) {
-                err = "odometry edges in both directions between the same poses (not supported)";
-                return BOS_ERR_UNSUPPORTED;
-            }
-        }
     // lanes per pose and their bearing segments (lane 0 also takes the odometry entries; a run of
     // duplicate observations of one pair never straddles two lanes)
     const double avg = NP ? (double)Mb / NP : 0.0;
     B.lpp = avg >= 32 ? 2 : 1;   // measured on config 3 (K = 10): 1 lane per pose beats 2 and 4
-    if (const char* e = std::getenv("BOS_LANES_PER_POSE")) {   // tuning override: 1 or 2
-        const int v = std::atoi(e);
-        if (v == 1 || v == 2) B.lpp = v;
-    }
     const int L = B.lpp;
     auto same_lm = [&](int i, int j) { return pi.b_lm[pb_obs[i]] == pi.b_lm[pb_obs[j]]; };
     std::vector<int32_t> lane_ptr((size_t)NP * L + 1, 0);
@@ -686,9 +690,7 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
         B.lm_lane_lm.resize(NL);
         for (int l = 0; l < NL; ++l) B.lm_lane_lm[l] = l;
         auto deg = [&](int l) { return lb_ptr[l + 1] - lb_ptr[l]; };
-        const char* no_sort = std::getenv("BOS_LM_SORT");   // tuning override: 0 = landmark order
-        if (!no_sort || std::atoi(no_sort) != 0)
-            for (int w0 = 0; w0 < NL; w0 += kLmWindow)
+        for (int w0 = 0; w0 < NL; w0 += kLmWindow)
                 std::stable_sort(B.lm_lane_lm.begin() + w0, B.lm_lane_lm.begin() + std::min(NL, w0 + kLmWindow),
                                  [&](int a, int b) { return deg(a) > deg(b); });
         std::vector<int32_t> lptr(NL + 1, 0), litems(Mb);
@@ -935,7 +937,6 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
     }
     F.rmap_off[ns] = (int64_t)F.rmap.size();
     F.nlevels = 0;
-    const bool stats = std::getenv("BOS_MF_STATS") != nullptr;   // diagnostics: per-level front sizes
     for (int s = 0; s < ns; ++s) F.nlevels = std::max(F.nlevels, lev[s] + 1);
     F.level_ptr.assign(F.nlevels + 1, 0);
     for (int s = 0; s < ns; ++s) if (!folded[s]) ++F.level_ptr[lev[s] + 1];
@@ -947,30 +948,6 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
     }
     F.fold_list.clear();
     for (int s = 0; s < ns; ++s) if (folded[s]) F.fold_list.push_back(s);
-    if (stats)
-        for (int l = 0; l < F.nlevels; ++l) {
-            double sk = 0, sr = 0, fl = 0;
-            int mk = 0, mr = 0, mm = 0, n = F.level_ptr[l + 1] - F.level_ptr[l];
-            for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
-                const int s = F.level[q];
-                sk += F.k[s]; sr += F.r[s];
-                mk = std::max(mk, F.k[s]); mr = std::max(mr, F.r[s]); mm = std::max(mm, F.k[s] + F.r[s]);
-                fl += (double)F.k[s] * F.k[s] * F.k[s] / 3 + (double)F.k[s] * F.k[s] * F.r[s] + (double)F.k[s] * F.r[s] * F.r[s];
-            }
-            int h[4] = {0, 0, 0, 0};   // m <= 16, 32, 48, 64
-            for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
-                const int m = F.k[F.level[q]] + F.r[F.level[q]];
-                if (m <= 64) ++h[(m - 1) / 16];
-            }
-            int single = 0;   // fronts with exactly one (non-folded) child
-            for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
-                const int s2 = F.level[q];
-                single += F.child_ptr[s2 + 1] - F.child_ptr[s2] - F.fold_cnt[s2] == 1;
-            }
-            std::fprintf(stderr, "mf level %2d: %6d fronts, k mean %5.1f max %3d, r mean %5.1f max %3d, m max %3d, "
-                         "m<=16/32/48/64: %d %d %d %d, flops %.3g, one child %d\n", l, n, sk / n, mk, sr / n, mr, mm, h[0], h[1], h[2],
-                         h[3], fl, single);
-        }
     // assembly map: every stored entry of H (row i >= col j) goes to the front of col j's supernode,
     // read from its block value
     std::vector<int32_t> sn_of_dof(P.n);
@@ -1090,11 +1067,12 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
             const int32_t e = B.po_ent[x];
             const int k = e >> 1;
             if ((e & 1) ? pi.o_dst[k] != p : pi.o_src[k] != p) { err = "odometry entry of the wrong pose"; return BOS_ERR_INVALID; }
-            if (e & 1) continue;
-            ++chi[pi.Mb + k];
+            if (!(e & 1)) ++chi[pi.Mb + k];
+            const int q = (e & 1) ? pi.o_src[k] : pi.o_dst[k];
             const int u = B.po_blk[x];
-            if (x + 1 == B.po_ptr[p + 1] || B.po_blk[x + 1] != u) {
-                if (u < B.uo_ptr[p] || u >= B.uo_ptr[p + 1] || B.uo_dst[u] != pi.o_dst[k] ||
+            if ((u >= 0) != (q > p)) { err = "pose-pose block on the wrong side"; return BOS_ERR_INVALID; }
+            if (u >= 0 && (x + 1 == B.po_ptr[p + 1] || B.po_blk[x + 1] != u)) {
+                if (u < B.uo_ptr[p] || u >= B.uo_ptr[p + 1] || B.uo_dst[u] != q ||
                     !mark(B.off_pp + 6 * (int64_t)u, 6)) {
                     err = "pose-pose block misplaced";
                     return BOS_ERR_INVALID;
@@ -1134,9 +1112,9 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
         }
     for (size_t v = 0; v < bhit.size(); ++v)
         if (bhit[v] != bown[v]) { err = "b entry coverage"; return BOS_ERR_INVALID; }
-    if (P.world == 1)   // single shard: every observation's chi^2 counted once
+    if (P.world == 1)   // single shard: every observation's chi^2 counted once (self-loops: by the stats)
         for (size_t k = 0; k < chi.size(); ++k)
-            if (chi[k] != 1) { err = "chi^2 of observation " + std::to_string(k) + " counted " + std::to_string(chi[k]) + " times"; return BOS_ERR_INVALID; }
+            if (chi[k] != ((k >= (size_t)pi.Mb && pi.o_src[k - pi.Mb] == pi.o_dst[k - pi.Mb]) ? 0 : 1)) { err = "chi^2 of observation " + std::to_string(k) + " counted " + std::to_string(chi[k]) + " times"; return BOS_ERR_INVALID; }
     // every stored entry reads a block value written by its owner; pose-pose blocks are symmetric
     // (off-diagonal values read twice), every other value at most once
     std::vector<uint8_t> refs(B.size, 0);

@@ -33,9 +33,9 @@ struct ProblemIndex {
 //   [off_ldiag, off_pl)   landmark diagonal blocks, 3 per landmark (00, 10, 11)
 //   [off_pl, off_pp)      pose-landmark blocks H_pl (3 x 2 row-major), 6 values per bearing slot
 //                         (below); a pair observed more than once uses the slot of its last bearing
-//   [off_pp, size)        pose-pose blocks H_sd, one per unique odometry (src, dst) pair, ordered by
-//                         src then dst; H_sd = -J_s^T Omega J_s is symmetric (J_d = -J_s), so 6
-//                         values like a diagonal block
+//   [off_pp, size)        pose-pose blocks, one per unordered pair {p < q} joined by odometry edges
+//                         (either direction), ordered by p then q: the sum of the edges' H_sd =
+//                         -J_s^T Omega J_s, symmetric (J_d = -J_s), so 6 values like a diagonal block
 // b stays in the reference dof numbering (3 per pose, then 2 per landmark; the fixed pose's entries
 // are computed but not used). Diagonal blocks and b include all nodes, the fixed pose too.
 //
@@ -67,11 +67,13 @@ struct BlockLayout {
     std::vector<int32_t> ub_ptr;        // [NP + 1] pose-landmark blocks of each pose
     std::vector<int32_t> ub_lm;         // [nub] landmark of each pose-landmark block (ascending per pose)
     std::vector<int32_t> ub_slot;       // [nub] bearing slot holding the block
-    std::vector<int32_t> po_ptr;        // [NP + 1] odometry entries of each pose
-    std::vector<int32_t> po_ent;        // edge << 1 | 1 when the pose is the destination
-    std::vector<int32_t> po_blk;        // pose-pose block of a source-side entry, -1 on the destination side
-    std::vector<int32_t> uo_ptr;        // [NP + 1] pose-pose blocks of each pose (as source)
-    std::vector<int32_t> uo_dst;        // [nuo] destination pose of each pose-pose block
+    std::vector<int32_t> po_ptr;        // [NP + 1] odometry entries of each pose (self-loops have none)
+    std::vector<int32_t> po_ent;        // edge << 1 | 1 when the pose is the destination; per pose
+                                        // sorted by (other pose, edge)
+    std::vector<int32_t> po_blk;        // pose-pose block an entry adds to when the other pose is the
+                                        // higher one (this pose stores it), else -1
+    std::vector<int32_t> uo_ptr;        // [NP + 1] pose-pose blocks stored by each pose (the lower one)
+    std::vector<int32_t> uo_dst;        // [nuo] the higher pose of each pose-pose block
     std::vector<int32_t> csr_src;       // [nnzA] block value of each stored entry of P^T H_nf P
     int nub() const { return ub_ptr.empty() ? 0 : ub_ptr.back(); }
     int nuo() const { return uo_ptr.empty() ? 0 : uo_ptr.back(); }
@@ -132,6 +134,12 @@ struct Multifrontal {
     std::vector<int32_t> fold_list;         // folded supernodes
     int64_t L_size = 0, U_size = 0, u_size = 0;
     double flops = 0;
+    // Schur plans (build_plan): whether every front fits the fast kernels (m <= kMfWaveMaxM, and
+    // m <= kMfFlowMaxM from level 2 up), the largest front from level 2 up, and the separator balance
+    // (percent) of the plan kept
+    bool fits = true;
+    int max_m_upper = 0;
+    int balance_pct = 40;
 };
 
 struct Plan {
@@ -165,6 +173,10 @@ enum FactorMode {
                               // supernode), then nested dissection of the poses on the graph of the
                               // Schur complement S = H_pp - H_pl H_ll^-1 H_lp
 };
+
+// Test hook: poses per nested-dissection leaf of the Schur ordering (0 = the default, 10). Larger
+// leaves give fronts the fast kernels do not take (exercises build_plan's fallback).
+extern int g_schur_leaf;
 
 // Builds the plan. Returns 0 or a negative BOS_ERR_* code with a message in err.
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& out, std::string& err);

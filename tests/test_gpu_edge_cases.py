@@ -2,8 +2,11 @@
 reference dataset (C1) and small synthetic worlds. Each case exercises a kernel path the
 headline configs do not: duplicate (pose, landmark) observations (summed into one block, the
 run-continuation flag), duplicate odometry pairs, poses with more than two odometry entries (loop
-closures), bearing weights (HAS_W), poses without bearings and landmarks without observations
-(empty lanes), two lanes per pose (dense poses), odd list lengths (the pair loop's tail).
+closures), odometry edges in both directions between the same poses (one shared pose-pose block
+stored by the lower pose), odometry self-loops (zero Jacobian in the reference: chi^2 only),
+bearing weights (HAS_W), poses without bearings and landmarks without observations (empty lanes),
+two lanes per pose (dense poses), odd list lengths (the pair loop's tail). Every GN step must
+report solver_info == 0.
 
 Tolerances as tests/test_gpu_parity.py: fp64 H within 1e-12 of max |H| (b 1e-11), fp32 within 2e-4;
 state after 3 GN steps within rtol 1e-6 / atol 1e-9 of the oracle's."""
@@ -59,6 +62,29 @@ def _loop_closures(P, n=30, gap=50, seed=3):
                     o_z=np.concatenate([P.o_z, z]), o_omega=np.concatenate([P.o_omega, P.o_omega[:n]]))
 
 
+def _reversed_edges(P, n=25, seed=6):
+    """Edges (d, s) added next to existing (s, d): g2o files hold such reversed loop closures, and
+    the reference sums both into H(s, d) / H(d, s) (slam/solver.cpp:48-62)."""
+    rng = np.random.default_rng(seed)
+    k = rng.choice(len(P.o_z), n, replace=False)
+    Q = to_oracle(P)
+    src, dst = P.o_dst[k].astype(np.int32), P.o_src[k].astype(np.int32)
+    z = np.array([O.predict_odometry(Q.pose_xyt[s], Q.pose_xyt[d]) for s, d in zip(src, dst)]) + rng.normal(0, 0.03, (n, 3))
+    return _variant(P, o_src=np.concatenate([P.o_src, src]), o_dst=np.concatenate([P.o_dst, dst]),
+                    o_z=np.concatenate([P.o_z, z]), o_omega=np.concatenate([P.o_omega, P.o_omega[k]]))
+
+
+def _self_loops(P, n=7, seed=7):
+    """Odometry edges (i, i): their Jacobian is zero in the reference (the two 3x3 blocks land on
+    the same columns and cancel exactly), so they add chi^2 (and may trip the robust count) only."""
+    rng = np.random.default_rng(seed)
+    p = rng.choice(P.NP, n, replace=False).astype(np.int32)
+    z = rng.normal(0, 0.05, (n, 3))
+    z[0] = (2.0, -1.0, 0.5)   # rho far above the kernel threshold
+    return _variant(P, o_src=np.concatenate([P.o_src, p]), o_dst=np.concatenate([P.o_dst, p]),
+                    o_z=np.concatenate([P.o_z, z]), o_omega=np.concatenate([P.o_omega, P.o_omega[:n]]))
+
+
 def _weights(P, seed=4):
     rng = np.random.default_rng(seed)
     return _variant(P, b_omega=rng.uniform(0.5, 2.0, len(P.b_z)))
@@ -80,20 +106,27 @@ CASES = {
     "loop_closures": _loop_closures,
     "weights": _weights,
     "poses_without_bearings": _poses_without_bearings,
-    "everything": lambda P: _weights(_loop_closures(_dup_odometry(_dup_bearings(_poses_without_bearings(P))))),
+    "reversed_edges": _reversed_edges,
+    "self_loops": _self_loops,
+    "everything": lambda P: _self_loops(_reversed_edges(_weights(_loop_closures(_dup_odometry(_dup_bearings(
+        _poses_without_bearings(P))))))),
 }
 
 
 def _steps_match(P, precision=bos.BOS_FP64, n=3, rtol=1e-6):
     Q = to_oracle(P)
     S = bos.Solver(P, precision=precision)
+    chis = []
     for _ in range(n):
-        S.step()
+        st = S.step()
+        assert st["solver_info"] == 0
+        chis.append(st["chi2"])
     pg, lg = S.get_state()
     S.close()
     po, lo = Q.copy_state()
-    for _ in range(n):
-        O.step(Q, po, lo)
+    for i in range(n):
+        c, _, _ = O.step(Q, po, lo)
+        assert abs(chis[i] - c) <= 1e-9 * max(c, 1.0), (i, chis[i], c)
     return close_state(pg, lg, po, lo, rtol=rtol)
 
 

@@ -200,11 +200,97 @@ def test_plan_exchange_covers_every_rank(world, which):
 
 @pytest.mark.parametrize("seed", [1, 2, 3, 4])
 def test_schur_plan_fronts_fit_the_wave_kernels(seed):
-    """The Schur plan retries other separator balances until no front exceeds one wavefront's
-    rows (m <= 64): the default 40 % leaves a 66-row front on some of these worlds."""
+    """The Schur plan retries other separator balances until every front fits the fast kernels:
+    m <= 64 (one wavefront) everywhere and m <= 48 (the dataflow launch) from level 2 up; the
+    default 40 % leaves a 66-row front on some of these worlds."""
     P = bos.synthetic(30000, 60000, 10, seed=seed)
     info = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR)
-    assert info["mf_max_front"] <= 64
+    assert info["mf_fits"]
+    assert info["mf_max_front"] <= 64 and info["mf_max_front_upper"] <= 48
+    assert info["mf_balance_pct"] in (40, 35, 45, 30, 20)
+
+
+def test_schur_plan_fallback_keeps_a_valid_plan():
+    """When no separator balance fits (forced here with 40-pose leaves: every leaf front has more
+    than 64 rows), the first (40 %) plan is kept; it still validates and solves like SciPy."""
+    P = bos.load_g2o(C1)
+    L = bos.lib()
+    L.bos_debug_set_schur_leaf(40)
+    try:
+        info = bos.plan_inspect(P, 0, 1, entries=True, solver=bos.BOS_SOLVER_SCHUR)
+    finally:
+        L.bos_debug_set_schur_leaf(0)
+    assert not info["mf_fits"] and info["mf_balance_pct"] == 40 and info["mf_max_front"] > 64
+    Q = to_oracle(P)
+    lin = O.linearize(Q)
+    Hl = oracle_lower_nf(Q, lin).tocsr()
+    vals = np.asarray(Hl[info["rows"], info["cols"]]).ravel()
+    perm = info["perm_to_ref"][:info["n"]]
+    L.bos_debug_set_schur_leaf(40)
+    try:
+        x = bos.plan_mf_selftest(P, vals, lin.b[perm], solver=bos.BOS_SOLVER_SCHUR)
+    finally:
+        L.bos_debug_set_schur_leaf(0)
+    Hf = (Hl + sp.tril(Hl, -1).T).tocsc()
+    keep = np.ones(P.N, dtype=bool)
+    keep[3 * P.fixed:3 * P.fixed + 3] = False
+    idx = np.nonzero(keep)[0]
+    xr = np.zeros(P.N)
+    xr[idx] = spla.spsolve(Hf[idx][:, idx], lin.b[idx])
+    assert np.abs(x - xr[perm]).max() <= 1e-8 * np.abs(xr).max()
+
+
+def _with_odometry(P, src, dst, z, om):
+    return bos.Problem(P.pose_xyt, P.lm_xy, P.b_pose, P.b_lm, P.b_z, np.concatenate([P.o_src, src]),
+                       np.concatenate([P.o_dst, dst]), np.concatenate([P.o_z, z]), np.concatenate([P.o_omega, om]),
+                       P.fixed, pose_ids=P.pose_ids, lm_ids=P.lm_ids)
+
+
+@pytest.mark.parametrize("solver", [bos.BOS_SOLVER_SCHUR, bos.BOS_SOLVER_SUPERNODAL, bos.BOS_SOLVER_ROCSOLVER_RF])
+def test_plan_accepts_reversed_edges_and_self_loops(solver):
+    """Inputs the reference handles (slam/solver.cpp:48-62): odometry edges in both directions
+    between two poses, and self-loops. The plan validates (every block written once), the reversed
+    pair shares one pose-pose block, and the multifrontal tree still solves like SciPy."""
+    P = bos.load_g2o(C1)
+    k = np.arange(0, 40, 4)
+    src = np.concatenate([P.o_dst[k], [5, 77]]).astype(np.int32)
+    dst = np.concatenate([P.o_src[k], [5, 77]]).astype(np.int32)
+    z = np.zeros((len(src), 3))
+    z[:len(k)] = -P.o_z[k]
+    om = np.concatenate([P.o_omega[k], P.o_omega[:2]])
+    V = _with_odometry(P, src, dst, z, om)
+    info = bos.plan_inspect(V, 0, 1, entries=True, solver=solver)
+    base = bos.plan_inspect(P, 0, 1, solver=solver)
+    assert info["nnz_lower"] == base["nnz_lower"]   # no new structure: same pairs, loops add nothing
+    if solver == bos.BOS_SOLVER_ROCSOLVER_RF:
+        return
+    Q = to_oracle(V)
+    lin = O.linearize(Q)
+    Hl = oracle_lower_nf(Q, lin).tocsr()
+    vals = np.asarray(Hl[info["rows"], info["cols"]]).ravel()
+    perm = info["perm_to_ref"][:info["n"]]
+    x = bos.plan_mf_selftest(V, vals, lin.b[perm], solver=solver)
+    Hf = (Hl + sp.tril(Hl, -1).T).tocsc()
+    keep = np.ones(V.N, dtype=bool)
+    keep[3 * V.fixed:3 * V.fixed + 3] = False
+    idx = np.nonzero(keep)[0]
+    xr = np.zeros(V.N)
+    xr[idx] = spla.spsolve(Hf[idx][:, idx], lin.b[idx])
+    assert np.abs(x - xr[perm]).max() <= 1e-8 * np.abs(xr).max()
+
+
+def test_oracle_self_loop_adds_chi2_only():
+    """The oracle's self-loop semantics (J_s + J_d = 0 exactly): H and b are those of the problem
+    without the loop; chi^2 grows by the loop's rho = z^T Omega z (theta wrapped)."""
+    P = bos.load_g2o(C1)
+    z = np.array([[0.3, -0.2, 0.1]])
+    om = P.o_omega[:1]
+    V = _with_odometry(P, np.array([9], np.int32), np.array([9], np.int32), z, om)
+    a, b = O.linearize(to_oracle(P)), O.linearize(to_oracle(V))
+    assert np.array_equal(a.pose_diag, b.pose_diag) and np.array_equal(a.b, b.b)
+    assert np.all(b.hoff[-1] == 0.0)
+    e = -z[0]
+    assert abs(b.chi2 - a.chi2 - e @ om[0] @ e) < 1e-12
 
 
 def test_parallel_g2o_parser_equals_line_parser(tmp_path, monkeypatch):
@@ -221,9 +307,11 @@ def test_parallel_g2o_parser_equals_line_parser(tmp_path, monkeypatch):
         f.write("\n" * (3 << 20))
     keys = ("pose_xyt", "lm_xy", "b_pose", "b_lm", "b_z", "o_src", "o_dst", "o_z", "o_omega", "pose_ids", "lm_ids")
     for p in (C1, path):
-        monkeypatch.setenv("BOS_G2O_SIMPLE", "1")
-        A = bos.load_g2o(p)
-        monkeypatch.delenv("BOS_G2O_SIMPLE")
+        bos.lib().bos_debug_set_g2o_parser(1)
+        try:
+            A = bos.load_g2o(p)
+        finally:
+            bos.lib().bos_debug_set_g2o_parser(0)
         B = bos.load_g2o(p)
         assert A.fixed == B.fixed
         for k in keys:
