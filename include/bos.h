@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define BOS_ABI_VERSION 1
+#define BOS_ABI_VERSION 2
 
 /* status codes */
 #define BOS_OK 0
@@ -79,9 +79,11 @@ typedef struct bos_options {
     int32_t device;                 /* HIP device ordinal, -1 = current                          */
     int32_t rank;                   /* shard index (0 for one GPU)                               */
     int32_t world_size;             /* number of shards (1 for one GPU)                          */
-    const void* nccl_unique_id;     /* 128-byte ncclUniqueId; required when world_size > 1. Given
-                                       with world_size 1 it still creates the communicator and runs
-                                       the exchange collectives (single-GPU test of that path)     */
+    const void* nccl_unique_id;     /* 128-byte ncclUniqueId: bos_step runs the sharded step's two
+                                       exchanges as RCCL all-gathers. NULL with world_size > 1:
+                                       external exchange, the caller drives bos_step_phase and moves
+                                       the buffers (bos_exchange_*). Given with world_size 1 it runs
+                                       the sharded phases and RCCL with one rank (one-GPU test)      */
     double kernel_threshold;        /* robust kernel threshold, reference default 1.0 (:16)      */
     double damping;                 /* damping factor, reference default 0.01 (:17)              */
     void* stream;                   /* hipStream_t to launch on, NULL = the handle's own stream  */
@@ -108,11 +110,11 @@ typedef struct bos_system_info {
     int64_t nnz_factor;             /* entries of the Cholesky factor (sparse solver)            */
     int64_t algorithmic_bytes;      /* SURVEY §8(d) J+H bytes for this problem and precision      */
     int64_t num_block_values;       /* size of the block array of H the J+H kernel writes        */
-    int32_t lanes_per_pose;         /* J+H work split: lanes per pose (1, 2 or 4)                */
-    int32_t owned_first_pose;       /* this shard's poses [first, last) and landmarks            */
-    int32_t owned_last_pose;
-    int32_t owned_first_landmark;
-    int32_t owned_last_landmark;
+    int32_t lanes_per_pose;         /* J+H work split: lanes per pose (1 or 2)                   */
+    int32_t pose_lane_groups;       /* J+H pose lane groups this rank runs (own, padding, top)   */
+    int32_t landmark_lanes;         /* J+H landmark lanes this rank runs                         */
+    int32_t own_fronts;             /* multifrontal fronts of this rank's subtrees               */
+    int32_t top_fronts;             /* fronts of the replicated top (0 on one GPU)               */
 } bos_system_info;
 
 void bos_default_options(bos_options* opt);
@@ -158,6 +160,25 @@ int bos_system_info_get(const struct bos_solver* s, bos_system_info* info);
  */
 int bos_export_system(const struct bos_solver* s, int64_t capacity, int32_t* rows, int32_t* cols, double* vals,
                       double* b);
+/*
+ * Multi-GPU (one process per GPU, world_size > 1, BOS_SOLVER_SCHUR / _SUPERNODAL). The sparse
+ * Cholesky's assembly tree is cut into per-rank subtrees below a replicated top; each rank builds
+ * the part of H its fronts read (its own and the top nodes' J+H lanes), factors its subtrees, and
+ * two all-gathers per iteration move the subtree roots' update matrices (exchange 1) and the
+ * boundary solution (exchange 2). With a communicator bos_step does everything. Without one
+ * (external exchange) the caller runs, per iteration:
+ *   bos_step_phase(s, 0); all-gather of every rank's exchange-1 buffer (bos_exchange_download /
+ *   bos_exchange_upload, rank order); bos_step_phase(s, 1); the same for exchange 2;
+ *   bos_step_phase(s, 2, stats)   (synchronous, like bos_step).
+ * After a step a rank's state is current on the nodes it owns, the top and the boundary nodes
+ * (bos_node_owner: owning rank per node, -1 top, -2 fixed pose); merge per owner for the full state.
+ */
+int bos_step_phase(struct bos_solver* s, int32_t phase, bos_step_stats* stats);
+int bos_exchange_size(const struct bos_solver* s, int32_t which, int64_t* doubles_per_rank);
+int bos_exchange_download(struct bos_solver* s, int32_t which, double* send);
+int bos_exchange_upload(struct bos_solver* s, int32_t which, const double* recv_all_ranks);
+int bos_node_owner(const struct bos_solver* s, int32_t* owner);
+
 /* State read/write in stix order (State::poses / landmarks, framework/state.hpp:47-48) */
 int bos_get_state(const struct bos_solver* s, double* pose_xyt, double* landmark_xy);
 int bos_set_state(struct bos_solver* s, const double* pose_xyt, const double* landmark_xy);

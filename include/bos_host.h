@@ -55,14 +55,24 @@ typedef struct bos_plan_info {
     int64_t mf_fits;                /* Schur: every front fits the fast kernels (m <= 64, m <= 48 from level 2 up) */
     int64_t mf_max_front_upper;     /* Schur: largest front from tree level 2 up                  */
     int64_t mf_balance_pct;         /* Schur: separator balance of the plan kept (40 = first try)   */
+    /* multi-GPU shard of rank `rank` (multifrontal solvers; one GPU: everything own, no top) */
+    int64_t shard_own_fronts;       /* fronts of this rank's subtrees                             */
+    int64_t shard_top_fronts;       /* fronts of the replicated top                               */
+    int64_t shard_roots;            /* this rank's subtree roots below the top (exchange 1)       */
+    int64_t shard_ex1_doubles;      /* exchange 1 buffer per rank (doubles)                        */
+    int64_t shard_ex2_doubles;      /* exchange 2 buffer per rank (doubles)                        */
+    int64_t shard_pose_lanes;       /* J+H pose lane groups (own, padding, top)                    */
+    int64_t shard_own_pose_lanes;
+    int64_t shard_lm_lanes;
+    int64_t shard_update_nodes;     /* nodes the box-plus updates (own, top, boundary)             */
 } bos_plan_info;
 
 /* Build the static plan on the host (what bos_create does before touching the GPU) for solver
  * `solver` (BOS_SOLVER_*: it selects the ordering).
  * If ref_rows/ref_cols/owned are given (capacity >= nnz_lower) they receive, for every stored
  * entry of the lower triangle of H_nf, its (row, col) in the reference dof numbering
- * (row >= col) and whether rank `rank` of `world` writes it; b_owned (n + 3 entries, reference
- * order of the N dofs minus nothing: indexed by reference dof) marks the b entries it writes;
+ * (row >= col) and whether rank `rank` of `world` computes it (its J+H lanes write the block);
+ * b_owned (n + 3 entries, indexed by reference dof) marks the b entries its lanes write;
  * perm_to_ref (n + 3 entries) maps the permuted dof order used on the device to reference dofs. */
 int bos_plan_inspect(const bos_problem* problem, int32_t solver, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
                      int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref, bos_plan_info* info);
@@ -72,10 +82,18 @@ int bos_plan_inspect(const bos_problem* problem, int32_t solver, int32_t rank, i
  * dof order). Not used by any solve. */
 int bos_plan_mf_selftest(const bos_problem* problem, int32_t solver, const double* vals, const double* rhs, double* x);
 
-/* Test hook: the sharded exchange (pack / all-gather / unpack of every rank's pieces of H and b)
- * simulated on the host for all `world` ranks; BOS_OK when every rank ends with every value the
- * solver reads and every b entry but the fixed pose's. */
-int bos_plan_exchange_selftest(const bos_problem* problem, int32_t world);
+/* Owner of every node (NP poses, then NL landmarks) when the multifrontal solve is sharded over
+ * `world` ranks: the rank, -1 for the replicated top, -2 for the fixed pose. */
+int bos_plan_node_owner(const bos_problem* problem, int32_t solver, int32_t world, int32_t* owner);
+
+/* Test hook: the sharded GN solve (plan.hpp Shard) simulated on the host for all `world` ranks,
+ * both exchanges included: per-rank plans, each rank's J+H outputs only, subtree factorization,
+ * exchange 1, replicated top, backward, exchange 2. BOS_OK when the merged solution x (permuted
+ * order, n) equals the one-rank solution bit for bit, the ranks agree on the top, every observation's
+ * chi^2 is counted by one rank and every node a rank's J+H reads is kept current by its box-plus.
+ * vals / rhs as for bos_plan_mf_selftest. */
+int bos_plan_shard_selftest(const bos_problem* problem, int32_t solver, int32_t world, const double* vals,
+                            const double* rhs, double* x);
 
 /* Benchmark helpers (bench.py; HIP events on the handle's stream, no torch):
  * bos_time_linearize: n J+H builds (+ the exchange when sharded). flush_caches = 0: back to back,

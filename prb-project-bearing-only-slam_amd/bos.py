@@ -40,7 +40,9 @@ EXPORTED_SYMBOLS = [
     "bos_dataset_load_g2o", "bos_dataset_synthetic", "bos_dataset_problem", "bos_dataset_pose_ids",
     "bos_dataset_landmark_ids", "bos_dataset_fixed_pose_id", "bos_dataset_bound", "bos_dataset_ground_truth",
     "bos_dataset_write_g2o", "bos_dataset_free", "bos_plan_inspect", "bos_plan_mf_selftest",
-    "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async", "bos_plan_exchange_selftest",
+    "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async", "bos_plan_shard_selftest",
+    "bos_plan_node_owner", "bos_step_phase", "bos_exchange_size", "bos_exchange_download", "bos_exchange_upload",
+    "bos_node_owner",
     "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall",
     "bos_time_linearize", "bos_time_triangulate",
 ]
@@ -79,9 +81,8 @@ class bos_step_stats(ctypes.Structure):
 class bos_system_info(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("nnz_lower", ctypes.c_int64), ("nnz_factor", ctypes.c_int64),
                 ("algorithmic_bytes", ctypes.c_int64), ("num_block_values", ctypes.c_int64),
-                ("lanes_per_pose", ctypes.c_int32), ("owned_first_pose", ctypes.c_int32),
-                ("owned_last_pose", ctypes.c_int32), ("owned_first_landmark", ctypes.c_int32),
-                ("owned_last_landmark", ctypes.c_int32)]
+                ("lanes_per_pose", ctypes.c_int32), ("pose_lane_groups", ctypes.c_int32),
+                ("landmark_lanes", ctypes.c_int32), ("own_fronts", ctypes.c_int32), ("top_fronts", ctypes.c_int32)]
 
 
 class bos_plan_info(ctypes.Structure):
@@ -91,7 +92,12 @@ class bos_plan_info(ctypes.Structure):
                 ("ordering", ctypes.c_char * 32), ("mf_supernodes", ctypes.c_int64),
                 ("mf_levels", ctypes.c_int64), ("mf_max_front", ctypes.c_int64), ("mf_flops", ctypes.c_double),
                 ("mf_update_bytes", ctypes.c_int64), ("mf_fits", ctypes.c_int64),
-                ("mf_max_front_upper", ctypes.c_int64), ("mf_balance_pct", ctypes.c_int64)]
+                ("mf_max_front_upper", ctypes.c_int64), ("mf_balance_pct", ctypes.c_int64),
+                ("shard_own_fronts", ctypes.c_int64), ("shard_top_fronts", ctypes.c_int64),
+                ("shard_roots", ctypes.c_int64), ("shard_ex1_doubles", ctypes.c_int64),
+                ("shard_ex2_doubles", ctypes.c_int64), ("shard_pose_lanes", ctypes.c_int64),
+                ("shard_own_pose_lanes", ctypes.c_int64), ("shard_lm_lanes", ctypes.c_int64),
+                ("shard_update_nodes", ctypes.c_int64)]
 
 
 _lib = None
@@ -145,7 +151,14 @@ def lib():
                                             ctypes.c_int64, _ip, _ip, ctypes.POINTER(ctypes.c_uint8),
                                             ctypes.POINTER(ctypes.c_uint8), _ip, ctypes.POINTER(bos_plan_info)]),
         "bos_plan_mf_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, _dp, _dp, _dp]),
-        "bos_plan_exchange_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32]),
+        "bos_plan_shard_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32, _dp,
+                                                   _dp, _dp]),
+        "bos_plan_node_owner": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32, _ip]),
+        "bos_step_phase": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.POINTER(bos_step_stats)]),
+        "bos_exchange_size": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
+        "bos_exchange_download": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
+        "bos_exchange_upload": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
+        "bos_node_owner": (ctypes.c_int, [vp, _ip]),
         "bos_debug_set_schur_leaf": (None, [ctypes.c_int32]),
         "bos_debug_set_g2o_parser": (None, [ctypes.c_int32]),
         "bos_debug_inject_stall": (ctypes.c_int, [vp]),
@@ -304,6 +317,7 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
            "mf_levels": info.mf_levels, "mf_max_front": info.mf_max_front, "mf_flops": info.mf_flops,
            "mf_update_bytes": info.mf_update_bytes, "mf_fits": bool(info.mf_fits),
            "mf_max_front_upper": info.mf_max_front_upper, "mf_balance_pct": info.mf_balance_pct}
+    out.update({k: getattr(info, k) for k, _ in bos_plan_info._fields_ if k.startswith("shard_")})
     if entries:
         nnz = info.nnz_lower
         rows = np.zeros(nnz, dtype=np.int32)
@@ -329,11 +343,25 @@ def plan_mf_selftest(P: Problem, vals, rhs, solver: int = BOS_SOLVER_SUPERNODAL)
     return x
 
 
-def plan_exchange_selftest(P: Problem, world: int) -> None:
-    """Host simulation of the sharded exchange for all `world` ranks (test hook); raises if a rank
-    would miss a value of H or b after the all-gather."""
+def plan_shard_selftest(P: Problem, world: int, vals, rhs, solver: int = BOS_SOLVER_SCHUR):
+    """Host simulation of the sharded solve over `world` ranks, exchanges included (test hook):
+    raises unless the merged solution equals the one-rank solution bit for bit and every rank's J+H
+    reads only nodes its box-plus keeps current; returns x (permuted order)."""
     cs = P.c_struct()
-    _check(lib().bos_plan_exchange_selftest(ctypes.byref(cs), world), "plan_exchange_selftest")
+    v = np.ascontiguousarray(vals, dtype=np.float64)
+    b = np.ascontiguousarray(rhs, dtype=np.float64)
+    x = np.zeros_like(b)
+    _check(lib().bos_plan_shard_selftest(ctypes.byref(cs), solver, world, _ptr(v, ctypes.c_double),
+                                         _ptr(b, ctypes.c_double), _ptr(x, ctypes.c_double)), "plan_shard_selftest")
+    return x
+
+
+def plan_node_owner(P: Problem, world: int, solver: int = BOS_SOLVER_SCHUR) -> np.ndarray:
+    """Owner rank of every node (poses, then landmarks) of a `world`-rank shard; -1 top, -2 fixed pose."""
+    cs = P.c_struct()
+    o = np.zeros(P.NP + P.NL, dtype=np.int32)
+    _check(lib().bos_plan_node_owner(ctypes.byref(cs), solver, world, _ptr(o, ctypes.c_int32)), "plan_node_owner")
+    return o
 
 
 def nccl_unique_id() -> bytes:
@@ -415,6 +443,34 @@ class Solver:
         _check(lib().bos_debug_linearize_timeline(self._h, n.value, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                                                   ctypes.byref(n)), "timeline")
         return out
+
+    # ---- sharded (multi-GPU) step, external exchange: see include/bos.h
+    def step_phase(self, phase: int):
+        st = bos_step_stats()
+        _check(lib().bos_step_phase(self._h, phase, ctypes.byref(st)), f"bos_step_phase({phase})")
+        if phase == 2:
+            self.last_stats = st.as_dict()
+            return self.last_stats
+        return None
+
+    def exchange_size(self, which: int) -> int:
+        n = ctypes.c_int64(0)
+        _check(lib().bos_exchange_size(self._h, which, ctypes.byref(n)), "bos_exchange_size")
+        return n.value
+
+    def exchange_download(self, which: int) -> np.ndarray:
+        out = np.zeros(self.exchange_size(which))
+        _check(lib().bos_exchange_download(self._h, which, _ptr(out, ctypes.c_double)), "bos_exchange_download")
+        return out
+
+    def exchange_upload(self, which: int, all_ranks: np.ndarray):
+        a = np.ascontiguousarray(all_ranks, dtype=np.float64)
+        _check(lib().bos_exchange_upload(self._h, which, _ptr(a, ctypes.c_double)), "bos_exchange_upload")
+
+    def node_owner(self) -> np.ndarray:
+        o = np.zeros(self.P.NP + self.P.NL, dtype=np.int32)
+        _check(lib().bos_node_owner(self._h, _ptr(o, ctypes.c_int32)), "bos_node_owner")
+        return o
 
     def debug_inject_stall(self):
         """Test hook: the next step's factor dataflow launch skips its first front (a stalled

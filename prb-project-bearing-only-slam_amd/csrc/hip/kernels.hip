@@ -202,9 +202,10 @@ __device__ __forceinline__ void put_pl(T* blkp, const T o[6], T acc[6], bool las
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP>
 __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, double& chi, int& nrob,
                                            unsigned long long* st) {
-    const int g = P.p_begin * LPP + blk * kBlock + threadIdx.x;   // lane; shards start at a wave
-    const int p = g / LPP, sub = g % LPP, t = g & 63;
-    const bool active = p < P.p_end;
+    const int g = blk * kBlock + threadIdx.x;   // lane
+    const int grp = g / LPP, sub = g % LPP, t = g & 63;
+    const int p = grp < P.n_groups ? P.lane_pose[grp] : -1;
+    const bool active = p >= 0;
     T h[6] = {0, 0, 0, 0, 0, 0}, gb[3] = {0, 0, 0};
     if (active) {
         // Dependent load stages, the bearing chain (count/base -> records -> landmarks) and the
@@ -314,8 +315,8 @@ __device__ __forceinline__ void landmark_bearing(const LinParams<T>& P, const V4
 
 template <typename T, bool HAS_W>
 __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int blk, unsigned long long* st) {
-    const int g = P.l_begin + blk * kBlock + threadIdx.x;   // lane; shards start at a lane window
-    if (g >= P.l_end) return;
+    const int g = blk * kBlock + threadIdx.x;   // lane
+    if (g >= P.n_lm_lanes) return;
     const int l = P.ll_lm[g];
     const int n = P.ll_cnt[g];
     const int sl = P.lw_base[g >> 6] + (g & 63);
@@ -400,13 +401,15 @@ __device__ __forceinline__ double nan_max(double a, double b) { return (a != a |
 // State::apply_boxplus (framework/state.cpp:69-80): dx = -x (the solve ran on +b). Skipped (state
 // untouched) when the solver reports an aborted factorization.
 template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_kernel(const UpdateParams<T> U) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = U.nodes ? (t < U.n_nodes ? U.nodes[t] : -1) : t;
     double m = 0.0;
     if (U.info && (*U.info & kStepAbort)) {
         if (threadIdx.x == 0) U.max_part[blockIdx.x] = 0.0;
         return;
     }
-    if (i < U.NP) {
+    if (i < 0) {
+    } else if (i < U.NP) {
         if (i != U.fixed) {
             const int d = U.node_dof[i];
             const double dx = -U.x[d], dy = -U.x[d + 1], dth = -U.x[d + 2];
@@ -572,6 +575,82 @@ __global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* seg
         dst[i] = src[i];
 }
 
+__global__ __launch_bounds__(256) void shard_header1_kernel(const double* chi_part, const int32_t* nrob_part, int n,
+                                                           double* send1) {
+    __shared__ double sc[256];
+    __shared__ long long sr[256];
+    double c = 0.0;
+    long long r = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) { c += chi_part[i]; r += nrob_part[i]; }
+    sc[threadIdx.x] = c;
+    sr[threadIdx.x] = r;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) { sc[threadIdx.x] += sc[threadIdx.x + o]; sr[threadIdx.x] += sr[threadIdx.x + o]; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { send1[0] = sc[0]; send1[1] = (double)sr[0]; }
+}
+
+// per-block max |x| over the dofs of a node list (poses 3 dofs, landmarks 2)
+__global__ __launch_bounds__(256) void node_absmax_kernel(const double* x, const int32_t* nodes, int n,
+                                                          const int32_t* node_dof, int NP, double* part) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    double m = 0.0;
+    if (t < n) {
+        const int u = nodes[t], d = node_dof[u];
+        m = nan_max(fabs(x[d]), fabs(x[d + 1]));
+        if (u < NP) m = nan_max(m, fabs(x[d + 2]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o));
+    __shared__ double sm[4];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = nan_max(nan_max(sm[0], sm[1]), nan_max(sm[2], sm[3]));
+}
+
+// block 0 thread 0: header (max of the partials, the solver word, which is then zeroed); every
+// thread: the boundary payload
+__global__ __launch_bounds__(256) void shard_pack2_kernel(const double* x, const double* part, int n_part, int32_t* info,
+                                                          const int32_t* bnd, int n_bnd, double* send2) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        double m = 0.0;
+        for (int i = 0; i < n_part; ++i) m = nan_max(m, part[i]);
+        send2[0] = m;
+        send2[1] = (double)*info;
+        *info = 0;
+    }
+    for (int i = t; i < n_bnd; i += gridDim.x * blockDim.x) send2[2 + i] = x[bnd[i]];
+}
+
+__global__ void index_copy_kernel(const double* src, const int32_t* si, double* dst, const int32_t* di, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[di ? di[i] : i] = src[si ? si[i] : i];
+}
+
+__global__ void shard_combine_kernel(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
+                                     double chi_const, int32_t nrob_const, int first, StepStatus* out) {
+    if (threadIdx.x != 0) return;
+    double chi = 0.0, m = 0.0;
+    long long nr = 0, piv = 0;
+    int32_t abort_bits = 0;
+    for (int q = 0; q < world; ++q) {
+        chi += recv1[q * c1];
+        nr += (long long)recv1[q * c1 + 1];
+        m = nan_max(m, recv2[q * c2]);
+        const int32_t inf = (int32_t)recv2[q * c2 + 1];
+        piv += inf & ~kStepAbort;
+        abort_bits |= inf & kStepAbort;
+    }
+    out->chi2 = chi + chi_const;
+    out->n_robust = (int32_t)nr + nrob_const;
+    out->max_dx = m;
+    out->info = (int32_t)min(piv, (long long)(kStepAbort - 1)) | abort_bits;
+    out->aborted = (first ? 0 : out->aborted) | abort_bits;
+}
+
 __global__ __launch_bounds__(256) void cache_scrub_kernel(const double* buf, int64_t n, double* sink) {
     double acc = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -600,7 +679,7 @@ __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colin
 
 template <typename T, bool W, bool D, int LPP, int MINW>
 hipError_t launch_lin_k(LinParams<T> p, hipStream_t s) {
-    const int lm_blocks = (p.l_end - p.l_begin + kBlock - 1) / kBlock;
+    const int lm_blocks = (p.n_lm_lanes + kBlock - 1) / kBlock;
     const int grid = p.pose_blocks + lm_blocks;
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((linearize_kernel<T, W, D, LPP, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
@@ -630,7 +709,7 @@ hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has
 }
 
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s) {
-    const int n = p.NP + p.NL;
+    const int n = p.nodes ? p.n_nodes : p.NP + p.NL;
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL((boxplus_kernel<T>), dim3((n + kUpdateBlock - 1) / kUpdateBlock), dim3(kUpdateBlock), 0, s, p);
     return hipGetLastError();
@@ -655,6 +734,37 @@ hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part,
                                StepStatus* out, hipStream_t s) {
     hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n, chi_const, nrob_const,
                        max_part, n_max, info, (int)first, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_header1(const double* chi_part, const int32_t* nrob_part, int n_parts, double* send1,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(shard_header1_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n_parts, send1);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes, const int32_t* node_dof, int NP,
+                              int32_t* info, const int32_t* bnd, int n_bnd, double* part, double* send2,
+                              hipStream_t s) {
+    const int nb = std::max(1, (n_nodes + 255) / 256);
+    hipLaunchKernelGGL(node_absmax_kernel, dim3(nb), dim3(256), 0, s, x, nodes, n_nodes, node_dof, NP, part);
+    const int pb = std::max(1, std::min(256, (n_bnd + 255) / 256));
+    hipLaunchKernelGGL(shard_pack2_kernel, dim3(pb), dim3(256), 0, s, x, part, nb, info, bnd, n_bnd, send2);
+    return hipGetLastError();
+}
+
+hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* dst, const int32_t* dst_idx, int64_t n,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(index_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, src_idx, dst, dst_idx, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
+                                double chi_const, int32_t nrob_const, bool first, StepStatus* out, hipStream_t s) {
+    hipLaunchKernelGGL(shard_combine_kernel, dim3(1), dim3(64), 0, s, recv1, c1, recv2, c2, world, chi_const, nrob_const,
+                       (int)first, out);
     return hipGetLastError();
 }
 

@@ -20,16 +20,17 @@ constexpr int32_t kIdxMask = 0x7fffffff;
 // A lane list item is the other endpoint (landmark for the pose lists, pose for the landmark lists)
 // and the measured bearing, stored as two arrays (index, z) so each is read exactly once.
 
-// J+H build (host/plan.hpp BlockLayout). Blocks [0, pose_blocks) run lane groups of lpp lanes
-// per owned pose, the rest one lane per owned landmark. Lane lists are wave-interleaved: item j of
-// lane t of wave w is slot w_base[w] + 64 j + t.
+// J+H build (host/plan.hpp BlockLayout). Blocks [0, pose_blocks) run lane groups of lpp lanes, group
+// i for pose lane_pose[i] (-1: padding), the rest one lane per landmark lane (landmark ll_lm[g]).
+// Lane lists are wave-interleaved: item j of lane t of wave w is slot w_base[w] + 64 j + t.
 template <typename T> struct LinParams {
     // state caches (T precision): host-computed at create / set_state, then kept by the box-plus kernel
     const T* pc;          // [NP][4] x, y, cos(theta), sin(theta)
     const T* pth;         // [NP] theta
     const T* lc;          // [NL][2]
     int NP;
-    int p_begin, p_end, l_begin, l_end, pose_blocks;
+    const int32_t* lane_pose;  // [n_groups] pose of each lane group, -1 = padding
+    int n_groups, n_lm_lanes, pose_blocks;
     // pose lanes
     const int32_t* pw_base;   // [waves + 1]
     const int32_t* pl_cnt;    // [NP * lpp]
@@ -73,6 +74,8 @@ template <typename T> struct UpdateParams {
     T* lc;
     double* max_part;         // [update blocks] max |dx| of each block (reduced by reduce_stats)
     const int32_t* info;      // solver status word or null; | kStepAbort => the update is skipped
+    const int32_t* nodes;     // nodes to update (sharded: own, top, boundary), null = all NP + NL
+    int n_nodes;
 };
 
 // Solver status bit: the factorization's results are invalid (a dataflow launch timed out,
@@ -119,6 +122,25 @@ hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, in
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);
 template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStream_t s);
+
+// Sharded GN step (host/plan.hpp Shard, hip/solver_capi.hip). Exchange buffers are doubles with a
+// kExHeader-double header per rank.
+// Exchange 1 header: this rank's chi^2 and robust count (sums of the J+H partials [0, n_parts)).
+hipError_t launch_shard_header1(const double* chi_part, const int32_t* nrob_part, int n_parts, double* send1,
+                                hipStream_t s);
+// Exchange 2: header = max |x| over the dofs of nodes[0, n_nodes) (the rank's own and top nodes)
+// and the solver word *info (then zeroed for the next iteration); payload = x[bnd[i]].
+hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes, const int32_t* node_dof, int NP,
+                              int32_t* info, const int32_t* bnd, int n_bnd, double* part, double* send2,
+                              hipStream_t s);
+// dst[dst_idx[i]] = src[src_idx[i]], i < n
+hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* dst, const int32_t* dst_idx, int64_t n,
+                             hipStream_t s);
+// All ranks' headers -> *out (chi^2 and robust count summed in rank order plus the self-loop
+// terms, max |dx| the max, info: non-positive pivots summed, abort bits or-ed; `aborted` sticky
+// unless first), identical on every rank.
+hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
+                                double chi_const, int32_t nrob_const, bool first, StepStatus* out, hipStream_t s);
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
 // Reduces the J+H kernel's chi^2 / robust-count partials (plus the constant terms of odometry
 // self-loops, chi_const / nrob_const) and the box-plus max |dx| partials (when max_part is set; a NaN

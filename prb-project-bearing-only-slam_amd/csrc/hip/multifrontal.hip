@@ -457,8 +457,10 @@ struct Flow {
     int* exits;             // waves that have left the launch (same life cycle)
     uint32_t* done;         // per supernode: epoch of its last completion
     uint32_t epoch;
-    const int32_t* slev;    // level of every supernode
-    int lev0;               // factor: children below this level were finished by earlier launches
+    const int8_t* fid;      // per supernode: the flow launch (id) that processes it, 0 = none; a front
+                            // waits only for fronts of its own launch (the others finished earlier:
+                            // per-level launches, the other program, or another rank's exchange)
+    int id;
 };
 
 constexpr int kStall = kMfStall;               // or-ed into info when a dependency wait times out
@@ -601,7 +603,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     wave_sync();
     if constexpr (FLOW) {
         for (int ci = a.child_ptr[s]; ci < ce; ++ci)
-            if (f->slev[a.child[ci]] >= f->lev0) wait_done(*f, a.child[ci], a.info);
+            if (f->fid[a.child[ci]] == f->id) wait_done(*f, a.child[ci], a.info);
     }
     // extend-add, children in list order (deterministic)
     if (cb < ce) child_vals<COH>(lane, p0);
@@ -773,7 +775,7 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
     stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
     for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
     if constexpr (FLOW) {
-        if (parent[s] >= 0) wait_done(*f, parent[s], a.info);
+        if (parent[s] >= 0 && f->fid[parent[s]] == f->id) wait_done(*f, parent[s], a.info);
     }
     if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
     for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
@@ -911,38 +913,22 @@ template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
 constexpr int kClasses = 5;
 inline int front_class(int m) { return m <= kMfWaveMaxM ? (m - 1) / 16 : 4; }
 
-struct MfDevice {
-    int nlevels = 0;
-    // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
-    // the level's other classes
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    static constexpr int tiny16 = 256;   // class-16 launches of at most this many fronts go to the side stream too
-    // supernodes of (level l, class c) = list[ptr[l * kClasses + c], ptr[l * kClasses + c + 1])
-    std::vector<int32_t> ptr;
+// The fronts one launch sequence processes: every front on one GPU; a rank's own subtrees or the
+// replicated top when sharded (plan.hpp Shard). Levels below flow_lev0 run per level (binned by
+// front class), the rest of the factorization as one dataflow launch; the backward solve as one
+// dataflow launch over levels >= solve_lev0 (top-down), then per level, then the folded landmarks.
+struct Prog {
+    int id = 0;                     // flow id (1: own / everything, 2: top)
+    std::vector<int32_t> ptr;       // (level l, class c) = list[ptr[l * kClasses + c], ...)
     std::vector<int> lds_factor, lds_fwd, lds_bwd;   // per (level, class): dynamic LDS bytes
     int32_t* list = nullptr;
-    // dataflow launches: the factorization of levels >= flow_lev0 (all fronts there <= 64) and both
-    // solves over the whole tree (when their LDS fits), each as one work-queue launch
-    int flow_lev0 = 0, n_flow_factor = 0, nsuper = 0, ncu = 256;
+    int flow_lev0 = 0, n_flow_factor = 0;
+    int32_t* order_factor = nullptr;
     bool flow_solve = false;
-    int solve_lev0 = 0, n_flow_solve = 0;   // solves: levels < solve_lev0 per level, the rest one flow each
-    int lds_bwd_flow = 0;
-    int32_t *order_factor = nullptr, *order_bwd = nullptr, *slev = nullptr, *parent = nullptr;
-    uint32_t* done = nullptr;   // [3][nsuper]: factor, forward, backward
-    int* tickets = nullptr;     // [2 * kMfTickets]: work-queue tickets, then the launches' exit counters
-    uint32_t epoch = 0;
-    int32_t *fold_cnt = nullptr, *fold_cptr = nullptr, *fold_chunk = nullptr, *fold_rec = nullptr,
-            *fold_list = nullptr;
+    int solve_lev0 = 0, n_flow_solve = 0, lds_bwd_flow = 0;
+    int32_t* order_bwd = nullptr;
+    int32_t* fold_list = nullptr;   // folded landmarks whose parent is in this program
     int n_fold = 0;
-    int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
-            *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
-            *info = nullptr;
-    int64_t *L_off = nullptr, *U_off = nullptr, *u_off = nullptr, *scratch_off = nullptr, *rmap_off = nullptr,
-            *findex_off = nullptr;
-    double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
-
-    // classes [c0, c1) of level lev are contiguous in the list
     int count(int lev, int c0, int c1) const { return ptr[lev * kClasses + c1] - ptr[lev * kClasses + c0]; }
     int count(int lev, int c) const { return count(lev, c, c + 1); }
     int lds_max(const std::vector<int>& v, int lev, int c0, int c1) const {
@@ -950,10 +936,33 @@ struct MfDevice {
         for (int c = c0; c < c1; ++c) b = std::max(b, v[lev * kClasses + c]);
         return b;
     }
-    MfArgs args(int lev, int c, const double* A, double* x) const {
+};
+
+struct MfDevice {
+    int nlevels = 0, nsuper = 0, ncu = 256;
+    // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
+    // the level's other classes
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    static constexpr int tiny16 = 256;   // class-16 launches of at most this many fronts go to the side stream too
+    Prog prog[2];                 // [0]: own (or every front), [1]: the replicated top (sharded only)
+    int8_t *fid_f = nullptr, *fid_b = nullptr;   // flow membership: factor, backward
+    int32_t* parent = nullptr;
+    uint32_t* done = nullptr;     // [2][nsuper]: factor, backward
+    int* tickets = nullptr;       // [2 * kMfTickets]: work-queue tickets, then the launches' exit counters
+    uint32_t epoch = 0;
+    int32_t *fold_cnt = nullptr, *fold_cptr = nullptr, *fold_chunk = nullptr, *fold_rec = nullptr;
+    int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
+            *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
+            *info = nullptr;
+    int64_t *L_off = nullptr, *U_off = nullptr, *u_off = nullptr, *scratch_off = nullptr, *rmap_off = nullptr,
+            *findex_off = nullptr;
+    double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
+
+    MfArgs args(const Prog& P, int lev, int c, const double* A, double* x) const {
         MfArgs g;
-        g.level = list + ptr[lev * kClasses + c];
-        g.count = count(lev, c);
+        g.level = P.list + (P.ptr.empty() ? 0 : P.ptr[lev * kClasses + c]);
+        g.count = P.ptr.empty() ? 0 : P.count(lev, c);
         g.col0 = col0; g.k = k; g.r = r; g.L_off = L_off; g.U_off = U_off; g.u_off = u_off;
         g.scratch_off = scratch_off; g.child_ptr = child_ptr; g.child = child; g.rmap_off = rmap_off; g.rmap = rmap;
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
@@ -963,94 +972,125 @@ struct MfDevice {
     }
 };
 
-int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
-    MfDevice* d = new MfDevice();
-    *out = d;
-    d->nlevels = F.nlevels;
-    std::vector<int64_t> scr(F.nsuper, -1);
-    int64_t scratch_size = 0;
-    for (int s = 0; s < F.nsuper; ++s) {
-        const int m = F.k[s] + F.r[s];
-        if (m > kLdsCapM) { scr[s] = scratch_size; scratch_size += (int64_t)m * m; }
-    }
+namespace {
+
+int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Prog& P, std::vector<int8_t>& fid_f,
+               std::vector<int8_t>& fid_b, std::string& err) {
+    P.id = id;
     const int L = F.nlevels;
-    d->lds_factor.assign(L * kClasses, 0); d->lds_fwd.assign(L * kClasses, 0); d->lds_bwd.assign(L * kClasses, 0);
-    d->ptr.assign(L * kClasses + 1, 0);
+    P.lds_factor.assign(L * kClasses, 0); P.lds_fwd.assign(L * kClasses, 0); P.lds_bwd.assign(L * kClasses, 0);
+    P.ptr.assign(L * kClasses + 1, 0);
+    auto mine = [&](int s) { return sel[s] == id; };
     std::vector<int32_t> lst;
     for (int l = 0; l < L; ++l)
         for (int c = 0; c < kClasses; ++c) {
             const int lc = l * kClasses + c;
             for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
                 const int s = F.level[q], k = F.k[s], m = k + F.r[s];
-                if (front_class(m) != c) continue;
+                if (!mine(s) || front_class(m) != c) continue;
                 lst.push_back(s);
                 if (c < 4) {
-                    d->lds_fwd[lc] = std::max(d->lds_fwd[lc], (m + m * k) * 8);
-                    d->lds_bwd[lc] = std::max(d->lds_bwd[lc], (2 * k + (m - k) + m * k) * 8);
+                    P.lds_fwd[lc] = std::max(P.lds_fwd[lc], (m + m * k) * 8);
+                    P.lds_bwd[lc] = std::max(P.lds_bwd[lc], (2 * k + (m - k) + m * k) * 8);
                 } else {
-                    if (m <= kLdsCapM) d->lds_factor[lc] = std::max(d->lds_factor[lc], m * m * 8);
-                    d->lds_fwd[lc] = std::max(d->lds_fwd[lc], m * 8);
-                    d->lds_bwd[lc] = std::max(d->lds_bwd[lc], 2 * k * 8);
+                    if (m <= kLdsCapM) P.lds_factor[lc] = std::max(P.lds_factor[lc], m * m * 8);
+                    P.lds_fwd[lc] = std::max(P.lds_fwd[lc], m * 8);
+                    P.lds_bwd[lc] = std::max(P.lds_bwd[lc], 2 * k * 8);
                 }
             }
             // longest fronts first (estimated by flops plus folded rows): the launch's tail is
             // then made of short fronts
-            {
-                auto cost = [&](int s2) {
-                    const double k = F.k[s2], r = F.r[s2];
-                    double c = k * k * k / 3 + k * k * r + k * r * r;
-                    if (!F.fold_cnt.empty())
-                        for (int ci = F.child_ptr[s2]; ci < F.child_ptr[s2] + F.fold_cnt[s2]; ++ci)
-                            c += 4.0 * F.r[F.child[ci]] * F.r[F.child[ci]];
-                    return c;
-                };
-                std::stable_sort(lst.begin() + d->ptr[lc], lst.end(), [&](int x, int y) { return cost(x) > cost(y); });
-            }
-            d->ptr[lc + 1] = (int32_t)lst.size();
+            auto cost = [&](int s2) {
+                const double k = F.k[s2], r = F.r[s2];
+                double cc = k * k * k / 3 + k * k * r + k * r * r;
+                if (!F.fold_cnt.empty())
+                    for (int ci = F.child_ptr[s2]; ci < F.child_ptr[s2] + F.fold_cnt[s2]; ++ci)
+                        cc += 4.0 * F.r[F.child[ci]] * F.r[F.child[ci]];
+                return cc;
+            };
+            std::stable_sort(lst.begin() + P.ptr[lc], lst.end(), [&](int x, int y) { return cost(x) > cost(y); });
+            P.ptr[lc + 1] = (int32_t)lst.size();
         }
-    // dataflow set-up
+    // dataflow ranges: the lowest level from which every front of the program is <= kFlowMaxM
+    // (and >= 2) starts the factor flow; the solves run per level below 2
+    P.flow_lev0 = L;
+    while (P.flow_lev0 > 2) {
+        bool small = true;
+        for (int q = F.level_ptr[P.flow_lev0 - 1]; q < F.level_ptr[P.flow_lev0] && small; ++q)
+            small = !mine(F.level[q]) || F.k[F.level[q]] + F.r[F.level[q]] <= kFlowMaxM;
+        if (!small) break;
+        --P.flow_lev0;
+    }
+    std::vector<int32_t> ofac, ofwd;
+    for (int q = F.level_ptr[std::min(P.flow_lev0, L)]; q < F.level_ptr[L]; ++q)
+        if (mine(F.level[q])) { ofac.push_back(F.level[q]); fid_f[F.level[q]] = (int8_t)id; }
+    P.n_flow_factor = (int)ofac.size();
+    P.solve_lev0 = std::min(2, L);
+    for (int q = F.level_ptr[P.solve_lev0]; q < F.level_ptr[L]; ++q) {
+        const int s = F.level[q], k = F.k[s], m = k + F.r[s];
+        if (!mine(s)) continue;
+        ofwd.push_back(s);
+        P.lds_bwd_flow = std::max(P.lds_bwd_flow, (2 * k + (m - k) + m * k) * 8);
+    }
+    std::vector<int32_t> obwd(ofwd.rbegin(), ofwd.rend());
+    P.n_flow_solve = (int)ofwd.size();
+    P.flow_solve = P.n_flow_solve > 0 && P.lds_bwd_flow <= 48 * 1024;
+    if (!P.flow_solve) P.solve_lev0 = L;
+    else
+        for (int s : obwd) fid_b[s] = (int8_t)id;
+    std::vector<int32_t> folds;
+    for (int s : F.fold_list)
+        if (mine(F.parent[s])) folds.push_back(s);
+    P.n_fold = (int)folds.size();
+    int rc;
+    if ((rc = up(&P.list, lst, err)) || (rc = up(&P.order_factor, ofac, err)) || (rc = up(&P.order_bwd, obwd, err)) ||
+        (rc = up(&P.fold_list, folds, err)))
+        return rc;
+    return 0;
+}
+
+void free_prog(Prog& P) {
+    void* bufs[] = {P.list, P.order_factor, P.order_bwd, P.fold_list};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+}
+
+}  // namespace
+
+int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** out, std::string& err) {
+    MfDevice* d = new MfDevice();
+    *out = d;
+    d->nlevels = F.nlevels;
     d->nsuper = F.nsuper;
+    std::vector<int64_t> scr(F.nsuper, -1);
+    int64_t scratch_size = 0;
+    for (int s = 0; s < F.nsuper; ++s) {
+        const int m = F.k[s] + F.r[s];
+        if (m > kLdsCapM) { scr[s] = scratch_size; scratch_size += (int64_t)m * m; }
+    }
     {
         int dev = 0, ncu = 0;
         if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
             d->ncu = ncu;
     }
-    std::vector<int32_t> slev(F.nsuper, 0), ofac, ofwd, obwd;   // ofwd: the solve flow range, bottom-up
-    for (int l = 0; l < L; ++l)
-        for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) slev[F.level[q]] = l;
-    d->flow_lev0 = L;   // lowest level from which every front is <= kFlowMaxM (and >= 2)
-    while (d->flow_lev0 > 2) {
-        bool small = true;
-        for (int q = F.level_ptr[d->flow_lev0 - 1]; q < F.level_ptr[d->flow_lev0] && small; ++q)
-            small = F.k[F.level[q]] + F.r[F.level[q]] <= kFlowMaxM;
-        if (!small) break;
-        --d->flow_lev0;
-    }
-    for (int q = F.level_ptr[d->flow_lev0]; q < F.level_ptr[L]; ++q) ofac.push_back(F.level[q]);
-    d->n_flow_factor = (int)ofac.size();
-    // solves: the two lowest levels (many independent fronts) stay per-level launches
-    d->solve_lev0 = std::min(2, L);
-    for (int q = F.level_ptr[d->solve_lev0]; q < F.level_ptr[L]; ++q) {
-        const int s = F.level[q], k = F.k[s], m = k + F.r[s];
-        ofwd.push_back(s);
-        d->lds_bwd_flow = std::max(d->lds_bwd_flow, (2 * k + (m - k) + m * k) * 8);
-    }
-    obwd.assign(ofwd.rbegin(), ofwd.rend());
-    d->n_flow_solve = (int)ofwd.size();
-    d->flow_solve = d->n_flow_solve > 0 && d->lds_bwd_flow <= 48 * 1024;
-    if (!d->flow_solve) d->solve_lev0 = L;
-    int rc = 0;
-    if ((rc = up(&d->order_factor, ofac, err)) || (rc = up(&d->order_bwd, obwd, err)) ||
-        (rc = up(&d->slev, slev, err)) || (rc = up(&d->parent, F.parent, err)))
+    // program of every supernode: 1 = own (everything on one GPU), 2 = top, 0 = another rank's
+    std::vector<int8_t> sel(F.nsuper, 1), fid_f(F.nsuper, 0), fid_b(F.nsuper, 0);
+    if (owner)
+        for (int s = 0; s < F.nsuper; ++s) sel[s] = owner[s] == rank ? 1 : owner[s] == -1 ? 2 : 0;
+    int rc;
+    if ((rc = build_prog(F, sel, 1, d->prog[0], fid_f, fid_b, err)) ||
+        (owner && (rc = build_prog(F, sel, 2, d->prog[1], fid_f, fid_b, err))))
         return rc;
-    if (hipMalloc((void**)&d->done, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(d->done, 0, 3 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
+    if ((rc = up(&d->fid_f, fid_f, err)) || (rc = up(&d->fid_b, fid_b, err)) || (rc = up(&d->parent, F.parent, err)))
+        return rc;
+    if (hipMalloc((void**)&d->done, 2 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(d->done, 0, 2 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void**)&d->tickets, 2 * kMfTickets * sizeof(int)) != hipSuccess ||
         hipMemset(d->tickets, 0, 2 * kMfTickets * sizeof(int)) != hipSuccess) {
         err = "hipMalloc failed (multifrontal flow)";
         return -2;
     }
-    if ((rc = up(&d->list, lst, err)) || (rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
+    if ((rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
         (rc = up(&d->r, F.r, err)) || (rc = up(&d->child_ptr, F.child_ptr, err)) || (rc = up(&d->child, F.child, err)) ||
         (rc = up(&d->rmap, F.rmap, err)) || (rc = up(&d->amap_ptr, F.amap_ptr, err)) ||
         (rc = up(&d->amap_src, F.amap_src, err)) || (rc = up(&d->amap_dst, F.amap_dst, err)) ||
@@ -1058,10 +1098,8 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
         (rc = up(&d->u_off, F.u_off, err)) || (rc = up(&d->scratch_off, scr, err)) ||
         (rc = up(&d->rmap_off, F.rmap_off, err)) || (rc = up(&d->findex_off, F.findex_off, err)) ||
         (rc = up(&d->fold_cnt, F.fold_cnt, err)) || (rc = up(&d->fold_cptr, F.fold_cptr, err)) ||
-        (rc = up(&d->fold_chunk, F.fold_chunk, err)) || (rc = up(&d->fold_rec, F.fold_rec, err)) ||
-        (rc = up(&d->fold_list, F.fold_list, err)))
+        (rc = up(&d->fold_chunk, F.fold_chunk, err)) || (rc = up(&d->fold_rec, F.fold_rec, err)))
         return rc;
-    d->n_fold = (int)F.fold_list.size();
     if (hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) {
@@ -1083,7 +1121,10 @@ int mf_create(const Multifrontal& F, MfDevice** out, std::string& err) {
 
 void mf_destroy(MfDevice* d) {
     if (!d) return;
-    void* bufs[] = {d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->fold_list, d->order_factor, d->order_bwd, d->slev, d->parent, d->done, d->tickets, d->list, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
+    free_prog(d->prog[0]);
+    free_prog(d->prog[1]);
+    void* bufs[] = {d->fid_f, d->fid_b, d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->parent, d->done,
+                    d->tickets, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
     for (void* b : bufs)
@@ -1096,71 +1137,74 @@ void mf_destroy(MfDevice* d) {
 
 // info is zero on entry: zeroed at creation and, after every iteration, by the end-of-step
 // reduce_stats launch (mf_info_ptr). The work-queue tickets reset themselves (leave_flow).
-hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s) {
+hipError_t mf_factor(MfDevice* d, int which, const double* A, double* x, hipStream_t s) {
     hipError_t e;
+    const Prog& P = d->prog[which];
+    if (P.ptr.empty()) return hipSuccess;
     const uint32_t epoch = ++d->epoch;
-    for (int l = 0; l < d->flow_lev0; ++l) {
+    for (int l = 0; l < std::min(P.flow_lev0, d->nlevels); ++l) {
         int n;
-        const bool fork = d->side && d->count(l, 3) > 0;
+        const bool fork = d->side && P.count(l, 3) > 0;
         // a handful of class-16 fronts (one latency-bound round, negligible load) follow them there
-        const bool tiny16 = fork && d->count(l, 0) <= d->tiny16;
+        const bool tiny16 = fork && P.count(l, 0) <= d->tiny16;
         if (fork) {
             if ((e = hipEventRecord(d->ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(d->side, d->ev_fork, 0)) != hipSuccess)
                 return e;
-            hipLaunchKernelGGL(mf_factor_reg<64>, dim3(d->count(l, 3)), dim3(64), 0, d->side, d->args(l, 3, A, x));
-            if (tiny16 && (n = d->count(l, 0)))
-                hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, d->side, d->args(l, 0, A, x));
+            hipLaunchKernelGGL(mf_factor_reg<64>, dim3(P.count(l, 3)), dim3(64), 0, d->side, d->args(P, l, 3, A, x));
+            if (tiny16 && (n = P.count(l, 0)))
+                hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, d->side, d->args(P, l, 0, A, x));
             if ((e = hipEventRecord(d->ev_join, d->side)) != hipSuccess) return e;
         }
-        if ((n = d->count(l, 0)) && !tiny16) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(l, 0, A, x));
-        if ((n = d->count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(l, 1, A, x));
-        if ((n = d->count(l, 2))) hipLaunchKernelGGL(mf_factor_reg<48>, dim3(n), dim3(64), 0, s, d->args(l, 2, A, x));
-        if ((n = d->count(l, 3)) && !fork) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(l, 3, A, x));
+        if ((n = P.count(l, 0)) && !tiny16) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(P, l, 0, A, x));
+        if ((n = P.count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(P, l, 1, A, x));
+        if ((n = P.count(l, 2))) hipLaunchKernelGGL(mf_factor_reg<48>, dim3(n), dim3(64), 0, s, d->args(P, l, 2, A, x));
+        if ((n = P.count(l, 3)) && !fork) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
         if (fork && (e = hipStreamWaitEvent(s, d->ev_join, 0)) != hipSuccess) return e;
-        if ((n = d->count(l, 4))) {   // large fronts: workgroup factorization, then their forward step
-            hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), d->lds_factor[l * kClasses + 4], s,
-                               d->args(l, 4, A, x));
-            hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), d->lds_fwd[l * kClasses + 4], s,
-                               d->args(l, 4, A, x));
+        if ((n = P.count(l, 4))) {   // large fronts: workgroup factorization, then their forward step
+            hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), P.lds_factor[l * kClasses + 4], s,
+                               d->args(P, l, 4, A, x));
+            hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), P.lds_fwd[l * kClasses + 4], s,
+                               d->args(P, l, 4, A, x));
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (d->n_flow_factor > 0) {
-        const Flow f{d->order_factor, d->n_flow_factor, d->tickets, d->tickets + kMfTickets, d->done, epoch, d->slev,
-                     d->flow_lev0};
-        const int grid = std::min(d->n_flow_factor, d->ncu * 8);   // 2 waves per SIMD resident
-        hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(0, 0, A, x), f);
+    if (P.n_flow_factor > 0) {
+        const Flow f{P.order_factor, P.n_flow_factor, d->tickets, d->tickets + kMfTickets, d->done, epoch, d->fid_f, P.id};
+        const int grid = std::min(P.n_flow_factor, d->ncu * 8);   // 2 waves per SIMD resident
+        hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(P, 0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
 }
 
-hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
+hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
     // backward substitution (the forward one ran inside mf_factor): one flow launch over the levels
     // >= solve_lev0 (top-down), then per-level launches below it
     hipError_t e;
+    const Prog& P = d->prog[which];
+    if (P.ptr.empty()) return hipSuccess;
     const uint32_t epoch = ++d->epoch;
-    if (d->flow_solve) {
-        const Flow fb{d->order_bwd, d->n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1, d->done + d->nsuper,
-                      epoch, d->slev, d->solve_lev0};
-        const int grid = std::min(d->n_flow_solve, d->ncu * 8);
-        hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), d->lds_bwd_flow, s, d->args(0, 0, nullptr, x), fb,
+    if (P.flow_solve) {
+        const Flow fb{P.order_bwd, P.n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1, d->done + d->nsuper,
+                      epoch, d->fid_b, P.id};
+        const int grid = std::min(P.n_flow_solve, d->ncu * 8);
+        hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), P.lds_bwd_flow, s, d->args(P, 0, 0, nullptr, x), fb,
                            (const int32_t*)d->parent);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    for (int l = std::min(d->solve_lev0, d->nlevels) - 1; l >= 0; --l) {
+    for (int l = std::min(P.solve_lev0, d->nlevels) - 1; l >= 0; --l) {
         int n;
-        if ((n = d->count(l, 0, 4)))
-            hipLaunchKernelGGL(mf_backward_wave, dim3(n), dim3(64), d->lds_max(d->lds_bwd, l, 0, 4), s, d->args(l, 0, nullptr, x));
-        if ((n = d->count(l, 4)))
-            hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), d->lds_bwd[l * kClasses + 4], s, d->args(l, 4, nullptr, x));
+        if ((n = P.count(l, 0, 4)))
+            hipLaunchKernelGGL(mf_backward_wave, dim3(n), dim3(64), P.lds_max(P.lds_bwd, l, 0, 4), s, d->args(P, l, 0, nullptr, x));
+        if ((n = P.count(l, 4)))
+            hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), P.lds_bwd[l * kClasses + 4], s, d->args(P, l, 4, nullptr, x));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (d->n_fold > 0) {   // folded landmarks last: their rows are poses, final by now
-        MfArgs g = d->args(0, 0, nullptr, x);
-        g.level = d->fold_list;
-        g.count = d->n_fold;
-        hipLaunchKernelGGL(mf_backward_fold, dim3(((int64_t)d->n_fold * kFoldLanes + kMfBlock - 1) / kMfBlock), dim3(kMfBlock), 0, s, g);
+    if (P.n_fold > 0) {   // folded landmarks last: their rows are poses, final by now
+        MfArgs g = d->args(P, 0, 0, nullptr, x);
+        g.level = P.fold_list;
+        g.count = P.n_fold;
+        hipLaunchKernelGGL(mf_backward_fold, dim3(((int64_t)P.n_fold * kFoldLanes + kMfBlock - 1) / kMfBlock), dim3(kMfBlock), 0, s, g);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -1168,9 +1212,11 @@ hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s) {
 
 int32_t* mf_info_ptr(const MfDevice* d) { return d->info; }
 int32_t* mf_tickets_ptr(const MfDevice* d) { return d->tickets; }
+double* mf_update_ptr(const MfDevice* d) { return d->U; }
+double* mf_uvec_ptr(const MfDevice* d) { return d->u; }
 
 hipError_t mf_debug_skip_next_front(MfDevice* d, hipStream_t s) {
-    if (d->n_flow_factor == 0) return hipErrorInvalidValue;
+    if (d->prog[0].n_flow_factor == 0) return hipErrorInvalidValue;
     static const int one = 1;
     return hipMemcpyAsync(d->tickets, &one, sizeof(int), hipMemcpyHostToDevice, s);
 }

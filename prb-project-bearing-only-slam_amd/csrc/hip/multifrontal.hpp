@@ -11,14 +11,23 @@ namespace dev {
 
 struct MfDevice;
 
-// Upload the static tree / maps and allocate factor buffers. Returns 0 or < 0 with err.
-int mf_create(const Multifrontal& F, MfDevice** out, std::string& err);
+// Upload the static tree / maps and allocate factor buffers. owner (per supernode, plan.hpp
+// Shard::sn_owner) null: one GPU, every front in program 0. Otherwise program 0 = the fronts owned
+// by `rank`, program 1 = the replicated top (owner -1); other ranks' fronts are never processed.
+// Returns 0 or < 0 with err.
+int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** out, std::string& err);
 void mf_destroy(MfDevice* d);
-// Numeric factorization of H (read from the block array A through the assembly map, fp64), fused
-// with the forward substitution: x (permuted order) holds b on entry and L^{-1} b on exit.
-hipError_t mf_factor(MfDevice* d, const double* A, double* x, hipStream_t s);
-// Backward substitution: x <- L^{-T} x, completing x = H^{-1} b.
-hipError_t mf_solve(MfDevice* d, double* x, hipStream_t s);
+// Numeric factorization of a program's fronts (H read from the block array A through the assembly
+// map, fp64), fused with the forward substitution: x (permuted order) holds b on entry and L^{-1} b
+// on exit for those fronts' dofs. Sharded: program 0 (own subtrees), then — once the other ranks'
+// subtree roots' U / u are in place — program 1 (the top).
+hipError_t mf_factor(MfDevice* d, int program, const double* A, double* x, hipStream_t s);
+// Backward substitution of a program's fronts (x <- L^{-T} x); sharded: program 1, then program 0.
+hipError_t mf_solve(MfDevice* d, int program, double* x, hipStream_t s);
+// the update matrices / u-vectors (offsets Multifrontal::U_off / u_off): exchange 1 reads and
+// writes the subtree roots' there
+double* mf_update_ptr(const MfDevice* d);
+double* mf_uvec_ptr(const MfDevice* d);
 // device word of the last factorization: count of non-positive pivots, | kMfStall when a dataflow
 // launch timed out waiting for a dependency (its results are then invalid)
 int32_t* mf_info_ptr(const MfDevice* d);

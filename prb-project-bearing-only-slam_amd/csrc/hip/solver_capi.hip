@@ -3,11 +3,16 @@
 //
 // One GN iteration (reference Solver::step, slam/solver.cpp:27-97):
 //   1. linearize_kernel          J+H build into the block array of H and b (+ damping)
-//   2. [world > 1] RCCL broadcasts of every rank's owned blocks and b entries (the exchange step)
-//   3. sparse Cholesky factorization + solve: the GPU supernodal multifrontal solver (default;
+//   2. sparse Cholesky factorization + solve: the GPU supernodal multifrontal solver (default;
 //      structure analysed once, like SimplicialLDLT::analyzePattern at solver.cpp:77-80), or
 //      rocSOLVER csrrf / dense potrf-potrs on a gathered CSR copy
-//   4. boxplus_kernel            left-multiplicative box-plus with dx = -x (state.cpp:69-80)
+//   3. boxplus_kernel            left-multiplicative box-plus with dx = -x (state.cpp:69-80)
+// Sharded over world > 1 ranks (host/plan.hpp Shard, host/shard.cpp): the J+H runs this rank's own
+// and the top nodes' lanes, the multifrontal solve its subtrees, then (exchange 1, all-gather of
+// the subtree roots' U / u) the replicated top, the backward solves, then (exchange 2, all-gather
+// of the boundary solution) the box-plus of its own, top and boundary nodes. The exchanges run on
+// RCCL, or — external mode, no communicator — the caller moves the buffers between the phases
+// (bos_step_phase; tests on one GPU, gloo).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <rocblas/rocblas.h>
@@ -105,11 +110,22 @@ struct bos_solver {
     double* d_chi_part = nullptr;
     int32_t* d_nrob_part = nullptr;
     bos::dev::StepStatus* d_status = nullptr;   // end-of-iteration summary (one read-back)
-    // exchange (world > 1): own ranges packed into ex_send, all-gathered into ex_recv, unpacked
-    void *ex_send = nullptr, *ex_recv = nullptr;
-    bos::dev::ExSeg *ex_pack = nullptr, *ex_unpack = nullptr;
-    int ex_npack = 0, ex_nunpack = 0;
-    int64_t ex_count = 0, ex_maxlen_pack = 0, ex_maxlen_unpack = 0;
+    // sharded step (world > 1)
+    bool sharded = false, external = false;
+    int32_t* lane_pose = nullptr;            // J+H pose lane groups (Shard::lane_poses)
+    int chi_parts = 0;                       // J+H chi^2 partial blocks this rank counts
+    double *ex1_send = nullptr, *ex1_recv = nullptr, *ex2_send = nullptr, *ex2_recv = nullptr;
+    int64_t ex1_count = 0, ex2_count = 0;
+    bos::dev::ExSeg *ex1_pack = nullptr, *ex1_unpack = nullptr;
+    int n1p = 0, n1u = 0;
+    int64_t maxlen1p = 0, maxlen1u = 0;
+    int32_t *ex2_bnd = nullptr, *ex2_usrc = nullptr, *ex2_udst = nullptr;   // pack / unpack index lists
+    int n_bnd = 0, n_bnd_remote = 0;
+    int32_t* upd_nodes = nullptr;
+    int n_upd = 0, n_upd_local = 0;
+    double* abs_part = nullptr;
+    int phase = 0;                           // next bos_step_phase expected (external mode)
+    bool phase_first = true;
     // triangulation inputs: bearings grouped by landmark (file order), their pose and z (fp64)
     int32_t *tri_ptr = nullptr, *tri_obs = nullptr, *tri_pose = nullptr;
     double *tri_z = nullptr, *tri_scr = nullptr;
@@ -119,7 +135,7 @@ struct bos_solver {
     bos::dev::MfDevice* mf = nullptr;
     bool analyzed = false;
     ncclComm_t comm = nullptr;
-    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[8] = {};
     std::vector<int32_t> ref_dof;   // permuted dof -> reference dof (size n + 3)
     bool have_dx = false;
     // odometry self-loops: z[3] and Omega upper triangle [6] each (constant chi^2 terms)
@@ -145,7 +161,9 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.lc = (const T*)s->d_lc;
     const bos::Plan& P = s->plan;
     p.NP = s->NP;
-    p.p_begin = P.p_begin; p.p_end = P.p_end; p.l_begin = P.l_begin; p.l_end = P.l_end;
+    p.lane_pose = s->lane_pose;
+    p.n_groups = (int)P.blk.lane_pose.size();
+    p.n_lm_lanes = (int)P.blk.lm_lane_lm.size();
     p.pose_blocks = s->pose_blocks;
     p.pw_base = s->pw_base; p.pl_cnt = s->pl_cnt;
     p.pb_idx = s->pb_idx; p.pb_z = (const T*)s->pb_z; p.pb_w = (const T*)s->pb_w;
@@ -172,7 +190,9 @@ template <typename T> bos::dev::UpdateParams<T> upd_params(const bos_solver* s) 
     u.pose = s->d_pose; u.lm = s->d_lm;
     u.pc = (T*)s->d_pc; u.pth = (T*)s->d_pth; u.lc = (T*)s->d_lc;
     u.max_part = s->d_maxpart;
-    u.info = uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : nullptr;
+    u.info = s->sharded ? &s->d_status->info : uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : nullptr;
+    u.nodes = s->sharded ? s->upd_nodes : nullptr;
+    u.n_nodes = s->n_upd;
     return u;
 }
 
@@ -193,40 +213,16 @@ int enqueue_linearize(bos_solver* s) {
     return BOS_OK;
 }
 
-// RCCL exchange: every rank owns contiguous pieces of the block array (its poses' diagonal and
-// off-diagonal blocks, its landmarks' diagonal blocks) and of b. Each rank packs its pieces into one
-// buffer, one ncclAllGather of equal-size (padded) buffers moves them to every rank, and the
-// received pieces are copied to their places: every rank then holds the full system for the
-// replicated solve. (One collective instead of one broadcast per piece and rank.)
-int enqueue_exchange(bos_solver* s) {
-    if (!s->comm) return BOS_OK;
-    const ncclDataType_t ty = s->precision == BOS_FP32 ? ncclFloat : ncclDouble;
-    hipError_t e;
-    if (s->precision == BOS_FP32) {
-        e = bos::dev::launch_seg_copy<float>((float*)s->d_val, (float*)s->d_b, (float*)s->ex_send, (float*)s->ex_recv,
-                                            s->ex_pack, s->ex_npack, s->ex_maxlen_pack, s->stream);
-    } else {
-        e = bos::dev::launch_seg_copy<double>((double*)s->d_val, (double*)s->d_b, (double*)s->ex_send,
-                                             (double*)s->ex_recv, s->ex_pack, s->ex_npack, s->ex_maxlen_pack, s->stream);
-    }
-    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("exchange pack: ") + hipGetErrorString(e));
-    NC_TRY(ncclAllGather(s->ex_send, s->ex_recv, (size_t)s->ex_count, ty, s->comm, s->stream));
-    if (s->precision == BOS_FP32) {
-        e = bos::dev::launch_seg_copy<float>((float*)s->d_val, (float*)s->d_b, (float*)s->ex_send, (float*)s->ex_recv,
-                                            s->ex_unpack, s->ex_nunpack, s->ex_maxlen_unpack, s->stream);
-    } else {
-        e = bos::dev::launch_seg_copy<double>((double*)s->d_val, (double*)s->d_b, (double*)s->ex_send,
-                                             (double*)s->ex_recv, s->ex_unpack, s->ex_nunpack, s->ex_maxlen_unpack,
-                                             s->stream);
-    }
-    if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("exchange unpack: ") + hipGetErrorString(e));
-    return BOS_OK;
-}
-
-// Segment tables of the exchange (host/plan.cpp exchange_segments) and its buffers.
-int setup_exchange(bos_solver* s) {
+// Exchange tables and buffers of the sharded step (host/shard.cpp): exchange 1 by segments of the
+// update-matrix / u-vector arrays, exchange 2 by dof index lists.
+int setup_shard(bos_solver* s) {
+    const bos::Shard& S = s->plan.shard;
+    const int W = s->world;
+    int rc;
+    s->ex1_count = S.ex1_count;
+    s->ex2_count = S.ex2_count;
     std::vector<bos::ExchangeSeg> hp, hu;
-    bos::exchange_segments(s->plan, s->rank, hp, hu, s->ex_count);
+    bos::exchange1_segments(s->plan, hp, hu);
     auto conv = [](const std::vector<bos::ExchangeSeg>& v, int64_t& maxlen) {
         std::vector<bos::dev::ExSeg> o(v.size());
         for (size_t i = 0; i < v.size(); ++i) {
@@ -235,21 +231,30 @@ int setup_exchange(bos_solver* s) {
         }
         return o;
     };
-    const std::vector<bos::dev::ExSeg> pack = conv(hp, s->ex_maxlen_pack), unpack = conv(hu, s->ex_maxlen_unpack);
-    s->ex_npack = (int)pack.size();
-    s->ex_nunpack = (int)unpack.size();
-    const int W = s->world;
-    int rc;
-    if ((rc = upload(&s->ex_pack, pack)) || (rc = upload(&s->ex_unpack, unpack))) return rc;
-    if (s->precision == BOS_FP32) {
-        float *a = nullptr, *b = nullptr;
-        if ((rc = dalloc(&a, (size_t)s->ex_count)) || (rc = dalloc(&b, (size_t)s->ex_count * W))) return rc;
-        s->ex_send = a; s->ex_recv = b;
-    } else {
-        double *a = nullptr, *b = nullptr;
-        if ((rc = dalloc(&a, (size_t)s->ex_count)) || (rc = dalloc(&b, (size_t)s->ex_count * W))) return rc;
-        s->ex_send = a; s->ex_recv = b;
+    const std::vector<bos::dev::ExSeg> pack = conv(hp, s->maxlen1p), unpack = conv(hu, s->maxlen1u);
+    s->n1p = (int)pack.size();
+    s->n1u = (int)unpack.size();
+    std::vector<int32_t> bnd(S.bnd_dof.begin() + S.bnd_ptr[s->rank], S.bnd_dof.begin() + S.bnd_ptr[s->rank + 1]);
+    std::vector<int32_t> usrc, udst;
+    for (int q = 0; q < W; ++q) {
+        if (q == s->rank) continue;
+        for (int i = S.bnd_ptr[q]; i < S.bnd_ptr[q + 1]; ++i) {
+            usrc.push_back((int32_t)((int64_t)q * S.ex2_count + bos::kExHeader + (i - S.bnd_ptr[q])));
+            udst.push_back(S.bnd_dof[i]);
+        }
     }
+    s->n_bnd = (int)bnd.size();
+    s->n_bnd_remote = (int)usrc.size();
+    s->n_upd = (int)S.upd_nodes.size();
+    s->n_upd_local = S.n_upd_local;
+    if ((rc = upload(&s->ex1_pack, pack)) || (rc = upload(&s->ex1_unpack, unpack)) || (rc = upload(&s->ex2_bnd, bnd)) ||
+        (rc = upload(&s->ex2_usrc, usrc)) || (rc = upload(&s->ex2_udst, udst)) || (rc = upload(&s->upd_nodes, S.upd_nodes)) ||
+        (rc = dalloc(&s->ex1_send, (size_t)s->ex1_count)) || (rc = dalloc(&s->ex1_recv, (size_t)s->ex1_count * W)) ||
+        (rc = dalloc(&s->ex2_send, (size_t)s->ex2_count)) || (rc = dalloc(&s->ex2_recv, (size_t)s->ex2_count * W)) ||
+        (rc = dalloc(&s->abs_part, (size_t)std::max(1, (S.n_upd_local + 255) / 256))))
+        return rc;
+    HIP_TRY(hipMemset(s->ex1_send, 0, s->ex1_count * sizeof(double)));
+    HIP_TRY(hipMemset(s->ex2_send, 0, s->ex2_count * sizeof(double)));
     return BOS_OK;
 }
 
@@ -284,15 +289,32 @@ int enqueue_stats(bos_solver* s, bool with_update, bool first = true) {
     int32_t nrob_c = 0;
     if (s->precision == BOS_FP32) self_loop_terms<float>(s, chi_c, nrob_c);
     else self_loop_terms<double>(s, chi_c, nrob_c);
-    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->pose_blocks, chi_c, nrob_c,
+    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->chi_parts, chi_c, nrob_c,
                                           with_update ? s->d_maxpart : nullptr, nupd, info, first, s->d_status,
                                           s->stream));
-    if (s->comm) {
-        NC_TRY(ncclGroupStart());
-        NC_TRY(ncclAllReduce(&s->d_status->chi2, &s->d_status->chi2, 1, ncclDouble, ncclSum, s->comm, s->stream));
-        NC_TRY(ncclAllReduce(&s->d_status->n_robust, &s->d_status->n_robust, 1, ncclInt32, ncclSum, s->comm, s->stream));
-        NC_TRY(ncclGroupEnd());
-    }
+    return BOS_OK;
+}
+
+double self_loop_chi(const bos_solver* s, int32_t& nrob) {
+    double c = 0.0;
+    if (s->precision == BOS_FP32) self_loop_terms<float>(s, c, nrob);
+    else self_loop_terms<double>(s, c, nrob);
+    return c;
+}
+
+// the block array as the multifrontal solver reads it (fp64)
+const double* mf_matrix(const bos_solver* s) {
+    return s->precision == BOS_FP32 ? s->d_val64 : (const double*)s->d_val;
+}
+
+// right-hand side in elimination order, and the fp64 copy of an fp32 block array
+int enqueue_solver_inputs(bos_solver* s) {
+    const int64_t n = s->plan.n;
+    const bool f32 = s->precision == BOS_FP32;
+    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream)
+                : bos::dev::launch_gather_f64<double>((const double*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream));
+    if (f32 && uses_mf(s))
+        HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.blk.size, s->stream));
     return BOS_OK;
 }
 
@@ -301,18 +323,12 @@ int enqueue_solve(bos_solver* s, bool& ran_analysis) {
     ran_analysis = false;
     if (n == 0) return BOS_OK;
     const bool f32 = s->precision == BOS_FP32;
-    // right-hand side in elimination order
-    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream)
-                : bos::dev::launch_gather_f64<double>((const double*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream));
+    int rc;
+    if ((rc = enqueue_solver_inputs(s))) return rc;
     const rocblas_int nn = (rocblas_int)n;
     if (uses_mf(s)) {   // reads the block array through its assembly map
-        const double* A = (const double*)s->d_val;
-        if (f32) {
-            HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.blk.size, s->stream));
-            A = s->d_val64;
-        }
-        HIP_TRY(bos::dev::mf_factor(s->mf, A, s->d_rhs, s->stream));
-        HIP_TRY(bos::dev::mf_solve(s->mf, s->d_rhs, s->stream));
+        HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
+        HIP_TRY(bos::dev::mf_solve(s->mf, 0, s->d_rhs, s->stream));
         return BOS_OK;
     }
     double* A = s->d_csr64;
@@ -409,15 +425,103 @@ int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr) {
     return BOS_OK;
 }
 
-// One GN iteration. first: the first of a bos_step_n batch (resets the sticky abort flag); sync:
-// the last one (reads the status back). A factorization whose dataflow launch timed out leaves the
-// state untouched (the box-plus kernel checks the solver word) and fails the call.
-int do_step(bos_solver* s, bos_step_stats* st, bool first, bool sync) {
+// ---- sharded GN iteration in three phases (exchanges between them)
+// phase 0: J+H (own + top lanes), solver inputs, own subtrees factored (and forward-solved),
+// exchange-1 buffer packed (roots' U / u, this rank's chi^2 partials)
+int shard_phase0(bos_solver* s) {
     int rc;
     HIP_TRY(hipEventRecord(s->ev[0], s->stream));
     if ((rc = enqueue_linearize(s))) return rc;
     HIP_TRY(hipEventRecord(s->ev[1], s->stream));
-    if ((rc = enqueue_exchange(s))) return rc;
+    if ((rc = enqueue_solver_inputs(s))) return rc;
+    HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
+    double* U = bos::dev::mf_update_ptr(s->mf);
+    double* u = bos::dev::mf_uvec_ptr(s->mf);
+    HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_pack, s->n1p, s->maxlen1p, s->stream));
+    HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream));
+    HIP_TRY(hipEventRecord(s->ev[2], s->stream));
+    return BOS_OK;
+}
+
+// phase 1: the other ranks' roots in place, the top factored and solved, own subtrees solved
+// backward, exchange-2 buffer packed (max |x| of own + top, solver word, boundary solution)
+int shard_phase1(bos_solver* s) {
+    HIP_TRY(hipEventRecord(s->ev[3], s->stream));
+    double* U = bos::dev::mf_update_ptr(s->mf);
+    double* u = bos::dev::mf_uvec_ptr(s->mf);
+    HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_unpack, s->n1u, s->maxlen1u, s->stream));
+    HIP_TRY(bos::dev::mf_factor(s->mf, 1, mf_matrix(s), s->d_rhs, s->stream));
+    HIP_TRY(bos::dev::mf_solve(s->mf, 1, s->d_rhs, s->stream));
+    HIP_TRY(bos::dev::mf_solve(s->mf, 0, s->d_rhs, s->stream));
+    HIP_TRY(bos::dev::launch_shard_pack2(s->d_rhs, s->upd_nodes, s->n_upd_local, s->node_dof, s->NP,
+                                         bos::dev::mf_info_ptr(s->mf), s->ex2_bnd, s->n_bnd, s->abs_part, s->ex2_send,
+                                         s->stream));
+    HIP_TRY(hipEventRecord(s->ev[4], s->stream));
+    return BOS_OK;
+}
+
+// phase 2: boundary solution in place, step status combined from every rank's headers, box-plus of
+// own + top + boundary nodes (skipped when any rank's factorization aborted)
+int shard_phase2(bos_solver* s, bool first) {
+    HIP_TRY(hipEventRecord(s->ev[5], s->stream));
+    HIP_TRY(bos::dev::launch_index_copy(s->ex2_recv, s->ex2_usrc, s->d_rhs, s->ex2_udst, s->n_bnd_remote, s->stream));
+    int32_t nrob_c = 0;
+    const double chi_c = self_loop_chi(s, nrob_c);
+    HIP_TRY(bos::dev::launch_shard_combine(s->ex1_recv, s->ex1_count, s->ex2_recv, s->ex2_count, s->world, chi_c, nrob_c,
+                                           first, s->d_status, s->stream));
+    int rc;
+    if ((rc = enqueue_update(s))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[6], s->stream));
+    return BOS_OK;
+}
+
+int rccl_allgather(bos_solver* s, const double* send, double* recv, int64_t count) {
+    NC_TRY(ncclAllGather(send, recv, (size_t)count, ncclDouble, s->comm, s->stream));
+    return BOS_OK;
+}
+
+int finish_step(bos_solver* s, bos_step_stats* st);
+
+int do_step_sharded(bos_solver* s, bos_step_stats* st, bool first, bool sync) {
+    if (!s->comm) return fail(BOS_ERR_INVALID, "sharded handle without a communicator: drive bos_step_phase");
+    int rc;
+    if ((rc = shard_phase0(s)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
+        (rc = shard_phase1(s)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)) ||
+        (rc = shard_phase2(s, first)))
+        return rc;
+    s->have_dx = true;
+    if (!sync) return BOS_OK;
+    return finish_step(s, st);
+}
+
+// reads the status of the step just enqueued (sharded: phases 0-2), fails an aborted one
+int finish_step(bos_solver* s, bos_step_stats* st) {
+    int rc;
+    int32_t aborted = 0;
+    if ((rc = read_stats(s, st, &aborted))) return rc;
+    if (aborted) {
+        s->have_dx = false;
+        return fail(BOS_ERR_SOLVER, "sparse factorization aborted: a dataflow dependency wait timed out (state "
+                                    "left unchanged by the failed iteration)");
+    }
+    if (st && s->sharded) {
+        st->t_linearize_ms = elapsed(s->ev[0], s->ev[1]);
+        st->t_exchange_ms = elapsed(s->ev[2], s->ev[3]) + elapsed(s->ev[4], s->ev[5]);
+        st->t_solve_ms = elapsed(s->ev[1], s->ev[2]) + elapsed(s->ev[3], s->ev[4]);
+        st->t_update_ms = elapsed(s->ev[5], s->ev[6]);
+    }
+    return BOS_OK;
+}
+
+// One GN iteration. first: the first of a bos_step_n batch (resets the sticky abort flag); sync:
+// the last one (reads the status back). A factorization whose dataflow launch timed out leaves the
+// state untouched (the box-plus kernel checks the solver word) and fails the call.
+int do_step(bos_solver* s, bos_step_stats* st, bool first, bool sync) {
+    if (s->sharded) return do_step_sharded(s, st, first, sync);
+    int rc;
+    HIP_TRY(hipEventRecord(s->ev[0], s->stream));
+    if ((rc = enqueue_linearize(s))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[1], s->stream));
     HIP_TRY(hipEventRecord(s->ev[2], s->stream));
     bool analysed_now = false;
     if ((rc = enqueue_solve(s, analysed_now))) return rc;
@@ -485,7 +589,8 @@ int bos_destroy(bos_solver* s) {
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_status,
                     s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr,
-                    s->ex_send, s->ex_recv, s->ex_pack, s->ex_unpack, s->scrub};
+                    s->scrub, s->lane_pose, s->ex1_send, s->ex1_recv, s->ex2_send, s->ex2_recv, s->ex1_pack,
+                    s->ex1_unpack, s->ex2_bnd, s->ex2_usrc, s->ex2_udst, s->upd_nodes, s->abs_part};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (s->rf) rocsolver_destroy_rfinfo(s->rf);
@@ -518,7 +623,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(BOS_ERR_DEVICE, "no HIP device visible (the HIP path has no CPU fallback)");
-    if (opt.world_size > 1 && !opt.nccl_unique_id) return fail(BOS_ERR_INVALID, "world_size > 1 needs nccl_unique_id");
+    if (opt.world_size < 1 || opt.rank < 0 || opt.rank >= opt.world_size) return fail(BOS_ERR_INVALID, "bad rank / world_size");
 
     bos_solver* s = new bos_solver();
     auto bail = [&](int rc) { bos_destroy(s); return rc; };
@@ -582,13 +687,18 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         if (rocsolver_set_rfinfo_mode(s->rf, rocsolver_rfinfo_mode_cholesky) != rocblas_status_success)
             return bail(fail(BOS_ERR_SOLVER, "set_rfinfo_mode"));
     }
-    if (opt.nccl_unique_id) {   // world_size 1 with an id runs the exchange path on one GPU (tests)
+    // sharded: world > 1, or a communicator given with world 1 (the sharded phases and their RCCL
+    // all-gathers run with one rank: a one-GPU test of that path)
+    s->sharded = s->world > 1 || opt.nccl_unique_id;
+    s->external = s->sharded && !opt.nccl_unique_id;
+    if (s->sharded && !uses_mf(s)) return bail(fail(BOS_ERR_UNSUPPORTED, "sharding needs a multifrontal solver"));
+    if (opt.nccl_unique_id) {
         ncclUniqueId id;
         std::memcpy(&id, opt.nccl_unique_id, sizeof(id));
         ncclResult_t r = ncclCommInitRank(&s->comm, s->world, id, s->rank);
         if (r != ncclSuccess) return bail(fail(BOS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
-        if ((rc = setup_exchange(s))) return bail(rc);
     }
+    if (s->sharded && (rc = setup_shard(s))) return bail(rc);
 
     // ---- upload
     const int NP = s->NP, NL = s->NL;
@@ -651,7 +761,10 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             for (size_t i = 0; i < lo.size(); ++i) if (lo[i] >= 0) lbw[i] = pb->bearing_omega[lo[i]];
             if ((rc = upload_Tv(&s->pb_w, pbw)) || (rc = upload_Tv(&s->lb_w, lbw))) return bail(rc);
         }
-        s->pose_blocks = (int)(((int64_t)(P.p_end - P.p_begin) * B.lpp + bos::dev::kBlock - 1) / bos::dev::kBlock);
+        s->pose_blocks = (int)(((int64_t)B.lane_pose.size() * B.lpp + bos::dev::kBlock - 1) / bos::dev::kBlock);
+        // chi^2 partials: own lanes (a whole number of blocks when sharded), the top lanes on rank 0
+        s->chi_parts = s->rank == 0 ? s->pose_blocks : (int)((int64_t)P.shard.own_pose_lanes * B.lpp / bos::dev::kBlock);
+        if ((rc = upload(&s->lane_pose, B.lane_pose))) return bail(rc);
     }
     for (int k = 0; k < s->Mo; ++k)
         if (pb->odom_src[k] == pb->odom_dst[k]) {
@@ -695,7 +808,8 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         return bail(rc);
     if (uses_mf(s)) {
         std::string merr;
-        if (bos::dev::mf_create(P.mf, &s->mf, merr)) return bail(fail(BOS_ERR_DEVICE, merr));
+        if (bos::dev::mf_create(P.mf, s->sharded ? P.shard.sn_owner.data() : nullptr, s->rank, &s->mf, merr))
+            return bail(fail(BOS_ERR_DEVICE, merr));
     } else if (s->solver_kind == BOS_SOLVER_ROCSOLVER_RF) {
         std::vector<int32_t> piv(P.n);
         for (int64_t i = 0; i < P.n; ++i) piv[i] = (int32_t)i;   // ordering already applied in the layout
@@ -765,16 +879,14 @@ int bos_step_n(bos_solver* s, int n, bos_step_stats* last) {
 
 int bos_linearize_async(bos_solver* s) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
-    int rc = enqueue_linearize(s);
-    if (rc) return rc;
-    return enqueue_exchange(s);
+    return enqueue_linearize(s);
 }
 
 int bos_debug_linearize_timeline(bos_solver* s, int64_t capacity, uint64_t* stamps, int64_t* n_waves) {
     if (!s || !n_waves) return fail(BOS_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(s->device));
     const bos::Plan& P = s->plan;
-    const int64_t grid = s->pose_blocks + (P.l_end - P.l_begin + bos::dev::kBlock - 1) / bos::dev::kBlock;
+    const int64_t grid = s->pose_blocks + ((int64_t)P.blk.lm_lane_lm.size() + bos::dev::kBlock - 1) / bos::dev::kBlock;
     const int64_t waves = grid * (bos::dev::kBlock / 64);
     *n_waves = waves;
     if (!stamps || capacity < waves) return BOS_OK;
@@ -848,6 +960,54 @@ int bos_time_triangulate(bos_solver* s, int32_t n, double* ms_per_call) {
     return BOS_OK;
 }
 
+int bos_step_phase(bos_solver* s, int32_t phase, bos_step_stats* st) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    if (!s->sharded) return fail(BOS_ERR_INVALID, "bos_step_phase needs a sharded handle (world_size > 1)");
+    if (phase != s->phase) return fail(BOS_ERR_INVALID, "bos_step_phase: phases run 0, 1, 2 in order");
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = phase == 0 ? shard_phase0(s) : phase == 1 ? shard_phase1(s) : shard_phase2(s, true);
+    if (rc) { s->phase = 0; return rc; }
+    s->phase = (phase + 1) % 3;
+    if (phase < 2) return BOS_OK;
+    s->have_dx = true;
+    return finish_step(s, st);
+}
+
+int bos_exchange_size(const bos_solver* s, int32_t which, int64_t* doubles_per_rank) {
+    if (!s || !doubles_per_rank || (which != 1 && which != 2)) return fail(BOS_ERR_INVALID, "bad argument");
+    if (!s->sharded) return fail(BOS_ERR_INVALID, "not a sharded handle");
+    *doubles_per_rank = which == 1 ? s->ex1_count : s->ex2_count;
+    return BOS_OK;
+}
+
+int bos_exchange_download(bos_solver* s, int32_t which, double* send) {
+    if (!s || !send || (which != 1 && which != 2)) return fail(BOS_ERR_INVALID, "bad argument");
+    if (!s->sharded) return fail(BOS_ERR_INVALID, "not a sharded handle");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    const int64_t c = which == 1 ? s->ex1_count : s->ex2_count;
+    HIP_TRY(hipMemcpy(send, which == 1 ? s->ex1_send : s->ex2_send, c * sizeof(double), hipMemcpyDeviceToHost));
+    return BOS_OK;
+}
+
+int bos_exchange_upload(bos_solver* s, int32_t which, const double* recv_all) {
+    if (!s || !recv_all || (which != 1 && which != 2)) return fail(BOS_ERR_INVALID, "bad argument");
+    if (!s->sharded) return fail(BOS_ERR_INVALID, "not a sharded handle");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    const int64_t c = (which == 1 ? s->ex1_count : s->ex2_count) * s->world;
+    HIP_TRY(hipMemcpy(which == 1 ? s->ex1_recv : s->ex2_recv, recv_all, c * sizeof(double), hipMemcpyHostToDevice));
+    return BOS_OK;
+}
+
+int bos_node_owner(const bos_solver* s, int32_t* owner) {
+    if (!s || !owner) return fail(BOS_ERR_INVALID, "null argument");
+    const std::vector<int32_t>& o = s->plan.shard.node_owner;
+    if (o.empty()) return fail(BOS_ERR_UNSUPPORTED, "no shard (not a multifrontal solver)");
+    std::copy(o.begin(), o.end(), owner);
+    return BOS_OK;
+}
+
 int bos_debug_inject_stall(bos_solver* s) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
     if (!uses_mf(s)) return fail(BOS_ERR_UNSUPPORTED, "no dataflow launch in this solver");
@@ -886,7 +1046,6 @@ int bos_linearize(bos_solver* s, bos_step_stats* st) {
     HIP_TRY(hipEventRecord(s->ev[0], s->stream));
     if ((rc = enqueue_linearize(s))) return rc;
     HIP_TRY(hipEventRecord(s->ev[1], s->stream));
-    if ((rc = enqueue_exchange(s))) return rc;
     HIP_TRY(hipEventRecord(s->ev[2], s->stream));
     if ((rc = enqueue_stats(s, false))) return rc;
     if ((rc = read_stats(s, st))) return rc;
@@ -910,10 +1069,10 @@ int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
                                                        : 64 * Mb + 152 * Mo + 120 * NP + 64 * NL;
     info->num_block_values = P.blk.size;
     info->lanes_per_pose = P.blk.lpp;
-    info->owned_first_pose = P.p_begin;
-    info->owned_last_pose = P.p_end;
-    info->owned_first_landmark = P.l_begin;
-    info->owned_last_landmark = P.l_end;
+    info->pose_lane_groups = (int32_t)P.blk.lane_pose.size();
+    info->landmark_lanes = (int32_t)P.blk.lm_lane_lm.size();
+    info->own_fronts = P.shard.n_own_fronts;
+    info->top_fronts = P.shard.n_top_fronts;
     return BOS_OK;
 }
 

@@ -390,7 +390,7 @@ int order_nodes(const ProblemIndex& pi, int mode, std::vector<int32_t>& node_pos
 
 int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err);
 int build_layout(const ProblemIndex& pi, Plan& P, std::string& err);
-void build_ownership(const ProblemIndex& pi, Plan& P, int rank, int world);
+int build_shard(const ProblemIndex& pi, Plan& P, int rank, int world, std::string& err);
 int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& inv, std::string& err);
 
 int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,
@@ -500,12 +500,28 @@ int build_plan_once(const ProblemIndex& pi, int rank, int world, int factor_mode
         }
     }
 
+    // one GPU: every node's lanes, in stix order
+    P.shard = Shard();
+    P.shard.lane_poses.resize(NP);
+    std::iota(P.shard.lane_poses.begin(), P.shard.lane_poses.end(), 0);
+    P.shard.own_pose_lanes = NP;
+    P.shard.lane_lms.resize(NL);
+    std::iota(P.shard.lane_lms.begin(), P.shard.lane_lms.end(), 0);
     if ((rc = build_layout(pi, P, err))) return rc;
-    build_ownership(pi, P, rank, world);
     if ((rc = build_csr_src(pi, P, inv, err))) return rc;
     // Schur: the first NL blocks are the landmarks, candidates for folding into their parents
     const int n_fold_cand = factor_mode == kFactorSchur ? NL : 0;
     if (multifrontal && (rc = build_multifrontal(g, NP, P, inv, blocks, n_fold_cand, err))) return rc;
+    if (multifrontal && (rc = build_shard(pi, P, rank, world, err))) return rc;
+    if (world > 1) {
+        if (!multifrontal) { err = "world_size > 1 needs a multifrontal solver (schur or supernodal)"; return BOS_ERR_UNSUPPORTED; }
+        // this rank's lanes only: the layout, its stored-entry sources and the maps built from them
+        // (the tree and every offset are the same on every rank)
+        if ((rc = build_layout(pi, P, err)) || (rc = build_csr_src(pi, P, inv, err)) ||
+            (rc = build_multifrontal(g, NP, P, inv, blocks, n_fold_cand, err)))
+            return rc;
+        if (P.shard.lane_poses.size() != P.blk.lane_pose.size()) { err = "shard: lane rebuild"; return BOS_ERR_INVALID; }
+    }
     return validate_plan(pi, P, err);
 }
 
@@ -549,34 +565,6 @@ int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Pla
     P = std::move(first);   // no balance fits: the default plan (fronts the fast kernels do not take run
                             // on the general workgroup path)
     return BOS_OK;
-}
-
-void exchange_segments(const Plan& P, int rank, std::vector<ExchangeSeg>& pack, std::vector<ExchangeSeg>& unpack,
-                       int64_t& count) {
-    const int W = P.world;
-    pack.clear();
-    unpack.clear();
-    auto piece = [&](int r, int q) -> const Range& {
-        return q < 4 ? P.rank_val_ranges[4 * (size_t)r + q] : P.rank_b_ranges[2 * (size_t)r + (q - 4)];
-    };
-    count = 1;
-    for (int r = 0; r < W; ++r) {
-        int64_t t = 0;
-        for (int q = 0; q < 6; ++q) t += std::max<int64_t>(0, piece(r, q).end - piece(r, q).begin);
-        count = std::max(count, t);
-    }
-    for (int r = 0; r < W; ++r) {
-        int64_t off = 0;
-        for (int q = 0; q < 6; ++q) {
-            const Range& g = piece(r, q);
-            const int64_t len = g.end - g.begin;
-            if (len <= 0) continue;
-            const int32_t kind = q < 4 ? 0 : 1;
-            if (r == rank) pack.push_back({g.begin, off, len, kind, 2});
-            else unpack.push_back({(int64_t)r * count + off, g.begin, len, 3, kind});
-            off += len;
-        }
-    }
 }
 
 // Wave-interleaved lane lists (LaneLists in plan.hpp) from per-lane item ranges.
@@ -664,55 +652,74 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     B.lpp = avg >= 32 ? 2 : 1;   // measured on config 3 (K = 10): 1 lane per pose beats 2 and 4
     const int L = B.lpp;
     auto same_lm = [&](int i, int j) { return pi.b_lm[pb_obs[i]] == pi.b_lm[pb_obs[j]]; };
-    std::vector<int32_t> lane_ptr((size_t)NP * L + 1, 0);
-    for (int p = 0; p < NP; ++p) {
-        const int b0 = pb_ptr[p], b1 = pb_ptr[p + 1], nb = b1 - b0;
-        const int no = B.po_ptr[p + 1] - B.po_ptr[p];
-        const int share = (nb + no + L - 1) / L;
-        const int q0 = std::min(nb, std::max(0, share - no));
-        int prev = b0;
-        for (int j = 0; j < L; ++j) {
-            lane_ptr[(size_t)p * L + j] = prev;
-            if (j + 1 < L) {
-                int c = b0 + q0 + (int)((int64_t)(nb - q0) * j / std::max(1, L - 1));
-                c = std::max(c, prev);
-                while (c > b0 && c < b1 && same_lm(c, c - 1)) ++c;
-                prev = c;
-            }
-        }
-    }
-    lane_ptr[(size_t)NP * L] = Mb;
     for (int p = 0; p < NP; ++p)
         for (int i = pb_ptr[p] + 1; i < pb_ptr[p + 1]; ++i)
             if (same_lm(i, i - 1)) B.has_dups = true;
-    make_lane_lists(NP * L, lane_ptr, pb_obs, B.pose_lanes, true);
-    {   // landmark lanes, degree-sorted inside each window (ties by id: deterministic)
-        B.lm_lane_lm.resize(NL);
-        for (int l = 0; l < NL; ++l) B.lm_lane_lm[l] = l;
-        auto deg = [&](int l) { return lb_ptr[l + 1] - lb_ptr[l]; };
-        for (int w0 = 0; w0 < NL; w0 += kLmWindow)
-                std::stable_sort(B.lm_lane_lm.begin() + w0, B.lm_lane_lm.begin() + std::min(NL, w0 + kLmWindow),
-                                 [&](int a, int b) { return deg(a) > deg(b); });
-        std::vector<int32_t> lptr(NL + 1, 0), litems(Mb);
-        for (int g = 0; g < NL; ++g) {
-            const int l = B.lm_lane_lm[g];
-            std::copy(lb_obs.begin() + lb_ptr[l], lb_obs.begin() + lb_ptr[l + 1], litems.begin() + lptr[g]);
-            lptr[g + 1] = lptr[g] + deg(l);
+    // pose lane groups in the shard's order (every pose in stix order on one GPU); lane g's items
+    // are pb_obs[lane_b0[g], lane_b0[g] + count)
+    B.lane_pose = P.shard.lane_poses;
+    const int G = (int)B.lane_pose.size();
+    std::vector<int32_t> lane_ptr((size_t)G * L + 1, 0), lane_b0((size_t)G * L, 0), pitems;
+    pitems.reserve(Mb);
+    for (int i = 0; i < G; ++i) {
+        const int p = B.lane_pose[i];
+        int cut[3] = {0, 0, 0};   // bearing range of each lane (as pb_obs offsets)
+        if (p >= 0) {
+            const int b0 = pb_ptr[p], b1 = pb_ptr[p + 1], nb = b1 - b0;
+            const int no = B.po_ptr[p + 1] - B.po_ptr[p];
+            const int share = (nb + no + L - 1) / L;
+            const int q0 = std::min(nb, std::max(0, share - no));
+            int prev = b0;
+            for (int j = 0; j < L; ++j) {
+                cut[j] = prev;
+                if (j + 1 < L) {
+                    int c = b0 + q0 + (int)((int64_t)(nb - q0) * j / std::max(1, L - 1));
+                    c = std::max(c, prev);
+                    while (c > b0 && c < b1 && same_lm(c, c - 1)) ++c;
+                    prev = c;
+                }
+            }
+            cut[L] = b1;
         }
-        make_lane_lists(NL, lptr, litems, B.lm_lanes, false);
+        for (int j = 0; j < L; ++j) {
+            const size_t g = (size_t)i * L + j;
+            lane_b0[g] = cut[j];
+            pitems.insert(pitems.end(), pb_obs.begin() + cut[j], pb_obs.begin() + cut[j + 1]);
+            lane_ptr[g + 1] = (int32_t)pitems.size();
+        }
     }
-    // pose-landmark blocks: the slot of the last bearing of each (pose, landmark) run
+    make_lane_lists(G * L, lane_ptr, pitems, B.pose_lanes, true);
+    {   // landmark lanes in the shard's order, degree-sorted inside each window (ties by id: deterministic)
+        B.lm_lane_lm = P.shard.lane_lms;
+        const int NLL = (int)B.lm_lane_lm.size();
+        auto deg = [&](int l) { return lb_ptr[l + 1] - lb_ptr[l]; };
+        for (int w0 = 0; w0 < NLL; w0 += kLmWindow)
+            std::stable_sort(B.lm_lane_lm.begin() + w0, B.lm_lane_lm.begin() + std::min(NLL, w0 + kLmWindow),
+                             [&](int a, int b) { return deg(a) > deg(b); });
+        std::vector<int32_t> lptr(NLL + 1, 0), litems;
+        for (int g = 0; g < NLL; ++g) {
+            const int l = B.lm_lane_lm[g];
+            litems.insert(litems.end(), lb_obs.begin() + lb_ptr[l], lb_obs.begin() + lb_ptr[l + 1]);
+            lptr[g + 1] = (int32_t)litems.size();
+        }
+        make_lane_lists(NLL, lptr, litems, B.lm_lanes, false);
+    }
+    // pose-landmark blocks of the lane poses: the slot of the last bearing of each (pose, landmark) run
+    std::vector<int32_t> group_of(NP, -1);
+    for (int i = 0; i < G; ++i)
+        if (B.lane_pose[i] >= 0) group_of[B.lane_pose[i]] = i;
     B.ub_ptr.assign(NP + 1, 0);
     for (int p = 0; p < NP; ++p) {
-        for (int sub = 0; sub < L; ++sub) {
-            const int g = p * L + sub;
-            const int n = B.pose_lanes.cnt[g], i0 = lane_ptr[g];
-            for (int j = 0; j < n; ++j)
-                if (j + 1 == n || !same_lm(i0 + j + 1, i0 + j)) {
-                    B.ub_lm.push_back(pi.b_lm[pb_obs[i0 + j]]);
-                    B.ub_slot.push_back(lane_slot(B.pose_lanes, g, j));
-                }
-        }
+        if (group_of[p] >= 0)
+            for (int sub = 0; sub < L; ++sub) {
+                const int g = group_of[p] * L + sub;
+                const int n = B.pose_lanes.cnt[g], i0 = lane_b0[g];
+                for (int j = 0; j < n; ++j)
+                    if (j + 1 == n || !same_lm(i0 + j + 1, i0 + j)) {
+                        B.ub_lm.push_back(pi.b_lm[pb_obs[i0 + j]]);
+                        B.ub_slot.push_back(lane_slot(B.pose_lanes, g, j));
+                    }
+            }
         B.ub_ptr[p + 1] = (int32_t)B.ub_lm.size();
     }
     B.off_ldiag = 6 * (int64_t)NP;
@@ -721,55 +728,6 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     B.size = B.off_pp + 6 * (int64_t)B.nuo();
     if (B.size > INT32_MAX) { err = "block array exceeds 32-bit indices"; return BOS_ERR_UNSUPPORTED; }
     return BOS_OK;
-}
-
-// Ownership cuts for observation sharding: contiguous ranges of whole waves of pose lanes and of
-// landmark lanes, balanced by the observations they evaluate.
-void build_ownership(const ProblemIndex& pi, Plan& P, int rank, int world) {
-    const BlockLayout& B = P.blk;
-    const int ppw = B.poses_per_wave();
-    auto cuts = [&](int n, int unit, auto&& work) {   // cut [0, n) at multiples of unit
-        const int nu = (n + unit - 1) / unit;
-        std::vector<int64_t> wu(nu, 0);
-        int64_t total = 0;
-        for (int i = 0; i < n; ++i) { wu[i / unit] += work(i); total += work(i); }
-        std::vector<int32_t> c(world + 1, n);
-        c[0] = 0;
-        int64_t acc = 0;
-        int r = 1;
-        for (int u = 0; u < nu && r < world; ++u) {
-            acc += wu[u];
-            while (r < world && acc * world >= total * r) c[r++] = std::min(n, (u + 1) * unit);
-        }
-        return c;
-    };
-    auto npose_items = [&](int p) {
-        int64_t c = 1 + B.po_ptr[p + 1] - B.po_ptr[p];
-        for (int s = 0; s < B.lpp; ++s) c += B.pose_lanes.cnt[(size_t)p * B.lpp + s];
-        return c;
-    };
-    P.rank_pose = cuts(pi.NP, ppw, npose_items);
-    // landmark lanes cut at window boundaries: each rank owns a contiguous landmark range
-    P.rank_lm = cuts(pi.NL, kLmWindow, [&](int g) { return (int64_t)1 + B.lm_lanes.cnt[g]; });
-    P.rank = rank;
-    P.world = world;
-    P.p_begin = P.rank_pose[rank]; P.p_end = P.rank_pose[rank + 1];
-    P.l_begin = P.rank_lm[rank]; P.l_end = P.rank_lm[rank + 1];
-    P.rank_val_ranges.resize(4 * (size_t)world);
-    P.rank_b_ranges.resize(2 * (size_t)world);
-    const std::vector<int32_t>& wb = B.pose_lanes.w_base;
-    auto wave_of = [&](int p) { return (int)(((int64_t)p * B.lpp + 63) / 64); };   // p is wave aligned or NP
-    for (int r = 0; r < world; ++r) {
-        const int p0 = P.rank_pose[r], p1 = P.rank_pose[r + 1], l0 = P.rank_lm[r], l1 = P.rank_lm[r + 1];
-        Range* v = &P.rank_val_ranges[4 * (size_t)r];
-        v[0] = {6 * (int64_t)p0, 6 * (int64_t)p1};
-        v[1] = {B.off_ldiag + 3 * (int64_t)l0, B.off_ldiag + 3 * (int64_t)l1};
-        v[2] = {B.off_pl + 6 * (int64_t)wb[wave_of(p0)], B.off_pl + 6 * (int64_t)wb[wave_of(p1)]};
-        v[3] = {B.off_pp + 6 * (int64_t)B.uo_ptr[p0], B.off_pp + 6 * (int64_t)B.uo_ptr[p1]};
-        Range* bb = &P.rank_b_ranges[2 * (size_t)r];
-        bb[0] = {3 * (int64_t)p0, 3 * (int64_t)p1};
-        bb[1] = {3 * (int64_t)pi.NP + 2 * (int64_t)l0, 3 * (int64_t)pi.NP + 2 * (int64_t)l1};
-    }
 }
 
 // Block value feeding every stored entry (row >= col) of the lower triangle of P^T H_nf P.
@@ -790,25 +748,34 @@ int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& i
         const auto it = std::lower_bound(b, e, d);
         return (it != e && *it == d) ? (int64_t)(it - B.uo_dst.begin()) : -1;
     };
+    // which nodes' lanes this rank's J+H runs (all of them on one GPU); a block is computed by the
+    // lane of its pose (pose-landmark), of its lower pose (pose-pose) or of its node (diagonal)
+    std::vector<char> lane_node(pi.NP + pi.NL, 0);
+    for (int32_t p : B.lane_pose) if (p >= 0) lane_node[p] = 1;
+    for (int32_t l : B.lm_lane_lm) lane_node[NP + l] = 1;
     P.blk.csr_src.resize(P.nnzA());
     for (int64_t row = 0; row < P.n; ++row) {
         const int U = dof_node[row], a = dof_loc[row];
         for (int64_t e = P.rowptr[row]; e < P.rowptr[row + 1]; ++e) {
             const int V = dof_node[P.colind[e]], c = dof_loc[P.colind[e]];
             int64_t v = -1;
+            int owner = U;   // the node whose lane computes the block
             if (U == V) {
                 v = U < NP ? 6 * (int64_t)U + tri(a, c) : B.off_ldiag + 3 * (int64_t)(U - NP) + tri(a, c);
             } else if (U < NP && V >= NP) {
                 const int64_t k = pl_slot(U, V - NP);
                 if (k >= 0) v = B.off_pl + 6 * k + 2 * a + c;
             } else if (U >= NP && V < NP) {
+                owner = V;
                 const int64_t k = pl_slot(V, U - NP);
                 if (k >= 0) v = B.off_pl + 6 * k + 2 * c + a;
             } else if (U < NP && V < NP) {
+                owner = std::min(U, V);
                 int64_t k = pp_block(U, V);
                 if (k < 0) k = pp_block(V, U);
                 if (k >= 0) v = B.off_pp + 6 * k + tri(a, c);
             }
+            if (!lane_node[owner]) { P.blk.csr_src[e] = -2; continue; }   // another rank's
             if (v < 0) { err = "internal error: stored entry without a block"; return BOS_ERR_INVALID; }
             P.blk.csr_src[e] = (int32_t)v;
         }
@@ -1022,12 +989,14 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
 }
 
 // Proves, on the host, that the J+H kernel's writes (simulated here exactly as hip/kernels.hip
-// issues them) stay inside this rank's ranges of the block array, write every value at most once
-// and every value the solver reads exactly once, cover b exactly, and that chi^2 counts every
-// observation once. O(slots + nnz).
+// issues them for this rank's lanes) write every value of the block array and every b entry at
+// most once, that every value a front this rank factors reads (assembly map and fold records) is
+// written exactly once by this rank, and that chi^2 counts every observation once (one GPU; the
+// sharded count is checked across ranks by bos_plan_shard_selftest). O(slots + nnz).
 int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
     const int NP = pi.NP, NL = pi.NL;
     const BlockLayout& B = P.blk;
+    const Shard& S = P.shard;
     const int L = B.lpp;
     const LaneLists& PL = B.pose_lanes;
     const LaneLists& LL = B.lm_lanes;
@@ -1038,23 +1007,27 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
         for (int i = 0; i < cnt; ++i) ++hit[v0 + i];
         return true;
     };
-    if (((P.p_begin * (int64_t)L) % 64 && P.p_begin != NP) || (P.l_begin % 64 && P.l_begin != NL)) {
-        err = "shard does not start at a wave";
-        return BOS_ERR_INVALID;
-    }
     std::vector<int32_t> slot_block(PL.slots(), -1);   // landmark whose block lives in the slot
     for (int p = 0; p < NP; ++p)
         for (int u = B.ub_ptr[p]; u < B.ub_ptr[p + 1]; ++u) slot_block[B.ub_slot[u]] = B.ub_lm[u];
-    for (int p = P.p_begin; p < P.p_end; ++p) {
+    if ((int64_t)PL.cnt.size() != (int64_t)B.lane_pose.size() * L) { err = "pose lane count"; return BOS_ERR_INVALID; }
+    for (size_t i = 0; i < B.lane_pose.size(); ++i) {
+        const int p = B.lane_pose[i];
+        if (p < 0) {
+            for (int sub = 0; sub < L; ++sub)
+                if (PL.cnt[i * L + sub]) { err = "padding lane with items"; return BOS_ERR_INVALID; }
+            continue;
+        }
         if (!mark(6 * (int64_t)p, 6)) { err = "pose diagonal out of range"; return BOS_ERR_INVALID; }
         for (int d = 0; d < 3; ++d) ++bhit[3 * (size_t)p + d];
+        const bool counts = (int)i < S.own_pose_lanes || S.rank == 0;   // chi^2 of top lanes: rank 0
         for (int sub = 0; sub < L; ++sub) {
-            const int g = p * L + sub, n = PL.cnt[g];
+            const int g = (int)i * L + sub, n = PL.cnt[g];
             if (n > PL.w_len[g / 64]) { err = "lane longer than its wave"; return BOS_ERR_INVALID; }
             for (int j = 0; j < n; ++j) {
                 const int32_t sl = lane_slot(PL, g, j), k = PL.obs[sl];
                 if (k < 0 || pi.b_pose[k] != p) { err = "bearing slot of the wrong pose"; return BOS_ERR_INVALID; }
-                ++chi[k];
+                if (counts) ++chi[k];
                 if (j + 1 == n || pi.b_lm[PL.obs[lane_slot(PL, g, j + 1)]] != pi.b_lm[k]) {
                     if (slot_block[sl] != pi.b_lm[k] || !mark(B.off_pl + 6 * (int64_t)sl, 6)) {
                         err = "pose-landmark block misplaced";
@@ -1067,7 +1040,7 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
             const int32_t e = B.po_ent[x];
             const int k = e >> 1;
             if ((e & 1) ? pi.o_dst[k] != p : pi.o_src[k] != p) { err = "odometry entry of the wrong pose"; return BOS_ERR_INVALID; }
-            if (!(e & 1)) ++chi[pi.Mb + k];
+            if (!(e & 1) && counts) ++chi[pi.Mb + k];
             const int q = (e & 1) ? pi.o_src[k] : pi.o_dst[k];
             const int u = B.po_blk[x];
             if ((u >= 0) != (q > p)) { err = "pose-pose block on the wrong side"; return BOS_ERR_INVALID; }
@@ -1080,13 +1053,10 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
             }
         }
     }
-    if ((P.l_begin % kLmWindow && P.l_begin != NL) || (P.l_end % kLmWindow && P.l_end != NL)) {
-        err = "landmark shard not aligned to a lane window";
-        return BOS_ERR_INVALID;
-    }
-    for (int g = P.l_begin; g < P.l_end; ++g) {
+    const int NLL = (int)B.lm_lane_lm.size();
+    if ((int)LL.cnt.size() != NLL) { err = "landmark lane count"; return BOS_ERR_INVALID; }
+    for (int g = 0; g < NLL; ++g) {
         const int l = B.lm_lane_lm[g];
-        if (l / kLmWindow != g / kLmWindow) { err = "landmark lane outside its window"; return BOS_ERR_INVALID; }
         if (LL.cnt[g] > LL.w_len[g / 64]) { err = "lane longer than its wave"; return BOS_ERR_INVALID; }
         for (int j = 0; j < LL.cnt[g]; ++j) {
             const int32_t k = LL.obs[lane_slot(LL, g, j)];
@@ -1095,33 +1065,44 @@ int validate_plan(const ProblemIndex& pi, const Plan& P, std::string& err) {
         if (!mark(B.off_ldiag + 3 * (int64_t)l, 3)) { err = "landmark diagonal out of range"; return BOS_ERR_INVALID; }
         for (int d = 0; d < 2; ++d) ++bhit[3 * (size_t)NP + 2 * (size_t)l + d];
     }
-    // at most once, only inside this rank's ranges; everything the solver reads there exactly once
-    std::vector<uint8_t> own(B.size, 0), bown(bhit.size(), 0);
-    for (int q = 0; q < 4; ++q) {
-        const Range& g = P.rank_val_ranges[4 * (size_t)P.rank + q];
-        for (int64_t v = g.begin; v < g.end; ++v) own[v] = 1;
-    }
-    for (int q = 0; q < 2; ++q) {
-        const Range& g = P.rank_b_ranges[2 * (size_t)P.rank + q];
-        for (int64_t v = g.begin; v < g.end; ++v) bown[v] = 1;
-    }
     for (int64_t v = 0; v < B.size; ++v)
-        if (hit[v] > own[v]) {
+        if (hit[v] > 1) {
             err = "block value " + std::to_string(v) + " written " + std::to_string((int)hit[v]) + " times";
             return BOS_ERR_INVALID;
         }
     for (size_t v = 0; v < bhit.size(); ++v)
-        if (bhit[v] != bown[v]) { err = "b entry coverage"; return BOS_ERR_INVALID; }
-    if (P.world == 1)   // single shard: every observation's chi^2 counted once (self-loops: by the stats)
+        if (bhit[v] > 1 || (S.world == 1 && bhit[v] != 1)) { err = "b entry coverage"; return BOS_ERR_INVALID; }
+    if (S.world == 1)   // every observation's chi^2 counted once (self-loops: by the step's stats)
         for (size_t k = 0; k < chi.size(); ++k)
-            if (chi[k] != ((k >= (size_t)pi.Mb && pi.o_src[k - pi.Mb] == pi.o_dst[k - pi.Mb]) ? 0 : 1)) { err = "chi^2 of observation " + std::to_string(k) + " counted " + std::to_string(chi[k]) + " times"; return BOS_ERR_INVALID; }
-    // every stored entry reads a block value written by its owner; pose-pose blocks are symmetric
-    // (off-diagonal values read twice), every other value at most once
+            if (chi[k] != ((k >= (size_t)pi.Mb && pi.o_src[k - pi.Mb] == pi.o_dst[k - pi.Mb]) ? 0 : 1)) {
+                err = "chi^2 of observation " + std::to_string(k) + " counted " + std::to_string(chi[k]) + " times";
+                return BOS_ERR_INVALID;
+            }
+    // every stored entry this rank computes reads a block value it writes; pose-pose blocks are
+    // symmetric (off-diagonal values read twice), every other value at most once
     std::vector<uint8_t> refs(B.size, 0);
     for (int32_t v : B.csr_src) {
+        if (v == -2) { if (S.world == 1) { err = "stored entry not computed"; return BOS_ERR_INVALID; } continue; }
         if (v < 0 || v >= B.size) { err = "stored entry reads outside the block array"; return BOS_ERR_INVALID; }
         if (++refs[v] > (v >= B.off_pp ? 2 : 1)) { err = "block value read by two stored entries"; return BOS_ERR_INVALID; }
-        if (own[v] && hit[v] != 1) { err = "block value read by the solver is never written"; return BOS_ERR_INVALID; }
+        if (hit[v] != 1) { err = "block value read by the solver is never written"; return BOS_ERR_INVALID; }
+    }
+    // the fronts this rank factors (its own and the top) read only values it computes
+    const Multifrontal& F = P.mf;
+    for (int s = 0; s < F.nsuper; ++s) {
+        if (S.sn_owner.empty() || (S.sn_owner[s] != S.rank && S.sn_owner[s] != -1)) continue;
+        for (int q = F.amap_ptr[s]; q < F.amap_ptr[s + 1]; ++q)
+            if (F.amap_src[q] < 0) { err = "a front of this rank reads H computed by another rank"; return BOS_ERR_INVALID; }
+    }
+    for (int p = 0; p < F.nsuper; ++p) {
+        if (F.fold_cnt.empty() || S.sn_owner.empty() || (S.sn_owner[p] != S.rank && S.sn_owner[p] != -1)) continue;
+        for (int ch = F.fold_cptr[p]; ch < F.fold_cptr[p + 1]; ++ch)
+            for (int q = F.fold_chunk[ch]; q < F.fold_chunk[ch + 1]; ++q)
+                for (int t = 0; t < 5; ++t)
+                    if (F.fold_rec[(size_t)kFoldRec * q + t] == -2) {
+                        err = "a folded landmark of this rank reads H computed by another rank";
+                        return BOS_ERR_INVALID;
+                    }
     }
     return BOS_OK;
 }

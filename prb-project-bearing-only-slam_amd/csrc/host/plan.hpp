@@ -59,10 +59,14 @@ struct BlockLayout {
     int64_t off_ldiag = 0, off_pl = 0, off_pp = 0, size = 0;
     int lpp = 1;                        // lanes per pose: 1 or 2
     bool has_dups = false;              // some (pose, landmark) or (src, dst) pair repeats
-    LaneLists pose_lanes;               // lanes = NP * lpp
-    LaneLists lm_lanes;                 // lanes = NL, lane g -> landmark lm_lane_lm[g]
-    // landmark of each landmark lane: inside each window of kLmWindow lanes the window's landmarks
-    // sorted by degree (descending), so the lanes of a wave walk lists of similar length
+    // pose lane groups: group i (lanes i * lpp ... + lpp - 1) runs pose lane_pose[i] (-1: padding);
+    // one rank runs the poses of Shard::lane_poses (all poses in stix order on one GPU)
+    std::vector<int32_t> lane_pose;
+    LaneLists pose_lanes;               // lanes = lane_pose.size() * lpp
+    LaneLists lm_lanes;                 // lane g -> landmark lm_lane_lm[g]
+    // landmark of each landmark lane (Shard::lane_lms): inside each window of kLmWindow lanes the
+    // window's landmarks sorted by degree (descending), so the lanes of a wave walk lists of similar
+    // length
     std::vector<int32_t> lm_lane_lm;
     std::vector<int32_t> ub_ptr;        // [NP + 1] pose-landmark blocks of each pose
     std::vector<int32_t> ub_lm;         // [nub] landmark of each pose-landmark block (ascending per pose)
@@ -74,14 +78,13 @@ struct BlockLayout {
                                         // higher one (this pose stores it), else -1
     std::vector<int32_t> uo_ptr;        // [NP + 1] pose-pose blocks stored by each pose (the lower one)
     std::vector<int32_t> uo_dst;        // [nuo] the higher pose of each pose-pose block
-    std::vector<int32_t> csr_src;       // [nnzA] block value of each stored entry of P^T H_nf P
+    std::vector<int32_t> csr_src;       // [nnzA] block value of each stored entry of P^T H_nf P; -2 when
+                                        // this rank's J+H does not compute it (sharded plans)
     int nub() const { return ub_ptr.empty() ? 0 : ub_ptr.back(); }
     int nuo() const { return uo_ptr.empty() ? 0 : uo_ptr.back(); }
     int poses_per_wave() const { return 64 / lpp; }
 };
 
-// A contiguous piece of the block array / b that one rank writes (and broadcasts).
-struct Range { int64_t begin = 0, end = 0; };
 
 struct OrderingReport {
     std::string chosen;                // "temporal" or "nested-dissection"
@@ -142,6 +145,35 @@ struct Multifrontal {
     int balance_pct = 40;
 };
 
+// Multi-GPU sharding of the multifrontal solve. The assembly tree is cut into
+// subtrees, each owned by one rank, below a replicated top (the separators above the cut, factored
+// and solved by every rank). A rank's J+H runs the lanes of its own and of the top nodes, which is
+// everything its fronts read (validate_plan proves it); no part of H crosses between ranks. Two
+// exchanges per GN iteration: the subtree roots' update matrices and u-vectors before the top is
+// factored, and the solution of the boundary nodes (subtree nodes a top lane reads) after the
+// backward solve. One GPU: world 1, every node owned by rank 0, no top, no exchange.
+constexpr int kExHeader = 2;   // doubles at the head of each rank's exchange buffer (stats partials)
+struct Shard {
+    int rank = 0, world = 1;
+    std::vector<int8_t> sn_owner;      // per supernode: owning rank, -1 = top (every rank)
+    std::vector<int32_t> node_owner;   // per node: owning rank, -1 = top, -2 = the fixed pose (no supernode;
+                                       // its lane runs as a top lane: chi^2 only)
+    std::vector<int32_t> lane_poses;   // J+H pose lanes: own poses, padding (-1) to a J+H block, top poses
+    int own_pose_lanes = 0;            // lane_poses[0, own_pose_lanes): own poses (and padding)
+    std::vector<int32_t> lane_lms;     // J+H landmark lanes: own landmarks, then top landmarks
+    // exchange 1: subtree roots (with a parent) of rank q = roots[root_ptr[q], root_ptr[q + 1])
+    std::vector<int32_t> root_ptr, roots;
+    int64_t ex1_count = 0;             // doubles per rank: header + the largest rank's U / u payload
+    // exchange 2: boundary dofs (permuted numbering) of rank q = bnd_dof[bnd_ptr[q], bnd_ptr[q + 1])
+    std::vector<int32_t> bnd_ptr, bnd_dof;
+    int64_t ex2_count = 0;
+    // nodes this rank's box-plus updates: own + top (the first n_upd_local), then the boundary nodes
+    // of the other ranks (their solution arrives with exchange 2)
+    std::vector<int32_t> upd_nodes;
+    int n_upd_local = 0;
+    int n_top_fronts = 0, n_own_fronts = 0;
+};
+
 struct Plan {
     int NP = 0, NL = 0, Mb = 0, Mo = 0, fixed = -1;
     int64_t n = 0;                         // system size N - 3
@@ -152,15 +184,7 @@ struct Plan {
     Multifrontal mf;                       // built when factor_mode == kFactorMultifrontal
     BlockLayout blk;
     OrderingReport ordering;
-    // observation sharding: rank r owns poses [rank_pose[r], rank_pose[r + 1]) and landmarks
-    // [rank_lm[r], rank_lm[r + 1]), i.e. their diagonal blocks, b entries and the off-diagonal
-    // blocks of the observations its poses own
-    int rank = 0, world = 1;
-    std::vector<int32_t> rank_pose, rank_lm;     // [world + 1]
-    int32_t p_begin = 0, p_end = 0, l_begin = 0, l_end = 0;
-    // per rank: 4 block-array ranges (pose diag, landmark diag, pose-landmark, pose-pose) and 2 b
-    // ranges (poses, landmarks)
-    std::vector<Range> rank_val_ranges, rank_b_ranges;   // [world * 4], [world * 2]
+    Shard shard;
     int64_t nnzA() const { return rowptr.empty() ? 0 : rowptr.back(); }
     int64_t nnzL() const { return Lptr.empty() ? 0 : Lptr.back(); }
 };
@@ -181,17 +205,14 @@ extern int g_schur_leaf;
 // Builds the plan. Returns 0 or a negative BOS_ERR_* code with a message in err.
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& out, std::string& err);
 
-// The sharded J+H exchange (hip/solver_capi.hip enqueue_exchange): rank r packs its pieces of the
-// block array (kind 0) and of b (kind 1) — rank_val_ranges then rank_b_ranges, in order — into a
-// send buffer (kind 2) of `count` elements (the largest rank's total), one all-gather concatenates
-// the W send buffers into the receive buffer (kind 3), and every other rank's pieces are copied
-// back to their places.
+// Segments of exchange 1 for rank `rank` (hip/solver_capi.hip): pack = this rank's roots' U / u into
+// its send buffer, unpack = every other rank's roots from the receive buffer (kinds: 0 U, 1 u, 2 send,
+// 3 receive; offsets in doubles).
 struct ExchangeSeg {
-    int64_t src, dst, len;      // element offsets and count
+    int64_t src, dst, len;
     int32_t src_kind, dst_kind;
 };
-void exchange_segments(const Plan& P, int rank, std::vector<ExchangeSeg>& pack, std::vector<ExchangeSeg>& unpack,
-                       int64_t& count);
+void exchange1_segments(const Plan& P, std::vector<ExchangeSeg>& pack, std::vector<ExchangeSeg>& unpack);
 
 // Node ordering only (positions) and its symbolic cost. mode kFactorScalar / kFactorNone: the
 // cheapest of temporal, landmarks-first and nested dissection; kFactorMultifrontal: nested

@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
     missing = [n for n in sorted(names) if not hasattr(L, n)]
     assert not missing, missing
     assert set(bos.EXPORTED_SYMBOLS) == names
-    assert L.bos_abi_version() == 1
+    assert L.bos_abi_version() == 2
 
 
 @pytest.mark.skipif(bos.device_count() > 0, reason="a HIP device is visible")
@@ -173,29 +173,66 @@ def test_multifrontal_structure_solves_like_scipy(which, solver):
         assert info["mf_supernodes"] > P.NL and set(perm[:2 * P.NL].tolist()) == set(range(3 * P.NP, P.N))
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 4])
-def test_plan_shards_partition_rows(world):
-    P = bos.load_g2o(C1)
-    owned = np.zeros(0)
-    b_owned = np.zeros(P.N, dtype=int)
-    for r in range(world):
-        info = bos.plan_inspect(P, r, world, entries=True)
-        owned = info["owned"].astype(int) if r == 0 else owned + info["owned"]
-        b_owned += info["b_owned"]
-    assert np.all(owned == 1)                       # every stored entry written by exactly one rank
-    keep = np.ones(P.N, dtype=bool)
-    keep[3 * P.fixed:3 * P.fixed + 3] = False
-    assert np.all(b_owned[keep] == 1)
+def _system(P, solver):
+    """Stored entries of H_nf (one-rank plan order) and the right-hand side in the permuted order."""
+    Q = to_oracle(P)
+    lin = O.linearize(Q)
+    Hl = oracle_lower_nf(Q, lin).tocsr()
+    info = bos.plan_inspect(P, entries=True, solver=solver)
+    vals = np.asarray(Hl[info["rows"], info["cols"]]).ravel()
+    perm = info["perm_to_ref"][:info["n"]]
+    return vals, lin.b[perm], Hl, lin, perm
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("which", ["c1", "synthetic"])
-def test_plan_exchange_covers_every_rank(world, which):
-    """The segment tables of the sharded exchange (pack own pieces, all-gather, unpack the others')
-    leave every rank with every value of H the solver reads and every b entry: the N>1 data path
-    checked on the host, since one GPU cannot host two RCCL ranks."""
+@pytest.mark.parametrize("solver", ["schur", "supernodal"])
+def test_sharded_solve_equals_one_rank(world, which, solver):
+    """The multi-GPU algorithm (subtree shards + replicated top, two exchanges; host/shard.cpp) run on
+    the host for every rank: each rank holds only the H its own J+H lanes compute, the merged
+    solution equals the one-rank solution bit for bit, the ranks agree on the top, every observation's
+    chi^2 is counted by exactly one rank, and every node a rank's J+H reads stays current (the
+    selftest raises otherwise). The N>1 data path checked without N GPUs."""
     P = bos.load_g2o(C1) if which == "c1" else bos.synthetic(3000, 6000, 10, seed=5)
-    bos.plan_exchange_selftest(P, world)
+    kind = bos.BOS_SOLVER_SCHUR if solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
+    vals, rhs, Hl, lin, perm = _system(P, kind)
+    x = bos.plan_shard_selftest(P, world, vals, rhs, solver=kind)
+    x1 = bos.plan_mf_selftest(P, vals, rhs, solver=kind)
+    assert np.array_equal(x, x1)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_shard_partition(world):
+    """Every node but the fixed pose has one owner (a rank or the replicated top); every rank has
+    subtrees; each rank's plan computes exactly the stored entries of H its fronts read (validated
+    per rank) and together the ranks compute every entry; the J+H lanes of all ranks cover every
+    pose and landmark; the top is small next to the subtrees."""
+    P = bos.synthetic(10000, 20000, 10, seed=3)
+    own = bos.plan_node_owner(P, world)
+    assert own[P.fixed] == -2 and np.all(own[np.arange(P.NP + P.NL) != P.fixed] >= -1)
+    counts = np.bincount(own[own >= 0], minlength=world)
+    assert np.all(counts > 0)
+    assert (own == -1).sum() < 0.05 * len(own)
+    assert counts.max() <= 1.25 * counts.mean()
+    computed = None
+    b_cov = np.zeros(P.N, dtype=int)
+    for r in range(world):
+        info = bos.plan_inspect(P, r, world, entries=True, solver=bos.BOS_SOLVER_SCHUR)
+        computed = info["owned"].astype(int) if computed is None else computed + info["owned"]
+        b_cov += info["b_owned"]
+        assert info["shard_top_fronts"] > 0 and info["shard_own_fronts"] > 0
+    assert np.all(computed >= 1)
+    keep = np.ones(P.N, dtype=bool)
+    keep[3 * P.fixed:3 * P.fixed + 3] = False
+    assert np.all(b_cov[keep] >= 1)
+
+
+def test_shard_world1_is_the_unsharded_plan():
+    P = bos.load_g2o(C1)
+    a = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR)
+    assert a["shard_top_fronts"] == 0 and a["shard_pose_lanes"] == P.NP and a["shard_lm_lanes"] == P.NL
+    own = bos.plan_node_owner(P, 1)
+    assert np.all(own[np.arange(P.NP + P.NL) != P.fixed] == 0)
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3, 4])
