@@ -5,12 +5,14 @@
 A *step* is one J+H build (reference slam/solver.cpp:28-69) over the whole synthetic
 config-3 world (100k poses / 200k landmarks / 1M bearings / 99 999 odometry edges), inputs
 resident in HBM. ``value`` = observations (bearings + odometry edges) processed per second by
-the whole job. With ``--gpus N > 1`` the same world is sharded across N ranks (strong scaling)
-and a step includes the RCCL exchange of every rank's rows of H and b.
+the whole job. With ``--gpus N > 1`` the same world is sharded across N ranks (strong scaling):
+each rank builds the part of H its subtrees and the replicated top read, so the
+J+H needs no exchange; a GN iteration has two RCCL all-gathers.
 
-Also reported: GN iterations/s (full steps: J+H + exchange + sparse Cholesky + box-plus),
-the J+H kernel's HBM roofline fraction (algorithmic bytes) and the CPU
-baseline (the oracle, oracle/bos_oracle.cpp, timed on this host).
+Also reported: GN iterations/s (full steps: J+H + sparse Cholesky + exchanges + box-plus), the
+J+H kernel's HBM roofline fraction from cold caches (in-step) and back to back (algorithmic
+bytes), and the CPU baselines (the oracle, oracle/bos_oracle.cpp, timed on this
+host's usable cores).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|fp64]
 """
@@ -104,21 +106,31 @@ def cpu_baseline(P, precision, cpus, budget_s=12.0):
             "forms_obs_per_s": forms, "host": cpus}
 
 
-def cpu_gn_baseline(P, cpus, budget_s=10.0):
-    """Full CPU GN steps (oracle J+H + SciPy sparse solve + box-plus), bounded sample."""
-    import oracle as O
-    from helpers import to_oracle
-    Q = to_oracle(P)
-    p, l = Q.copy_state()
-    t0 = time.perf_counter()
-    n = 0
-    while time.perf_counter() - t0 < budget_s or n == 0:
-        O.step(Q, p, l, threads=cpus["usable"])
-        n += 1
-    dt = (time.perf_counter() - t0) / n
-    return {"value": 1.0 / dt, "unit": "it/s", "cores": cpus["usable"], "kind": "port",
-            "sample": f"{n} GN iterations of config 3 (oracle J+H fp64 on {cpus['usable']} threads + SciPy SuperLU "
-                      f"spsolve, single-threaded + box-plus)", "host": cpus}
+def cpu_gn_baseline(P, cpus, budget_s=8.0):
+    """Full CPU GN iterations of config 3 by the build's own C++ CPU backend (include/bos_host.h
+    bos_cpu_gn_*: the plan's J+H lanes, the host multifrontal Cholesky with each tree level's fronts
+    in parallel, box-plus; fp64), bounded sample, on 1 thread and on every usable CPU; the faster one
+    is the baseline."""
+    forms = {}
+    best = None
+    for th in sorted({1, cpus["usable"]}):
+        c = bos.CpuGN(P, th)
+        c.step()   # warm-up (first-touch of the factor buffers)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < budget_s / 2 or n < 2:
+            c.step()
+            n += 1
+        dt = (time.perf_counter() - t0) / n
+        c.close()
+        forms[f"{th} threads"] = 1.0 / dt
+        log(f"cpu GN (host multifrontal) threads={th}: {dt * 1e3:.0f} ms/iteration ({n} iterations)")
+        if best is None or 1.0 / dt > best[0]:
+            best = (1.0 / dt, th, n)
+    return {"value": best[0], "unit": "it/s", "cores": best[1], "kind": "port",
+            "sample": f"{best[2]} GN iterations of config 3 by the build's C++ CPU backend (fp64 J+H, host "
+                      f"multifrontal Cholesky, box-plus) on {best[1]} threads; best of 1 and {cpus['usable']} threads",
+            "forms_it_per_s": forms, "host": cpus}
 
 
 PROFILE_TAG = "r02"   # profiles/<tag>_pmc_linearize_<prec>.json, written by tools/pmc_summary.py
@@ -151,6 +163,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gn-other", action="store_true", help="skip timing the other solver ordering")
     ap.add_argument("--tri-steps", type=int, default=20, help="device triangulations timed (0: skip)")
+    ap.add_argument("--exchange", choices=["rccl", "gloo"], default="rccl",
+                    help="N > 1: the sharded step's two all-gathers on RCCL (default), or through host memory "
+                         "and gloo (rehearsal of the N-rank path on fewer GPUs, with --same-device)")
+    ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (rehearsal only)")
     ap.add_argument("--solver", choices=["supernodal", "schur"], default="schur",
                     help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
                          "nested-dissection multifrontal; the other one is timed too (gn_other)")
@@ -177,13 +193,14 @@ def main():
         f"({time.perf_counter() - t_gen:.1f} s)")
 
     nccl_id = None
-    if world > 1:
+    if world > 1 and args.exchange == "rccl":
         obj = [bos.nccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         nccl_id = obj[0]
+    device = 0 if args.same_device else local_rank
     t_create = time.perf_counter()
     solver = bos.BOS_SOLVER_SCHUR if args.solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
-    S = bos.Solver(P, precision=precision, solver=solver, device=local_rank, rank=rank, world_size=world,
+    S = bos.Solver(P, precision=precision, solver=solver, device=device, rank=rank, world_size=world,
                    nccl_id=nccl_id)
     info = S.system_info()
     log(f"rank {rank}: bos_create {time.perf_counter() - t_create:.1f} s, n={info['n']} "
@@ -215,12 +232,27 @@ def main():
     # iteration, where the solver's factor streams between two builds
     cold_ms = S.time_linearize(args.cold_steps, flush_caches=True) if args.cold_steps > 0 else None
 
-    # ---- full GN iterations (J+H + exchange + solve + update)
+    # ---- full GN iterations (J+H + exchanges + solve + update)
+    def gloo_allgather(h, which):
+        mine = torch.from_numpy(h.exchange_download(which))
+        parts = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        h.exchange_upload(which, torch.cat(parts).numpy())
+
+    def gn_step(h):
+        if world == 1 or args.exchange == "rccl":
+            return h.step()
+        h.step_phase(0)
+        gloo_allgather(h, 1)
+        h.step_phase(1)
+        gloo_allgather(h, 2)
+        return h.step_phase(2)
+
     def time_gn(solver_handle):
-        solver_handle.step()   # first iteration includes the one-time factorization analysis
+        gn_step(solver_handle)   # first iteration includes the one-time factorization analysis
         barrier()
         tg = time.perf_counter()
-        stats = [solver_handle.step() for _ in range(args.gn_steps)]
+        stats = [gn_step(solver_handle) for _ in range(args.gn_steps)]
         barrier()
         gn_wall = max_over_ranks(time.perf_counter() - tg)
         assert all(g["solver_info"] == 0 for g in stats), "non-positive pivot in a benchmarked GN step"
@@ -283,7 +315,8 @@ def main():
                             "edges; J+H build " + ("fp32" if precision == bos.BOS_FP32 else "fp64") +
                             " (solve fp64, " + args.solver + ")",
                 "poses": P.NP, "landmarks": P.NL, "bearings": int(len(P.b_z)), "odometry": int(len(P.o_z)),
-                "parallelism": f"observation-sharded x{world}" if world > 1 else "single GPU",
+                "parallelism": (f"subtree-sharded x{world} ({'RCCL' if args.exchange == 'rccl' else 'gloo rehearsal'} "
+                                f"all-gathers; top fronts replicated: {info['top_fronts']})") if world > 1 else "single GPU",
             },
             "gn_iters_per_s": gn_it_s,
             "gn_phase_ms": phase,

@@ -95,6 +95,16 @@ int bos_plan_node_owner(const bos_problem* problem, int32_t solver, int32_t worl
 int bos_plan_shard_selftest(const bos_problem* problem, int32_t solver, int32_t world, const double* vals,
                             const double* rhs, double* x);
 
+/* CPU baseline of bench.py (the build's own C++ CPU backend on the host's cores):
+ * one GN iteration per bos_cpu_gn_step — J+H over the plan's lanes (fp64), the multifrontal
+ * factorization and solves of the plan's tree with each level's fronts in parallel, box-plus — on
+ * `threads` threads. A separate object: bos_create / bos_step never use it (no CPU fallback). */
+typedef struct bos_cpu_gn bos_cpu_gn;
+int bos_cpu_gn_create(const bos_problem* problem, int32_t solver, int32_t threads, bos_cpu_gn** out);
+int bos_cpu_gn_step(bos_cpu_gn* c, double* chi2);
+int bos_cpu_gn_get_state(const bos_cpu_gn* c, double* pose_xyt, double* landmark_xy);
+void bos_cpu_gn_destroy(bos_cpu_gn* c);
+
 /* Benchmark helpers (bench.py; HIP events on the handle's stream, no torch):
  * bos_time_linearize: n J+H builds (+ the exchange when sharded). flush_caches = 0: back to back,
  * the average per build; flush_caches = 1: 1 GiB is read before each build so its inputs come from

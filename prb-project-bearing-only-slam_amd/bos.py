@@ -44,7 +44,8 @@ EXPORTED_SYMBOLS = [
     "bos_plan_node_owner", "bos_step_phase", "bos_exchange_size", "bos_exchange_download", "bos_exchange_upload",
     "bos_node_owner",
     "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall",
-    "bos_time_linearize", "bos_time_triangulate",
+    "bos_time_linearize", "bos_time_triangulate", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
+    "bos_cpu_gn_destroy",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -164,6 +165,11 @@ def lib():
         "bos_debug_inject_stall": (ctypes.c_int, [vp]),
         "bos_time_linearize": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, _dp]),
         "bos_time_triangulate": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
+        "bos_cpu_gn_create": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.POINTER(vp)]),
+        "bos_cpu_gn_step": (ctypes.c_int, [vp, _dp]),
+        "bos_cpu_gn_get_state": (ctypes.c_int, [vp, _dp, _dp]),
+        "bos_cpu_gn_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -362,6 +368,40 @@ def plan_node_owner(P: Problem, world: int, solver: int = BOS_SOLVER_SCHUR) -> n
     o = np.zeros(P.NP + P.NL, dtype=np.int32)
     _check(lib().bos_plan_node_owner(ctypes.byref(cs), solver, world, _ptr(o, ctypes.c_int32)), "plan_node_owner")
     return o
+
+
+class CpuGN:
+    """The CPU baseline of bench.py (include/bos_host.h bos_cpu_gn_*): the same GN iteration on the
+    host's cores with the build's own host multifrontal Cholesky. Not a fallback of Solver."""
+
+    def __init__(self, P: Problem, threads: int, solver: int = BOS_SOLVER_SCHUR):
+        self.P = P
+        self._h = ctypes.c_void_p()
+        cs = P.c_struct()
+        _check(lib().bos_cpu_gn_create(ctypes.byref(cs), solver, threads, ctypes.byref(self._h)), "bos_cpu_gn_create")
+
+    def step(self) -> float:
+        c = ctypes.c_double(0)
+        _check(lib().bos_cpu_gn_step(self._h, ctypes.byref(c)), "bos_cpu_gn_step")
+        return c.value
+
+    def get_state(self):
+        pose = np.zeros((self.P.NP, 3))
+        lm = np.zeros((self.P.NL, 2))
+        _check(lib().bos_cpu_gn_get_state(self._h, _ptr(pose, ctypes.c_double), _ptr(lm, ctypes.c_double)),
+               "bos_cpu_gn_get_state")
+        return pose, lm
+
+    def close(self):
+        if self._h:
+            lib().bos_cpu_gn_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def nccl_unique_id() -> bytes:

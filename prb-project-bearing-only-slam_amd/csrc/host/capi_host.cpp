@@ -11,6 +11,7 @@
 
 #include "../../../include/bos_host.h"
 #include "g2o_utils.hpp"
+#include "host_mf.hpp"
 #include "plan.hpp"
 #include "synthetic.hpp"
 #include "triangulation.hpp"
@@ -110,139 +111,6 @@ bos::ProblemIndex index_of(const bos_problem* pb) {
     pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
     return pi;
 }
-
-// The multifrontal algorithm of hip/multifrontal.hip on the host (test hooks only): factor, forward
-// and backward over the fronts a predicate selects, in level order, with the plan's maps. The block
-// array holds what this plan's J+H writes: vals (stored entries of H_nf, one-rank order) through
-// its csr_src.
-struct HostMf {
-    const bos::Plan& P;
-    const bos::Multifrontal& F;
-    std::vector<double> hval, L, U, u, x;
-    std::vector<std::vector<double>> fwv;
-    HostMf(const bos::Plan& plan, const double* vals, const double* rhs)
-        : P(plan), F(plan.mf), hval(plan.blk.size, 0.0), L(plan.mf.L_size), U(plan.mf.U_size), u(plan.mf.u_size),
-          x(rhs, rhs + plan.n), fwv(plan.mf.nsuper) {
-        for (int64_t e = 0; e < P.nnzA(); ++e)
-            if (P.blk.csr_src[e] >= 0) hval[P.blk.csr_src[e]] = vals[e];
-    }
-    // folded landmark children (Schur ordering): the fold records, as fold_children reads them;
-    // their u entries accumulate per parent in fwv
-    void fold(int s, std::vector<double>& W, int m) {
-        fwv[s].assign(m, 0.0);
-        for (int ch = F.fold_cptr[s]; ch < F.fold_cptr[s + 1]; ++ch) {
-            const int q0 = F.fold_chunk[ch], nq = F.fold_chunk[ch + 1] - q0;
-            std::vector<double> l0(nq), l1(nq);
-            std::vector<int> pos(nq), rcs(nq);
-            for (int q = 0; q < nq; ++q) {
-                const int32_t* rec = F.fold_rec.data() + (size_t)bos::kFoldRec * (q0 + q);
-                auto v = [&](int32_t src) { return src >= 0 ? hval[src] : 0.0; };
-                const int col0 = rec[5], t = rec[6] & 63, rc = (rec[6] >> 6) & 63;
-                const double l00 = std::sqrt(std::max(v(rec[2]), 1e-300)), l10 = v(rec[3]) / l00;
-                const double l11 = std::sqrt(std::max(v(rec[4]) - l10 * l10, 1e-300));
-                l0[q] = v(rec[0]) / l00;
-                l1[q] = (v(rec[1]) - l0[q] * l10) / l11;
-                const double y0 = x[col0] / l00, y1 = (x[col0 + 1] - l10 * y0) / l11;
-                double* Lc = L.data() + rec[7];
-                const int mc = 2 + rc;
-                Lc[2 + t] = l0[q];
-                Lc[mc + 2 + t] = l1[q];
-                if (t == 0) { Lc[0] = l00; Lc[1] = l10; Lc[mc + 1] = l11; }
-                pos[q] = (rec[6] >> 12) & 63;
-                rcs[q] = rc;
-                fwv[s][pos[q]] -= l0[q] * y0 + l1[q] * y1;
-            }
-            for (int q = 0; q < nq; ++q) {   // the landmarks' forward results, after every row used them
-                const int32_t* rec = F.fold_rec.data() + (size_t)bos::kFoldRec * (q0 + q);
-                if ((rec[6] & 63) == 0) {
-                    const int col0 = rec[5];
-                    const double* Lc = L.data() + rec[7];
-                    const double y0 = x[col0] / Lc[0];
-                    x[col0 + 1] = (x[col0 + 1] - Lc[1] * y0) / Lc[2 + ((rec[6] >> 6) & 63) + 1];
-                    x[col0] = y0;
-                }
-            }
-            for (int c0 = 0; c0 < nq; c0 += rcs[c0])
-                for (int j = c0; j < c0 + rcs[c0]; ++j)
-                    for (int i = j; i < c0 + rcs[c0]; ++i)
-                        W[pos[i] + (size_t)pos[j] * m] -= l0[i] * l0[j] + l1[i] * l1[j];
-        }
-    }
-    template <typename Pred> void factor(Pred sel) {
-        for (int lv = 0; lv < F.nlevels; ++lv)
-            for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
-                const int s = F.level[q], k = F.k[s], r = F.r[s], m = k + r;
-                if (!sel(s)) continue;
-                std::vector<double> W((size_t)m * m, 0.0);
-                for (int a = F.amap_ptr[s]; a < F.amap_ptr[s + 1]; ++a) {
-                    int64_t d = F.amap_dst[a];
-                    if (m <= bos::kMfWaveMaxM) {   // packed lower column-major -> (i, j)
-                        int64_t j = 0;
-                        while (d >= m - j) { d -= m - j; ++j; }
-                        d = (j + d) + j * m;
-                    }
-                    W[d] = hval[F.amap_src[a]];
-                }
-                fold(s, W, m);
-                for (int ci = F.child_ptr[s] + F.fold_cnt[s]; ci < F.child_ptr[s + 1]; ++ci) {
-                    const int c = F.child[ci], rc2 = F.r[c];
-                    const int32_t* map = F.rmap.data() + F.rmap_off[c];
-                    for (int j = 0; j < rc2; ++j)
-                        for (int i = j; i < rc2; ++i) W[map[i] + (size_t)map[j] * m] += U[F.U_off[c] + bos::mf_packed(i, j, rc2)];
-                }
-                for (int j = 0; j < k; ++j) {
-                    const double d = std::sqrt(std::max(W[j + (size_t)j * m], 1e-300));
-                    W[j + (size_t)j * m] = d;
-                    for (int i = j + 1; i < m; ++i) W[i + (size_t)j * m] /= d;
-                    for (int l = j + 1; l < m; ++l)
-                        for (int i = l; i < m; ++i) W[i + (size_t)l * m] -= W[i + (size_t)j * m] * W[l + (size_t)j * m];
-                }
-                for (int j = 0; j < k; ++j)
-                    for (int i = 0; i < m; ++i) L[F.L_off[s] + i + (size_t)j * m] = W[i + (size_t)j * m];
-                for (int j = 0; j < r; ++j)
-                    for (int i = j; i < r; ++i) U[F.U_off[s] + bos::mf_packed(i, j, r)] = W[(k + i) + (size_t)(k + j) * m];
-            }
-    }
-    template <typename Pred> void forward(Pred sel) {
-        for (int lv = 0; lv < F.nlevels; ++lv)
-            for (int q = F.level_ptr[lv]; q < F.level_ptr[lv + 1]; ++q) {
-                const int s = F.level[q], k = F.k[s], r = F.r[s], m = k + r;
-                if (!sel(s)) continue;
-                std::vector<double> w(m, 0.0);
-                for (int i = 0; i < k; ++i) w[i] = x[F.col0[s] + i];
-                for (size_t i = 0; i < fwv[s].size(); ++i) w[i] += fwv[s][i];
-                for (int ci = F.child_ptr[s] + F.fold_cnt[s]; ci < F.child_ptr[s + 1]; ++ci) {
-                    const int c = F.child[ci];
-                    for (int t = 0; t < F.r[c]; ++t) w[F.rmap[F.rmap_off[c] + t]] += u[F.u_off[c] + t];
-                }
-                const double* Ls = L.data() + F.L_off[s];
-                for (int j = 0; j < k; ++j) {
-                    w[j] /= Ls[j + (size_t)j * m];
-                    for (int i = j + 1; i < m; ++i) w[i] -= Ls[i + (size_t)j * m] * w[j];
-                }
-                for (int i = 0; i < k; ++i) x[F.col0[s] + i] = w[i];
-                for (int t = 0; t < r; ++t) u[F.u_off[s] + t] = w[k + t];
-            }
-    }
-    // top-down over the selected fronts, then their folded landmarks
-    template <typename Pred> void backward(Pred sel) {
-        std::vector<int32_t> bwd;
-        for (auto it = F.level.rbegin(); it != F.level.rend(); ++it)
-            if (sel(*it)) bwd.push_back(*it);
-        for (int s : F.fold_list)
-            if (sel(F.parent[s])) bwd.push_back(s);
-        for (int s : bwd) {
-            const int k = F.k[s], m = k + F.r[s];
-            const double* Ls = L.data() + F.L_off[s];
-            const int32_t* fi = F.findex.data() + F.findex_off[s];
-            for (int j = k - 1; j >= 0; --j) {
-                double acc = x[F.col0[s] + j];
-                for (int i = j + 1; i < m; ++i) acc -= Ls[i + (size_t)j * m] * x[fi[i]];
-                x[F.col0[s] + j] = acc / Ls[j + (size_t)j * m];
-            }
-        }
-    }
-};
 
 }  // namespace
 
@@ -457,7 +325,7 @@ int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* va
     std::string err;
     const int rc = bos::build_plan(index_of(pb), 0, 1, factor_mode_of(solver), P, err);
     if (rc) return hfail(rc, err);
-    HostMf M(P, vals, rhs);
+    bos::HostMf M(P, vals, rhs);
     auto all = [](int) { return true; };
     M.factor(all);
     M.forward(all);
@@ -495,12 +363,12 @@ int bos_plan_shard_selftest(const bos_problem* pb, int32_t solver, int32_t world
     }
     const int64_t n = one.n;
     // the one-rank run: the values each rank's J+H computes are the one-rank values of those entries
-    HostMf ref(one, vals, rhs);
+    bos::HostMf ref(one, vals, rhs);
     auto all = [](int) { return true; };
     ref.factor(all);
     ref.forward(all);
     ref.backward(all);
-    std::vector<HostMf> M;
+    std::vector<bos::HostMf> M;
     M.reserve(world);
     for (int r = 0; r < world; ++r) {
         const bos::Plan& P = plans[r];

@@ -31,48 +31,72 @@ Solver::Solver(const State& st, const BearingObservationVector& bear_obs, const 
     : state(st), bearing_observations(bear_obs), odometry_observations(odom_obs), fixed_pose_id_(fixed_pose_id) {
     // SoA problem in stix order; ids resolved once (std::map::at throws on unknown ids like the reference)
     const int NP = state.number_of_poses(), NL = state.number_of_landmarks();
-    std::vector<double> pose(3 * (size_t)NP), lm(2 * (size_t)NL);
+    pose_.resize(3 * (size_t)NP);
+    lm_.resize(2 * (size_t)NL);
     for (int i = 0; i < NP; ++i) {
         const NEPose& p = state.poses_vec()[i];
-        pose[3 * i] = p.x; pose[3 * i + 1] = p.y; pose[3 * i + 2] = p.theta;
+        pose_[3 * i] = p.x; pose_[3 * i + 1] = p.y; pose_[3 * i + 2] = p.theta;
     }
-    for (int j = 0; j < NL; ++j) { lm[2 * j] = state.landmarks_vec()[j].x; lm[2 * j + 1] = state.landmarks_vec()[j].y; }
+    for (int j = 0; j < NL; ++j) { lm_[2 * j] = state.landmarks_vec()[j].x; lm_[2 * j + 1] = state.landmarks_vec()[j].y; }
     const size_t Mb = bearing_observations.size(), Mo = odometry_observations.size();
-    std::vector<int32_t> bp(Mb), bl(Mb), os(Mo), od(Mo);
-    std::vector<double> bz(Mb), bw(Mb), oz(3 * Mo), om(9 * Mo);
-    bool w1 = true;
+    bp_.resize(Mb); bl_.resize(Mb); os_.resize(Mo); od_.resize(Mo);
+    bz_.resize(Mb); bw_.resize(Mb); oz_.resize(3 * Mo); om_.resize(9 * Mo);
     for (size_t k = 0; k < Mb; ++k) {
         const BearingObservation& o = bearing_observations[k];
-        bp[k] = state.pose_stix(o.get_pose_id());
-        bl[k] = state.landmark_stix(o.get_lm_id());
-        bz[k] = o.get_bearing_angle();
-        bw[k] = o.get_omega();
-        w1 = w1 && bw[k] == 1.0;
+        bp_[k] = state.pose_stix(o.get_pose_id());
+        bl_[k] = state.landmark_stix(o.get_lm_id());
+        bz_[k] = o.get_bearing_angle();
+        bw_[k] = o.get_omega();
+        w1_ = w1_ && bw_[k] == 1.0;
     }
     for (size_t k = 0; k < Mo; ++k) {
         const OdometryObservation& o = odometry_observations[k];
-        os[k] = state.pose_stix(o.get_source_id());
-        od[k] = state.pose_stix(o.get_dest_id());
+        os_[k] = state.pose_stix(o.get_source_id());
+        od_[k] = state.pose_stix(o.get_dest_id());
         const EPose z = o.get_transformation();
-        oz[3 * k] = z.x; oz[3 * k + 1] = z.y; oz[3 * k + 2] = z.z;
+        oz_[3 * k] = z.x; oz_[3 * k + 1] = z.y; oz_[3 * k + 2] = z.z;
         const Mat3 m = o.get_omega();
         for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) om[9 * k + 3 * r + c] = m(r, c);
+            for (int c = 0; c < 3; ++c) om_[9 * k + 3 * r + c] = m(r, c);
+    }
+    (void)state.pose_stix(fixed_pose_id);   // unknown fixed pose id: std::out_of_range now, like the reference
+    bos_default_options(&opt_);
+    if (options) opt_ = *options;
+}
+
+bos_solver* Solver::ensure() {
+    if (h_) return h_;
+    // the public state as it is now (the reference's step() reads its member state)
+    for (int i = 0; i < state.number_of_poses(); ++i) {
+        const NEPose& p = state.poses_vec()[i];
+        pose_[3 * i] = p.x; pose_[3 * i + 1] = p.y; pose_[3 * i + 2] = p.theta;
+    }
+    for (int j = 0; j < state.number_of_landmarks(); ++j) {
+        lm_[2 * j] = state.landmarks_vec()[j].x;
+        lm_[2 * j + 1] = state.landmarks_vec()[j].y;
     }
     bos_problem pb;
-    pb.num_poses = NP; pb.num_landmarks = NL; pb.num_bearings = (int32_t)Mb; pb.num_odometry = (int32_t)Mo;
-    pb.pose_xyt = pose.data(); pb.landmark_xy = lm.data();
-    pb.bearing_pose = bp.data(); pb.bearing_landmark = bl.data(); pb.bearing_z = bz.data();
-    pb.bearing_omega = w1 ? nullptr : bw.data();
-    pb.odom_src = os.data(); pb.odom_dst = od.data(); pb.odom_z = oz.data(); pb.odom_omega = om.data();
-    pb.fixed_pose = state.pose_stix(fixed_pose_id);
-    check(bos_create(&pb, options, &h_), "bos_create");
+    pb.num_poses = state.number_of_poses(); pb.num_landmarks = state.number_of_landmarks();
+    pb.num_bearings = (int32_t)bz_.size(); pb.num_odometry = (int32_t)os_.size();
+    pb.pose_xyt = pose_.data(); pb.landmark_xy = lm_.data();
+    pb.bearing_pose = bp_.data(); pb.bearing_landmark = bl_.data(); pb.bearing_z = bz_.data();
+    pb.bearing_omega = w1_ ? nullptr : bw_.data();
+    pb.odom_src = os_.data(); pb.odom_dst = od_.data(); pb.odom_z = oz_.data(); pb.odom_omega = om_.data();
+    pb.fixed_pose = state.pose_stix(fixed_pose_id_);
+    check(bos_create(&pb, &opt_, &h_), "bos_create");
+    return h_;
 }
 
 Solver::~Solver() { bos_destroy(h_); }
 
-void Solver::set_kernel_threshold(float kt) { check(bos_set_kernel_threshold(h_, kt), "set_kernel_threshold"); }
-void Solver::set_damping_factor(float df) { check(bos_set_damping_factor(h_, df), "set_damping_factor"); }
+void Solver::set_kernel_threshold(float kt) {
+    opt_.kernel_threshold = kt;
+    if (h_) check(bos_set_kernel_threshold(h_, kt), "set_kernel_threshold");
+}
+void Solver::set_damping_factor(float df) {
+    opt_.damping = df;
+    if (h_) check(bos_set_damping_factor(h_, df), "set_damping_factor");
+}
 
 void Solver::sync_state() {
     const int NP = state.number_of_poses(), NL = state.number_of_landmarks();
@@ -83,12 +107,12 @@ void Solver::sync_state() {
 }
 
 void Solver::step() {
-    check(bos_step(h_, &stats_), "bos_step");
+    check(bos_step(ensure(), &stats_), "bos_step");
     sync_state();
 }
 
 void Solver::step_n(int n) {
-    check(bos_step_n(h_, n, &stats_), "bos_step_n");
+    check(bos_step_n(ensure(), n, &stats_), "bos_step_n");
     sync_state();
 }
 

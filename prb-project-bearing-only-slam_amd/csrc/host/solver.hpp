@@ -1,5 +1,9 @@
 // proj02::Solver — C++ façade with the reference's API (slam/solver.hpp:21-92) over the C ABI
 // (include/bos.h). step() runs on the GPU (HIP kernels + GPU sparse Cholesky); there is no CPU path.
+// Like the reference's ctor (slam/solver.cpp:5-18) the constructor only copies and resolves ids
+// (an unknown id throws std::out_of_range); the device handle is created by the first call that
+// needs it (step, step_n, handle), so the per-observation API (predict_*, error_and_*jacobian) —
+// what the reference's harness tests/solver_stuff.cpp calls — works on a host without a GPU.
 //
 // Differences to the reference, all documented in INTEGRATION.md:
 //  - SparseMatrixXf Jacobians (Eigen) become small dense blocks with their column indices
@@ -50,7 +54,7 @@ class Solver {
     void step();                           // :36 — one GN iteration, state updated on return
     void step_n(int n);                    // n iterations, one state download at the end
     const bos_step_stats& last_stats() const { return stats_; }
-    bos_solver* handle() { return h_; }
+    bos_solver* handle() { return ensure(); }
 
     // :38-44
     void error_and_jacobian(const State& state, const BearingObservation& obs, double& error, JacobianRow& J);
@@ -66,9 +70,15 @@ class Solver {
 
   private:
     void sync_state();
+    bos_solver* ensure();   // creates the device handle on first use
     bos_solver* h_ = nullptr;
     int fixed_pose_id_;
     bos_step_stats stats_ = {};
+    // the problem in the C ABI's SoA form (bos_create copies it)
+    std::vector<double> pose_, lm_, bz_, bw_, oz_, om_;
+    std::vector<int32_t> bp_, bl_, os_, od_;
+    bool w1_ = true;
+    bos_options opt_;
 };
 
 }  // namespace proj02

@@ -271,3 +271,23 @@ def test_stall_is_an_error_and_leaves_the_state(c2):
         S.step_n(3)
     S.close()
     R.close()
+
+
+def test_headless_driver_50_iterations_matches_oracle(c1, tmp_path):
+    """The drop-in executable (csrc/apps/bearing_only_slam.cpp: the reference's main flow through the
+    proj02::Solver façade, executables/bearing_only_slam.cpp:40-116) run for the reference's 50
+    iterations with --dump: the written state equals the oracle's 50-iteration state within the C1
+    bound (1e-6 relative, 1e-9 absolute)."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    exe = os.path.join(ROOT, "prb-project-bearing-only-slam_amd", "lib", "bearing_only_slam")
+    out = tmp_path / "c1_50.g2o"
+    res = subprocess.run([exe, C1, "--iters", "50", "--quiet", "--dump", str(out)], capture_output=True, text=True,
+                         timeout=120)
+    assert res.returncode == 0, res.stdout + res.stderr
+    D = bos.load_g2o(str(out), triangulate=False)
+    assert np.array_equal(D.pose_ids, c1.pose_ids) and np.array_equal(D.lm_ids, c1.lm_ids)
+    po, lo, _ = O.run(to_oracle(c1), 50)
+    ok, ep, el = _close_state(D.pose_xyt, D.lm_xy, po, lo)
+    assert ok, (ep, el)

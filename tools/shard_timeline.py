@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-rank phase times of the sharded GN step on ONE GPU (ranks run one after another, each alone
+on the device, exchanges by host copies): what each rank's GPU would spend per iteration on an
+N-GPU node, minus the two RCCL all-gathers. Config 3, fp32 J+H, Schur solver.
+
+    python tools/shard_timeline.py [worlds...]      (default 1 2 4 8)
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "prb-project-bearing-only-slam_amd"))
+import numpy as np  # noqa: E402
+
+import bos  # noqa: E402
+
+worlds = [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]
+P = bos.synthetic(100000, 200000, 10, seed=0xB05EED01 + 3)
+out = {}
+for W in worlds:
+    t0 = time.perf_counter()
+    if W == 1:
+        S = [bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, rank=0, world_size=1,
+                        nccl_id=bos.nccl_unique_id())]
+    else:
+        S = [bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=W) for r in range(W)]
+    t_create = time.perf_counter() - t0
+    rows = []
+    for it in range(6):
+        if W == 1:
+            st = [S[0].step()]
+        else:
+            for h in S:
+                h.step_phase(0)
+                h.synchronize()
+            recv = np.concatenate([h.exchange_download(1) for h in S])
+            for h in S:
+                h.exchange_upload(1, recv)
+                h.step_phase(1)
+                h.synchronize()
+            recv = np.concatenate([h.exchange_download(2) for h in S])
+            for h in S:
+                h.exchange_upload(2, recv)
+            st = [h.step_phase(2) for h in S]
+        if it >= 1:
+            rows.append([[s["t_linearize_ms"], s["t_solve_ms"], s["t_update_ms"]] for s in st])
+    a = np.median(np.array(rows), axis=0)   # [rank][phase]
+    per_rank = a.sum(axis=1)
+    info = [h.system_info() for h in S]
+    out[W] = {"create_s": t_create, "jh_ms": a[:, 0].tolist(), "solve_ms": a[:, 1].tolist(), "update_ms": a[:, 2].tolist(),
+              "max_rank_ms": float(per_rank.max()), "own_fronts": [i["own_fronts"] for i in info],
+              "top_fronts": info[0]["top_fronts"], "pose_lane_groups": [i["pose_lane_groups"] for i in info]}
+    print(f"W={W}: per-rank compute (J+H + solve + update) max {per_rank.max():.3f} ms "
+          f"(J+H {a[:, 0].max():.3f}, solve {a[:, 1].max():.3f}, update {a[:, 2].max():.3f}); top fronts "
+          f"{info[0]['top_fronts']}; create {t_create:.1f} s", flush=True)
+    for h in S:
+        h.close()
+print(json.dumps(out))
