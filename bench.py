@@ -218,7 +218,8 @@ def main():
         return float(t.item())
 
     # ---- J+H build throughput: K builds back to back (the timed region), warm caches
-    S.time_linearize(args.warmup)
+    if args.warmup > 0:
+        S.time_linearize(args.warmup)
     S.synchronize()
     barrier()
     S.synchronize()

@@ -122,6 +122,9 @@ void bos_debug_set_g2o_parser(int32_t line_by_line);
  * wait times out — bos_step must then fail with BOS_ERR_SOLVER and leave the state untouched.
  * BOS_ERR_UNSUPPORTED when the handle's solver has no dataflow launch. */
 int bos_debug_inject_stall(struct bos_solver* s);
+/* Test hook: run the one-GPU GN step as individual launches (enable = 0) instead of the captured
+ * hipGraph replay (1, default). The same kernels in the same order either way. */
+int bos_debug_set_step_graph(struct bos_solver* s, int32_t enable);
 
 /* Diagnostics: one J+H launch with per-wave timeline stamps, 8 x uint64 per wave: block, wave in
  * block, kind (0 pose lanes / 1 landmark lanes), t_start, t_loop, t_loop_end, t_end (realtime clock,

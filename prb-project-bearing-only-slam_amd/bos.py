@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async", "bos_plan_shard_selftest",
     "bos_plan_node_owner", "bos_step_phase", "bos_exchange_size", "bos_exchange_download", "bos_exchange_upload",
     "bos_node_owner",
-    "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall",
+    "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph",
     "bos_time_linearize", "bos_time_triangulate", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
     "bos_cpu_gn_destroy",
 ]
@@ -163,6 +163,7 @@ def lib():
         "bos_debug_set_schur_leaf": (None, [ctypes.c_int32]),
         "bos_debug_set_g2o_parser": (None, [ctypes.c_int32]),
         "bos_debug_inject_stall": (ctypes.c_int, [vp]),
+        "bos_debug_set_step_graph": (ctypes.c_int, [vp, ctypes.c_int32]),
         "bos_time_linearize": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, _dp]),
         "bos_time_triangulate": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
         "bos_cpu_gn_create": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32,
@@ -516,6 +517,10 @@ class Solver:
         """Test hook: the next step's factor dataflow launch skips its first front (a stalled
         dependency); that step must fail with BOS_ERR_SOLVER and leave the state unchanged."""
         _check(lib().bos_debug_inject_stall(self._h), "bos_debug_inject_stall")
+
+    def debug_set_step_graph(self, enable: bool):
+        """Test hook: GN steps as individual launches (False) or the captured graph (True, default)."""
+        _check(lib().bos_debug_set_step_graph(self._h, int(enable)), "bos_debug_set_step_graph")
 
     def time_linearize(self, n: int, flush_caches: bool = False) -> float:
         """ms per J+H build (HIP events on the handle's stream, see bos_time_linearize)."""

@@ -367,6 +367,7 @@ __global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams
     const int64_t b = blockIdx.x < P.pose_blocks ? xcd_contiguous(blockIdx.x, 0, P.pose_blocks)
                                                  : xcd_contiguous(blockIdx.x, P.pose_blocks, nb);
     unsigned long long st[3] = {0, 0, 0};
+    if (P.t_start && blockIdx.x == 0 && threadIdx.x == 0) *P.t_start = __builtin_amdgcn_s_memrealtime();
     stamp(P.diag_stamps, st, 0);
     if (b >= P.pose_blocks) {   // block-uniform branch
         landmark_lane<T, HAS_W>(P, (int)(b - P.pose_blocks), st);
@@ -452,7 +453,7 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
 
 __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
                                     int32_t nrob_const, const double* max_part, int n_max, int32_t* info,
-                                    int first, StepStatus* out) {
+                                    StepStatus* out) {
     __shared__ double sc[256];
     __shared__ double sm[256];
     __shared__ long long sr[256];
@@ -479,9 +480,15 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
         out->max_dx = sm[0];
         const int32_t inf = info ? *info : 0;
         out->info = inf;
-        out->aborted = (first ? 0 : out->aborted) | (inf & kStepAbort);
+        out->aborted |= inf & kStepAbort;
         if (info) *info = 0;
+        out->stamp[3] = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+__global__ void step_mark_kernel(unsigned long long* stamp, uint32_t* epoch) {
+    if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
+    if (epoch) *epoch += 1u;
 }
 
 // triangulate_one_landmark (slam/triangulation.cpp:21-62): the rows [sin(th + z), -cos(th + z)],
@@ -631,7 +638,7 @@ __global__ void index_copy_kernel(const double* src, const int32_t* si, double* 
 }
 
 __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                     double chi_const, int32_t nrob_const, int first, StepStatus* out) {
+                                     double chi_const, int32_t nrob_const, StepStatus* out) {
     if (threadIdx.x != 0) return;
     double chi = 0.0, m = 0.0;
     long long nr = 0, piv = 0;
@@ -648,7 +655,8 @@ __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const doub
     out->n_robust = (int32_t)nr + nrob_const;
     out->max_dx = m;
     out->info = (int32_t)min(piv, (long long)(kStepAbort - 1)) | abort_bits;
-    out->aborted = (first ? 0 : out->aborted) | abort_bits;
+    out->aborted |= abort_bits;
+    out->stamp[3] = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ __launch_bounds__(256) void cache_scrub_kernel(const double* buf, int64_t n, double* sink) {
@@ -730,10 +738,15 @@ template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipSt
 }
 
 hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
-                               int32_t nrob_const, const double* max_part, int n_max, int32_t* info, bool first,
+                               int32_t nrob_const, const double* max_part, int n_max, int32_t* info,
                                StepStatus* out, hipStream_t s) {
     hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n, chi_const, nrob_const,
-                       max_part, n_max, info, (int)first, out);
+                       max_part, n_max, info, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_step_mark(unsigned long long* stamp, uint32_t* epoch, hipStream_t s) {
+    hipLaunchKernelGGL(step_mark_kernel, dim3(1), dim3(1), 0, s, stamp, epoch);
     return hipGetLastError();
 }
 
@@ -762,9 +775,9 @@ hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* 
 }
 
 hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                double chi_const, int32_t nrob_const, bool first, StepStatus* out, hipStream_t s) {
+                                double chi_const, int32_t nrob_const, StepStatus* out, hipStream_t s) {
     hipLaunchKernelGGL(shard_combine_kernel, dim3(1), dim3(64), 0, s, recv1, c1, recv2, c2, world, chi_const, nrob_const,
-                       (int)first, out);
+                       out);
     return hipGetLastError();
 }
 

@@ -61,6 +61,7 @@ template <typename T> struct LinParams {
     T kt;                     // robust kernel threshold
     T lambda;                 // damping
     unsigned long long* diag_stamps;   // timeline diagnostics only (8 x u64 per wave), null otherwise
+    unsigned long long* t_start;       // phase timing: block 0 writes the realtime clock at its start, or null
 };
 
 template <typename T> struct UpdateParams {
@@ -88,9 +89,13 @@ struct StepStatus {
     double max_dx;
     int32_t n_robust;
     int32_t info;     // solver status: count of non-positive pivots, | kStepAbort (see above)
-    int32_t aborted;  // kStepAbort if any step since the last reset (first step of a bos_step_n batch) aborted
+    int32_t aborted;  // sticky: kStepAbort once any step aborted; the host clears it when it reports it
     int32_t pad;
+    // phase boundaries of the last step, realtime clock (100 MHz): J+H start, J+H end / solve start,
+    // solve end / update start, step end (written by the step's own kernels: no events in the step)
+    unsigned long long stamp[4];
 };
+constexpr double kStampMs = 1e-5;   // one realtime tick in ms
 
 constexpr int kUpdateBlock = 256;
 
@@ -138,17 +143,21 @@ hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* 
                              hipStream_t s);
 // All ranks' headers -> *out (chi^2 and robust count summed in rank order plus the self-loop
 // terms, max |dx| the max, info: non-positive pivots summed, abort bits or-ed; `aborted` sticky
-// unless first), identical on every rank.
+// sticky), identical on every rank.
 hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                double chi_const, int32_t nrob_const, bool first, StepStatus* out, hipStream_t s);
+                                double chi_const, int32_t nrob_const, StepStatus* out, hipStream_t s);
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
 // Reduces the J+H kernel's chi^2 / robust-count partials (plus the constant terms of odometry
 // self-loops, chi_const / nrob_const) and the box-plus max |dx| partials (when max_part is set; a NaN
 // propagates) into *out, moves *info into out->info and zeroes *info for the next iteration: one
-// launch replaces the per-step memsets and read-backs.
+// launch replaces the per-step memsets and read-backs. out->aborted is sticky; out->stamp[3] gets the
+// realtime clock at the end.
 hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
-                               int32_t nrob_const, const double* max_part, int n_max, int32_t* info, bool first,
+                               int32_t nrob_const, const double* max_part, int n_max, int32_t* info,
                                StepStatus* out, hipStream_t s);
+// One thread: *stamp = realtime clock (if stamp), ++*epoch (if epoch: the multifrontal dataflow
+// launches' completion epoch, multifrontal.hpp mf_epoch_ptr). Graph-capturable phase marker.
+hipError_t launch_step_mark(unsigned long long* stamp, uint32_t* epoch, hipStream_t s);
 // Reads n doubles (all of them: the sum is compared with an impossible value), so L2 and the
 // Infinity Cache hold clean lines of this buffer afterwards (cold-cache timing, bos_time_linearize).
 hipError_t launch_cache_scrub(const double* buf, int64_t n, double* sink, hipStream_t s);

@@ -456,7 +456,9 @@ struct Flow {
     int* ticket;            // zero at launch; zeroed again by the launch's last wave
     int* exits;             // waves that have left the launch (same life cycle)
     uint32_t* done;         // per supernode: epoch of its last completion
-    uint32_t epoch;
+    const uint32_t* epoch_src;   // device word: this step's epoch (bumped once per GN step by the
+                                 // step_mark kernel before the first flow launch, mf_epoch_ptr)
+    uint32_t epoch;              // *epoch_src, read by the launch itself (graph-replayable)
     const int8_t* fid;      // per supernode: the flow launch (id) that processes it, 0 = none; a front
                             // waits only for fronts of its own launch (the others finished earlier:
                             // per-level launches, the other program, or another rank's exchange)
@@ -882,10 +884,16 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
     leave_flow(f);
 }
 
-__global__ __launch_bounds__(64, 2) void mf_factor_flow(const MfArgs a, const Flow f) { factor_flow_body(a, f); }
+__global__ __launch_bounds__(64, 2) void mf_factor_flow(const MfArgs a, const Flow f_in) {
+    Flow f = f_in;
+    f.epoch = *f_in.epoch_src;
+    factor_flow_body(a, f);
+}
 
-__global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flow f, const int32_t* parent) {
+__global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flow f_in, const int32_t* parent) {
     extern __shared__ __attribute__((aligned(16))) double w[];
+    Flow f = f_in;
+    f.epoch = *f_in.epoch_src;
     for (int it = 0; it <= f.n; ++it) {
         const int t = next_ticket(f.ticket);
         if (t >= f.n) break;
@@ -950,7 +958,7 @@ struct MfDevice {
     int32_t* parent = nullptr;
     uint32_t* done = nullptr;     // [2][nsuper]: factor, backward
     int* tickets = nullptr;       // [2 * kMfTickets]: work-queue tickets, then the launches' exit counters
-    uint32_t epoch = 0;
+    uint32_t* epoch = nullptr;    // device word, 1 at creation (done[] starts at 0), bumped per GN step
     int32_t *fold_cnt = nullptr, *fold_cptr = nullptr, *fold_chunk = nullptr, *fold_rec = nullptr;
     int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
             *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
@@ -1086,9 +1094,17 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
     if (hipMalloc((void**)&d->done, 2 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(d->done, 0, 2 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void**)&d->tickets, 2 * kMfTickets * sizeof(int)) != hipSuccess ||
-        hipMemset(d->tickets, 0, 2 * kMfTickets * sizeof(int)) != hipSuccess) {
+        hipMemset(d->tickets, 0, 2 * kMfTickets * sizeof(int)) != hipSuccess ||
+        hipMalloc((void**)&d->epoch, sizeof(uint32_t)) != hipSuccess) {
         err = "hipMalloc failed (multifrontal flow)";
         return -2;
+    }
+    {
+        const uint32_t one = 1;
+        if (hipMemcpy(d->epoch, &one, sizeof(one), hipMemcpyHostToDevice) != hipSuccess) {
+            err = "hipMemcpy failed (multifrontal epoch)";
+            return -2;
+        }
     }
     if ((rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
         (rc = up(&d->r, F.r, err)) || (rc = up(&d->child_ptr, F.child_ptr, err)) || (rc = up(&d->child, F.child, err)) ||
@@ -1123,7 +1139,7 @@ void mf_destroy(MfDevice* d) {
     if (!d) return;
     free_prog(d->prog[0]);
     free_prog(d->prog[1]);
-    void* bufs[] = {d->fid_f, d->fid_b, d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->parent, d->done,
+    void* bufs[] = {d->epoch, d->fid_f, d->fid_b, d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->parent, d->done,
                     d->tickets, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};
@@ -1136,12 +1152,13 @@ void mf_destroy(MfDevice* d) {
 }
 
 // info is zero on entry: zeroed at creation and, after every iteration, by the end-of-step
-// reduce_stats launch (mf_info_ptr). The work-queue tickets reset themselves (leave_flow).
+// reduce_stats launch (mf_info_ptr). The work-queue tickets reset themselves (leave_flow). Every
+// launch argument is fixed (the flows read the step's epoch from the device), so the sequence can be
+// captured once into a hipGraph and replayed.
 hipError_t mf_factor(MfDevice* d, int which, const double* A, double* x, hipStream_t s) {
     hipError_t e;
     const Prog& P = d->prog[which];
     if (P.ptr.empty()) return hipSuccess;
-    const uint32_t epoch = ++d->epoch;
     for (int l = 0; l < std::min(P.flow_lev0, d->nlevels); ++l) {
         int n;
         const bool fork = d->side && P.count(l, 3) > 0;
@@ -1169,7 +1186,8 @@ hipError_t mf_factor(MfDevice* d, int which, const double* A, double* x, hipStre
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (P.n_flow_factor > 0) {
-        const Flow f{P.order_factor, P.n_flow_factor, d->tickets, d->tickets + kMfTickets, d->done, epoch, d->fid_f, P.id};
+        const Flow f{P.order_factor, P.n_flow_factor, d->tickets, d->tickets + kMfTickets, d->done, d->epoch, 0u,
+                     d->fid_f, P.id};
         const int grid = std::min(P.n_flow_factor, d->ncu * 8);   // 2 waves per SIMD resident
         hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(P, 0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1183,10 +1201,9 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
     hipError_t e;
     const Prog& P = d->prog[which];
     if (P.ptr.empty()) return hipSuccess;
-    const uint32_t epoch = ++d->epoch;
     if (P.flow_solve) {
         const Flow fb{P.order_bwd, P.n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1, d->done + d->nsuper,
-                      epoch, d->fid_b, P.id};
+                      d->epoch, 0u, d->fid_b, P.id};
         const int grid = std::min(P.n_flow_solve, d->ncu * 8);
         hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), P.lds_bwd_flow, s, d->args(P, 0, 0, nullptr, x), fb,
                            (const int32_t*)d->parent);
@@ -1211,6 +1228,7 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
 }
 
 int32_t* mf_info_ptr(const MfDevice* d) { return d->info; }
+uint32_t* mf_epoch_ptr(const MfDevice* d) { return d->epoch; }
 int32_t* mf_tickets_ptr(const MfDevice* d) { return d->tickets; }
 double* mf_update_ptr(const MfDevice* d) { return d->U; }
 double* mf_uvec_ptr(const MfDevice* d) { return d->u; }

@@ -31,6 +31,10 @@ double* mf_uvec_ptr(const MfDevice* d);
 // device word of the last factorization: count of non-positive pivots, | kMfStall when a dataflow
 // launch timed out waiting for a dependency (its results are then invalid)
 int32_t* mf_info_ptr(const MfDevice* d);
+// device word the dataflow launches compare completion flags with: must be bumped (step_mark
+// kernel, kernels.hpp) once per GN step before the step's first mf_factor; all flows of one step
+// (factor and backward, both programs when sharded) share it
+uint32_t* mf_epoch_ptr(const MfDevice* d);
 constexpr int32_t kMfStall = 1 << 30;
 // work-queue tickets (kMfTickets ints, then kMfTickets exit counters); every flow launch leaves its
 // ticket zero (the last wave out resets it)

@@ -141,6 +141,11 @@ struct bos_solver {
     // odometry self-loops: z[3] and Omega upper triangle [6] each (constant chi^2 terms)
     std::vector<double> loop_z, loop_om;
     double* scrub = nullptr;   // bos_time_linearize(flush_caches): 1 GiB read between launches
+    // one-GPU multifrontal GN step captured once into a graph (every launch argument is fixed:
+    // kernel threshold and damping are baked in, so setting them drops the graph)
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    bool graph_failed = false;   // capture not possible on this stream (e.g. the legacy null stream)
 };
 
 static_assert(bos::dev::kStepAbort == bos::dev::kMfStall, "solver abort bit");
@@ -179,6 +184,7 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.kt = (T)s->kt;
     p.lambda = (T)s->damping;
     p.diag_stamps = nullptr;
+    p.t_start = nullptr;
     return p;
 }
 
@@ -204,11 +210,18 @@ template <typename T> int upload_T(void** p, const std::vector<double>& v) {
     return rc;
 }
 
-int enqueue_linearize(bos_solver* s) {
+int enqueue_linearize(bos_solver* s, unsigned long long* t_start = nullptr) {
     hipError_t e;
     const int lpp = s->plan.blk.lpp;
-    if (s->precision == BOS_FP32) e = bos::dev::launch_linearize<float>(lin_params<float>(s), lpp, s->has_w, s->has_dups, s->stream);
-    else e = bos::dev::launch_linearize<double>(lin_params<double>(s), lpp, s->has_w, s->has_dups, s->stream);
+    if (s->precision == BOS_FP32) {
+        bos::dev::LinParams<float> p = lin_params<float>(s);
+        p.t_start = t_start;
+        e = bos::dev::launch_linearize<float>(p, lpp, s->has_w, s->has_dups, s->stream);
+    } else {
+        bos::dev::LinParams<double> p = lin_params<double>(s);
+        p.t_start = t_start;
+        e = bos::dev::launch_linearize<double>(p, lpp, s->has_w, s->has_dups, s->stream);
+    }
     if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("linearize launch: ") + hipGetErrorString(e));
     return BOS_OK;
 }
@@ -282,7 +295,7 @@ template <typename T> void self_loop_terms(const bos_solver* s, double& chi, int
     }
 }
 
-int enqueue_stats(bos_solver* s, bool with_update, bool first = true) {
+int enqueue_stats(bos_solver* s, bool with_update) {
     int32_t* info = uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : (s->solver_kind == BOS_SOLVER_DENSE_CHOL ? s->d_info : nullptr);
     const int nupd = (s->NP + s->NL + bos::dev::kUpdateBlock - 1) / bos::dev::kUpdateBlock;
     double chi_c = 0.0;
@@ -290,7 +303,7 @@ int enqueue_stats(bos_solver* s, bool with_update, bool first = true) {
     if (s->precision == BOS_FP32) self_loop_terms<float>(s, chi_c, nrob_c);
     else self_loop_terms<double>(s, chi_c, nrob_c);
     HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->chi_parts, chi_c, nrob_c,
-                                          with_update ? s->d_maxpart : nullptr, nupd, info, first, s->d_status,
+                                          with_update ? s->d_maxpart : nullptr, nupd, info, s->d_status,
                                           s->stream));
     return BOS_OK;
 }
@@ -410,16 +423,29 @@ int enqueue_triangulate(bos_solver* s) {
     return BOS_OK;
 }
 
+// The step status (one copy). The sticky abort flag is cleared here once reported, so every
+// bos_step / bos_step_n batch starts with it clear.
 int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr) {
     bos::dev::StepStatus h;
     HIP_TRY(hipMemcpyAsync(&h, s->d_status, sizeof(h), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    if (h.aborted) {
+        HIP_TRY(hipMemsetAsync(&s->d_status->aborted, 0, sizeof(int32_t), s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
     if (st) {
         std::memset(st, 0, sizeof(*st));
         st->chi2 = h.chi2;
         st->n_robust = h.n_robust;
         st->solver_info = h.info & ~bos::dev::kStepAbort;
         st->max_abs_dx = h.max_dx;
+        if (!s->sharded) {   // phase boundaries stamped by the step's kernels
+            auto d = [](unsigned long long a, unsigned long long b) { return b > a ? (double)(b - a) * bos::dev::kStampMs : 0.0; };
+            st->t_linearize_ms = d(h.stamp[0], h.stamp[1]);
+            st->t_exchange_ms = 0.0;
+            st->t_solve_ms = d(h.stamp[1], h.stamp[2]);
+            st->t_update_ms = d(h.stamp[2], h.stamp[3]);
+        }
     }
     if (aborted) *aborted = h.aborted;
     return BOS_OK;
@@ -433,6 +459,7 @@ int shard_phase0(bos_solver* s) {
     HIP_TRY(hipEventRecord(s->ev[0], s->stream));
     if ((rc = enqueue_linearize(s))) return rc;
     HIP_TRY(hipEventRecord(s->ev[1], s->stream));
+    HIP_TRY(bos::dev::launch_step_mark(nullptr, bos::dev::mf_epoch_ptr(s->mf), s->stream));   // this step's flow epoch
     if ((rc = enqueue_solver_inputs(s))) return rc;
     HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
     double* U = bos::dev::mf_update_ptr(s->mf);
@@ -462,13 +489,13 @@ int shard_phase1(bos_solver* s) {
 
 // phase 2: boundary solution in place, step status combined from every rank's headers, box-plus of
 // own + top + boundary nodes (skipped when any rank's factorization aborted)
-int shard_phase2(bos_solver* s, bool first) {
+int shard_phase2(bos_solver* s) {
     HIP_TRY(hipEventRecord(s->ev[5], s->stream));
     HIP_TRY(bos::dev::launch_index_copy(s->ex2_recv, s->ex2_usrc, s->d_rhs, s->ex2_udst, s->n_bnd_remote, s->stream));
     int32_t nrob_c = 0;
     const double chi_c = self_loop_chi(s, nrob_c);
     HIP_TRY(bos::dev::launch_shard_combine(s->ex1_recv, s->ex1_count, s->ex2_recv, s->ex2_count, s->world, chi_c, nrob_c,
-                                           first, s->d_status, s->stream));
+                                           s->d_status, s->stream));
     int rc;
     if ((rc = enqueue_update(s))) return rc;
     HIP_TRY(hipEventRecord(s->ev[6], s->stream));
@@ -482,12 +509,12 @@ int rccl_allgather(bos_solver* s, const double* send, double* recv, int64_t coun
 
 int finish_step(bos_solver* s, bos_step_stats* st);
 
-int do_step_sharded(bos_solver* s, bos_step_stats* st, bool first, bool sync) {
+int do_step_sharded(bos_solver* s, bos_step_stats* st, bool sync) {
     if (!s->comm) return fail(BOS_ERR_INVALID, "sharded handle without a communicator: drive bos_step_phase");
     int rc;
     if ((rc = shard_phase0(s)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
         (rc = shard_phase1(s)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)) ||
-        (rc = shard_phase2(s, first)))
+        (rc = shard_phase2(s)))
         return rc;
     s->have_dx = true;
     if (!sync) return BOS_OK;
@@ -513,22 +540,60 @@ int finish_step(bos_solver* s, bos_step_stats* st) {
     return BOS_OK;
 }
 
-// One GN iteration. first: the first of a bos_step_n batch (resets the sticky abort flag); sync:
-// the last one (reads the status back). A factorization whose dataflow launch timed out leaves the
-// state untouched (the box-plus kernel checks the solver word) and fails the call.
-int do_step(bos_solver* s, bos_step_stats* st, bool first, bool sync) {
-    if (s->sharded) return do_step_sharded(s, st, first, sync);
+// The device work of one GN iteration on one GPU: J+H (stamp 0 at its start), step mark (stamp 1,
+// the flows' epoch), solve, step mark (stamp 2), box-plus, status (stamp 3 at its end). No events
+// and no host synchronisation: the sequence is captured once into a hipGraph and replayed.
+int enqueue_step(bos_solver* s) {
     int rc;
-    HIP_TRY(hipEventRecord(s->ev[0], s->stream));
-    if ((rc = enqueue_linearize(s))) return rc;
-    HIP_TRY(hipEventRecord(s->ev[1], s->stream));
-    HIP_TRY(hipEventRecord(s->ev[2], s->stream));
+    unsigned long long* st = s->d_status->stamp;
+    if ((rc = enqueue_linearize(s, st))) return rc;
+    HIP_TRY(bos::dev::launch_step_mark(st + 1, uses_mf(s) ? bos::dev::mf_epoch_ptr(s->mf) : nullptr, s->stream));
     bool analysed_now = false;
     if ((rc = enqueue_solve(s, analysed_now))) return rc;
-    HIP_TRY(hipEventRecord(s->ev[3], s->stream));
+    HIP_TRY(bos::dev::launch_step_mark(st + 2, nullptr, s->stream));
     if ((rc = enqueue_update(s))) return rc;
-    if ((rc = enqueue_stats(s, true, first))) return rc;
-    HIP_TRY(hipEventRecord(s->ev[4], s->stream));
+    return enqueue_stats(s, true);
+}
+
+void drop_graph(bos_solver* s) {
+    if (s->graph_exec) (void)hipGraphExecDestroy(s->graph_exec);
+    if (s->graph) (void)hipGraphDestroy(s->graph);
+    s->graph_exec = nullptr;
+    s->graph = nullptr;
+}
+
+// Capture enqueue_step into s->graph_exec (multifrontal solvers: rocSOLVER's paths are not
+// captured). A stream that cannot be captured leaves graph_failed set and the step runs eagerly,
+// the same launches in the same order.
+int build_graph(bos_solver* s) {
+    drop_graph(s);
+    if (hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        s->graph_failed = true;
+        return BOS_OK;
+    }
+    const int rc = enqueue_step(s);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s->stream, &g);
+    if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    if (e != hipSuccess || !g) return fail(BOS_ERR_DEVICE, std::string("step graph capture: ") + hipGetErrorString(e));
+    s->graph = g;
+    HIP_TRY(hipGraphInstantiate(&s->graph_exec, g, nullptr, nullptr, 0));
+    return BOS_OK;
+}
+
+// One GN iteration. sync: read the status back (the last step of a bos_step_n batch). A
+// factorization whose dataflow launch timed out leaves the state untouched (the box-plus kernel
+// checks the solver word) and fails the call.
+int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
+    if (s->sharded) return do_step_sharded(s, st, sync);
+    int rc;
+    if (uses_mf(s) && !s->graph_exec && !s->graph_failed && (rc = build_graph(s))) return rc;
+    if (s->graph_exec) HIP_TRY(hipGraphLaunch(s->graph_exec, s->stream));
+    else if ((rc = enqueue_step(s))) return rc;
     s->have_dx = true;
     if (!sync) return BOS_OK;
     int32_t aborted = 0;
@@ -537,12 +602,6 @@ int do_step(bos_solver* s, bos_step_stats* st, bool first, bool sync) {
         s->have_dx = false;
         return fail(BOS_ERR_SOLVER, "sparse factorization aborted: a dataflow dependency wait timed out (state "
                                     "left unchanged by the failed iteration)");
-    }
-    if (st) {
-        st->t_linearize_ms = elapsed(s->ev[0], s->ev[1]);
-        st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
-        st->t_solve_ms = elapsed(s->ev[2], s->ev[3]);
-        st->t_update_ms = elapsed(s->ev[3], s->ev[4]);
     }
     return BOS_OK;
 }
@@ -583,6 +642,7 @@ int bos_destroy(bos_solver* s) {
     if (!s) return BOS_OK;
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    drop_graph(s);
     void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pl_cnt, s->lw_base, s->ll_cnt, s->ll_lm,
                     s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
@@ -828,6 +888,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     HIP_TRY(hipMemset(s->d_chi_part, 0, nt * sizeof(double)));
     HIP_TRY(hipMemset(s->d_nrob_part, 0, nt * sizeof(int32_t)));
     HIP_TRY(hipMemset(s->d_info, 0, sizeof(int32_t)));
+    HIP_TRY(hipMemset(s->d_status, 0, sizeof(bos::dev::StepStatus)));   // the abort flag is sticky
     {   // triangulation inputs (kept for bos_triangulate)
         std::vector<int32_t> tptr(NL + 1, 0), tobs(s->Mb), tpose(pb->bearing_pose, pb->bearing_pose + s->Mb);
         for (int k = 0; k < s->Mb; ++k) ++tptr[pb->bearing_landmark[k] + 1];
@@ -851,12 +912,14 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
 
 int bos_set_kernel_threshold(bos_solver* s, double kt) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    if (kt != s->kt) drop_graph(s);
     s->kt = kt;
     return BOS_OK;
 }
 
 int bos_set_damping_factor(bos_solver* s, double df) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    if (df != s->damping) drop_graph(s);
     s->damping = df;
     return BOS_OK;
 }
@@ -864,14 +927,14 @@ int bos_set_damping_factor(bos_solver* s, double df) {
 int bos_step(bos_solver* s, bos_step_stats* st) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
     HIP_TRY(hipSetDevice(s->device));
-    return do_step(s, st, true, true);
+    return do_step(s, st, true);
 }
 
 int bos_step_n(bos_solver* s, int n, bos_step_stats* last) {
     if (!s || n < 0) return fail(BOS_ERR_INVALID, "bad argument");
     HIP_TRY(hipSetDevice(s->device));
     for (int i = 0; i < n; ++i) {
-        int rc = do_step(s, last, i == 0, i + 1 == n);
+        int rc = do_step(s, last, i + 1 == n);
         if (rc) return rc;
     }
     return BOS_OK;
@@ -965,7 +1028,7 @@ int bos_step_phase(bos_solver* s, int32_t phase, bos_step_stats* st) {
     if (!s->sharded) return fail(BOS_ERR_INVALID, "bos_step_phase needs a sharded handle (world_size > 1)");
     if (phase != s->phase) return fail(BOS_ERR_INVALID, "bos_step_phase: phases run 0, 1, 2 in order");
     HIP_TRY(hipSetDevice(s->device));
-    int rc = phase == 0 ? shard_phase0(s) : phase == 1 ? shard_phase1(s) : shard_phase2(s, true);
+    int rc = phase == 0 ? shard_phase0(s) : phase == 1 ? shard_phase1(s) : shard_phase2(s);
     if (rc) { s->phase = 0; return rc; }
     s->phase = (phase + 1) % 3;
     if (phase < 2) return BOS_OK;
@@ -1018,6 +1081,13 @@ int bos_debug_inject_stall(bos_solver* s) {
     return BOS_OK;
 }
 
+int bos_debug_set_step_graph(bos_solver* s, int32_t enable) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    drop_graph(s);
+    s->graph_failed = !enable;
+    return BOS_OK;
+}
+
 int bos_triangulate(bos_solver* s) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
     HIP_TRY(hipSetDevice(s->device));
@@ -1052,6 +1122,7 @@ int bos_linearize(bos_solver* s, bos_step_stats* st) {
     if (st) {
         st->t_linearize_ms = elapsed(s->ev[0], s->ev[1]);
         st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);
+        st->t_solve_ms = st->t_update_ms = 0.0;
     }
     return BOS_OK;
 }

@@ -120,6 +120,42 @@ def test_step_n_equals_repeated_step(c1):
     assert np.array_equal(pa, pb) and np.array_equal(la, lb)
 
 
+def test_settings_changed_between_replayed_steps(c1):
+    """The one-GPU step is a captured graph with the kernel threshold and damping baked in:
+    set_kernel_threshold / set_damping_factor between steps must rebuild it (reference setters,
+    slam/solver.hpp:33-34, take effect at the next step())."""
+    Q = to_oracle(c1)
+    S = bos.Solver(c1)
+    po, lo = Q.copy_state()
+    for it in range(6):
+        kt, damping = (1.0, 0.01) if it < 2 else (1e-3, 0.5) if it < 4 else (1.0, 0.01)
+        if it in (2, 4):
+            S.set_kernel_threshold(kt)
+            S.set_damping_factor(damping)
+        st = S.step()
+        assert st["solver_info"] == 0
+        chi, _, _ = O.step(Q, po, lo, kernel_threshold=kt, damping=damping)
+        assert abs(st["chi2"] - chi) <= 1e-9 * max(1.0, chi)
+    pg, lg = S.get_state()
+    ok, ep, el = _close_state(pg, lg, po, lo)
+    assert ok, (ep, el)
+
+
+def test_step_phase_times_are_stamped(c1):
+    """Phase times come from realtime stamps written by the step's own kernels (no events inside
+    the captured step): all positive, and their sum within the host-measured wall time."""
+    import time
+    S = bos.Solver(c1)
+    S.step()
+    t0 = time.perf_counter()
+    st = S.step()
+    wall = (time.perf_counter() - t0) * 1e3
+    ph = [st["t_linearize_ms"], st["t_solve_ms"], st["t_update_ms"]]
+    assert all(p > 0 for p in ph), ph
+    assert sum(ph) <= wall, (ph, wall)
+    assert st["t_exchange_ms"] == 0.0
+
+
 def test_set_state_roundtrip(c1):
     S = bos.Solver(c1)
     p0, l0 = S.get_state()
