@@ -128,9 +128,11 @@ int bos_debug_set_step_graph(struct bos_solver* s, int32_t enable);
 
 /* Diagnostics: one J+H launch with per-wave timeline stamps, 8 x uint64 per wave: block, wave in
  * block, kind (0 pose lanes / 1 landmark lanes), t_start, t_loop, t_loop_end, t_end (realtime clock,
- * 100 MHz ticks), hw_id | xcc_id << 32. capacity in waves; *n_waves = waves of the launch. Not part
+ * 100 MHz ticks), hw_id | xcc_id << 32. capacity in waves; *n_waves = waves of the launch;
+ * flush_caches = 1: 1 GiB read before the launch (inputs from HBM, as in a GN step). Not part
  * of the drop-in boundary; the product launches never carry stamps. */
-int bos_debug_linearize_timeline(struct bos_solver* s, int64_t capacity, uint64_t* stamps, int64_t* n_waves);
+int bos_debug_linearize_timeline(struct bos_solver* s, int64_t capacity, uint64_t* stamps, int64_t* n_waves,
+                                 int32_t flush_caches);
 
 #ifdef __cplusplus
 }

@@ -131,7 +131,7 @@ def lib():
         "bos_triangulate": (ctypes.c_int, [vp]),
         "bos_triangulate_async": (ctypes.c_int, [vp]),
         "bos_debug_linearize_timeline": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64),
-                                                        ctypes.POINTER(ctypes.c_int64)]),
+                                                        ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]),
         "bos_system_info_get": (ctypes.c_int, [vp, ctypes.POINTER(bos_system_info)]),
         "bos_export_system": (ctypes.c_int, [vp, ctypes.c_int64, _ip, _ip, _dp, _dp]),
         "bos_get_state": (ctypes.c_int, [vp, _dp, _dp]),
@@ -475,14 +475,15 @@ class Solver:
     def linearize_async(self):
         _check(lib().bos_linearize_async(self._h), "bos_linearize_async")
 
-    def debug_timeline(self) -> np.ndarray:
+    def debug_timeline(self, flush_caches: bool = False) -> np.ndarray:
         """One J+H launch with per-wave stamps (diagnostics): rows of [block, wave, kind, t_start,
-        t_loop, t_loop_end, t_end, hw_id | xcc << 32], times in 100 MHz ticks."""
+        t_loop, t_loop_end, t_end, hw_id | xcc << 32], times in 100 MHz ticks; flush_caches: the
+        launch reads its inputs from HBM (1 GiB read before it)."""
         n = ctypes.c_int64(0)
-        _check(lib().bos_debug_linearize_timeline(self._h, 0, None, ctypes.byref(n)), "timeline")
+        _check(lib().bos_debug_linearize_timeline(self._h, 0, None, ctypes.byref(n), 0), "timeline")
         out = np.zeros((n.value, 8), dtype=np.uint64)
         _check(lib().bos_debug_linearize_timeline(self._h, n.value, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
-                                                  ctypes.byref(n)), "timeline")
+                                                  ctypes.byref(n), int(flush_caches)), "timeline")
         return out
 
     # ---- sharded (multi-GPU) step, external exchange: see include/bos.h

@@ -22,7 +22,8 @@ constexpr int32_t kIdxMask = 0x7fffffff;
 
 // J+H build (host/plan.hpp BlockLayout). Blocks [0, pose_blocks) run lane groups of lpp lanes, group
 // i for pose lane_pose[i] (-1: padding), the rest one lane per landmark lane (landmark ll_lm[g]).
-// Lane lists are wave-interleaved: item j of lane t of wave w is slot w_base[w] + 64 j + t.
+// Lane lists are wave-interleaved: item j of lane t of wave w is slot w_base[w] + w_stride[w] j + t
+// (plan.hpp LaneLists: groups of equal-length waves stored step-major).
 template <typename T> struct LinParams {
     // state caches (T precision): host-computed at create / set_state, then kept by the box-plus kernel
     const T* pc;          // [NP][4] x, y, cos(theta), sin(theta)
@@ -33,6 +34,7 @@ template <typename T> struct LinParams {
     int n_groups, n_lm_lanes, pose_blocks;
     // pose lanes
     const int32_t* pw_base;   // [waves + 1]
+    const int32_t* pw_stride; // [waves]
     const int32_t* pl_cnt;    // [NP * lpp]
     const int32_t* pb_idx;    // [slots] landmark (| kRunCont); the pose-landmark block of a slot is at off_pl + 6 slot
     const T* pb_z;            // [slots] measured bearing
@@ -47,6 +49,7 @@ template <typename T> struct LinParams {
     const T* o_om;            // [M_o][6] upper triangle (00, 01, 02, 11, 12, 22)
     // landmark lanes
     const int32_t* lw_base;   // [waves + 1]
+    const int32_t* lw_stride; // [waves]
     const int32_t* ll_cnt;    // [NL] per lane
     const int32_t* ll_lm;     // [NL] landmark of each lane (degree-sorted inside 256-lane windows)
     const int32_t* lb_idx;    // [slots] pose

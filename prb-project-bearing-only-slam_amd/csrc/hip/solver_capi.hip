@@ -86,7 +86,7 @@ struct bos_solver {
     void* d_pth = nullptr;
     void* d_lc = nullptr;
     // J+H work lists (host/plan.hpp BlockLayout)
-    int32_t *pw_base = nullptr, *pl_cnt = nullptr, *lw_base = nullptr, *ll_cnt = nullptr, *ll_lm = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_oth = nullptr, *po_blk = nullptr, *csr_src = nullptr,
+    int32_t *pw_base = nullptr, *pw_stride = nullptr, *pl_cnt = nullptr, *lw_base = nullptr, *lw_stride = nullptr, *ll_cnt = nullptr, *ll_lm = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_oth = nullptr, *po_blk = nullptr, *csr_src = nullptr,
             *elim_ref = nullptr;
     int32_t *pb_idx = nullptr, *lb_idx = nullptr;
     void *pb_z = nullptr, *pb_w = nullptr, *lb_z = nullptr, *lb_w = nullptr;
@@ -170,11 +170,11 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.n_groups = (int)P.blk.lane_pose.size();
     p.n_lm_lanes = (int)P.blk.lm_lane_lm.size();
     p.pose_blocks = s->pose_blocks;
-    p.pw_base = s->pw_base; p.pl_cnt = s->pl_cnt;
+    p.pw_base = s->pw_base; p.pw_stride = s->pw_stride; p.pl_cnt = s->pl_cnt;
     p.pb_idx = s->pb_idx; p.pb_z = (const T*)s->pb_z; p.pb_w = (const T*)s->pb_w;
     p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_oth = s->po_oth; p.po_blk = s->po_blk;
     p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
-    p.lw_base = s->lw_base; p.ll_cnt = s->ll_cnt; p.ll_lm = s->ll_lm;
+    p.lw_base = s->lw_base; p.lw_stride = s->lw_stride; p.ll_cnt = s->ll_cnt; p.ll_lm = s->ll_lm;
     p.lb_idx = s->lb_idx; p.lb_z = (const T*)s->lb_z; p.lb_w = (const T*)s->lb_w;
     p.hval = (T*)s->d_val;
     p.b = (T*)s->d_b;
@@ -606,6 +606,18 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     return BOS_OK;
 }
 
+// 1 GiB read (4x the Infinity Cache): L2 and the Infinity Cache hold none of the build's inputs
+int scrub_caches(bos_solver* s) {
+    constexpr int64_t kScrub = (int64_t)1 << 27;   // doubles
+    int rc;
+    if (!s->scrub) {
+        if ((rc = dalloc(&s->scrub, kScrub + 1))) return rc;
+        HIP_TRY(hipMemset(s->scrub, 0, (kScrub + 1) * sizeof(double)));
+    }
+    HIP_TRY(bos::dev::launch_cache_scrub(s->scrub, kScrub, s->scrub + kScrub, s->stream));
+    return BOS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -643,7 +655,7 @@ int bos_destroy(bos_solver* s) {
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     drop_graph(s);
-    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pl_cnt, s->lw_base, s->ll_cnt, s->ll_lm,
+    void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pw_stride, s->pl_cnt, s->lw_base, s->lw_stride, s->ll_cnt, s->ll_lm,
                     s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
@@ -798,8 +810,8 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             const bos::LaneLists& PLn = B.pose_lanes;
             for (size_t g = 0; g < PLn.cnt.size(); ++g)
                 for (int j = 0; j + 1 < PLn.cnt[g]; ++j) {
-                    const int64_t sl = PLn.w_base[g / 64] + 64 * (int64_t)j + (int64_t)(g & 63);
-                    if (pbi[sl] == pbi[sl + 64]) pbi[sl] |= bos::dev::kRunCont;
+                    const int64_t sl = PLn.slot((int)g, j), sn = PLn.slot((int)g, j + 1);
+                    if (pbi[sl] == pbi[sn]) pbi[sl] |= bos::dev::kRunCont;
                 }
         }
         std::vector<int32_t> po_oth(B.po_ent.size());
@@ -808,6 +820,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             po_oth[x] = (e & 1) ? pb->odom_src[e >> 1] : pb->odom_dst[e >> 1];
         }
         if ((rc = upload(&s->pw_base, B.pose_lanes.w_base)) || (rc = upload(&s->pl_cnt, B.pose_lanes.cnt)) ||
+            (rc = upload(&s->pw_stride, B.pose_lanes.w_stride)) || (rc = upload(&s->lw_stride, B.lm_lanes.w_stride)) ||
             (rc = upload(&s->lw_base, B.lm_lanes.w_base)) || (rc = upload(&s->ll_cnt, B.lm_lanes.cnt)) ||
             (rc = upload(&s->ll_lm, B.lm_lane_lm)) ||
             (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, B.po_ent)) ||
@@ -945,7 +958,7 @@ int bos_linearize_async(bos_solver* s) {
     return enqueue_linearize(s);
 }
 
-int bos_debug_linearize_timeline(bos_solver* s, int64_t capacity, uint64_t* stamps, int64_t* n_waves) {
+int bos_debug_linearize_timeline(bos_solver* s, int64_t capacity, uint64_t* stamps, int64_t* n_waves, int32_t flush_caches) {
     if (!s || !n_waves) return fail(BOS_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(s->device));
     const bos::Plan& P = s->plan;
@@ -957,6 +970,7 @@ int bos_debug_linearize_timeline(bos_solver* s, int64_t capacity, uint64_t* stam
     int rc = dalloc(&d, 8 * (size_t)waves);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(d, 0, 8 * (size_t)waves * sizeof(unsigned long long), s->stream));
+    if (flush_caches && (rc = scrub_caches(s))) { (void)hipFree(d); return rc; }
     hipError_t e;
     const int lpp = P.blk.lpp;
     if (s->precision == BOS_FP32) {
@@ -991,14 +1005,9 @@ int bos_time_linearize(bos_solver* s, int32_t n, int32_t flush_caches, double* m
     // cold: before every build, 1 GiB is read (4x the Infinity Cache) so the build's inputs come
     // from HBM, as inside a GN step where the solver streams its factor between two builds; each
     // build is timed alone
-    constexpr int64_t kScrub = (int64_t)1 << 27;   // doubles
-    if (!s->scrub) {
-        if ((rc = dalloc(&s->scrub, kScrub + 1))) return rc;
-        HIP_TRY(hipMemset(s->scrub, 0, (kScrub + 1) * sizeof(double)));
-    }
     double total = 0.0;
     for (int i = 0; i < n; ++i) {
-        HIP_TRY(bos::dev::launch_cache_scrub(s->scrub, kScrub, s->scrub + kScrub, s->stream));
+        if ((rc = scrub_caches(s))) return rc;
         HIP_TRY(hipEventRecord(s->ev[0], s->stream));
         if ((rc = enqueue_linearize(s))) return rc;
         HIP_TRY(hipEventRecord(s->ev[1], s->stream));

@@ -49,7 +49,7 @@ void jh_pose(bos_cpu_gn* c, int grp, double& chi) {
         const int n = B.pose_lanes.cnt[lane];
         double acc[6] = {0, 0, 0, 0, 0, 0};
         for (int j = 0; j < n; ++j) {
-            const int32_t sl = B.pose_lanes.w_base[lane / 64] + 64 * j + (lane & 63);
+            const int32_t sl = B.pose_lanes.slot(lane, j);
             const int k = B.pose_lanes.obs[sl];
             const int l = c->b_lm[k];
             double J[5];
@@ -65,7 +65,7 @@ void jh_pose(bos_cpu_gn* c, int grp, double& chi) {
             const double o[6] = {w0 * J[3], w0 * J[4], w1 * J[3], w1 * J[4], w2 * J[3], w2 * J[4]};
             for (int q = 0; q < 6; ++q) acc[q] += o[q];
             const bool last = j + 1 == n ||
-                              c->b_lm[B.pose_lanes.obs[B.pose_lanes.w_base[lane / 64] + 64 * (j + 1) + (lane & 63)]] != l;
+                              c->b_lm[B.pose_lanes.obs[B.pose_lanes.slot(lane, j + 1)]] != l;
             if (last) {
                 double* dst = hv + B.off_pl + 6 * (int64_t)sl;
                 for (int q = 0; q < 6; ++q) { dst[q] = acc[q]; acc[q] = 0.0; }
@@ -127,7 +127,7 @@ void jh_landmark(bos_cpu_gn* c, int lane) {
     const double lx = c->lm[2 * l], ly = c->lm[2 * l + 1];
     double h[3] = {0, 0, 0}, g[2] = {0, 0};
     for (int j = 0; j < B.lm_lanes.cnt[lane]; ++j) {
-        const int k = B.lm_lanes.obs[B.lm_lanes.w_base[lane / 64] + 64 * j + (lane & 63)];
+        const int k = B.lm_lanes.obs[B.lm_lanes.slot(lane, j)];
         const int p = c->b_pose[k];
         const double th = c->pose[3 * p + 2];
         double J[5];

@@ -580,13 +580,26 @@ void make_lane_lists(int lanes, const std::vector<int32_t>& lane_ptr, const std:
     }
     if (even)   // the J+H kernel walks pose lists in pairs and stores the second item of the last pair
         for (int w = 0; w < waves; ++w) L.w_len[w] += L.w_len[w] & 1;
-    for (int w = 0; w < waves; ++w) L.w_base[w + 1] = L.w_base[w] + 64 * L.w_len[w];
+    // groups of consecutive waves with equal list lengths, each stored step-major
+    L.w_stride.assign(waves, 64);
+    int64_t base = 0;
+    for (int w0 = 0; w0 < waves;) {
+        int w1 = w0 + 1;
+        while (w1 < waves && L.w_len[w1] == L.w_len[w0]) ++w1;
+        for (int w = w0; w < w1; ++w) {
+            L.w_base[w] = (int32_t)(base + 64 * (int64_t)(w - w0));
+            L.w_stride[w] = 64 * (w1 - w0);
+        }
+        base += 64 * (int64_t)(w1 - w0) * L.w_len[w0];
+        w0 = w1;
+    }
+    L.w_base[waves] = (int32_t)base;
     L.obs.assign(L.slots(), -1);
     for (int g = 0; g < lanes; ++g)
-        for (int j = 0; j < L.cnt[g]; ++j) L.obs[L.w_base[g / 64] + 64 * j + (g & 63)] = items[lane_ptr[g] + j];
+        for (int j = 0; j < L.cnt[g]; ++j) L.obs[L.slot(g, j)] = items[lane_ptr[g] + j];
 }
 
-inline int32_t lane_slot(const LaneLists& L, int g, int j) { return L.w_base[g / 64] + 64 * j + (g & 63); }
+inline int32_t lane_slot(const LaneLists& L, int g, int j) { return L.slot(g, j); }
 
 // Block layout of H and the J+H work split (see BlockLayout in plan.hpp).
 int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {

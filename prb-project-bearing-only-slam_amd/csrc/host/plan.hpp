@@ -42,15 +42,20 @@ struct ProblemIndex {
 // Work: lpp lanes per pose (lane g = pose * lpp + sub), one lane per landmark; lanes form waves of
 // 64. A lane walks a list of bearings (pose lanes: a segment of the pose's bearings sorted by
 // landmark, so duplicates of one pair are adjacent and merged by one lane; lane 0 of a pose also
-// walks its odometry entries). The lists are stored wave-interleaved (ELL per wave): item j of
-// lane t of wave w sits in slot w_base[w] + 64 j + t, so each step of a wave reads 64 consecutive
-// records and writes 64 consecutive blocks — whole cache lines, no re-fetch between steps.
+// walks its odometry entries). The lists are stored wave-interleaved: item j of lane t of wave w
+// sits in slot w_base[w] + w_stride[w] j + t, so each step of a wave reads 64 consecutive records
+// and writes 64 consecutive blocks (whole cache lines). Consecutive waves with the same list length
+// form a group stored step-major (w_stride = 64 x the group's waves): the waves of a group, which run
+// their steps side by side, then read and write one contiguous stretch per step (HBM page locality)
+// instead of one stretch per wave.
 struct LaneLists {
-    std::vector<int32_t> w_base;    // [waves + 1] first slot of each wave (64 * w_len slots)
+    std::vector<int32_t> w_base;    // [waves + 1] slot of item 0 of lane 0 of each wave; [waves] = slots
+    std::vector<int32_t> w_stride;  // [waves] slots between items j and j + 1 of a lane
     std::vector<int32_t> w_len;     // [waves] items per lane in the wave (max over its lanes)
     std::vector<int32_t> cnt;       // [lanes] items of each lane
     std::vector<int32_t> obs;       // [slots] bearing in each slot, -1 = padding
     int64_t slots() const { return w_base.empty() ? 0 : w_base.back(); }
+    int32_t slot(int g, int j) const { return w_base[g / 64] + w_stride[g / 64] * j + (g & 63); }
 };
 
 constexpr int kLmWindow = 256;   // landmark lanes are permuted only inside aligned windows of this size

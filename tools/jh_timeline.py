@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-wave timeline of the J+H kernel (config 3): where the waves of one launch spend their time.
-Diagnostics only (bos_debug_linearize_timeline). Usage: python tools/jh_timeline.py [fp32|fp64]"""
+Diagnostics only (bos_debug_linearize_timeline). Usage: python tools/jh_timeline.py [fp32|fp64] [cold]"""
 import os
 import sys
 
@@ -16,7 +16,9 @@ S = bos.Solver(P, precision=prec, device=0)
 for _ in range(30):
     S.linearize_async()
 S.synchronize()
-runs = [S.debug_timeline() for _ in range(5)]
+cold = len(sys.argv) > 2 and sys.argv[2] == "cold"
+runs = [S.debug_timeline(flush_caches=cold) for _ in range(5)]
+print("caches:", "cold (1 GiB read before each launch)" if cold else "warm (back to back)")
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 np.save(os.path.join(ROOT, "gpurun_out", f"timeline_{sys.argv[1] if len(sys.argv) > 1 else 'fp32'}.npy"), np.stack(runs))
 T = runs[-1].astype(np.int64)
