@@ -415,6 +415,7 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = U.nodes ? (t < U.n_nodes ? U.nodes[t] : -1) : t;
     double m = 0.0;
+    if (U.t_start && blockIdx.x == 0 && threadIdx.x == 0) *U.t_start = __builtin_amdgcn_s_memrealtime();
     if (U.info && (*U.info & kStepAbort)) {
         if (threadIdx.x == 0) U.max_part[blockIdx.x] = 0.0;
         return;
@@ -463,7 +464,7 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
 
 __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
                                     int32_t nrob_const, const double* max_part, int n_max, int32_t* info,
-                                    StepStatus* out) {
+                                    StepStatus* out, StepStatus* mirror) {
     __shared__ double sc[256];
     __shared__ double sm[256];
     __shared__ long long sr[256];
@@ -493,12 +494,8 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
         out->aborted |= inf & kStepAbort;
         if (info) *info = 0;
         out->stamp[3] = __builtin_amdgcn_s_memrealtime();
+        if (mirror) *mirror = *out;
     }
-}
-
-__global__ void step_mark_kernel(unsigned long long* stamp, uint32_t* epoch) {
-    if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
-    if (epoch) *epoch += 1u;
 }
 
 // triangulate_one_landmark (slam/triangulation.cpp:21-62): the rows [sin(th + z), -cos(th + z)],
@@ -648,7 +645,7 @@ __global__ void index_copy_kernel(const double* src, const int32_t* si, double* 
 }
 
 __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                     double chi_const, int32_t nrob_const, StepStatus* out) {
+                                     double chi_const, int32_t nrob_const, StepStatus* out, StepStatus* mirror) {
     if (threadIdx.x != 0) return;
     double chi = 0.0, m = 0.0;
     long long nr = 0, piv = 0;
@@ -667,6 +664,7 @@ __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const doub
     out->info = (int32_t)min(piv, (long long)(kStepAbort - 1)) | abort_bits;
     out->aborted |= abort_bits;
     out->stamp[3] = __builtin_amdgcn_s_memrealtime();
+    if (mirror) *mirror = *out;
 }
 
 __global__ __launch_bounds__(256) void cache_scrub_kernel(const double* buf, int64_t n, double* sink) {
@@ -681,7 +679,13 @@ template <typename T> __global__ void to_f64_kernel(const T* in, double* out, in
         out[i] = (double)in[i];
 }
 
-template <typename T> __global__ void gather_f64_kernel(const T* in, const int32_t* idx, double* out, int64_t n) {
+template <typename T>
+__global__ void gather_f64_kernel(const T* in, const int32_t* idx, double* out, int64_t n, unsigned long long* stamp,
+                                  uint32_t* epoch) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
+        if (epoch) *epoch += 1u;
+    }
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = (double)in[idx[i]];
 }
@@ -749,14 +753,9 @@ template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipSt
 
 hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
                                int32_t nrob_const, const double* max_part, int n_max, int32_t* info,
-                               StepStatus* out, hipStream_t s) {
+                               StepStatus* out, StepStatus* mirror, hipStream_t s) {
     hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n, chi_const, nrob_const,
-                       max_part, n_max, info, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_step_mark(unsigned long long* stamp, uint32_t* epoch, hipStream_t s) {
-    hipLaunchKernelGGL(step_mark_kernel, dim3(1), dim3(1), 0, s, stamp, epoch);
+                       max_part, n_max, info, out, mirror);
     return hipGetLastError();
 }
 
@@ -785,9 +784,10 @@ hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* 
 }
 
 hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                double chi_const, int32_t nrob_const, StepStatus* out, hipStream_t s) {
+                                double chi_const, int32_t nrob_const, StepStatus* out, StepStatus* mirror,
+                                hipStream_t s) {
     hipLaunchKernelGGL(shard_combine_kernel, dim3(1), dim3(64), 0, s, recv1, c1, recv2, c2, world, chi_const, nrob_const,
-                       out);
+                       out, mirror);
     return hipGetLastError();
 }
 
@@ -804,10 +804,11 @@ template <typename T> hipError_t launch_to_f64(const T* in, double* out, int64_t
 }
 
 template <typename T>
-hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL((gather_f64_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n);
+hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
+                             unsigned long long* stamp, uint32_t* epoch) {
+    if (n == 0 && !stamp && !epoch) return hipSuccess;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+    hipLaunchKernelGGL((gather_f64_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n, stamp, epoch);
     return hipGetLastError();
 }
 
@@ -828,8 +829,10 @@ template hipError_t launch_seg_copy<float>(float*, float*, float*, float*, const
 template hipError_t launch_triangulate<float>(const TriParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);
-template hipError_t launch_gather_f64<double>(const double*, const int32_t*, double*, int64_t, hipStream_t);
-template hipError_t launch_gather_f64<float>(const float*, const int32_t*, double*, int64_t, hipStream_t);
+template hipError_t launch_gather_f64<double>(const double*, const int32_t*, double*, int64_t, hipStream_t,
+                                              unsigned long long*, uint32_t*);
+template hipError_t launch_gather_f64<float>(const float*, const int32_t*, double*, int64_t, hipStream_t,
+                                             unsigned long long*, uint32_t*);
 
 }  // namespace dev
 }  // namespace bos

@@ -80,6 +80,7 @@ template <typename T> struct UpdateParams {
     const int32_t* info;      // solver status word or null; | kStepAbort => the update is skipped
     const int32_t* nodes;     // nodes to update (sharded: own, top, boundary), null = all NP + NL
     int n_nodes;
+    unsigned long long* t_start;   // phase timing: block 0 writes the realtime clock at its start, or null
 };
 
 // Solver status bit: the factorization's results are invalid (a dataflow launch timed out,
@@ -148,25 +149,28 @@ hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* 
 // terms, max |dx| the max, info: non-positive pivots summed, abort bits or-ed; `aborted` sticky
 // sticky), identical on every rank.
 hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                double chi_const, int32_t nrob_const, StepStatus* out, hipStream_t s);
+                                double chi_const, int32_t nrob_const, StepStatus* out, StepStatus* mirror,
+                                hipStream_t s);
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
 // Reduces the J+H kernel's chi^2 / robust-count partials (plus the constant terms of odometry
 // self-loops, chi_const / nrob_const) and the box-plus max |dx| partials (when max_part is set; a NaN
 // propagates) into *out, moves *info into out->info and zeroes *info for the next iteration: one
 // launch replaces the per-step memsets and read-backs. out->aborted is sticky; out->stamp[3] gets the
-// realtime clock at the end.
+// realtime clock at the end. The finished summary is also copied to *mirror (host-mapped memory the
+// host reads after synchronising: no copy launch per step), if set.
 hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
                                int32_t nrob_const, const double* max_part, int n_max, int32_t* info,
-                               StepStatus* out, hipStream_t s);
-// One thread: *stamp = realtime clock (if stamp), ++*epoch (if epoch: the multifrontal dataflow
-// launches' completion epoch, multifrontal.hpp mf_epoch_ptr). Graph-capturable phase marker.
-hipError_t launch_step_mark(unsigned long long* stamp, uint32_t* epoch, hipStream_t s);
+                               StepStatus* out, StepStatus* mirror, hipStream_t s);
 // Reads n doubles (all of them: the sum is compared with an impossible value), so L2 and the
 // Infinity Cache hold clean lines of this buffer afterwards (cold-cache timing, bos_time_linearize).
 hipError_t launch_cache_scrub(const double* buf, int64_t n, double* sink, hipStream_t s);
 template <typename T> hipError_t launch_to_f64(const T* in, double* out, int64_t n, hipStream_t s);
-// out[i] = (double)in[idx[i]]
-template <typename T> hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s);
+// out[i] = (double)in[idx[i]]. Block 0 also writes the realtime clock to *stamp and bumps *epoch (the
+// multifrontal flows' step epoch, multifrontal.hpp mf_epoch_ptr) when those are set: the right-hand
+// side gather opens the solve of a GN step, so the step needs no marker launches.
+template <typename T>
+hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
+                             unsigned long long* stamp = nullptr, uint32_t* epoch = nullptr);
 hipError_t launch_scatter_dense(const int32_t* rowptr, const int32_t* colind, const double* val, int n, double* dense,
                                 hipStream_t s);
 

@@ -826,10 +826,17 @@ __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
     backward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x, nullptr, nullptr);
 }
 
-// Backward substitution of the folded landmarks (k = 2), 16 lanes each (rows of the landmark's
-// two L columns across the lanes, coalesced): t = L21^T x_rows reduced over the 16 lanes, then
-// x1 = (y1 - t1) / L11, x0 = (y0 - t0 - L10 x1) / L00.
-constexpr int kFoldLanes = 16;
+// Backward substitution of the folded landmarks (k = 2), kFoldLanes lanes each (rows of the
+// landmark's two L columns across the lanes, coalesced): t = L21^T x_rows reduced over the lanes,
+// then x1 = (y1 - t1) / L11, x0 = (y0 - t0 - L10 x1) / L00. A lane takes up to four rows per pass
+// with every load of the pass issued at once (row indices and L values, then the x gathers), and
+// the landmark's own values are loaded before them: the launch is latency bound (few dependent
+// hops per landmark, 200k landmarks), so fewer lanes per landmark with more loads in flight each
+// beat one row per lane.
+#ifndef BOS_FOLD_LANES
+#define BOS_FOLD_LANES 4
+#endif
+constexpr int kFoldLanes = BOS_FOLD_LANES;
 __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const int g = (blockIdx.x * kMfBlock + threadIdx.x) / kFoldLanes;
     const int q0 = threadIdx.x % kFoldLanes;
@@ -838,22 +845,40 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const int r = valid ? a.r[s] : 0, m = 2 + r;
     const double* Ls = a.L + (valid ? a.L_off[s] : 0);
     const int32_t* fi = a.findex + (valid ? a.findex_off[s] : 0) + 2;
+    const int c0 = valid ? a.col0[s] : 0;
+    const bool head = valid && q0 == 0;
+    double y0 = 0.0, y1 = 0.0, L00 = 1.0, L10 = 0.0, L11 = 1.0;
+    if (head) { y0 = a.x[c0]; y1 = a.x[c0 + 1]; L00 = Ls[0]; L10 = Ls[1]; L11 = Ls[m + 1]; }
     double t0 = 0.0, t1 = 0.0;
-    for (int q = q0; q < r; q += kFoldLanes) {
-        const double xv = a.x[fi[q]];
-        t0 += Ls[2 + q] * xv;
-        t1 += Ls[m + 2 + q] * xv;
+    const int rl = r > 0 ? r - 1 : 0;   // reads of rows past r are clamped (and their products dropped)
+    for (int q = q0; q < r; q += 4 * kFoldLanes) {
+        int idx[4];
+        double la[4], lb[4], xv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int qq = min(q + u * kFoldLanes, rl);
+            idx[u] = fi[qq];
+            la[u] = Ls[2 + qq];
+            lb[u] = Ls[m + 2 + qq];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) xv[u] = a.x[idx[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool ok = q + u * kFoldLanes < r;
+            t0 += ok ? la[u] * xv[u] : 0.0;
+            t1 += ok ? lb[u] * xv[u] : 0.0;
+        }
     }
 #pragma unroll
     for (int o = kFoldLanes / 2; o > 0; o >>= 1) {
         t0 += __shfl_xor(t0, o, kFoldLanes);
         t1 += __shfl_xor(t1, o, kFoldLanes);
     }
-    if (valid && q0 == 0) {
-        const int c0 = a.col0[s];
-        const double x1 = (a.x[c0 + 1] - t1) / Ls[m + 1];
-        t0 += Ls[1] * x1;
-        a.x[c0] = (a.x[c0] - t0) / Ls[0];
+    if (head) {
+        const double x1 = (y1 - t1) / L11;
+        t0 += L10 * x1;
+        a.x[c0] = (y0 - t0) / L00;
         a.x[c0 + 1] = x1;
     }
 }

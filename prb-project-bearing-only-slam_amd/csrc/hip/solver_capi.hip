@@ -109,7 +109,9 @@ struct bos_solver {
     int32_t* d_info = nullptr;
     double* d_chi_part = nullptr;
     int32_t* d_nrob_part = nullptr;
-    bos::dev::StepStatus* d_status = nullptr;   // end-of-iteration summary (one read-back)
+    bos::dev::StepStatus* d_status = nullptr;   // end-of-iteration summary (device)
+    bos::dev::StepStatus* h_status = nullptr;   // its host-mapped mirror, written by the step's last kernel
+    bos::dev::StepStatus* m_status = nullptr;   // device address of h_status
     // sharded step (world > 1)
     bool sharded = false, external = false;
     int32_t* lane_pose = nullptr;            // J+H pose lane groups (Shard::lane_poses)
@@ -199,6 +201,7 @@ template <typename T> bos::dev::UpdateParams<T> upd_params(const bos_solver* s) 
     u.info = s->sharded ? &s->d_status->info : uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : nullptr;
     u.nodes = s->sharded ? s->upd_nodes : nullptr;
     u.n_nodes = s->n_upd;
+    u.t_start = nullptr;
     return u;
 }
 
@@ -304,7 +307,7 @@ int enqueue_stats(bos_solver* s, bool with_update) {
     else self_loop_terms<double>(s, chi_c, nrob_c);
     HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->chi_parts, chi_c, nrob_c,
                                           with_update ? s->d_maxpart : nullptr, nupd, info, s->d_status,
-                                          s->stream));
+                                          s->m_status, s->stream));
     return BOS_OK;
 }
 
@@ -320,12 +323,15 @@ const double* mf_matrix(const bos_solver* s) {
     return s->precision == BOS_FP32 ? s->d_val64 : (const double*)s->d_val;
 }
 
-// right-hand side in elimination order, and the fp64 copy of an fp32 block array
+// right-hand side in elimination order, and the fp64 copy of an fp32 block array. The gather also
+// stamps the solve's start and opens the step's flow epoch (the first solver launch of a GN step).
 int enqueue_solver_inputs(bos_solver* s) {
     const int64_t n = s->plan.n;
     const bool f32 = s->precision == BOS_FP32;
-    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream)
-                : bos::dev::launch_gather_f64<double>((const double*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream));
+    unsigned long long* stamp = s->d_status->stamp + 1;
+    uint32_t* epoch = uses_mf(s) ? bos::dev::mf_epoch_ptr(s->mf) : nullptr;
+    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch)
+                : bos::dev::launch_gather_f64<double>((const double*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch));
     if (f32 && uses_mf(s))
         HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.blk.size, s->stream));
     return BOS_OK;
@@ -369,8 +375,16 @@ int enqueue_solve(bos_solver* s, bool& ran_analysis) {
 }
 
 int enqueue_update(bos_solver* s) {
-    hipError_t e = s->precision == BOS_FP32 ? bos::dev::launch_boxplus<float>(upd_params<float>(s), s->stream)
-                                            : bos::dev::launch_boxplus<double>(upd_params<double>(s), s->stream);
+    hipError_t e;
+    if (s->precision == BOS_FP32) {
+        bos::dev::UpdateParams<float> u = upd_params<float>(s);
+        u.t_start = s->d_status->stamp + 2;
+        e = bos::dev::launch_boxplus<float>(u, s->stream);
+    } else {
+        bos::dev::UpdateParams<double> u = upd_params<double>(s);
+        u.t_start = s->d_status->stamp + 2;
+        e = bos::dev::launch_boxplus<double>(u, s->stream);
+    }
     if (e != hipSuccess) return fail(BOS_ERR_DEVICE, std::string("boxplus launch: ") + hipGetErrorString(e));
     return BOS_OK;
 }
@@ -426,9 +440,9 @@ int enqueue_triangulate(bos_solver* s) {
 // The step status (one copy). The sticky abort flag is cleared here once reported, so every
 // bos_step / bos_step_n batch starts with it clear.
 int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr) {
-    bos::dev::StepStatus h;
-    HIP_TRY(hipMemcpyAsync(&h, s->d_status, sizeof(h), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    bos::dev::StepStatus h;
+    std::memcpy(&h, (const void*)s->h_status, sizeof(h));   // written by the step's last kernel
     if (h.aborted) {
         HIP_TRY(hipMemsetAsync(&s->d_status->aborted, 0, sizeof(int32_t), s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
@@ -459,8 +473,7 @@ int shard_phase0(bos_solver* s) {
     HIP_TRY(hipEventRecord(s->ev[0], s->stream));
     if ((rc = enqueue_linearize(s))) return rc;
     HIP_TRY(hipEventRecord(s->ev[1], s->stream));
-    HIP_TRY(bos::dev::launch_step_mark(nullptr, bos::dev::mf_epoch_ptr(s->mf), s->stream));   // this step's flow epoch
-    if ((rc = enqueue_solver_inputs(s))) return rc;
+    if ((rc = enqueue_solver_inputs(s))) return rc;   // opens this step's flow epoch
     HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
     double* U = bos::dev::mf_update_ptr(s->mf);
     double* u = bos::dev::mf_uvec_ptr(s->mf);
@@ -495,7 +508,7 @@ int shard_phase2(bos_solver* s) {
     int32_t nrob_c = 0;
     const double chi_c = self_loop_chi(s, nrob_c);
     HIP_TRY(bos::dev::launch_shard_combine(s->ex1_recv, s->ex1_count, s->ex2_recv, s->ex2_count, s->world, chi_c, nrob_c,
-                                           s->d_status, s->stream));
+                                           s->d_status, s->m_status, s->stream));
     int rc;
     if ((rc = enqueue_update(s))) return rc;
     HIP_TRY(hipEventRecord(s->ev[6], s->stream));
@@ -540,17 +553,15 @@ int finish_step(bos_solver* s, bos_step_stats* st) {
     return BOS_OK;
 }
 
-// The device work of one GN iteration on one GPU: J+H (stamp 0 at its start), step mark (stamp 1,
-// the flows' epoch), solve, step mark (stamp 2), box-plus, status (stamp 3 at its end). No events
-// and no host synchronisation: the sequence is captured once into a hipGraph and replayed.
+// The device work of one GN iteration on one GPU: J+H (stamp 0 at its start), solve (its first
+// launch stamps 1 and opens the flows' epoch), box-plus (stamp 2), status (stamp 3 at its end, then
+// the host-mapped copy). No events, no marker launches, no host synchronisation: the sequence is
+// captured once into a hipGraph and replayed.
 int enqueue_step(bos_solver* s) {
     int rc;
-    unsigned long long* st = s->d_status->stamp;
-    if ((rc = enqueue_linearize(s, st))) return rc;
-    HIP_TRY(bos::dev::launch_step_mark(st + 1, uses_mf(s) ? bos::dev::mf_epoch_ptr(s->mf) : nullptr, s->stream));
+    if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
     bool analysed_now = false;
     if ((rc = enqueue_solve(s, analysed_now))) return rc;
-    HIP_TRY(bos::dev::launch_step_mark(st + 2, nullptr, s->stream));
     if ((rc = enqueue_update(s))) return rc;
     return enqueue_stats(s, true);
 }
@@ -665,6 +676,7 @@ int bos_destroy(bos_solver* s) {
                     s->ex1_unpack, s->ex2_bnd, s->ex2_usrc, s->ex2_udst, s->upd_nodes, s->abs_part};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    if (s->h_status) (void)hipHostFree(s->h_status);
     if (s->rf) rocsolver_destroy_rfinfo(s->rf);
     if (s->mf) bos::dev::mf_destroy(s->mf);
     if (s->rb) rocblas_destroy_handle(s->rb);
@@ -902,6 +914,10 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     HIP_TRY(hipMemset(s->d_nrob_part, 0, nt * sizeof(int32_t)));
     HIP_TRY(hipMemset(s->d_info, 0, sizeof(int32_t)));
     HIP_TRY(hipMemset(s->d_status, 0, sizeof(bos::dev::StepStatus)));   // the abort flag is sticky
+    if (hipHostMalloc((void**)&s->h_status, sizeof(bos::dev::StepStatus), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&s->m_status, s->h_status, 0) != hipSuccess)
+        return bail(fail(BOS_ERR_DEVICE, "host-mapped status allocation failed"));
+    std::memset(s->h_status, 0, sizeof(bos::dev::StepStatus));
     {   // triangulation inputs (kept for bos_triangulate)
         std::vector<int32_t> tptr(NL + 1, 0), tobs(s->Mb), tpose(pb->bearing_pose, pb->bearing_pose + s->Mb);
         for (int k = 0; k < s->Mb; ++k) ++tptr[pb->bearing_landmark[k] + 1];
