@@ -133,6 +133,35 @@ def cpu_gn_baseline(P, cpus, budget_s=8.0):
             "forms_it_per_s": forms, "host": cpus}
 
 
+FP64_PEAK_TFLOPS = 78.6    # MI355X fp64 (vector and matrix), spec
+HANDOFF_US = 1.5           # one cross-CU flag + payload hand-off under load (MI355X_MICROARCH.md,
+                           # handoff rows: 0.8-1.0 idle, 1.5-3 with streaming neighbours)
+
+
+def solver_model(P, phase, world):
+    """What bounds the sparse solve (solver.cpp:75-85 replaced by the multifrontal Cholesky):
+    its flops at the fp64 peak, its compulsory bytes at the achievable HBM rate, and the dependency
+    chain of the elimination tree (levels x two hand-offs, factor and backward) — the measured
+    t_solve_ms against each."""
+    if world != 1:
+        return None
+    info = bos.plan_inspect(P, solver=bos.BOS_SOLVER_SCHUR)
+    flops = float(info["mf_flops"])
+    nnz_l = float(info["nnz_factor"])
+    nnz_h = float(info["nnz_lower"])
+    levels = int(info["mf_levels"])
+    # L written once (factor) and read once (backward), H read once in fp64
+    byts = 8.0 * (2.0 * nnz_l + nnz_h)
+    t_solve_us = phase["t_solve_ms"] * 1e3
+    t_flops = flops / (FP64_PEAK_TFLOPS * 1e12) * 1e6
+    t_bytes = byts / (6.3e12) * 1e6
+    t_chain = levels * 2 * 2 * HANDOFF_US
+    return {"flops": flops, "nnz_factor": nnz_l, "tree_levels": levels, "supernodes": int(info["mf_supernodes"]),
+            "bytes": byts, "t_flops_us": t_flops, "t_bytes_us": t_bytes, "t_chain_us": t_chain,
+            "t_solve_us": t_solve_us, "bound": "dependency chain (latency)",
+            "frac_of_chain_bound": t_chain / t_solve_us, "frac_of_bytes_bound": t_bytes / t_solve_us}
+
+
 PROFILE_TAG = "r02"   # profiles/<tag>_pmc_linearize_<prec>.json, written by tools/pmc_summary.py
 
 
@@ -250,6 +279,10 @@ def main():
         return h.step_phase(2)
 
     def time_gn(solver_handle):
+        """GN iterations/s two ways: one synchronous bos_step per iteration (Solver::step() returns with
+        the state updated; the host round trip is inside every iteration), and bos_step_n batches
+        (the reference driver's loop of steps, executables/bearing_only_slam.cpp:95-98: every
+        iteration runs in full, the host synchronises once per batch)."""
         gn_step(solver_handle)   # first iteration includes the one-time factorization analysis
         barrier()
         tg = time.perf_counter()
@@ -259,17 +292,26 @@ def main():
         assert all(g["solver_info"] == 0 for g in stats), "non-positive pivot in a benchmarked GN step"
         ph = {k: float(np.median([g[k] for g in stats])) for k in
               ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
-        return args.gn_steps / gn_wall, ph
+        batched = None
+        if world == 1 or args.exchange == "rccl":
+            barrier()
+            tg = time.perf_counter()
+            last = solver_handle.step_n(args.gn_steps)
+            barrier()
+            batched = args.gn_steps / max_over_ranks(time.perf_counter() - tg)
+            assert last["solver_info"] == 0, "non-positive pivot in a benchmarked GN step"
+        return args.gn_steps / gn_wall, ph, batched
 
-    gn_it_s, phase, gn_other = None, None, None
+    gn_it_s, phase, gn_other, gn_batched = None, None, None, None
     if args.gn_steps > 0:
-        gn_it_s, phase = time_gn(S)
+        gn_it_s, phase, gn_batched = time_gn(S)
         if world == 1 and not args.no_gn_other:   # the other multifrontal ordering, for comparison
             other = "supernodal" if args.solver == "schur" else "schur"
             S2 = bos.Solver(P, precision=precision, device=local_rank,
                             solver=bos.BOS_SOLVER_SUPERNODAL if other == "supernodal" else bos.BOS_SOLVER_SCHUR)
-            it2, ph2 = time_gn(S2)
-            gn_other = {"solver": other, "gn_iters_per_s": it2, "t_solve_ms": ph2["t_solve_ms"]}
+            it2, ph2, b2 = time_gn(S2)
+            gn_other = {"solver": other, "gn_iters_per_s": it2, "gn_iters_per_s_batched": b2,
+                        "t_solve_ms": ph2["t_solve_ms"]}
             S2.close()
 
     # ---- landmark triangulation on the device (slam/triangulation.cpp:65-74), config 3 (run last:
@@ -320,7 +362,9 @@ def main():
                                 f"all-gathers; top fronts replicated: {info['top_fronts']})") if world > 1 else "single GPU",
             },
             "gn_iters_per_s": gn_it_s,
+            "gn_iters_per_s_batched": gn_batched,
             "gn_phase_ms": phase,
+            "solver_model": solver_model(P, phase, world) if phase else None,
             "gn_solver": args.solver,
             "gn_other": gn_other,
             "triangulation": tri,

@@ -125,6 +125,12 @@ int bos_debug_inject_stall(struct bos_solver* s);
 /* Test hook: run the one-GPU GN step as individual launches (enable = 0) instead of the captured
  * hipGraph replay (1, default). The same kernels in the same order either way. */
 int bos_debug_set_step_graph(struct bos_solver* s, int32_t enable);
+/* Diagnostics: one GN step (individual launches) whose multifrontal dataflow launches stamp every
+ * front they process: stamps[16 * nsuper] = factor stamps [nsuper][8] (start, folded, assembled,
+ * children ready, extend-added, factored, written, published), then backward stamps [nsuper][8]
+ * (start, staged, parent ready, solved, published; 0 = not in a flow launch); realtime clock,
+ * 100 MHz. meta[4 * nsuper] = tree level (-1 folded), k, r, folded children. */
+int bos_debug_solver_stamps(struct bos_solver* s, int64_t capacity, uint64_t* stamps, int32_t* meta);
 
 /* Diagnostics: one J+H launch with per-wave timeline stamps, 8 x uint64 per wave: block, wave in
  * block, kind (0 pose lanes / 1 landmark lanes), t_start, t_loop, t_loop_end, t_end (realtime clock,

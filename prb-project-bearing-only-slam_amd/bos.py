@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async", "bos_plan_shard_selftest",
     "bos_plan_node_owner", "bos_step_phase", "bos_exchange_size", "bos_exchange_download", "bos_exchange_upload",
     "bos_node_owner",
-    "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph",
+    "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph", "bos_debug_solver_stamps",
     "bos_time_linearize", "bos_time_triangulate", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
     "bos_cpu_gn_destroy",
 ]
@@ -164,6 +164,8 @@ def lib():
         "bos_debug_set_g2o_parser": (None, [ctypes.c_int32]),
         "bos_debug_inject_stall": (ctypes.c_int, [vp]),
         "bos_debug_set_step_graph": (ctypes.c_int, [vp, ctypes.c_int32]),
+        "bos_debug_solver_stamps": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64),
+                                                   ctypes.POINTER(ctypes.c_int32)]),
         "bos_time_linearize": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, _dp]),
         "bos_time_triangulate": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
         "bos_cpu_gn_create": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32,
@@ -518,6 +520,14 @@ class Solver:
         """Test hook: the next step's factor dataflow launch skips its first front (a stalled
         dependency); that step must fail with BOS_ERR_SOLVER and leave the state unchanged."""
         _check(lib().bos_debug_inject_stall(self._h), "bos_debug_inject_stall")
+
+    def debug_solver_stamps(self, nsuper: int):
+        """Diagnostics: one GN step with per-front stamps of the dataflow launches (bos_host.h)."""
+        st = np.zeros((2, nsuper, 8), dtype=np.uint64)
+        meta = np.zeros((nsuper, 4), dtype=np.int32)
+        _check(lib().bos_debug_solver_stamps(self._h, st.size, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                             meta.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "solver stamps")
+        return st, meta
 
     def debug_set_step_graph(self, enable: bool):
         """Test hook: GN steps as individual launches (False) or the captured graph (True, default)."""

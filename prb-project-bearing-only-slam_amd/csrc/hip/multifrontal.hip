@@ -104,6 +104,8 @@ struct MfArgs {
     const int32_t* fold_cptr;
     const int32_t* fold_chunk;
     const int32_t* fold_rec;
+    unsigned long long* stamps_f;   // diagnostics (mf_debug_set_stamps): factor / backward stamps, or null
+    unsigned long long* stamps_b;
 };
 
 // LDS of one wave's fold chunk: the y (forward-step) values of its landmarks, two per landmark
@@ -463,7 +465,13 @@ struct Flow {
                             // waits only for fronts of its own launch (the others finished earlier:
                             // per-level launches, the other program, or another rank's exchange)
     int id;
+    unsigned long long* stamps;   // diagnostics (bos_debug_solver_stamps): 8 realtime stamps per front, or null
 };
+
+// phase stamp k of front s (lane 0; the product launches pass no stamp buffer)
+__device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
+    if (stp && threadIdx.x == 0) stp[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 constexpr int kStall = kMfStall;               // or-ed into info when a dependency wait times out
 constexpr uint64_t kWaitTicks = 5000000;        // 50 ms of the 100 MHz realtime clock
@@ -591,6 +599,8 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     // the folded landmarks first (their W uses F's LDS): F and the u-vector accumulator wv start
     // from minus their contribution, the assembly then adds H
     const bool fold = nfold > 0;
+    unsigned long long* const stp = f ? f->stamps : a.stamps_f;
+    fstamp(stp, s, 0);
     if (fold) {
         FoldAcc<MAXM> facc;
         fold_children<MAXM>(a, s, F, fb, m, lane, facc);
@@ -601,12 +611,15 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         for (int i = lane; i < m; i += 64) wv[i] = 0.0;    // children's u-vectors accumulate here
     }
     wave_sync();
+    fstamp(stp, s, 1);
     assemble_wave(a, s, F, lane, fold);
     wave_sync();
+    fstamp(stp, s, 2);
     if constexpr (FLOW) {
         for (int ci = a.child_ptr[s]; ci < ce; ++ci)
             if (f->fid[a.child[ci]] == f->id) wait_done(*f, a.child[ci], a.info);
     }
+    fstamp(stp, s, 3);
     // extend-add, children in list order (deterministic)
     if (cb < ce) child_vals<COH>(lane, p0);
     if (cb + 1 < ce) child_vals<COH>(lane, p1);
@@ -630,6 +643,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = 0.0;
         }
     }
+    fstamp(stp, s, 4);
     double wi = live ? wv[lane] + xo : 0.0;   // forward elimination, fused into the pivot loop
     // Right-looking, with a rotating register window: before step j, row[t] holds column j + t of
     // this lane's row, so the pivot column is always row[0] and the update of column j + 1 + t is
@@ -733,6 +747,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         }
     }
     if (nbad && lane == 0) atomicAdd(a.info, nbad);
+    fstamp(stp, s, 5);
     // the update matrix: row[t] holds column k + t
 #pragma unroll
     for (int t0 = 0; t0 < MAXM; t0 += 8) {
@@ -774,11 +789,15 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
     double* xs = w + 2 * k;
     double* Lw = w + 2 * k + r;
     const int xi0 = lane < r ? fi[k + lane] : 0;   // where the first 64 rows' x live (static)
+    unsigned long long* const stp = f ? f->stamps : a.stamps_b;
+    fstamp(stp, s, 0);
     stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
     for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
+    fstamp(stp, s, 1);
     if constexpr (FLOW) {
         if (parent[s] >= 0 && f->fid[parent[s]] == f->id) wait_done(*f, parent[s], a.info);
     }
+    fstamp(stp, s, 2);
     if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
     for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     wave_sync();
@@ -799,6 +818,7 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         }
         if (own) stc<COH>(a.x + c0 + lane, xv);
         wave_sync();
+        fstamp(stp, s, 3);
         return;
     }
     // t_j = sum_i L[k + i, j] x[fi[k + i]]: fixed-order wave reduction per column
@@ -833,10 +853,7 @@ __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
 // the landmark's own values are loaded before them: the launch is latency bound (few dependent
 // hops per landmark, 200k landmarks), so fewer lanes per landmark with more loads in flight each
 // beat one row per lane.
-#ifndef BOS_FOLD_LANES
-#define BOS_FOLD_LANES 4
-#endif
-constexpr int kFoldLanes = BOS_FOLD_LANES;
+constexpr int kFoldLanes = 4;   // measured: 22 us at 4 lanes, 23 at 8, 34 at 16 (config 3)
 __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const int g = (blockIdx.x * kMfBlock + threadIdx.x) / kFoldLanes;
     const int q0 = threadIdx.x % kFoldLanes;
@@ -904,7 +921,9 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
         if (t >= f.n) break;
         const int s = f.order[t];
         factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, smap, wv, &fb, lane, &f);   // m <= kFlowMaxM
+        fstamp(f.stamps, s, 6);
         publish_done(f, s);
+        fstamp(f.stamps, s, 7);
     }
     leave_flow(f);
 }
@@ -925,6 +944,7 @@ __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flo
         const int s = f.order[t];
         backward_front<true>(a, s, w, threadIdx.x, &f, parent);
         publish_done(f, s);
+        fstamp(f.stamps, s, 4);
     }
     leave_flow(f);
 }
@@ -971,6 +991,17 @@ struct Prog {
     }
 };
 
+// Dataflow launch geometry (config 3, measured with tools/solver_stamps.py and variant builds): a
+// wave waiting on a dependency polls its flag, and waiting waves slow the ones working, so the flows
+// run few waves: 6 per CU for the factorization (solve 593 us at 6 against 599 at 8, 602 at 4, 682
+// at 12) and 4 per CU for the backward substitution (582 us at 4, 617 at 6, 636 at 8 with the
+// bottom split below, 706 at 16). The backward flow covers only the narrow top of the tree: levels
+// with at least kFlowWideLevel fronts (all independent, throughput bound) run as per-level launches
+// before it reaches them (config 3: levels 0-5, solve 659 -> 582 us; a factor flow started above
+// level 2 measured slower: 602 / 628 us at levels 3 / 4).
+constexpr int kFlowWavesFactor = 6;
+constexpr int kFlowWavesBackward = 4;
+constexpr int kFlowWideLevel = 256;
 struct MfDevice {
     int nlevels = 0, nsuper = 0, ncu = 256;
     // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
@@ -984,6 +1015,7 @@ struct MfDevice {
     uint32_t* done = nullptr;     // [2][nsuper]: factor, backward
     int* tickets = nullptr;       // [2 * kMfTickets]: work-queue tickets, then the launches' exit counters
     uint32_t* epoch = nullptr;    // device word, 1 at creation (done[] starts at 0), bumped per GN step
+    unsigned long long* stamps = nullptr;   // diagnostics: [2][nsuper][8] flow stamps (factor, backward), or null
     int32_t *fold_cnt = nullptr, *fold_cptr = nullptr, *fold_chunk = nullptr, *fold_rec = nullptr;
     int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
             *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
@@ -1001,6 +1033,8 @@ struct MfDevice {
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
         g.findex = findex; g.A = A; g.L = L; g.U = U; g.u = u; g.scratch = scratch; g.x = x; g.info = info;
         g.fold_cnt = fold_cnt; g.fold_cptr = fold_cptr; g.fold_chunk = fold_chunk; g.fold_rec = fold_rec;
+        g.stamps_f = stamps;
+        g.stamps_b = stamps ? stamps + 8 * (int64_t)nsuper : nullptr;
         return g;
     }
 };
@@ -1059,6 +1093,12 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
         if (mine(F.level[q])) { ofac.push_back(F.level[q]); fid_f[F.level[q]] = (int8_t)id; }
     P.n_flow_factor = (int)ofac.size();
     P.solve_lev0 = std::min(2, L);
+    auto mine_in_level = [&](int l) {
+        int c = 0;
+        for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) c += mine(F.level[q]);
+        return c;
+    };
+    while (P.solve_lev0 < L && mine_in_level(P.solve_lev0) >= kFlowWideLevel) ++P.solve_lev0;
     for (int q = F.level_ptr[P.solve_lev0]; q < F.level_ptr[L]; ++q) {
         const int s = F.level[q], k = F.k[s], m = k + F.r[s];
         if (!mine(s)) continue;
@@ -1212,8 +1252,8 @@ hipError_t mf_factor(MfDevice* d, int which, const double* A, double* x, hipStre
     }
     if (P.n_flow_factor > 0) {
         const Flow f{P.order_factor, P.n_flow_factor, d->tickets, d->tickets + kMfTickets, d->done, d->epoch, 0u,
-                     d->fid_f, P.id};
-        const int grid = std::min(P.n_flow_factor, d->ncu * 8);   // 2 waves per SIMD resident
+                     d->fid_f, P.id, d->stamps};
+        const int grid = std::min(P.n_flow_factor, d->ncu * kFlowWavesFactor);
         hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(P, 0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
@@ -1228,8 +1268,8 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
     if (P.ptr.empty()) return hipSuccess;
     if (P.flow_solve) {
         const Flow fb{P.order_bwd, P.n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1, d->done + d->nsuper,
-                      d->epoch, 0u, d->fid_b, P.id};
-        const int grid = std::min(P.n_flow_solve, d->ncu * 8);
+                      d->epoch, 0u, d->fid_b, P.id, d->stamps ? d->stamps + 8 * (int64_t)d->nsuper : nullptr};
+        const int grid = std::min(P.n_flow_solve, d->ncu * kFlowWavesBackward);
         hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), P.lds_bwd_flow, s, d->args(P, 0, 0, nullptr, x), fb,
                            (const int32_t*)d->parent);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1254,6 +1294,7 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
 
 int32_t* mf_info_ptr(const MfDevice* d) { return d->info; }
 uint32_t* mf_epoch_ptr(const MfDevice* d) { return d->epoch; }
+void mf_debug_set_stamps(MfDevice* d, unsigned long long* stamps) { d->stamps = stamps; }
 int32_t* mf_tickets_ptr(const MfDevice* d) { return d->tickets; }
 double* mf_update_ptr(const MfDevice* d) { return d->U; }
 double* mf_uvec_ptr(const MfDevice* d) { return d->u; }

@@ -35,6 +35,9 @@ int32_t* mf_info_ptr(const MfDevice* d);
 // kernel, kernels.hpp) once per GN step before the step's first mf_factor; all flows of one step
 // (factor and backward, both programs when sharded) share it
 uint32_t* mf_epoch_ptr(const MfDevice* d);
+// Diagnostics: the dataflow launches write 8 realtime stamps per front into stamps ([2][nsuper][8]:
+// factor, backward); null (the default) turns them off.
+void mf_debug_set_stamps(MfDevice* d, unsigned long long* stamps);
 constexpr int32_t kMfStall = 1 << 30;
 // work-queue tickets (kMfTickets ints, then kMfTickets exit counters); every flow launch leaves its
 // ticket zero (the last wave out resets it)

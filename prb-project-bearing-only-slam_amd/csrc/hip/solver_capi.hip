@@ -1106,6 +1106,40 @@ int bos_debug_inject_stall(bos_solver* s) {
     return BOS_OK;
 }
 
+int bos_debug_solver_stamps(bos_solver* s, int64_t capacity, uint64_t* stamps, int32_t* meta) {
+    if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    if (!uses_mf(s) || s->sharded) return fail(BOS_ERR_UNSUPPORTED, "one-GPU multifrontal handles only");
+    const bos::Multifrontal& F = s->plan.mf;
+    const int64_t need = 16 * (int64_t)F.nsuper;
+    if (!stamps || !meta || capacity < need) return fail(BOS_ERR_INVALID, "stamps: capacity 16 * supernodes");
+    HIP_TRY(hipSetDevice(s->device));
+    unsigned long long* d = nullptr;
+    int rc = dalloc(&d, (size_t)need);
+    if (rc) return rc;
+    HIP_TRY(hipMemset(d, 0, need * sizeof(unsigned long long)));
+    drop_graph(s);
+    const bool gf = s->graph_failed;
+    s->graph_failed = true;   // one eager step with the stamps
+    bos::dev::mf_debug_set_stamps(s->mf, d);
+    rc = do_step(s, nullptr, true);
+    bos::dev::mf_debug_set_stamps(s->mf, nullptr);
+    s->graph_failed = gf;
+    if (!rc && hipMemcpy(stamps, d, need * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(BOS_ERR_DEVICE, "stamps copy");
+    (void)hipFree(d);
+    if (rc) return rc;
+    std::vector<int32_t> lev(F.nsuper, -1);
+    for (int l = 0; l < F.nlevels; ++l)
+        for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) lev[F.level[q]] = l;
+    for (int x = 0; x < F.nsuper; ++x) {
+        meta[4 * x] = lev[x];
+        meta[4 * x + 1] = F.k[x];
+        meta[4 * x + 2] = F.r[x];
+        meta[4 * x + 3] = F.fold_cnt.empty() ? 0 : F.fold_cnt[x];
+    }
+    return BOS_OK;
+}
+
 int bos_debug_set_step_graph(bos_solver* s, int32_t enable) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
     drop_graph(s);
