@@ -258,7 +258,7 @@ def main():
     wall = max_over_ranks(time.perf_counter() - t0)
     ms_per_step = wall / args.steps * 1e3
     value = nobs * args.steps / wall
-    # ---- the same build from cold caches (1 GiB read before each): what it costs inside a GN
+    # ---- the same build from cold caches (512 MiB read before each): what it costs inside a GN
     # iteration, where the solver's factor streams between two builds
     cold_ms = S.time_linearize(args.cold_steps, flush_caches=True) if args.cold_steps > 0 else None
 
@@ -335,11 +335,17 @@ def main():
         algo = info["algorithmic_bytes"]
         traffic = traffic_from_profile(precision) if world == 1 else None
 
-        def roof(ms, label):
+        def roof(ms, label, timing):
             a = algo / (ms * 1e-3) / 1e9
             return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
-                    "traffic": traffic.get(label) if traffic else None, "algorithmic_bytes_per_launch": algo,
-                    "kernel_ms": ms, "caches": label}
+                    "traffic": traffic.get("warm" if label == "warm" else "cold") if traffic else None,
+                    "algorithmic_bytes_per_launch": algo, "kernel_ms": ms, "caches": label, "timing": timing}
+        instep = phase["t_linearize_ms"] if phase else None
+        r_instep = roof(instep, "in-step", "median over the timed GN steps of the device realtime clock from the "
+                        "J+H launch's start to the next launch's start (stamped by the step's kernels)") if instep else None
+        r_cold = roof(cold_ms, "cold", "HIP events around each build, 512 MiB read before it (event cost included)") \
+            if cold_ms else None
+        r_warm = roof(kernel_ms, "warm", "HIP events around the back-to-back builds")
         line = {
             "metric": METRIC,
             "value": value,
@@ -368,10 +374,12 @@ def main():
             "gn_solver": args.solver,
             "gn_other": gn_other,
             "triangulation": tri,
-            # in-step figure (inputs from HBM, as inside a GN iteration) first; the back-to-back
-            # replay (working set partly served by the Infinity Cache) second
-            "roofline": roof(cold_ms, "cold") if cold_ms else roof(kernel_ms, "warm"),
-            "roofline_warm_replay": roof(kernel_ms, "warm"),
+            # the J+H as it runs inside the GN iteration (inputs from HBM after the solver's stream)
+            # first; the same from cold caches by events, and the back-to-back replay (working set
+            # partly served by the Infinity Cache), beside it
+            "roofline": r_instep or r_cold or r_warm,
+            "roofline_cold_events": r_cold,
+            "roofline_warm_replay": r_warm,
         }
         if world == 1 and not args.no_cpu_baseline:
             cpus = host_cpus()

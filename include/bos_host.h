@@ -106,9 +106,9 @@ int bos_cpu_gn_get_state(const bos_cpu_gn* c, double* pose_xyt, double* landmark
 void bos_cpu_gn_destroy(bos_cpu_gn* c);
 
 /* Benchmark helpers (bench.py; HIP events on the handle's stream, no torch):
- * bos_time_linearize: n J+H builds (+ the exchange when sharded). flush_caches = 0: back to back,
- * the average per build; flush_caches = 1: 1 GiB is read before each build so its inputs come from
- * HBM (as inside a GN step), each build timed alone (J+H only).
+ * bos_time_linearize: n J+H builds. flush_caches = 0: back to back, the average per build;
+ * flush_caches = 1: 512 MiB (of two alternating buffers) are read before each build so its inputs
+ * come from HBM (as inside a GN step); each build timed alone by its own pair of events.
  * bos_time_triangulate: n device triangulations back to back (re-estimates the landmarks). */
 int bos_time_linearize(struct bos_solver* s, int32_t n, int32_t flush_caches, double* ms_per_build);
 int bos_time_triangulate(struct bos_solver* s, int32_t n, double* ms_per_call);
@@ -135,7 +135,7 @@ int bos_debug_solver_stamps(struct bos_solver* s, int64_t capacity, uint64_t* st
 /* Diagnostics: one J+H launch with per-wave timeline stamps, 8 x uint64 per wave: block, wave in
  * block, kind (0 pose lanes / 1 landmark lanes), t_start, t_loop, t_loop_end, t_end (realtime clock,
  * 100 MHz ticks), hw_id | xcc_id << 32. capacity in waves; *n_waves = waves of the launch;
- * flush_caches = 1: 1 GiB read before the launch (inputs from HBM, as in a GN step). Not part
+ * flush_caches = 1: 512 MiB read before the launch (inputs from HBM, as in a GN step). Not part
  * of the drop-in boundary; the product launches never carry stamps. */
 int bos_debug_linearize_timeline(struct bos_solver* s, int64_t capacity, uint64_t* stamps, int64_t* n_waves,
                                  int32_t flush_caches);

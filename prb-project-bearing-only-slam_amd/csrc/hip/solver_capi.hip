@@ -142,7 +142,8 @@ struct bos_solver {
     bool have_dx = false;
     // odometry self-loops: z[3] and Omega upper triangle [6] each (constant chi^2 terms)
     std::vector<double> loop_z, loop_om;
-    double* scrub = nullptr;   // bos_time_linearize(flush_caches): 1 GiB read between launches
+    double* scrub = nullptr;   // bos_time_linearize(flush_caches): 2 x 512 MiB, one read between launches
+    int scrub_turn = 0;
     // one-GPU multifrontal GN step captured once into a graph (every launch argument is fixed:
     // kernel threshold and damping are baked in, so setting them drops the graph)
     hipGraph_t graph = nullptr;
@@ -617,15 +618,18 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     return BOS_OK;
 }
 
-// 1 GiB read (4x the Infinity Cache): L2 and the Infinity Cache hold none of the build's inputs
+// 512 MiB read (2x the Infinity Cache) from one of two buffers, alternately: afterwards L2 and the
+// Infinity Cache hold none of the build's inputs, and no scrub finds the previous scrub's lines there
+// (so the time of a scrub does not depend on what ran before it)
 int scrub_caches(bos_solver* s) {
-    constexpr int64_t kScrub = (int64_t)1 << 27;   // doubles
+    constexpr int64_t kScrub = (int64_t)1 << 26;   // doubles per buffer
     int rc;
     if (!s->scrub) {
-        if ((rc = dalloc(&s->scrub, kScrub + 1))) return rc;
-        HIP_TRY(hipMemset(s->scrub, 0, (kScrub + 1) * sizeof(double)));
+        if ((rc = dalloc(&s->scrub, 2 * kScrub + 1))) return rc;
+        HIP_TRY(hipMemset(s->scrub, 0, (2 * kScrub + 1) * sizeof(double)));
     }
-    HIP_TRY(bos::dev::launch_cache_scrub(s->scrub, kScrub, s->scrub + kScrub, s->stream));
+    const double* buf = s->scrub + (s->scrub_turn++ & 1) * kScrub;
+    HIP_TRY(bos::dev::launch_cache_scrub(buf, kScrub, s->scrub + 2 * kScrub, s->stream));
     return BOS_OK;
 }
 
@@ -1018,9 +1022,9 @@ int bos_time_linearize(bos_solver* s, int32_t n, int32_t flush_caches, double* m
         *ms_per_build = elapsed(s->ev[0], s->ev[1]) / n;
         return BOS_OK;
     }
-    // cold: before every build, 1 GiB is read (4x the Infinity Cache) so the build's inputs come
-    // from HBM, as inside a GN step where the solver streams its factor between two builds; each
-    // build is timed alone
+    // cold: before every build, 512 MiB are read (scrub_caches) so the build's inputs come from HBM,
+    // as inside a GN step where the solver streams its factor between two builds; each build is
+    // bracketed by its own events (their cost included: conservative)
     double total = 0.0;
     for (int i = 0; i < n; ++i) {
         if ((rc = scrub_caches(s))) return rc;

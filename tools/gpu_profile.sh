@@ -1,6 +1,6 @@
 # Profile set for the committed numbers ($1 = tag, e.g. r02): for fp32 and fp64 J+H builds
 #   * three separate --pmc passes on the J+H kernel (read requests by size | writes | SQ), once on
-#     back-to-back builds (warm) and once on builds from cold caches (1 GiB read before each)
+#     back-to-back builds (warm) and once on builds from cold caches (512 MiB read before each)
 #   * rocprofv3 --kernel-trace --stats of the bench command (bench JSON + kernel stats), and of a
 #     cold-only bench run (its linearize_kernel average is the bench line's roofline.kernel_ms)
 # Results land in gpurun_out/prof_<tag>/; tools/collect_profiles.py copies the summaries.
