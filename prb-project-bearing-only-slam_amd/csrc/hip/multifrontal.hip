@@ -965,6 +965,13 @@ template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
 // front size classes: m <= 16, 32, 48, 64 (one wavefront, registers / LDS) and larger (workgroup)
 constexpr int kClasses = 5;
 inline int front_class(int m) { return m <= kMfWaveMaxM ? (m - 1) / 16 : 4; }
+// The launch a front goes to: fronts with 16 < m <= 32 run in the class-48 launch of their level (one
+// launch packs the level's waves better than two in a row on one stream: solve 589 -> 564 us on
+// config 3; moving the m <= 16 fronts too measured 570)
+inline int launch_class(int m) {
+    const int c = front_class(m);
+    return c == 1 ? 2 : c;
+}
 
 // The fronts one launch sequence processes: every front on one GPU; a rank's own subtrees or the
 // replicated top when sharded (plan.hpp Shard). Levels below flow_lev0 run per level (binned by
@@ -1054,7 +1061,7 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
             const int lc = l * kClasses + c;
             for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) {
                 const int s = F.level[q], k = F.k[s], m = k + F.r[s];
-                if (!mine(s) || front_class(m) != c) continue;
+                if (!mine(s) || launch_class(m) != c) continue;
                 lst.push_back(s);
                 if (c < 4) {
                     P.lds_fwd[lc] = std::max(P.lds_fwd[lc], (m + m * k) * 8);
