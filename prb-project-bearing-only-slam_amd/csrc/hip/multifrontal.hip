@@ -1001,14 +1001,16 @@ struct Prog {
 // Dataflow launch geometry (config 3, measured with tools/solver_stamps.py and variant builds): a
 // wave waiting on a dependency polls its flag, and waiting waves slow the ones working, so the flows
 // run few waves: 6 per CU for the factorization (solve 593 us at 6 against 599 at 8, 602 at 4, 682
-// at 12) and 4 per CU for the backward substitution (582 us at 4, 617 at 6, 636 at 8 with the
-// bottom split below, 706 at 16). The backward flow covers only the narrow top of the tree: levels
-// with at least kFlowWideLevel fronts (all independent, throughput bound) run as per-level launches
-// before it reaches them (config 3: levels 0-5, solve 659 -> 582 us; a factor flow started above
-// level 2 measured slower: 602 / 628 us at levels 3 / 4).
+// at 12) and 4 per CU for the backward substitution (582 us at 4, 617 at 6, 636 at 8, 706 at 16).
+// The flows take only the narrow top of the tree; wide levels (independent fronts, throughput
+// bound) run as per-level launches: the backward substitution of levels with >= kSolveWideLevel
+// fronts before the flow reaches them (config 3: levels 0-5, solve 659 -> 582 us), the
+// factorization of levels with >= kFactorWideLevel fronts before its flow starts (config 3: levels
+// 0-2, 564 -> 556 us; also level 3: 567).
 constexpr int kFlowWavesFactor = 6;
 constexpr int kFlowWavesBackward = 4;
-constexpr int kFlowWideLevel = 256;
+constexpr int kSolveWideLevel = 256;
+constexpr int kFactorWideLevel = 2048;
 struct MfDevice {
     int nlevels = 0, nsuper = 0, ncu = 256;
     // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
@@ -1085,8 +1087,13 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
             std::stable_sort(lst.begin() + P.ptr[lc], lst.end(), [&](int x, int y) { return cost(x) > cost(y); });
             P.ptr[lc + 1] = (int32_t)lst.size();
         }
-    // dataflow ranges: the lowest level from which every front of the program is <= kFlowMaxM
-    // (and >= 2) starts the factor flow; the solves run per level below 2
+    auto mine_in_level = [&](int l) {
+        int c = 0;
+        for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) c += mine(F.level[q]);
+        return c;
+    };
+    // dataflow ranges: the factor flow starts at the lowest level (>= 2) from which every front of
+    // the program is <= kFlowMaxM, and above the wide levels
     P.flow_lev0 = L;
     while (P.flow_lev0 > 2) {
         bool small = true;
@@ -1095,17 +1102,17 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
         if (!small) break;
         --P.flow_lev0;
     }
+    {
+        int wide = std::min(2, L);
+        while (wide < L && mine_in_level(wide) >= kFactorWideLevel) ++wide;
+        P.flow_lev0 = std::max(P.flow_lev0, wide);
+    }
     std::vector<int32_t> ofac, ofwd;
     for (int q = F.level_ptr[std::min(P.flow_lev0, L)]; q < F.level_ptr[L]; ++q)
         if (mine(F.level[q])) { ofac.push_back(F.level[q]); fid_f[F.level[q]] = (int8_t)id; }
     P.n_flow_factor = (int)ofac.size();
     P.solve_lev0 = std::min(2, L);
-    auto mine_in_level = [&](int l) {
-        int c = 0;
-        for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) c += mine(F.level[q]);
-        return c;
-    };
-    while (P.solve_lev0 < L && mine_in_level(P.solve_lev0) >= kFlowWideLevel) ++P.solve_lev0;
+    while (P.solve_lev0 < L && mine_in_level(P.solve_lev0) >= kSolveWideLevel) ++P.solve_lev0;
     for (int q = F.level_ptr[P.solve_lev0]; q < F.level_ptr[L]; ++q) {
         const int s = F.level[q], k = F.k[s], m = k + F.r[s];
         if (!mine(s)) continue;
