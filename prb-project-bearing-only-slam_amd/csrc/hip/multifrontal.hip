@@ -104,6 +104,8 @@ struct MfArgs {
     const int32_t* fold_cptr;
     const int32_t* fold_chunk;
     const int32_t* fold_rec;
+    const int16_t* emap;            // extend-add positions: entry e of child c's packed update matrix goes to
+    const int64_t* emap_off;        // packed position emap[emap_off[c] + e] of its parent's front (wave fronts)
     unsigned long long* stamps_f;   // diagnostics (mf_debug_set_stamps): factor / backward stamps, or null
     unsigned long long* stamps_b;
 };
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
 // One wavefront per front with m <= MAXM, the factorization in registers: lane i holds row i of
 // the (lower) front in a compile-time-indexed array; each column step broadcasts the pivot column
 // through a small LDS buffer (one store per lane, broadcast reads). LDS otherwise only stages the
-// assembly. F: packed front (MAXM (MAXM + 1) / 2), colbuf: 2 MAXM, smap: 64 ints.
+// assembly. F: packed front (MAXM (MAXM + 1) / 2), colbuf: 2 MAXM.
 __device__ __forceinline__ double readlane_d(double x, int l) {
     const long long b = __double_as_longlong(x);
     const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
@@ -514,14 +516,17 @@ __device__ __forceinline__ void publish_done(const Flow& f, int s) {
 }
 
 // A child's extend-add inputs: its r, row map entry (lane < rc) and where its update matrix and
-// u-vector live — static structure, loaded before the child has finished — then its values: the
-// u-vector entry and the first 256 entries of the packed update matrix (4 per lane).
+// u-vector live, and the parent-front positions of the first 256 entries of its packed update
+// matrix (4 per lane) — static structure, loaded before the child has finished — then its values:
+// the u-vector entry and those 256 entries.
 struct ChildPre {
     int rc, smap_v;
     double uval;
     double v[4];
+    int pos[4];
     const double* Uc;
     const double* uc;
+    const int16_t* ec;
 };
 
 __device__ __forceinline__ void child_meta(const MfArgs& a, int c, int lane, ChildPre& p) {
@@ -530,6 +535,10 @@ __device__ __forceinline__ void child_meta(const MfArgs& a, int c, int lane, Chi
     p.smap_v = lane < rc ? a.rmap[a.rmap_off[c] + lane] : 0;
     p.Uc = a.U + a.U_off[c];
     p.uc = a.u + a.u_off[c];
+    p.ec = a.emap + a.emap_off[c];
+    const int ne = rc * (rc + 1) / 2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p.pos[u] = 64 * u + lane < ne ? p.ec[64 * u + lane] : 0;
 }
 
 template <bool COH>
@@ -541,32 +550,26 @@ __device__ __forceinline__ void child_vals(int lane, ChildPre& p) {
     for (int u = 0; u < 4; ++u) p.v[u] = 64 * u + lane < ne ? ldc<COH>(p.Uc + 64 * u + lane) : 0.0;
 }
 
-// Extend-add of one child: its row map staged in LDS, its packed update matrix swept by all lanes
-// ((row, column) decoded incrementally). Positions of one child are distinct.
+// Extend-add of one child: every entry of its packed update matrix added at its precomputed position
+// in the parent's packed front (positions of one child are distinct), then its u-vector.
 template <bool COH>
-__device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p, double* F, double* wv, int* smap,
-                                             int m, int lane) {
+__device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p, double* F, double* wv, int m, int lane) {
     const int rc = p.rc;
-    if (lane < rc) smap[lane] = p.smap_v;
-    wave_sync();
     const int ne = rc * (rc + 1) / 2;
-    int j = 0, len = rc, o = lane;
-    while (len > 0 && o >= len) { o -= len; ++j; --len; }
     for (int e0 = 0; e0 < ne; e0 += 256) {
         double v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            v[u] = e0 == 0 ? p.v[u] : (e0 + 64 * u + lane < ne ? ldc<COH>(p.Uc + e0 + 64 * u + lane) : 0.0);
+        int pos[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if (len > 0) {
-                F[pk32(smap[j + o], smap[j], m)] += v[u];
-                o += 64;
-                while (len > 0 && o >= len) { o -= len; ++j; --len; }
-            }
+            const int e = e0 + 64 * u + lane;
+            v[u] = e0 == 0 ? p.v[u] : (e < ne ? ldc<COH>(p.Uc + e) : 0.0);
+            pos[u] = e0 == 0 ? p.pos[u] : (e < ne ? p.ec[e] : 0);
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (e0 + 64 * u + lane < ne) F[pos[u]] += v[u];
     }
-    if (lane < rc) wv[smap[lane]] += p.uval;
+    if (lane < rc) wv[p.smap_v] += p.uval;
     wave_sync();
 }
 
@@ -576,7 +579,7 @@ __device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p,
 // registers): y_j = w_j / L_jj, w_i -= L_ij y_j. y goes to x, the remaining w (rows >= k) to the
 // front's u-vector for its parent.
 template <int MAXM, bool FLOW>
-__device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf, int* smap,
+__device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf,
                                                  double* wv, FoldBuf* fb, int lane, const Flow* f) {
     constexpr bool COH = FLOW;
     const int k = a.k[s], r = a.r[s], m = k + r;
@@ -623,13 +626,13 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     // extend-add, children in list order (deterministic)
     if (cb < ce) child_vals<COH>(lane, p0);
     if (cb + 1 < ce) child_vals<COH>(lane, p1);
-    if (cb < ce) extend_child<COH>(a, p0, F, wv, smap, m, lane);
-    if (cb + 1 < ce) extend_child<COH>(a, p1, F, wv, smap, m, lane);
+    if (cb < ce) extend_child<COH>(a, p0, F, wv, m, lane);
+    if (cb + 1 < ce) extend_child<COH>(a, p1, F, wv, m, lane);
     for (int ci = cb + 2; ci < ce; ++ci) {
         ChildPre pq;
         child_meta(a, a.child[ci], lane, pq);
         child_vals<COH>(lane, pq);
-        extend_child<COH>(a, pq, F, wv, smap, m, lane);
+        extend_child<COH>(a, pq, F, wv, m, lane);
     }
     const bool live = lane < m;
     double row[MAXM];
@@ -769,9 +772,8 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * MAXM];
     __shared__ __attribute__((aligned(16))) double wv[MAXM];
-    __shared__ int smap[64];
     __shared__ FoldBuf fb;
-    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, smap, wv, &fb, threadIdx.x, nullptr);
+    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, wv, &fb, threadIdx.x, nullptr);
 }
 
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
@@ -911,7 +913,6 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
     __shared__ __attribute__((aligned(16))) double F[kFlowMaxM * (kFlowMaxM + 1) / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * kFlowMaxM];
     __shared__ __attribute__((aligned(16))) double wv[kFlowMaxM];
-    __shared__ int smap[64];
     __shared__ FoldBuf fb;
     const int lane = threadIdx.x;
     // a wave takes at most n + 1 tickets: the loop is bounded (an unbounded for (;;) version of
@@ -920,7 +921,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
         const int t = next_ticket(f.ticket);
         if (t >= f.n) break;
         const int s = f.order[t];
-        factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, smap, wv, &fb, lane, &f);   // m <= kFlowMaxM
+        factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, wv, &fb, lane, &f);   // m <= kFlowMaxM
         fstamp(f.stamps, s, 6);
         publish_done(f, s);
         fstamp(f.stamps, s, 7);
@@ -1026,6 +1027,8 @@ struct MfDevice {
     uint32_t* epoch = nullptr;    // device word, 1 at creation (done[] starts at 0), bumped per GN step
     unsigned long long* stamps = nullptr;   // diagnostics: [2][nsuper][8] flow stamps (factor, backward), or null
     int32_t *fold_cnt = nullptr, *fold_cptr = nullptr, *fold_chunk = nullptr, *fold_rec = nullptr;
+    int16_t* emap = nullptr;
+    int64_t* emap_off = nullptr;
     int32_t *col0 = nullptr, *k = nullptr, *r = nullptr, *child_ptr = nullptr, *child = nullptr,
             *rmap = nullptr, *amap_ptr = nullptr, *amap_src = nullptr, *amap_dst = nullptr, *findex = nullptr,
             *info = nullptr;
@@ -1042,6 +1045,7 @@ struct MfDevice {
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
         g.findex = findex; g.A = A; g.L = L; g.U = U; g.u = u; g.scratch = scratch; g.x = x; g.info = info;
         g.fold_cnt = fold_cnt; g.fold_cptr = fold_cptr; g.fold_chunk = fold_chunk; g.fold_rec = fold_rec;
+        g.emap = emap; g.emap_off = emap_off;
         g.stamps_f = stamps;
         g.stamps_b = stamps ? stamps + 8 * (int64_t)nsuper : nullptr;
         return g;
@@ -1185,6 +1189,29 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
             return -2;
         }
     }
+    {   // extend-add positions of every child whose parent is a wave front (m <= kMfWaveMaxM)
+        std::vector<int64_t> eoff(F.nsuper, 0);
+        std::vector<int16_t> em;
+        for (int c = 0; c < F.nsuper; ++c) {
+            const int p = F.parent[c];
+            if (p < 0) continue;
+            const int mp = F.k[p] + F.r[p], rc = F.r[c];
+            if (mp > kMfWaveMaxM || rc == 0) continue;
+            bool folded = false;
+            for (int ci = F.child_ptr[p]; ci < F.child_ptr[p] + (F.fold_cnt.empty() ? 0 : F.fold_cnt[p]); ++ci)
+                folded = folded || F.child[ci] == c;
+            if (folded) continue;
+            eoff[c] = (int64_t)em.size();
+            const int32_t* rm = F.rmap.data() + F.rmap_off[c];
+            for (int j = 0; j < rc; ++j)
+                for (int i = j; i < rc; ++i) {
+                    const int I = rm[i], J = rm[j];
+                    if (I < J || I >= mp) { err = "multifrontal: child row map not increasing"; return -1; }
+                    em.push_back((int16_t)(J * mp - J * (J - 1) / 2 + (I - J)));
+                }
+        }
+        if ((rc = up(&d->emap, em, err)) || (rc = up(&d->emap_off, eoff, err))) return rc;
+    }
     if ((rc = up(&d->col0, F.col0, err)) || (rc = up(&d->k, F.k, err)) ||
         (rc = up(&d->r, F.r, err)) || (rc = up(&d->child_ptr, F.child_ptr, err)) || (rc = up(&d->child, F.child, err)) ||
         (rc = up(&d->rmap, F.rmap, err)) || (rc = up(&d->amap_ptr, F.amap_ptr, err)) ||
@@ -1218,7 +1245,7 @@ void mf_destroy(MfDevice* d) {
     if (!d) return;
     free_prog(d->prog[0]);
     free_prog(d->prog[1]);
-    void* bufs[] = {d->epoch, d->fid_f, d->fid_b, d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->parent, d->done,
+    void* bufs[] = {d->emap, d->emap_off, d->epoch, d->fid_f, d->fid_b, d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->parent, d->done,
                     d->tickets, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch};

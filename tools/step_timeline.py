@@ -13,7 +13,8 @@ busy = 0.0
 for x in r[a + 1:b + 1]:
     s, e = int(x["Start_Timestamp"]), int(x["End_Timestamp"])
     busy += (e - s) / 1e3
-    name = x["Kernel_Name"].split("(")[0].replace("bos::dev::(anonymous namespace)::", "").replace("void ", "")
+    name = x["Kernel_Name"].replace("bos::dev::(anonymous namespace)::", "").replace("void ", "")
+    name = name[:name.index("(")] if "(" in name else name
     print(f"{(s - t0) / 1e3:8.1f} {(e - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {name[:60]:60s} grid {x['Grid_Size_X']:>8s} "
           f"vgpr {x['VGPR_Count']:>3s} agpr {x.get('Accum_VGPR_Count', ''):>3s} lds {x['LDS_Block_Size']:>6s} stream {x['Stream_Id']}")
 print(f"step span {(int(r[b]['End_Timestamp']) - t0) / 1e3:.1f} us (from the previous step's end), kernel busy {busy:.1f} us")
