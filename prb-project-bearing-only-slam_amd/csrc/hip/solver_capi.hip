@@ -148,6 +148,8 @@ struct bos_solver {
     // kernel threshold and damping are baked in, so setting them drops the graph)
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
+    hipGraph_t pgraph[3] = {};          // sharded step: one graph per phase
+    hipGraphExec_t pexec[3] = {};
     bool graph_failed = false;   // capture not possible on this stream (e.g. the legacy null stream)
 };
 
@@ -466,55 +468,60 @@ int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr) {
     return BOS_OK;
 }
 
-// ---- sharded GN iteration in three phases (exchanges between them)
+// ---- sharded GN iteration in three phases (exchanges between them). Each phase's launches are
+// captured once into a graph (like the one-GPU step) and replayed; the exchanges run between the
+// graphs (RCCL on the handle's stream, or the caller's buffer moves in external mode).
 // phase 0: J+H (own + top lanes), solver inputs, own subtrees factored (and forward-solved),
 // exchange-1 buffer packed (roots' U / u, this rank's chi^2 partials)
-int shard_phase0(bos_solver* s) {
-    int rc;
-    HIP_TRY(hipEventRecord(s->ev[0], s->stream));
-    if ((rc = enqueue_linearize(s))) return rc;
-    HIP_TRY(hipEventRecord(s->ev[1], s->stream));
-    if ((rc = enqueue_solver_inputs(s))) return rc;   // opens this step's flow epoch
-    HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
-    double* U = bos::dev::mf_update_ptr(s->mf);
-    double* u = bos::dev::mf_uvec_ptr(s->mf);
-    HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_pack, s->n1p, s->maxlen1p, s->stream));
-    HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream));
-    HIP_TRY(hipEventRecord(s->ev[2], s->stream));
-    return BOS_OK;
-}
-
 // phase 1: the other ranks' roots in place, the top factored and solved, own subtrees solved
 // backward, exchange-2 buffer packed (max |x| of own + top, solver word, boundary solution)
-int shard_phase1(bos_solver* s) {
-    HIP_TRY(hipEventRecord(s->ev[3], s->stream));
+// phase 2: boundary solution in place, step status combined from every rank's headers, box-plus of
+// own + top + boundary nodes (skipped when any rank's factorization aborted)
+int shard_enqueue(bos_solver* s, int phase) {
+    int rc;
     double* U = bos::dev::mf_update_ptr(s->mf);
     double* u = bos::dev::mf_uvec_ptr(s->mf);
-    HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_unpack, s->n1u, s->maxlen1u, s->stream));
-    HIP_TRY(bos::dev::mf_factor(s->mf, 1, mf_matrix(s), s->d_rhs, s->stream));
-    HIP_TRY(bos::dev::mf_solve(s->mf, 1, s->d_rhs, s->stream));
-    HIP_TRY(bos::dev::mf_solve(s->mf, 0, s->d_rhs, s->stream));
-    HIP_TRY(bos::dev::launch_shard_pack2(s->d_rhs, s->upd_nodes, s->n_upd_local, s->node_dof, s->NP,
-                                         bos::dev::mf_info_ptr(s->mf), s->ex2_bnd, s->n_bnd, s->abs_part, s->ex2_send,
-                                         s->stream));
-    HIP_TRY(hipEventRecord(s->ev[4], s->stream));
+    if (phase == 0) {
+        if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
+        if ((rc = enqueue_solver_inputs(s))) return rc;   // opens this step's flow epoch
+        HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
+        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_pack, s->n1p, s->maxlen1p, s->stream));
+        HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream));
+    } else if (phase == 1) {
+        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_unpack, s->n1u, s->maxlen1u, s->stream));
+        HIP_TRY(bos::dev::mf_factor(s->mf, 1, mf_matrix(s), s->d_rhs, s->stream));
+        HIP_TRY(bos::dev::mf_solve(s->mf, 1, s->d_rhs, s->stream));
+        HIP_TRY(bos::dev::mf_solve(s->mf, 0, s->d_rhs, s->stream));
+        HIP_TRY(bos::dev::launch_shard_pack2(s->d_rhs, s->upd_nodes, s->n_upd_local, s->node_dof, s->NP,
+                                             bos::dev::mf_info_ptr(s->mf), s->ex2_bnd, s->n_bnd, s->abs_part, s->ex2_send,
+                                             s->stream));
+    } else {
+        HIP_TRY(bos::dev::launch_index_copy(s->ex2_recv, s->ex2_usrc, s->d_rhs, s->ex2_udst, s->n_bnd_remote, s->stream));
+        int32_t nrob_c = 0;
+        const double chi_c = self_loop_chi(s, nrob_c);
+        HIP_TRY(bos::dev::launch_shard_combine(s->ex1_recv, s->ex1_count, s->ex2_recv, s->ex2_count, s->world, chi_c,
+                                               nrob_c, s->d_status, s->m_status, s->stream));
+        if ((rc = enqueue_update(s))) return rc;
+    }
     return BOS_OK;
 }
 
-// phase 2: boundary solution in place, step status combined from every rank's headers, box-plus of
-// own + top + boundary nodes (skipped when any rank's factorization aborted)
-int shard_phase2(bos_solver* s) {
-    HIP_TRY(hipEventRecord(s->ev[5], s->stream));
-    HIP_TRY(bos::dev::launch_index_copy(s->ex2_recv, s->ex2_usrc, s->d_rhs, s->ex2_udst, s->n_bnd_remote, s->stream));
-    int32_t nrob_c = 0;
-    const double chi_c = self_loop_chi(s, nrob_c);
-    HIP_TRY(bos::dev::launch_shard_combine(s->ex1_recv, s->ex1_count, s->ex2_recv, s->ex2_count, s->world, chi_c, nrob_c,
-                                           s->d_status, s->m_status, s->stream));
+int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec);
+
+// one phase: its graph (captured on first use), bracketed by the phase events
+int shard_phase(bos_solver* s, int phase) {
+    static const int evb[3] = {0, 3, 5}, eve[3] = {2, 4, 6};
     int rc;
-    if ((rc = enqueue_update(s))) return rc;
-    HIP_TRY(hipEventRecord(s->ev[6], s->stream));
+    HIP_TRY(hipEventRecord(s->ev[evb[phase]], s->stream));
+    if (!s->pexec[phase] && !s->graph_failed && (rc = capture(s, phase, &s->pgraph[phase], &s->pexec[phase]))) return rc;
+    if (s->pexec[phase]) HIP_TRY(hipGraphLaunch(s->pexec[phase], s->stream));
+    else if ((rc = shard_enqueue(s, phase))) return rc;
+    HIP_TRY(hipEventRecord(s->ev[eve[phase]], s->stream));
     return BOS_OK;
 }
+int shard_phase0(bos_solver* s) { return shard_phase(s, 0); }
+int shard_phase1(bos_solver* s) { return shard_phase(s, 1); }
+int shard_phase2(bos_solver* s) { return shard_phase(s, 2); }
 
 int rccl_allgather(bos_solver* s, const double* send, double* recv, int64_t count) {
     NC_TRY(ncclAllGather(send, recv, (size_t)count, ncclDouble, s->comm, s->stream));
@@ -545,10 +552,12 @@ int finish_step(bos_solver* s, bos_step_stats* st) {
         return fail(BOS_ERR_SOLVER, "sparse factorization aborted: a dataflow dependency wait timed out (state "
                                     "left unchanged by the failed iteration)");
     }
-    if (st && s->sharded) {
-        st->t_linearize_ms = elapsed(s->ev[0], s->ev[1]);
+    if (st && s->sharded) {   // J+H from the device stamps, the rest from the phase events
+        bos::dev::StepStatus h;
+        std::memcpy(&h, (const void*)s->h_status, sizeof(h));
+        st->t_linearize_ms = h.stamp[1] > h.stamp[0] ? (double)(h.stamp[1] - h.stamp[0]) * bos::dev::kStampMs : 0.0;
         st->t_exchange_ms = elapsed(s->ev[2], s->ev[3]) + elapsed(s->ev[4], s->ev[5]);
-        st->t_solve_ms = elapsed(s->ev[1], s->ev[2]) + elapsed(s->ev[3], s->ev[4]);
+        st->t_solve_ms = std::max(0.0, elapsed(s->ev[0], s->ev[2]) - st->t_linearize_ms) + elapsed(s->ev[3], s->ev[4]);
         st->t_update_ms = elapsed(s->ev[5], s->ev[6]);
     }
     return BOS_OK;
@@ -572,19 +581,25 @@ void drop_graph(bos_solver* s) {
     if (s->graph) (void)hipGraphDestroy(s->graph);
     s->graph_exec = nullptr;
     s->graph = nullptr;
+    for (int i = 0; i < 3; ++i) {
+        if (s->pexec[i]) (void)hipGraphExecDestroy(s->pexec[i]);
+        if (s->pgraph[i]) (void)hipGraphDestroy(s->pgraph[i]);
+        s->pexec[i] = nullptr;
+        s->pgraph[i] = nullptr;
+    }
 }
 
-// Capture enqueue_step into s->graph_exec (multifrontal solvers: rocSOLVER's paths are not
-// captured). A stream that cannot be captured leaves graph_failed set and the step runs eagerly,
-// the same launches in the same order.
-int build_graph(bos_solver* s) {
-    drop_graph(s);
+// Capture the launches of one GN step (phase -1: the one-GPU step, enqueue_step; 0-2: a sharded
+// phase) into *exec (multifrontal solvers: rocSOLVER's paths are not captured). A stream that
+// cannot be captured leaves graph_failed set and the launches run eagerly, the same ones in the
+// same order.
+int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec) {
     if (hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
         (void)hipGetLastError();
         s->graph_failed = true;
         return BOS_OK;
     }
-    const int rc = enqueue_step(s);
+    const int rc = phase < 0 ? enqueue_step(s) : shard_enqueue(s, phase);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s->stream, &g);
     if (rc) {
@@ -592,8 +607,8 @@ int build_graph(bos_solver* s) {
         return rc;
     }
     if (e != hipSuccess || !g) return fail(BOS_ERR_DEVICE, std::string("step graph capture: ") + hipGetErrorString(e));
-    s->graph = g;
-    HIP_TRY(hipGraphInstantiate(&s->graph_exec, g, nullptr, nullptr, 0));
+    *graph = g;
+    HIP_TRY(hipGraphInstantiate(exec, g, nullptr, nullptr, 0));
     return BOS_OK;
 }
 
@@ -603,7 +618,7 @@ int build_graph(bos_solver* s) {
 int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     if (s->sharded) return do_step_sharded(s, st, sync);
     int rc;
-    if (uses_mf(s) && !s->graph_exec && !s->graph_failed && (rc = build_graph(s))) return rc;
+    if (uses_mf(s) && !s->graph_exec && !s->graph_failed && (rc = capture(s, -1, &s->graph, &s->graph_exec))) return rc;
     if (s->graph_exec) HIP_TRY(hipGraphLaunch(s->graph_exec, s->stream));
     else if ((rc = enqueue_step(s))) return rc;
     s->have_dx = true;
