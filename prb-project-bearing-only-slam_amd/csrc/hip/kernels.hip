@@ -681,13 +681,16 @@ template <typename T> __global__ void to_f64_kernel(const T* in, double* out, in
 
 template <typename T>
 __global__ void gather_f64_kernel(const T* in, const int32_t* idx, double* out, int64_t n, unsigned long long* stamp,
-                                  uint32_t* epoch) {
+                                  uint32_t* epoch, const T* cin, double* cout, int64_t cn) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
         if (epoch) *epoch += 1u;
     }
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = (double)in[idx[i]];
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n + cn; i += step) {
+        if (i < n) out[i] = (double)in[idx[i]];
+        else cout[i - n] = (double)cin[i - n];
+    }
 }
 
 __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colind, const double* val, int n,
@@ -805,10 +808,11 @@ template <typename T> hipError_t launch_to_f64(const T* in, double* out, int64_t
 
 template <typename T>
 hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
-                             unsigned long long* stamp, uint32_t* epoch) {
-    if (n == 0 && !stamp && !epoch) return hipSuccess;
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
-    hipLaunchKernelGGL((gather_f64_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n, stamp, epoch);
+                             unsigned long long* stamp, uint32_t* epoch, const T* cin, double* cout, int64_t cn) {
+    if (n + cn == 0 && !stamp && !epoch) return hipSuccess;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + cn + 255) / 256, 8192));
+    hipLaunchKernelGGL((gather_f64_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n, stamp, epoch,
+                       cin, cout, cn);
     return hipGetLastError();
 }
 
@@ -830,9 +834,9 @@ template hipError_t launch_triangulate<float>(const TriParams<float>&, hipStream
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);
 template hipError_t launch_gather_f64<double>(const double*, const int32_t*, double*, int64_t, hipStream_t,
-                                              unsigned long long*, uint32_t*);
+                                              unsigned long long*, uint32_t*, const double*, double*, int64_t);
 template hipError_t launch_gather_f64<float>(const float*, const int32_t*, double*, int64_t, hipStream_t,
-                                             unsigned long long*, uint32_t*);
+                                             unsigned long long*, uint32_t*, const float*, double*, int64_t);
 
 }  // namespace dev
 }  // namespace bos

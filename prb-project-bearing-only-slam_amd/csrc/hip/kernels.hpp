@@ -165,12 +165,15 @@ hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part,
 // Infinity Cache hold clean lines of this buffer afterwards (cold-cache timing, bos_time_linearize).
 hipError_t launch_cache_scrub(const double* buf, int64_t n, double* sink, hipStream_t s);
 template <typename T> hipError_t launch_to_f64(const T* in, double* out, int64_t n, hipStream_t s);
-// out[i] = (double)in[idx[i]]. Block 0 also writes the realtime clock to *stamp and bumps *epoch (the
-// multifrontal flows' step epoch, multifrontal.hpp mf_epoch_ptr) when those are set: the right-hand
-// side gather opens the solve of a GN step, so the step needs no marker launches.
+// out[i] = (double)in[idx[i]], i < n, and (when cn > 0) cout[i] = (double)cin[i], i < cn, in one
+// launch. Block 0 also writes the realtime clock to *stamp and bumps *epoch (the multifrontal flows'
+// step epoch, multifrontal.hpp mf_epoch_ptr) when those are set: the right-hand side gather (with
+// the fp64 copy of an fp32 block array) opens the solve of a GN step, so the step needs no marker
+// launches.
 template <typename T>
 hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
-                             unsigned long long* stamp = nullptr, uint32_t* epoch = nullptr);
+                             unsigned long long* stamp = nullptr, uint32_t* epoch = nullptr, const T* cin = nullptr,
+                             double* cout = nullptr, int64_t cn = 0);
 hipError_t launch_scatter_dense(const int32_t* rowptr, const int32_t* colind, const double* val, int n, double* dense,
                                 hipStream_t s);
 

@@ -333,10 +333,11 @@ int enqueue_solver_inputs(bos_solver* s) {
     const bool f32 = s->precision == BOS_FP32;
     unsigned long long* stamp = s->d_status->stamp + 1;
     uint32_t* epoch = uses_mf(s) ? bos::dev::mf_epoch_ptr(s->mf) : nullptr;
-    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch)
+    const bool conv = f32 && uses_mf(s);   // the fp64 copy of the block array, in the same launch
+    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch,
+                                                     conv ? (const float*)s->d_val : nullptr, conv ? s->d_val64 : nullptr,
+                                                     conv ? s->plan.blk.size : 0)
                 : bos::dev::launch_gather_f64<double>((const double*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch));
-    if (f32 && uses_mf(s))
-        HIP_TRY(bos::dev::launch_to_f64<float>((const float*)s->d_val, s->d_val64, s->plan.blk.size, s->stream));
     return BOS_OK;
 }
 
@@ -724,6 +725,10 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         (pb->num_odometry && (!pb->odom_src || !pb->odom_dst || !pb->odom_z || !pb->odom_omega)))
         return fail(BOS_ERR_INVALID, "null problem array");
     int ndev = 0;
+    // host waits spin instead of sleeping (bos_step is synchronous: its wait is on the critical path
+    // of every iteration); only possible before the process's first device use, ignored afterwards
+    (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+    (void)hipGetLastError();
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(BOS_ERR_DEVICE, "no HIP device visible (the HIP path has no CPU fallback)");
     if (opt.world_size < 1 || opt.rank < 0 || opt.rank >= opt.world_size) return fail(BOS_ERR_INVALID, "bad rank / world_size");
