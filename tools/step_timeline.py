@@ -1,19 +1,19 @@
 """Kernel timeline of one GN step from a rocprofv3 kernel trace (diagnostics): the step after the
-last-but-one reduce_stats launch. Usage: python tools/step_timeline.py <rocprofv3 output dir>"""
+last-but-one box-plus launch (graph replays do not report the stats launch). Usage: python tools/step_timeline.py <rocprofv3 output dir>"""
 import csv
 import glob
 import sys
 
 path = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
 r = sorted(csv.DictReader(open(path)), key=lambda x: int(x["Start_Timestamp"]))
-idx = [i for i, x in enumerate(r) if "reduce_stats" in x["Kernel_Name"]]
+idx = [i for i, x in enumerate(r) if "boxplus_kernel" in x["Kernel_Name"]]
 a, b = idx[-2], idx[-1]
 t0 = int(r[a]["End_Timestamp"])
 busy = 0.0
 for x in r[a + 1:b + 1]:
     s, e = int(x["Start_Timestamp"]), int(x["End_Timestamp"])
     busy += (e - s) / 1e3
-    name = x["Kernel_Name"].replace("bos::dev::(anonymous namespace)::", "").replace("void ", "")
+    name = x["Kernel_Name"].replace("(anonymous namespace)::", "").replace("bos::dev::", "").replace("void ", "")
     name = name[:name.index("(")] if "(" in name else name
     print(f"{(s - t0) / 1e3:8.1f} {(e - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {name[:60]:60s} grid {x['Grid_Size_X']:>8s} "
           f"vgpr {x['VGPR_Count']:>3s} agpr {x.get('Accum_VGPR_Count', ''):>3s} lds {x['LDS_Block_Size']:>6s} stream {x['Stream_Id']}")
