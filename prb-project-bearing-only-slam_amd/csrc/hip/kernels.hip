@@ -208,7 +208,9 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
                                            unsigned long long* st) {
     const int g = blk * kBlock + threadIdx.x;   // lane
     const int grp = g / LPP, sub = g % LPP, t = g & 63;
-    const int p = grp < P.n_groups ? P.lane_pose[grp] : -1;
+    // group i runs pose i unless a table says otherwise (sharded ranks): one dependent load fewer
+    // at the head of both of the lane's load chains
+    const int p = grp < P.n_groups ? (P.lane_pose ? P.lane_pose[grp] : grp) : -1;
     const bool active = p >= 0;
     T h[6] = {0, 0, 0, 0, 0, 0}, gb[3] = {0, 0, 0};
     if (active) {

@@ -30,7 +30,7 @@ template <typename T> struct LinParams {
     const T* pth;         // [NP] theta
     const T* lc;          // [NL][2]
     int NP;
-    const int32_t* lane_pose;  // [n_groups] pose of each lane group, -1 = padding
+    const int32_t* lane_pose;  // [n_groups] pose of each lane group, -1 = padding; null: group i = pose i
     int n_groups, n_lm_lanes, pose_blocks;
     // pose lanes
     const int32_t* pw_base;   // [waves + 1]

@@ -115,6 +115,7 @@ struct bos_solver {
     // sharded step (world > 1)
     bool sharded = false, external = false;
     int32_t* lane_pose = nullptr;            // J+H pose lane groups (Shard::lane_poses)
+    bool lane_identity = false;              // group i runs pose i (one GPU): the kernel skips the table
     int chi_parts = 0;                       // J+H chi^2 partial blocks this rank counts
     double *ex1_send = nullptr, *ex1_recv = nullptr, *ex2_send = nullptr, *ex2_recv = nullptr;
     int64_t ex1_count = 0, ex2_count = 0;
@@ -171,7 +172,7 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.lc = (const T*)s->d_lc;
     const bos::Plan& P = s->plan;
     p.NP = s->NP;
-    p.lane_pose = s->lane_pose;
+    p.lane_pose = s->lane_identity ? nullptr : s->lane_pose;
     p.n_groups = (int)P.blk.lane_pose.size();
     p.n_lm_lanes = (int)P.blk.lm_lane_lm.size();
     p.pose_blocks = s->pose_blocks;
@@ -874,6 +875,8 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         // chi^2 partials: own lanes (a whole number of blocks when sharded), the top lanes on rank 0
         s->chi_parts = s->rank == 0 ? s->pose_blocks : (int)((int64_t)P.shard.own_pose_lanes * B.lpp / bos::dev::kBlock);
         if ((rc = upload(&s->lane_pose, B.lane_pose))) return bail(rc);
+        s->lane_identity = true;
+        for (size_t i = 0; i < B.lane_pose.size() && s->lane_identity; ++i) s->lane_identity = B.lane_pose[i] == (int32_t)i;
     }
     for (int k = 0; k < s->Mo; ++k)
         if (pb->odom_src[k] == pb->odom_dst[k]) {

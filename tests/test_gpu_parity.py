@@ -109,15 +109,21 @@ def test_solvers_agree(c1, other):
     assert A.last_stats["solver_info"] == 0 and B.last_stats["solver_info"] == 0
 
 
-def test_step_n_equals_repeated_step(c1):
+@pytest.mark.parametrize("n", [7, 16, 19])
+def test_step_n_equals_repeated_step(c1, n):
+    """bos_step_n (one host synchronisation at the end) runs the same iterations as n bos_step calls,
+    bit for bit, including the status of the last one."""
     A = bos.Solver(c1)
     B = bos.Solver(c1)
-    assert A.step_n(7)["solver_info"] == 0
-    for _ in range(7):
-        assert B.step()["solver_info"] == 0
+    sa = A.step_n(n)
+    assert sa["solver_info"] == 0
+    for _ in range(n):
+        sb = B.step()
+        assert sb["solver_info"] == 0
     pa, la = A.get_state()
     pb, lb = B.get_state()
     assert np.array_equal(pa, pb) and np.array_equal(la, lb)
+    assert sa["chi2"] == sb["chi2"] and sa["max_abs_dx"] == sb["max_abs_dx"] and sa["n_robust"] == sb["n_robust"]
 
 
 def test_settings_changed_between_replayed_steps(c1):
