@@ -25,7 +25,13 @@ S.step()
 st = [S.step() for _ in range(10)]
 lin = np.median([x["t_linearize_ms"] for x in st]) * 1e3
 sol = np.median([x["t_solve_ms"] for x in st]) * 1e3
+upd = np.median([x["t_update_ms"] for x in st]) * 1e3
+import time  # noqa: E402
+t0 = time.perf_counter()
+for _ in range(50):
+    S.step()
+gn = 50 / (time.perf_counter() - t0)
 pose, lm = S.get_state()
 print(f"  chi2 after 11 steps {st[-1]['chi2']:.10e}  state sum {pose.sum():.12e} {lm.sum():.12e}")
 print(f"{sys.argv[1]}: warm {warm * 1e3:6.2f} us  cold {cold * 1e3:6.2f} us  cold span {np.median(spans):6.2f} us  "
-      f"in-step J+H {lin:6.2f} us  solve {sol:6.1f} us", flush=True)
+      f"in-step J+H {lin:6.2f} us  solve {sol:6.1f} us  update {upd:5.1f} us  GN {gn:7.1f} it/s", flush=True)
