@@ -37,5 +37,5 @@ for P in fp32 fp64; do
     python3 bench.py --steps 1 --warmup 0 --cold-steps 50 --gn-steps 0 --tri-steps 0 --no-cpu-baseline --precision $P \
     > $O/bench_${P}_cold.json 2> $O/bench_${P}_cold.err || exit 1
   timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/trace_$P -o run --output-format csv -- \
-    python3 bench.py --steps 200 --warmup 20 --gn-steps 10 --precision $P $CPU > $O/bench_$P.json 2> $O/bench_$P.err || exit 1
+    python3 bench.py --steps 200 --warmup 20 --precision $P $CPU > $O/bench_$P.json 2> $O/bench_$P.err || exit 1
 done
