@@ -280,12 +280,23 @@ def main():
         return h.step_phase(2)
 
     def time_gn(solver_handle):
-        """GN iterations/s two ways: one synchronous bos_step per iteration (Solver::step() returns with
-        the state updated; the host round trip is inside every iteration), and bos_step_n batches
-        (the reference driver's loop of steps, executables/bearing_only_slam.cpp:95-98: every
-        iteration runs in full, the host synchronises once per batch)."""
+        """GN iterations/s three ways: synchronous bos_step calls in a C loop (bos_time_steps: each
+        call returns with the state updated and the status read, as Solver::step() in the reference's
+        C++ driver; the host round trip is inside every iteration), the same calls one by one from
+        Python through ctypes (the binding's per-call overhead included), and bos_step_n batches (the
+        reference driver's loop of steps, executables/bearing_only_slam.cpp:95-98: every iteration
+        runs in full, the host synchronises once per batch). Every timed run starts from the initial
+        guess (bos_set_state), so each times the same iterations 1..gn_steps of the solve; run on past
+        convergence, the fp32 J+H build of this world loses positive definiteness after ~150
+        iterations (tools/gn_trajectory.py)."""
+        init = solver_handle.get_state()
+
+        def restart():
+            solver_handle.set_state(*init)
+            barrier()
+
         gn_step(solver_handle)   # first iteration includes the one-time factorization analysis
-        barrier()
+        restart()
         tg = time.perf_counter()
         stats = [gn_step(solver_handle) for _ in range(args.gn_steps)]
         barrier()
@@ -293,25 +304,27 @@ def main():
         assert all(g["solver_info"] == 0 for g in stats), "non-positive pivot in a benchmarked GN step"
         ph = {k: float(np.median([g[k] for g in stats])) for k in
               ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
-        batched = None
+        batched, c_loop = None, None
         if world == 1 or args.exchange == "rccl":
-            solver_handle.step_n(args.gn_steps)   # untimed: the batch graph is captured on first use
-            barrier()
+            restart()
+            c_loop = 1e3 / max_over_ranks(solver_handle.time_steps(args.gn_steps))
+            restart()
             tg = time.perf_counter()
             last = solver_handle.step_n(args.gn_steps)
             barrier()
             batched = args.gn_steps / max_over_ranks(time.perf_counter() - tg)
             assert last["solver_info"] == 0, "non-positive pivot in a benchmarked GN step"
-        return args.gn_steps / gn_wall, ph, batched
+        restart()
+        return c_loop if c_loop else args.gn_steps / gn_wall, ph, batched, args.gn_steps / gn_wall
 
-    gn_it_s, phase, gn_other, gn_batched = None, None, None, None
+    gn_it_s, phase, gn_other, gn_batched, gn_python = None, None, None, None, None
     if args.gn_steps > 0:
-        gn_it_s, phase, gn_batched = time_gn(S)
+        gn_it_s, phase, gn_batched, gn_python = time_gn(S)
         if world == 1 and not args.no_gn_other:   # the other multifrontal ordering, for comparison
             other = "supernodal" if args.solver == "schur" else "schur"
             S2 = bos.Solver(P, precision=precision, device=local_rank,
                             solver=bos.BOS_SOLVER_SUPERNODAL if other == "supernodal" else bos.BOS_SOLVER_SCHUR)
-            it2, ph2, b2 = time_gn(S2)
+            it2, ph2, b2, _ = time_gn(S2)
             gn_other = {"solver": other, "gn_iters_per_s": it2, "gn_iters_per_s_batched": b2,
                         "t_solve_ms": ph2["t_solve_ms"]}
             S2.close()
@@ -371,6 +384,7 @@ def main():
             },
             "gn_iters_per_s": gn_it_s,
             "gn_iters_per_s_batched": gn_batched,
+            "gn_iters_per_s_python": gn_python,
             "gn_phase_ms": phase,
             "solver_model": solver_model(P, phase, world) if phase else None,
             "gn_solver": args.solver,

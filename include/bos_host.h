@@ -109,9 +109,14 @@ void bos_cpu_gn_destroy(bos_cpu_gn* c);
  * bos_time_linearize: n J+H builds. flush_caches = 0: back to back, the average per build;
  * flush_caches = 1: 512 MiB (of two alternating buffers) are read before each build so its inputs
  * come from HBM (as inside a GN step); each build timed alone by its own pair of events.
- * bos_time_triangulate: n device triangulations back to back (re-estimates the landmarks). */
+ * bos_time_triangulate: n device triangulations back to back (re-estimates the landmarks).
+ * bos_time_steps: n GN iterations, each exactly a bos_step call (launch, wait, status read and
+ * checked), timed on the host clock in a C loop: the synchronous rate a C++ caller of the drop-in
+ * (the reference's driver, executables/bearing_only_slam.cpp:95-98) sees, without a binding's
+ * per-call overhead. */
 int bos_time_linearize(struct bos_solver* s, int32_t n, int32_t flush_caches, double* ms_per_build);
 int bos_time_triangulate(struct bos_solver* s, int32_t n, double* ms_per_call);
+int bos_time_steps(struct bos_solver* s, int32_t n, double* ms_per_step);
 
 /* Test hooks (process-wide, default 0 = product behaviour; not part of the drop-in boundary):
  * poses per nested-dissection leaf of the Schur ordering (forces the plan fallback when large),

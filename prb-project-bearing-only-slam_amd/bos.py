@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = [
     "bos_plan_node_owner", "bos_step_phase", "bos_exchange_size", "bos_exchange_download", "bos_exchange_upload",
     "bos_node_owner",
     "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph", "bos_debug_solver_stamps",
-    "bos_time_linearize", "bos_time_triangulate", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
+    "bos_time_linearize", "bos_time_triangulate", "bos_time_steps", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
     "bos_cpu_gn_destroy",
 ]
 
@@ -168,6 +168,7 @@ def lib():
                                                    ctypes.POINTER(ctypes.c_int32)]),
         "bos_time_linearize": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, _dp]),
         "bos_time_triangulate": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
+        "bos_time_steps": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
         "bos_cpu_gn_create": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32,
                                              ctypes.POINTER(vp)]),
         "bos_cpu_gn_step": (ctypes.c_int, [vp, _dp]),
@@ -537,6 +538,12 @@ class Solver:
         """ms per J+H build (HIP events on the handle's stream, see bos_time_linearize)."""
         ms = ctypes.c_double(0)
         _check(lib().bos_time_linearize(self._h, n, int(flush_caches), ctypes.byref(ms)), "bos_time_linearize")
+        return ms.value
+
+    def time_steps(self, n: int) -> float:
+        """ms per synchronous GN iteration over n bos_step calls made from C (bos_time_steps)."""
+        ms = ctypes.c_double(0)
+        _check(lib().bos_time_steps(self._h, n, ctypes.byref(ms)), "bos_time_steps")
         return ms.value
 
     def time_triangulate(self, n: int) -> float:

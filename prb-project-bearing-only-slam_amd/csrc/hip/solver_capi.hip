@@ -19,6 +19,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -1072,6 +1073,20 @@ int bos_time_triangulate(bos_solver* s, int32_t n, double* ms_per_call) {
     HIP_TRY(hipEventSynchronize(s->ev[1]));
     *ms_per_call = elapsed(s->ev[0], s->ev[1]) / n;
     s->have_dx = false;
+    return BOS_OK;
+}
+
+int bos_time_steps(bos_solver* s, int32_t n, double* ms_per_step) {
+    if (!s || n <= 0 || !ms_per_step) return fail(BOS_ERR_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(s->device));
+    bos_step_stats st;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n; ++i) {   // exactly bos_step: launch, wait, status read and checked
+        const int rc = do_step(s, &st, true);
+        if (rc) return rc;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    *ms_per_step = std::chrono::duration<double, std::milli>(t1 - t0).count() / n;
     return BOS_OK;
 }
 
