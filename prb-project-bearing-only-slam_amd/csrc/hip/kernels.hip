@@ -496,7 +496,19 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
         out->aborted |= inf & kStepAbort;
         if (info) *info = 0;
         out->stamp[3] = __builtin_amdgcn_s_memrealtime();
-        if (mirror) *mirror = *out;
+        out->seq += 1;
+        if (mirror) {   // the summary, then (after a system-scope release) its sequence number: a host
+                        // that sees the new seq sees the whole summary (read_stats polls it)
+            const StepStatus v = *out;
+            mirror->chi2 = v.chi2;
+            mirror->max_dx = v.max_dx;
+            mirror->n_robust = v.n_robust;
+            mirror->info = v.info;
+            mirror->aborted = v.aborted;
+            for (int k = 0; k < 4; ++k) mirror->stamp[k] = v.stamp[k];
+            __threadfence_system();
+            __hip_atomic_store(&mirror->seq, v.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 

@@ -94,7 +94,7 @@ struct StepStatus {
     int32_t n_robust;
     int32_t info;     // solver status: count of non-positive pivots, | kStepAbort (see above)
     int32_t aborted;  // sticky: kStepAbort once any step aborted; the host clears it when it reports it
-    int32_t pad;
+    int32_t seq;      // steps summarised so far (reduce_stats); written to the host mirror last
     // phase boundaries of the last step, realtime clock (100 MHz): J+H start, J+H end / solve start,
     // solve end / update start, step end (written by the step's own kernels: no events in the step)
     unsigned long long stamp[4];

@@ -19,6 +19,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <string>
@@ -153,6 +154,9 @@ struct bos_solver {
     hipGraph_t pgraph[3] = {};          // sharded step: one graph per phase
     hipGraphExec_t pexec[3] = {};
     bool graph_failed = false;   // capture not possible on this stream (e.g. the legacy null stream)
+    // one GPU: the status sequence number last seen, and the status launches enqueued since (each
+    // bumps the device counter once; wait_status polls for seq_seen + seq_pending)
+    int32_t seq_seen = 0, seq_pending = 0;
 };
 
 static_assert(bos::dev::kStepAbort == bos::dev::kMfStall, "solver abort bit");
@@ -445,8 +449,44 @@ int enqueue_triangulate(bos_solver* s) {
 
 // The step status (one copy). The sticky abort flag is cleared here once reported, so every
 // bos_step / bos_step_n batch starts with it clear.
-int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr) {
+// Waits for the status of the last enqueued step. One GPU: the host polls the sequence number the
+// step's last kernel writes to the host-mapped mirror after the summary (a system-scope release in
+// between), which it sees ~10 us before a stream synchronisation returns (tools/sync_step_trace.py);
+// the stream is not synchronised (every later call that reads device memory synchronises it, and
+// launches are stream ordered). A fault or an unexpected state falls back to the stream wait.
+int wait_status(bos_solver* s, bool sync) {
+    if (!sync && !s->sharded && s->seq_pending > 0) {
+        const int32_t target = s->seq_seen + s->seq_pending;
+        s->seq_seen = target;
+        s->seq_pending = 0;
+        const volatile int32_t* q = &s->h_status->seq;
+        for (uint64_t it = 1;; ++it) {
+            if (*q == target) {
+                std::atomic_thread_fence(std::memory_order_acquire);
+                return BOS_OK;
+            }
+            if ((it & 4095) == 0) {   // the stream done (or failed) without the number: report it
+                const hipError_t e = hipStreamQuery(s->stream);
+                if (e != hipErrorNotReady) {
+                    if (e != hipSuccess) HIP_TRY(e);
+                    if (*q == target) break;
+                    return fail(BOS_ERR_DEVICE, "step status sequence number not written");
+                }
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return BOS_OK;
+    }
     HIP_TRY(hipStreamSynchronize(s->stream));
+    s->seq_seen = s->h_status->seq;   // the device counter, whatever ran
+    s->seq_pending = 0;
+    return BOS_OK;
+}
+
+// sync: wait for the stream (callers that read events or device memory next), not only the status
+int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr, bool sync = false) {
+    int rc;
+    if ((rc = wait_status(s, sync))) return rc;
     bos::dev::StepStatus h;
     std::memcpy(&h, (const void*)s->h_status, sizeof(h));   // written by the step's last kernel
     if (h.aborted) {
@@ -568,15 +608,21 @@ int finish_step(bos_solver* s, bos_step_stats* st) {
 
 // The device work of one GN iteration on one GPU: J+H (stamp 0 at its start), solve (its first
 // launch stamps 1 and opens the flows' epoch), box-plus (stamp 2), status (stamp 3 at its end, then
-// the host-mapped copy). No events, no marker launches, no host synchronisation: the sequence is
-// captured once into a hipGraph and replayed.
-int enqueue_step(bos_solver* s) {
+// the host-mapped copy). No events, no marker launches, no host synchronisation: the sequence after
+// the J+H build is captured once into a hipGraph and replayed (do_step).
+// the step after the J+H build (the captured graph: see do_step)
+int enqueue_step_tail(bos_solver* s) {
     int rc;
-    if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
     bool analysed_now = false;
     if ((rc = enqueue_solve(s, analysed_now))) return rc;
     if ((rc = enqueue_update(s))) return rc;
     return enqueue_stats(s, true);
+}
+
+int enqueue_step(bos_solver* s) {
+    int rc;
+    if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
+    return enqueue_step_tail(s);
 }
 
 void drop_graph(bos_solver* s) {
@@ -592,8 +638,8 @@ void drop_graph(bos_solver* s) {
     }
 }
 
-// Capture the launches of one GN step (phase -1: the one-GPU step, enqueue_step; 0-2: a sharded
-// phase) into *exec (multifrontal solvers: rocSOLVER's paths are not captured). A stream that
+// Capture the launches of one GN step (phase -1: the one-GPU step after its J+H build,
+// enqueue_step_tail; 0-2: a sharded phase) into *exec (multifrontal solvers: rocSOLVER's paths are not captured). A stream that
 // cannot be captured leaves graph_failed set and the launches run eagerly, the same ones in the
 // same order.
 int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec) {
@@ -602,7 +648,7 @@ int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec) {
         s->graph_failed = true;
         return BOS_OK;
     }
-    const int rc = phase < 0 ? enqueue_step(s) : shard_enqueue(s, phase);
+    const int rc = phase < 0 ? enqueue_step_tail(s) : shard_enqueue(s, phase);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s->stream, &g);
     if (rc) {
@@ -622,8 +668,17 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     if (s->sharded) return do_step_sharded(s, st, sync);
     int rc;
     if (uses_mf(s) && !s->graph_exec && !s->graph_failed && (rc = capture(s, -1, &s->graph, &s->graph_exec))) return rc;
-    if (s->graph_exec) HIP_TRY(hipGraphLaunch(s->graph_exec, s->stream));
-    else if ((rc = enqueue_step(s))) return rc;
+    ++s->seq_pending;   // the step's status launch bumps the device counter once
+    if (s->graph_exec) {
+        // the J+H build launched directly (it starts a few us after the call), the rest of the step
+        // as the graph, submitted while the build runs (a graph's first kernel starts 13-25 us after
+        // hipGraphLaunch, tools/sync_step_trace.py; launching the input gather directly too measured
+        // slower: 1 760 against 1 790 it/s)
+        if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
+        HIP_TRY(hipGraphLaunch(s->graph_exec, s->stream));
+    } else if ((rc = enqueue_step(s))) {
+        return rc;
+    }
     s->have_dx = true;
     if (!sync) return BOS_OK;
     int32_t aborted = 0;
@@ -1164,6 +1219,7 @@ int bos_debug_solver_stamps(bos_solver* s, int64_t capacity, uint64_t* stamps, i
     s->graph_failed = true;   // one eager step with the stamps
     bos::dev::mf_debug_set_stamps(s->mf, d);
     rc = do_step(s, nullptr, true);
+    if (!rc && hipStreamSynchronize(s->stream) != hipSuccess) rc = fail(BOS_ERR_DEVICE, "stamps step");
     bos::dev::mf_debug_set_stamps(s->mf, nullptr);
     s->graph_failed = gf;
     if (!rc && hipMemcpy(stamps, d, need * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
@@ -1219,7 +1275,7 @@ int bos_linearize(bos_solver* s, bos_step_stats* st) {
     HIP_TRY(hipEventRecord(s->ev[1], s->stream));
     HIP_TRY(hipEventRecord(s->ev[2], s->stream));
     if ((rc = enqueue_stats(s, false))) return rc;
-    if ((rc = read_stats(s, st))) return rc;
+    if ((rc = read_stats(s, st, nullptr, true))) return rc;   // the events are read next
     if (st) {
         st->t_linearize_ms = elapsed(s->ev[0], s->ev[1]);
         st->t_exchange_ms = elapsed(s->ev[1], s->ev[2]);

@@ -162,6 +162,30 @@ def test_step_phase_times_are_stamped(c1):
     assert st["t_exchange_ms"] == 0.0
 
 
+def test_status_read_across_mixed_calls(c1):
+    """bos_step returns once the step's status has landed in host memory (a sequence number the
+    step's last kernel writes after the summary), without a stream synchronisation: mixing builds
+    (which synchronise), single steps, batches, state reads and a restart keeps every returned status
+    the current one and the iterations those of an undisturbed run."""
+    A = bos.Solver(c1)
+    B = bos.Solver(c1)
+    p0, l0 = A.get_state()
+    A.linearize()
+    sa = [A.step()]
+    sa.append(A.step_n(3))
+    A.linearize()
+    A.get_state()
+    sa.append(A.step())
+    sb = [B.step() for _ in range(5)]
+    for got, want in ((sa[0], sb[0]), (sa[1], sb[3]), (sa[2], sb[4])):
+        assert got["chi2"] == want["chi2"] and got["max_abs_dx"] == want["max_abs_dx"], (got, want)
+    pa, la = A.get_state()
+    pb, lb = B.get_state()
+    assert np.array_equal(pa, pb) and np.array_equal(la, lb)
+    A.set_state(p0, l0)
+    assert A.step()["chi2"] == sb[0]["chi2"]
+
+
 def test_set_state_roundtrip(c1):
     S = bos.Solver(c1)
     p0, l0 = S.get_state()
