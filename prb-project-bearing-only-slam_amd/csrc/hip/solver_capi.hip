@@ -149,8 +149,10 @@ struct bos_solver {
     int scrub_turn = 0;
     // one-GPU multifrontal GN step captured once into a graph (every launch argument is fixed:
     // kernel threshold and damping are baked in, so setting them drops the graph)
-    hipGraph_t graph = nullptr;
+    hipGraph_t graph = nullptr;          // the step after its J+H build (synchronous steps)
     hipGraphExec_t graph_exec = nullptr;
+    hipGraph_t graph_full = nullptr;     // the whole step (the steps of a batch before its last)
+    hipGraphExec_t exec_full = nullptr;
     hipGraph_t pgraph[3] = {};          // sharded step: one graph per phase
     hipGraphExec_t pexec[3] = {};
     bool graph_failed = false;   // capture not possible on this stream (e.g. the legacy null stream)
@@ -630,6 +632,10 @@ void drop_graph(bos_solver* s) {
     if (s->graph) (void)hipGraphDestroy(s->graph);
     s->graph_exec = nullptr;
     s->graph = nullptr;
+    if (s->exec_full) (void)hipGraphExecDestroy(s->exec_full);
+    if (s->graph_full) (void)hipGraphDestroy(s->graph_full);
+    s->exec_full = nullptr;
+    s->graph_full = nullptr;
     for (int i = 0; i < 3; ++i) {
         if (s->pexec[i]) (void)hipGraphExecDestroy(s->pexec[i]);
         if (s->pgraph[i]) (void)hipGraphDestroy(s->pgraph[i]);
@@ -639,16 +645,16 @@ void drop_graph(bos_solver* s) {
 }
 
 // Capture the launches of one GN step (phase -1: the one-GPU step after its J+H build,
-// enqueue_step_tail; 0-2: a sharded phase) into *exec (multifrontal solvers: rocSOLVER's paths are not captured). A stream that
-// cannot be captured leaves graph_failed set and the launches run eagerly, the same ones in the
-// same order.
+// enqueue_step_tail; -2: the whole one-GPU step; 0-2: a sharded phase) into *exec (multifrontal
+// solvers: rocSOLVER's paths are not captured). A stream that cannot be captured leaves
+// graph_failed set and the launches run eagerly, the same ones in the same order.
 int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec) {
     if (hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
         (void)hipGetLastError();
         s->graph_failed = true;
         return BOS_OK;
     }
-    const int rc = phase < 0 ? enqueue_step_tail(s) : shard_enqueue(s, phase);
+    const int rc = phase == -1 ? enqueue_step_tail(s) : phase == -2 ? enqueue_step(s) : shard_enqueue(s, phase);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s->stream, &g);
     if (rc) {
@@ -668,12 +674,17 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     if (s->sharded) return do_step_sharded(s, st, sync);
     int rc;
     if (uses_mf(s) && !s->graph_exec && !s->graph_failed && (rc = capture(s, -1, &s->graph, &s->graph_exec))) return rc;
+    if (uses_mf(s) && !s->exec_full && !s->graph_failed && (rc = capture(s, -2, &s->graph_full, &s->exec_full)))
+        return rc;   // both graphs at the first step, so neither kind of call pays a capture later
     ++s->seq_pending;   // the step's status launch bumps the device counter once
-    if (s->graph_exec) {
-        // the J+H build launched directly (it starts a few us after the call), the rest of the step
-        // as the graph, submitted while the build runs (a graph's first kernel starts 13-25 us after
-        // hipGraphLaunch, tools/sync_step_trace.py; launching the input gather directly too measured
-        // slower: 1 760 against 1 790 it/s)
+    if (!sync && s->exec_full) {
+        // a batch's step before its last: the host is ahead of the device, one graph per step
+        HIP_TRY(hipGraphLaunch(s->exec_full, s->stream));
+    } else if (s->graph_exec) {
+        // synchronous: the J+H build launched directly (it starts a few us after the call), the
+        // rest of the step as the graph, submitted while the build runs (a graph's first kernel
+        // starts 13-25 us after hipGraphLaunch, tools/sync_step_trace.py; launching the input
+        // gather directly too measured slower: 1 760 against 1 790 it/s)
         if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
         HIP_TRY(hipGraphLaunch(s->graph_exec, s->stream));
     } else if ((rc = enqueue_step(s))) {
