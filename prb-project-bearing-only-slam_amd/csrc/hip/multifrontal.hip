@@ -40,16 +40,16 @@ __device__ __forceinline__ int64_t pk(int64_t i, int64_t j, int64_t m) { return 
 __device__ __forceinline__ int pk32(int i, int j, int m) { return j * m - j * (j - 1) / 2 + (i - j); }   // LDS fronts
 
 // Copy n doubles global -> LDS by one wavefront, 8 independent loads in flight per lane.
-__device__ __forceinline__ void stage_lds(double* dst, const double* src, int n, int lane) {
-    for (int e0 = 0; e0 < n; e0 += 512) {
-        double v[8];
+template <int U = 8> __device__ __forceinline__ void stage_lds(double* dst, const double* src, int n, int lane) {
+    for (int e0 = 0; e0 < n; e0 += 64 * U) {
+        double v[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int e = e0 + 64 * u + lane;
             v[u] = e < n ? src[e] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int e = e0 + 64 * u + lane;
             if (e < n) dst[e] = v[u];
         }
@@ -793,15 +793,27 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
     const int xi0 = lane < r ? fi[k + lane] : 0;   // where the first 64 rows' x live (static)
     unsigned long long* const stp = f ? f->stamps : a.stamps_b;
     fstamp(stp, s, 0);
-    stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
-    for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
-    fstamp(stp, s, 1);
-    if constexpr (FLOW) {
+    if constexpr (!FLOW) {
+        // per-level launch: the parents' x are final (earlier launches), so the front's own
+        // right-hand side and the first 64 rows' x are loaded beside the panel, all in flight at once
+        const double y0 = lane < k ? a.x[c0 + lane] : 0.0;
+        const double xr0 = lane < r ? a.x[xi0] : 0.0;
+        stage_lds<16>(Lw, a.L + a.L_off[s], m * k, lane);
+        if (lane < k) w[lane] = y0;
+        for (int j = 64 + lane; j < k; j += 64) w[j] = a.x[c0 + j];
+        fstamp(stp, s, 1);
+        fstamp(stp, s, 2);
+        if (lane < r) xs[lane] = xr0;
+        for (int i = 64 + lane; i < r; i += 64) xs[i] = a.x[fi[k + i]];
+    } else {
+        stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
+        for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
+        fstamp(stp, s, 1);
         if (parent[s] >= 0 && f->fid[parent[s]] == f->id) wait_done(*f, parent[s], a.info);
+        fstamp(stp, s, 2);
+        if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
+        for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     }
-    fstamp(stp, s, 2);
-    if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
-    for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     wave_sync();
     if (k <= 64) {
         // lane j < k: t_j = sum_i L[k + i, j] x[fi[k + i]] in row order, then the triangular

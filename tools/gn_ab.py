@@ -1,0 +1,52 @@
+"""A/B timing of libbos.so build variants on the bench's config-3 world (fp32 J+H, fp64 Schur
+solve; experiments). Each variant runs in its own process, alternating A B A B ...; per run: the
+median device-stamped phases of 50 synchronous steps, synchronous GN it/s (bos_time_steps, best of
+3 x 50) and a checksum of the state after 50 iterations (equal for variants that compute the same).
+
+    python tools/gn_ab.py <libA.so> <libB.so> [rounds]
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(lib):
+    sys.path.insert(0, os.path.join(ROOT, "prb-project-bearing-only-slam_amd"))
+    import numpy as np
+    import bos
+    bos.LIB_PATH = os.path.abspath(lib)
+    P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
+    S = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, device=0)
+    init = S.get_state()
+    S.step()
+    S.set_state(*init)
+    st = [S.step() for _ in range(50)]
+    assert all(g["solver_info"] == 0 for g in st)
+    ph = {k: float(np.median([g[k] for g in st])) * 1e3 for k in ("t_linearize_ms", "t_solve_ms", "t_update_ms")}
+    pose, lm = S.get_state()
+    ck = float(np.abs(pose).sum() + np.abs(lm).sum())
+    best = 0.0
+    for _ in range(3):
+        S.set_state(*init)
+        best = max(best, 1e3 / S.time_steps(50))
+    print(f"{os.path.basename(lib)}: J+H {ph['t_linearize_ms']:.2f} us  solve {ph['t_solve_ms']:.1f} us  "
+          f"update {ph['t_update_ms']:.1f} us  GN {best:.0f} it/s  state {ck!r}", flush=True)
+
+
+def main():
+    if sys.argv[1] == "--child":
+        child(sys.argv[2])
+        return
+    libs = sys.argv[1:3]
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    for _ in range(rounds):
+        for lib in libs:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib], timeout=120)
+            if r.returncode != 0:
+                sys.exit(r.returncode)
+
+
+if __name__ == "__main__":
+    main()
