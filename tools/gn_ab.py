@@ -3,7 +3,7 @@ solve; experiments). Each variant runs in its own process, alternating A B A B .
 median device-stamped phases of 50 synchronous steps, synchronous GN it/s (bos_time_steps, best of
 3 x 50) and a checksum of the state after 50 iterations (equal for variants that compute the same).
 
-    python tools/gn_ab.py <libA.so> <libB.so> [rounds]
+    python tools/gn_ab.py <libA.so> <libB.so> [<libC.so> ...] [rounds]
 """
 import os
 import subprocess
@@ -39,8 +39,9 @@ def main():
     if sys.argv[1] == "--child":
         child(sys.argv[2])
         return
-    libs = sys.argv[1:3]
-    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    libs = [a for a in sys.argv[1:] if a.endswith(".so")]
+    rest = [a for a in sys.argv[1:] if not a.endswith(".so")]
+    rounds = int(rest[0]) if rest else 2
     for _ in range(rounds):
         for lib in libs:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib], timeout=120)
