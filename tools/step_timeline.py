@@ -1,5 +1,5 @@
-"""Kernel timeline of one GN step from a rocprofv3 kernel trace (diagnostics): the step after the
-last-but-one box-plus launch (graph replays do not report the stats launch). Usage: python tools/step_timeline.py <rocprofv3 output dir>"""
+"""Kernel timeline of one GN step from a rocprofv3 kernel trace (diagnostics): the last Schur-ordering
+step (between two box-plus launches, with the folded landmarks' backward launch) (graph replays do not report the stats launch). Usage: python tools/step_timeline.py <rocprofv3 output dir>"""
 import csv
 import glob
 import sys
@@ -7,7 +7,10 @@ import sys
 path = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
 r = sorted(csv.DictReader(open(path)), key=lambda x: int(x["Start_Timestamp"]))
 idx = [i for i, x in enumerate(r) if "boxplus_kernel" in x["Kernel_Name"]]
-a, b = idx[-2], idx[-1]
+# the last step of the default (Schur) solver: its steps run the folded landmarks' backward launch
+# (the bench times the nested-dissection ordering after it)
+pairs = [(p, q) for p, q in zip(idx, idx[1:]) if any("mf_backward_fold" in x["Kernel_Name"] for x in r[p:q])]
+a, b = pairs[-1] if pairs else (idx[-2], idx[-1])
 t0 = int(r[a]["End_Timestamp"])
 busy = 0.0
 for x in r[a + 1:b + 1]:
