@@ -700,10 +700,22 @@ __global__ void gather_f64_kernel(const T* in, const int32_t* idx, double* out, 
         if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
         if (epoch) *epoch += 1u;
     }
-    const int64_t step = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n + cn; i += step) {
-        if (i < n) out[i] = (double)in[idx[i]];
-        else cout[i - n] = (double)cin[i - n];
+    // items [0, n): the gather; then the copy, four values per item (16-byte fp32 loads, two 16-byte
+    // fp64 stores; both arrays are allocation-aligned), then its last cn % 4 values one per item
+    const int64_t step = (int64_t)gridDim.x * blockDim.x, cv = cn >> 2;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n + cv + (cn & 3); i += step) {
+        if (i < n) {
+            out[i] = (double)in[idx[i]];
+        } else if (i < n + cv) {
+            const int64_t j = i - n;
+            const V4<T> v = load4(cin + 4 * j);
+            V2<double>* o = (V2<double>*)(cout + 4 * j);
+            o[0] = V2<double>{(double)v.x, (double)v.y};
+            o[1] = V2<double>{(double)v.z, (double)v.w};
+        } else {
+            const int64_t j = 4 * cv + (i - n - cv);
+            cout[j] = (double)cin[j];
+        }
     }
 }
 
@@ -824,7 +836,8 @@ template <typename T>
 hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
                              unsigned long long* stamp, uint32_t* epoch, const T* cin, double* cout, int64_t cn) {
     if (n + cn == 0 && !stamp && !epoch) return hipSuccess;
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + cn + 255) / 256, 8192));
+    const int64_t items = n + (cn >> 2) + (cn & 3);
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 8192));
     hipLaunchKernelGGL((gather_f64_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n, stamp, epoch,
                        cin, cout, cn);
     return hipGetLastError();
