@@ -418,16 +418,15 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
     const int i = U.nodes ? (t < U.n_nodes ? U.nodes[t] : -1) : t;
     double m = 0.0;
     if (U.t_start && blockIdx.x == 0 && threadIdx.x == 0) *U.t_start = __builtin_amdgcn_s_memrealtime();
-    if (U.info && (*U.info & kStepAbort)) {
-        if (threadIdx.x == 0) U.max_part[blockIdx.x] = 0.0;
-        return;
-    }
-    if (i < 0) {
-    } else if (i < U.NP) {
-        if (i != U.fixed) {
-            const int d = U.node_dof[i];
-            const double dx = -U.x[d], dy = -U.x[d + 1], dth = -U.x[d + 2];
-            double x = U.pose[3 * i], y = U.pose[3 * i + 1], th = U.pose[3 * i + 2];
+    // the node's dof, its state and the abort word are loaded together (one dependent hop, to the
+    // solution, follows); nothing is written when the solver aborted
+    const bool is_pose = i >= 0 && i < U.NP && i != U.fixed, is_lm = i >= U.NP && i < U.NP + U.NL;
+    const int d = is_pose || is_lm ? U.node_dof[i] : 0;
+    const int32_t inf = U.info ? *U.info : 0;
+    if (is_pose) {
+        double x = U.pose[3 * i], y = U.pose[3 * i + 1], th = U.pose[3 * i + 2];
+        const double dx = -U.x[d], dy = -U.x[d + 1], dth = -U.x[d + 2];
+        if (!(inf & kStepAbort)) {
             bos::boxplus_pose<double>(x, y, th, dx, dy, dth);
             U.pose[3 * i] = x;
             U.pose[3 * i + 1] = y;
@@ -439,16 +438,18 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
             U.pth[i] = (T)th;
             m = nan_max(fabs(dx), nan_max(fabs(dy), fabs(dth)));
         }
-    } else if (i < U.NP + U.NL) {
+    } else if (is_lm) {
         const int j = i - U.NP;
-        const int d = U.node_dof[i];
+        const double lx = U.lm[2 * j], ly = U.lm[2 * j + 1];
         const double dx = -U.x[d], dy = -U.x[d + 1];
-        const double x = U.lm[2 * j] + dx, y = U.lm[2 * j + 1] + dy;
-        U.lm[2 * j] = x;
-        U.lm[2 * j + 1] = y;
-        U.lc[2 * j] = (T)x;
-        U.lc[2 * j + 1] = (T)y;
-        m = nan_max(fabs(dx), fabs(dy));
+        if (!(inf & kStepAbort)) {
+            const double x = lx + dx, y = ly + dy;
+            U.lm[2 * j] = x;
+            U.lm[2 * j + 1] = y;
+            U.lc[2 * j] = (T)x;
+            U.lc[2 * j + 1] = (T)y;
+            m = nan_max(fabs(dx), fabs(dy));
+        }
     }
     // block max into its partial slot (max is order independent: deterministic; no atomics, which
     // would serialize on one address)
@@ -472,6 +473,7 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
     __shared__ long long sr[256];
     double c = 0.0, m = 0.0;
     long long r = 0;
+    const int32_t inf = info && threadIdx.x == 0 ? *info : 0;   // loaded with the partials
     for (int i = threadIdx.x; i < n; i += blockDim.x) { c += chi_part[i]; r += nrob_part[i]; }
     if (max_part)
         for (int i = threadIdx.x; i < n_max; i += blockDim.x) m = nan_max(m, max_part[i]);
@@ -491,7 +493,6 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
         out->chi2 = sc[0] + chi_const;
         out->n_robust = (int32_t)sr[0] + nrob_const;
         out->max_dx = sm[0];
-        const int32_t inf = info ? *info : 0;
         out->info = inf;
         out->aborted |= inf & kStepAbort;
         if (info) *info = 0;
