@@ -780,6 +780,8 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
 // L panel (m x k). The rows below the supernode are ancestors' dofs, already final in x.
 // The L panel and the front's own forward results do not depend on the ancestors, so the flow
 // kernel stages them before it waits for the parent (FLOW: f and parent set).
+constexpr int kBwdRegK = 32;   // fronts with k <= this solve their triangle from registers
+
 template <bool FLOW>
 __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w, int lane, const Flow* f,
                                                const int32_t* parent) {
@@ -825,10 +827,26 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         // 1 / L_jj by every lane at once, off the sequential chain below
         const double yv = own ? w[lane] : 0.0, rjj = own ? 1.0 / Lw[lane + lane * m] : 1.0;
         double xv = 0.0;
-        for (int j = k - 1; j >= 0; --j) {
-            const double xj = readlane_d((yv - tj) * rjj, j);
-            if (lane == j) xv = xj;
-            else if (lane < j) tj += Lw[j + lane * m] * xj;
+        if (!FLOW && k <= kBwdRegK) {   // per-level launches only (the flow keeps its registers)
+            // the lane's column of the k x k block in registers, read from LDS before the chain, so
+            // each step of the sequential chain is arithmetic and a lane read only
+            double lr[kBwdRegK];
+#pragma unroll
+            for (int j = 0; j < kBwdRegK; ++j) lr[j] = own && j < k ? Lw[j + lane * m] : 0.0;
+#pragma unroll
+            for (int j = kBwdRegK - 1; j >= 0; --j) {
+                if (j < k) {   // uniform
+                    const double xj = readlane_d((yv - tj) * rjj, j);
+                    if (lane == j) xv = xj;
+                    else if (lane < j) tj += lr[j] * xj;
+                }
+            }
+        } else {
+            for (int j = k - 1; j >= 0; --j) {
+                const double xj = readlane_d((yv - tj) * rjj, j);
+                if (lane == j) xv = xj;
+                else if (lane < j) tj += Lw[j + lane * m] * xj;
+            }
         }
         if (own) stc<COH>(a.x + c0 + lane, xv);
         wave_sync();
