@@ -1,24 +1,35 @@
-#!/usr/bin/env python3
 """Benchmark of the GN hot path (J+H build) on MI355X — BASELINE.json metric:
 "GN iterations/sec + observations/sec (J+H build) at 1/2/4/8 GPUs vs CPU".
 
-A *step* is one J+H build (reference slam/solver.cpp:28-69) over the whole synthetic
-config-3 world (100k poses / 200k landmarks / 1M bearings / 99 999 odometry edges), inputs
-resident in HBM. ``value`` = observations (bearings + odometry edges) processed per second by
-the whole job. With ``--gpus N > 1`` the same world is sharded across N ranks (strong scaling):
-each rank builds the part of H its subtrees and the replicated top read, so the
-J+H needs no exchange; a GN iteration has two RCCL all-gathers.
+A *step* is one Gauss-Newton iteration of the reference's Solver::step (slam/solver.cpp:27-97) over
+the whole synthetic config-3 world (100k poses / 200k landmarks / 1M bearings / 99 999 odometry
+edges), inputs resident in HBM. The timed region is K such steps (synchronous bos_step calls,
+restarting from the initial guess every 50 steps outside the timed region: each run times iterations
+1..50 of the solve, the reference UI's batch). ``value`` = observations (bearings + odometry edges)
+per second of the J+H build *as it runs inside those steps* (device realtime stamps written by the
+step's own kernels, median over the K steps, the slowest rank); ``ms_per_step`` is that J+H time
+(= roofline.kernel_ms). The steps' wall rate is ``gn_iters_per_s``.
 
-Also reported: GN iterations/s (full steps: J+H + sparse Cholesky + exchanges + box-plus), the
-J+H kernel's HBM roofline fraction from cold caches (in-step) and back to back (algorithmic
-bytes), and the CPU baselines (the oracle, oracle/bos_oracle.cpp, timed on this
-host's usable cores).
+With ``--gpus N > 1`` the same world is split over N ranks (strong scaling), one process per GPU:
+under torch.distributed.run (RANK / WORLD_SIZE set), or — without a launcher — this script starts the N
+rank processes itself before anything touches the GPU. Every rank checks that its RCCL communicator
+holds N ranks (``ranks_seen``, ncclCommCount) and exits non-zero otherwise. The default partition
+(BOS_PARTITION_SUBTREE) gives each rank the subtrees of the Schur assembly tree below a
+replicated top: its J+H builds only the H its fronts read, two all-gathers per iteration. The north
+star's partition (BOS_PARTITION_OBSERVATIONS: the J+H lanes split by measurement order, one
+all-reduce of (H, b), the solve replicated) is timed beside it (``partition_observations``).
+
+Also reported: the J+H kernel's HBM roofline fraction (in-step; from cold caches by events; back to
+back), GN iterations/s, and the CPU baselines (the oracle, oracle/bos_oracle.cpp, and the build's
+C++ CPU backend, timed on this host's usable cores).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|fp64]
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,13 +38,7 @@ sys.path.insert(0, os.path.join(ROOT, "prb-project-bearing-only-slam_amd"))
 
 import numpy as np  # noqa: E402
 
-import bos  # noqa: E402
-
-# libbos.so (and the system ROCm 7.2 libraries it links: HIP runtime, rocBLAS/rocSOLVER, RCCL) is
-# loaded before torch, exactly as in the test suite (tests/conftest.py): whichever copy of those
-# sonames loads first serves the process, so the benchmarked binary runs on the runtime the parity
-# tests validated, not on torch's bundled copies.
-bos.lib()
+bos = None   # the product binding, imported in main() after the rank launcher (no HIP in a launcher)
 
 METRIC = "GN iterations/sec + observations/sec (J+H build) at 1/2/4/8 GPUs vs CPU"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, HBM3E peak (spec)
@@ -181,34 +186,101 @@ def traffic_from_profile(precision):
     return out
 
 
+def free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """No launcher but --gpus N > 1: start N rank processes of this script (one per GPU, env as
+    torch.distributed.run sets it), relay rank 0's JSON line, exit with the worst exit code. Runs
+    before anything in this process touches HIP."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0]
+    rcs = [procs[0].returncode]
+    for p in procs[1:]:
+        try:
+            rcs.append(p.wait(timeout=600))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            rcs.append(p.wait())
+    if out:
+        sys.stdout.write(out.decode())
+        sys.stdout.flush()
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        log(f"launcher: rank exit codes {rcs}")
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50, help="GN iterations timed (restart from the initial guess every 50)")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed GN iterations before the timed ones")
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
-    ap.add_argument("--gn-steps", type=int, default=50,
-                    help="GN iterations timed (sync and as one bos_step_n batch: the reference UI steps 50 at a time)")
-    ap.add_argument("--cold-steps", type=int, default=20, help="J+H builds timed from cold caches (in-step roofline)")
+    ap.add_argument("--replay-steps", type=int, default=200, help="J+H builds back to back (warm-replay roofline)")
+    ap.add_argument("--cold-steps", type=int, default=20, help="J+H builds timed from cold caches by events")
+    ap.add_argument("--batch", type=int, default=50, help="GN iterations per bos_step_n batch (the reference UI's 50)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gn-other", action="store_true", help="skip timing the other solver ordering")
+    ap.add_argument("--no-partition-other", action="store_true", help="N > 1: skip the observations partition")
     ap.add_argument("--tri-steps", type=int, default=20, help="device triangulations timed (0: skip)")
     ap.add_argument("--exchange", choices=["rccl", "gloo"], default="rccl",
-                    help="N > 1: the sharded step's two all-gathers on RCCL (default), or through host memory "
-                         "and gloo (rehearsal of the N-rank path on fewer GPUs, with --same-device)")
+                    help="N > 1: the exchanges on RCCL (default), or through host memory and gloo (rehearsal of "
+                         "the N-rank path on fewer GPUs, with --same-device)")
     ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (rehearsal only)")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="launch / rendezvous check only (no GPU): every rank joins the gloo group, rank 0 prints "
+                         "the ranks seen")
     ap.add_argument("--solver", choices=["supernodal", "schur"], default="schur",
                     help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
                          "nested-dissection multifrontal; the other one is timed too (gn_other)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    # torch only for the rendezvous (gloo, host memory): the GPU work and its timing go through
-    # libbos.so (HIP events on the handle's stream), and the exchange runs on RCCL inside it
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
+
+    if args.check_launch:   # the rank processes and their rendezvous, nothing else (tests/test_bench.py)
+        seen = 1
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            t = torch.tensor([rank], dtype=torch.int64)
+            parts = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            seen = len({int(x) for x in parts})
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"check_launch": True, "ranks_seen": seen, "world": world}), flush=True)
+        sys.exit(0 if seen == args.gpus else 3)
+
+    global bos
+    import bos as _bos
+    bos = _bos
+    # libbos.so (and the system ROCm 7.2 libraries it links: HIP runtime, rocBLAS/rocSOLVER, RCCL) is
+    # loaded before torch, exactly as in the test suite (tests/conftest.py): whichever copy of those
+    # sonames loads first serves the process, so the benchmarked binary runs on the runtime the parity
+    # tests validated, not on torch's bundled copies.
+    bos.lib()
+
+    # torch only for the rendezvous and the gloo rehearsal (host memory): the GPU work and its timing
+    # go through libbos.so, and the exchanges run on RCCL inside it
     dist = None
     if world > 1:
         import torch
@@ -222,20 +294,6 @@ def main():
     log(f"rank {rank}: config 3 world NP={P.NP} NL={P.NL} Mb={len(P.b_z)} Mo={len(P.o_z)} "
         f"({time.perf_counter() - t_gen:.1f} s)")
 
-    nccl_id = None
-    if world > 1 and args.exchange == "rccl":
-        obj = [bos.nccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        nccl_id = obj[0]
-    device = 0 if args.same_device else local_rank
-    t_create = time.perf_counter()
-    solver = bos.BOS_SOLVER_SCHUR if args.solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
-    S = bos.Solver(P, precision=precision, solver=solver, device=device, rank=rank, world_size=world,
-                   nccl_id=nccl_id)
-    info = S.system_info()
-    log(f"rank {rank}: bos_create {time.perf_counter() - t_create:.1f} s, n={info['n']} "
-        f"nnz(H lower)={info['nnz_lower']} nnz(L)={info['nnz_factor']}")
-
     def barrier():
         if world > 1:
             dist.barrier()
@@ -247,87 +305,139 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    # ---- J+H build throughput: K builds back to back (the timed region), warm caches
-    if args.warmup > 0:
-        S.time_linearize(args.warmup)
-    S.synchronize()
-    barrier()
-    S.synchronize()
-    t0 = time.perf_counter()
-    kernel_ms = S.time_linearize(args.steps)   # synchronises the handle's stream
-    barrier()
-    wall = max_over_ranks(time.perf_counter() - t0)
-    ms_per_step = wall / args.steps * 1e3
-    value = nobs * args.steps / wall
-    # ---- the same build from cold caches (512 MiB read before each): what it costs inside a GN
-    # iteration, where the solver's factor streams between two builds
-    cold_ms = S.time_linearize(args.cold_steps, flush_caches=True) if args.cold_steps > 0 else None
+    device = 0 if args.same_device else local_rank
+    solver = bos.BOS_SOLVER_SCHUR if args.solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
 
-    # ---- full GN iterations (J+H + exchanges + solve + update)
+    def make_handle(partition):
+        nccl_id = None
+        if world > 1 and args.exchange == "rccl":
+            obj = [bos.nccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            nccl_id = obj[0]
+        t0 = time.perf_counter()
+        h = bos.Solver(P, precision=precision, solver=solver, device=device, rank=rank, world_size=world,
+                       nccl_id=nccl_id, partition=partition)
+        inf = h.system_info()
+        # the ranks the exchange actually spans: the communicator's count (RCCL), or gloo's
+        seen = inf["comm_ranks"] if nccl_id is not None else (dist.get_world_size() if world > 1 else 1)
+        log(f"rank {rank}: bos_create ({'observations' if partition else 'subtree'} partition) "
+            f"{time.perf_counter() - t0:.1f} s, n={inf['n']} nnz(H lower)={inf['nnz_lower']} "
+            f"nnz(L)={inf['nnz_factor']}, ranks seen {seen}")
+        if seen != args.gpus:
+            log(f"error: rank {rank}: the exchange spans {seen} ranks, --gpus {args.gpus}")
+            sys.exit(3)
+        return h, inf, seen
+
+    S, info, ranks_seen = make_handle(bos.BOS_PARTITION_SUBTREE)
+
+    # ---- one GN iteration, per exchange mode
     def gloo_allgather(h, which):
         mine = torch.from_numpy(h.exchange_download(which))
         parts = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(parts, mine)
         h.exchange_upload(which, torch.cat(parts).numpy())
 
-    def gn_step(h):
+    def gloo_allreduce(h):
+        t = torch.from_numpy(h.exchange_download(1))
+        dist.all_reduce(t)
+        h.exchange_upload(1, t.numpy())
+
+    def gn_step(h, partition):
         if world == 1 or args.exchange == "rccl":
             return h.step()
+        if partition == bos.BOS_PARTITION_OBSERVATIONS:
+            h.step_phase(0)
+            gloo_allreduce(h)
+            return h.step_phase(1)
         h.step_phase(0)
         gloo_allgather(h, 1)
         h.step_phase(1)
         gloo_allgather(h, 2)
         return h.step_phase(2)
 
-    def time_gn(solver_handle):
-        """GN iterations/s three ways: synchronous bos_step calls in a C loop (bos_time_steps: each
-        call returns with the state updated and the status read, as Solver::step() in the reference's
-        C++ driver; the host round trip is inside every iteration), the same calls one by one from
-        Python through ctypes (the binding's per-call overhead included), and bos_step_n batches (the
-        reference driver's loop of steps, executables/bearing_only_slam.cpp:95-98: every iteration
-        runs in full, the host synchronises once per batch). Every timed run starts from the initial
-        guess (bos_set_state), so each times the same iterations 1..gn_steps of the solve; run on past
-        convergence, the fp32 J+H build of this world loses positive definiteness after ~150
-        iterations (tools/gn_trajectory.py)."""
-        init = solver_handle.get_state()
-
-        def restart():
-            solver_handle.set_state(*init)
+    def timed_steps(h, partition, k, warmup):
+        """k GN iterations in chunks of <= 50 from the initial guess (restart outside the timed
+        region), after `warmup` untimed ones: (wall seconds of the timed steps, max over ranks;
+        per-step stats)."""
+        init = h.get_state()
+        for _ in range(warmup):
+            gn_step(h, partition)
+        stats, wall, done = [], 0.0, 0
+        while done < k:
+            n = min(50, k - done)
+            h.set_state(*init)
+            h.synchronize()
             barrier()
-
-        gn_step(solver_handle)   # first iteration includes the one-time factorization analysis
-        restart()
-        tg = time.perf_counter()
-        stats = [gn_step(solver_handle) for _ in range(args.gn_steps)]
-        barrier()
-        gn_wall = max_over_ranks(time.perf_counter() - tg)
+            h.synchronize()
+            t0 = time.perf_counter()
+            stats += [gn_step(h, partition) for _ in range(n)]
+            h.synchronize()
+            barrier()
+            h.synchronize()
+            wall += max_over_ranks(time.perf_counter() - t0)
+            done += n
+        h.set_state(*init)
         assert all(g["solver_info"] == 0 for g in stats), "non-positive pivot in a benchmarked GN step"
-        ph = {k: float(np.median([g[k] for g in stats])) for k in
-              ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
-        batched, c_loop = None, None
-        if world == 1 or args.exchange == "rccl":
-            restart()
-            c_loop = 1e3 / max_over_ranks(solver_handle.time_steps(args.gn_steps))
-            restart()
-            tg = time.perf_counter()
-            last = solver_handle.step_n(args.gn_steps)
-            barrier()
-            batched = args.gn_steps / max_over_ranks(time.perf_counter() - tg)
-            assert last["solver_info"] == 0, "non-positive pivot in a benchmarked GN step"
-        restart()
-        return c_loop if c_loop else args.gn_steps / gn_wall, ph, batched, args.gn_steps / gn_wall
+        return wall, stats
 
-    gn_it_s, phase, gn_other, gn_batched, gn_python = None, None, None, None, None
-    if args.gn_steps > 0:
-        gn_it_s, phase, gn_batched, gn_python = time_gn(S)
-        if world == 1 and not args.no_gn_other:   # the other multifrontal ordering, for comparison
-            other = "supernodal" if args.solver == "schur" else "schur"
-            S2 = bos.Solver(P, precision=precision, device=local_rank,
-                            solver=bos.BOS_SOLVER_SUPERNODAL if other == "supernodal" else bos.BOS_SOLVER_SCHUR)
-            it2, ph2, b2, _ = time_gn(S2)
-            gn_other = {"solver": other, "gn_iters_per_s": it2, "gn_iters_per_s_batched": b2,
-                        "t_solve_ms": ph2["t_solve_ms"]}
-            S2.close()
+    def phases(stats):
+        return {k: float(np.median([g[k] for g in stats])) for k in
+                ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
+
+    # ---- the timed region: K GN iterations; the J+H inside them is the headline
+    wall, stats = timed_steps(S, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup)
+    phase = phases(stats)
+    jh_ms = max_over_ranks(phase["t_linearize_ms"])      # the slowest rank's in-step J+H
+    gn_it_s = args.steps / wall
+    log(f"rank {rank}: {args.steps} GN steps in {wall * 1e3:.1f} ms ({gn_it_s:.0f} it/s); phases {phase}")
+
+    # ---- other GN loops (the headline's timed region above is the reference for value)
+    gn_c_loop, gn_batched = None, None
+    init = S.get_state()
+    if world == 1 or args.exchange == "rccl":
+        gn_c_loop = 1e3 / max_over_ranks(S.time_steps(min(args.steps, 50)))   # bos_step in a C loop
+        S.set_state(*init)
+        barrier()
+        tg = time.perf_counter()
+        last = S.step_n(args.batch)                       # executables/bearing_only_slam.cpp:95-98
+        S.synchronize()
+        barrier()
+        gn_batched = args.batch / max_over_ranks(time.perf_counter() - tg)
+        assert last["solver_info"] == 0, "non-positive pivot in a benchmarked GN step"
+        S.set_state(*init)
+
+    # ---- the J+H alone: back to back (warm replay) and from cold caches (events)
+    barrier()
+    replay_ms = S.time_linearize(args.replay_steps) if args.replay_steps > 0 else None
+    cold_ms = S.time_linearize(args.cold_steps, flush_caches=True) if args.cold_steps > 0 else None
+    replay_ms = max_over_ranks(replay_ms) if replay_ms else None
+    cold_ms = max_over_ranks(cold_ms) if cold_ms else None
+
+    gn_other = None
+    if world == 1 and not args.no_gn_other and args.steps > 0:   # the other multifrontal ordering
+        other = "supernodal" if args.solver == "schur" else "schur"
+        S2 = bos.Solver(P, precision=precision, device=local_rank,
+                        solver=bos.BOS_SOLVER_SUPERNODAL if other == "supernodal" else bos.BOS_SOLVER_SCHUR)
+        w2, st2 = timed_steps(S2, bos.BOS_PARTITION_SUBTREE, min(args.steps, 50), 1)
+        gn_other = {"solver": other, "gn_iters_per_s": min(args.steps, 50) / w2, "t_solve_ms": phases(st2)["t_solve_ms"]}
+        S2.close()
+
+    # ---- N > 1: the north star's partition (observations by measurement order, all-reduce of H, b)
+    part_obs = None
+    if world > 1 and not args.no_partition_other:
+        S3, _, seen3 = make_handle(bos.BOS_PARTITION_OBSERVATIONS)
+        w3, st3 = timed_steps(S3, bos.BOS_PARTITION_OBSERVATIONS, args.steps, args.warmup)
+        ph3 = phases(st3)
+        jh3 = max_over_ranks(ph3["t_linearize_ms"])
+        ex3 = max_over_ranks(ph3["t_exchange_ms"])
+        part_obs = {"partition": "observations (measurement-order lane ranges, one all-reduce of (H, b) per "
+                                 "iteration, solve replicated)",
+                    "ranks_seen": seen3, "gn_iters_per_s": args.steps / w3, "gn_phase_ms": ph3,
+                    "jh_ms_max_rank": jh3, "jh_obs_per_s": nobs / (jh3 * 1e-3) if jh3 > 0 else None,
+                    "jh_plus_allreduce_obs_per_s": nobs / ((jh3 + ex3) * 1e-3) if jh3 + ex3 > 0 else None,
+                    "allreduce_bytes": int(info["num_block_values"] + 3 * P.NP + 2 * P.NL) *
+                    (4 if precision == bos.BOS_FP32 else 8)}
+        S3.close()
 
     # ---- landmark triangulation on the device (slam/triangulation.cpp:65-74), config 3 (run last:
     # it re-estimates the landmarks of S)
@@ -355,20 +465,20 @@ def main():
             return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
                     "traffic": traffic.get("warm" if label == "warm" else "cold") if traffic else None,
                     "algorithmic_bytes_per_launch": algo, "kernel_ms": ms, "caches": label, "timing": timing}
-        instep = phase["t_linearize_ms"] if phase else None
-        r_instep = roof(instep, "in-step", "median over the timed GN steps of the device realtime clock from the "
-                        "J+H launch's start to the next launch's start (stamped by the step's kernels)") if instep else None
+        r_instep = roof(jh_ms, "in-step", "median over the timed GN steps of the device realtime clock from the "
+                        "J+H launch's start to the next launch's start (stamped by the step's kernels); max over ranks")
         r_cold = roof(cold_ms, "cold", "HIP events around each build, 512 MiB read before it (event cost included)") \
             if cold_ms else None
-        r_warm = roof(kernel_ms, "warm", "HIP events around the back-to-back builds")
+        r_warm = roof(replay_ms, "warm", "HIP events around the back-to-back builds") if replay_ms else None
+        value = nobs / (jh_ms * 1e-3)
         line = {
             "metric": METRIC,
             "value": value,
             "unit": "obs/s",
-            "n_gpus": world,
+            "n_gpus": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
+            "ms_per_step": jh_ms,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -377,23 +487,27 @@ def main():
             "config": {
                 "workload": "config 3: synthetic 100k poses / 200k landmarks / 1M bearings / 99999 odometry "
                             "edges; J+H build " + ("fp32" if precision == bos.BOS_FP32 else "fp64") +
-                            " (solve fp64, " + args.solver + ")",
+                            " inside full GN iterations (solve fp64, " + args.solver + ")",
                 "poses": P.NP, "landmarks": P.NL, "bearings": int(len(P.b_z)), "odometry": int(len(P.o_z)),
                 "parallelism": (f"subtree-sharded x{world} ({'RCCL' if args.exchange == 'rccl' else 'gloo rehearsal'} "
                                 f"all-gathers; top fronts replicated: {info['top_fronts']})") if world > 1 else "single GPU",
             },
+            "ranks_seen": ranks_seen,
+            "devices": 1 if (args.same_device or world == 1) else world,
+            "timed_region_ms": wall * 1e3,
             "gn_iters_per_s": gn_it_s,
+            "gn_iters_per_s_c_loop": gn_c_loop,
             "gn_iters_per_s_batched": gn_batched,
-            "gn_iters_per_s_python": gn_python,
             "gn_phase_ms": phase,
-            "solver_model": solver_model(P, phase, world) if phase else None,
+            "solver_model": solver_model(P, phase, world),
             "gn_solver": args.solver,
             "gn_other": gn_other,
+            "partition_observations": part_obs,
             "triangulation": tri,
-            # the J+H as it runs inside the GN iteration (inputs from HBM after the solver's stream)
-            # first; the same from cold caches by events, and the back-to-back replay (working set
-            # partly served by the Infinity Cache), beside it
-            "roofline": r_instep or r_cold or r_warm,
+            # the J+H as it runs inside the GN iteration (inputs from HBM after the solver's stream);
+            # the same from cold caches by events, and the back-to-back replay (working set partly
+            # cache resident), beside it
+            "roofline": r_instep,
             "roofline_cold_events": r_cold,
             "roofline_warm_replay": r_warm,
         }
@@ -402,8 +516,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(P, precision, cpus)
             line["cpu_baseline_gn"] = cpu_gn_baseline(P, cpus)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
-            if gn_it_s:
-                line["gn_speedup_vs_cpu"] = gn_it_s / line["cpu_baseline_gn"]["value"]
+            line["gn_speedup_vs_cpu"] = gn_it_s / line["cpu_baseline_gn"]["value"]
         print(json.dumps(line), flush=True)
     S.close()
     if world > 1:

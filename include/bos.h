@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define BOS_ABI_VERSION 2
+#define BOS_ABI_VERSION 3
 
 /* status codes */
 #define BOS_OK 0
@@ -47,6 +47,14 @@ extern "C" {
 #define BOS_SOLVER_SCHUR 3        /* same GPU engine, landmarks eliminated first (default): the pose fronts
                                      factor the Schur complement S = H_pp - H_pl H_ll^-1 H_lp (config 5) */
 #define BOS_SOLVER_SPARSE_CHOL BOS_SOLVER_SCHUR
+
+/* how a world_size > 1 step is split over the ranks */
+#define BOS_PARTITION_SUBTREE 0       /* default: per-rank subtrees of the Schur assembly tree below a
+                                         replicated top; a rank builds only the H its fronts read, two
+                                         all-gathers per iteration (subtree roots' updates, boundary x) */
+#define BOS_PARTITION_OBSERVATIONS 1  /* BASELINE north star: the J+H lanes (observations in measurement
+                                         order) split into contiguous ranges, one all-reduce (sum) of the
+                                         whole (H, b) per iteration, the solve and update replicated */
 
 /*
  * Problem in stix order (framework/state.hpp:47-53): poses in file order, landmarks in
@@ -87,6 +95,12 @@ typedef struct bos_options {
     double kernel_threshold;        /* robust kernel threshold, reference default 1.0 (:16)      */
     double damping;                 /* damping factor, reference default 0.01 (:17)              */
     void* stream;                   /* hipStream_t to launch on, NULL = the handle's own stream  */
+    int32_t partition;              /* BOS_PARTITION_SUBTREE (default) / _OBSERVATIONS (world_size > 1) */
+    int32_t lanes_per_pose;         /* J+H lanes per pose: 0 = the plan's choice, else 1, 2 or 4   */
+    int32_t schur_leaf;             /* poses per nested-dissection leaf of the Schur ordering: 0 = the
+                                       default (10); larger leaves give fronts over 64 rows, which run
+                                       on the workgroup kernels (a planning option: the arithmetic of
+                                       a front is the same)                                         */
 } bos_options;
 
 /* Per-iteration statistics (the reference prints nothing; step() returns void). */
@@ -97,7 +111,8 @@ typedef struct bos_step_stats {
                                        (reported and continued, like the reference's NumericalIssue
                                        message, slam/solver.cpp:82-84)                            */
     double max_abs_dx;              /* max |dx| of the applied update (NaN if the update was not finite) */
-    double t_linearize_ms;          /* J+H build only (the exchange is t_exchange_ms), hipEvent timed */
+    double t_linearize_ms;          /* J+H build only (the exchange is t_exchange_ms), timed on the
+                                       device by the step's own kernels (realtime clock stamps)     */
     double t_exchange_ms;           /* RCCL exchange part (0 on one GPU)                         */
     double t_solve_ms;              /* factorization + triangular solves                         */
     double t_update_ms;             /* box-plus                                                  */
@@ -115,6 +130,8 @@ typedef struct bos_system_info {
     int32_t landmark_lanes;         /* J+H landmark lanes this rank runs                         */
     int32_t own_fronts;             /* multifrontal fronts of this rank's subtrees               */
     int32_t top_fronts;             /* fronts of the replicated top (0 on one GPU)               */
+    int32_t comm_ranks;             /* ranks the RCCL communicator holds (ncclCommCount), 0 without one */
+    int32_t partition;              /* BOS_PARTITION_* of a sharded handle                       */
 } bos_system_info;
 
 void bos_default_options(bos_options* opt);
@@ -160,6 +177,11 @@ int bos_system_info_get(const struct bos_solver* s, bos_system_info* info);
  */
 int bos_export_system(const struct bos_solver* s, int64_t capacity, int32_t* rows, int32_t* cols, double* vals,
                       double* b);
+/* On sharded handles (world_size > 1, or a communicator) bos_linearize is BOS_ERR_UNSUPPORTED (a
+ * rank builds only part of H); bos_export_system and bos_get_last_dx are supported with
+ * BOS_PARTITION_OBSERVATIONS after a step (every rank holds the all-reduced system and the whole
+ * dx) and BOS_ERR_UNSUPPORTED with BOS_PARTITION_SUBTREE (a rank holds H and x of its own, top and
+ * boundary nodes only). */
 /*
  * Multi-GPU (one process per GPU, world_size > 1, BOS_SOLVER_SCHUR / _SUPERNODAL). The sparse
  * Cholesky's assembly tree is cut into per-rank subtrees below a replicated top; each rank builds
@@ -172,6 +194,12 @@ int bos_export_system(const struct bos_solver* s, int64_t capacity, int32_t* row
  *   bos_step_phase(s, 2, stats)   (synchronous, like bos_step).
  * After a step a rank's state is current on the nodes it owns, the top and the boundary nodes
  * (bos_node_owner: owning rank per node, -1 top, -2 fixed pose); merge per owner for the full state.
+ *
+ * BOS_PARTITION_OBSERVATIONS (the north star's form): phase 0 is rank r's range of J+H lanes, the one
+ * exchange is an all-reduce (sum) of every rank's exchange-1 buffer (its chi^2 partials and its
+ * (H, b) values, zero outside its range; bos_exchange_upload then takes the element-wise SUM, one
+ * rank's size, not the concatenation), phase 1 runs the solve and the box-plus of every node and
+ * returns the stats (phase 2 does not exist). Every rank then holds the whole state.
  */
 int bos_step_phase(struct bos_solver* s, int32_t phase, bos_step_stats* stats);
 int bos_exchange_size(const struct bos_solver* s, int32_t which, int64_t* doubles_per_rank);

@@ -67,24 +67,26 @@ typedef struct bos_plan_info {
     int64_t shard_update_nodes;     /* nodes the box-plus updates (own, top, boundary)             */
 } bos_plan_info;
 
-/* Build the static plan on the host (what bos_create does before touching the GPU) for solver
- * `solver` (BOS_SOLVER_*: it selects the ordering).
+/* Build the static plan on the host (what bos_create does before touching the GPU) with the
+ * planning fields of `options` (NULL = bos_default_options): solver (BOS_SOLVER_*: it selects the
+ * ordering), partition, lanes_per_pose, schur_leaf; its rank / world_size are ignored (the
+ * arguments below give them).
  * If ref_rows/ref_cols/owned are given (capacity >= nnz_lower) they receive, for every stored
  * entry of the lower triangle of H_nf, its (row, col) in the reference dof numbering
  * (row >= col) and whether rank `rank` of `world` computes it (its J+H lanes write the block);
  * b_owned (n + 3 entries, indexed by reference dof) marks the b entries its lanes write;
  * perm_to_ref (n + 3 entries) maps the permuted dof order used on the device to reference dofs. */
-int bos_plan_inspect(const bos_problem* problem, int32_t solver, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
+int bos_plan_inspect(const bos_problem* problem, const bos_options* options, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
                      int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref, bos_plan_info* info);
 
 /* Test hook: the GPU multifrontal algorithm re-run on the host with the plan's tree and maps
- * (solver BOS_SOLVER_SUPERNODAL or _SCHUR; vals in the plan's CSR order, rhs/x in its permuted
+ * (options->solver BOS_SOLVER_SUPERNODAL or _SCHUR; vals in the plan's CSR order, rhs/x in its permuted
  * dof order). Not used by any solve. */
-int bos_plan_mf_selftest(const bos_problem* problem, int32_t solver, const double* vals, const double* rhs, double* x);
+int bos_plan_mf_selftest(const bos_problem* problem, const bos_options* options, const double* vals, const double* rhs, double* x);
 
 /* Owner of every node (NP poses, then NL landmarks) when the multifrontal solve is sharded over
  * `world` ranks: the rank, -1 for the replicated top, -2 for the fixed pose. */
-int bos_plan_node_owner(const bos_problem* problem, int32_t solver, int32_t world, int32_t* owner);
+int bos_plan_node_owner(const bos_problem* problem, const bos_options* options, int32_t world, int32_t* owner);
 
 /* Test hook: the sharded GN solve (plan.hpp Shard) simulated on the host for all `world` ranks,
  * both exchanges included: per-rank plans, each rank's J+H outputs only, subtree factorization,
@@ -92,7 +94,7 @@ int bos_plan_node_owner(const bos_problem* problem, int32_t solver, int32_t worl
  * order, n) equals the one-rank solution bit for bit, the ranks agree on the top, every observation's
  * chi^2 is counted by one rank and every node a rank's J+H reads is kept current by its box-plus.
  * vals / rhs as for bos_plan_mf_selftest. */
-int bos_plan_shard_selftest(const bos_problem* problem, int32_t solver, int32_t world, const double* vals,
+int bos_plan_shard_selftest(const bos_problem* problem, const bos_options* options, int32_t world, const double* vals,
                             const double* rhs, double* x);
 
 /* CPU baseline of bench.py (the build's own C++ CPU backend on the host's cores):
@@ -118,10 +120,8 @@ int bos_time_linearize(struct bos_solver* s, int32_t n, int32_t flush_caches, do
 int bos_time_triangulate(struct bos_solver* s, int32_t n, double* ms_per_call);
 int bos_time_steps(struct bos_solver* s, int32_t n, double* ms_per_step);
 
-/* Test hooks (process-wide, default 0 = product behaviour; not part of the drop-in boundary):
- * poses per nested-dissection leaf of the Schur ordering (forces the plan fallback when large),
- * and the line-by-line g2o parser instead of the chunked one (the tests prove them identical). */
-void bos_debug_set_schur_leaf(int32_t poses);
+/* Test hook (process-wide, default 0 = product behaviour; not part of the drop-in boundary): the
+ * line-by-line g2o parser instead of the chunked one (the tests prove them identical). */
 void bos_debug_set_g2o_parser(int32_t line_by_line);
 /* Test hook: the next bos_step's factor dataflow launch skips its first front, so a dependency
  * wait times out — bos_step must then fail with BOS_ERR_SOLVER and leave the state untouched.

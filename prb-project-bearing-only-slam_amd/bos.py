@@ -30,6 +30,9 @@ BOS_SOLVER_DENSE_CHOL = 1
 BOS_SOLVER_ROCSOLVER_RF = 2
 BOS_SOLVER_SCHUR = 3
 BOS_SOLVER_SPARSE_CHOL = BOS_SOLVER_SCHUR
+BOS_PARTITION_SUBTREE = 0
+BOS_PARTITION_OBSERVATIONS = 1
+ABI_VERSION = 3
 
 # every symbol declared in include/bos.h and include/bos_host.h
 EXPORTED_SYMBOLS = [
@@ -43,7 +46,7 @@ EXPORTED_SYMBOLS = [
     "bos_debug_linearize_timeline", "bos_triangulate", "bos_triangulate_async", "bos_plan_shard_selftest",
     "bos_plan_node_owner", "bos_step_phase", "bos_exchange_size", "bos_exchange_download", "bos_exchange_upload",
     "bos_node_owner",
-    "bos_debug_set_schur_leaf", "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph", "bos_debug_solver_stamps",
+    "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph", "bos_debug_solver_stamps",
     "bos_time_linearize", "bos_time_triangulate", "bos_time_steps", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
     "bos_cpu_gn_destroy",
 ]
@@ -67,7 +70,8 @@ class bos_problem(ctypes.Structure):
 class bos_options(ctypes.Structure):
     _fields_ = [("precision", ctypes.c_int32), ("solver", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32), ("nccl_unique_id", ctypes.c_void_p),
-                ("kernel_threshold", ctypes.c_double), ("damping", ctypes.c_double), ("stream", ctypes.c_void_p)]
+                ("kernel_threshold", ctypes.c_double), ("damping", ctypes.c_double), ("stream", ctypes.c_void_p),
+                ("partition", ctypes.c_int32), ("lanes_per_pose", ctypes.c_int32), ("schur_leaf", ctypes.c_int32)]
 
 
 class bos_step_stats(ctypes.Structure):
@@ -83,7 +87,8 @@ class bos_system_info(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("nnz_lower", ctypes.c_int64), ("nnz_factor", ctypes.c_int64),
                 ("algorithmic_bytes", ctypes.c_int64), ("num_block_values", ctypes.c_int64),
                 ("lanes_per_pose", ctypes.c_int32), ("pose_lane_groups", ctypes.c_int32),
-                ("landmark_lanes", ctypes.c_int32), ("own_fronts", ctypes.c_int32), ("top_fronts", ctypes.c_int32)]
+                ("landmark_lanes", ctypes.c_int32), ("own_fronts", ctypes.c_int32), ("top_fronts", ctypes.c_int32),
+                ("comm_ranks", ctypes.c_int32), ("partition", ctypes.c_int32)]
 
 
 class bos_plan_info(ctypes.Structure):
@@ -148,19 +153,18 @@ def lib():
         "bos_dataset_ground_truth": (ctypes.c_int, [vp, ctypes.POINTER(_dp), ctypes.POINTER(_dp)]),
         "bos_dataset_write_g2o": (ctypes.c_int, [vp, ctypes.c_char_p, _dp, _dp, ctypes.c_int]),
         "bos_dataset_free": (None, [vp]),
-        "bos_plan_inspect": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                            ctypes.c_int64, _ip, _ip, ctypes.POINTER(ctypes.c_uint8),
+        "bos_plan_inspect": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options), ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int64, _ip, _ip, ctypes.POINTER(ctypes.c_uint8),
                                             ctypes.POINTER(ctypes.c_uint8), _ip, ctypes.POINTER(bos_plan_info)]),
-        "bos_plan_mf_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, _dp, _dp, _dp]),
-        "bos_plan_shard_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32, _dp,
-                                                   _dp, _dp]),
-        "bos_plan_node_owner": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.c_int32, ctypes.c_int32, _ip]),
+        "bos_plan_mf_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options), _dp, _dp, _dp]),
+        "bos_plan_shard_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options), ctypes.c_int32,
+                                                   _dp, _dp, _dp]),
+        "bos_plan_node_owner": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options), ctypes.c_int32, _ip]),
         "bos_step_phase": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.POINTER(bos_step_stats)]),
         "bos_exchange_size": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
         "bos_exchange_download": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
         "bos_exchange_upload": (ctypes.c_int, [vp, ctypes.c_int32, _dp]),
         "bos_node_owner": (ctypes.c_int, [vp, _ip]),
-        "bos_debug_set_schur_leaf": (None, [ctypes.c_int32]),
         "bos_debug_set_g2o_parser": (None, [ctypes.c_int32]),
         "bos_debug_inject_stall": (ctypes.c_int, [vp]),
         "bos_debug_set_step_graph": (ctypes.c_int, [vp, ctypes.c_int32]),
@@ -312,14 +316,25 @@ def write_g2o(P: Problem, path: str, pose_xyt=None, lm_xy=None, with_landmarks=T
         L.bos_dataset_free(h)
 
 
+def options(solver: int = BOS_SOLVER_SUPERNODAL, partition: int = BOS_PARTITION_SUBTREE, lanes_per_pose: int = 0,
+            schur_leaf: int = 0, precision: int = BOS_FP64) -> bos_options:
+    """bos_options with the planning fields set (bos_default_options for the rest)."""
+    o = bos_options()
+    lib().bos_default_options(ctypes.byref(o))
+    o.solver, o.partition, o.lanes_per_pose, o.schur_leaf, o.precision = solver, partition, lanes_per_pose, schur_leaf, precision
+    return o
+
+
 def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = False,
-                 solver: int = BOS_SOLVER_SUPERNODAL):
+                 solver: int = BOS_SOLVER_SUPERNODAL, partition: int = BOS_PARTITION_SUBTREE, lanes_per_pose: int = 0,
+                 schur_leaf: int = 0):
     """Host-only plan build (ordering, CSR layout, shard ownership) — no GPU needed."""
     L = lib()
     cs = P.c_struct()
     info = bos_plan_info()
-    _check(L.bos_plan_inspect(ctypes.byref(cs), solver, rank, world, 0, None, None, None, None, None, ctypes.byref(info)),
-           "plan_inspect")
+    opt = options(solver, partition, lanes_per_pose, schur_leaf)
+    _check(L.bos_plan_inspect(ctypes.byref(cs), ctypes.byref(opt), rank, world, 0, None, None, None, None, None,
+                              ctypes.byref(info)), "plan_inspect")
     out = {"n": info.n, "nnz_lower": info.nnz_lower, "nnz_factor": info.nnz_factor,
            "num_block_values": info.num_block_values, "lanes_per_pose": info.lanes_per_pose,
            "flops_temporal": info.flops_temporal, "flops_nested_dissection": info.flops_nested_dissection,
@@ -335,21 +350,22 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
         owned = np.zeros(nnz, dtype=np.uint8)
         b_owned = np.zeros(P.N, dtype=np.uint8)
         perm = np.zeros(P.N, dtype=np.int32)
-        _check(L.bos_plan_inspect(ctypes.byref(cs), solver, rank, world, nnz, _ptr(rows, ctypes.c_int32),
+        _check(L.bos_plan_inspect(ctypes.byref(cs), ctypes.byref(opt), rank, world, nnz, _ptr(rows, ctypes.c_int32),
                                   _ptr(cols, ctypes.c_int32), _ptr(owned, ctypes.c_uint8),
                                   _ptr(b_owned, ctypes.c_uint8), _ptr(perm, ctypes.c_int32), None), "plan_inspect")
         out.update(rows=rows, cols=cols, owned=owned.astype(bool), b_owned=b_owned.astype(bool), perm_to_ref=perm)
     return out
 
 
-def plan_mf_selftest(P: Problem, vals, rhs, solver: int = BOS_SOLVER_SUPERNODAL):
+def plan_mf_selftest(P: Problem, vals, rhs, solver: int = BOS_SOLVER_SUPERNODAL, schur_leaf: int = 0):
     """Host re-run of the GPU multifrontal algorithm on the plan's tree (test hook)."""
     cs = P.c_struct()
     v = np.ascontiguousarray(vals, dtype=np.float64)
     b = np.ascontiguousarray(rhs, dtype=np.float64)
     x = np.zeros_like(b)
-    _check(lib().bos_plan_mf_selftest(ctypes.byref(cs), solver, _ptr(v, ctypes.c_double), _ptr(b, ctypes.c_double),
-                                      _ptr(x, ctypes.c_double)), "plan_mf_selftest")
+    opt = options(solver, schur_leaf=schur_leaf)
+    _check(lib().bos_plan_mf_selftest(ctypes.byref(cs), ctypes.byref(opt), _ptr(v, ctypes.c_double),
+                                      _ptr(b, ctypes.c_double), _ptr(x, ctypes.c_double)), "plan_mf_selftest")
     return x
 
 
@@ -361,7 +377,8 @@ def plan_shard_selftest(P: Problem, world: int, vals, rhs, solver: int = BOS_SOL
     v = np.ascontiguousarray(vals, dtype=np.float64)
     b = np.ascontiguousarray(rhs, dtype=np.float64)
     x = np.zeros_like(b)
-    _check(lib().bos_plan_shard_selftest(ctypes.byref(cs), solver, world, _ptr(v, ctypes.c_double),
+    opt = options(solver)
+    _check(lib().bos_plan_shard_selftest(ctypes.byref(cs), ctypes.byref(opt), world, _ptr(v, ctypes.c_double),
                                          _ptr(b, ctypes.c_double), _ptr(x, ctypes.c_double)), "plan_shard_selftest")
     return x
 
@@ -370,7 +387,9 @@ def plan_node_owner(P: Problem, world: int, solver: int = BOS_SOLVER_SCHUR) -> n
     """Owner rank of every node (poses, then landmarks) of a `world`-rank shard; -1 top, -2 fixed pose."""
     cs = P.c_struct()
     o = np.zeros(P.NP + P.NL, dtype=np.int32)
-    _check(lib().bos_plan_node_owner(ctypes.byref(cs), solver, world, _ptr(o, ctypes.c_int32)), "plan_node_owner")
+    opt = options(solver)
+    _check(lib().bos_plan_node_owner(ctypes.byref(cs), ctypes.byref(opt), world, _ptr(o, ctypes.c_int32)),
+           "plan_node_owner")
     return o
 
 
@@ -419,9 +438,11 @@ class Solver:
 
     def __init__(self, P: Problem, precision: int = BOS_FP64, solver: int = BOS_SOLVER_SPARSE_CHOL,
                  device: int = -1, kernel_threshold: float = 1.0, damping: float = 0.01, stream: int = 0,
-                 rank: int = 0, world_size: int = 1, nccl_id: Optional[bytes] = None, triangulate: bool = False):
+                 rank: int = 0, world_size: int = 1, nccl_id: Optional[bytes] = None, triangulate: bool = False,
+                 partition: int = BOS_PARTITION_SUBTREE, lanes_per_pose: int = 0, schur_leaf: int = 0):
         """triangulate=True: ignore P.lm_xy and triangulate the landmarks on the device from the
-        initial poses (bos_problem.landmark_xy = NULL)."""
+        initial poses (bos_problem.landmark_xy = NULL). partition / lanes_per_pose / schur_leaf: the
+        bos_options fields of the same names."""
         L = lib()
         self.P = P
         opt = bos_options()
@@ -430,6 +451,7 @@ class Solver:
         opt.kernel_threshold, opt.damping = kernel_threshold, damping
         opt.stream = stream or None
         opt.rank, opt.world_size = rank, world_size
+        opt.partition, opt.lanes_per_pose, opt.schur_leaf = partition, lanes_per_pose, schur_leaf
         self._nid = None
         if nccl_id is not None:
             self._nid = ctypes.create_string_buffer(nccl_id, len(nccl_id))
@@ -509,6 +531,8 @@ class Solver:
         return out
 
     def exchange_upload(self, which: int, all_ranks: np.ndarray):
+        """Subtree partition: every rank's buffer concatenated in rank order (all-gather);
+        observations partition: the element-wise sum over the ranks (all-reduce)."""
         a = np.ascontiguousarray(all_ranks, dtype=np.float64)
         _check(lib().bos_exchange_upload(self._h, which, _ptr(a, ctypes.c_double)), "bos_exchange_upload")
 

@@ -375,9 +375,11 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t s0, int64_t
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams<T> P) {
     const int64_t nb = gridDim.x;
-    // pose blocks first, then landmark blocks, each range in XCD-contiguous order
-    const int64_t b = blockIdx.x < P.pose_blocks ? xcd_contiguous(blockIdx.x, 0, P.pose_blocks)
-                                                 : xcd_contiguous(blockIdx.x, P.pose_blocks, nb);
+    // pose blocks first, then landmark blocks, each range in XCD-contiguous order; b numbers the
+    // blocks of the whole build (pose blocks, then landmark blocks from pose_blocks on)
+    const int64_t b = blockIdx.x < P.n_pose_run
+                          ? P.pose_b0 + xcd_contiguous(blockIdx.x, 0, P.n_pose_run)
+                          : P.pose_blocks + P.lm_b0 + xcd_contiguous(blockIdx.x, P.n_pose_run, nb) - P.n_pose_run;
     unsigned long long st[3] = {0, 0, 0};
     if (P.t_start && blockIdx.x == 0 && threadIdx.x == 0) *P.t_start = __builtin_amdgcn_s_memrealtime();
     stamp(P.diag_stamps, st, 0);
@@ -474,7 +476,12 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
     double c = 0.0, m = 0.0;
     long long r = 0;
     const int32_t inf = info && threadIdx.x == 0 ? *info : 0;   // loaded with the partials
-    for (int i = threadIdx.x; i < n; i += blockDim.x) { c += chi_part[i]; r += nrob_part[i]; }
+    if (nrob_part) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) { c += chi_part[i]; r += nrob_part[i]; }
+    } else if (threadIdx.x == 0) {   // an all-reduced header
+        c = chi_part[0];
+        r = (long long)chi_part[1];
+    }
     if (max_part)
         for (int i = threadIdx.x; i < n_max; i += blockDim.x) m = nan_max(m, max_part[i]);
     sc[threadIdx.x] = c;
@@ -506,7 +513,7 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
             mirror->n_robust = v.n_robust;
             mirror->info = v.info;
             mirror->aborted = v.aborted;
-            for (int k = 0; k < 4; ++k) mirror->stamp[k] = v.stamp[k];
+            for (int k = 0; k < 6; ++k) mirror->stamp[k] = v.stamp[k];
             __threadfence_system();
             __hip_atomic_store(&mirror->seq, v.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -605,7 +612,7 @@ __global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* seg
 }
 
 __global__ __launch_bounds__(256) void shard_header1_kernel(const double* chi_part, const int32_t* nrob_part, int n,
-                                                           double* send1) {
+                                                           double* send1, unsigned long long* stamp) {
     __shared__ double sc[256];
     __shared__ long long sr[256];
     double c = 0.0;
@@ -618,7 +625,11 @@ __global__ __launch_bounds__(256) void shard_header1_kernel(const double* chi_pa
         if ((int)threadIdx.x < o) { sc[threadIdx.x] += sc[threadIdx.x + o]; sr[threadIdx.x] += sr[threadIdx.x + o]; }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { send1[0] = sc[0]; send1[1] = (double)sr[0]; }
+    if (threadIdx.x == 0) {
+        send1[0] = sc[0];
+        send1[1] = (double)sr[0];
+        if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // per-block max |x| over the dofs of a node list (poses 3 dofs, landmarks 2)
@@ -694,6 +705,11 @@ template <typename T> __global__ void to_f64_kernel(const T* in, double* out, in
         out[i] = (double)in[i];
 }
 
+template <typename T> __global__ void from_f64_kernel(const double* in, T* out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (T)in[i];
+}
+
 template <typename T>
 __global__ void gather_f64_kernel(const T* in, const int32_t* idx, double* out, int64_t n, unsigned long long* stamp,
                                   uint32_t* epoch, const T* cin, double* cout, int64_t cn) {
@@ -732,7 +748,10 @@ __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colin
 template <typename T, bool W, bool D, int LPP, int MINW>
 hipError_t launch_lin_k(LinParams<T> p, hipStream_t s) {
     const int lm_blocks = (p.n_lm_lanes + kBlock - 1) / kBlock;
-    const int grid = p.pose_blocks + lm_blocks;
+    if (p.pose_b0 < 0 || p.n_pose_run < 0 || p.pose_b0 + p.n_pose_run > p.pose_blocks || p.lm_b0 < 0 || p.n_lm_run < 0 ||
+        p.lm_b0 + p.n_lm_run > lm_blocks)
+        return hipErrorInvalidValue;   // a block range outside the build (checked before any launch)
+    const int grid = p.n_pose_run + p.n_lm_run;
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((linearize_kernel<T, W, D, LPP, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
     return hipGetLastError();
@@ -743,6 +762,7 @@ hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, hipStream_t s) {
     switch (lpp) {
         case 1: return launch_lin_k<T, W, D, 1, MINW>(p, s);
         case 2: return launch_lin_k<T, W, D, 2, MINW>(p, s);
+        case 4: return launch_lin_k<T, W, D, 4, MINW>(p, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -790,8 +810,8 @@ hipError_t launch_reduce_stats(const double* chi_part, const int32_t* nrob_part,
 }
 
 hipError_t launch_shard_header1(const double* chi_part, const int32_t* nrob_part, int n_parts, double* send1,
-                                hipStream_t s) {
-    hipLaunchKernelGGL(shard_header1_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n_parts, send1);
+                                hipStream_t s, unsigned long long* stamp) {
+    hipLaunchKernelGGL(shard_header1_kernel, dim3(1), dim3(256), 0, s, chi_part, nrob_part, n_parts, send1, stamp);
     return hipGetLastError();
 }
 
@@ -833,6 +853,13 @@ template <typename T> hipError_t launch_to_f64(const T* in, double* out, int64_t
     return hipGetLastError();
 }
 
+template <typename T> hipError_t launch_from_f64(const double* in, T* out, int64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL((from_f64_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, in, out, n);
+    return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
                              unsigned long long* stamp, uint32_t* epoch, const T* cin, double* cout, int64_t cn) {
@@ -861,6 +888,8 @@ template hipError_t launch_seg_copy<float>(float*, float*, float*, float*, const
 template hipError_t launch_triangulate<float>(const TriParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);
+template hipError_t launch_from_f64<double>(const double*, double*, int64_t, hipStream_t);
+template hipError_t launch_from_f64<float>(const double*, float*, int64_t, hipStream_t);
 template hipError_t launch_gather_f64<double>(const double*, const int32_t*, double*, int64_t, hipStream_t,
                                               unsigned long long*, uint32_t*, const double*, double*, int64_t);
 template hipError_t launch_gather_f64<float>(const float*, const int32_t*, double*, int64_t, hipStream_t,

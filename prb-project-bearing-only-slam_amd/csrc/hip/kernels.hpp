@@ -32,6 +32,9 @@ template <typename T> struct LinParams {
     int NP;
     const int32_t* lane_pose;  // [n_groups] pose of each lane group, -1 = padding; null: group i = pose i
     int n_groups, n_lm_lanes, pose_blocks;
+    // the blocks this launch runs: pose blocks [pose_b0, pose_b0 + n_pose_run), landmark blocks
+    // [lm_b0, lm_b0 + n_lm_run) (everything on one GPU; a range of each with BOS_PARTITION_OBSERVATIONS)
+    int pose_b0, n_pose_run, lm_b0, n_lm_run;
     // pose lanes
     const int32_t* pw_base;   // [waves + 1]
     const int32_t* pw_stride; // [waves]
@@ -96,8 +99,9 @@ struct StepStatus {
     int32_t aborted;  // sticky: kStepAbort once any step aborted; the host clears it when it reports it
     int32_t seq;      // steps summarised so far (reduce_stats); written to the host mirror last
     // phase boundaries of the last step, realtime clock (100 MHz): J+H start, J+H end / solve start,
-    // solve end / update start, step end (written by the step's own kernels: no events in the step)
-    unsigned long long stamp[4];
+    // solve end / update start, step end (written by the step's own kernels: no events in the step);
+    // BOS_PARTITION_OBSERVATIONS: [1] = J+H end (before the all-reduce), [4] = solve start (after it)
+    unsigned long long stamp[6];
 };
 constexpr double kStampMs = 1e-5;   // one realtime tick in ms
 
@@ -134,9 +138,13 @@ template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStr
 
 // Sharded GN step (host/plan.hpp Shard, hip/solver_capi.hip). Exchange buffers are doubles with a
 // kExHeader-double header per rank.
-// Exchange 1 header: this rank's chi^2 and robust count (sums of the J+H partials [0, n_parts)).
+// Exchange 1 header: this rank's chi^2 and robust count (sums of the J+H partials [0, n_parts));
+// *stamp (if set) gets the realtime clock at its end.
 hipError_t launch_shard_header1(const double* chi_part, const int32_t* nrob_part, int n_parts, double* send1,
-                                hipStream_t s);
+                                hipStream_t s, unsigned long long* stamp = nullptr);
+// out[i] = (T)in[i]: the all-reduced exchange buffer (fp64 on the host side of the external exchange)
+// back into the system's precision (exact: the values are T values summed with zeros)
+template <typename T> hipError_t launch_from_f64(const double* in, T* out, int64_t n, hipStream_t s);
 // Exchange 2: header = max |x| over the dofs of nodes[0, n_nodes) (the rank's own and top nodes)
 // and the solver word *info (then zeroed for the next iteration); payload = x[bnd[i]].
 hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes, const int32_t* node_dof, int NP,
@@ -152,7 +160,8 @@ hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* r
                                 double chi_const, int32_t nrob_const, StepStatus* out, StepStatus* mirror,
                                 hipStream_t s);
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
-// Reduces the J+H kernel's chi^2 / robust-count partials (plus the constant terms of odometry
+// Reduces the J+H kernel's chi^2 / robust-count partials (nrob_part null: chi_part is an
+// all-reduced header [chi^2, robust count], n ignored) (plus the constant terms of odometry
 // self-loops, chi_const / nrob_const) and the box-plus max |dx| partials (when max_part is set; a NaN
 // propagates) into *out, moves *info into out->info and zeroes *info for the next iteration: one
 // launch replaces the per-step memsets and read-backs. out->aborted is sticky; out->stamp[3] gets the

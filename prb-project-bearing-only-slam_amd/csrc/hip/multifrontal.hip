@@ -484,6 +484,28 @@ __device__ __forceinline__ int next_ticket(int* ticket) {
     return __builtin_amdgcn_readfirstlane(t);
 }
 
+// Memory ordering of the in-launch hand-off (the form cdna_hip_programming.md §6 Guideline 16 and
+// MI355X_MICROARCH.md § visibility, "Valid forms", allow without an agent-scope acquire; gfx950 has
+// 8 XCDs with private L2s and per-CU L1s that other CUs' stores never refresh):
+//  (1) every handed-off byte (update matrices U, u-vectors, backward x rows) is stored sc1
+//      (stc<true>: a relaxed agent-scope atomic store = global_store ... sc1, write-through: the line
+//      leaves the XCD's L2 for the memory-side coherence point and is dropped from it);
+//  (2) every storing wave drains them (s_waitcnt vmcnt(0), publish_done) before its flag store, and
+//      the wave that stores is the wave that signals (one wave per front);
+//  (3) the flag is an agent-scope atomic store (sc1) and is polled with agent-scope atomic loads;
+//  (4) every load of handed-off bytes is an sc1 vector load to registers (ldc<true>: a relaxed
+//      agent-scope atomic load = global_load ... sc1, which bypasses the CU's L1 and reads the
+//      coherence point, never a stale L1/L2 copy), issued after the poll has seen the flag; every
+//      other load in the flow launches reads bytes no workgroup of the same launch writes (static
+//      structure, H, and L / y of earlier launches, made visible by the kernel boundary).
+// Checked in the disassembly (hipcc -S of this file): the flow kernels' loads and stores of handed-off
+// data are global_load/store_dwordx2 sc1 and global_load/store_dword sc1 (flags), no flat_ access,
+// no scalar load of handed-off data. Under (1)-(4) the acquire reduces to a compiler barrier that
+// keeps the payload loads below the poll: fence(acquire, "wavefront") (no instruction). Data of an
+// ancestor further up (a backward front reads x rows of its parent's ancestors) is covered by the
+// chain: each ancestor drained its sc1 stores before its flag, which its child observed before
+// publishing its own. The formal agent-scope acquire (buffer_inv sc1 after the poll) measured
+// costlier and bit-identical: DESIGN.md §4 (build flag BOS_MF_AGENT_ACQUIRE).
 __device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
     if (threadIdx.x == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -496,7 +518,11 @@ __device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
             __builtin_amdgcn_s_sleep(2);
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef BOS_MF_AGENT_ACQUIRE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the formal form (measurement builds only)
+#else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
     wave_sync();
 }
 
@@ -509,8 +535,9 @@ __device__ __forceinline__ void leave_flow(const Flow& f) {
 }
 
 __device__ __forceinline__ void publish_done(const Flow& f, int s) {
-    // drain this wave's sc1 stores before the flag (a workgroup-scope fence emits no vmcnt wait)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    // drain this wave's sc1 stores before the flag (see wait_done: condition (2)); the fence only
+    // keeps the compiler from sinking stores below the wait
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -7,12 +7,14 @@
 //      structure analysed once, like SimplicialLDLT::analyzePattern at solver.cpp:77-80), or
 //      rocSOLVER csrrf / dense potrf-potrs on a gathered CSR copy
 //   3. boxplus_kernel            left-multiplicative box-plus with dx = -x (state.cpp:69-80)
-// Sharded over world > 1 ranks (host/plan.hpp Shard, host/shard.cpp): the J+H runs this rank's own
-// and the top nodes' lanes, the multifrontal solve its subtrees, then (exchange 1, all-gather of
-// the subtree roots' U / u) the replicated top, the backward solves, then (exchange 2, all-gather
-// of the boundary solution) the box-plus of its own, top and boundary nodes. The exchanges run on
-// RCCL, or — external mode, no communicator — the caller moves the buffers between the phases
-// (bos_step_phase; tests on one GPU, gloo).
+// Sharded over world > 1 ranks, BOS_PARTITION_SUBTREE (host/plan.hpp Shard, host/shard.cpp): the
+// J+H runs this rank's own and the top nodes' lanes, the multifrontal solve its subtrees, then
+// (exchange 1, all-gather of the subtree roots' U / u) the replicated top, the backward solves, then
+// (exchange 2, all-gather of the boundary solution) the box-plus of its own, top and boundary nodes.
+// BOS_PARTITION_OBSERVATIONS (the north star's form): the J+H runs a contiguous range of the
+// one-GPU plan's lanes, one all-reduce (sum) of (H, b) and the chi^2 header, then the one-GPU solve
+// and box-plus on every rank. The exchanges run on RCCL, or — external mode, no communicator — the
+// caller moves the buffers between the phases (bos_step_phase; tests on one GPU, gloo).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <rocblas/rocblas.h>
@@ -114,8 +116,16 @@ struct bos_solver {
     bos::dev::StepStatus* d_status = nullptr;   // end-of-iteration summary (device)
     bos::dev::StepStatus* h_status = nullptr;   // its host-mapped mirror, written by the step's last kernel
     bos::dev::StepStatus* m_status = nullptr;   // device address of h_status
-    // sharded step (world > 1)
+    // sharded step (world > 1): BOS_PARTITION_SUBTREE (sharded) or _OBSERVATIONS (obs)
     bool sharded = false, external = false;
+    int partition = BOS_PARTITION_SUBTREE;
+    bool obs = false;
+    int64_t pose_b0 = 0, n_pose_run = 0, lm_b0 = 0, n_lm_run = 0;   // J+H blocks this rank runs
+    void* d_sys = nullptr;        // obs: the all-reduced [H values | b] (T) the solve reads
+    void* sys_val = nullptr;      // the block array and b the solve reads (d_val / d_b, or d_sys)
+    void* sys_b = nullptr;
+    int64_t vb_count = 0;         // obs: T values of [block array (even length) | b]
+    int solve_stamp = 1;          // StepStatus stamp slot the solve's first launch writes
     int32_t* lane_pose = nullptr;            // J+H pose lane groups (Shard::lane_poses)
     bool lane_identity = false;              // group i runs pose i (one GPU): the kernel skips the table
     int chi_parts = 0;                       // J+H chi^2 partial blocks this rank counts
@@ -183,6 +193,10 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.n_groups = (int)P.blk.lane_pose.size();
     p.n_lm_lanes = (int)P.blk.lm_lane_lm.size();
     p.pose_blocks = s->pose_blocks;
+    p.pose_b0 = (int)s->pose_b0;
+    p.n_pose_run = (int)s->n_pose_run;
+    p.lm_b0 = (int)s->lm_b0;
+    p.n_lm_run = (int)s->n_lm_run;
     p.pw_base = s->pw_base; p.pw_stride = s->pw_stride; p.pl_cnt = s->pl_cnt;
     p.pb_idx = s->pb_idx; p.pb_z = (const T*)s->pb_z; p.pb_w = (const T*)s->pb_w;
     p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_oth = s->po_oth; p.po_blk = s->po_blk;
@@ -286,11 +300,11 @@ int setup_shard(bos_solver* s) {
 }
 
 // chi^2 and robust count of the odometry self-loops: constant (e = -z whatever the state, their
-// Jacobian is zero, see host/plan.cpp build_layout), evaluated in T like the kernel; rank 0 adds them
+// Jacobian is zero, see host/plan.cpp build_layout), evaluated in T like the kernel. No J+H lane
+// counts them, so every rank adds them once to the step's combined (summed over ranks) chi^2.
 template <typename T> void self_loop_terms(const bos_solver* s, double& chi, int32_t& nrob) {
     chi = 0.0;
     nrob = 0;
-    if (s->rank != 0) return;
     const T kt = (T)s->kt;
     for (size_t i = 0; i < s->loop_z.size() / 3; ++i) {
         const T* z = nullptr;
@@ -316,9 +330,10 @@ int enqueue_stats(bos_solver* s, bool with_update) {
     int32_t nrob_c = 0;
     if (s->precision == BOS_FP32) self_loop_terms<float>(s, chi_c, nrob_c);
     else self_loop_terms<double>(s, chi_c, nrob_c);
-    HIP_TRY(bos::dev::launch_reduce_stats(s->d_chi_part, s->d_nrob_part, s->chi_parts, chi_c, nrob_c,
-                                          with_update ? s->d_maxpart : nullptr, nupd, info, s->d_status,
-                                          s->m_status, s->stream));
+    // observations partition: the all-reduced header [chi^2, robust count] instead of the partials
+    HIP_TRY(bos::dev::launch_reduce_stats(s->obs ? s->ex1_recv : s->d_chi_part, s->obs ? nullptr : s->d_nrob_part,
+                                          s->chi_parts, chi_c, nrob_c, with_update ? s->d_maxpart : nullptr, nupd, info,
+                                          s->d_status, s->m_status, s->stream));
     return BOS_OK;
 }
 
@@ -331,7 +346,7 @@ double self_loop_chi(const bos_solver* s, int32_t& nrob) {
 
 // the block array as the multifrontal solver reads it (fp64)
 const double* mf_matrix(const bos_solver* s) {
-    return s->precision == BOS_FP32 ? s->d_val64 : (const double*)s->d_val;
+    return s->precision == BOS_FP32 ? s->d_val64 : (const double*)s->sys_val;
 }
 
 // right-hand side in elimination order, and the fp64 copy of an fp32 block array. The gather also
@@ -339,13 +354,13 @@ const double* mf_matrix(const bos_solver* s) {
 int enqueue_solver_inputs(bos_solver* s) {
     const int64_t n = s->plan.n;
     const bool f32 = s->precision == BOS_FP32;
-    unsigned long long* stamp = s->d_status->stamp + 1;
+    unsigned long long* stamp = s->d_status->stamp + s->solve_stamp;
     uint32_t* epoch = uses_mf(s) ? bos::dev::mf_epoch_ptr(s->mf) : nullptr;
     const bool conv = f32 && uses_mf(s);   // the fp64 copy of the block array, in the same launch
-    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch,
-                                                     conv ? (const float*)s->d_val : nullptr, conv ? s->d_val64 : nullptr,
+    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->sys_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch,
+                                                     conv ? (const float*)s->sys_val : nullptr, conv ? s->d_val64 : nullptr,
                                                      conv ? s->plan.blk.size : 0)
-                : bos::dev::launch_gather_f64<double>((const double*)s->d_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch));
+                : bos::dev::launch_gather_f64<double>((const double*)s->sys_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch));
     return BOS_OK;
 }
 
@@ -363,8 +378,8 @@ int enqueue_solve(bos_solver* s, bool& ran_analysis) {
         return BOS_OK;
     }
     double* A = s->d_csr64;
-    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->d_val, s->csr_src, A, s->plan.nnzA(), s->stream)
-                : bos::dev::launch_gather_f64<double>((const double*)s->d_val, s->csr_src, A, s->plan.nnzA(), s->stream));
+    HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->sys_val, s->csr_src, A, s->plan.nnzA(), s->stream)
+                : bos::dev::launch_gather_f64<double>((const double*)s->sys_val, s->csr_src, A, s->plan.nnzA(), s->stream));
     if (s->solver_kind == BOS_SOLVER_DENSE_CHOL) {
         HIP_TRY(hipMemsetAsync(s->d_dense, 0, (size_t)n * n * sizeof(double), s->stream));
         HIP_TRY(bos::dev::launch_scatter_dense(s->d_rowptr, s->d_colind, A, nn, s->d_dense, s->stream));
@@ -470,8 +485,9 @@ int wait_status(bos_solver* s, bool sync) {
             if ((it & 4095) == 0) {   // the stream done (or failed) without the number: report it
                 const hipError_t e = hipStreamQuery(s->stream);
                 if (e != hipErrorNotReady) {
-                    if (e != hipSuccess) HIP_TRY(e);
                     if (*q == target) break;
+                    s->seq_seen = *q;   // what the device actually wrote: the next step waits for its own number
+                    if (e != hipSuccess) HIP_TRY(e);
                     return fail(BOS_ERR_DEVICE, "step status sequence number not written");
                 }
             }
@@ -504,8 +520,9 @@ int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr, bo
         if (!s->sharded) {   // phase boundaries stamped by the step's kernels
             auto d = [](unsigned long long a, unsigned long long b) { return b > a ? (double)(b - a) * bos::dev::kStampMs : 0.0; };
             st->t_linearize_ms = d(h.stamp[0], h.stamp[1]);
-            st->t_exchange_ms = 0.0;
-            st->t_solve_ms = d(h.stamp[1], h.stamp[2]);
+            // observations partition: J+H end [1], the all-reduce, solve start [4]
+            st->t_exchange_ms = s->obs ? d(h.stamp[1], h.stamp[4]) : 0.0;
+            st->t_solve_ms = d(h.stamp[s->solve_stamp], h.stamp[2]);
             st->t_update_ms = d(h.stamp[2], h.stamp[3]);
         }
     }
@@ -552,6 +569,51 @@ int shard_enqueue(bos_solver* s, int phase) {
 }
 
 int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec);
+int enqueue_step_tail(bos_solver* s);
+
+// ---- BOS_PARTITION_OBSERVATIONS step (the north star's form): phase 0 = this rank's range of J+H
+// lanes and its chi^2 / robust-count header (external mode: the whole [header | H values | b] in
+// fp64 into the exchange buffer); one all-reduce (sum) over the ranks; phase 1 = (external: the
+// summed buffer back into T) the one-GPU solve, box-plus of every node and stats. Every value of H and
+// b is written by exactly one rank's lanes and is zero on the others, so the sum is exact and every
+// rank solves the one-GPU system bit for bit.
+int obs_enqueue(bos_solver* s, int phase) {
+    int rc;
+    const bool f32 = s->precision == BOS_FP32;
+    if (phase == 0) {
+        if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
+        HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream,
+                                               s->d_status->stamp + 1));
+        if (s->external)
+            HIP_TRY(f32 ? bos::dev::launch_to_f64<float>((const float*)s->d_val, s->ex1_send + bos::kExHeader, s->vb_count, s->stream)
+                        : bos::dev::launch_to_f64<double>((const double*)s->d_val, s->ex1_send + bos::kExHeader, s->vb_count, s->stream));
+        return BOS_OK;
+    }
+    if (s->external)
+        HIP_TRY(f32 ? bos::dev::launch_from_f64<float>(s->ex1_recv + bos::kExHeader, (float*)s->d_sys, s->vb_count, s->stream)
+                    : bos::dev::launch_from_f64<double>(s->ex1_recv + bos::kExHeader, (double*)s->d_sys, s->vb_count, s->stream));
+    return enqueue_step_tail(s);
+}
+
+int obs_phase(bos_solver* s, int phase) {
+    int rc;
+    if (!s->pexec[phase] && !s->graph_failed && (rc = capture(s, 10 + phase, &s->pgraph[phase], &s->pexec[phase]))) return rc;
+    if (s->pexec[phase]) HIP_TRY(hipGraphLaunch(s->pexec[phase], s->stream));
+    else if ((rc = obs_enqueue(s, phase))) return rc;
+    return BOS_OK;
+}
+
+// the one exchange: (H values | b) in T and the header, summed over the ranks (one RCCL group)
+int rccl_allreduce_obs(bos_solver* s) {
+    const ncclDataType_t t = s->precision == BOS_FP32 ? ncclFloat : ncclDouble;
+    NC_TRY(ncclGroupStart());
+    const ncclResult_t r1 = ncclAllReduce(s->d_val, s->d_sys, (size_t)s->vb_count, t, ncclSum, s->comm, s->stream);
+    const ncclResult_t r2 = ncclAllReduce(s->ex1_send, s->ex1_recv, bos::kExHeader, ncclDouble, ncclSum, s->comm, s->stream);
+    NC_TRY(ncclGroupEnd());
+    NC_TRY(r1);
+    NC_TRY(r2);
+    return BOS_OK;
+}
 
 // one phase: its graph (captured on first use), bracketed by the phase events
 int shard_phase(bos_solver* s, int phase) {
@@ -628,6 +690,9 @@ int enqueue_step(bos_solver* s) {
 }
 
 void drop_graph(bos_solver* s) {
+    // bos_step returns on the status sequence number, before the stream has drained: a graph may
+    // still be running
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->graph_exec) (void)hipGraphExecDestroy(s->graph_exec);
     if (s->graph) (void)hipGraphDestroy(s->graph);
     s->graph_exec = nullptr;
@@ -645,7 +710,8 @@ void drop_graph(bos_solver* s) {
 }
 
 // Capture the launches of one GN step (phase -1: the one-GPU step after its J+H build,
-// enqueue_step_tail; -2: the whole one-GPU step; 0-2: a sharded phase) into *exec (multifrontal
+// enqueue_step_tail; -2: the whole one-GPU step; 0-2: a subtree-sharded phase; 10-11: an
+// observations-partition phase) into *exec (multifrontal
 // solvers: rocSOLVER's paths are not captured). A stream that cannot be captured leaves
 // graph_failed set and the launches run eagerly, the same ones in the same order.
 int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec) {
@@ -654,7 +720,10 @@ int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec) {
         s->graph_failed = true;
         return BOS_OK;
     }
-    const int rc = phase == -1 ? enqueue_step_tail(s) : phase == -2 ? enqueue_step(s) : shard_enqueue(s, phase);
+    const int rc = phase == -1   ? enqueue_step_tail(s)
+                   : phase == -2 ? enqueue_step(s)
+                   : phase >= 10 ? obs_enqueue(s, phase - 10)
+                                 : shard_enqueue(s, phase);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s->stream, &g);
     if (rc) {
@@ -667,16 +736,39 @@ int capture(bos_solver* s, int phase, hipGraph_t* graph, hipGraphExec_t* exec) {
     return BOS_OK;
 }
 
+int launch_step(bos_solver* s, bool sync);
+
 // One GN iteration. sync: read the status back (the last step of a bos_step_n batch). A
 // factorization whose dataflow launch timed out leaves the state untouched (the box-plus kernel
 // checks the solver word) and fails the call.
 int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     if (s->sharded) return do_step_sharded(s, st, sync);
     int rc;
+    if (s->obs) {
+        if (!s->comm) return fail(BOS_ERR_INVALID, "observations-partition handle without a communicator: drive bos_step_phase");
+        if ((rc = obs_phase(s, 0)) || (rc = rccl_allreduce_obs(s)) || (rc = obs_phase(s, 1))) return rc;
+    } else if ((rc = launch_step(s, sync))) {
+        return rc;
+    }
+    ++s->seq_pending;   // the step's status launch (now enqueued) bumps the device counter once
+    s->have_dx = true;
+    if (!sync) return BOS_OK;
+    int32_t aborted = 0;
+    if ((rc = read_stats(s, st, &aborted))) return rc;
+    if (aborted) {
+        s->have_dx = false;
+        return fail(BOS_ERR_SOLVER, "sparse factorization aborted: a dataflow dependency wait timed out (state "
+                                    "left unchanged by the failed iteration)");
+    }
+    return BOS_OK;
+}
+
+// The launches of one one-GPU GN iteration (see do_step)
+int launch_step(bos_solver* s, bool sync) {
+    int rc;
     if (uses_mf(s) && !s->graph_exec && !s->graph_failed && (rc = capture(s, -1, &s->graph, &s->graph_exec))) return rc;
     if (uses_mf(s) && !s->exec_full && !s->graph_failed && (rc = capture(s, -2, &s->graph_full, &s->exec_full)))
         return rc;   // both graphs at the first step, so neither kind of call pays a capture later
-    ++s->seq_pending;   // the step's status launch bumps the device counter once
     if (!sync && s->exec_full) {
         // a batch's step before its last: the host is ahead of the device, one graph per step
         HIP_TRY(hipGraphLaunch(s->exec_full, s->stream));
@@ -689,15 +781,6 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
         HIP_TRY(hipGraphLaunch(s->graph_exec, s->stream));
     } else if ((rc = enqueue_step(s))) {
         return rc;
-    }
-    s->have_dx = true;
-    if (!sync) return BOS_OK;
-    int32_t aborted = 0;
-    if ((rc = read_stats(s, st, &aborted))) return rc;
-    if (aborted) {
-        s->have_dx = false;
-        return fail(BOS_ERR_SOLVER, "sparse factorization aborted: a dataflow dependency wait timed out (state "
-                                    "left unchanged by the failed iteration)");
     }
     return BOS_OK;
 }
@@ -756,7 +839,8 @@ int bos_destroy(bos_solver* s) {
     drop_graph(s);
     void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pw_stride, s->pl_cnt, s->lw_base, s->lw_stride, s->ll_cnt, s->ll_lm,
                     s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w,
-                    s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->d_b, s->d_val64, s->d_csr64,
+                    s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->obs ? nullptr : s->d_b, s->d_sys,
+                    s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_status,
                     s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr,
@@ -786,6 +870,8 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     if (opt.solver != BOS_SOLVER_SUPERNODAL && opt.solver != BOS_SOLVER_DENSE_CHOL &&
         opt.solver != BOS_SOLVER_ROCSOLVER_RF && opt.solver != BOS_SOLVER_SCHUR)
         return fail(BOS_ERR_INVALID, "unknown solver");
+    if (opt.partition != BOS_PARTITION_SUBTREE && opt.partition != BOS_PARTITION_OBSERVATIONS)
+        return fail(BOS_ERR_INVALID, "unknown partition");
     if (pb->num_poses <= 0 || pb->num_landmarks < 0 || pb->num_bearings < 0 || pb->num_odometry < 0)
         return fail(BOS_ERR_INVALID, "bad problem sizes");
     if (!pb->pose_xyt ||
@@ -824,12 +910,21 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     pi.NP = s->NP; pi.NL = s->NL; pi.Mb = s->Mb; pi.Mo = s->Mo; pi.fixed = pb->fixed_pose;
     pi.b_pose = pb->bearing_pose; pi.b_lm = pb->bearing_landmark; pi.o_src = pb->odom_src; pi.o_dst = pb->odom_dst;
     pi.b_omega = pb->bearing_omega; pi.o_omega = pb->odom_omega;
+    pi.lpp = opt.lanes_per_pose;
+    pi.schur_leaf = opt.schur_leaf;
+    // multi-rank (world > 1, or a communicator given with world 1: a one-GPU test of the path)
+    const bool multi = s->world > 1 || opt.nccl_unique_id;
+    s->partition = opt.partition;
+    s->obs = multi && opt.partition == BOS_PARTITION_OBSERVATIONS;
+    s->sharded = multi && opt.partition == BOS_PARTITION_SUBTREE;
+    s->external = multi && !opt.nccl_unique_id;
     std::string err;
     const int fmode = s->solver_kind == BOS_SOLVER_SUPERNODAL    ? bos::kFactorMultifrontal
                       : s->solver_kind == BOS_SOLVER_SCHUR        ? bos::kFactorSchur
                       : s->solver_kind == BOS_SOLVER_ROCSOLVER_RF ? bos::kFactorScalar
                                                                   : bos::kFactorNone;
-    int rc = bos::build_plan(pi, s->rank, s->world, fmode, s->plan, err);
+    // the observations partition runs a range of the one-GPU plan's lanes
+    int rc = s->obs ? bos::build_plan(pi, 0, 1, fmode, s->plan, err) : bos::build_plan(pi, s->rank, s->world, fmode, s->plan, err);
     if (rc) return bail(fail(rc, "plan: " + err));
     const bos::Plan& P = s->plan;
     if (s->solver_kind == BOS_SOLVER_DENSE_CHOL && P.n > 40000)
@@ -863,16 +958,18 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         if (rocsolver_set_rfinfo_mode(s->rf, rocsolver_rfinfo_mode_cholesky) != rocblas_status_success)
             return bail(fail(BOS_ERR_SOLVER, "set_rfinfo_mode"));
     }
-    // sharded: world > 1, or a communicator given with world 1 (the sharded phases and their RCCL
-    // all-gathers run with one rank: a one-GPU test of that path)
-    s->sharded = s->world > 1 || opt.nccl_unique_id;
-    s->external = s->sharded && !opt.nccl_unique_id;
-    if (s->sharded && !uses_mf(s)) return bail(fail(BOS_ERR_UNSUPPORTED, "sharding needs a multifrontal solver"));
+    if (multi && !uses_mf(s)) return bail(fail(BOS_ERR_UNSUPPORTED, "sharding needs a multifrontal solver"));
     if (opt.nccl_unique_id) {
         ncclUniqueId id;
         std::memcpy(&id, opt.nccl_unique_id, sizeof(id));
         ncclResult_t r = ncclCommInitRank(&s->comm, s->world, id, s->rank);
         if (r != ncclSuccess) return bail(fail(BOS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
+        int count = 0;   // the ranks the communicator actually holds
+        r = ncclCommCount(s->comm, &count);
+        if (r != ncclSuccess) return bail(fail(BOS_ERR_COMM, std::string("ncclCommCount: ") + ncclGetErrorString(r)));
+        if (count != s->world)
+            return bail(fail(BOS_ERR_COMM, "communicator holds " + std::to_string(count) + " ranks, world_size " +
+                                               std::to_string(s->world)));
     }
     if (s->sharded && (rc = setup_shard(s))) return bail(rc);
 
@@ -938,9 +1035,21 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             for (size_t i = 0; i < lo.size(); ++i) if (lo[i] >= 0) lbw[i] = pb->bearing_omega[lo[i]];
             if ((rc = upload_Tv(&s->pb_w, pbw)) || (rc = upload_Tv(&s->lb_w, lbw))) return bail(rc);
         }
-        s->pose_blocks = (int)(((int64_t)B.lane_pose.size() * B.lpp + bos::dev::kBlock - 1) / bos::dev::kBlock);
-        // chi^2 partials: own lanes (a whole number of blocks when sharded), the top lanes on rank 0
-        s->chi_parts = s->rank == 0 ? s->pose_blocks : (int)((int64_t)P.shard.own_pose_lanes * B.lpp / bos::dev::kBlock);
+        static_assert(bos::kJhBlock == bos::dev::kBlock, "J+H block size");
+        s->pose_blocks = (int)B.pose_blocks();
+        // J+H blocks this rank runs: all of them, or (observations partition) its ranges
+        if (s->obs) {
+            int64_t pb1 = 0, lb1 = 0;
+            bos::observation_lanes(P, s->rank, s->world, s->pose_b0, pb1, s->lm_b0, lb1, nullptr);
+            s->n_pose_run = pb1 - s->pose_b0;
+            s->n_lm_run = lb1 - s->lm_b0;
+        } else {
+            s->n_pose_run = s->pose_blocks;
+            s->n_lm_run = B.lm_blocks();
+        }
+        // chi^2 partials: own lanes (a whole number of blocks when sharded), the top lanes on rank 0;
+        // observations partition: every block (the others' partials stay 0)
+        s->chi_parts = s->rank == 0 || s->obs ? s->pose_blocks : (int)((int64_t)P.shard.own_pose_lanes * B.lpp / bos::dev::kBlock);
         if ((rc = upload(&s->lane_pose, B.lane_pose))) return bail(rc);
         s->lane_identity = true;
         for (size_t i = 0; i < B.lane_pose.size() && s->lane_identity; ++i) s->lane_identity = B.lane_pose[i] == (int32_t)i;
@@ -972,11 +1081,31 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     }
     const int64_t nval = std::max<int64_t>(P.blk.size, 1), nb = 3 * (int64_t)NP + 2 * (int64_t)NL;
     if ((rc = upload(&s->node_dof, P.node_dof))) return bail(rc);
-    if ((rc = alloc_T(&s->d_val, nval)) || (rc = alloc_T(&s->d_b, nb)) || (rc = dalloc(&s->d_rhs, std::max<int64_t>(P.n, 1))))
-        return bail(rc);
+    if (s->obs) {
+        // [block array (even length) | b] in one buffer, all-reduced in one call into d_sys; the
+        // values outside this rank's lanes stay 0
+        const int64_t nv2 = (nval + 1) & ~(int64_t)1;
+        s->vb_count = nv2 + nb;
+        if ((rc = alloc_T(&s->d_val, s->vb_count)) || (rc = alloc_T(&s->d_sys, s->vb_count))) return bail(rc);
+        s->d_b = (char*)s->d_val + nv2 * s->tsize;
+        s->sys_val = s->d_sys;
+        s->sys_b = (char*)s->d_sys + nv2 * s->tsize;
+        HIP_TRY(hipMemset(s->d_val, 0, s->vb_count * s->tsize));
+        HIP_TRY(hipMemset(s->d_sys, 0, s->vb_count * s->tsize));
+        s->ex1_count = bos::kExHeader + (s->external ? s->vb_count : 0);
+        if ((rc = dalloc(&s->ex1_send, (size_t)s->ex1_count)) || (rc = dalloc(&s->ex1_recv, (size_t)s->ex1_count))) return bail(rc);
+        HIP_TRY(hipMemset(s->ex1_send, 0, s->ex1_count * sizeof(double)));
+        HIP_TRY(hipMemset(s->ex1_recv, 0, s->ex1_count * sizeof(double)));
+        s->solve_stamp = 4;
+    } else {
+        if ((rc = alloc_T(&s->d_val, nval)) || (rc = alloc_T(&s->d_b, nb))) return bail(rc);
+        s->sys_val = s->d_val;
+        s->sys_b = s->d_b;
+        HIP_TRY(hipMemset(s->d_val, 0, nval * s->tsize));
+        HIP_TRY(hipMemset(s->d_b, 0, nb * s->tsize));
+    }
+    if ((rc = dalloc(&s->d_rhs, std::max<int64_t>(P.n, 1)))) return bail(rc);
     if (f32 && uses_mf(s) && (rc = dalloc(&s->d_val64, nval))) return bail(rc);
-    HIP_TRY(hipMemset(s->d_val, 0, nval * s->tsize));
-    HIP_TRY(hipMemset(s->d_b, 0, nb * s->tsize));
     {
         std::vector<int32_t> er(s->ref_dof.begin(), s->ref_dof.begin() + P.n);
         if ((rc = upload(&s->elim_ref, er))) return bail(rc);
@@ -1158,6 +1287,17 @@ int bos_time_steps(bos_solver* s, int32_t n, double* ms_per_step) {
 
 int bos_step_phase(bos_solver* s, int32_t phase, bos_step_stats* st) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    if (s->obs) {   // observations partition: phases 0 and 1, the all-reduce between them
+        if (phase != s->phase) return fail(BOS_ERR_INVALID, "bos_step_phase: phases run 0, 1 in order");
+        HIP_TRY(hipSetDevice(s->device));
+        const int rc = obs_phase(s, phase);
+        if (rc) { s->phase = 0; return rc; }
+        s->phase = (phase + 1) % 2;
+        if (phase == 0) return BOS_OK;
+        ++s->seq_pending;
+        s->have_dx = true;
+        return finish_step(s, st);
+    }
     if (!s->sharded) return fail(BOS_ERR_INVALID, "bos_step_phase needs a sharded handle (world_size > 1)");
     if (phase != s->phase) return fail(BOS_ERR_INVALID, "bos_step_phase: phases run 0, 1, 2 in order");
     HIP_TRY(hipSetDevice(s->device));
@@ -1171,14 +1311,14 @@ int bos_step_phase(bos_solver* s, int32_t phase, bos_step_stats* st) {
 
 int bos_exchange_size(const bos_solver* s, int32_t which, int64_t* doubles_per_rank) {
     if (!s || !doubles_per_rank || (which != 1 && which != 2)) return fail(BOS_ERR_INVALID, "bad argument");
-    if (!s->sharded) return fail(BOS_ERR_INVALID, "not a sharded handle");
+    if (!s->sharded && !(s->obs && which == 1)) return fail(BOS_ERR_INVALID, "not a sharded handle / no such exchange");
     *doubles_per_rank = which == 1 ? s->ex1_count : s->ex2_count;
     return BOS_OK;
 }
 
 int bos_exchange_download(bos_solver* s, int32_t which, double* send) {
     if (!s || !send || (which != 1 && which != 2)) return fail(BOS_ERR_INVALID, "bad argument");
-    if (!s->sharded) return fail(BOS_ERR_INVALID, "not a sharded handle");
+    if (!s->sharded && !(s->obs && which == 1)) return fail(BOS_ERR_INVALID, "not a sharded handle / no such exchange");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
     const int64_t c = which == 1 ? s->ex1_count : s->ex2_count;
@@ -1188,16 +1328,18 @@ int bos_exchange_download(bos_solver* s, int32_t which, double* send) {
 
 int bos_exchange_upload(bos_solver* s, int32_t which, const double* recv_all) {
     if (!s || !recv_all || (which != 1 && which != 2)) return fail(BOS_ERR_INVALID, "bad argument");
-    if (!s->sharded) return fail(BOS_ERR_INVALID, "not a sharded handle");
+    if (!s->sharded && !(s->obs && which == 1)) return fail(BOS_ERR_INVALID, "not a sharded handle / no such exchange");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    const int64_t c = (which == 1 ? s->ex1_count : s->ex2_count) * s->world;
+    // subtree partition: every rank's buffer (all-gather); observations partition: their sum
+    const int64_t c = s->obs ? s->ex1_count : (which == 1 ? s->ex1_count : s->ex2_count) * s->world;
     HIP_TRY(hipMemcpy(which == 1 ? s->ex1_recv : s->ex2_recv, recv_all, c * sizeof(double), hipMemcpyHostToDevice));
     return BOS_OK;
 }
 
 int bos_node_owner(const bos_solver* s, int32_t* owner) {
     if (!s || !owner) return fail(BOS_ERR_INVALID, "null argument");
+    if (s->obs) return fail(BOS_ERR_UNSUPPORTED, "observations partition: every rank holds every node");
     const std::vector<int32_t>& o = s->plan.shard.node_owner;
     if (o.empty()) return fail(BOS_ERR_UNSUPPORTED, "no shard (not a multifrontal solver)");
     std::copy(o.begin(), o.end(), owner);
@@ -1216,7 +1358,7 @@ int bos_debug_inject_stall(bos_solver* s) {
 
 int bos_debug_solver_stamps(bos_solver* s, int64_t capacity, uint64_t* stamps, int32_t* meta) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
-    if (!uses_mf(s) || s->sharded) return fail(BOS_ERR_UNSUPPORTED, "one-GPU multifrontal handles only");
+    if (!uses_mf(s) || s->sharded || s->obs) return fail(BOS_ERR_UNSUPPORTED, "one-GPU multifrontal handles only");
     const bos::Multifrontal& F = s->plan.mf;
     const int64_t need = 16 * (int64_t)F.nsuper;
     if (!stamps || !meta || capacity < need) return fail(BOS_ERR_INVALID, "stamps: capacity 16 * supernodes");
@@ -1279,6 +1421,7 @@ int bos_synchronize(bos_solver* s) {
 
 int bos_linearize(bos_solver* s, bos_step_stats* st) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    if (s->sharded || s->obs) return fail(BOS_ERR_UNSUPPORTED, "bos_linearize on a sharded handle (a rank builds part of H)");
     HIP_TRY(hipSetDevice(s->device));
     int rc;
     HIP_TRY(hipEventRecord(s->ev[0], s->stream));
@@ -1312,11 +1455,19 @@ int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
     info->landmark_lanes = (int32_t)P.blk.lm_lane_lm.size();
     info->own_fronts = P.shard.n_own_fronts;
     info->top_fronts = P.shard.n_top_fronts;
+    info->partition = s->partition;
+    info->comm_ranks = 0;
+    if (s->comm) {
+        int count = 0;
+        NC_TRY(ncclCommCount(s->comm, &count));
+        info->comm_ranks = count;
+    }
     return BOS_OK;
 }
 
 int bos_export_system(const bos_solver* s, int64_t capacity, int32_t* rows, int32_t* cols, double* vals, double* b) {
     if (!s) return fail(BOS_ERR_INVALID, "null handle");
+    if (s->sharded) return fail(BOS_ERR_UNSUPPORTED, "bos_export_system on a subtree-sharded handle (a rank holds part of H)");
     const bos::Plan& P = s->plan;
     const int64_t nnz = P.nnzA();
     if ((rows || cols || vals) && capacity < nnz) return fail(BOS_ERR_INVALID, "export capacity < nnz_lower");
@@ -1327,10 +1478,10 @@ int bos_export_system(const bos_solver* s, int64_t capacity, int32_t* rows, int3
         std::vector<double> v(nv);
         if (s->precision == BOS_FP32) {
             std::vector<float> f(nv);
-            if (nv) HIP_TRY(hipMemcpy(f.data(), s->d_val, nv * sizeof(float), hipMemcpyDeviceToHost));
+            if (nv) HIP_TRY(hipMemcpy(f.data(), s->sys_val, nv * sizeof(float), hipMemcpyDeviceToHost));
             for (int64_t i = 0; i < nv; ++i) v[i] = f[i];
         } else if (nv) {
-            HIP_TRY(hipMemcpy(v.data(), s->d_val, nv * sizeof(double), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(v.data(), s->sys_val, nv * sizeof(double), hipMemcpyDeviceToHost));
         }
         for (int64_t e = 0; e < nnz; ++e) vals[e] = v[P.blk.csr_src[e]];
     }
@@ -1346,10 +1497,10 @@ int bos_export_system(const bos_solver* s, int64_t capacity, int32_t* rows, int3
         const int64_t nb = 3 * (int64_t)s->NP + 2 * (int64_t)s->NL;
         if (s->precision == BOS_FP32) {
             std::vector<float> v(nb);
-            HIP_TRY(hipMemcpy(v.data(), s->d_b, nb * sizeof(float), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(v.data(), s->sys_b, nb * sizeof(float), hipMemcpyDeviceToHost));
             for (int64_t i = 0; i < nb; ++i) b[i] = v[i];
         } else {
-            HIP_TRY(hipMemcpy(b, s->d_b, nb * sizeof(double), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(b, s->sys_b, nb * sizeof(double), hipMemcpyDeviceToHost));
         }
         for (int d = 0; d < 3; ++d) b[3 * (int64_t)P.fixed + d] = 0.0;
     }
@@ -1385,6 +1536,7 @@ int bos_set_state(bos_solver* s, const double* pose_xyt, const double* landmark_
 
 int bos_get_last_dx(const bos_solver* s, double* dx) {
     if (!s || !dx) return fail(BOS_ERR_INVALID, "null argument");
+    if (s->sharded) return fail(BOS_ERR_UNSUPPORTED, "bos_get_last_dx on a subtree-sharded handle (a rank holds part of x)");
     if (!s->have_dx) return fail(BOS_ERR_INVALID, "no step has been run");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));

@@ -225,22 +225,56 @@ int factor_mode_of(int32_t solver) {
         default: return -1;
     }
 }
+
+// The planning fields of an options struct (NULL = defaults): the problem index with the plan
+// options, the factor mode, and the options themselves
+int plan_args(const bos_problem* pb, const bos_options* in, bos::ProblemIndex& pi, int& fmode, bos_options& opt) {
+    bos_default_options(&opt);
+    if (in) opt = *in;
+    fmode = factor_mode_of(opt.solver);
+    if (fmode < 0) return hfail(BOS_ERR_INVALID, "unknown solver");
+    if (opt.partition != BOS_PARTITION_SUBTREE && opt.partition != BOS_PARTITION_OBSERVATIONS)
+        return hfail(BOS_ERR_INVALID, "unknown partition");
+    pi = index_of(pb);
+    pi.lpp = opt.lanes_per_pose;
+    pi.schur_leaf = opt.schur_leaf;
+    return BOS_OK;
+}
+
+// The plan of rank `rank` of `world`: BOS_PARTITION_OBSERVATIONS plans are one-GPU plans (every rank
+// holds the whole structure and runs a range of its lanes)
+int plan_for(const bos::ProblemIndex& pi, const bos_options& opt, int fmode, int rank, int world, bos::Plan& P,
+             std::string& err) {
+    if (opt.partition == BOS_PARTITION_OBSERVATIONS) return bos::build_plan(pi, 0, 1, fmode, P, err);
+    return bos::build_plan(pi, rank, world, fmode, P, err);
+}
 }  // namespace
 
-void bos_debug_set_schur_leaf(int32_t poses) { bos::g_schur_leaf = poses > 0 ? poses : 0; }
 void bos_debug_set_g2o_parser(int32_t line_by_line) { proj02::g_g2o_line_parser = line_by_line != 0; }
 
-int bos_plan_inspect(const bos_problem* pb, int32_t solver, int32_t rank, int32_t world, int64_t capacity, int32_t* ref_rows,
-                     int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref,
+int bos_plan_inspect(const bos_problem* pb, const bos_options* options, int32_t rank, int32_t world, int64_t capacity,
+                     int32_t* ref_rows, int32_t* ref_cols, uint8_t* owned, uint8_t* b_owned, int32_t* perm_to_ref,
                      bos_plan_info* info) {
     if (!pb) return hfail(BOS_ERR_INVALID, "null problem");
-    const int fmode = factor_mode_of(solver);
-    if (fmode < 0) return hfail(BOS_ERR_INVALID, "unknown solver");
-    const bos::ProblemIndex pi = index_of(pb);
+    if (world < 1 || rank < 0 || rank >= world) return hfail(BOS_ERR_INVALID, "bad rank/world");
+    bos::ProblemIndex pi;
+    bos_options opt;
+    int fmode = 0;
+    int rc = plan_args(pb, options, pi, fmode, opt);
+    if (rc) return rc;
     bos::Plan P;
     std::string err;
-    const int rc = bos::build_plan(pi, rank, world, fmode, P, err);
+    rc = plan_for(pi, opt, fmode, rank, world, P, err);
     if (rc) return hfail(rc, err);
+    // observations partition: this rank's share of the one-GPU plan's lanes
+    const bool obs = opt.partition == BOS_PARTITION_OBSERVATIONS && world > 1;
+    std::vector<char> lane_node;
+    std::vector<uint8_t> own_e;
+    if (obs) {
+        int64_t pb0, pb1, lb0, lb1;
+        bos::observation_lanes(P, rank, world, pb0, pb1, lb0, lb1, &lane_node);
+        bos::owned_entries(P, lane_node, own_e);
+    }
     const int NP = pi.NP;
     std::vector<int32_t> ref(P.n + 3);
     for (int u = 0; u < pi.NP + pi.NL; ++u) {
@@ -284,7 +318,7 @@ int bos_plan_inspect(const bos_problem* pb, int32_t solver, int32_t rank, int32_
                 const int32_t a = ref[r], c = ref[P.colind[e]];
                 if (ref_rows) ref_rows[e] = std::max(a, c);
                 if (ref_cols) ref_cols[e] = std::min(a, c);
-                if (owned) owned[e] = P.blk.csr_src[e] >= 0 ? 1 : 0;
+                if (owned) owned[e] = obs ? own_e[e] : P.blk.csr_src[e] >= 0 ? 1 : 0;
             }
     }
     if (perm_to_ref)
@@ -292,21 +326,27 @@ int bos_plan_inspect(const bos_problem* pb, int32_t solver, int32_t rank, int32_
     if (b_owned) {   // b lives in the reference numbering; a lane writes its node's entries
         for (int64_t i = 0; i < P.n + 3; ++i) b_owned[i] = 0;
         for (int32_t p : P.blk.lane_pose)
-            if (p >= 0)
+            if (p >= 0 && (!obs || lane_node[p]))
                 for (int d = 0; d < 3; ++d) b_owned[3 * (int64_t)p + d] = 1;
         for (int32_t l : P.blk.lm_lane_lm)
-            for (int d = 0; d < 2; ++d) b_owned[3 * (int64_t)NP + 2 * (int64_t)l + d] = 1;
+            if (!obs || lane_node[NP + l])
+                for (int d = 0; d < 2; ++d) b_owned[3 * (int64_t)NP + 2 * (int64_t)l + d] = 1;
     }
     return BOS_OK;
 }
 
-int bos_plan_node_owner(const bos_problem* pb, int32_t solver, int32_t world, int32_t* owner) {
-    if (!pb || !owner) return hfail(BOS_ERR_INVALID, "null argument");
-    const int fmode = factor_mode_of(solver);
-    if (fmode < 0) return hfail(BOS_ERR_INVALID, "unknown solver");
+int bos_plan_node_owner(const bos_problem* pb, const bos_options* options, int32_t world, int32_t* owner) {
+    if (!pb || !owner || world < 1) return hfail(BOS_ERR_INVALID, "bad argument");
+    bos::ProblemIndex pi;
+    bos_options opt;
+    int fmode = 0;
+    int rc = plan_args(pb, options, pi, fmode, opt);
+    if (rc) return rc;
+    if (opt.partition == BOS_PARTITION_OBSERVATIONS)
+        return hfail(BOS_ERR_UNSUPPORTED, "observations partition: every rank holds every node");
     bos::Plan P;
     std::string err;
-    const int rc = bos::build_plan(index_of(pb), 0, world, fmode, P, err);
+    rc = bos::build_plan(pi, 0, world, fmode, P, err);
     if (rc) return hfail(rc, err);
     if (P.shard.node_owner.empty()) return hfail(BOS_ERR_UNSUPPORTED, "no shard (not a multifrontal solver)");
     std::copy(P.shard.node_owner.begin(), P.shard.node_owner.end(), owner);
@@ -317,13 +357,19 @@ int bos_plan_node_owner(const bos_problem* pb, int32_t solver, int32_t world, in
 // tree and maps (validates the symbolic structure without a GPU). vals: values of the stored
 // entries of H_nf in bos_plan_inspect's order (scattered into the block array here), rhs / x:
 // permuted order of length n. Not used by any solve path.
-int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* vals, const double* rhs, double* x) {
+int bos_plan_mf_selftest(const bos_problem* pb, const bos_options* options, const double* vals, const double* rhs,
+                         double* x) {
     if (!pb || !vals || !rhs || !x) return hfail(BOS_ERR_INVALID, "null argument");
-    if (solver != BOS_SOLVER_SUPERNODAL && solver != BOS_SOLVER_SCHUR)
+    bos::ProblemIndex pi;
+    bos_options opt;
+    int fmode = 0;
+    int rc = plan_args(pb, options, pi, fmode, opt);
+    if (rc) return rc;
+    if (opt.solver != BOS_SOLVER_SUPERNODAL && opt.solver != BOS_SOLVER_SCHUR)
         return hfail(BOS_ERR_INVALID, "selftest needs a multifrontal solver");
     bos::Plan P;
     std::string err;
-    const int rc = bos::build_plan(index_of(pb), 0, 1, factor_mode_of(solver), P, err);
+    rc = bos::build_plan(pi, 0, 1, fmode, P, err);
     if (rc) return hfail(rc, err);
     bos::HostMf M(P, vals, rhs);
     auto all = [](int) { return true; };
@@ -342,23 +388,28 @@ int bos_plan_mf_selftest(const bos_problem* pb, int32_t solver, const double* va
 // boundary solution (exchange 2). Checks: the ranks agree on the top bit for bit; the merged x
 // (each node from its owner) equals the one-rank run bit for bit; every observation's chi^2 is
 // counted by exactly one rank; every node a rank's J+H lanes read is in its box-plus set.
-int bos_plan_shard_selftest(const bos_problem* pb, int32_t solver, int32_t world, const double* vals, const double* rhs,
-                            double* x) {
+int bos_plan_shard_selftest(const bos_problem* pb, const bos_options* options, int32_t world, const double* vals,
+                            const double* rhs, double* x) {
     if (!pb || !vals || !rhs || !x || world < 1) return hfail(BOS_ERR_INVALID, "bad argument");
-    if (solver != BOS_SOLVER_SUPERNODAL && solver != BOS_SOLVER_SCHUR)
+    bos::ProblemIndex pi;
+    bos_options opt;
+    int fmode = 0;
+    const int arc = plan_args(pb, options, pi, fmode, opt);
+    if (arc) return arc;
+    if (opt.solver != BOS_SOLVER_SUPERNODAL && opt.solver != BOS_SOLVER_SCHUR)
         return hfail(BOS_ERR_INVALID, "selftest needs a multifrontal solver");
-    const bos::ProblemIndex pi = index_of(pb);
+    if (opt.partition != BOS_PARTITION_SUBTREE) return hfail(BOS_ERR_INVALID, "selftest of the subtree partition");
     const int NP = pi.NP, NL = pi.NL;
     std::vector<bos::Plan> plans(world);
     for (int r = 0; r < world; ++r) {
         std::string err;
-        const int rc = bos::build_plan(pi, r, world, factor_mode_of(solver), plans[r], err);
+        const int rc = bos::build_plan(pi, r, world, fmode, plans[r], err);
         if (rc) return hfail(rc, err);
     }
     bos::Plan one;
     {
         std::string err;
-        const int rc = bos::build_plan(pi, 0, 1, factor_mode_of(solver), one, err);
+        const int rc = bos::build_plan(pi, 0, 1, fmode, one, err);
         if (rc) return hfail(rc, err);
     }
     const int64_t n = one.n;

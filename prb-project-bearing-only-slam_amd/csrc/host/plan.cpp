@@ -17,7 +17,6 @@ constexpr int kMfLeaf = 12;          // nested-dissection leaf size (nodes) for 
 constexpr int kSchurLeaf = 10;
 }  // namespace
 
-int g_schur_leaf = 0;   // test hook (bos_debug_set_schur_leaf); 0 = kSchurLeaf
 
 namespace {
 
@@ -318,7 +317,7 @@ int order_nodes(const ProblemIndex& pi, int mode, std::vector<int32_t>& node_pos
         for (int u = 0; u < NP; ++u) active[u] = u != pi.fixed;
         std::vector<int32_t> ord_p;
         std::vector<std::pair<int32_t, int32_t>> pblocks;
-        const int leaf = g_schur_leaf > 0 ? g_schur_leaf : kSchurLeaf;
+        const int leaf = pi.schur_leaf > 0 ? pi.schur_leaf : kSchurLeaf;
         nested_dissection(build_schur_graph(pi), active, ord_p, leaf, &pblocks);
         if ((int)ord_p.size() != NP - 1) { err = "nested dissection of the pose graph lost nodes"; return BOS_ERR_INVALID; }
         order.insert(order.end(), ord_p.begin(), ord_p.end());
@@ -662,7 +661,9 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     // lanes per pose and their bearing segments (lane 0 also takes the odometry entries; a run of
     // duplicate observations of one pair never straddles two lanes)
     const double avg = NP ? (double)Mb / NP : 0.0;
-    B.lpp = avg >= 32 ? 2 : 1;   // measured on config 3 (K = 10): 1 lane per pose beats 2 and 4
+    // measured on config 3 (K = 10): 1 lane per pose beats 2 and 4 (bos_options.lanes_per_pose forces it)
+    B.lpp = pi.lpp > 0 ? pi.lpp : avg >= 32 ? 2 : 1;
+    if (B.lpp != 1 && B.lpp != 2 && B.lpp != 4) { err = "lanes per pose must be 1, 2 or 4"; return BOS_ERR_INVALID; }
     const int L = B.lpp;
     auto same_lm = [&](int i, int j) { return pi.b_lm[pb_obs[i]] == pi.b_lm[pb_obs[j]]; };
     for (int p = 0; p < NP; ++p)
@@ -676,7 +677,7 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     pitems.reserve(Mb);
     for (int i = 0; i < G; ++i) {
         const int p = B.lane_pose[i];
-        int cut[3] = {0, 0, 0};   // bearing range of each lane (as pb_obs offsets)
+        int cut[5] = {0, 0, 0, 0, 0};   // bearing range of each lane (as pb_obs offsets)
         if (p >= 0) {
             const int b0 = pb_ptr[p], b1 = pb_ptr[p + 1], nb = b1 - b0;
             const int no = B.po_ptr[p + 1] - B.po_ptr[p];
@@ -794,6 +795,43 @@ int build_csr_src(const ProblemIndex& pi, Plan& P, const std::vector<int32_t>& i
         }
     }
     return BOS_OK;
+}
+
+void observation_lanes(const Plan& P, int rank, int world, int64_t& pb0, int64_t& pb1, int64_t& lb0, int64_t& lb1,
+                       std::vector<char>* lane_node) {
+    const BlockLayout& B = P.blk;
+    split_range(B.pose_blocks(), rank, world, pb0, pb1);
+    split_range(B.lm_blocks(), rank, world, lb0, lb1);
+    if (!lane_node) return;
+    lane_node->assign((size_t)P.NP + P.NL, 0);
+    const int64_t G = (int64_t)B.lane_pose.size() * B.lpp, NLL = (int64_t)B.lm_lane_lm.size();
+    for (int64_t g = pb0 * kJhBlock; g < std::min(G, pb1 * kJhBlock); ++g)
+        if (B.lane_pose[g / B.lpp] >= 0) (*lane_node)[B.lane_pose[g / B.lpp]] = 1;
+    for (int64_t g = lb0 * kJhBlock; g < std::min(NLL, lb1 * kJhBlock); ++g) (*lane_node)[P.NP + B.lm_lane_lm[g]] = 1;
+}
+
+void owned_entries(const Plan& P, const std::vector<char>& lane_node, std::vector<uint8_t>& owned) {
+    const BlockLayout& B = P.blk;
+    // the pose whose lane writes each pose-landmark slot, and the lower pose of each pose-pose block
+    std::vector<int32_t> slot_pose(B.pose_lanes.slots(), -1), pp_pose(B.nuo(), -1);
+    for (int64_t g = 0; g < (int64_t)B.lane_pose.size() * B.lpp; ++g) {
+        const int p = B.lane_pose[g / B.lpp];
+        if (p < 0) continue;
+        for (int j = 0; j < B.pose_lanes.w_len[g / 64]; ++j) slot_pose[B.pose_lanes.slot((int)g, j)] = p;
+    }
+    for (int p = 0; p < P.NP; ++p)
+        for (int q = B.uo_ptr[p]; q < B.uo_ptr[p + 1]; ++q) pp_pose[q] = p;
+    owned.assign(P.nnzA(), 0);
+    for (int64_t e = 0; e < P.nnzA(); ++e) {
+        const int64_t v = B.csr_src[e];
+        if (v < 0) continue;
+        int owner;
+        if (v < B.off_ldiag) owner = (int)(v / 6);
+        else if (v < B.off_pl) owner = P.NP + (int)((v - B.off_ldiag) / 3);
+        else if (v < B.off_pp) owner = slot_pose[(v - B.off_pl) / 6];
+        else owner = pp_pose[(v - B.off_pp) / 6];
+        owned[e] = owner >= 0 && lane_node[owner] ? 1 : 0;
+    }
 }
 
 int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_t>& inv,

@@ -24,7 +24,21 @@ struct ProblemIndex {
     const int32_t* o_dst = nullptr;
     const double* b_omega = nullptr;   // [Mb] or null (= 1)
     const double* o_omega = nullptr;   // [Mo * 9]
+    // planning options (bos_options): J+H lanes per pose (0 = by the bearings per pose) and poses per
+    // nested-dissection leaf of the Schur ordering (0 = kSchurLeaf)
+    int lpp = 0;
+    int schur_leaf = 0;
 };
+
+// J+H launch geometry shared by the host plan and the kernel (hip/kernels.hpp kBlock)
+constexpr int kJhBlock = 256;
+// Contiguous share [a, b) of n items for rank r of W (BOS_PARTITION_OBSERVATIONS: each rank runs a
+// range of the J+H's pose blocks and one of its landmark blocks, i.e. of the observations in
+// measurement order)
+inline void split_range(int64_t n, int r, int W, int64_t& a, int64_t& b) {
+    a = n * r / W;
+    b = n * (r + 1) / W;
+}
 
 // Block-sparse storage of H that the J+H kernel (hip/kernels.hip) writes, in observation order
 // rather than in the solver's order (the solver reads it through index maps: Multifrontal::amap_src
@@ -62,7 +76,7 @@ constexpr int kLmWindow = 256;   // landmark lanes are permuted only inside alig
 
 struct BlockLayout {
     int64_t off_ldiag = 0, off_pl = 0, off_pp = 0, size = 0;
-    int lpp = 1;                        // lanes per pose: 1 or 2
+    int lpp = 1;                        // lanes per pose: 1, 2 or 4
     bool has_dups = false;              // some (pose, landmark) or (src, dst) pair repeats
     // pose lane groups: group i (lanes i * lpp ... + lpp - 1) runs pose lane_pose[i] (-1: padding);
     // one rank runs the poses of Shard::lane_poses (all poses in stix order on one GPU)
@@ -88,6 +102,8 @@ struct BlockLayout {
     int nub() const { return ub_ptr.empty() ? 0 : ub_ptr.back(); }
     int nuo() const { return uo_ptr.empty() ? 0 : uo_ptr.back(); }
     int poses_per_wave() const { return 64 / lpp; }
+    int64_t pose_blocks() const { return ((int64_t)lane_pose.size() * lpp + kJhBlock - 1) / kJhBlock; }
+    int64_t lm_blocks() const { return ((int64_t)lm_lane_lm.size() + kJhBlock - 1) / kJhBlock; }
 };
 
 
@@ -203,12 +219,17 @@ enum FactorMode {
                               // Schur complement S = H_pp - H_pl H_ll^-1 H_lp
 };
 
-// Test hook: poses per nested-dissection leaf of the Schur ordering (0 = the default, 10). Larger
-// leaves give fronts the fast kernels do not take (exercises build_plan's fallback).
-extern int g_schur_leaf;
-
 // Builds the plan. Returns 0 or a negative BOS_ERR_* code with a message in err.
 int build_plan(const ProblemIndex& pi, int rank, int world, int factor_mode, Plan& out, std::string& err);
+
+// BOS_PARTITION_OBSERVATIONS on a one-GPU plan: the J+H block ranges of rank r of W (pose blocks
+// [pb0, pb1), landmark blocks [lb0, lb1)), and which nodes' lanes they run (lane_node[u] = 1)
+void observation_lanes(const Plan& P, int rank, int world, int64_t& pb0, int64_t& pb1, int64_t& lb0, int64_t& lb1,
+                       std::vector<char>* lane_node);
+// The block value of every stored entry of the lower triangle whose J+H lane is in lane_node (the
+// rule of build_csr_src: a diagonal block by its node, a pose-landmark block by its pose, a pose-pose
+// block by the lower pose): owned[e] = 1
+void owned_entries(const Plan& P, const std::vector<char>& lane_node, std::vector<uint8_t>& owned);
 
 // Segments of exchange 1 for rank `rank` (hip/solver_capi.hip): pack = this rank's roots' U / u into
 // its send buffer, unpack = every other rank's roots from the receive buffer (kinds: 0 U, 1 u, 2 send,

@@ -19,10 +19,6 @@
 
 namespace bos {
 
-namespace {
-constexpr int kJhBlock = 256;   // J+H lanes per workgroup (hip/kernels.hpp kBlock)
-}
-
 // Ownership (cut of the assembly tree), lane sets, exchange tables. Needs P.mf (the tree) and
 // P.node_dof / P.n.
 int build_shard(const ProblemIndex& pi, Plan& P, int rank, int world, std::string& err) {

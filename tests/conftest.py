@@ -12,8 +12,8 @@ for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
 
 # Load the product library (and the ROCm 7.2 libraries it links) before any test module imports
 # torch: torch bundles its own ROCm runtime under the same sonames, and whichever loads first serves
-# the whole process. The tests exercise the library as shipped (system ROCm); bench.py, which needs
-# torch first, documents that it runs on torch's bundled runtime.
+# the whole process. The tests exercise the library as shipped (system ROCm); bench.py loads it the
+# same way, before torch.
 import bos  # noqa: E402
 
 bos.lib()

@@ -52,9 +52,9 @@ def close_state(pa, la, pb, lb, rtol=1e-6, atol=1e-9):
     return ok_p and ok_l, float(np.abs(dp).max()), float(np.abs(la - lb).max() if len(lb) else 0.0)
 
 
-def lin_parity(P, precision=bos.BOS_FP64, kt=1.0, damping=0.01, tol=1e-12, p999=None, btol=None):
+def lin_parity(P, precision=bos.BOS_FP64, kt=1.0, damping=0.01, tol=1e-12, p999=None, btol=None, **solver_kw):
     Q = to_oracle(P)
-    S = bos.Solver(P, precision=precision, kernel_threshold=kt, damping=damping)
+    S = bos.Solver(P, precision=precision, kernel_threshold=kt, damping=damping, **solver_kw)
     st = S.linearize()
     rows, cols, vals, b = S.export_system()
     lin = O.linearize(Q, kernel_threshold=kt, damping=damping, precision=32 if precision == bos.BOS_FP32 else 64)

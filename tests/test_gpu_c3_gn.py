@@ -1,22 +1,26 @@
 """GN-step parity at full config 3 on the benchmark's own world (bench.py CONFIG3: 100k poses /
 200k landmarks / 1M bearings / 99 999 odometry edges, seed 0xB05EED01 + 3), for the configuration
-bench.py times and for the fp64 path. Reference: Solver::step, slam/solver.cpp:27-97.
+bench.py times and for the fp64 path, over the iterations the bench times (it restarts from the
+initial guess for every timed run: iterations 1..K of the solve, the reference UI's batch of 50 at
+/root/reference/executables/bearing_only_slam.cpp:93-99). Reference: Solver::step,
+slam/solver.cpp:27-97.
 
 Oracle per iteration: the C++ oracle's J+H build (oracle/bos_oracle.cpp, reference accumulation
 order) + SciPy sparse direct solve of H_nf dx = -b_nf + box-plus, in the precisions the HIP path
 uses (fp64 J+H or fp32 J+H; the solve and the master state fp64).
 
 Tolerances (stated here, measured margins in DESIGN.md §5):
-  * fp64 J+H + fp64 Schur solve, 2 iterations: state within 1e-6 relative + 1e-9 absolute (the C1
-    50-iteration bound), dx of iteration 1 within 1e-8 of max |dx| (two direct factorizations of one
-    SPD system, as on C1), chi^2 within 1e-9 relative.
-  * fp32 J+H + fp64 Schur solve (the benchmarked path), 2 iterations, against the oracle's fp32 J+H
+  * fp64 J+H + fp64 Schur solve, 20 iterations: chi^2 of every iteration within 1e-9 relative, dx
+    of iteration 1 within 1e-8 of max |dx| (two direct factorizations of one SPD system, as on C1),
+    the state after 20 iterations within 1e-6 relative + 1e-9 absolute (the C1 50-iteration bound).
+  * fp32 J+H + fp64 Schur solve (the benchmarked path), 10 iterations, against the oracle's fp32 J+H
     + fp64 solve/state: the two fp32 builds sum each pose's terms in different orders, so H and b
     differ by fp32 rounding (2e-2 max-relative / 5e-4 p99.9 per entry at config 3, see
     tests/test_gpu_parity.py). dx inherits that times the conditioning of H_nf; the bounds (poses
     absolute, landmarks through the bearings they predict, chi^2 1e-3 relative) and their
     calibration against the oracle's own fp32-vs-fp64 spread are in the test's docstring.
-  * Every step reports solver_info == 0 (no non-positive pivot, no dataflow stall).
+  * Every step reports solver_info == 0 (no non-positive pivot, no dataflow stall); a system forced
+    to lose positive definiteness reports its non-positive pivots instead (slam/solver.cpp:82-84).
 """
 import numpy as np
 import pytest
@@ -47,7 +51,7 @@ def oracle_step(Q, pose, lm, jh_precision):
     return lin.chi2, dx
 
 
-def run_pair(P, precision, iters=2):
+def run_pair(P, precision, iters):
     Q = to_oracle(P)
     S = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR)
     po, lo = Q.copy_state()
@@ -63,16 +67,19 @@ def run_pair(P, precision, iters=2):
     return out, (pg, lg), (po, lo), Q
 
 
+@pytest.mark.timeout(900)
 def test_c3_gn_fp64_schur_matches_oracle(world):
-    out, (pg, lg), (po, lo), _ = run_pair(world, bos.BOS_FP64)
+    out, (pg, lg), (po, lo), _ = run_pair(world, bos.BOS_FP64, 20)
+    worst = 0.0
     for chig, chio, dxg, dxo in out:
+        worst = max(worst, abs(chig - chio) / chio)
         assert abs(chig - chio) <= 1e-9 * chio, (chig, chio)
     _, _, dxg, dxo = out[0]
     e = np.abs(dxg - dxo).max() / np.abs(dxo).max()
-    print(f"c3 fp64: dx rel err {e:.3g}")
+    print(f"c3 fp64: chi2 worst rel err over 20 iterations {worst:.3g}; dx(1) rel err {e:.3g}")
     assert e <= 1e-8
     ok, ep, el = close_state(pg, lg, po, lo, rtol=1e-6, atol=1e-9)
-    print(f"c3 fp64: state max abs err poses {ep:.3g} landmarks {el:.3g}")
+    print(f"c3 fp64 after 20 iterations: state max abs err poses {ep:.3g} landmarks {el:.3g}")
     assert ok, (ep, el)
     assert np.array_equal(pg[world.fixed], world.pose_xyt[world.fixed])
 
@@ -95,27 +102,57 @@ def fp32_state_errors(P, pg, lg, po, lo):
     return np.abs(dp).max(), np.quantile(db, 0.999), db.max()
 
 
+@pytest.mark.timeout(900)
 def test_c3_gn_fp32_jh_schur_matches_oracle(world):
     """The benchmarked configuration (fp32 J+H, fp64 Schur multifrontal solve, fp64 state) against
-    the oracle's fp32 J+H + fp64 solve and state, 2 iterations. Poses are compared in absolute
+    the oracle's fp32 J+H + fp64 solve and state, 10 iterations. Poses are compared in absolute
     terms, landmarks through the bearing each observation predicts (a
     landmark seen twice from a short baseline is weakly determined along its ray).
 
     The tolerance is calibrated by fp32 itself: the oracle's fp32 path and its fp64 path differ by
-    1.2e-2 in the poses and 1.4e-4 rad (p99.9) in the predicted bearings on this world (one
-    2-observation landmark flips sides of its poses: 3 rad at the worst bearing). The HIP fp32 path
-    must stay closer to the oracle's fp32 path than that, and within fixed bounds: poses 5e-4
-    (measured 1.2e-4), bearings p99.9 1e-4 and max 5e-3 rad (measured 3.8e-5 and 9.8e-4)."""
-    out, (pg, lg), (po, lo), Q = run_pair(world, bos.BOS_FP32)
+    1.2e-2 in the poses and 1.4e-4 rad (p99.9) in the predicted bearings on this world after 2
+    iterations (one 2-observation landmark flips sides of its poses: 3 rad at the worst bearing).
+    The HIP fp32 path must stay closer to the oracle's fp32 path than that, at every checked
+    iteration, and within fixed bounds: poses 5e-4, bearings p99.9 1e-4 and max 5e-3 rad
+    (measured values printed)."""
+    iters = 10
+    out, (pg, lg), (po, lo), Q = run_pair(world, bos.BOS_FP32, iters)
     for chig, chio, _, _ in out:
         assert abs(chig - chio) <= 1e-3 * chio, (chig, chio)
     ep, eq, eb = fp32_state_errors(world, pg, lg, po, lo)
     Q64 = to_oracle(world)
     p64, l64 = Q64.copy_state()
-    for _ in range(2):
+    for _ in range(iters):
         oracle_step(Q64, p64, l64, 64)
     rp, rq, rb = fp32_state_errors(world, po, lo, p64, l64)
-    print(f"c3 fp32 HIP vs oracle fp32 J+H: pose {ep:.3g}, bearing p99.9 {eq:.3g} max {eb:.3g} rad; "
-          f"oracle fp32 vs fp64: pose {rp:.3g}, bearing p99.9 {rq:.3g} max {rb:.3g}")
+    print(f"c3 fp32 after {iters} iterations, HIP vs oracle fp32 J+H: pose {ep:.3g}, bearing p99.9 {eq:.3g} "
+          f"max {eb:.3g} rad; oracle fp32 vs fp64: pose {rp:.3g}, bearing p99.9 {rq:.3g} max {rb:.3g}")
     assert ep <= 5e-4 and eq <= 1e-4 and eb <= 5e-3
     assert ep < rp and eq < rq
+
+
+def test_c3_fp32_reports_non_positive_pivots():
+    """A system that is not positive definite: the benchmark's world with 500 landmarks stripped of
+    every observation and the damping set to 0 (slam/solver.cpp:64-69 adds 0), so each such
+    landmark's 2 x 2 block of H is exactly zero. The fp32 J+H + Schur solve must report 2
+    non-positive pivots per such landmark in solver_info and still apply the step, as the
+    reference reports LDLT's NumericalIssue and continues (slam/solver.cpp:82-84); the observed
+    nodes' update stays finite (the zero blocks are decoupled). With the reference damping (0.01)
+    the same world reports 0."""
+    P = bos.synthetic(100000, 200000, 10, seed=BENCH_SEED)
+    rng = np.random.default_rng(9)
+    drop = rng.choice(P.NL, 500, replace=False)
+    keep = ~np.isin(P.b_lm, drop)
+    V = bos.Problem(P.pose_xyt, P.lm_xy, P.b_pose[keep], P.b_lm[keep], P.b_z[keep], P.o_src, P.o_dst, P.o_z,
+                    P.o_omega, P.fixed)
+    S = bos.Solver(V, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, damping=0.0)
+    st = S.step()
+    assert st["solver_info"] == 2 * len(drop), st
+    pg, lg = S.get_state()
+    assert np.all(np.isfinite(pg))
+    seen = np.setdiff1d(np.arange(P.NL), drop)
+    assert np.all(np.isfinite(lg[seen]))
+    S.close()
+    S = bos.Solver(V, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR)
+    assert S.step()["solver_info"] == 0
+    S.close()

@@ -277,22 +277,24 @@ def test_c3_step_properties(c3):
 
 
 def test_exchange_path_single_rank(c1):
-    """The RCCL exchange (grouped ncclBroadcast of every rank's block ranges and b ranges, and
-    the chi^2 all-reduce) run with a one-rank communicator: results equal the plain path. The
-    multi-rank partition itself is covered by tests/test_sharding.py (gloo) and the plan tests."""
+    """Both multi-GPU step forms with a one-rank RCCL communicator (subtree partition: the sharded
+    phases and their two ncclAllGather calls; observations partition: the grouped ncclAllReduce of
+    (H, b) and the chi^2 header) give the plain path's states bit for bit. The multi-rank forms are
+    covered by tests/test_sharding.py and tests/test_partitions.py (external exchange, gloo)."""
     S0 = bos.Solver(c1)
     S1 = bos.Solver(c1, rank=0, world_size=1, nccl_id=bos.nccl_unique_id())
-    a, b = S0.linearize(), S1.linearize()
-    assert a["chi2"] == b["chi2"] and a["n_robust"] == b["n_robust"]
-    r0, c0, v0, b0 = S0.export_system()
-    r1, c1_, v1, b1 = S1.export_system()
-    assert np.array_equal(v0, v1) and np.array_equal(b0, b1)
+    S2 = bos.Solver(c1, rank=0, world_size=1, nccl_id=bos.nccl_unique_id(), partition=bos.BOS_PARTITION_OBSERVATIONS)
+    assert S1.system_info()["comm_ranks"] == S2.system_info()["comm_ranks"] == 1
     for _ in range(3):
-        S0.step()
-        S1.step()
+        a, b, c = S0.step(), S1.step(), S2.step()
+        assert a["n_robust"] == b["n_robust"] == c["n_robust"]
     p0, l0 = S0.get_state()
-    p1, l1 = S1.get_state()
-    assert np.array_equal(p0, p1) and np.array_equal(l0, l1)
+    for S in (S1, S2):
+        p1, l1 = S.get_state()
+        assert np.array_equal(p0, p1) and np.array_equal(l0, l1)
+    r0, c0, v0, b0 = S0.export_system()
+    r2, c2, v2, b2 = S2.export_system()
+    assert np.array_equal(v0, v2) and np.array_equal(b0, b2)
 
 
 def test_c3_repeatable_across_handles(c3):

@@ -2,8 +2,8 @@
 than 64 rows: the workgroup factorization / forward / backward launches, mf_factor_level and
 friends, instead of the register kernels), against the oracle's GN iterations
 (/root/reference/slam/solver.cpp:27-97). The plan is forced with 40-pose Schur leaves
-(bos_debug_set_schur_leaf, a planning test hook: it changes the ordering, never the arithmetic of
-a front), as in tests/test_host.py::test_schur_plan_fallback_keeps_a_valid_plan."""
+(bos_options.schur_leaf, a planning option: it changes the ordering, never the arithmetic of a
+front), as in tests/test_host.py::test_schur_plan_fallback_keeps_a_valid_plan."""
 import pytest
 
 import bos
@@ -15,13 +15,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _solver_with_leaf(P, leaf):
-    L = bos.lib()
-    L.bos_debug_set_schur_leaf(leaf)
-    try:
-        info = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR)
-        S = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR)
-    finally:
-        L.bos_debug_set_schur_leaf(0)
+    info = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR, schur_leaf=leaf)
+    S = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR, schur_leaf=leaf)
     return S, info
 
 

@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
     missing = [n for n in sorted(names) if not hasattr(L, n)]
     assert not missing, missing
     assert set(bos.EXPORTED_SYMBOLS) == names
-    assert L.bos_abi_version() == 2
+    assert L.bos_abi_version() == bos.ABI_VERSION == 3
 
 
 @pytest.mark.skipif(bos.device_count() > 0, reason="a HIP device is visible")
@@ -251,23 +251,14 @@ def test_schur_plan_fallback_keeps_a_valid_plan():
     """When no separator balance fits (forced here with 40-pose leaves: every leaf front has more
     than 64 rows), the first (40 %) plan is kept; it still validates and solves like SciPy."""
     P = bos.load_g2o(C1)
-    L = bos.lib()
-    L.bos_debug_set_schur_leaf(40)
-    try:
-        info = bos.plan_inspect(P, 0, 1, entries=True, solver=bos.BOS_SOLVER_SCHUR)
-    finally:
-        L.bos_debug_set_schur_leaf(0)
+    info = bos.plan_inspect(P, 0, 1, entries=True, solver=bos.BOS_SOLVER_SCHUR, schur_leaf=40)
     assert not info["mf_fits"] and info["mf_balance_pct"] == 40 and info["mf_max_front"] > 64
     Q = to_oracle(P)
     lin = O.linearize(Q)
     Hl = oracle_lower_nf(Q, lin).tocsr()
     vals = np.asarray(Hl[info["rows"], info["cols"]]).ravel()
     perm = info["perm_to_ref"][:info["n"]]
-    L.bos_debug_set_schur_leaf(40)
-    try:
-        x = bos.plan_mf_selftest(P, vals, lin.b[perm], solver=bos.BOS_SOLVER_SCHUR)
-    finally:
-        L.bos_debug_set_schur_leaf(0)
+    x = bos.plan_mf_selftest(P, vals, lin.b[perm], solver=bos.BOS_SOLVER_SCHUR, schur_leaf=40)
     Hf = (Hl + sp.tril(Hl, -1).T).tocsc()
     keep = np.ones(P.N, dtype=bool)
     keep[3 * P.fixed:3 * P.fixed + 3] = False

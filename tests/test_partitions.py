@@ -1,0 +1,287 @@
+"""Both multi-GPU partitions of the GN step (include/bos.h BOS_PARTITION_*) and the
+J+H lanes-per-pose option, against the one-GPU step and the oracle.
+
+* BOS_PARTITION_OBSERVATIONS is BASELINE.json's north-star form: rank r runs a contiguous range of
+  the one-GPU plan's J+H lanes (the observations in measurement order: pose lanes hold a pose's
+  bearings and odometry entries, landmark lanes a landmark's bearings), one all-reduce (sum) of
+  (H, b) and the chi^2 header, then the one-GPU solve and box-plus on every rank. Every value of H
+  and b is written by exactly one rank (zero on the others), so the sum is exact: every rank's state
+  must equal the one-GPU state bit for bit.
+* BOS_PARTITION_SUBTREE (the default) is covered by tests/test_sharding.py; here: the odometry
+  self-loop terms of the combined chi^2 on every rank, and the calls a rank cannot answer.
+
+CPU (no GPU): the ranks' lane ranges cover every stored entry of H_nf and every b entry exactly
+once (world 2, 4, 8; C1 and a synthetic world), in-process and across gloo processes.
+GPU (one MI355X; RCCL refuses two ranks on one device, so W > 1 runs the external phase API with a
+host-side sum): W = 2, 4, 8 handles at config 2 (fp64) and the benchmark's config-3 world (fp32),
+and world 1 with an RCCL communicator (the grouped ncclAllReduce with one rank)."""
+import os
+
+import numpy as np
+import pytest
+
+import bos
+import oracle as O
+from conftest import C1
+from helpers import lin_parity, to_oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OBS = bos.BOS_PARTITION_OBSERVATIONS
+
+
+# ----------------------------------------------------------------------------- CPU
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("which", ["c1", "synthetic"])
+def test_observation_ranges_cover_every_entry_once(world, which):
+    P = bos.load_g2o(C1) if which == "c1" else bos.synthetic(3000, 6000, 10, seed=7)
+    cov, bcov, mine = None, None, []
+    for r in range(world):
+        info = bos.plan_inspect(P, r, world, entries=True, solver=bos.BOS_SOLVER_SCHUR, partition=OBS)
+        o = info["owned"].astype(np.int32)
+        b = info["b_owned"].astype(np.int32)
+        cov = o if cov is None else cov + o
+        bcov = b if bcov is None else bcov + b
+        mine.append(int(o.sum()))
+    assert np.all(cov == 1), "every stored entry of H_nf computed by exactly one rank"
+    assert np.all(bcov == 1), "every b entry written by exactly one rank"
+    assert sum(m > 0 for m in mine) >= min(world, 2)   # small worlds leave some ranks idle
+    # ranges follow the measurement order: same plan (structure) on every rank
+    one = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR)
+    assert info["nnz_lower"] == one["nnz_lower"] and info["n"] == one["n"]
+
+
+def _obs_plan_worker(rank, world, port, q):
+    try:
+        import sys
+        for p in (os.path.join(ROOT, "prb-project-bearing-only-slam_amd"), os.path.join(ROOT, "tests")):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        import bos as B
+        B.lib()
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        P = B.synthetic(3000, 6000, 10, seed=7)
+        info = B.plan_inspect(P, rank, world, entries=True, solver=B.BOS_SOLVER_SCHUR, partition=B.BOS_PARTITION_OBSERVATIONS)
+        cov = torch.from_numpy(info["owned"].astype(np.int32))
+        dist.all_reduce(cov)
+        bcov = torch.from_numpy(info["b_owned"].astype(np.int32))
+        dist.all_reduce(bcov)
+        ok = bool((cov == 1).all()) and bool((bcov == 1).all())
+        dist.destroy_process_group()
+        q.put((rank, ok, None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, False, repr(e)))
+
+
+def test_observation_ranges_across_gloo_processes():
+    """Each rank's process builds its plan alone; together (all-reduce of the ownership masks over
+    gloo) they cover every entry of H_nf and b exactly once."""
+    from test_sharding import _spawn
+    for rank, ok, _ in _spawn(_obs_plan_worker, 2, (), timeout=240):
+        assert ok, rank
+
+
+@pytest.mark.parametrize("lpp", [1, 2, 4])
+def test_lanes_per_pose_option(lpp):
+    P = bos.synthetic(1000, 2000, 20)
+    assert bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=lpp)["lanes_per_pose"] == lpp
+
+
+def test_lanes_per_pose_rejects_3():
+    P = bos.synthetic(1000, 2000, 20)
+    with pytest.raises(bos.BosError):
+        bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=3)
+
+
+def test_observation_partition_has_no_node_owner():
+    P = bos.load_g2o(C1)
+    with pytest.raises(bos.BosError):
+        L = bos.lib()
+        cs = P.c_struct()
+        o = np.zeros(P.NP + P.NL, dtype=np.int32)
+        opt = bos.options(bos.BOS_SOLVER_SCHUR, partition=OBS)
+        import ctypes
+        bos._check(L.bos_plan_node_owner(ctypes.byref(cs), ctypes.byref(opt), 2,
+                                         o.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "node_owner")
+
+
+# ----------------------------------------------------------------------------- GPU
+def _run_obs_local(P, world, iters, precision):
+    """W observation-partition handles on one GPU; the all-reduce is a host-side sum."""
+    S = [bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=world, partition=OBS)
+         for r in range(world)]
+    stats = []
+    for _ in range(iters):
+        for h in S:
+            h.step_phase(0)
+        tot = np.sum([h.exchange_download(1) for h in S], axis=0)
+        it = []
+        for h in S:
+            h.exchange_upload(1, tot)
+            it.append(h.step_phase(1))
+        stats.append(it)
+    states = [h.get_state() for h in S]
+    dx = [h.last_dx() for h in S]
+    info = [h.system_info() for h in S]
+    for h in S:
+        h.close()
+    return states, stats, dx, info
+
+
+def _run_one(P, iters, precision):
+    A = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR)
+    st = [A.step() for _ in range(iters)]
+    s = A.get_state()
+    dx = A.last_dx()
+    A.close()
+    return s, st, dx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("which", ["c2", "c3"])
+def test_observation_partition_equals_single_gpu(world, which):
+    P = bos.synthetic(1000, 2000, 20) if which == "c2" else bos.synthetic(100000, 200000, 10, seed=0xB05EED01 + 3)
+    prec = bos.BOS_FP64 if which == "c2" else bos.BOS_FP32
+    states, stats, dx, info = _run_obs_local(P, world, 3, prec)
+    (p1, l1), st1, dx1 = _run_one(P, 3, prec)
+    for r in range(world):
+        assert np.array_equal(states[r][0], p1) and np.array_equal(states[r][1], l1), r
+        assert np.array_equal(dx[r], dx1), r
+        assert info[r]["partition"] == OBS and info[r]["comm_ranks"] == 0
+        for it in range(3):
+            # the chi^2 header is summed per rank, then over ranks: equal to rounding
+            assert abs(stats[it][r]["chi2"] - st1[it]["chi2"]) <= 1e-12 * st1[it]["chi2"], (it, r)
+            assert stats[it][r]["n_robust"] == st1[it]["n_robust"]
+            assert stats[it][r]["max_abs_dx"] == st1[it]["max_abs_dx"]
+            assert stats[it][r]["solver_info"] == 0
+            assert stats[it][r]["t_linearize_ms"] > 0 and stats[it][r]["t_solve_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_observation_partition_rccl_one_rank():
+    """world 1 with a communicator: the observations partition's grouped ncclAllReduce (one rank)
+    and its two phase graphs equal the plain step bit for bit; the communicator reports 1 rank."""
+    P = bos.synthetic(1000, 2000, 20)
+    A = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR)
+    B = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR, rank=0, world_size=1, nccl_id=bos.nccl_unique_id(), partition=OBS)
+    assert B.system_info()["comm_ranks"] == 1
+    for _ in range(3):
+        a, b = A.step(), B.step()
+        assert abs(a["chi2"] - b["chi2"]) <= 1e-12 * a["chi2"] and a["max_abs_dx"] == b["max_abs_dx"]
+        assert b["t_exchange_ms"] > 0
+    b = B.step_n(5)
+    a = A.step_n(5)
+    assert a["max_abs_dx"] == b["max_abs_dx"]
+    pa, la = A.get_state()
+    pb, lb = B.get_state()
+    assert np.array_equal(pa, pb) and np.array_equal(la, lb)
+    assert np.array_equal(A.last_dx(), B.last_dx())
+    A.close()
+    B.close()
+
+
+@pytest.mark.gpu
+def test_observation_partition_export_system():
+    """After a step every rank holds the all-reduced system: its export equals the one-GPU export."""
+    P = bos.load_g2o(C1)
+    world = 3
+    S = [bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=world, partition=OBS) for r in range(world)]
+    for h in S:
+        h.step_phase(0)
+    tot = np.sum([h.exchange_download(1) for h in S], axis=0)
+    for h in S:
+        h.exchange_upload(1, tot)
+        h.step_phase(1)
+    A = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR)
+    A.step()
+    ref = A.export_system()
+    for h in S:
+        got = h.export_system()
+        for x, y in zip(got, ref):
+            assert np.array_equal(x, y)
+        with pytest.raises(bos.BosError):
+            h.linearize()
+        h.close()
+    A.close()
+
+
+def _with_self_loops(P, n=7, seed=7):
+    rng = np.random.default_rng(seed)
+    p = rng.choice(P.NP, n, replace=False).astype(np.int32)
+    z = rng.normal(0, 0.05, (n, 3))
+    z[0] = (2.0, -1.0, 0.5)   # rho far above the kernel threshold
+    return bos.Problem(P.pose_xyt, P.lm_xy, P.b_pose, P.b_lm, P.b_z, np.concatenate([P.o_src, p]),
+                       np.concatenate([P.o_dst, p]), np.concatenate([P.o_z, z]),
+                       np.concatenate([P.o_omega, P.o_omega[:n]]), P.fixed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("partition", [bos.BOS_PARTITION_SUBTREE, OBS])
+def test_sharded_self_loops_every_rank(partition):
+    """Odometry self-loops add a constant chi^2 no J+H lane counts: every rank's combined chi^2 and
+    robust count include them once (both partitions), equal to the one-GPU step's."""
+    from test_sharding import _run_local_shards
+    P = _with_self_loops(bos.synthetic(1000, 2000, 20))
+    (p1, l1), st1, _ = _run_one(P, 3, bos.BOS_FP64)
+    if partition == OBS:
+        states, stats, _, _ = _run_obs_local(P, 4, 3, bos.BOS_FP64)
+        for r in range(4):
+            assert np.array_equal(states[r][0], p1) and np.array_equal(states[r][1], l1)
+    else:
+        (pm, lm_), stats, _, _, _ = _run_local_shards(P, 4, 3, bos.BOS_FP64)
+        assert np.array_equal(pm, p1) and np.array_equal(lm_, l1)
+    for it in range(3):
+        for r in range(4):
+            assert abs(stats[it][r]["chi2"] - st1[it]["chi2"]) <= 1e-12 * st1[it]["chi2"], (it, r)
+            assert stats[it][r]["n_robust"] == st1[it]["n_robust"], (it, r)
+
+
+@pytest.mark.gpu
+def test_subtree_sharded_handle_refuses_partial_answers():
+    """A subtree-sharded rank holds H and x of its own, top and boundary nodes only: bos_linearize,
+    bos_export_system and bos_get_last_dx are BOS_ERR_UNSUPPORTED instead of partial results."""
+    P = bos.synthetic(1000, 2000, 20)
+    S = [bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=2) for r in range(2)]
+    for h in S:
+        h.step_phase(0)
+    recv = np.concatenate([h.exchange_download(1) for h in S])
+    for h in S:
+        h.exchange_upload(1, recv)
+        h.step_phase(1)
+    recv = np.concatenate([h.exchange_download(2) for h in S])
+    for h in S:
+        h.exchange_upload(2, recv)
+        h.step_phase(2)
+    for h in S:
+        for call in (h.linearize, h.export_system, h.last_dx):
+            with pytest.raises(bos.BosError) as e:
+                call()
+            assert "(-5)" in str(e.value)
+        h.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lpp", [2, 4])
+@pytest.mark.parametrize("which", ["c1", "c2"])
+def test_lanes_per_pose_matches_oracle(lpp, which):
+    """lanes_per_pose 2 and 4 (bearing segments per pose, the lane group's butterfly combine):
+    H and b against the oracle at the fp64 bounds, and 3 GN steps against the oracle's."""
+    P = bos.load_g2o(C1) if which == "c1" else bos.synthetic(1000, 2000, 20)
+    lin_parity(P, lanes_per_pose=lpp)
+    Q = to_oracle(P)
+    S = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=lpp)
+    assert S.system_info()["lanes_per_pose"] == lpp
+    for _ in range(3):
+        assert S.step()["solver_info"] == 0
+    pg, lg = S.get_state()
+    S.close()
+    po, lo = Q.copy_state()
+    for _ in range(3):
+        O.step(Q, po, lo)
+    from helpers import close_state
+    ok, ep, el = close_state(pg, lg, po, lo)
+    assert ok, (ep, el)

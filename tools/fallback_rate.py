@@ -3,13 +3,10 @@ import os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "prb-project-bearing-only-slam_amd"))
 import bos
 P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
-L = bos.lib()
 for leaf in (0, 40):
-    L.bos_debug_set_schur_leaf(leaf)
     t = time.perf_counter()
-    info = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR)
-    S = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR)
-    L.bos_debug_set_schur_leaf(0)
+    info = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR, schur_leaf=leaf)
+    S = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, schur_leaf=leaf)
     tc = time.perf_counter() - t
     st = S.step()
     init = S.get_state()

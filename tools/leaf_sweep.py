@@ -1,4 +1,4 @@
-"""Schur ordering leaf size vs GN time on config 3 (experiments; bos_debug_set_schur_leaf).
+"""Schur ordering leaf size vs GN time on config 3 (experiments; bos_options.schur_leaf).
 Usage: python tools/leaf_sweep.py 10 8 12 ..."""
 import os
 import sys
@@ -11,10 +11,9 @@ import bos  # noqa: E402
 
 P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
 for leaf in [int(a) for a in sys.argv[1:]]:
-    bos.lib().bos_debug_set_schur_leaf(leaf)
     t0 = time.perf_counter()
-    info = bos.plan_inspect(P, solver=bos.BOS_SOLVER_SCHUR)
-    S = bos.Solver(P, precision=bos.BOS_FP32, device=0)
+    info = bos.plan_inspect(P, solver=bos.BOS_SOLVER_SCHUR, schur_leaf=leaf)
+    S = bos.Solver(P, precision=bos.BOS_FP32, device=0, solver=bos.BOS_SOLVER_SCHUR, schur_leaf=leaf)
     tc = time.perf_counter() - t0
     S.step()
     st = [S.step() for _ in range(10)]
@@ -26,4 +25,3 @@ for leaf in [int(a) for a in sys.argv[1:]]:
           f"fits {info['mf_fits']} balance {info['mf_balance_pct']} flops {info['mf_flops']:.3g} nnzL {info['nnz_factor']} "
           f"create+plan {tc:.1f} s  solve {sol:.1f} us  GN batched {it:.0f} it/s chi2 {st[-1]['chi2']:.8e}", flush=True)
     S.close()
-bos.lib().bos_debug_set_schur_leaf(0)
