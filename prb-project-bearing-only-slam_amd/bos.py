@@ -445,6 +445,7 @@ class Solver:
         bos_options fields of the same names."""
         L = lib()
         self.P = P
+        self.partition = partition
         opt = bos_options()
         L.bos_default_options(ctypes.byref(opt))
         opt.precision, opt.solver, opt.device = precision, solver, device
@@ -513,9 +514,11 @@ class Solver:
 
     # ---- sharded (multi-GPU) step, external exchange: see include/bos.h
     def step_phase(self, phase: int):
+        """One phase of an external-exchange step; returns the step's stats from its last phase
+        (2 for the subtree partition, 1 for the observations partition), else None."""
         st = bos_step_stats()
         _check(lib().bos_step_phase(self._h, phase, ctypes.byref(st)), f"bos_step_phase({phase})")
-        if phase == 2:
+        if phase == (1 if self.partition == BOS_PARTITION_OBSERVATIONS else 2):
             self.last_stats = st.as_dict()
             return self.last_stats
         return None

@@ -20,6 +20,16 @@
 
 #include "../host/bos_math.hpp"
 
+// J+H build variants (measurement builds only; the defaults are the product): pose items per chunk
+// of the ILP lanes (fp32) and their waves-per-SIMD bound; BOS_JH_PAIRS selects the pair loop for
+// every launch
+#ifndef BOS_JH_NIP
+#define BOS_JH_NIP 12
+#endif
+#ifndef BOS_JH_MINW
+#define BOS_JH_MINW 4
+#endif
+
 namespace bos {
 namespace dev {
 
@@ -363,6 +373,164 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int blk, un
     bl[0] = gl[0]; bl[1] = gl[1];
 }
 
+// ---- the J+H with every load of a lane issued up front (the common case: unit bearing weights,
+// no duplicate pairs). A lane's inputs are three dependent hops away — its header (count, list base
+// and stride, pose, odometry range), its records (landmark index and z of each item, the odometry
+// entries), then the gathers (landmark / pose state, the odometry edges' other pose and data) — and
+// each hop costs a memory latency (1.5-2 us from HBM under this kernel's load). Here the records of
+// the first NI items are read at once (indices clamped to the lane's last item, no predicated
+// loads: a predicated load is a branch with its wait inside), then all their gathers, then the
+// arithmetic: three latencies per lane instead of three plus one per pair of items. Lists longer
+// than NI continue in chunks of NI. Same arithmetic in the same order as the pair loop above (the
+// result is bit-identical to it).
+template <typename T, int NI>
+struct PoseChunk {
+    int idx[NI];
+    T z[NI];
+};
+
+template <typename T, int LPP, int NI>
+__device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int blk, double& chi, int& nrob,
+                                               unsigned long long* st) {
+    const int g = blk * kBlock + threadIdx.x;   // lane
+    const int grp = g / LPP, sub = g % LPP, t = g & 63;
+    const int p = grp < P.n_groups ? (P.lane_pose ? P.lane_pose[grp] : grp) : -1;
+    const bool active = p >= 0;
+    T h[6] = {0, 0, 0, 0, 0, 0}, gb[3] = {0, 0, 0};
+    if (active) {
+        // hop 1: addressed by the lane and its pose only
+        const V4<T> X = load4(P.pc + 4 * p);
+        const T th = P.pth[p];
+        const int n = P.pl_cnt[g];
+        const int sl = P.pw_base[g >> 6] + t;   // slot of item j: sl + S j
+        const int S = P.pw_stride[g >> 6];
+        const int x0 = P.po_ptr[p], x1 = P.po_ptr[p + 1];
+        // hop 2: the records of items 0 .. NI - 1 (clamped to the last item; padded arrays) and the
+        // first two odometry entries (lane 0 of the group walks them; the arrays are padded)
+        const int jl = n > 0 ? n - 1 : 0;
+        PoseChunk<T, NI> c;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int sj = sl + S * min(i, jl);
+            c.idx[i] = P.pb_idx[sj];
+            c.z[i] = P.pb_z[sj];
+        }
+        const int ne = sub == 0 ? x1 - x0 : 0;
+        OdoIn<T> oa, ob;
+        int otha, othb;
+        odo_fetch_ids(P, x0, oa, otha);
+        odo_fetch_ids(P, x0 + 1 < x1 ? x0 + 1 : x0, ob, othb);
+        // hop 3: every gather
+        V2<T> L[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) L[i] = load2(P.lc + 2 * (c.idx[i] & kIdxMask));
+        odo_fetch_data(P, otha, oa);
+        odo_fetch_data(P, othb, ob);
+        // odometry first, then the bearings (the pair loop's order)
+        T acc6[6] = {0, 0, 0, 0, 0, 0};
+        if (ne > 0) odometry_entry<T, false>(P, x0, x1, oa, X, th, h, gb, acc6, chi, nrob);
+        if (ne > 1) odometry_entry<T, false>(P, x0 + 1, x1, ob, X, th, h, gb, acc6, chi, nrob);
+        for (int x = x0 + 2; x < x0 + ne; ++x) {
+            OdoIn<T> oc;
+            int othc;
+            odo_fetch_ids(P, x, oc, othc);
+            odo_fetch_data(P, othc, oc);
+            odometry_entry<T, false>(P, x, x1, oc, X, th, h, gb, acc6, chi, nrob);
+        }
+        stamp(P.diag_stamps, st, 1);
+        T* const blk0 = P.hval + P.off_pl + 6 * (int64_t)sl;
+        T o[6];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            if (i < n) {
+                pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob);
+                store6(blk0 + 6 * (int64_t)S * i, o[0], o[1], o[2], o[3], o[4], o[5]);
+            }
+        }
+        // items past NI (lists longer than NI: not at config 3), NI at a time
+        for (int j0 = NI; j0 < n; j0 += NI) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int sj = sl + S * min(j0 + i, jl);
+                c.idx[i] = P.pb_idx[sj];
+                c.z[i] = P.pb_z[sj];
+            }
+#pragma unroll
+            for (int i = 0; i < NI; ++i) L[i] = load2(P.lc + 2 * (c.idx[i] & kIdxMask));
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                if (j0 + i < n) {
+                    pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob);
+                    store6(blk0 + 6 * (int64_t)S * (j0 + i), o[0], o[1], o[2], o[3], o[4], o[5]);
+                }
+            }
+        }
+        stamp(P.diag_stamps, st, 2);
+    }
+    // combine the lane group's partial sums (fixed butterfly: deterministic)
+#pragma unroll
+    for (int o = 1; o < LPP; o <<= 1) {
+#pragma unroll
+        for (int v = 0; v < 6; ++v) h[v] += __shfl_xor(h[v], o);
+#pragma unroll
+        for (int v = 0; v < 3; ++v) gb[v] += __shfl_xor(gb[v], o);
+    }
+    if (active && sub == 0) {
+        const T lam = P.lambda;
+        store6(P.hval + 6 * p, h[0] + lam, h[1], h[2] + lam, h[3], h[4], h[5] + lam);
+        T* bp = P.b + 3 * p;
+        bp[0] = gb[0]; bp[1] = gb[1]; bp[2] = gb[2];
+    }
+}
+
+template <typename T, int NI>
+__device__ __forceinline__ void landmark_lane_ilp(const LinParams<T>& P, int blk, unsigned long long* st) {
+    const int g = blk * kBlock + threadIdx.x;   // lane
+    if (g >= P.n_lm_lanes) return;
+    // hop 1: the lane's header
+    const int l = P.ll_lm[g];
+    const int n = P.ll_cnt[g];
+    const int sl = P.lw_base[g >> 6] + (g & 63);
+    const int S = P.lw_stride[g >> 6];
+    const int jl = n > 0 ? n - 1 : 0;
+    // hop 2: the landmark and the records of items 0 .. NI - 1; hop 3: the pose gathers
+    const V2<T> Lm = load2(P.lc + 2 * l);
+    int idx[NI];
+    T z[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int sj = sl + S * min(i, jl);
+        idx[i] = P.lb_idx[sj];
+        z[i] = P.lb_z[sj];
+    }
+    V4<T> X[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) X[i] = load4(P.pc + 4 * idx[i]);
+    stamp(P.diag_stamps, st, 1);
+    T hl[3] = {0, 0, 0}, gl[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+        if (i < n) landmark_bearing<T>(P, X[i], Lm, z[i], (T)1, hl, gl);
+    for (int j0 = NI; j0 < n; j0 += NI) {   // lists longer than NI
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int sj = sl + S * min(j0 + i, jl);
+            idx[i] = P.lb_idx[sj];
+            z[i] = P.lb_z[sj];
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) X[i] = load4(P.pc + 4 * idx[i]);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            if (j0 + i < n) landmark_bearing<T>(P, X[i], Lm, z[i], (T)1, hl, gl);
+    }
+    stamp(P.diag_stamps, st, 2);
+    T* hp = P.hval + P.off_ldiag + 3 * l;
+    hp[0] = hl[0] + P.lambda; hp[1] = hl[1]; hp[2] = hl[2] + P.lambda;
+    T* bl = P.b + 3 * P.NP + 2 * l;
+    bl[0] = gl[0]; bl[1] = gl[1];
+}
+
 // XCD-aware block order: blocks b and b + 8 share an XCD (and its L2), so a segment [s0, s1) of
 // the grid is renumbered to give each XCD a contiguous run of it; the pose (landmark) blocks an
 // XCD runs then cover a stretch of the trajectory, and the landmark (pose) cache lines their
@@ -394,6 +562,41 @@ __global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams
     pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, pb0, chi, nrob, st);
     stamp_flush(P.diag_stamps, st, 0);
     // per-block chi^2 / robust count in a fixed order
+    __shared__ double sc[kBlock / 64];
+    __shared__ int sr[kBlock / 64];
+    chi = wave_sum(chi);
+    nrob = (int)wave_sum((double)nrob);
+    if ((threadIdx.x & 63) == 0) { sc[threadIdx.x >> 6] = chi; sr[threadIdx.x >> 6] = nrob; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double c = 0.0;
+        int r = 0;
+        for (int w = 0; w < kBlock / 64; ++w) { c += sc[w]; r += sr[w]; }
+        P.chi2_part[pb0] = c;
+        P.nrob_part[pb0] = r;
+    }
+}
+
+// The J+H launch of the common case (unit weights, no duplicate pairs): the ILP lanes above.
+template <typename T, int LPP, int NIP, int NIL, int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void linearize_ilp_kernel(const LinParams<T> P) {
+    const int64_t nb = gridDim.x;
+    const int64_t b = blockIdx.x < P.n_pose_run
+                          ? P.pose_b0 + xcd_contiguous(blockIdx.x, 0, P.n_pose_run)
+                          : P.pose_blocks + P.lm_b0 + xcd_contiguous(blockIdx.x, P.n_pose_run, nb) - P.n_pose_run;
+    unsigned long long st[3] = {0, 0, 0};
+    if (P.t_start && blockIdx.x == 0 && threadIdx.x == 0) *P.t_start = __builtin_amdgcn_s_memrealtime();
+    stamp(P.diag_stamps, st, 0);
+    if (b >= P.pose_blocks) {   // block-uniform branch
+        landmark_lane_ilp<T, NIL>(P, (int)(b - P.pose_blocks), st);
+        stamp_flush(P.diag_stamps, st, 1);
+        return;
+    }
+    const int pb0 = (int)b;
+    double chi = 0.0;
+    int nrob = 0;
+    pose_lanes_ilp<T, LPP, NIP>(P, pb0, chi, nrob, st);
+    stamp_flush(P.diag_stamps, st, 0);
     __shared__ double sc[kBlock / 64];
     __shared__ int sr[kBlock / 64];
     chi = wave_sum(chi);
@@ -757,8 +960,32 @@ hipError_t launch_lin_k(LinParams<T> p, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <typename T, int LPP, int MINW>
+hipError_t launch_lin_ilp(LinParams<T> p, hipStream_t s) {
+    const int lm_blocks = (p.n_lm_lanes + kBlock - 1) / kBlock;
+    if (p.pose_b0 < 0 || p.n_pose_run < 0 || p.pose_b0 + p.n_pose_run > p.pose_blocks || p.lm_b0 < 0 || p.n_lm_run < 0 ||
+        p.lm_b0 + p.n_lm_run > lm_blocks)
+        return hipErrorInvalidValue;
+    const int grid = p.n_pose_run + p.n_lm_run;
+    if (grid == 0) return hipSuccess;
+    // items read per chunk: 12 pose / 8 landmark items (fp32), 8 / 8 (fp64: twice the registers)
+    constexpr int NIP = sizeof(T) == 4 ? BOS_JH_NIP : 8, NIL = 8;
+    hipLaunchKernelGGL((linearize_ilp_kernel<T, LPP, NIP, NIL, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+}
+
 template <typename T, bool W, bool D, int MINW>
 hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, hipStream_t s) {
+#ifndef BOS_JH_PAIRS
+    if (!W && !D) {   // the common case: every load of a lane up front
+        switch (lpp) {
+            case 1: return launch_lin_ilp<T, 1, BOS_JH_MINW>(p, s);
+            case 2: return launch_lin_ilp<T, 2, BOS_JH_MINW>(p, s);
+            case 4: return launch_lin_ilp<T, 4, BOS_JH_MINW>(p, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
+#endif
     switch (lpp) {
         case 1: return launch_lin_k<T, W, D, 1, MINW>(p, s);
         case 2: return launch_lin_k<T, W, D, 2, MINW>(p, s);

@@ -129,20 +129,21 @@ struct FoldAcc {
 
 // Assembly of H entries into a front by one wavefront (F[dst] = A[src], or += when the front
 // already holds the folded landmarks' part), 4 entries per lane in flight: index loads, then value
-// gathers, then LDS stores.
-__device__ __forceinline__ void assemble_wave(const MfArgs& a, int s, double* F, int lane, bool add) {
-    const int q1 = a.amap_ptr[s + 1];
-    for (int q0 = a.amap_ptr[s]; q0 < q1; q0 += 256) {
+// gathers, then LDS stores. Loads past the front's range are clamped to its last entry instead of
+// predicated: a predicated load becomes a branch with the load's wait inside it, which serialises
+// the four loads (one memory latency each instead of one for all four).
+__device__ __forceinline__ void assemble_wave(const MfArgs& a, int q0_, int q1, double* F, int lane, bool add) {
+    for (int q0 = q0_; q0 < q1; q0 += 256) {
         int src[4], dst[4];
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int q = q0 + 64 * u + lane;
-            src[u] = q < q1 ? a.amap_src[q] : 0;
-            dst[u] = q < q1 ? a.amap_dst[q] : 0;
+            const int q = min(q0 + 64 * u + lane, q1 - 1);
+            src[u] = a.amap_src[q];
+            dst[u] = a.amap_dst[q];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = q0 + 64 * u + lane < q1 ? a.A[src[u]] : 0.0;
+        for (int u = 0; u < 4; ++u) v[u] = a.A[src[u]];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if (q0 + 64 * u + lane < q1) F[dst[u]] = add ? F[dst[u]] + v[u] : v[u];
@@ -315,16 +316,37 @@ struct FoldVals {
 };
 
 __device__ __forceinline__ FoldVals fold_vals(const MfArgs& a, const int4& r0, const int4& r1, bool mine) {
+    // every load unconditional (indices clamped to valid ones), the value selected afterwards: a
+    // predicated load would be a branch with its wait inside, and the next chunk's values must stay
+    // in flight while the current chunk is processed
+    const double ht0 = a.A[max(r0.x, 0)], ht1 = a.A[max(r0.y, 0)], a00 = a.A[max(r0.z, 0)], a10 = a.A[max(r0.w, 0)];
+    const double a11 = a.A[max(r1.x, 0)];
+    const int xi = mine ? r1.y : 0;
+    const double x0 = a.x[xi], x1 = a.x[xi + 1];
     FoldVals v;
-    v.ht0 = r0.x >= 0 ? a.A[r0.x] : 0.0;
-    v.ht1 = r0.y >= 0 ? a.A[r0.y] : 0.0;
-    v.a00 = r0.z >= 0 ? a.A[r0.z] : 0.0;
-    v.a10 = r0.w >= 0 ? a.A[r0.w] : 0.0;
-    v.a11 = r1.x >= 0 ? a.A[r1.x] : 0.0;
-    v.x0 = mine ? a.x[r1.y] : 0.0;
-    v.x1 = mine ? a.x[r1.y + 1] : 0.0;
+    v.ht0 = r0.x >= 0 ? ht0 : 0.0;
+    v.ht1 = r0.y >= 0 ? ht1 : 0.0;
+    v.a00 = r0.z >= 0 ? a00 : 0.0;
+    v.a10 = r0.w >= 0 ? a10 : 0.0;
+    v.a11 = r1.x >= 0 ? a11 : 0.0;
+    v.x0 = mine ? x0 : 0.0;
+    v.x1 = mine ? x1 : 0.0;
     return v;
 }
+
+// The chunk boundaries of a front (fold_chunk[c], c uniform) from one register holding 64 of them
+// (lane i: fold_chunk[base + i]), re-read only when a front has more chunks than that: the loop then
+// needs no dependent load per chunk (a vector load whose value decides the next loads would make
+// the wave wait for every load issued before it, the prefetched values included).
+struct ChunkTable {
+    int base, v;
+    __device__ __forceinline__ void load(const MfArgs& a, int b, int lane) {
+        base = b;
+        v = a.fold_chunk[b + lane];   // padded array (up()): in bounds
+    }
+    // fold_chunk[c] for c in [base, base + 64)
+    __device__ __forceinline__ int at(int c) const { return __builtin_amdgcn_readlane(v, c - base); }
+};
 
 template <int MAXM>
 __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W, FoldBuf* fb, int m, int lane,
@@ -337,15 +359,26 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
     acc.w = 0.0;
     for (int e = lane; e < MAXM * WS; e += 64) W[e] = 0.0;
     const int ch0 = a.fold_cptr[s], ch1 = a.fold_cptr[s + 1];
-    int n = a.fold_chunk[ch0 + 1] - a.fold_chunk[ch0];
-    int4 r0 = make_int4(-1, -1, -1, -1), r1 = make_int4(0, 0, 0, 0);
-    if (lane < n) { r0 = fold_rec_load(a, a.fold_chunk[ch0] + lane, 0); r1 = fold_rec_load(a, a.fold_chunk[ch0] + lane, 1); }
+    ChunkTable tb;
+    tb.load(a, ch0, lane);
+    // chunk c: rows [at(c), at(c + 1)); records of a lane past the chunk's rows (or of a chunk past
+    // the front's last) are read at a valid index and never used
+    auto rec = [&](int c, int n, int4& q0, int4& q1) {
+        const int q = tb.at(c) + min(lane, max(n - 1, 0));
+        q0 = fold_rec_load(a, q, 0);
+        q1 = fold_rec_load(a, q, 1);
+    };
+    auto len = [&](int c) { return c < ch1 ? tb.at(c + 1) - tb.at(c) : 0; };
+    int n = len(ch0);
+    int4 r0, r1;
+    rec(ch0, n, r0, r1);
     FoldVals v = fold_vals(a, r0, r1, lane < n);
     // next chunk's records, then (inside the loop) its values, both one chunk ahead
-    int nn = ch0 + 1 < ch1 ? a.fold_chunk[ch0 + 2] - a.fold_chunk[ch0 + 1] : 0;
-    int4 n0 = make_int4(-1, -1, -1, -1), n1 = make_int4(0, 0, 0, 0);
-    if (lane < nn) { n0 = fold_rec_load(a, a.fold_chunk[ch0 + 1] + lane, 0); n1 = fold_rec_load(a, a.fold_chunk[ch0 + 1] + lane, 1); }
+    int nn = len(ch0 + 1);
+    int4 n0, n1;
+    rec(ch0 + 1, nn, n0, n1);
     for (int ch = ch0; ch < ch1; ++ch) {
+        if (ch + 3 - tb.base > 63) tb.load(a, ch, lane);   // (uniform; fronts with > 60 chunks only)
         const double ht0 = v.ht0, ht1 = v.ht1, a00 = v.a00, a10 = v.a10, a11 = v.a11;
         const int t = r1.z & 63, rc = (r1.z >> 6) & 63, pos = (r1.z >> 12) & 63, lml = (r1.z >> 18) & 63;
         const bool mine = lane < n;
@@ -357,8 +390,8 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
         v = fold_vals(a, n0, n1, lane < nn);
         r0 = n0;
         r1 = n1;
-        const int n2 = ch + 2 < ch1 ? a.fold_chunk[ch + 3] - a.fold_chunk[ch + 2] : 0;
-        if (lane < n2) { n0 = fold_rec_load(a, a.fold_chunk[ch + 2] + lane, 0); n1 = fold_rec_load(a, a.fold_chunk[ch + 2] + lane, 1); }
+        const int n2 = len(ch + 2);
+        rec(ch + 2, n2, n0, n1);
         if (mine) {
             double d0 = a00;
             int bad = 0;
@@ -556,25 +589,38 @@ struct ChildPre {
     const int16_t* ec;
 };
 
+// (Every structure and value array is padded by kMfPad elements, so the clamped reads below stay in
+// bounds even for an empty child range; see up().)
 __device__ __forceinline__ void child_meta(const MfArgs& a, int c, int lane, ChildPre& p) {
     const int rc = a.r[c];   // rc < m <= MAXM
+    const int roff = a.rmap_off[c];
     p.rc = rc;
-    p.smap_v = lane < rc ? a.rmap[a.rmap_off[c] + lane] : 0;
     p.Uc = a.U + a.U_off[c];
     p.uc = a.u + a.u_off[c];
     p.ec = a.emap + a.emap_off[c];
+    const int sv = a.rmap[roff + min(lane, max(rc - 1, 0))];
+    p.smap_v = lane < rc ? sv : 0;
     const int ne = rc * (rc + 1) / 2;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) p.pos[u] = 64 * u + lane < ne ? p.ec[64 * u + lane] : 0;
+    for (int u = 0; u < 4; ++u) {
+        const int e = 64 * u + lane;
+        const int pv = p.ec[min(e, max(ne - 1, 0))];
+        p.pos[u] = e < ne ? pv : 0;
+    }
 }
 
 template <bool COH>
 __device__ __forceinline__ void child_vals(int lane, ChildPre& p) {
     const int rc = p.rc;
-    p.uval = lane < rc ? ldc<COH>(p.uc + lane) : 0.0;
+    const double uv = ldc<COH>(p.uc + min(lane, max(rc - 1, 0)));
+    p.uval = lane < rc ? uv : 0.0;
     const int ne = rc * (rc + 1) / 2;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) p.v[u] = 64 * u + lane < ne ? ldc<COH>(p.Uc + 64 * u + lane) : 0.0;
+    for (int u = 0; u < 4; ++u) {
+        const int e = 64 * u + lane;
+        const double v = ldc<COH>(p.Uc + min(e, max(ne - 1, 0)));
+        p.v[u] = e < ne ? v : 0.0;
+    }
 }
 
 // Extend-add of one child: every entry of its packed update matrix added at its precomputed position
@@ -588,9 +634,9 @@ __device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p,
         int pos[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int e = e0 + 64 * u + lane;
-            v[u] = e0 == 0 ? p.v[u] : (e < ne ? ldc<COH>(p.Uc + e) : 0.0);
-            pos[u] = e0 == 0 ? p.pos[u] : (e < ne ? p.ec[e] : 0);
+            const int e = min(e0 + 64 * u + lane, ne - 1);   // clamped (see assemble_wave)
+            v[u] = e0 == 0 ? p.v[u] : ldc<COH>(p.Uc + e);
+            pos[u] = e0 == 0 ? p.pos[u] : p.ec[e];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -612,6 +658,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     const int k = a.k[s], r = a.r[s], m = k + r;
     const int nfold = a.fold_cnt[s];
     const int c0 = a.col0[s];
+    const int aq0 = a.amap_ptr[s], aq1 = a.amap_ptr[s + 1];   // the assembly's range, loaded up front
     const int np = m * (m + 1) / 2;
     const double xo = lane < k ? a.x[c0 + lane] : 0.0;   // right-hand side of the own dofs (k < 64)
     // output offsets up front: their loads complete during the assembly instead of before the pivots
@@ -642,7 +689,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     }
     wave_sync();
     fstamp(stp, s, 1);
-    assemble_wave(a, s, F, lane, fold);
+    assemble_wave(a, aq0, aq1, F, lane, fold);
     wave_sync();
     fstamp(stp, s, 2);
     if constexpr (FLOW) {
@@ -819,14 +866,16 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
     double* t = w + k;
     double* xs = w + 2 * k;
     double* Lw = w + 2 * k + r;
-    const int xi0 = lane < r ? fi[k + lane] : 0;   // where the first 64 rows' x live (static)
+    // where the first 64 rows' x live (static); clamped, branch-free reads (see assemble_wave)
+    const int xi0 = fi[k + min(lane, max(r - 1, 0))];
     unsigned long long* const stp = f ? f->stamps : a.stamps_b;
     fstamp(stp, s, 0);
     if constexpr (!FLOW) {
         // per-level launch: the parents' x are final (earlier launches), so the front's own
         // right-hand side and the first 64 rows' x are loaded beside the panel, all in flight at once
-        const double y0 = lane < k ? a.x[c0 + lane] : 0.0;
-        const double xr0 = lane < r ? a.x[xi0] : 0.0;
+        const double y0v = a.x[c0 + min(lane, k - 1)], xr0v = a.x[xi0];
+        const double y0 = lane < k ? y0v : 0.0;
+        const double xr0 = lane < r ? xr0v : 0.0;
         stage_lds<16>(Lw, a.L + a.L_off[s], m * k, lane);
         if (lane < k) w[lane] = y0;
         for (int j = 64 + lane; j < k; j += 64) w[j] = a.x[c0 + j];
@@ -923,8 +972,11 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const int32_t* fi = a.findex + (valid ? a.findex_off[s] : 0) + 2;
     const int c0 = valid ? a.col0[s] : 0;
     const bool head = valid && q0 == 0;
-    double y0 = 0.0, y1 = 0.0, L00 = 1.0, L10 = 0.0, L11 = 1.0;
-    if (head) { y0 = a.x[c0]; y1 = a.x[c0 + 1]; L00 = Ls[0]; L10 = Ls[1]; L11 = Ls[m + 1]; }
+    // the landmark's own values, read by all its lanes (one address: no extra traffic) so no branch
+    // holds a wait; only the head lane uses them
+    const double y0v = a.x[c0], y1v = a.x[c0 + 1], L00v = Ls[0], L10v = Ls[1], L11v = Ls[m + 1];
+    const double y0 = head ? y0v : 0.0, y1 = head ? y1v : 0.0;
+    const double L00 = head ? L00v : 1.0, L10 = head ? L10v : 0.0, L11 = head ? L11v : 1.0;
     double t0 = 0.0, t1 = 0.0;
     const int rl = r > 0 ? r - 1 : 0;   // reads of rows past r are clamped (and their products dropped)
     for (int q = q0; q < r; q += 4 * kFoldLanes) {
@@ -1007,11 +1059,17 @@ __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flo
     leave_flow(f);
 }
 
+// Structure arrays carry kMfPad zeroed elements after their end: the kernels read clamped indices
+// unconditionally (branch-free loads, see assemble_wave) and may touch up to one chunk / 64 lanes past
+// a range's last element.
+constexpr int64_t kMfPad = 64;
 template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
     *p = nullptr;
     if (v.empty()) return 0;
-    if (hipMalloc((void**)p, v.size() * sizeof(X)) != hipSuccess) { err = "hipMalloc failed (multifrontal)"; return -2; }
-    if (hipMemcpy(*p, v.data(), v.size() * sizeof(X), hipMemcpyHostToDevice) != hipSuccess) {
+    const size_t bytes = v.size() * sizeof(X), padded = bytes + kMfPad * sizeof(X);
+    if (hipMalloc((void**)p, padded) != hipSuccess) { err = "hipMalloc failed (multifrontal)"; return -2; }
+    if (hipMemcpy(*p, v.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset((char*)*p + bytes, 0, padded - bytes) != hipSuccess) {
         err = "hipMemcpy failed (multifrontal)";
         return -2;
     }
@@ -1285,9 +1343,10 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         err = "side stream creation failed (multifrontal)";
         return -2;
     }
-    auto alloc = [&](double** p, int64_t n) -> int {
+    auto alloc = [&](double** p, int64_t n) -> int {   // + kMfPad: clamped reads (up())
         if (n <= 0) n = 1;
-        if (hipMalloc((void**)p, n * sizeof(double)) != hipSuccess) { err = "hipMalloc failed (multifrontal buffers)"; return -2; }
+        if (hipMalloc((void**)p, (n + kMfPad) * sizeof(double)) != hipSuccess) { err = "hipMalloc failed (multifrontal buffers)"; return -2; }
+        if (hipMemset(*p, 0, (n + kMfPad) * sizeof(double)) != hipSuccess) { err = "hipMemset failed (multifrontal buffers)"; return -2; }
         return 0;
     };
     if ((rc = alloc(&d->L, F.L_size)) || (rc = alloc(&d->U, F.U_size)) || (rc = alloc(&d->u, F.u_size)) ||

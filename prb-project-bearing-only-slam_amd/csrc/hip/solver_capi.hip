@@ -1015,8 +1015,12 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
                     if (pbi[sl] == pbi[sn]) pbi[sl] |= bos::dev::kRunCont;
                 }
         }
-        std::vector<int32_t> po_oth(B.po_ent.size());
-        for (size_t x = 0; x < po_oth.size(); ++x) {
+        // odometry entries, padded (entry 0 / other pose 0 / no block): the J+H reads a pose's first
+        // two entries unconditionally, in bounds even for the last pose without entries
+        std::vector<int32_t> po_oth(B.po_ent.size() + pad, 0), po_ent(B.po_ent), po_blk(B.po_blk);
+        po_ent.resize(B.po_ent.size() + pad, 0);
+        po_blk.resize(B.po_blk.size() + pad, -1);
+        for (size_t x = 0; x < B.po_ent.size(); ++x) {
             const int32_t e = B.po_ent[x];
             po_oth[x] = (e & 1) ? pb->odom_src[e >> 1] : pb->odom_dst[e >> 1];
         }
@@ -1024,9 +1028,9 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             (rc = upload(&s->pw_stride, B.pose_lanes.w_stride)) || (rc = upload(&s->lw_stride, B.lm_lanes.w_stride)) ||
             (rc = upload(&s->lw_base, B.lm_lanes.w_base)) || (rc = upload(&s->ll_cnt, B.lm_lanes.cnt)) ||
             (rc = upload(&s->ll_lm, B.lm_lane_lm)) ||
-            (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, B.po_ent)) ||
+            (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, po_ent)) ||
             (rc = upload(&s->po_oth, po_oth)) ||
-            (rc = upload(&s->po_blk, B.po_blk)) || (rc = upload(&s->pb_idx, pbi)) || (rc = upload_Tv(&s->pb_z, pbz)) ||
+            (rc = upload(&s->po_blk, po_blk)) || (rc = upload(&s->pb_idx, pbi)) || (rc = upload_Tv(&s->pb_z, pbz)) ||
             (rc = upload(&s->lb_idx, lbi)) || (rc = upload_Tv(&s->lb_z, lbz)))
             return bail(rc);
         if (s->has_w) {
@@ -1062,7 +1066,9 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         }
     {
         std::vector<int32_t> os(pb->odom_src, pb->odom_src + s->Mo), od(pb->odom_dst, pb->odom_dst + s->Mo);
-        std::vector<double> oz(pb->odom_z, pb->odom_z + 3 * (size_t)s->Mo), om(6 * (size_t)s->Mo);
+        // one zero edge of padding (the J+H's unconditional reads of entry 0 when there is none)
+        std::vector<double> oz(pb->odom_z, pb->odom_z + 3 * (size_t)s->Mo), om(6 * (size_t)s->Mo + 6, 0.0);
+        oz.resize(3 * (size_t)s->Mo + 3, 0.0);
         for (int k = 0; k < s->Mo; ++k) {
             const double* m = pb->odom_omega + 9 * (size_t)k;
             const double u[6] = {m[0], m[1], m[2], m[4], m[5], m[8]};
