@@ -20,9 +20,9 @@
 
 #include "../host/bos_math.hpp"
 
-// J+H build variants (measurement builds only; the defaults are the product): pose items per chunk
-// of the ILP lanes (fp32) and their waves-per-SIMD bound; BOS_JH_PAIRS selects the pair loop for
-// every launch
+// J+H build variants (measurement builds only; the defaults are the product): BOS_JH_ILP launches
+// the ILP lanes for the common case (no faster, and the GN step slower), with
+// BOS_JH_NIP pose items per chunk (fp32) and BOS_JH_MINW waves per SIMD
 #ifndef BOS_JH_NIP
 #define BOS_JH_NIP 12
 #endif
@@ -50,6 +50,20 @@ template <typename T> __device__ __forceinline__ void store6(T* p, T a, T b, T c
     __builtin_nontemporal_store(v2{a, b}, q);
     __builtin_nontemporal_store(v2{c, d}, q + 1);
     __builtin_nontemporal_store(v2{e, f}, q + 2);
+}
+
+// Timing diagnostics only (results wrong): the pose-landmark block stores dropped, or written as
+// six 256-byte coalesced runs per wave step (value v of lane t at 64 v + t of the step's 384 values)
+template <typename T> __device__ __forceinline__ void store_pl(T* base, int64_t slot, const T o[6]) {
+#if defined(BOS_JH_DIAG_NOPLSTORE)
+    if (o[0] == (T)1.2345e-30) base[6 * slot] = o[1];   // keeps the arithmetic alive
+#elif defined(BOS_JH_DIAG_SOASTORE)
+    T* q = base + 384 * (slot >> 6) + (slot & 63);
+#pragma unroll
+    for (int v = 0; v < 6; ++v) __builtin_nontemporal_store(o[v], q + 64 * v);
+#else
+    store6(base + 6 * slot, o[0], o[1], o[2], o[3], o[4], o[5]);
+#endif
 }
 
 template <typename T> __device__ __forceinline__ T wave_sum(T v) {
@@ -199,17 +213,17 @@ __device__ __forceinline__ void pose_bearing(const LinParams<T>& P, const V4<T>&
 // run of equal landmarks and stored at the run's last slot (records of earlier slots of a run carry
 // kRunCont in their index).
 template <typename T, bool HAS_DUPS>
-__device__ __forceinline__ void put_pl(T* blkp, const T o[6], T acc[6], bool last) {
+__device__ __forceinline__ void put_pl(T* plbase, int64_t slot, const T o[6], T acc[6], bool last) {
     if (HAS_DUPS) {
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] += o[q];
         if (last) {
-            store6(blkp, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5]);
+            store6(plbase + 6 * slot, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5]);
 #pragma unroll
             for (int q = 0; q < 6; ++q) acc[q] = (T)0;
         }
     } else {
-        store6(blkp, o[0], o[1], o[2], o[3], o[4], o[5]);
+        store_pl(plbase, slot, o);
     }
 }
 
@@ -273,12 +287,12 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
         };
         if (kOdoFirst) odometry();
         T acc[6] = {0, 0, 0, 0, 0, 0}, o[6];
-        T* const blk0 = P.hval + P.off_pl + 6 * (int64_t)sl;
+        T* const plbase = P.hval + P.off_pl;
         stamp(P.diag_stamps, st, 1);
         for (int j = 0; j < n; j += 2) {
             // item j (set A), then refill A: item j + 2's gather and z, item j + 4's index
             pose_bearing<T>(P, X, LA, zA, wA, h, gb, o, chi, nrob);
-            put_pl<T, HAS_DUPS>(blk0 + 6 * (int64_t)S * j, o, acc, lastA);
+            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * j, o, acc, lastA);
             lastA = !(iA & kRunCont);
             LA = load2(P.lc + 2 * (iA & kIdxMask));
             zA = zp[at(j + 2)];
@@ -293,7 +307,7 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
 #pragma unroll
                 for (int q = 0; q < 6; ++q) o[q] = (T)0;
             }
-            put_pl<T, HAS_DUPS>(blk0 + 6 * (int64_t)S * (j + 1), o, acc, lastB);
+            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * (j + 1), o, acc, lastB);
             lastB = !(iB & kRunCont);
             LB = load2(P.lc + 2 * (iB & kIdxMask));
             zB = zp[at(j + 3)];
@@ -423,7 +437,13 @@ __device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int blk, d
         // hop 3: every gather
         V2<T> L[NI];
 #pragma unroll
-        for (int i = 0; i < NI; ++i) L[i] = load2(P.lc + 2 * (c.idx[i] & kIdxMask));
+        for (int i = 0; i < NI; ++i) {
+#ifdef BOS_JH_DIAG_NOGATHER   // timing diagnostics only: no gather (results wrong)
+            L[i] = V2<T>{(T)(c.idx[i] & 1023), (T)(c.idx[i] & 511)};
+#else
+            L[i] = load2(P.lc + 2 * (c.idx[i] & kIdxMask));
+#endif
+        }
         odo_fetch_data(P, otha, oa);
         odo_fetch_data(P, othb, ob);
         // odometry first, then the bearings (the pair loop's order)
@@ -443,7 +463,12 @@ __device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int blk, d
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             if (i < n) {
+#ifdef BOS_JH_DIAG_NOCOMPUTE   // timing diagnostics only: loads and stores, no arithmetic (results wrong)
+                o[0] = L[i].x; o[1] = L[i].y; o[2] = c.z[i]; o[3] = X.x; o[4] = X.y; o[5] = X.z;
+                h[0] += L[i].x;
+#else
                 pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob);
+#endif
                 store6(blk0 + 6 * (int64_t)S * i, o[0], o[1], o[2], o[3], o[4], o[5]);
             }
         }
@@ -505,12 +530,24 @@ __device__ __forceinline__ void landmark_lane_ilp(const LinParams<T>& P, int blk
     }
     V4<T> X[NI];
 #pragma unroll
-    for (int i = 0; i < NI; ++i) X[i] = load4(P.pc + 4 * idx[i]);
+    for (int i = 0; i < NI; ++i) {
+#ifdef BOS_JH_DIAG_NOGATHER
+        X[i] = V4<T>{(T)(idx[i] & 1023), (T)(idx[i] & 511), (T)0.5, (T)0.5};
+#else
+        X[i] = load4(P.pc + 4 * idx[i]);
+#endif
+    }
     stamp(P.diag_stamps, st, 1);
     T hl[3] = {0, 0, 0}, gl[2] = {0, 0};
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-        if (i < n) landmark_bearing<T>(P, X[i], Lm, z[i], (T)1, hl, gl);
+        if (i < n) {
+#ifdef BOS_JH_DIAG_NOCOMPUTE
+            hl[0] += X[i].x + z[i]; hl[1] += X[i].y; hl[2] += X[i].z + Lm.x; gl[0] += X[i].w + Lm.y;
+#else
+            landmark_bearing<T>(P, X[i], Lm, z[i], (T)1, hl, gl);
+#endif
+        }
     for (int j0 = NI; j0 < n; j0 += NI) {   // lists longer than NI
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -976,8 +1013,8 @@ hipError_t launch_lin_ilp(LinParams<T> p, hipStream_t s) {
 
 template <typename T, bool W, bool D, int MINW>
 hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, hipStream_t s) {
-#ifndef BOS_JH_PAIRS
-    if (!W && !D) {   // the common case: every load of a lane up front
+#ifdef BOS_JH_ILP
+    if (!W && !D) {   // every load of a lane up front (measurement builds: DESIGN.md §4)
         switch (lpp) {
             case 1: return launch_lin_ilp<T, 1, BOS_JH_MINW>(p, s);
             case 2: return launch_lin_ilp<T, 2, BOS_JH_MINW>(p, s);
