@@ -192,7 +192,7 @@ __device__ __forceinline__ void odometry_entry(const LinParams<T>& P, int x, int
 // pose's diagonal block h and b, returns the pose-landmark block o (J_p^T w J_l).
 template <typename T>
 __device__ __forceinline__ void pose_bearing(const LinParams<T>& P, const V4<T>& X, const V2<T>& Lm, T z, T w,
-                                             T h[6], T gb[3], T o[6], double& chi, int& nrob) {
+                                             T h[6], T gb[3], T o[6], double& chi, int& nrob, T jf[3]) {
     T J[5];
     T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, z, J);   // :9-95
     const T rho = e * w * e;                                                       // solver.cpp:37
@@ -207,13 +207,26 @@ __device__ __forceinline__ void pose_bearing(const LinParams<T>& P, const V4<T>&
     h[3] += w2 * J[0]; h[4] += w2 * J[1]; h[5] += w2 * J[2];
     gb[0] += w0 * e; gb[1] += w1 * e; gb[2] += w2 * e;
     o[0] = w0 * J[3]; o[1] = w0 * J[4]; o[2] = w1 * J[3]; o[3] = w1 * J[4]; o[4] = w2 * J[3]; o[5] = w2 * J[4];
+    jf[0] = J[2]; jf[1] = J[3]; jf[2] = J[4];
 }
 
 // The pose-landmark block of a bearing: stored at its slot, or (duplicate pairs) summed over the
 // run of equal landmarks and stored at the run's last slot (records of earlier slots of a run carry
 // kRunCont in their index).
+// Three values at slot s of a factored pose-landmark region (LinParams::pl_factored), streamed out
+template <typename T> __device__ __forceinline__ void store3(T* p, T a, T b, T c) {
+    __builtin_nontemporal_store(a, p);
+    __builtin_nontemporal_store(b, p + 1);
+    __builtin_nontemporal_store(c, p + 2);
+}
+
 template <typename T, bool HAS_DUPS>
-__device__ __forceinline__ void put_pl(T* plbase, int64_t slot, const T o[6], T acc[6], bool last) {
+__device__ __forceinline__ void put_pl(T* plbase, int64_t slot, const T o[6], T acc[6], bool last, bool factored,
+                                       const T jf[3]) {
+    if (!HAS_DUPS && factored) {   // (uniform branch: one value per launch)
+        store3(plbase + 3 * slot, jf[0], jf[1], jf[2]);
+        return;
+    }
     if (HAS_DUPS) {
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] += o[q];
@@ -286,13 +299,14 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
             }
         };
         if (kOdoFirst) odometry();
-        T acc[6] = {0, 0, 0, 0, 0, 0}, o[6];
+        T acc[6] = {0, 0, 0, 0, 0, 0}, o[6], jf[3];
+        const bool factored = P.pl_factored != 0;
         T* const plbase = P.hval + P.off_pl;
         stamp(P.diag_stamps, st, 1);
         for (int j = 0; j < n; j += 2) {
             // item j (set A), then refill A: item j + 2's gather and z, item j + 4's index
-            pose_bearing<T>(P, X, LA, zA, wA, h, gb, o, chi, nrob);
-            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * j, o, acc, lastA);
+            pose_bearing<T>(P, X, LA, zA, wA, h, gb, o, chi, nrob, jf);
+            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * j, o, acc, lastA, factored, jf);
             lastA = !(iA & kRunCont);
             LA = load2(P.lc + 2 * (iA & kIdxMask));
             zA = zp[at(j + 2)];
@@ -302,12 +316,13 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
             // of the lane's wave: pose-lane waves have an even number of slots per lane), so both
             // paths issue the same memory operations and the loop's waits stay exact.
             if (j + 1 < n) {
-                pose_bearing<T>(P, X, LB, zB, wB, h, gb, o, chi, nrob);
+                pose_bearing<T>(P, X, LB, zB, wB, h, gb, o, chi, nrob, jf);
             } else {
 #pragma unroll
                 for (int q = 0; q < 6; ++q) o[q] = (T)0;
+                jf[0] = jf[1] = jf[2] = (T)0;
             }
-            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * (j + 1), o, acc, lastB);
+            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * (j + 1), o, acc, lastB, factored, jf);
             lastB = !(iB & kRunCont);
             LB = load2(P.lc + 2 * (iB & kIdxMask));
             zB = zp[at(j + 3)];
@@ -459,7 +474,7 @@ __device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int blk, d
         }
         stamp(P.diag_stamps, st, 1);
         T* const blk0 = P.hval + P.off_pl + 6 * (int64_t)sl;
-        T o[6];
+        T o[6], jf[3];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             if (i < n) {
@@ -467,9 +482,10 @@ __device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int blk, d
                 o[0] = L[i].x; o[1] = L[i].y; o[2] = c.z[i]; o[3] = X.x; o[4] = X.y; o[5] = X.z;
                 h[0] += L[i].x;
 #else
-                pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob);
+                pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob, jf);
 #endif
-                store6(blk0 + 6 * (int64_t)S * i, o[0], o[1], o[2], o[3], o[4], o[5]);
+                if (P.pl_factored) store3(P.hval + P.off_pl + 3 * ((int64_t)sl + (int64_t)S * i), jf[0], jf[1], jf[2]);
+                else store6(blk0 + 6 * (int64_t)S * i, o[0], o[1], o[2], o[3], o[4], o[5]);
             }
         }
         // items past NI (lists longer than NI: not at config 3), NI at a time
@@ -485,8 +501,9 @@ __device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int blk, d
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 if (j0 + i < n) {
-                    pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob);
-                    store6(blk0 + 6 * (int64_t)S * (j0 + i), o[0], o[1], o[2], o[3], o[4], o[5]);
+                    pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob, jf);
+                    if (P.pl_factored) store3(P.hval + P.off_pl + 3 * ((int64_t)sl + (int64_t)S * (j0 + i)), jf[0], jf[1], jf[2]);
+                    else store6(blk0 + 6 * (int64_t)S * (j0 + i), o[0], o[1], o[2], o[3], o[4], o[5]);
                 }
             }
         }
@@ -976,6 +993,41 @@ __global__ void gather_f64_kernel(const T* in, const int32_t* idx, double* out, 
     }
 }
 
+// gather_f64_kernel with a factored pose-landmark region (LinParams::pl_factored): items [0, n) the
+// right-hand side gather, then the block array in pairs of values outside the region and one slot
+// per item inside it (3 fp32 values in, 6 fp64 values out: the block J_p^T J_l, J_p = (-J_lx, -J_ly,
+// J_theta), each product rounded in fp32 as the unfactored kernel rounds it)
+__global__ void gather_f64_factored_kernel(const float* in, const int32_t* idx, double* out, int64_t n,
+                                           unsigned long long* stamp, uint32_t* epoch, const float* cin, double* cout,
+                                           int64_t cn, int64_t pl_off, int64_t pl_slots) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
+        if (epoch) *epoch += 1u;
+    }
+    const int64_t pa = pl_off >> 1;                          // value pairs before the region (pl_off even)
+    const int64_t pend = pl_off + 6 * pl_slots;              // even
+    const int64_t pb = (cn - pend + 1) >> 1;                 // value pairs after it (the last may be single)
+    const int64_t step = (int64_t)gridDim.x * blockDim.x, items = n + pa + pl_slots + pb;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < items; i += step) {
+        if (i < n) {
+            out[i] = (double)in[idx[i]];
+        } else if (i < n + pa + pl_slots && i >= n + pa) {
+            const int64_t sl = i - n - pa;
+            const float* f = cin + pl_off + 3 * sl;
+            const float jt = f[0], jx = f[1], jy = f[2];
+            const float px = -jx, py = -jy;
+            V2<double>* o = (V2<double>*)(cout + pl_off + 6 * sl);
+            o[0] = V2<double>{(double)(px * jx), (double)(px * jy)};
+            o[1] = V2<double>{(double)(py * jx), (double)(py * jy)};
+            o[2] = V2<double>{(double)(jt * jx), (double)(jt * jy)};
+        } else {
+            const int64_t j = i < n + pa ? 2 * (i - n) : pend + 2 * (i - n - pa - pl_slots);
+            cout[j] = (double)cin[j];
+            if (j + 1 < cn) cout[j + 1] = (double)cin[j + 1];
+        }
+    }
+}
+
 __global__ void scatter_dense_kernel(const int32_t* rowptr, const int32_t* colind, const double* val, int n,
                                      double* dense) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1133,6 +1185,29 @@ hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64
     hipLaunchKernelGGL((gather_f64_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n, stamp, epoch,
                        cin, cout, cn);
     return hipGetLastError();
+}
+
+hipError_t launch_gather_f64_factored(const float* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
+                                      unsigned long long* stamp, uint32_t* epoch, const float* cin, double* cout,
+                                      int64_t cn, int64_t pl_off, int64_t pl_slots) {
+    if ((pl_off & 1) || pl_off + 6 * pl_slots > cn) return hipErrorInvalidValue;   // checked before launching
+    const int64_t items = n + (pl_off >> 1) + pl_slots + ((cn - pl_off - 6 * pl_slots + 1) >> 1);
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 8192));
+    hipLaunchKernelGGL(gather_f64_factored_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n, stamp, epoch,
+                       cin, cout, cn, pl_off, pl_slots);
+    return hipGetLastError();
+}
+
+void expand_factored_host(const float* in, double* out, int64_t n, int64_t pl_off, int64_t pl_slots) {
+    for (int64_t i = 0; i < n; ++i) out[i] = in[i];
+    for (int64_t sl = 0; sl < pl_slots; ++sl) {
+        const float* f = in + pl_off + 3 * sl;
+        const float jt = f[0], jx = f[1], jy = f[2], px = -jx, py = -jy;
+        double* o = out + pl_off + 6 * sl;
+        o[0] = (double)(px * jx); o[1] = (double)(px * jy);
+        o[2] = (double)(py * jx); o[3] = (double)(py * jy);
+        o[4] = (double)(jt * jx); o[5] = (double)(jt * jy);
+    }
 }
 
 hipError_t launch_scatter_dense(const int32_t* rowptr, const int32_t* colind, const double* val, int n, double* dense,

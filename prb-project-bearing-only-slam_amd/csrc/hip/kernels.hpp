@@ -62,6 +62,12 @@ template <typename T> struct LinParams {
     T* hval;                  // block array (BlockLayout)
     T* b;                     // [3 NP + 2 NL], reference dof numbering
     int off_ldiag, off_pl, off_pp;
+    // factored pose-landmark blocks (fp32 build, unit bearing weights, no duplicate pairs): slot s
+    // holds (J_theta, J_lx, J_ly) at off_pl + 3 s instead of the 6 block values at off_pl + 6 s; the
+    // block is J_p^T J_l with J_p = (-J_lx, -J_ly, J_theta) exactly (solver_jacobians.cpp:51-64:
+    // the translation columns of the bearing Jacobian are minus its landmark columns), expanded by
+    // the solver's fp64 conversion (launch_gather_f64)
+    int pl_factored;
     double* chi2_part;        // [pose_blocks]
     int32_t* nrob_part;       // [pose_blocks]
     T kt;                     // robust kernel threshold
@@ -183,6 +189,15 @@ template <typename T>
 hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
                              unsigned long long* stamp = nullptr, uint32_t* epoch = nullptr, const T* cin = nullptr,
                              double* cout = nullptr, int64_t cn = 0);
+// The same with a block array whose pose-landmark region [pl_off, pl_off + 6 pl_slots) is stored
+// factored (LinParams::pl_factored): that region is expanded to the 6 block values per slot in fp64
+// (the products rounded in T, so the values equal those of an unfactored build), the rest copied.
+hipError_t launch_gather_f64_factored(const float* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
+                                      unsigned long long* stamp, uint32_t* epoch, const float* cin, double* cout,
+                                      int64_t cn, int64_t pl_off, int64_t pl_slots);
+// Host-side expansion of a factored block array (bos_export_system): region as above, in place on a
+// copy of the fp32 array converted to double
+void expand_factored_host(const float* in, double* out, int64_t n, int64_t pl_off, int64_t pl_slots);
 hipError_t launch_scatter_dense(const int32_t* rowptr, const int32_t* colind, const double* val, int n, double* dense,
                                 hipStream_t s);
 

@@ -82,6 +82,9 @@ struct bos_solver {
     bos::Plan plan;
     int NP = 0, NL = 0, Mb = 0, Mo = 0;
     bool has_w = false, has_dups = false;
+    // fp32 build with a multifrontal solve, unit weights, no duplicate pairs: the J+H writes the
+    // pose-landmark blocks factored (LinParams::pl_factored), the solver's fp64 conversion expands them
+    bool pl_factored = false;
     size_t tsize = 8;   // sizeof(T)
     // state
     double* d_pose = nullptr;
@@ -208,6 +211,7 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.off_ldiag = (int)P.blk.off_ldiag; p.off_pl = (int)P.blk.off_pl; p.off_pp = (int)P.blk.off_pp;
     p.chi2_part = s->d_chi_part;
     p.nrob_part = s->d_nrob_part;
+    p.pl_factored = s->pl_factored ? 1 : 0;
     p.kt = (T)s->kt;
     p.lambda = (T)s->damping;
     p.diag_stamps = nullptr;
@@ -357,6 +361,12 @@ int enqueue_solver_inputs(bos_solver* s) {
     unsigned long long* stamp = s->d_status->stamp + s->solve_stamp;
     uint32_t* epoch = uses_mf(s) ? bos::dev::mf_epoch_ptr(s->mf) : nullptr;
     const bool conv = f32 && uses_mf(s);   // the fp64 copy of the block array, in the same launch
+    if (s->pl_factored) {   // the copy expands the factored pose-landmark blocks
+        HIP_TRY(bos::dev::launch_gather_f64_factored((const float*)s->sys_b, s->elim_ref, s->d_rhs, n, s->stream, stamp,
+                                                     epoch, (const float*)s->sys_val, s->d_val64, s->plan.blk.size,
+                                                     s->plan.blk.off_pl, s->plan.blk.pose_lanes.slots()));
+        return BOS_OK;
+    }
     HIP_TRY(f32 ? bos::dev::launch_gather_f64<float>((const float*)s->sys_b, s->elim_ref, s->d_rhs, n, s->stream, stamp, epoch,
                                                      conv ? (const float*)s->sys_val : nullptr, conv ? s->d_val64 : nullptr,
                                                      conv ? s->plan.blk.size : 0)
@@ -934,6 +944,9 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     if (pb->bearing_omega)
         for (int k = 0; k < s->Mb; ++k)
             if (pb->bearing_omega[k] != 1.0) { s->has_w = true; break; }
+#ifndef BOS_JH_NO_FACTOR   // (measurement builds: the unfactored layout for comparison)
+    s->pl_factored = s->precision == BOS_FP32 && uses_mf(s) && !s->has_w && !s->has_dups;
+#endif
 
     // ---- streams / events / libraries
     if (opt.stream) {
@@ -1485,7 +1498,8 @@ int bos_export_system(const bos_solver* s, int64_t capacity, int32_t* rows, int3
         if (s->precision == BOS_FP32) {
             std::vector<float> f(nv);
             if (nv) HIP_TRY(hipMemcpy(f.data(), s->sys_val, nv * sizeof(float), hipMemcpyDeviceToHost));
-            for (int64_t i = 0; i < nv; ++i) v[i] = f[i];
+            if (s->pl_factored) bos::dev::expand_factored_host(f.data(), v.data(), nv, P.blk.off_pl, P.blk.pose_lanes.slots());
+            else for (int64_t i = 0; i < nv; ++i) v[i] = f[i];
         } else if (nv) {
             HIP_TRY(hipMemcpy(v.data(), s->sys_val, nv * sizeof(double), hipMemcpyDeviceToHost));
         }

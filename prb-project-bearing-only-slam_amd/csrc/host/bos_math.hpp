@@ -96,11 +96,11 @@ BOS_HD T bearing_error_jacobian(T px, T py, T c, T s, T lx, T ly, T z, T J[5]) {
     const T a0 = f * (-gy), a1 = f * gx;                                 // :47-48
     const T gth_x = c * ly + s * (-lx);                                  // R^T [[0,1],[-1,0]] l (:60)
     const T gth_y = -s * ly + c * (-lx);
-    J[0] = a0 * (-c) + a1 * (s);                                         // -R^T (:59)
-    J[1] = a0 * (-s) + a1 * (-c);
-    J[2] = a0 * gth_x + a1 * gth_y;
     J[3] = a0 * c + a1 * (-s);                                           // R^T (:64)
     J[4] = a0 * s + a1 * c;
+    J[0] = -J[3];                                                        // -R^T (:59): exactly minus
+    J[1] = -J[4];                                                        // the landmark columns
+    J[2] = a0 * gth_x + a1 * gth_y;
     return e;
 }
 

@@ -1,9 +1,12 @@
-# tests (new ones first) + bench N=1 + two-rank no-launcher gloo rehearsal + lanes-per-pose sweep
+# J+H factored / unfactored A/B (J+H alone, then GN with state checksums), tests (new ones first),
+# bench N=1, two-rank no-launcher gloo rehearsal, lanes-per-pose sweep
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r03e
 mkdir -p $O
+timeout -k 10 200 python -u tools/jh_diag_timing.py gpurun_exp/libbos_unfact.so gpurun_exp/libbos_fact.so gpurun_exp/libbos_unfact.so gpurun_exp/libbos_fact.so > $O/jh_ab.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/gn_ab.py gpurun_exp/libbos_unfact.so gpurun_exp/libbos_fact.so 2 > $O/gn_ab.log 2>&1 || exit 1
 timeout -k 10 900 python -u -m pytest tests/test_gpu_c3_gn.py tests/test_gpu_scenarios.py tests/test_partitions.py -x -v -m gpu --timeout 900 --timeout-method thread -p no:cacheprovider > $O/pytest_new.log 2>&1 || exit 1
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 900 --timeout-method thread -p no:cacheprovider > $O/pytest_all.log 2>&1 || exit 1
 timeout -k 10 400 python bench.py > $O/bench_n1.json 2> $O/bench_n1.err || exit 1
