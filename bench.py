@@ -148,7 +148,7 @@ def solver_model(P, phase, world):
     its flops at the fp64 peak, its compulsory bytes at the achievable HBM rate, and the dependency
     chain of the elimination tree (levels x two hand-offs, factor and backward) — the measured
     t_solve_ms against each."""
-    if world != 1:
+    if world != 1 or not phase:
         return None
     info = bos.plan_inspect(P, solver=bos.BOS_SOLVER_SCHUR)
     flops = float(info["mf_flops"])
@@ -167,16 +167,16 @@ def solver_model(P, phase, world):
             "frac_of_chain_bound": t_chain / t_solve_us, "frac_of_bytes_bound": t_bytes / t_solve_us}
 
 
-PROFILE_TAG = "r02"   # profiles/<tag>_pmc_linearize_<prec>.json, written by tools/pmc_summary.py
+PROFILE_TAG = "r03"   # profiles/<tag>_pmc_linearize_<prec>_<mode>.json, written by tools/pmc_summary.py
 
 
 def traffic_from_profile(precision):
     """Fabric bytes per launch of the J+H kernel from the committed rocprofv3 PMC summaries
-    (L2 <-> fabric requests by size, tools/gpu_profile.sh): {"warm": ..., "cold": ...}."""
+    (L2 <-> fabric requests by size, tools/gpu_profile.sh): the in-step launches of the timed GN steps
+    ("instep") and back-to-back builds ("warm")."""
     out = {}
-    for label in ("warm", "cold"):
-        name = f"{PROFILE_TAG}_pmc_linearize_" + ("fp32" if precision == bos.BOS_FP32 else "fp64") + \
-            ("_cold" if label == "cold" else "") + ".json"
+    for label in ("instep", "warm"):
+        name = f"{PROFILE_TAG}_pmc_linearize_" + ("fp32" if precision == bos.BOS_FP32 else "fp64") + f"_{label}.json"
         path = os.path.join(ROOT, "profiles", name)
         try:
             with open(path) as f:
@@ -384,17 +384,20 @@ def main():
         return {k: float(np.median([g[k] for g in stats])) for k in
                 ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
 
-    # ---- the timed region: K GN iterations; the J+H inside them is the headline
-    wall, stats = timed_steps(S, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup)
-    phase = phases(stats)
-    jh_ms = max_over_ranks(phase["t_linearize_ms"])      # the slowest rank's in-step J+H
-    gn_it_s = args.steps / wall
-    log(f"rank {rank}: {args.steps} GN steps in {wall * 1e3:.1f} ms ({gn_it_s:.0f} it/s); phases {phase}")
+    # ---- the timed region: K GN iterations; the J+H inside them is the headline (K = 0: no GN steps,
+    # the J+H builds alone, for profiling runs)
+    wall, stats, phase, jh_ms, gn_it_s = 0.0, [], None, None, None
+    if args.steps > 0:
+        wall, stats = timed_steps(S, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup)
+        phase = phases(stats)
+        jh_ms = max_over_ranks(phase["t_linearize_ms"])      # the slowest rank's in-step J+H
+        gn_it_s = args.steps / wall
+        log(f"rank {rank}: {args.steps} GN steps in {wall * 1e3:.1f} ms ({gn_it_s:.0f} it/s); phases {phase}")
 
     # ---- other GN loops (the headline's timed region above is the reference for value)
     gn_c_loop, gn_batched = None, None
     init = S.get_state()
-    if world == 1 or args.exchange == "rccl":
+    if args.steps > 0 and (world == 1 or args.exchange == "rccl"):
         gn_c_loop = 1e3 / max_over_ranks(S.time_steps(min(args.steps, 50)))   # bos_step in a C loop
         S.set_state(*init)
         barrier()
@@ -424,7 +427,7 @@ def main():
 
     # ---- N > 1: the north star's partition (observations by measurement order, all-reduce of H, b)
     part_obs = None
-    if world > 1 and not args.no_partition_other:
+    if world > 1 and not args.no_partition_other and args.steps > 0:
         S3, _, seen3 = make_handle(bos.BOS_PARTITION_OBSERVATIONS)
         w3, st3 = timed_steps(S3, bos.BOS_PARTITION_OBSERVATIONS, args.steps, args.warmup)
         ph3 = phases(st3)
@@ -463,14 +466,16 @@ def main():
         def roof(ms, label, timing):
             a = algo / (ms * 1e-3) / 1e9
             return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
-                    "traffic": traffic.get("warm" if label == "warm" else "cold") if traffic else None,
+                    "traffic": traffic.get("warm" if label == "warm" else "instep") if traffic else None,
                     "algorithmic_bytes_per_launch": algo, "kernel_ms": ms, "caches": label, "timing": timing}
         r_instep = roof(jh_ms, "in-step", "median over the timed GN steps of the device realtime clock from the "
-                        "J+H launch's start to the next launch's start (stamped by the step's kernels); max over ranks")
+                        "J+H launch's start to the next launch's start (stamped by the step's kernels); max over ranks") \
+            if jh_ms else None
         r_cold = roof(cold_ms, "cold", "HIP events around each build, 512 MiB read before it (event cost included)") \
             if cold_ms else None
         r_warm = roof(replay_ms, "warm", "HIP events around the back-to-back builds") if replay_ms else None
-        value = nobs / (jh_ms * 1e-3)
+        head_ms = jh_ms if jh_ms else replay_ms   # K = 0 (profiling runs): the back-to-back builds
+        value = nobs / (head_ms * 1e-3)
         line = {
             "metric": METRIC,
             "value": value,
@@ -478,7 +483,7 @@ def main():
             "n_gpus": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": jh_ms,
+            "ms_per_step": head_ms,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -507,7 +512,7 @@ def main():
             # the J+H as it runs inside the GN iteration (inputs from HBM after the solver's stream);
             # the same from cold caches by events, and the back-to-back replay (working set partly
             # cache resident), beside it
-            "roofline": r_instep,
+            "roofline": r_instep or r_warm,
             "roofline_cold_events": r_cold,
             "roofline_warm_replay": r_warm,
         }
@@ -516,7 +521,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(P, precision, cpus)
             line["cpu_baseline_gn"] = cpu_gn_baseline(P, cpus)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
-            line["gn_speedup_vs_cpu"] = gn_it_s / line["cpu_baseline_gn"]["value"]
+            if gn_it_s:
+                line["gn_speedup_vs_cpu"] = gn_it_s / line["cpu_baseline_gn"]["value"]
         print(json.dumps(line), flush=True)
     S.close()
     if world > 1:
