@@ -211,9 +211,11 @@ def launch_ranks(n):
         except subprocess.TimeoutExpired:
             p.kill()
             rcs.append(p.wait())
-    if out:
-        sys.stdout.write(out.decode())
-        sys.stdout.flush()
+    for ln in (out or b"").decode(errors="replace").splitlines():
+        # the JSON line to stdout; anything else rank 0's libraries printed there (gloo's connection
+        # notice) to stderr
+        (sys.stdout if ln.startswith("{") else sys.stderr).write(ln + "\n")
+    sys.stdout.flush()
     bad = [rc for rc in rcs if rc != 0]
     if bad:
         log(f"launcher: rank exit codes {rcs}")
@@ -461,13 +463,17 @@ def main():
 
     if rank == 0:
         algo = info["algorithmic_bytes"]
+        layout = info["layout_bytes"]
         traffic = traffic_from_profile(precision) if world == 1 else None
 
         def roof(ms, label, timing):
             a = algo / (ms * 1e-3) / 1e9
             return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
                     "traffic": traffic.get("warm" if label == "warm" else "instep") if traffic else None,
-                    "algorithmic_bytes_per_launch": algo, "kernel_ms": ms, "caches": label, "timing": timing}
+                    "algorithmic_bytes_per_launch": algo, "kernel_ms": ms, "caches": label, "timing": timing,
+                    # the bytes this layout moves at minimum (pose-landmark blocks stored as 3 factors
+                    # when pl_factored) and the fraction of the roofline on those
+                    "layout_bytes_per_launch": layout, "frac_layout": layout / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         r_instep = roof(jh_ms, "in-step", "median over the timed GN steps of the device realtime clock from the "
                         "J+H launch's start to the next launch's start (stamped by the step's kernels); max over ranks") \
             if jh_ms else None

@@ -132,6 +132,10 @@ typedef struct bos_system_info {
     int32_t top_fronts;             /* fronts of the replicated top (0 on one GPU)               */
     int32_t comm_ranks;             /* ranks the RCCL communicator holds (ncclCommCount), 0 without one */
     int32_t partition;              /* BOS_PARTITION_* of a sharded handle                       */
+    int32_t pl_factored;            /* 1: pose-landmark blocks stored factored (3 floats, fp32 J+H) */
+    int32_t reserved;
+    int64_t layout_bytes;           /* algorithmic_bytes with this layout's output: 12 B less per
+                                       pose-landmark block when pl_factored                       */
 } bos_system_info;
 
 void bos_default_options(bos_options* opt);

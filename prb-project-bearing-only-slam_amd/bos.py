@@ -88,7 +88,8 @@ class bos_system_info(ctypes.Structure):
                 ("algorithmic_bytes", ctypes.c_int64), ("num_block_values", ctypes.c_int64),
                 ("lanes_per_pose", ctypes.c_int32), ("pose_lane_groups", ctypes.c_int32),
                 ("landmark_lanes", ctypes.c_int32), ("own_fronts", ctypes.c_int32), ("top_fronts", ctypes.c_int32),
-                ("comm_ranks", ctypes.c_int32), ("partition", ctypes.c_int32)]
+                ("comm_ranks", ctypes.c_int32), ("partition", ctypes.c_int32),
+                ("pl_factored", ctypes.c_int32), ("reserved", ctypes.c_int32), ("layout_bytes", ctypes.c_int64)]
 
 
 class bos_plan_info(ctypes.Structure):

@@ -1468,6 +1468,8 @@ int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
     // compulsory reads of inputs + state, one write of every output block
     info->algorithmic_bytes = s->precision == BOS_FP32 ? 36 * Mb + 80 * Mo + 60 * NP + 32 * NL
                                                        : 64 * Mb + 152 * Mo + 120 * NP + 64 * NL;
+    info->pl_factored = s->pl_factored ? 1 : 0;
+    info->layout_bytes = info->algorithmic_bytes - (s->pl_factored ? 12 * Mb : 0);
     info->num_block_values = P.blk.size;
     info->lanes_per_pose = P.blk.lpp;
     info->pose_lane_groups = (int32_t)P.blk.lane_pose.size();

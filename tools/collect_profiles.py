@@ -30,4 +30,6 @@ json.dump(bench_line(os.path.join(src, "bench_fp32_default.json")),
           open(os.path.join(dst, f"{tag}_bench_fp32_default.json"), "w"), indent=1)
 shutil.copy(os.path.join(src, "trace_fp32_default", "run_kernel_stats.csv"),
             os.path.join(dst, f"{tag}_kernel_stats_fp32_default.csv"))
+for name in ("gn_step_timeline.txt", "solver_stamps.txt"):
+    shutil.copy(os.path.join(src, name), os.path.join(dst, f"{tag}_{name}"))
 print("default ok")

@@ -36,3 +36,5 @@ print((36 if '$P' == 'fp32' else 64) * len(P.b_z) + (80 if '$P' == 'fp32' else 1
 done
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace_fp32_default -o run --output-format csv -- \
   python3 bench.py > $O/bench_fp32_default.json 2> $O/bench_fp32_default.err || exit 1
+python3 tools/step_timeline.py $O/trace_fp32_default > $O/gn_step_timeline.txt || exit 1
+timeout -k 10 180 python3 tools/solver_stamps.py > $O/solver_stamps.txt 2> $O/solver_stamps.err || exit 1
