@@ -295,6 +295,11 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
     return y;
 }
 
+// phase stamp k of front s (lane 0; the product launches pass no stamp buffer)
+__device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
+    if (stp && threadIdx.x == 0) stp[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 // Folded landmark children (Schur ordering) of front s, eliminated by its wave: per chunk (whole
 // children, <= 64 rows, <= fold_chunk_landmarks(m) landmarks) lane q takes row t of landmark c
 // (one 32-byte record: sources of its two entries, of the landmark's 2 x 2 block, the landmark's
@@ -420,6 +425,9 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
             W[pos * WS + 2 * lml] = lt0;
             W[pos * WS + 2 * lml + 1] = lt1;
         }
+#ifdef BOS_MF_FOLD_STAMPS   // measurement builds: the first chunk's values have arrived (slot 6)
+        if (ch == ch0) fstamp(a.stamps_f, s, 6);
+#endif
         wave_sync();
         const int kc = 2 * nl;
         if (lane < m) {   // u-vector part: -(W y) at this lane's position
@@ -449,6 +457,9 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
         n = nn;
         nn = n2;
     }
+#ifdef BOS_MF_FOLD_STAMPS   // slot 7: the front's chunk count
+    if (a.stamps_f && lane == 0) a.stamps_f[8 * (int64_t)s + 7] = (unsigned long long)(ch1 - ch0);
+#endif
 }
 
 // The front before its assembly: every lower entry of F and of wv set to minus the folded
@@ -502,11 +513,6 @@ struct Flow {
     int id;
     unsigned long long* stamps;   // diagnostics (bos_debug_solver_stamps): 8 realtime stamps per front, or null
 };
-
-// phase stamp k of front s (lane 0; the product launches pass no stamp buffer)
-__device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
-    if (stp && threadIdx.x == 0) stp[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
-}
 
 constexpr int kStall = kMfStall;               // or-ed into info when a dependency wait times out
 constexpr uint64_t kWaitTicks = 5000000;        // 50 ms of the 100 MHz realtime clock
@@ -1343,6 +1349,10 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         err = "side stream creation failed (multifrontal)";
         return -2;
     }
+#ifdef BOS_MF_NO_SIDE   // measurement builds: every class of a level on the main stream
+    (void)hipStreamDestroy(d->side);
+    d->side = nullptr;
+#endif
     auto alloc = [&](double** p, int64_t n) -> int {   // + kMfPad: clamped reads (up())
         if (n <= 0) n = 1;
         if (hipMalloc((void**)p, (n + kMfPad) * sizeof(double)) != hipSuccess) { err = "hipMalloc failed (multifrontal buffers)"; return -2; }

@@ -34,4 +34,7 @@ for rep in range(3):
     bt = 50 / (time.perf_counter() - t0)
     ph = {k: round(float(np.median([g[k] for g in st])) * 1e3, 2) for k in ("t_linearize_ms", "t_solve_ms", "t_update_ms")}
     out.append(f"c-loop {c:7.1f}  python {py:7.1f}  batched {bt:7.1f} it/s  phases(us) {ph}")
+import hashlib  # noqa: E402
+pose, lm = S.get_state()   # after the last 50-iteration batch from the initial guess
+out.append("state sha1 " + hashlib.sha1(pose.tobytes() + lm.tobytes()).hexdigest()[:16])
 print(os.path.basename(sys.argv[2]), *out, sep="\n  ", flush=True)
