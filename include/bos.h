@@ -133,7 +133,8 @@ typedef struct bos_system_info {
     int32_t comm_ranks;             /* ranks the RCCL communicator holds (ncclCommCount), 0 without one */
     int32_t partition;              /* BOS_PARTITION_* of a sharded handle                       */
     int32_t pl_factored;            /* 1: pose-landmark blocks stored factored (3 floats, fp32 J+H) */
-    int32_t reserved;
+    int32_t fold_fp32;              /* 1: the solver's landmark folds read the fp32 block array (the fp64
+                                       copy skips the pose-landmark and landmark-diagonal region)  */
     int64_t layout_bytes;           /* algorithmic_bytes with this layout's output: 12 B less per
                                        pose-landmark block when pl_factored                       */
 } bos_system_info;

@@ -65,6 +65,9 @@ typedef struct bos_plan_info {
     int64_t shard_own_pose_lanes;
     int64_t shard_lm_lanes;
     int64_t shard_update_nodes;     /* nodes the box-plus updates (own, top, boundary)             */
+    int64_t mf_fold_fp32;           /* the folds alone read the pose-landmark / landmark-diagonal
+                                       region (mf_fold_reads_fp32): an fp32 build's folds read it
+                                       from the fp32 array (bos_system_info.fold_fp32)             */
 } bos_plan_info;
 
 /* Build the static plan on the host (what bos_create does before touching the GPU) with the

@@ -89,7 +89,7 @@ class bos_system_info(ctypes.Structure):
                 ("lanes_per_pose", ctypes.c_int32), ("pose_lane_groups", ctypes.c_int32),
                 ("landmark_lanes", ctypes.c_int32), ("own_fronts", ctypes.c_int32), ("top_fronts", ctypes.c_int32),
                 ("comm_ranks", ctypes.c_int32), ("partition", ctypes.c_int32),
-                ("pl_factored", ctypes.c_int32), ("reserved", ctypes.c_int32), ("layout_bytes", ctypes.c_int64)]
+                ("pl_factored", ctypes.c_int32), ("fold_fp32", ctypes.c_int32), ("layout_bytes", ctypes.c_int64)]
 
 
 class bos_plan_info(ctypes.Structure):
@@ -104,7 +104,7 @@ class bos_plan_info(ctypes.Structure):
                 ("shard_roots", ctypes.c_int64), ("shard_ex1_doubles", ctypes.c_int64),
                 ("shard_ex2_doubles", ctypes.c_int64), ("shard_pose_lanes", ctypes.c_int64),
                 ("shard_own_pose_lanes", ctypes.c_int64), ("shard_lm_lanes", ctypes.c_int64),
-                ("shard_update_nodes", ctypes.c_int64)]
+                ("shard_update_nodes", ctypes.c_int64), ("mf_fold_fp32", ctypes.c_int64)]
 
 
 _lib = None
@@ -342,7 +342,8 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
            "ordering": info.ordering.decode(), "mf_supernodes": info.mf_supernodes,
            "mf_levels": info.mf_levels, "mf_max_front": info.mf_max_front, "mf_flops": info.mf_flops,
            "mf_update_bytes": info.mf_update_bytes, "mf_fits": bool(info.mf_fits),
-           "mf_max_front_upper": info.mf_max_front_upper, "mf_balance_pct": info.mf_balance_pct}
+           "mf_max_front_upper": info.mf_max_front_upper, "mf_balance_pct": info.mf_balance_pct,
+           "mf_fold_fp32": bool(info.mf_fold_fp32)}
     out.update({k: getattr(info, k) for k, _ in bos_plan_info._fields_ if k.startswith("shard_")})
     if entries:
         nnz = info.nnz_lower

@@ -993,6 +993,29 @@ __global__ void gather_f64_kernel(const T* in, const int32_t* idx, double* out, 
     }
 }
 
+// gather_f64_kernel when the folds read the fp32 block array's pose-landmark and landmark-diagonal
+// region [lo, hi) themselves (multifrontal.hpp mf_set_fold_source): items [0, n) the right-hand side
+// gather, then the block array outside the region, in pairs of values (lo and hi even)
+__global__ void gather_f64_ranges_kernel(const float* in, const int32_t* idx, double* out, int64_t n,
+                                         unsigned long long* stamp, uint32_t* epoch, const float* cin, double* cout,
+                                         int64_t cn, int64_t lo, int64_t hi) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
+        if (epoch) *epoch += 1u;
+    }
+    const int64_t pa = lo >> 1, pb = (cn - hi + 1) >> 1;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x, items = n + pa + pb;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < items; i += step) {
+        if (i < n) {
+            out[i] = (double)in[idx[i]];
+        } else {
+            const int64_t j = i < n + pa ? 2 * (i - n) : hi + 2 * (i - n - pa);
+            cout[j] = (double)cin[j];
+            if (j + 1 < cn) cout[j + 1] = (double)cin[j + 1];
+        }
+    }
+}
+
 // gather_f64_kernel with a factored pose-landmark region (LinParams::pl_factored): items [0, n) the
 // right-hand side gather, then the block array in pairs of values outside the region and one slot
 // per item inside it (3 fp32 values in, 6 fp64 values out: the block J_p^T J_l, J_p = (-J_lx, -J_ly,
@@ -1195,6 +1218,17 @@ hipError_t launch_gather_f64_factored(const float* in, const int32_t* idx, doubl
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 8192));
     hipLaunchKernelGGL(gather_f64_factored_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n, stamp, epoch,
                        cin, cout, cn, pl_off, pl_slots);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_f64_ranges(const float* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
+                                    unsigned long long* stamp, uint32_t* epoch, const float* cin, double* cout,
+                                    int64_t cn, int64_t lo, int64_t hi) {
+    if ((lo & 1) || (hi & 1) || lo > hi || hi > cn) return hipErrorInvalidValue;   // checked before launching
+    const int64_t items = n + (lo >> 1) + ((cn - hi + 1) >> 1);
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 8192));
+    hipLaunchKernelGGL(gather_f64_ranges_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, idx, out, n, stamp, epoch,
+                       cin, cout, cn, lo, hi);
     return hipGetLastError();
 }
 

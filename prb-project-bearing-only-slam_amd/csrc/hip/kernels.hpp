@@ -195,6 +195,11 @@ hipError_t launch_gather_f64(const T* in, const int32_t* idx, double* out, int64
 hipError_t launch_gather_f64_factored(const float* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
                                       unsigned long long* stamp, uint32_t* epoch, const float* cin, double* cout,
                                       int64_t cn, int64_t pl_off, int64_t pl_slots);
+// the right-hand side gather and the fp64 copy of the block array outside [lo, hi) (the region the
+// folds read from the fp32 array themselves, mf_set_fold_source)
+hipError_t launch_gather_f64_ranges(const float* in, const int32_t* idx, double* out, int64_t n, hipStream_t s,
+                                    unsigned long long* stamp, uint32_t* epoch, const float* cin, double* cout,
+                                    int64_t cn, int64_t lo, int64_t hi);
 // Host-side expansion of a factored block array (bos_export_system): region as above, in place on a
 // copy of the fp32 array converted to double
 void expand_factored_host(const float* in, double* out, int64_t n, int64_t pl_off, int64_t pl_slots);

@@ -23,6 +23,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../host/plan.hpp"
@@ -94,6 +95,8 @@ struct MfArgs {
     const int64_t* findex_off;
     const int32_t* findex;
     const double* A;             // CSR values of H (fp64)
+    const float* A32;            // fp32 block array the fold reads instead of A (see mf_set_fold_source),
+    int64_t pl_lo;               // and where its factored pose-landmark region starts; A32 null otherwise
     double* L;
     double* U;
     double* u;
@@ -319,24 +322,68 @@ __device__ __forceinline__ int4 fold_rec_load(const MfArgs& a, int q, int half) 
 struct FoldVals {
     double ht0, ht1, a00, a10, a11, x0, x1;
 };
+// The same from the fp32 build (F32: mf_set_fold_source): the bearing's factored block (J_theta,
+// J_lx, J_ly) and the landmark's 2 x 2 block as loaded, the row's pose dof and the entries' presence
+// in flags; fold_decode forms the doubles the fp64 copy would hold (products in fp32, as
+// gather_f64_factored_kernel expands them), so the result is bit-identical.
+struct FoldVals32 {
+    float jt, jx, jy, a00, a10, a11;
+    int flags;   // pose dof of the row (0..2; 3: no entry) | a00, a10, a11 present << 2, 3, 4
+    double x0, x1;
+};
+template <bool F32> using FoldValsT = typename std::conditional<F32, FoldVals32, FoldVals>::type;
 
-__device__ __forceinline__ FoldVals fold_vals(const MfArgs& a, const int4& r0, const int4& r1, bool mine) {
+__device__ __forceinline__ FoldVals fold_decode(const FoldVals& v) { return v; }
+__device__ __forceinline__ FoldVals fold_decode(const FoldVals32& v) {
+    const int row = v.flags & 3;
+    const float p = row == 0 ? -v.jx : row == 1 ? -v.jy : v.jt;
+    FoldVals d;
+    d.ht0 = row == 3 ? 0.0 : (double)(p * v.jx);
+    d.ht1 = row == 3 ? 0.0 : (double)(p * v.jy);
+    d.a00 = (v.flags & 4) ? (double)v.a00 : 0.0;
+    d.a10 = (v.flags & 8) ? (double)v.a10 : 0.0;
+    d.a11 = (v.flags & 16) ? (double)v.a11 : 0.0;
+    d.x0 = v.x0;
+    d.x1 = v.x1;
+    return d;
+}
+
+template <bool F32>
+__device__ __forceinline__ FoldValsT<F32> fold_vals(const MfArgs& a, const int4& r0, const int4& r1, bool mine) {
+    if constexpr (F32) {
+        // records index the fp64 layout: pose-landmark entry (t, j) of slot q at pl_lo + 6 q + 2 t + j,
+        // held factored at pl_lo + 3 q of the fp32 array (mf_set_fold_source checked the records)
+        const int e = max(r0.x - (int)a.pl_lo, 0);
+        const int q = e / 6, row = (e - 6 * q) >> 1;
+        const float* f = a.A32 + a.pl_lo + 3 * (int64_t)q;
+        FoldVals32 v;
+        v.jt = f[0];
+        v.jx = f[1];
+        v.jy = f[2];
+        v.a00 = a.A32[max(r0.z, 0)];
+        v.a10 = a.A32[max(r0.w, 0)];
+        v.a11 = a.A32[max(r1.x, 0)];
+        v.x0 = a.x[r1.y];   // (a lane past the chunk's rows reads its last row's: see fold_chunk)
+        v.x1 = a.x[r1.y + 1];
+        v.flags = (r0.x >= 0 ? row : 3) | (r0.z >= 0 ? 4 : 0) | (r0.w >= 0 ? 8 : 0) | (r1.x >= 0 ? 16 : 0);
+        return v;
+    } else {
     // every load unconditional (indices clamped to valid ones), the value selected afterwards: a
     // predicated load would be a branch with its wait inside, and the next chunk's values must stay
     // in flight while the current chunk is processed
     const double ht0 = a.A[max(r0.x, 0)], ht1 = a.A[max(r0.y, 0)], a00 = a.A[max(r0.z, 0)], a10 = a.A[max(r0.w, 0)];
     const double a11 = a.A[max(r1.x, 0)];
-    const int xi = mine ? r1.y : 0;
-    const double x0 = a.x[xi], x1 = a.x[xi + 1];
+    const double x0 = a.x[r1.y], x1 = a.x[r1.y + 1];   // (lanes past the rows: their last row's)
     FoldVals v;
     v.ht0 = r0.x >= 0 ? ht0 : 0.0;
     v.ht1 = r0.y >= 0 ? ht1 : 0.0;
     v.a00 = r0.z >= 0 ? a00 : 0.0;
     v.a10 = r0.w >= 0 ? a10 : 0.0;
     v.a11 = r1.x >= 0 ? a11 : 0.0;
-    v.x0 = mine ? x0 : 0.0;
-    v.x1 = mine ? x1 : 0.0;
+    v.x0 = x0;
+    v.x1 = x1;
     return v;
+    }
 }
 
 // The chunk boundaries of a front (fold_chunk[c], c uniform) from one register holding 64 of them
@@ -349,21 +396,111 @@ struct ChunkTable {
         base = b;
         v = a.fold_chunk[b + lane];   // padded array (up()): in bounds
     }
+    // the same inside the chunk loop, waited for on the spot: a load left pending on this rarely taken
+    // path would make the compiler wait for every outstanding load at the loop's top on every path
+    __device__ __forceinline__ void reload(const MfArgs& a, int b, int lane) {
+        load(a, b, lane);
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) (expcnt, lgkmcnt: no wait)
+    }
     // fold_chunk[c] for c in [base, base + 64)
     __device__ __forceinline__ int at(int c) const { return __builtin_amdgcn_readlane(v, c - base); }
 };
 
-template <int MAXM>
-__device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W, FoldBuf* fb, int m, int lane,
-                                              FoldAcc<MAXM>& acc) {
+// One fold chunk's elimination (values v, records' meta q1, n rows): the landmarks' 2 x 2 factors, L
+// panels and forward steps, the chunk's W in LDS, and W W^T / -W y accumulated.
+template <int MAXM, typename VALS>
+__device__ __forceinline__ void fold_chunk(const MfArgs& a, double* W, FoldBuf* fb, int m, int lane,
+                                           FoldAcc<MAXM>& acc, const VALS& vraw, const int4& q1, int n,
+                                           bool first, int s, int& nbad) {
+    const FoldVals v = fold_decode(vraw);
     constexpr int NB = FoldAcc<MAXM>::NB;
     constexpr int WS = 2 * fold_chunk_landmarks(MAXM) + 1;   // W row stride (odd: no bank conflicts)
     const int nbm = (m + 15) >> 4;
+    const int t = q1.z & 63, rc = (q1.z >> 6) & 63, pos = (q1.z >> 12) & 63, lml = (q1.z >> 18) & 63;
+    const bool mine = lane < n;
+    const int nl = __builtin_amdgcn_readlane(lml, n - 1) + 1;   // landmarks of this chunk
+    const int col0 = q1.y;
+    const int64_t loff = q1.w;
+    // Every lane issues the same global stores: a store under a divergent branch leaves the number of
+    // memory operations after the next chunk's loads unknown to the compiler, which then waits for
+    // all of them (vmcnt(0)) at the top of every chunk instead of for the loads alone. A lane past
+    // the chunk's rows holds the record and values of its last row, and every row of a landmark the
+    // landmark's values, so the extra stores write the owners' values, bit for bit, to the owners'
+    // addresses (a shared sink instead was measured 17 us slower: every wave of the GPU wrote the
+    // same lines).
+    {
+        double d0 = v.a00;
+        const bool bad0 = !(d0 > 0.0);
+        d0 = bad0 ? 1e-300 : d0;
+        const double i0 = rsqrt_nr(d0), l00 = d0 * i0;
+        const double l10 = v.a10 * i0;
+        double d1 = v.a11 - l10 * l10;
+        const bool bad1 = !(d1 > 0.0);
+        d1 = bad1 ? 1e-300 : d1;
+        const double i1 = rsqrt_nr(d1), l11 = d1 * i1;
+        const double lt0 = v.ht0 * i0, lt1 = (v.ht1 - lt0 * l10) * i1;
+        const double y0 = v.x0 * i0, y1 = (v.x1 - l10 * y0) * i1;
+        const int mc = 2 + rc;
+        double* Lc = a.L + loff;
+        const bool head = mine && t == 0;
+        Lc[2 + t] = lt0;
+        Lc[mc + 2 + t] = lt1;
+        Lc[0] = l00;
+        Lc[1] = l10;
+        Lc[mc + 1] = l11;
+        a.x[col0] = y0;
+        a.x[col0 + 1] = y1;
+        nbad += head ? (int)bad0 + (int)bad1 : 0;
+        if (head) {
+            fb->y[2 * lml] = y0;
+            fb->y[2 * lml + 1] = y1;
+        }
+        if (mine) {
+            W[pos * WS + 2 * lml] = lt0;
+            W[pos * WS + 2 * lml + 1] = lt1;
+        }
+    }
+#ifdef BOS_MF_FOLD_STAMPS   // measurement builds: the first chunk's values have arrived (slot 6)
+    if (first) fstamp(a.stamps_f, s, 6);
+#endif
+    wave_sync();
+    const int kc = 2 * nl;
+    if (lane < m) {   // u-vector part: -(W y) at this lane's position
+        double w = 0.0;
+        for (int q = 0; q < kc; ++q) w += W[lane * WS + q] * fb->y[q];
+        acc.w -= w;
+    }
+    // W W^T, 4 columns per MFMA step; lane l feeds row 16 b + (l & 15), column 4 st + (l >> 4)
+    // of W to the blocks of row b (as A) and of column b (as B, the same values)
+    for (int st = 0; 4 * st < kc; ++st) {
+        double av[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) av[b] = b < nbm ? W[(16 * b + (lane & 15)) * WS + 4 * st + (lane >> 4)] : 0.0;
+        int q = 0;
+#pragma unroll
+        for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+            for (int bj = 0; bj <= bi; ++bj, ++q)
+                if (bi < nbm) acc.d[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], av[bj], acc.d[q], 0, 0, 0);
+    }
+    wave_sync();
+    if (mine) {   // clear this chunk's W entries for the next chunk
+        W[pos * WS + 2 * lml] = 0.0;
+        W[pos * WS + 2 * lml + 1] = 0.0;
+    }
+    wave_sync();
+}
+
+template <int MAXM, bool F32>
+__device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W, FoldBuf* fb, int m, int lane,
+                                              FoldAcc<MAXM>& acc) {
+    constexpr int WS = 2 * fold_chunk_landmarks(MAXM) + 1;
 #pragma unroll
     for (int q = 0; q < FoldAcc<MAXM>::NP; ++q) acc.d[q] = dbl4{0.0, 0.0, 0.0, 0.0};
     acc.w = 0.0;
     for (int e = lane; e < MAXM * WS; e += 64) W[e] = 0.0;
     const int ch0 = a.fold_cptr[s], ch1 = a.fold_cptr[s + 1];
+    int nbad = 0;   // non-positive 2 x 2 pivots of the folded landmarks (head lanes)
     ChunkTable tb;
     tb.load(a, ch0, lane);
     // chunk c: rows [at(c), at(c + 1)); records of a lane past the chunk's rows (or of a chunk past
@@ -377,86 +514,32 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
     int n = len(ch0);
     int4 r0, r1;
     rec(ch0, n, r0, r1);
-    FoldVals v = fold_vals(a, r0, r1, lane < n);
+    FoldValsT<F32> v = fold_vals<F32>(a, r0, r1, lane < n);
     // next chunk's records, then (inside the loop) its values, both one chunk ahead
     int nn = len(ch0 + 1);
     int4 n0, n1;
     rec(ch0 + 1, nn, n0, n1);
+    // Wait for the prologue's loads here: the loop's top then needs no wait on either path (from the
+    // back edge, the next chunk's records precede only the last chunk's stores). Left to the
+    // compiler, the top waits for every outstanding load and store (vmcnt(0)) because on the entry
+    // path the records are the last loads issued.
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     for (int ch = ch0; ch < ch1; ++ch) {
-        if (ch + 3 - tb.base > 63) tb.load(a, ch, lane);   // (uniform; fronts with > 60 chunks only)
-        const double ht0 = v.ht0, ht1 = v.ht1, a00 = v.a00, a10 = v.a10, a11 = v.a11;
-        const int t = r1.z & 63, rc = (r1.z >> 6) & 63, pos = (r1.z >> 12) & 63, lml = (r1.z >> 18) & 63;
-        const bool mine = lane < n;
-        const int nl = __builtin_amdgcn_readlane(lml, n - 1) + 1;   // landmarks of this chunk
-        const double x0 = v.x0, x1 = v.x1;
-        const int col0 = r1.y;
-        const int64_t loff = r1.w;
+        if (ch + 3 - tb.base > 63) tb.reload(a, ch, lane);   // (uniform; fronts with > 60 chunks only)
+        const FoldValsT<F32> cur = v;
+        const int4 q1 = r1;
+        const int ncur = n;
         // chunk ch + 1: values now (its records arrived during chunk ch - 1), records of ch + 2
-        v = fold_vals(a, n0, n1, lane < nn);
+        v = fold_vals<F32>(a, n0, n1, lane < nn);
         r0 = n0;
         r1 = n1;
         const int n2 = len(ch + 2);
         rec(ch + 2, n2, n0, n1);
-        if (mine) {
-            double d0 = a00;
-            int bad = 0;
-            if (!(d0 > 0.0)) { d0 = 1e-300; ++bad; }
-            const double i0 = rsqrt_nr(d0), l00 = d0 * i0;
-            const double l10 = a10 * i0;
-            double d1 = a11 - l10 * l10;
-            if (!(d1 > 0.0)) { d1 = 1e-300; ++bad; }
-            const double i1 = rsqrt_nr(d1), l11 = d1 * i1;
-            const double lt0 = ht0 * i0, lt1 = (ht1 - lt0 * l10) * i1;
-            const double y0 = x0 * i0, y1 = (x1 - l10 * y0) * i1;
-            const int mc = 2 + rc;
-            double* Lc = a.L + loff;
-            Lc[2 + t] = lt0;
-            Lc[mc + 2 + t] = lt1;
-            if (t == 0) {
-                Lc[0] = l00;
-                Lc[1] = l10;
-                Lc[mc + 1] = l11;
-                a.x[col0] = y0;
-                a.x[col0 + 1] = y1;
-                if (bad) atomicAdd(a.info, bad);
-                fb->y[2 * lml] = y0;
-                fb->y[2 * lml + 1] = y1;
-            }
-            W[pos * WS + 2 * lml] = lt0;
-            W[pos * WS + 2 * lml + 1] = lt1;
-        }
-#ifdef BOS_MF_FOLD_STAMPS   // measurement builds: the first chunk's values have arrived (slot 6)
-        if (ch == ch0) fstamp(a.stamps_f, s, 6);
-#endif
-        wave_sync();
-        const int kc = 2 * nl;
-        if (lane < m) {   // u-vector part: -(W y) at this lane's position
-            double w = 0.0;
-            for (int q = 0; q < kc; ++q) w += W[lane * WS + q] * fb->y[q];
-            acc.w -= w;
-        }
-        // W W^T, 4 columns per MFMA step; lane l feeds row 16 b + (l & 15), column 4 st + (l >> 4)
-        // of W to the blocks of row b (as A) and of column b (as B, the same values)
-        for (int st = 0; 4 * st < kc; ++st) {
-            double av[NB];
-#pragma unroll
-            for (int b = 0; b < NB; ++b) av[b] = b < nbm ? W[(16 * b + (lane & 15)) * WS + 4 * st + (lane >> 4)] : 0.0;
-            int q = 0;
-#pragma unroll
-            for (int bi = 0; bi < NB; ++bi)
-#pragma unroll
-                for (int bj = 0; bj <= bi; ++bj, ++q)
-                    if (bi < nbm) acc.d[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], av[bj], acc.d[q], 0, 0, 0);
-        }
-        wave_sync();
-        if (mine) {   // clear this chunk's W entries for the next chunk
-            W[pos * WS + 2 * lml] = 0.0;
-            W[pos * WS + 2 * lml + 1] = 0.0;
-        }
-        wave_sync();
+        fold_chunk<MAXM>(a, W, fb, m, lane, acc, cur, q1, ncur, ch == ch0, s, nbad);
         n = nn;
         nn = n2;
     }
+    if (nbad) atomicAdd(a.info, nbad);
 #ifdef BOS_MF_FOLD_STAMPS   // slot 7: the front's chunk count
     if (a.stamps_f && lane == 0) a.stamps_f[8 * (int64_t)s + 7] = (unsigned long long)(ch1 - ch0);
 #endif
@@ -657,7 +740,7 @@ __device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p,
 // their update matrices; after the partial Cholesky, lane i eliminates with its row of L (still in
 // registers): y_j = w_j / L_jj, w_i -= L_ij y_j. y goes to x, the remaining w (rows >= k) to the
 // front's u-vector for its parent.
-template <int MAXM, bool FLOW>
+template <int MAXM, bool FLOW, bool F32>
 __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf,
                                                  double* wv, FoldBuf* fb, int lane, const Flow* f) {
     constexpr bool COH = FLOW;
@@ -686,7 +769,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     fstamp(stp, s, 0);
     if (fold) {
         FoldAcc<MAXM> facc;
-        fold_children<MAXM>(a, s, F, fb, m, lane, facc);
+        fold_children<MAXM, F32>(a, s, F, fb, m, lane, facc);
         wave_sync();
         fold_store<MAXM>(facc, F, wv, m, lane);
     } else {
@@ -847,13 +930,13 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     wave_sync();
 }
 
-template <int MAXM>
+template <int MAXM, bool F32>
 __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * MAXM];
     __shared__ __attribute__((aligned(16))) double wv[MAXM];
     __shared__ FoldBuf fb;
-    factor_front_reg<MAXM, false>(a, a.level[blockIdx.x], F, colbuf, wv, &fb, threadIdx.x, nullptr);
+    factor_front_reg<MAXM, false, F32>(a, a.level[blockIdx.x], F, colbuf, wv, &fb, threadIdx.x, nullptr);
 }
 
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
@@ -1024,6 +1107,7 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
 // accordingly).
 constexpr int kFlowMaxM = kMfFlowMaxM;
 
+template <bool F32>
 __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f) {
     __shared__ __attribute__((aligned(16))) double F[kFlowMaxM * (kFlowMaxM + 1) / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * kFlowMaxM];
@@ -1036,7 +1120,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
         const int t = next_ticket(f.ticket);
         if (t >= f.n) break;
         const int s = f.order[t];
-        factor_front_reg<kFlowMaxM, true>(a, s, F, colbuf, wv, &fb, lane, &f);   // m <= kFlowMaxM
+        factor_front_reg<kFlowMaxM, true, F32>(a, s, F, colbuf, wv, &fb, lane, &f);   // m <= kFlowMaxM
         fstamp(f.stamps, s, 6);
         publish_done(f, s);
         fstamp(f.stamps, s, 7);
@@ -1044,10 +1128,11 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
     leave_flow(f);
 }
 
+template <bool F32>
 __global__ __launch_bounds__(64, 2) void mf_factor_flow(const MfArgs a, const Flow f_in) {
     Flow f = f_in;
     f.epoch = *f_in.epoch_src;
-    factor_flow_body(a, f);
+    factor_flow_body<F32>(a, f);
 }
 
 __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flow f_in, const int32_t* parent) {
@@ -1156,6 +1241,8 @@ struct MfDevice {
     int64_t *L_off = nullptr, *U_off = nullptr, *u_off = nullptr, *scratch_off = nullptr, *rmap_off = nullptr,
             *findex_off = nullptr;
     double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
+    const float* A32 = nullptr;   // mf_set_fold_source
+    int64_t pl_lo = 0;
 
     MfArgs args(const Prog& P, int lev, int c, const double* A, double* x) const {
         MfArgs g;
@@ -1164,7 +1251,7 @@ struct MfDevice {
         g.col0 = col0; g.k = k; g.r = r; g.L_off = L_off; g.U_off = U_off; g.u_off = u_off;
         g.scratch_off = scratch_off; g.child_ptr = child_ptr; g.child = child; g.rmap_off = rmap_off; g.rmap = rmap;
         g.amap_ptr = amap_ptr; g.amap_src = amap_src; g.amap_dst = amap_dst; g.findex_off = findex_off;
-        g.findex = findex; g.A = A; g.L = L; g.U = U; g.u = u; g.scratch = scratch; g.x = x; g.info = info;
+        g.findex = findex; g.A = A; g.A32 = A32; g.pl_lo = pl_lo; g.L = L; g.U = U; g.u = u; g.scratch = scratch; g.x = x; g.info = info;
         g.fold_cnt = fold_cnt; g.fold_cptr = fold_cptr; g.fold_chunk = fold_chunk; g.fold_rec = fold_rec;
         g.emap = emap; g.emap_off = emap_off;
         g.stamps_f = stamps;
@@ -1387,7 +1474,8 @@ void mf_destroy(MfDevice* d) {
 // reduce_stats launch (mf_info_ptr). The work-queue tickets reset themselves (leave_flow). Every
 // launch argument is fixed (the flows read the step's epoch from the device), so the sequence can be
 // captured once into a hipGraph and replayed.
-hipError_t mf_factor(MfDevice* d, int which, const double* A, double* x, hipStream_t s) {
+template <bool F32>
+hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipStream_t s) {
     hipError_t e;
     const Prog& P = d->prog[which];
     if (P.ptr.empty()) return hipSuccess;
@@ -1399,15 +1487,17 @@ hipError_t mf_factor(MfDevice* d, int which, const double* A, double* x, hipStre
         if (fork) {
             if ((e = hipEventRecord(d->ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(d->side, d->ev_fork, 0)) != hipSuccess)
                 return e;
-            hipLaunchKernelGGL(mf_factor_reg<64>, dim3(P.count(l, 3)), dim3(64), 0, d->side, d->args(P, l, 3, A, x));
+            hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(P.count(l, 3)), dim3(64), 0, d->side, d->args(P, l, 3, A, x));
             if (tiny16 && (n = P.count(l, 0)))
-                hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, d->side, d->args(P, l, 0, A, x));
+                hipLaunchKernelGGL((mf_factor_reg<16, F32>), dim3(n), dim3(64), 0, d->side, d->args(P, l, 0, A, x));
             if ((e = hipEventRecord(d->ev_join, d->side)) != hipSuccess) return e;
         }
-        if ((n = P.count(l, 0)) && !tiny16) hipLaunchKernelGGL(mf_factor_reg<16>, dim3(n), dim3(64), 0, s, d->args(P, l, 0, A, x));
-        if ((n = P.count(l, 1))) hipLaunchKernelGGL(mf_factor_reg<32>, dim3(n), dim3(64), 0, s, d->args(P, l, 1, A, x));
-        if ((n = P.count(l, 2))) hipLaunchKernelGGL(mf_factor_reg<48>, dim3(n), dim3(64), 0, s, d->args(P, l, 2, A, x));
-        if ((n = P.count(l, 3)) && !fork) hipLaunchKernelGGL(mf_factor_reg<64>, dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
+        if ((n = P.count(l, 0)) && !tiny16)
+            hipLaunchKernelGGL((mf_factor_reg<16, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 0, A, x));
+        if ((n = P.count(l, 1))) hipLaunchKernelGGL((mf_factor_reg<32, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 1, A, x));
+        if ((n = P.count(l, 2))) hipLaunchKernelGGL((mf_factor_reg<48, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 2, A, x));
+        if ((n = P.count(l, 3)) && !fork)
+            hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
         if (fork && (e = hipStreamWaitEvent(s, d->ev_join, 0)) != hipSuccess) return e;
         if ((n = P.count(l, 4))) {   // large fronts: workgroup factorization, then their forward step
             hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), P.lds_factor[l * kClasses + 4], s,
@@ -1421,10 +1511,19 @@ hipError_t mf_factor(MfDevice* d, int which, const double* A, double* x, hipStre
         const Flow f{P.order_factor, P.n_flow_factor, d->tickets, d->tickets + kMfTickets, d->done, d->epoch, 0u,
                      d->fid_f, P.id, d->stamps};
         const int grid = std::min(P.n_flow_factor, d->ncu * kFlowWavesFactor);
-        hipLaunchKernelGGL(mf_factor_flow, dim3(grid), dim3(64), 0, s, d->args(P, 0, 0, A, x), f);
+        hipLaunchKernelGGL((mf_factor_flow<F32>), dim3(grid), dim3(64), 0, s, d->args(P, 0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t mf_factor(MfDevice* d, int which, const double* A, double* x, hipStream_t s) {
+    return d->A32 ? mf_factor_t<true>(d, which, A, x, s) : mf_factor_t<false>(d, which, A, x, s);
+}
+
+void mf_set_fold_source(MfDevice* d, const float* A32, int64_t pl_lo) {
+    d->A32 = A32;
+    d->pl_lo = pl_lo;
 }
 
 hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {

@@ -22,6 +22,10 @@ void mf_destroy(MfDevice* d);
 // on exit for those fronts' dofs. Sharded: program 0 (own subtrees), then — once the other ranks'
 // subtree roots' U / u are in place — program 1 (the top).
 hipError_t mf_factor(MfDevice* d, int program, const double* A, double* x, hipStream_t s);
+// fp32 J+H with factored pose-landmark blocks whose pose-landmark and landmark-diagonal entries only
+// the folds read (bos::mf_fold_reads_fp32): the folds read them from the fp32 block array A32 (the
+// factored region starting at pl_lo), so the fp64 copy need not hold them. Null: the folds read A.
+void mf_set_fold_source(MfDevice* d, const float* A32, int64_t pl_lo);
 // Backward substitution of a program's fronts (x <- L^{-T} x); sharded: program 1, then program 0.
 hipError_t mf_solve(MfDevice* d, int program, double* x, hipStream_t s);
 // the update matrices / u-vectors (offsets Multifrontal::U_off / u_off): exchange 1 reads and

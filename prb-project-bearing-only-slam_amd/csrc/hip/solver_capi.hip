@@ -85,6 +85,9 @@ struct bos_solver {
     // fp32 build with a multifrontal solve, unit weights, no duplicate pairs: the J+H writes the
     // pose-landmark blocks factored (LinParams::pl_factored), the solver's fp64 conversion expands them
     bool pl_factored = false;
+    // ... and the folds read them (and the landmark diagonal blocks) from the fp32 array themselves, so
+    // the fp64 copy skips that region (bos::mf_fold_reads_fp32, mf_set_fold_source)
+    bool fold32 = false;
     size_t tsize = 8;   // sizeof(T)
     // state
     double* d_pose = nullptr;
@@ -361,6 +364,12 @@ int enqueue_solver_inputs(bos_solver* s) {
     unsigned long long* stamp = s->d_status->stamp + s->solve_stamp;
     uint32_t* epoch = uses_mf(s) ? bos::dev::mf_epoch_ptr(s->mf) : nullptr;
     const bool conv = f32 && uses_mf(s);   // the fp64 copy of the block array, in the same launch
+    if (s->fold32) {   // the copy skips what the folds read from the fp32 array
+        HIP_TRY(bos::dev::launch_gather_f64_ranges((const float*)s->sys_b, s->elim_ref, s->d_rhs, n, s->stream, stamp,
+                                                   epoch, (const float*)s->sys_val, s->d_val64, s->plan.blk.size,
+                                                   s->plan.blk.off_ldiag, s->plan.blk.off_pp));
+        return BOS_OK;
+    }
     if (s->pl_factored) {   // the copy expands the factored pose-landmark blocks
         HIP_TRY(bos::dev::launch_gather_f64_factored((const float*)s->sys_b, s->elim_ref, s->d_rhs, n, s->stream, stamp,
                                                      epoch, (const float*)s->sys_val, s->d_val64, s->plan.blk.size,
@@ -1137,6 +1146,10 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         std::string merr;
         if (bos::dev::mf_create(P.mf, s->sharded ? P.shard.sn_owner.data() : nullptr, s->rank, &s->mf, merr))
             return bail(fail(BOS_ERR_DEVICE, merr));
+#ifndef BOS_MF_NO_FOLD32   // (measurement builds: the folds read the fp64 copy)
+        s->fold32 = s->pl_factored && bos::mf_fold_reads_fp32(P);
+#endif
+        if (s->fold32) bos::dev::mf_set_fold_source(s->mf, (const float*)s->sys_val, P.blk.off_pl);
     } else if (s->solver_kind == BOS_SOLVER_ROCSOLVER_RF) {
         std::vector<int32_t> piv(P.n);
         for (int64_t i = 0; i < P.n; ++i) piv[i] = (int32_t)i;   // ordering already applied in the layout
@@ -1469,6 +1482,7 @@ int bos_system_info_get(const bos_solver* s, bos_system_info* info) {
     info->algorithmic_bytes = s->precision == BOS_FP32 ? 36 * Mb + 80 * Mo + 60 * NP + 32 * NL
                                                        : 64 * Mb + 152 * Mo + 120 * NP + 64 * NL;
     info->pl_factored = s->pl_factored ? 1 : 0;
+    info->fold_fp32 = s->fold32 ? 1 : 0;
     info->layout_bytes = info->algorithmic_bytes - (s->pl_factored ? 12 * Mb : 0);
     info->num_block_values = P.blk.size;
     info->lanes_per_pose = P.blk.lpp;

@@ -1039,6 +1039,32 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
     return BOS_OK;
 }
 
+bool mf_fold_reads_fp32(const Plan& P) {
+    const Multifrontal& F = P.mf;
+    const int ns = (int)F.k.size();
+    if (ns == 0 || F.fold_rec.empty()) return false;
+    const int64_t lo = P.blk.off_ldiag, pl = P.blk.off_pl, hi = P.blk.off_pp;
+    if (hi > INT32_MAX) return false;
+    std::vector<char> folded(ns, 0);
+    for (int p = 0; p < ns; ++p)
+        for (int ci = F.child_ptr[p]; ci < F.child_ptr[p] + F.fold_cnt[p]; ++ci) folded[F.child[ci]] = 1;
+    for (int s = 0; s < ns; ++s) {
+        if (folded[s]) continue;
+        for (int q = F.amap_ptr[s]; q < F.amap_ptr[s + 1]; ++q)
+            if (F.amap_src[q] >= lo && F.amap_src[q] < hi) return false;
+    }
+    const size_t nrec = F.fold_rec.size() / kFoldRec;
+    for (size_t q = 0; q < nrec; ++q) {
+        const int32_t* r = &F.fold_rec[kFoldRec * q];
+        if (r[0] >= 0 || r[1] >= 0) {
+            if (r[0] < pl || r[0] >= hi || ((r[0] - pl) & 1) || r[1] != r[0] + 1) return false;
+        }
+        for (int j = 2; j < 5; ++j)
+            if (r[j] >= 0 && (r[j] < lo || r[j] >= pl)) return false;
+    }
+    return true;
+}
+
 // Proves, on the host, that the J+H kernel's writes (simulated here exactly as hip/kernels.hip
 // issues them for this rank's lanes) write every value of the block array and every b entry at
 // most once, that every value a front this rank factors reads (assembly map and fold records) is

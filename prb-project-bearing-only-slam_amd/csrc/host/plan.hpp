@@ -231,6 +231,12 @@ void observation_lanes(const Plan& P, int rank, int world, int64_t& pb0, int64_t
 // block by the lower pose): owned[e] = 1
 void owned_entries(const Plan& P, const std::vector<char>& lane_node, std::vector<uint8_t>& owned);
 
+// True when the multifrontal plan reads the pose-landmark and landmark-diagonal entries of the block
+// array [off_ldiag, off_pp) only through fold records, each record's pose-landmark pair (t, 0), (t, 1)
+// of one slot and its landmark block inside the landmark-diagonal region: the folds can then read the
+// fp32 build's factored blocks directly (mf_set_fold_source) and the fp64 copy can skip the region.
+bool mf_fold_reads_fp32(const Plan& P);
+
 // Segments of exchange 1 for rank `rank` (hip/solver_capi.hip): pack = this rank's roots' U / u into
 // its send buffer, unpack = every other rank's roots from the receive buffer (kinds: 0 U, 1 u, 2 send,
 // 3 receive; offsets in doubles).

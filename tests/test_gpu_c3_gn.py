@@ -54,6 +54,9 @@ def oracle_step(Q, pose, lm, jh_precision):
 def run_pair(P, precision, iters):
     Q = to_oracle(P)
     S = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR)
+    # the benchmarked path: fp32 J+H with factored pose-landmark blocks that the folds read directly
+    info = S.system_info()
+    assert (info["pl_factored"], info["fold_fp32"]) == ((1, 1) if precision == bos.BOS_FP32 else (0, 0)), info
     po, lo = Q.copy_state()
     out = []
     for i in range(iters):

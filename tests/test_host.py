@@ -247,6 +247,17 @@ def test_schur_plan_fronts_fit_the_wave_kernels(seed):
     assert info["mf_balance_pct"] in (40, 35, 45, 30, 20)
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_schur_folds_alone_read_the_landmark_region(seed):
+    """With the Schur ordering every landmark is folded into a pose front, so only the folds read the
+    pose-landmark and landmark-diagonal entries of H (bos::mf_fold_reads_fp32): an fp32 build's folds
+    then read them from the fp32 block array and its fp64 copy skips the region. The
+    nested-dissection ordering factors landmark fronts itself, so it must not qualify."""
+    P = bos.synthetic(3000, 6000, 10, seed=seed)
+    assert bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR)["mf_fold_fp32"]
+    assert not bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SUPERNODAL)["mf_fold_fp32"]
+
+
 def test_schur_plan_fallback_keeps_a_valid_plan():
     """When no separator balance fits (forced here with 40-pose leaves: every leaf front has more
     than 64 rows), the first (40 %) plan is kept; it still validates and solves like SciPy."""
