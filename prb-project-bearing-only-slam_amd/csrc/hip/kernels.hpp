@@ -7,7 +7,10 @@
 namespace bos {
 namespace dev {
 
-constexpr int kBlock = 256;
+#ifndef BOS_JH_BLOCK
+#define BOS_JH_BLOCK 256
+#endif
+constexpr int kBlock = BOS_JH_BLOCK;   // J+H workgroup (host/plan.hpp kJhBlock)
 // padding records after each lane-list array: the J+H kernel reads records up to five items past a
 // lane's last one, unguarded
 constexpr int kRecPad = 512;

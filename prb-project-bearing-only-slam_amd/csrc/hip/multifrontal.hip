@@ -1430,9 +1430,12 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         (rc = up(&d->fold_cnt, F.fold_cnt, err)) || (rc = up(&d->fold_cptr, F.fold_cptr, err)) ||
         (rc = up(&d->fold_chunk, F.fold_chunk, err)) || (rc = up(&d->fold_rec, F.fold_rec, err)))
         return rc;
+#ifndef BOS_MF_EVENT_FLAGS   // (measurement builds: other fence scopes for the fork / join events)
+#define BOS_MF_EVENT_FLAGS 0
+#endif
     if (hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming | BOS_MF_EVENT_FLAGS) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming | BOS_MF_EVENT_FLAGS) != hipSuccess) {
         err = "side stream creation failed (multifrontal)";
         return -2;
     }

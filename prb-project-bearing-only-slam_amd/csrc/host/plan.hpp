@@ -31,7 +31,10 @@ struct ProblemIndex {
 };
 
 // J+H launch geometry shared by the host plan and the kernel (hip/kernels.hpp kBlock)
-constexpr int kJhBlock = 256;
+#ifndef BOS_JH_BLOCK   // (measurement builds: other J+H workgroup sizes, tools/build_full_variant.sh)
+#define BOS_JH_BLOCK 256
+#endif
+constexpr int kJhBlock = BOS_JH_BLOCK;
 // Contiguous share [a, b) of n items for rank r of W (BOS_PARTITION_OBSERVATIONS: each rank runs a
 // range of the J+H's pose blocks and one of its landmark blocks, i.e. of the observations in
 // measurement order)
