@@ -125,7 +125,7 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 // position lane, the u-vector part -W y.
 template <int MAXM>
 struct FoldAcc {
-    static constexpr int NB = MAXM / 16, NP = NB * (NB + 1) / 2;
+    static constexpr int NB = (MAXM + 15) / 16, NP = NB * (NB + 1) / 2;
     dbl4 d[NP];
     double w;
 };

@@ -17,10 +17,10 @@ _, meta = S.debug_solver_stamps(nsuper)
 lev, k, r = meta[:, 0], meta[:, 1], meta[:, 2]
 m = k + r
 folded = k == 2
-edges = [0, 16, 24, 32, 36, 40, 44, 48, 56, 64, 1 << 30]
+edges = [0, 16, 24, 32, 36, 40, 44, 48, 56, 64, 1 << 30]   # bin i: edges[i] < m <= edges[i + 1]
 print("level fronts " + " ".join(f"<={e:>3d}" if e < 1 << 30 else "  >64" for e in edges[1:]))
 for l in sorted(set(lev[~folded])):
     sel = (lev == l) & ~folded
-    h = np.histogram(m[sel], bins=edges)[0]
+    h = np.histogram(m[sel], bins=np.array(edges) + 0.5)[0]
     print(f"{l:5d} {sel.sum():6d} " + " ".join(f"{x:5d}" for x in h))
 S.close()
