@@ -300,7 +300,7 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 
 // phase stamp k of front s (lane 0; the product launches pass no stamp buffer)
 __device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
-    if (stp && threadIdx.x == 0) stp[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
+    if (stp && (threadIdx.x & 63) == 0) stp[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Folded landmark children (Schur ordering) of front s, eliminated by its wave: per chunk (whole
@@ -595,7 +595,18 @@ struct Flow {
                             // per-level launches, the other program, or another rank's exchange)
     int id;
     unsigned long long* stamps;   // diagnostics (bos_debug_solver_stamps): 8 realtime stamps per front, or null
+    // the top launch (one workgroup, mf_factor_top / mf_backward_top): its fronts' completion flags in
+    // LDS (by position in `order`), the position of the front a wave works on, and each position's
+    // dependencies inside the launch (children for the factorization, the parent backward)
+    int* lds_done;
+    int pos;
+    const int32_t* dep_ptr;   // [n + 1]
+    const int32_t* dep_pos;
 };
+
+// Front-processing modes: per-level launch (no waits), dataflow launch (flags in global memory,
+// coherent hand-off), top launch (one workgroup: flags in LDS, hand-off through the CU's caches)
+constexpr int kModeLevel = 0, kModeFlow = 1, kModeTop = 2;
 
 constexpr int kStall = kMfStall;               // or-ed into info when a dependency wait times out
 constexpr uint64_t kWaitTicks = 5000000;        // 50 ms of the 100 MHz realtime clock
@@ -654,6 +665,35 @@ __device__ __forceinline__ void leave_flow(const Flow& f) {
         __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(f.exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// The top launch's hand-off (one workgroup, so workgroup scope): the dependency's LDS flag, then an
+// acquire fence at workgroup scope (no cache invalidation: every wave of the workgroup shares the CU's
+// caches); bounded like wait_done.
+__device__ __forceinline__ void wait_lds(const Flow& f, int pos, int32_t* info) {
+    if ((threadIdx.x & 63) == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f.lds_done + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+            if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStall) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) {
+                atomicOr(info, kStall);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+}
+
+__device__ __forceinline__ void wait_deps_lds(const Flow& f, int32_t* info) {
+    for (int q = f.dep_ptr[f.pos]; q < f.dep_ptr[f.pos + 1]; ++q) wait_lds(f, f.dep_pos[q], info);
+}
+
+// release at workgroup scope (the front's stores complete before the flag), then the LDS flag
+__device__ __forceinline__ void publish_lds(const Flow& f) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(f.lds_done + f.pos, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 __device__ __forceinline__ void publish_done(const Flow& f, int s) {
@@ -740,10 +780,10 @@ __device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p,
 // their update matrices; after the partial Cholesky, lane i eliminates with its row of L (still in
 // registers): y_j = w_j / L_jj, w_i -= L_ij y_j. y goes to x, the remaining w (rows >= k) to the
 // front's u-vector for its parent.
-template <int MAXM, bool FLOW, bool F32>
+template <int MAXM, int MODE, bool F32>
 __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double* F, double* colbuf,
                                                  double* wv, FoldBuf* fb, int lane, const Flow* f) {
-    constexpr bool COH = FLOW;
+    constexpr bool COH = MODE == kModeFlow;
     const int k = a.k[s], r = a.r[s], m = k + r;
     const int nfold = a.fold_cnt[s];
     const int c0 = a.col0[s];
@@ -781,9 +821,11 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     assemble_wave(a, aq0, aq1, F, lane, fold);
     wave_sync();
     fstamp(stp, s, 2);
-    if constexpr (FLOW) {
+    if constexpr (MODE == kModeFlow) {
         for (int ci = a.child_ptr[s]; ci < ce; ++ci)
             if (f->fid[a.child[ci]] == f->id) wait_done(*f, a.child[ci], a.info);
+    } else if constexpr (MODE == kModeTop) {
+        wait_deps_lds(*f, a.info);
     }
     fstamp(stp, s, 3);
     // extend-add, children in list order (deterministic)
@@ -936,7 +978,7 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double colbuf[2 * MAXM];
     __shared__ __attribute__((aligned(16))) double wv[MAXM];
     __shared__ FoldBuf fb;
-    factor_front_reg<MAXM, false, F32>(a, a.level[blockIdx.x], F, colbuf, wv, &fb, threadIdx.x, nullptr);
+    factor_front_reg<MAXM, kModeLevel, F32>(a, a.level[blockIdx.x], F, colbuf, wv, &fb, threadIdx.x, nullptr);
 }
 
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
@@ -945,10 +987,10 @@ __global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
 // kernel stages them before it waits for the parent (FLOW: f and parent set).
 constexpr int kBwdRegK = 32;   // fronts with k <= this solve their triangle from registers
 
-template <bool FLOW>
+template <int MODE>
 __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w, int lane, const Flow* f,
                                                const int32_t* parent) {
-    constexpr bool COH = FLOW;
+    constexpr bool COH = MODE == kModeFlow;
     const int k = a.k[s], r = a.r[s], m = k + r;
     const int c0 = a.col0[s];
     const int32_t* fi = a.findex + a.findex_off[s];
@@ -959,7 +1001,7 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
     const int xi0 = fi[k + min(lane, max(r - 1, 0))];
     unsigned long long* const stp = f ? f->stamps : a.stamps_b;
     fstamp(stp, s, 0);
-    if constexpr (!FLOW) {
+    if constexpr (MODE == kModeLevel) {
         // per-level launch: the parents' x are final (earlier launches), so the front's own
         // right-hand side and the first 64 rows' x are loaded beside the panel, all in flight at once
         const double y0v = a.x[c0 + min(lane, k - 1)], xr0v = a.x[xi0];
@@ -976,7 +1018,11 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
         for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
         fstamp(stp, s, 1);
-        if (parent[s] >= 0 && f->fid[parent[s]] == f->id) wait_done(*f, parent[s], a.info);
+        if constexpr (MODE == kModeFlow) {
+            if (parent[s] >= 0 && f->fid[parent[s]] == f->id) wait_done(*f, parent[s], a.info);
+        } else {
+            wait_deps_lds(*f, a.info);
+        }
         fstamp(stp, s, 2);
         if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
         for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
@@ -992,7 +1038,7 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         // 1 / L_jj by every lane at once, off the sequential chain below
         const double yv = own ? w[lane] : 0.0, rjj = own ? 1.0 / Lw[lane + lane * m] : 1.0;
         double xv = 0.0;
-        if (!FLOW && k <= kBwdRegK) {   // per-level launches only (the flow keeps its registers)
+        if (MODE == kModeLevel && k <= kBwdRegK) {   // per-level launches only (the flow keeps its registers)
             // the lane's column of the k x k block in registers, read from LDS before the chain, so
             // each step of the sequential chain is arithmetic and a lane read only
             double lr[kBwdRegK];
@@ -1040,7 +1086,7 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
 
 __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
     extern __shared__ __attribute__((aligned(16))) double w[];
-    backward_front<false>(a, a.level[blockIdx.x], w, threadIdx.x, nullptr, nullptr);
+    backward_front<kModeLevel>(a, a.level[blockIdx.x], w, threadIdx.x, nullptr, nullptr);
 }
 
 // Backward substitution of the folded landmarks (k = 2), kFoldLanes lanes each (rows of the
@@ -1120,7 +1166,7 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
         const int t = next_ticket(f.ticket);
         if (t >= f.n) break;
         const int s = f.order[t];
-        factor_front_reg<kFlowMaxM, true, F32>(a, s, F, colbuf, wv, &fb, lane, &f);   // m <= kFlowMaxM
+        factor_front_reg<kFlowMaxM, kModeFlow, F32>(a, s, F, colbuf, wv, &fb, lane, &f);   // m <= kFlowMaxM
         fstamp(f.stamps, s, 6);
         publish_done(f, s);
         fstamp(f.stamps, s, 7);
@@ -1143,11 +1189,75 @@ __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flo
         const int t = next_ticket(f.ticket);
         if (t >= f.n) break;
         const int s = f.order[t];
-        backward_front<true>(a, s, w, threadIdx.x, &f, parent);
+        backward_front<kModeFlow>(a, s, w, threadIdx.x, &f, parent);
         publish_done(f, s);
         fstamp(f.stamps, s, 4);
     }
     leave_flow(f);
+}
+
+// The top of the tree as one workgroup of kTopWaves waves (levels with at most that many fronts,
+// mf_create): a wave takes the next front from an LDS ticket, waits for its children of this launch
+// on LDS flags, and hands its update matrix / u-vector over through plain stores and loads (the
+// workgroup's waves share the CU's caches), ordered by release / acquire fences at workgroup scope.
+// Fronts further down finished in earlier launches.
+constexpr int kTopWaves = kMfTopWaves;
+constexpr int kTopMax = 256;   // fronts of a top launch (mf_create keeps the top within this)
+
+__device__ __forceinline__ int lds_ticket(int* ticket) {
+    int t = 0;
+    if ((threadIdx.x & 63) == 0) t = atomicAdd(ticket, 1);
+    return __builtin_amdgcn_readfirstlane(t);
+}
+
+template <bool F32>
+__global__ __launch_bounds__(64 * kTopWaves) void mf_factor_top(const MfArgs a, const Flow f_in) {
+    __shared__ __attribute__((aligned(16))) double F[kTopWaves][kFlowMaxM * (kFlowMaxM + 1) / 2];
+    __shared__ __attribute__((aligned(16))) double colbuf[kTopWaves][2 * kFlowMaxM];
+    __shared__ __attribute__((aligned(16))) double wv[kTopWaves][kFlowMaxM];
+    __shared__ FoldBuf fb[kTopWaves];
+    __shared__ int done[kTopMax];
+    __shared__ int ticket;
+    for (int i = threadIdx.x; i < kTopMax; i += blockDim.x) done[i] = 0;
+    if (threadIdx.x == 0) ticket = 0;
+    __syncthreads();
+    const int wv_id = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    Flow f = f_in;
+    f.lds_done = done;
+    for (int it = 0; it <= f.n; ++it) {   // bounded (see factor_flow_body)
+        const int t = lds_ticket(&ticket);
+        if (t >= f.n) break;
+        f.pos = t;
+        const int s = f.order[t];
+        factor_front_reg<kFlowMaxM, kModeTop, F32>(a, s, F[wv_id], colbuf[wv_id], wv[wv_id], &fb[wv_id], lane, &f);
+        fstamp(f.stamps, s, 6);
+        publish_lds(f);
+        fstamp(f.stamps, s, 7);
+    }
+}
+
+// Backward substitution of the top, top-down in the same form (dependency: the parent); LDS per wave:
+// lds_bwd bytes (dynamic, kTopWaves slices)
+__global__ __launch_bounds__(64 * kTopWaves) void mf_backward_top(const MfArgs a, const Flow f_in, int slice) {
+    extern __shared__ __attribute__((aligned(16))) double wl[];
+    __shared__ int done[kTopMax];
+    __shared__ int ticket;
+    for (int i = threadIdx.x; i < kTopMax; i += blockDim.x) done[i] = 0;
+    if (threadIdx.x == 0) ticket = 0;
+    __syncthreads();
+    const int wv_id = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    Flow f = f_in;
+    f.lds_done = done;
+    double* w = wl + (int64_t)wv_id * slice;
+    for (int it = 0; it <= f.n; ++it) {
+        const int t = lds_ticket(&ticket);
+        if (t >= f.n) break;
+        f.pos = t;
+        const int s = f.order[t];
+        backward_front<kModeTop>(a, s, w, lane, &f, nullptr);
+        publish_lds(f);
+        fstamp(f.stamps, s, 4);
+    }
 }
 
 // Structure arrays carry kMfPad zeroed elements after their end: the kernels read clamped indices
@@ -1196,6 +1306,11 @@ struct Prog {
     int32_t* order_bwd = nullptr;
     int32_t* fold_list = nullptr;   // folded landmarks whose parent is in this program
     int n_fold = 0;
+    // the top launches (mf_factor_top / mf_backward_top): levels >= top_lev0 (factorization) and >=
+    // top_b0 (backward), at most kTopWaves fronts each; flow id id + 2; dependencies by position
+    int top_lev0 = 0, top_b0 = 0, n_top_f = 0, n_top_b = 0, top_slice = 0;
+    int32_t *order_top_f = nullptr, *dep_ptr_f = nullptr, *dep_pos_f = nullptr;
+    int32_t *order_top_b = nullptr, *dep_ptr_b = nullptr, *dep_pos_b = nullptr;
     int count(int lev, int c0, int c1) const { return ptr[lev * kClasses + c1] - ptr[lev * kClasses + c0]; }
     int count(int lev, int c) const { return count(lev, c, c + 1); }
     int lds_max(const std::vector<int>& v, int lev, int c0, int c1) const {
@@ -1215,6 +1330,11 @@ struct Prog {
 // factorization of levels with >= kFactorWideLevel fronts before its flow starts (config 3: levels
 // 0-2, 564 -> 556 us; also level 3: 567).
 constexpr int kFlowWavesFactor = 6;
+#ifndef BOS_MF_TOP   // measurement builds: 1 = the one-workgroup top launches (mf_factor_top /
+#define BOS_MF_TOP 0   // mf_backward_top); measured slower than the flows taking the top
+#endif
+constexpr bool kTopLaunch = BOS_MF_TOP != 0;
+constexpr int kTopMinLevels = 2;
 constexpr int kFlowWavesBackward = 4;
 constexpr int kSolveWideLevel = 256;
 constexpr int kFactorWideLevel = 2048;
@@ -1319,13 +1439,37 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
         while (wide < L && mine_in_level(wide) >= kFactorWideLevel) ++wide;
         P.flow_lev0 = std::max(P.flow_lev0, wide);
     }
-    std::vector<int32_t> ofac, ofwd;
-    for (int q = F.level_ptr[std::min(P.flow_lev0, L)]; q < F.level_ptr[L]; ++q)
-        if (mine(F.level[q])) { ofac.push_back(F.level[q]); fid_f[F.level[q]] = (int8_t)id; }
+    // the top: the highest levels of the flow range with at most kTopWaves fronts each (at least
+    // kTopMinLevels of them, at most kTopMax fronts)
+    P.top_lev0 = L;
+    if (kTopLaunch && P.flow_lev0 < L) {
+        int t0 = L, nt = 0;
+        while (t0 > P.flow_lev0 && mine_in_level(t0 - 1) <= kTopWaves && nt + mine_in_level(t0 - 1) <= kTopMax)
+            nt += mine_in_level(--t0);
+        if (L - t0 >= kTopMinLevels) P.top_lev0 = t0;
+    }
+    const int8_t top_id = (int8_t)(id + 2);
+    std::vector<int32_t> ofac, ofwd, otop;
+    for (int q = F.level_ptr[std::min(P.flow_lev0, L)]; q < F.level_ptr[L]; ++q) {
+        const int s = F.level[q];
+        if (!mine(s)) continue;
+        if (q < F.level_ptr[P.top_lev0]) { ofac.push_back(s); fid_f[s] = (int8_t)id; }
+        else { otop.push_back(s); fid_f[s] = top_id; }
+    }
     P.n_flow_factor = (int)ofac.size();
+    P.n_top_f = (int)otop.size();
+    std::vector<int32_t> pos_of(F.nsuper, -1), dptr_f(1, 0), dpos_f;
+    for (int t = 0; t < P.n_top_f; ++t) pos_of[otop[t]] = t;
+    for (int t = 0; t < P.n_top_f; ++t) {   // children of this launch (lower positions: level order)
+        const int s = otop[t];
+        for (int ci = F.child_ptr[s]; ci < F.child_ptr[s + 1]; ++ci)
+            if (fid_f[F.child[ci]] == top_id) dpos_f.push_back(pos_of[F.child[ci]]);
+        dptr_f.push_back((int32_t)dpos_f.size());
+    }
     P.solve_lev0 = std::min(2, L);
     while (P.solve_lev0 < L && mine_in_level(P.solve_lev0) >= kSolveWideLevel) ++P.solve_lev0;
-    for (int q = F.level_ptr[P.solve_lev0]; q < F.level_ptr[L]; ++q) {
+    P.top_b0 = P.top_lev0 < L ? std::max(P.top_lev0, P.solve_lev0) : L;
+    for (int q = F.level_ptr[P.solve_lev0]; q < F.level_ptr[P.top_b0]; ++q) {
         const int s = F.level[q], k = F.k[s], m = k + F.r[s];
         if (!mine(s)) continue;
         ofwd.push_back(s);
@@ -1334,22 +1478,38 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
     std::vector<int32_t> obwd(ofwd.rbegin(), ofwd.rend());
     P.n_flow_solve = (int)ofwd.size();
     P.flow_solve = P.n_flow_solve > 0 && P.lds_bwd_flow <= 48 * 1024;
-    if (!P.flow_solve) P.solve_lev0 = L;
+    if (!P.flow_solve) P.solve_lev0 = P.top_b0;
     else
         for (int s : obwd) fid_b[s] = (int8_t)id;
+    // backward top: top-down, each front after its parent (lower positions)
+    std::vector<int32_t> otopb, dptr_b(1, 0), dpos_b;
+    for (int q = F.level_ptr[L] - 1; q >= F.level_ptr[P.top_b0]; --q)
+        if (mine(F.level[q])) otopb.push_back(F.level[q]);
+    P.n_top_b = (int)otopb.size();
+    std::fill(pos_of.begin(), pos_of.end(), -1);
+    for (int t = 0; t < P.n_top_b; ++t) { pos_of[otopb[t]] = t; fid_b[otopb[t]] = top_id; }
+    for (int t = 0; t < P.n_top_b; ++t) {
+        const int s = otopb[t], k = F.k[s], m = k + F.r[s];
+        if (F.parent[s] >= 0 && pos_of[F.parent[s]] >= 0) dpos_b.push_back(pos_of[F.parent[s]]);
+        dptr_b.push_back((int32_t)dpos_b.size());
+        P.top_slice = std::max(P.top_slice, 2 * k + (m - k) + m * k);   // doubles per wave
+    }
     std::vector<int32_t> folds;
     for (int s : F.fold_list)
         if (mine(F.parent[s])) folds.push_back(s);
     P.n_fold = (int)folds.size();
     int rc;
     if ((rc = up(&P.list, lst, err)) || (rc = up(&P.order_factor, ofac, err)) || (rc = up(&P.order_bwd, obwd, err)) ||
-        (rc = up(&P.fold_list, folds, err)))
+        (rc = up(&P.fold_list, folds, err)) || (rc = up(&P.order_top_f, otop, err)) || (rc = up(&P.dep_ptr_f, dptr_f, err)) ||
+        (rc = up(&P.dep_pos_f, dpos_f, err)) || (rc = up(&P.order_top_b, otopb, err)) ||
+        (rc = up(&P.dep_ptr_b, dptr_b, err)) || (rc = up(&P.dep_pos_b, dpos_b, err)))
         return rc;
     return 0;
 }
 
 void free_prog(Prog& P) {
-    void* bufs[] = {P.list, P.order_factor, P.order_bwd, P.fold_list};
+    void* bufs[] = {P.list, P.order_factor, P.order_bwd, P.fold_list, P.order_top_f, P.dep_ptr_f, P.dep_pos_f,
+                    P.order_top_b, P.dep_ptr_b, P.dep_pos_b};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
 }
@@ -1517,6 +1677,13 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
         hipLaunchKernelGGL((mf_factor_flow<F32>), dim3(grid), dim3(64), 0, s, d->args(P, 0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    if (P.n_top_f > 0) {
+        Flow f{P.order_top_f, P.n_top_f, nullptr, nullptr, nullptr, nullptr, 0u, d->fid_f, P.id + 2, d->stamps};
+        f.dep_ptr = P.dep_ptr_f;
+        f.dep_pos = P.dep_pos_f;
+        hipLaunchKernelGGL((mf_factor_top<F32>), dim3(1), dim3(64 * kTopWaves), 0, s, d->args(P, 0, 0, A, x), f);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 
@@ -1535,6 +1702,15 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
     hipError_t e;
     const Prog& P = d->prog[which];
     if (P.ptr.empty()) return hipSuccess;
+    if (P.n_top_b > 0) {   // the top first (top-down)
+        Flow f{P.order_top_b, P.n_top_b, nullptr, nullptr, nullptr, nullptr, 0u, d->fid_b, P.id + 2,
+               d->stamps ? d->stamps + 8 * (int64_t)d->nsuper : nullptr};
+        f.dep_ptr = P.dep_ptr_b;
+        f.dep_pos = P.dep_pos_b;
+        hipLaunchKernelGGL(mf_backward_top, dim3(1), dim3(64 * kTopWaves), kTopWaves * P.top_slice * sizeof(double), s,
+                           d->args(P, 0, 0, nullptr, x), f, P.top_slice);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (P.flow_solve) {
         const Flow fb{P.order_bwd, P.n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1, d->done + d->nsuper,
                       d->epoch, 0u, d->fid_b, P.id, d->stamps ? d->stamps + 8 * (int64_t)d->nsuper : nullptr};

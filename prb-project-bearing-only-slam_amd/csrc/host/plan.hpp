@@ -127,6 +127,7 @@ struct OrderingReport {
 //  - L panels are m x k column-major (entries above the diagonal unused).
 constexpr int kMfWaveMaxM = 64;
 constexpr int kMfFlowMaxM = 48;   // fronts of the dataflow factor launch (hip/multifrontal.hip kFlowMaxM)
+constexpr int kMfTopWaves = 8;    // waves of the one-workgroup top launches (hip/multifrontal.hip kTopWaves)
 constexpr int kFoldChunk = 64;   // folded rows per chunk (one per lane)
 constexpr int kFoldRec = 8;      // ints per folded row
 // landmarks per fold chunk for a parent front of size m: the device forms the chunk's
