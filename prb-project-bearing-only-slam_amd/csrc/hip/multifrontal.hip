@@ -1309,6 +1309,11 @@ struct Prog {
     // the top launches (mf_factor_top / mf_backward_top): levels >= top_lev0 (factorization) and >=
     // top_b0 (backward), at most kTopWaves fronts each; flow id id + 2; dependencies by position
     int top_lev0 = 0, top_b0 = 0, n_top_f = 0, n_top_b = 0, top_slice = 0;
+    // per-level backward launches of the wave fronts (classes 0-3) split by their LDS need
+    // (kBwdSplit): level l's buckets are blist[bptr[l][b] .. bptr[l][b + 1]) with blds[l][b] bytes each
+    std::vector<std::vector<int32_t>> bptr;
+    std::vector<std::vector<int>> blds;
+    int32_t* blist = nullptr;
     int32_t *order_top_f = nullptr, *dep_ptr_f = nullptr, *dep_pos_f = nullptr;
     int32_t *order_top_b = nullptr, *dep_ptr_b = nullptr, *dep_pos_b = nullptr;
     int count(int lev, int c0, int c1) const { return ptr[lev * kClasses + c1] - ptr[lev * kClasses + c0]; }
@@ -1334,6 +1339,13 @@ constexpr int kFlowWavesFactor = 6;
 #define BOS_MF_TOP 0   // mf_backward_top); measured slower than the flows taking the top
 #endif
 constexpr bool kTopLaunch = BOS_MF_TOP != 0;
+// The per-level backward launch of a level's wave fronts gives every wave the LDS of the level's
+// largest panel (m k doubles): class-64 fronts (up to ~16 KB) then hold a level-0 launch to 8-10
+// waves per CU. Fronts needing more than kBwdSplit bytes go to a launch of their own, before the rest.
+#ifndef BOS_MF_BWD_SPLIT   // bytes; 0 = one launch per level (measurement builds)
+#define BOS_MF_BWD_SPLIT 0
+#endif
+constexpr int kBwdSplit = BOS_MF_BWD_SPLIT;
 constexpr int kTopMinLevels = 2;
 constexpr int kFlowWavesBackward = 4;
 constexpr int kSolveWideLevel = 256;
@@ -1424,6 +1436,25 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
         for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) c += mine(F.level[q]);
         return c;
     };
+    std::vector<int32_t> blst;
+    P.bptr.assign(L, {});
+    P.blds.assign(L, {});
+    for (int l = 0; l < L; ++l) {
+        // the level's wave fronts (classes 0-3, in list order: longest first), big panels first
+        const int q0 = P.ptr[l * kClasses], q1 = P.ptr[l * kClasses + 4];
+        auto need = [&](int s2) { const int k = F.k[s2], m = k + F.r[s2]; return (2 * k + (m - k) + m * k) * 8; };
+        std::vector<int32_t> big, small;
+        for (int q = q0; q < q1; ++q) (kBwdSplit > 0 && need(lst[q]) > kBwdSplit ? big : small).push_back(lst[q]);
+        for (auto* part : {&big, &small}) {
+            if (part->empty()) continue;
+            int mx = 0;
+            for (int s2 : *part) mx = std::max(mx, need(s2));
+            P.bptr[l].push_back((int32_t)blst.size());
+            P.blds[l].push_back(mx);
+            blst.insert(blst.end(), part->begin(), part->end());
+        }
+        P.bptr[l].push_back((int32_t)blst.size());
+    }
     // dataflow ranges: the factor flow starts at the lowest level (>= 2) from which every front of
     // the program is <= kFlowMaxM, and above the wide levels
     P.flow_lev0 = L;
@@ -1502,14 +1533,14 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
     if ((rc = up(&P.list, lst, err)) || (rc = up(&P.order_factor, ofac, err)) || (rc = up(&P.order_bwd, obwd, err)) ||
         (rc = up(&P.fold_list, folds, err)) || (rc = up(&P.order_top_f, otop, err)) || (rc = up(&P.dep_ptr_f, dptr_f, err)) ||
         (rc = up(&P.dep_pos_f, dpos_f, err)) || (rc = up(&P.order_top_b, otopb, err)) ||
-        (rc = up(&P.dep_ptr_b, dptr_b, err)) || (rc = up(&P.dep_pos_b, dpos_b, err)))
+        (rc = up(&P.dep_ptr_b, dptr_b, err)) || (rc = up(&P.dep_pos_b, dpos_b, err)) || (rc = up(&P.blist, blst, err)))
         return rc;
     return 0;
 }
 
 void free_prog(Prog& P) {
     void* bufs[] = {P.list, P.order_factor, P.order_bwd, P.fold_list, P.order_top_f, P.dep_ptr_f, P.dep_pos_f,
-                    P.order_top_b, P.dep_ptr_b, P.dep_pos_b};
+                    P.order_top_b, P.dep_ptr_b, P.dep_pos_b, P.blist};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
 }
@@ -1721,8 +1752,12 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
     }
     for (int l = std::min(P.solve_lev0, d->nlevels) - 1; l >= 0; --l) {
         int n;
-        if ((n = P.count(l, 0, 4)))
-            hipLaunchKernelGGL(mf_backward_wave, dim3(n), dim3(64), P.lds_max(P.lds_bwd, l, 0, 4), s, d->args(P, l, 0, nullptr, x));
+        for (size_t b = 0; b + 1 < P.bptr[l].size(); ++b) {
+            MfArgs g = d->args(P, l, 0, nullptr, x);
+            g.level = P.blist + P.bptr[l][b];
+            g.count = P.bptr[l][b + 1] - P.bptr[l][b];
+            hipLaunchKernelGGL(mf_backward_wave, dim3(g.count), dim3(64), P.blds[l][b], s, g);
+        }
         if ((n = P.count(l, 4)))
             hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), P.lds_bwd[l * kClasses + 4], s, d->args(P, l, 4, nullptr, x));
         if ((e = hipGetLastError()) != hipSuccess) return e;
