@@ -33,6 +33,9 @@ for rep in range(3):
     S.step_n(50)
     bt = 50 / (time.perf_counter() - t0)
     ph = {k: round(float(np.median([g[k] for g in st])) * 1e3, 2) for k in ("t_linearize_ms", "t_solve_ms", "t_update_ms")}
+    bad = [i for i, g in enumerate(st) if g["solver_info"] != 0]
+    ph["first_nonpd_iter"] = bad[0] + 1 if bad else None
+    ph["chi2_50"] = float(st[-1]["chi2"])
     out.append(f"c-loop {c:7.1f}  python {py:7.1f}  batched {bt:7.1f} it/s  phases(us) {ph}")
 import hashlib  # noqa: E402
 pose, lm = S.get_state()   # after the last 50-iteration batch from the initial guess
