@@ -22,7 +22,10 @@
 
 // J+H build variants (measurement builds only; the defaults are the product): BOS_JH_ILP launches
 // the ILP lanes for the common case (no faster, and the GN step slower), with
-// BOS_JH_NIP pose items per chunk (fp32) and BOS_JH_MINW waves per SIMD
+// BOS_JH_NIP pose items per chunk (fp32) and BOS_JH_MINW waves per SIMD; BOS_JH_LOOP_WAIT /
+// BOS_JH_LM_WAIT (a vmcnt(0) before the pose / landmark pair loop), BOS_JH_STORE_LATE (the
+// pose-landmark block stored after the refill loads), BOS_JH_PRIO (pose waves' issue priority),
+// BOS_JH_WG / BOS_JH_ORDER (kernels.hpp, jh_unit): measured, no gain
 #ifndef BOS_JH_NIP
 #define BOS_JH_NIP 12
 #endif
@@ -79,7 +82,7 @@ __device__ __forceinline__ void stamp(const unsigned long long* base, unsigned l
 }
 __device__ __forceinline__ void stamp_flush(unsigned long long* diag, const unsigned long long* st, int kind) {
     if (!diag || (threadIdx.x & 63)) return;
-    unsigned long long* d = diag + 8 * ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    unsigned long long* d = diag + 8 * ((int64_t)blockIdx.x * (kJhWg / 64) + (threadIdx.x >> 6));
     d[0] = blockIdx.x; d[1] = threadIdx.x >> 6; d[2] = kind;
     d[3] = st[0]; d[4] = st[1]; d[5] = st[2]; d[6] = __builtin_amdgcn_s_memrealtime();
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);           // HW_REG_HW_ID
@@ -241,9 +244,8 @@ __device__ __forceinline__ void put_pl(T* plbase, int64_t slot, const T o[6], T 
 }
 
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP>
-__device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, double& chi, int& nrob,
+__device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double& chi, int& nrob,
                                            unsigned long long* st) {
-    const int g = blk * kBlock + threadIdx.x;   // lane
     const int grp = g / LPP, sub = g % LPP, t = g & 63;
     // group i runs pose i unless a table says otherwise (sharded ranks): one dependent load fewer
     // at the head of both of the lane's load chains
@@ -303,15 +305,26 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
         const bool factored = P.pl_factored != 0;
         T* const plbase = P.hval + P.off_pl;
         stamp(P.diag_stamps, st, 1);
+#ifdef BOS_JH_LOOP_WAIT
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) once, before the loop (experiment)
+#endif
         for (int j = 0; j < n; j += 2) {
             // item j (set A), then refill A: item j + 2's gather and z, item j + 4's index
             pose_bearing<T>(P, X, LA, zA, wA, h, gb, o, chi, nrob, jf);
+#ifndef BOS_JH_STORE_LATE
             put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * j, o, acc, lastA, factored, jf);
             lastA = !(iA & kRunCont);
+#else
+            const bool lastA0 = lastA;
+            lastA = !(iA & kRunCont);
+#endif
             LA = load2(P.lc + 2 * (iA & kIdxMask));
             zA = zp[at(j + 2)];
             if (HAS_W) wA = P.pb_w[at(j + 2)];
             iA = ip[at(j + 4)];
+#ifdef BOS_JH_STORE_LATE   // (experiment) the store after the refill loads: vmcnt retires in order
+            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * j, o, acc, lastA0, factored, jf);
+#endif
             // item j + 1 (set B). Its block is stored even past the lane's last item (a padding slot
             // of the lane's wave: pose-lane waves have an even number of slots per lane), so both
             // paths issue the same memory operations and the loop's waits stay exact.
@@ -322,12 +335,20 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int blk, doubl
                 for (int q = 0; q < 6; ++q) o[q] = (T)0;
                 jf[0] = jf[1] = jf[2] = (T)0;
             }
+#ifndef BOS_JH_STORE_LATE
             put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * (j + 1), o, acc, lastB, factored, jf);
             lastB = !(iB & kRunCont);
+#else
+            const bool lastB0 = lastB;
+            lastB = !(iB & kRunCont);
+#endif
             LB = load2(P.lc + 2 * (iB & kIdxMask));
             zB = zp[at(j + 3)];
             if (HAS_W) wB = P.pb_w[at(j + 3)];
             iB = ip[at(j + 5)];
+#ifdef BOS_JH_STORE_LATE
+            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * (j + 1), o, acc, lastB0, factored, jf);
+#endif
         }
         stamp(P.diag_stamps, st, 2);
         if (!kOdoFirst) odometry();
@@ -362,8 +383,7 @@ __device__ __forceinline__ void landmark_bearing(const LinParams<T>& P, const V4
 }
 
 template <typename T, bool HAS_W>
-__device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int blk, unsigned long long* st) {
-    const int g = blk * kBlock + threadIdx.x;   // lane
+__device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int g, unsigned long long* st) {
     if (g >= P.n_lm_lanes) return;
     const int l = P.ll_lm[g];
     const int n = P.ll_cnt[g];
@@ -383,6 +403,9 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int blk, un
     iA = ip[at(2)];
     iB = ip[at(3)];
     stamp(P.diag_stamps, st, 1);
+#ifdef BOS_JH_LM_WAIT
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) once, before the loop (experiment)
+#endif
     for (int j = 0; j < n; j += 2) {
         landmark_bearing<T>(P, XA, Lm, zA, wA, hl, gl);
         XA = load4(P.pc + 4 * iA);
@@ -419,9 +442,8 @@ struct PoseChunk {
 };
 
 template <typename T, int LPP, int NI>
-__device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int blk, double& chi, int& nrob,
+__device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int g, double& chi, int& nrob,
                                                unsigned long long* st) {
-    const int g = blk * kBlock + threadIdx.x;   // lane
     const int grp = g / LPP, sub = g % LPP, t = g & 63;
     const int p = grp < P.n_groups ? (P.lane_pose ? P.lane_pose[grp] : grp) : -1;
     const bool active = p >= 0;
@@ -526,8 +548,7 @@ __device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int blk, d
 }
 
 template <typename T, int NI>
-__device__ __forceinline__ void landmark_lane_ilp(const LinParams<T>& P, int blk, unsigned long long* st) {
-    const int g = blk * kBlock + threadIdx.x;   // lane
+__device__ __forceinline__ void landmark_lane_ilp(const LinParams<T>& P, int g, unsigned long long* st) {
     if (g >= P.n_lm_lanes) return;
     // hop 1: the lane's header
     const int l = P.ll_lm[g];
@@ -594,76 +615,85 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t s0, int64_t
     return s0 + g * q + (g < rmd ? g : rmd) + (i >> 3);
 }
 
+// Launch order of the J+H units (kJhWg lanes each; kJhSub per block of lanes): pose units first,
+// then landmark units, each range XCD-contiguous (above). Pose waves are the longer chains (~12.7 us
+// against ~8.5 us per wave cold at config 3), so they get the head start; one-wave units spread
+// them evenly over the CUs (tools/jh_timeline.py, per-CU section: with 256-lane workgroups, 135 of
+// 256 CUs held two pose blocks and ended 2.7 us after the others). BOS_JH_ORDER=1 (measurement
+// builds) interleaves the two kinds in proportion instead: every CU the same mix, but the pose
+// waves lose their head start (measured slower). Returns true for a pose unit; u = the unit's
+// index in its range.
+#ifndef BOS_JH_ORDER
+#define BOS_JH_ORDER 0
+#endif
+__device__ __forceinline__ bool jh_unit(int64_t i, int64_t n_units, int64_t n_pose_units, int64_t& u) {
+#if BOS_JH_ORDER == 1
+    const int64_t j = xcd_contiguous(i, 0, n_units);
+    const int64_t cp = j * n_pose_units / n_units, cp1 = (j + 1) * n_pose_units / n_units;
+    u = cp1 > cp ? cp : j - cp;
+    return cp1 > cp;
+#else
+    if (i < n_pose_units) {
+        u = xcd_contiguous(i, 0, n_pose_units);
+        return true;
+    }
+    u = xcd_contiguous(i, n_pose_units, n_units) - n_pose_units;
+    return false;
+#endif
+}
+
+// per-wave chi^2 / robust count of a pose wave (fixed order: the stats kernel sums the waves)
+__device__ __forceinline__ void pose_wave_partials(double* chi2_part, int32_t* nrob_part, int g, double chi, int nrob) {
+    chi = wave_sum(chi);
+    nrob = (int)wave_sum((double)nrob);
+    if ((threadIdx.x & 63) == 0) {
+        chi2_part[g >> 6] = chi;
+        nrob_part[g >> 6] = nrob;
+    }
+}
+
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP, int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void linearize_kernel(const LinParams<T> P) {
-    const int64_t nb = gridDim.x;
-    // pose blocks first, then landmark blocks, each range in XCD-contiguous order; b numbers the
-    // blocks of the whole build (pose blocks, then landmark blocks from pose_blocks on)
-    const int64_t b = blockIdx.x < P.n_pose_run
-                          ? P.pose_b0 + xcd_contiguous(blockIdx.x, 0, P.n_pose_run)
-                          : P.pose_blocks + P.lm_b0 + xcd_contiguous(blockIdx.x, P.n_pose_run, nb) - P.n_pose_run;
+__global__ __launch_bounds__(kJhWg, MINW) void linearize_kernel(const LinParams<T> P) {
+    int64_t u;
+    const bool pose = jh_unit(blockIdx.x, gridDim.x, (int64_t)P.n_pose_run * kJhSub, u);
     unsigned long long st[3] = {0, 0, 0};
     if (P.t_start && blockIdx.x == 0 && threadIdx.x == 0) *P.t_start = __builtin_amdgcn_s_memrealtime();
     stamp(P.diag_stamps, st, 0);
-    if (b >= P.pose_blocks) {   // block-uniform branch
-        landmark_lane<T, HAS_W>(P, (int)(b - P.pose_blocks), st);
+    if (!pose) {   // workgroup-uniform branch
+        landmark_lane<T, HAS_W>(P, (int)(((int64_t)P.lm_b0 * kJhSub + u) * kJhWg + threadIdx.x), st);
         stamp_flush(P.diag_stamps, st, 1);
         return;
     }
-    const int pb0 = (int)b;
+    const int g = (int)(((int64_t)P.pose_b0 * kJhSub + u) * kJhWg + threadIdx.x);
     double chi = 0.0;
     int nrob = 0;
-    pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, pb0, chi, nrob, st);
+#ifdef BOS_JH_PRIO   // (experiment) pose waves, the longer chains, issue first
+    __builtin_amdgcn_s_setprio(BOS_JH_PRIO);
+#endif
+    pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, g, chi, nrob, st);
     stamp_flush(P.diag_stamps, st, 0);
-    // per-block chi^2 / robust count in a fixed order
-    __shared__ double sc[kBlock / 64];
-    __shared__ int sr[kBlock / 64];
-    chi = wave_sum(chi);
-    nrob = (int)wave_sum((double)nrob);
-    if ((threadIdx.x & 63) == 0) { sc[threadIdx.x >> 6] = chi; sr[threadIdx.x >> 6] = nrob; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double c = 0.0;
-        int r = 0;
-        for (int w = 0; w < kBlock / 64; ++w) { c += sc[w]; r += sr[w]; }
-        P.chi2_part[pb0] = c;
-        P.nrob_part[pb0] = r;
-    }
+    pose_wave_partials(P.chi2_part, P.nrob_part, g, chi, nrob);
 }
 
 // The J+H launch of the common case (unit weights, no duplicate pairs): the ILP lanes above.
 template <typename T, int LPP, int NIP, int NIL, int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void linearize_ilp_kernel(const LinParams<T> P) {
-    const int64_t nb = gridDim.x;
-    const int64_t b = blockIdx.x < P.n_pose_run
-                          ? P.pose_b0 + xcd_contiguous(blockIdx.x, 0, P.n_pose_run)
-                          : P.pose_blocks + P.lm_b0 + xcd_contiguous(blockIdx.x, P.n_pose_run, nb) - P.n_pose_run;
+__global__ __launch_bounds__(kJhWg, MINW) void linearize_ilp_kernel(const LinParams<T> P) {
+    int64_t u;
+    const bool pose = jh_unit(blockIdx.x, gridDim.x, (int64_t)P.n_pose_run * kJhSub, u);
     unsigned long long st[3] = {0, 0, 0};
     if (P.t_start && blockIdx.x == 0 && threadIdx.x == 0) *P.t_start = __builtin_amdgcn_s_memrealtime();
     stamp(P.diag_stamps, st, 0);
-    if (b >= P.pose_blocks) {   // block-uniform branch
-        landmark_lane_ilp<T, NIL>(P, (int)(b - P.pose_blocks), st);
+    if (!pose) {
+        landmark_lane_ilp<T, NIL>(P, (int)(((int64_t)P.lm_b0 * kJhSub + u) * kJhWg + threadIdx.x), st);
         stamp_flush(P.diag_stamps, st, 1);
         return;
     }
-    const int pb0 = (int)b;
+    const int g = (int)(((int64_t)P.pose_b0 * kJhSub + u) * kJhWg + threadIdx.x);
     double chi = 0.0;
     int nrob = 0;
-    pose_lanes_ilp<T, LPP, NIP>(P, pb0, chi, nrob, st);
+    pose_lanes_ilp<T, LPP, NIP>(P, g, chi, nrob, st);
     stamp_flush(P.diag_stamps, st, 0);
-    __shared__ double sc[kBlock / 64];
-    __shared__ int sr[kBlock / 64];
-    chi = wave_sum(chi);
-    nrob = (int)wave_sum((double)nrob);
-    if ((threadIdx.x & 63) == 0) { sc[threadIdx.x >> 6] = chi; sr[threadIdx.x >> 6] = nrob; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double c = 0.0;
-        int r = 0;
-        for (int w = 0; w < kBlock / 64; ++w) { c += sc[w]; r += sr[w]; }
-        P.chi2_part[pb0] = c;
-        P.nrob_part[pb0] = r;
-    }
+    pose_wave_partials(P.chi2_part, P.nrob_part, g, chi, nrob);
 }
 
 // max that propagates NaN (fmax returns the non-NaN operand): a non-finite update must not read
@@ -724,6 +754,28 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
     }
 }
 
+// This thread's share of the J+H chi^2 / robust-count partials (one per pose wave), in a fixed
+// order: four loads in flight per thread and step
+template <typename R>
+__device__ __forceinline__ void sum_partials(const double* chi_part, const int32_t* nrob_part, int n, double& c, R& r) {
+    for (int i0 = threadIdx.x; i0 < n; i0 += 4 * blockDim.x) {
+        double v[4];
+        int w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = min(i0 + k * (int)blockDim.x, n - 1);
+            v[k] = chi_part[i];
+            w[k] = nrob_part[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool in = i0 + k * (int)blockDim.x < n;
+            c += in ? v[k] : 0.0;
+            r += in ? w[k] : 0;
+        }
+    }
+}
+
 __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_part, int n, double chi_const,
                                     int32_t nrob_const, const double* max_part, int n_max, int32_t* info,
                                     StepStatus* out, StepStatus* mirror) {
@@ -734,7 +786,7 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
     long long r = 0;
     const int32_t inf = info && threadIdx.x == 0 ? *info : 0;   // loaded with the partials
     if (nrob_part) {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) { c += chi_part[i]; r += nrob_part[i]; }
+        sum_partials(chi_part, nrob_part, n, c, r);
     } else if (threadIdx.x == 0) {   // an all-reduced header
         c = chi_part[0];
         r = (long long)chi_part[1];
@@ -874,7 +926,7 @@ __global__ __launch_bounds__(256) void shard_header1_kernel(const double* chi_pa
     __shared__ long long sr[256];
     double c = 0.0;
     long long r = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) { c += chi_part[i]; r += nrob_part[i]; }
+    sum_partials(chi_part, nrob_part, n, c, r);
     sc[threadIdx.x] = c;
     sr[threadIdx.x] = r;
     __syncthreads();
@@ -1066,9 +1118,9 @@ hipError_t launch_lin_k(LinParams<T> p, hipStream_t s) {
     if (p.pose_b0 < 0 || p.n_pose_run < 0 || p.pose_b0 + p.n_pose_run > p.pose_blocks || p.lm_b0 < 0 || p.n_lm_run < 0 ||
         p.lm_b0 + p.n_lm_run > lm_blocks)
         return hipErrorInvalidValue;   // a block range outside the build (checked before any launch)
-    const int grid = p.n_pose_run + p.n_lm_run;
+    const int grid = (p.n_pose_run + p.n_lm_run) * kJhSub;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((linearize_kernel<T, W, D, LPP, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL((linearize_kernel<T, W, D, LPP, MINW>), dim3(grid), dim3(kJhWg), 0, s, p);
     return hipGetLastError();
 }
 
@@ -1078,11 +1130,11 @@ hipError_t launch_lin_ilp(LinParams<T> p, hipStream_t s) {
     if (p.pose_b0 < 0 || p.n_pose_run < 0 || p.pose_b0 + p.n_pose_run > p.pose_blocks || p.lm_b0 < 0 || p.n_lm_run < 0 ||
         p.lm_b0 + p.n_lm_run > lm_blocks)
         return hipErrorInvalidValue;
-    const int grid = p.n_pose_run + p.n_lm_run;
+    const int grid = (p.n_pose_run + p.n_lm_run) * kJhSub;
     if (grid == 0) return hipSuccess;
     // items read per chunk: 12 pose / 8 landmark items (fp32), 8 / 8 (fp64: twice the registers)
     constexpr int NIP = sizeof(T) == 4 ? BOS_JH_NIP : 8, NIL = 8;
-    hipLaunchKernelGGL((linearize_ilp_kernel<T, LPP, NIP, NIL, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL((linearize_ilp_kernel<T, LPP, NIP, NIL, MINW>), dim3(grid), dim3(kJhWg), 0, s, p);
     return hipGetLastError();
 }
 

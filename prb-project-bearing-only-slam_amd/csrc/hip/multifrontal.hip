@@ -972,8 +972,12 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     wave_sync();
 }
 
+// BOS_MF_C48_WAVES (measurement builds): waves per SIMD the class-48 launch is compiled for
+#ifndef BOS_MF_C48_WAVES
+#define BOS_MF_C48_WAVES 1
+#endif
 template <int MAXM, bool F32>
-__global__ __launch_bounds__(64) void mf_factor_reg(const MfArgs a) {
+__global__ __launch_bounds__(64, (MAXM == 48 ? BOS_MF_C48_WAVES : 1)) void mf_factor_reg(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * MAXM];
     __shared__ __attribute__((aligned(16))) double wv[MAXM];

@@ -53,3 +53,17 @@ for f in (0.1, 0.25, 0.5, 0.75, 0.9):
 xcc = (T[:, 7] >> 32) & 0xF
 print("waves per xcc", np.bincount(xcc.astype(int), minlength=8).tolist())
 print("last end per xcc (us)", [round(us(T[xcc == x, 6].max() - t0), 2) for x in range(8) if (xcc == x).any()])
+# per-CU load: HW_ID (gfx9 layout) cu_id [11:8], sh_id [12], se_id [15:13]; the CU key adds the xcc
+hw = T[:, 7] & 0xFFFFFFFF
+cu_key = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
+keys, inv = np.unique(cu_key, return_inverse=True)
+npose = np.bincount(inv, weights=(T[:, 2] == 0), minlength=len(keys))
+nlm = np.bincount(inv, weights=(T[:, 2] == 1), minlength=len(keys))
+last = np.zeros(len(keys))
+np.maximum.at(last, inv, us(T[:, 6] - t0))
+print(f"CUs seen {len(keys)}; waves per CU: pose {np.percentile(npose, [0, 50, 100]).tolist()}, "
+      f"landmark {np.percentile(nlm, [0, 50, 100]).tolist()}")
+for p in sorted(set(npose.astype(int).tolist())):
+    sel = npose == p
+    print(f"  CUs with {p:2d} pose waves: {int(sel.sum()):3d}  landmark waves median {np.median(nlm[sel]):5.1f}  "
+          f"last end median {np.median(last[sel]):6.2f} max {last[sel].max():6.2f} us")

@@ -4,6 +4,7 @@ on the device, exchanges by host copies): what each rank's GPU would spend per i
 N-GPU node, minus the two RCCL all-gathers. Config 3, fp32 J+H, Schur solver.
 
     python tools/shard_timeline.py [worlds...]      (default 1 2 4 8)
+    BOS_LPP=2|4: J+H lanes per pose (bos_options.lanes_per_pose; default: the plan's choice)
 """
 import json
 import os
@@ -17,15 +18,17 @@ import numpy as np  # noqa: E402
 import bos  # noqa: E402
 
 worlds = [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]
+LPP = int(os.environ.get("BOS_LPP", "0"))
 P = bos.synthetic(100000, 200000, 10, seed=0xB05EED01 + 3)
 out = {}
 for W in worlds:
     t0 = time.perf_counter()
     if W == 1:
         S = [bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, rank=0, world_size=1,
-                        nccl_id=bos.nccl_unique_id())]
+                        nccl_id=bos.nccl_unique_id(), lanes_per_pose=LPP)]
     else:
-        S = [bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=W) for r in range(W)]
+        S = [bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=W,
+                        lanes_per_pose=LPP) for r in range(W)]
     t_create = time.perf_counter() - t0
     rows = []
     for it in range(6):
