@@ -245,6 +245,12 @@ def main():
     ap.add_argument("--solver", choices=["supernodal", "schur"], default="schur",
                     help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
                          "nested-dissection multifrontal; the other one is timed too (gn_other)")
+    ap.add_argument("--lanes-per-pose", type=int, default=0, choices=[0, 1, 2, 4],
+                    help="J+H lanes per pose (bos_options.lanes_per_pose); 0 = by the ranks: 1 on one GPU, 2 for "
+                         "N > 1 (a rank's share of the lanes leaves the GPU room for shorter lanes: per-rank J+H at "
+                         "N = 4 / 8 11 us with 2 lanes against 13 us with 1; 4 lanes, 9 us at N = 8, make this fp32 "
+                         "trajectory hit a non-positive pivot at iteration 44, inside the timed window; "
+                         "profiles/r03_shard_lanes_per_pose.txt)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -310,6 +316,8 @@ def main():
     device = 0 if args.same_device else local_rank
     solver = bos.BOS_SOLVER_SCHUR if args.solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
 
+    lpp = args.lanes_per_pose or (1 if world == 1 else 2)
+
     def make_handle(partition):
         nccl_id = None
         if world > 1 and args.exchange == "rccl":
@@ -318,7 +326,7 @@ def main():
             nccl_id = obj[0]
         t0 = time.perf_counter()
         h = bos.Solver(P, precision=precision, solver=solver, device=device, rank=rank, world_size=world,
-                       nccl_id=nccl_id, partition=partition)
+                       nccl_id=nccl_id, partition=partition, lanes_per_pose=lpp)
         inf = h.system_info()
         # the ranks the exchange actually spans: the communicator's count (RCCL), or gloo's
         seen = inf["comm_ranks"] if nccl_id is not None else (dist.get_world_size() if world > 1 else 1)
@@ -502,6 +510,7 @@ def main():
                 "poses": P.NP, "landmarks": P.NL, "bearings": int(len(P.b_z)), "odometry": int(len(P.o_z)),
                 "parallelism": (f"subtree-sharded x{world} ({'RCCL' if args.exchange == 'rccl' else 'gloo rehearsal'} "
                                 f"all-gathers; top fronts replicated: {info['top_fronts']})") if world > 1 else "single GPU",
+                "lanes_per_pose": info["lanes_per_pose"],
             },
             "ranks_seen": ranks_seen,
             "devices": 1 if (args.same_device or world == 1) else world,
