@@ -1100,7 +1100,14 @@ __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
 // the landmark's own values are loaded before them: the launch is latency bound (few dependent
 // hops per landmark, 200k landmarks), so fewer lanes per landmark with more loads in flight each
 // beat one row per lane.
-constexpr int kFoldLanes = 4;   // measured: 22 us at 4 lanes, 23 at 8, 34 at 16 (config 3)
+// BOS_MF_FOLD_LANES (measurement builds): 1, 2 or 4 lanes per landmark, bit-identical (rows go to
+// the partial of their index mod 4, combined as the four-lane butterfly does: (p0 + p2) + (p1 + p3))
+#ifndef BOS_MF_FOLD_LANES
+#define BOS_MF_FOLD_LANES 4
+#endif
+constexpr int kFoldLanes = BOS_MF_FOLD_LANES;   // measured: 22 us at 4 lanes, 23 at 8, 34 at 16 (config 3)
+constexpr int kFoldParts = 4 / kFoldLanes;
+static_assert(kFoldParts * kFoldLanes == 4, "1, 2 or 4 lanes per folded landmark");
 __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const int g = (blockIdx.x * kMfBlock + threadIdx.x) / kFoldLanes;
     const int q0 = threadIdx.x % kFoldLanes;
@@ -1116,7 +1123,9 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const double y0v = a.x[c0], y1v = a.x[c0 + 1], L00v = Ls[0], L10v = Ls[1], L11v = Ls[m + 1];
     const double y0 = head ? y0v : 0.0, y1 = head ? y1v : 0.0;
     const double L00 = head ? L00v : 1.0, L10 = head ? L10v : 0.0, L11 = head ? L11v : 1.0;
-    double t0 = 0.0, t1 = 0.0;
+    double t0p[kFoldParts], t1p[kFoldParts];
+#pragma unroll
+    for (int k = 0; k < kFoldParts; ++k) t0p[k] = t1p[k] = 0.0;
     const int rl = r > 0 ? r - 1 : 0;   // reads of rows past r are clamped (and their products dropped)
     for (int q = q0; q < r; q += 4 * kFoldLanes) {
         int idx[4];
@@ -1133,9 +1142,17 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const bool ok = q + u * kFoldLanes < r;
-            t0 += ok ? la[u] * xv[u] : 0.0;
-            t1 += ok ? lb[u] * xv[u] : 0.0;
+            t0p[u % kFoldParts] += ok ? la[u] * xv[u] : 0.0;
+            t1p[u % kFoldParts] += ok ? lb[u] * xv[u] : 0.0;
         }
+    }
+    double t0 = t0p[0], t1 = t1p[0];
+    if constexpr (kFoldParts == 2) {
+        t0 += t0p[1];
+        t1 += t1p[1];
+    } else if constexpr (kFoldParts == 4) {
+        t0 = (t0p[0] + t0p[2]) + (t0p[1] + t0p[3]);
+        t1 = (t1p[0] + t1p[2]) + (t1p[1] + t1p[3]);
     }
 #pragma unroll
     for (int o = kFoldLanes / 2; o > 0; o >>= 1) {
