@@ -642,13 +642,21 @@ __device__ __forceinline__ bool jh_unit(int64_t i, int64_t n_units, int64_t n_po
 #endif
 }
 
-// per-wave chi^2 / robust count of a pose wave (fixed order: the stats kernel sums the waves)
-__device__ __forceinline__ void pose_wave_partials(double* chi2_part, int32_t* nrob_part, int g, double chi, int nrob) {
+// chi^2 / robust count of a pose workgroup, its waves summed in order (deterministic), one partial
+// per workgroup (the stats kernel sums them in a fixed order)
+__device__ __forceinline__ void pose_wg_partials(double* chi2_part, int32_t* nrob_part, int g, double chi, int nrob) {
+    __shared__ double sc[kJhWg / 64];
+    __shared__ int sr[kJhWg / 64];
     chi = wave_sum(chi);
     nrob = (int)wave_sum((double)nrob);
-    if ((threadIdx.x & 63) == 0) {
-        chi2_part[g >> 6] = chi;
-        nrob_part[g >> 6] = nrob;
+    if ((threadIdx.x & 63) == 0) { sc[threadIdx.x >> 6] = chi; sr[threadIdx.x >> 6] = nrob; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double c = 0.0;
+        int r = 0;
+        for (int w = 0; w < kJhWg / 64; ++w) { c += sc[w]; r += sr[w]; }
+        chi2_part[g / kJhWg] = c;
+        nrob_part[g / kJhWg] = r;
     }
 }
 
@@ -672,7 +680,7 @@ __global__ __launch_bounds__(kJhWg, MINW) void linearize_kernel(const LinParams<
 #endif
     pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, g, chi, nrob, st);
     stamp_flush(P.diag_stamps, st, 0);
-    pose_wave_partials(P.chi2_part, P.nrob_part, g, chi, nrob);
+    pose_wg_partials(P.chi2_part, P.nrob_part, g, chi, nrob);
 }
 
 // The J+H launch of the common case (unit weights, no duplicate pairs): the ILP lanes above.
@@ -693,7 +701,7 @@ __global__ __launch_bounds__(kJhWg, MINW) void linearize_ilp_kernel(const LinPar
     int nrob = 0;
     pose_lanes_ilp<T, LPP, NIP>(P, g, chi, nrob, st);
     stamp_flush(P.diag_stamps, st, 0);
-    pose_wave_partials(P.chi2_part, P.nrob_part, g, chi, nrob);
+    pose_wg_partials(P.chi2_part, P.nrob_part, g, chi, nrob);
 }
 
 // max that propagates NaN (fmax returns the non-NaN operand): a non-finite update must not read
@@ -754,8 +762,8 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
     }
 }
 
-// This thread's share of the J+H chi^2 / robust-count partials (one per pose wave), in a fixed
-// order: four loads in flight per thread and step
+// This thread's share of the J+H chi^2 / robust-count partials (one per pose workgroup), in a
+// fixed order: four loads in flight per thread and step
 template <typename R>
 __device__ __forceinline__ void sum_partials(const double* chi_part, const int32_t* nrob_part, int n, double& c, R& r) {
     for (int i0 = threadIdx.x; i0 < n; i0 += 4 * blockDim.x) {

@@ -11,15 +11,14 @@ namespace dev {
 #define BOS_JH_BLOCK 256
 #endif
 constexpr int kBlock = BOS_JH_BLOCK;   // J+H block of lanes (host/plan.hpp kJhBlock)
-// J+H launch: workgroups of kJhWg threads, kJhSub of them per block of lanes, the pose and landmark
-// units interleaved in launch order (linearize_kernel); chi^2 partials per wave
+// J+H launch: workgroups of kJhWg threads, kJhSub of them per block of lanes (linearize_kernel,
+// jh_unit); chi^2 partials: one per pose workgroup
 #ifndef BOS_JH_WG
 #define BOS_JH_WG 256
 #endif
 constexpr int kJhWg = BOS_JH_WG;
 constexpr int kJhSub = kBlock / kJhWg;
 static_assert(kJhSub * kJhWg == kBlock && kJhWg % 64 == 0, "J+H workgroup");
-constexpr int kWavesPerBlock = kBlock / 64;
 // padding records after each lane-list array: the J+H kernel reads records up to five items past a
 // lane's last one, unguarded
 constexpr int kRecPad = 512;
@@ -80,8 +79,8 @@ template <typename T> struct LinParams {
     // the translation columns of the bearing Jacobian are minus its landmark columns), expanded by
     // the solver's fp64 conversion (launch_gather_f64)
     int pl_factored;
-    double* chi2_part;        // [pose_blocks * kWavesPerBlock]: one per pose wave
-    int32_t* nrob_part;       // [pose_blocks * kWavesPerBlock]
+    double* chi2_part;        // [pose_blocks * kJhSub]: one per pose workgroup
+    int32_t* nrob_part;       // [pose_blocks * kJhSub]
     T kt;                     // robust kernel threshold
     T lambda;                 // damping
     unsigned long long* diag_stamps;   // timeline diagnostics only (8 x u64 per wave), null otherwise

@@ -1075,7 +1075,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         }
         // chi^2 partials: own lanes (a whole number of blocks when sharded), the top lanes on rank 0;
         // observations partition: every block (the others' partials stay 0)
-        s->chi_parts = bos::dev::kWavesPerBlock *
+        s->chi_parts = bos::dev::kJhSub *
                        (s->rank == 0 || s->obs ? s->pose_blocks : (int)((int64_t)P.shard.own_pose_lanes * B.lpp / bos::dev::kBlock));
         if ((rc = upload(&s->lane_pose, B.lane_pose))) return bail(rc);
         s->lane_identity = true;
@@ -1161,7 +1161,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     } else {
         if ((rc = dalloc(&s->d_dense, (size_t)P.n * P.n))) return bail(rc);
     }
-    const int nt = std::max(1, s->pose_blocks * bos::dev::kWavesPerBlock);   // chi^2 partials: one per pose wave
+    const int nt = std::max(1, s->pose_blocks * bos::dev::kJhSub);   // chi^2 partials: one per pose workgroup
     if ((rc = dalloc(&s->d_info, 1)) || (rc = dalloc(&s->d_chi_part, nt)) || (rc = dalloc(&s->d_nrob_part, nt)) ||
         (rc = dalloc(&s->d_status, 1)) ||
         (rc = dalloc(&s->d_maxpart, (size_t)std::max(1, (s->NP + s->NL + bos::dev::kUpdateBlock - 1) / bos::dev::kUpdateBlock))))
