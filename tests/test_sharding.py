@@ -121,10 +121,10 @@ def _merge(P, handles_states, owner):
     return pose, lm
 
 
-def _run_local_shards(P, world, iters, precision):
+def _run_local_shards(P, world, iters, precision, lpp=0):
     """W sharded handles on one GPU, exchanges by host copies (external phase API)."""
     import bos
-    S = [bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=world)
+    S = [bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=world, lanes_per_pose=lpp)
          for r in range(world)]
     stats = []
     for _ in range(iters):
@@ -146,9 +146,9 @@ def _run_local_shards(P, world, iters, precision):
     return _merge(P, states, owner), stats, states, owner, info
 
 
-def _run_one(P, iters, precision):
+def _run_one(P, iters, precision, lpp=0):
     import bos
-    A = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR)
+    A = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=lpp)
     st = [A.step() for _ in range(iters)]
     s = A.get_state()
     A.close()
@@ -178,6 +178,24 @@ def test_sharded_step_equals_single_gpu(world, which):
         assert np.array_equal(pg[top], p1[top])
     assert all(i["top_fronts"] > 0 for i in info)
     assert sum(i["own_fronts"] for i in info) + info[0]["top_fronts"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_step_two_lanes_per_pose(world):
+    """The bench's N > 1 configuration (bench.py: two J+H lanes per pose): the sharded step on the
+    benchmark's C3 world (fp32 J+H) equals the one-GPU step with the same lanes, bit for bit."""
+    import bos
+    P = bos.synthetic(100000, 200000, 10, seed=0xB05EED01 + 3)
+    (pm, lm_), stats, states, owner, info = _run_local_shards(P, world, 3, bos.BOS_FP32, lpp=2)
+    (p1, l1), st1 = _run_one(P, 3, bos.BOS_FP32, lpp=2)
+    assert all(i["lanes_per_pose"] == 2 for i in info)
+    assert np.array_equal(pm, p1) and np.array_equal(lm_, l1)
+    for it in range(3):
+        for r in range(world):
+            assert abs(stats[it][r]["chi2"] - st1[it]["chi2"]) <= 1e-12 * st1[it]["chi2"], (it, r)
+            assert stats[it][r]["n_robust"] == st1[it]["n_robust"]
+            assert stats[it][r]["solver_info"] == 0
 
 
 @pytest.mark.gpu
