@@ -1168,9 +1168,13 @@ hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, hipStream_t s) {
 
 // Minimum waves per SIMD the kernel is compiled for (register budget): 4 (<= 128 VGPRs); 5 (<= 102)
 // makes the fp64 variant spill, measured slower (36 vs 31 us on config 3).
+// BOS_JH_MINW_ALL (measurement builds): another register budget for every variant
+#ifndef BOS_JH_MINW_ALL
+#define BOS_JH_MINW_ALL 4
+#endif
 template <typename T, bool W, bool D>
 hipError_t launch_lin_w(const LinParams<T>& p, int lpp, hipStream_t s) {
-    return launch_lin_lpp<T, W, D, 4>(p, lpp, s);
+    return launch_lin_lpp<T, W, D, BOS_JH_MINW_ALL>(p, lpp, s);
 }
 
 template <typename T>
