@@ -38,6 +38,12 @@ int bos_dataset_write_g2o(const bos_dataset* ds, const char* path, const double*
                           int with_landmarks);
 void bos_dataset_free(bos_dataset* ds);
 
+/* Solver::normalized_angle (slam/solver.hpp:50, slam/solver_jacobians.cpp:325-333): the wrap into
+ * [-pi, pi) the kernels use (bos_math.hpp), compared in double as the reference does. An |a| past
+ * ~1e15 (or an infinite one), on which the reference's loops never end, gives NaN. */
+double bos_normalized_angle_f64(double a);
+float bos_normalized_angle_f32(float a);
+
 typedef struct bos_plan_info {
     int64_t n;
     int64_t nnz_lower;

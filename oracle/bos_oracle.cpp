@@ -43,7 +43,16 @@ constexpr double CV_PI_D = 3.1415926535897932384626433832795;
 constexpr double CV_2PI_D = 6.283185307179586476925286766559;
 
 // Solver::normalized_angle — slam/solver_jacobians.cpp:325-333. Half-open [-pi, pi).
+// Deviation: the reference's loops never end for an infinite angle or one whose ulp exceeds 2 pi;
+// here |angle| > 1e6 is first reduced by the nearest multiple of 2 pi, and a remainder that is
+// still outside [-4 pi, 4 pi] (a quotient past 2^53) or not finite gives NaN — the product's rule
+// (bos_math.hpp), restated. Every |angle| <= 1e6 runs exactly the reference's loops.
 template <typename T> inline T normalized_angle(T angle) {
+    if (!(std::fabs((double)angle) <= 1e6)) {
+        const double r = (double)angle - CV_2PI_D * std::nearbyint((double)angle / CV_2PI_D);
+        if (!(std::fabs((T)r) <= 2.0 * CV_2PI_D)) return std::numeric_limits<T>::quiet_NaN();
+        angle = (T)r;
+    }
     while ((double)angle < -CV_PI_D) angle = (T)((double)angle + CV_2PI_D);
     while ((double)angle >= CV_PI_D) angle = (T)((double)angle - CV_2PI_D);
     return angle;

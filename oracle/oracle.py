@@ -402,32 +402,55 @@ def linearize(P: Problem, pose_xyt=None, lm_xy=None, kernel_threshold=1.0, dampi
     return Linearization(pd[:NP], ld[:NL], hpl[:Mb], hoff[:Mo], b[:P.N], chi2.value, nrob.value)
 
 
-def assemble_H(P: Problem, lin: Linearization):
-    """Full symmetric N x N H (scipy CSR, reference dof order: poses 3*stix, landmarks
-    3*NP + 2*stix — slam/solver_jacobians.cpp:70-71)."""
-    import scipy.sparse as sp
+def _h_pattern(P: Problem):
+    """(rows, cols) of every H contribution in assemble_H's order: pose diagonal, landmark
+    diagonal, pose-landmark blocks and their transposes, odometry off-diagonal blocks and theirs."""
     NP = P.NP
-    rows, cols, vals = [], [], []
+    rows, cols = [], []
     pi = 3 * np.arange(NP)
     li = 3 * NP + 2 * np.arange(P.NL)
     for i in range(3):
         for j in range(3):
-            rows.append(pi + i); cols.append(pi + j); vals.append(lin.pose_diag[:, i, j])
+            rows.append(pi + i); cols.append(pi + j)
     for i in range(2):
         for j in range(2):
-            rows.append(li + i); cols.append(li + j); vals.append(lin.lm_diag[:, i, j])
+            rows.append(li + i); cols.append(li + j)
     bp = 3 * P.b_pose.astype(np.int64)
     bl = 3 * NP + 2 * P.b_lm.astype(np.int64)
     for i in range(3):
         for j in range(2):
-            rows += [bp + i, bl + j]; cols += [bl + j, bp + i]; vals += [lin.hpl[:, i, j]] * 2
+            rows += [bp + i, bl + j]; cols += [bl + j, bp + i]
     os_ = 3 * P.o_src.astype(np.int64)
     od = 3 * P.o_dst.astype(np.int64)
     for i in range(3):
         for j in range(3):
-            rows += [os_ + i, od + j]; cols += [od + j, os_ + i]; vals += [lin.hoff[:, i, j]] * 2
-    r = np.concatenate(rows); c = np.concatenate(cols); v = np.concatenate(vals)
-    return sp.coo_matrix((v, (r, c)), shape=(P.N, P.N)).tocsr()
+            rows += [os_ + i, od + j]; cols += [od + j, os_ + i]
+    return np.concatenate(rows), np.concatenate(cols)
+
+
+def _h_values(lin: Linearization):
+    vals = []
+    for i in range(3):
+        for j in range(3):
+            vals.append(lin.pose_diag[:, i, j])
+    for i in range(2):
+        for j in range(2):
+            vals.append(lin.lm_diag[:, i, j])
+    for i in range(3):
+        for j in range(2):
+            vals += [lin.hpl[:, i, j]] * 2
+    for i in range(3):
+        for j in range(3):
+            vals += [lin.hoff[:, i, j]] * 2
+    return np.concatenate(vals)
+
+
+def assemble_H(P: Problem, lin: Linearization):
+    """Full symmetric N x N H (scipy CSR, reference dof order: poses 3*stix, landmarks
+    3*NP + 2*stix — slam/solver_jacobians.cpp:70-71)."""
+    import scipy.sparse as sp
+    r, c = _h_pattern(P)
+    return sp.coo_matrix((_h_values(lin), (r, c)), shape=(P.N, P.N)).tocsr()
 
 
 def reduced_system(P: Problem, H, b):
@@ -437,6 +460,31 @@ def reduced_system(P: Problem, H, b):
     keep[3 * P.fixed:3 * P.fixed + 3] = False
     idx = np.nonzero(keep)[0]
     return H[idx][:, idx], b[idx], idx
+
+
+def reduced_system_csc(P: Problem, lin: Linearization):
+    """reduced_system(P, assemble_H(P, lin), lin.b) with H_nf as CSC, through a scatter map built
+    once per problem (the pattern is static, slam/solver.hpp:71-82): the same matrix, its
+    duplicates summed in another order (fp64 rounding)."""
+    import scipy.sparse as sp
+    cache = getattr(P, "_hnf_map", None)
+    keep = np.ones(P.N, dtype=bool)
+    keep[3 * P.fixed:3 * P.fixed + 3] = False
+    idx = np.nonzero(keep)[0]
+    n = len(idx)
+    if cache is None:
+        r, c = _h_pattern(P)
+        new = np.full(P.N, -1, dtype=np.int64)
+        new[idx] = np.arange(n)
+        rr, cc = new[r], new[c]
+        sel = (rr >= 0) & (cc >= 0)
+        uk, inv = np.unique(cc[sel] * n + rr[sel], return_inverse=True)
+        indptr = np.concatenate([[0], np.cumsum(np.bincount(uk // n, minlength=n))])
+        cache = (sel, inv, (uk % n).astype(np.int32), indptr.astype(np.int64), len(uk))
+        P._hnf_map = cache
+    sel, inv, indices, indptr, nnz = cache
+    data = np.bincount(inv, weights=_h_values(lin)[sel], minlength=nnz)
+    return sp.csc_matrix((data, indices, indptr), shape=(n, n)), lin.b[idx], idx
 
 
 def solve_dx(P: Problem, H, b) -> np.ndarray:

@@ -48,7 +48,7 @@ EXPORTED_SYMBOLS = [
     "bos_node_owner",
     "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph", "bos_debug_solver_stamps",
     "bos_time_linearize", "bos_time_triangulate", "bos_time_steps", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
-    "bos_cpu_gn_destroy",
+    "bos_cpu_gn_destroy", "bos_normalized_angle_f64", "bos_normalized_angle_f32",
 ]
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -179,6 +179,8 @@ def lib():
         "bos_cpu_gn_step": (ctypes.c_int, [vp, _dp]),
         "bos_cpu_gn_get_state": (ctypes.c_int, [vp, _dp, _dp]),
         "bos_cpu_gn_destroy": (None, [vp]),
+        "bos_normalized_angle_f64": (ctypes.c_double, [ctypes.c_double]),
+        "bos_normalized_angle_f32": (ctypes.c_float, [ctypes.c_float]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -20,18 +20,6 @@
 
 #include "../host/bos_math.hpp"
 
-// J+H build variants (measurement builds only; the defaults are the product): BOS_JH_ILP launches
-// the ILP lanes for the common case (no faster, and the GN step slower), with
-// BOS_JH_NIP pose items per chunk (fp32) and BOS_JH_MINW waves per SIMD; BOS_JH_LOOP_WAIT /
-// BOS_JH_LM_WAIT (a vmcnt(0) before the pose / landmark pair loop), BOS_JH_STORE_LATE (the
-// pose-landmark block stored after the refill loads), BOS_JH_PRIO (pose waves' issue priority),
-// BOS_JH_WG / BOS_JH_ORDER (kernels.hpp, jh_unit): measured, no gain
-#ifndef BOS_JH_NIP
-#define BOS_JH_NIP 12
-#endif
-#ifndef BOS_JH_MINW
-#define BOS_JH_MINW 4
-#endif
 
 namespace bos {
 namespace dev {
@@ -55,19 +43,6 @@ template <typename T> __device__ __forceinline__ void store6(T* p, T a, T b, T c
     __builtin_nontemporal_store(v2{e, f}, q + 2);
 }
 
-// Timing diagnostics only (results wrong): the pose-landmark block stores dropped, or written as
-// six 256-byte coalesced runs per wave step (value v of lane t at 64 v + t of the step's 384 values)
-template <typename T> __device__ __forceinline__ void store_pl(T* base, int64_t slot, const T o[6]) {
-#if defined(BOS_JH_DIAG_NOPLSTORE)
-    if (o[0] == (T)1.2345e-30) base[6 * slot] = o[1];   // keeps the arithmetic alive
-#elif defined(BOS_JH_DIAG_SOASTORE)
-    T* q = base + 384 * (slot >> 6) + (slot & 63);
-#pragma unroll
-    for (int v = 0; v < 6; ++v) __builtin_nontemporal_store(o[v], q + 64 * v);
-#else
-    store6(base + 6 * slot, o[0], o[1], o[2], o[3], o[4], o[5]);
-#endif
-}
 
 template <typename T> __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
@@ -239,7 +214,7 @@ __device__ __forceinline__ void put_pl(T* plbase, int64_t slot, const T o[6], T 
             for (int q = 0; q < 6; ++q) acc[q] = (T)0;
         }
     } else {
-        store_pl(plbase, slot, o);
+        store6(plbase + 6 * slot, o[0], o[1], o[2], o[3], o[4], o[5]);
     }
 }
 
@@ -283,9 +258,7 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
         T wA = HAS_W ? P.pb_w[at(0)] : (T)1, wB = HAS_W ? P.pb_w[at(1)] : (T)1;
         iA = ip[at(2)];
         iB = ip[at(3)];
-        // odometry first (fp32): its arithmetic covers the landmark gathers of items 0 and 1; the
-        // fp64 variant runs it after the bearings, which keeps it within 128 VGPRs
-        constexpr bool kOdoFirst = true;
+        // odometry first: its arithmetic covers the landmark gathers of items 0 and 1
         T acc6[6] = {0, 0, 0, 0, 0, 0};
         auto odometry = [&]() {
             if (x0 < x1) odo_fetch_data(P, otha, oa);
@@ -300,31 +273,20 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
                 odometry_entry<T, HAS_DUPS>(P, x, x1, oc, X, th, h, gb, acc6, chi, nrob);
             }
         };
-        if (kOdoFirst) odometry();
+        odometry();
         T acc[6] = {0, 0, 0, 0, 0, 0}, o[6], jf[3];
         const bool factored = P.pl_factored != 0;
         T* const plbase = P.hval + P.off_pl;
         stamp(P.diag_stamps, st, 1);
-#ifdef BOS_JH_LOOP_WAIT
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) once, before the loop (experiment)
-#endif
         for (int j = 0; j < n; j += 2) {
             // item j (set A), then refill A: item j + 2's gather and z, item j + 4's index
             pose_bearing<T>(P, X, LA, zA, wA, h, gb, o, chi, nrob, jf);
-#ifndef BOS_JH_STORE_LATE
             put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * j, o, acc, lastA, factored, jf);
             lastA = !(iA & kRunCont);
-#else
-            const bool lastA0 = lastA;
-            lastA = !(iA & kRunCont);
-#endif
             LA = load2(P.lc + 2 * (iA & kIdxMask));
             zA = zp[at(j + 2)];
             if (HAS_W) wA = P.pb_w[at(j + 2)];
             iA = ip[at(j + 4)];
-#ifdef BOS_JH_STORE_LATE   // (experiment) the store after the refill loads: vmcnt retires in order
-            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * j, o, acc, lastA0, factored, jf);
-#endif
             // item j + 1 (set B). Its block is stored even past the lane's last item (a padding slot
             // of the lane's wave: pose-lane waves have an even number of slots per lane), so both
             // paths issue the same memory operations and the loop's waits stay exact.
@@ -335,23 +297,14 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
                 for (int q = 0; q < 6; ++q) o[q] = (T)0;
                 jf[0] = jf[1] = jf[2] = (T)0;
             }
-#ifndef BOS_JH_STORE_LATE
             put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * (j + 1), o, acc, lastB, factored, jf);
             lastB = !(iB & kRunCont);
-#else
-            const bool lastB0 = lastB;
-            lastB = !(iB & kRunCont);
-#endif
             LB = load2(P.lc + 2 * (iB & kIdxMask));
             zB = zp[at(j + 3)];
             if (HAS_W) wB = P.pb_w[at(j + 3)];
             iB = ip[at(j + 5)];
-#ifdef BOS_JH_STORE_LATE
-            put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * (j + 1), o, acc, lastB0, factored, jf);
-#endif
         }
         stamp(P.diag_stamps, st, 2);
-        if (!kOdoFirst) odometry();
     }
     // combine the lane group's partial sums (fixed butterfly: deterministic)
 #pragma unroll
@@ -403,9 +356,6 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int g, unsi
     iA = ip[at(2)];
     iB = ip[at(3)];
     stamp(P.diag_stamps, st, 1);
-#ifdef BOS_JH_LM_WAIT
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) once, before the loop (experiment)
-#endif
     for (int j = 0; j < n; j += 2) {
         landmark_bearing<T>(P, XA, Lm, zA, wA, hl, gl);
         XA = load4(P.pc + 4 * iA);
@@ -425,187 +375,6 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int g, unsi
     bl[0] = gl[0]; bl[1] = gl[1];
 }
 
-// ---- the J+H with every load of a lane issued up front (the common case: unit bearing weights,
-// no duplicate pairs). A lane's inputs are three dependent hops away — its header (count, list base
-// and stride, pose, odometry range), its records (landmark index and z of each item, the odometry
-// entries), then the gathers (landmark / pose state, the odometry edges' other pose and data) — and
-// each hop costs a memory latency (1.5-2 us from HBM under this kernel's load). Here the records of
-// the first NI items are read at once (indices clamped to the lane's last item, no predicated
-// loads: a predicated load is a branch with its wait inside), then all their gathers, then the
-// arithmetic: three latencies per lane instead of three plus one per pair of items. Lists longer
-// than NI continue in chunks of NI. Same arithmetic in the same order as the pair loop above (the
-// result is bit-identical to it).
-template <typename T, int NI>
-struct PoseChunk {
-    int idx[NI];
-    T z[NI];
-};
-
-template <typename T, int LPP, int NI>
-__device__ __forceinline__ void pose_lanes_ilp(const LinParams<T>& P, int g, double& chi, int& nrob,
-                                               unsigned long long* st) {
-    const int grp = g / LPP, sub = g % LPP, t = g & 63;
-    const int p = grp < P.n_groups ? (P.lane_pose ? P.lane_pose[grp] : grp) : -1;
-    const bool active = p >= 0;
-    T h[6] = {0, 0, 0, 0, 0, 0}, gb[3] = {0, 0, 0};
-    if (active) {
-        // hop 1: addressed by the lane and its pose only
-        const V4<T> X = load4(P.pc + 4 * p);
-        const T th = P.pth[p];
-        const int n = P.pl_cnt[g];
-        const int sl = P.pw_base[g >> 6] + t;   // slot of item j: sl + S j
-        const int S = P.pw_stride[g >> 6];
-        const int x0 = P.po_ptr[p], x1 = P.po_ptr[p + 1];
-        // hop 2: the records of items 0 .. NI - 1 (clamped to the last item; padded arrays) and the
-        // first two odometry entries (lane 0 of the group walks them; the arrays are padded)
-        const int jl = n > 0 ? n - 1 : 0;
-        PoseChunk<T, NI> c;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int sj = sl + S * min(i, jl);
-            c.idx[i] = P.pb_idx[sj];
-            c.z[i] = P.pb_z[sj];
-        }
-        const int ne = sub == 0 ? x1 - x0 : 0;
-        OdoIn<T> oa, ob;
-        int otha, othb;
-        odo_fetch_ids(P, x0, oa, otha);
-        odo_fetch_ids(P, x0 + 1 < x1 ? x0 + 1 : x0, ob, othb);
-        // hop 3: every gather
-        V2<T> L[NI];
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-#ifdef BOS_JH_DIAG_NOGATHER   // timing diagnostics only: no gather (results wrong)
-            L[i] = V2<T>{(T)(c.idx[i] & 1023), (T)(c.idx[i] & 511)};
-#else
-            L[i] = load2(P.lc + 2 * (c.idx[i] & kIdxMask));
-#endif
-        }
-        odo_fetch_data(P, otha, oa);
-        odo_fetch_data(P, othb, ob);
-        // odometry first, then the bearings (the pair loop's order)
-        T acc6[6] = {0, 0, 0, 0, 0, 0};
-        if (ne > 0) odometry_entry<T, false>(P, x0, x1, oa, X, th, h, gb, acc6, chi, nrob);
-        if (ne > 1) odometry_entry<T, false>(P, x0 + 1, x1, ob, X, th, h, gb, acc6, chi, nrob);
-        for (int x = x0 + 2; x < x0 + ne; ++x) {
-            OdoIn<T> oc;
-            int othc;
-            odo_fetch_ids(P, x, oc, othc);
-            odo_fetch_data(P, othc, oc);
-            odometry_entry<T, false>(P, x, x1, oc, X, th, h, gb, acc6, chi, nrob);
-        }
-        stamp(P.diag_stamps, st, 1);
-        T* const blk0 = P.hval + P.off_pl + 6 * (int64_t)sl;
-        T o[6], jf[3];
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            if (i < n) {
-#ifdef BOS_JH_DIAG_NOCOMPUTE   // timing diagnostics only: loads and stores, no arithmetic (results wrong)
-                o[0] = L[i].x; o[1] = L[i].y; o[2] = c.z[i]; o[3] = X.x; o[4] = X.y; o[5] = X.z;
-                h[0] += L[i].x;
-#else
-                pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob, jf);
-#endif
-                if (P.pl_factored) store3(P.hval + P.off_pl + 3 * ((int64_t)sl + (int64_t)S * i), jf[0], jf[1], jf[2]);
-                else store6(blk0 + 6 * (int64_t)S * i, o[0], o[1], o[2], o[3], o[4], o[5]);
-            }
-        }
-        // items past NI (lists longer than NI: not at config 3), NI at a time
-        for (int j0 = NI; j0 < n; j0 += NI) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int sj = sl + S * min(j0 + i, jl);
-                c.idx[i] = P.pb_idx[sj];
-                c.z[i] = P.pb_z[sj];
-            }
-#pragma unroll
-            for (int i = 0; i < NI; ++i) L[i] = load2(P.lc + 2 * (c.idx[i] & kIdxMask));
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                if (j0 + i < n) {
-                    pose_bearing<T>(P, X, L[i], c.z[i], (T)1, h, gb, o, chi, nrob, jf);
-                    if (P.pl_factored) store3(P.hval + P.off_pl + 3 * ((int64_t)sl + (int64_t)S * (j0 + i)), jf[0], jf[1], jf[2]);
-                    else store6(blk0 + 6 * (int64_t)S * (j0 + i), o[0], o[1], o[2], o[3], o[4], o[5]);
-                }
-            }
-        }
-        stamp(P.diag_stamps, st, 2);
-    }
-    // combine the lane group's partial sums (fixed butterfly: deterministic)
-#pragma unroll
-    for (int o = 1; o < LPP; o <<= 1) {
-#pragma unroll
-        for (int v = 0; v < 6; ++v) h[v] += __shfl_xor(h[v], o);
-#pragma unroll
-        for (int v = 0; v < 3; ++v) gb[v] += __shfl_xor(gb[v], o);
-    }
-    if (active && sub == 0) {
-        const T lam = P.lambda;
-        store6(P.hval + 6 * p, h[0] + lam, h[1], h[2] + lam, h[3], h[4], h[5] + lam);
-        T* bp = P.b + 3 * p;
-        bp[0] = gb[0]; bp[1] = gb[1]; bp[2] = gb[2];
-    }
-}
-
-template <typename T, int NI>
-__device__ __forceinline__ void landmark_lane_ilp(const LinParams<T>& P, int g, unsigned long long* st) {
-    if (g >= P.n_lm_lanes) return;
-    // hop 1: the lane's header
-    const int l = P.ll_lm[g];
-    const int n = P.ll_cnt[g];
-    const int sl = P.lw_base[g >> 6] + (g & 63);
-    const int S = P.lw_stride[g >> 6];
-    const int jl = n > 0 ? n - 1 : 0;
-    // hop 2: the landmark and the records of items 0 .. NI - 1; hop 3: the pose gathers
-    const V2<T> Lm = load2(P.lc + 2 * l);
-    int idx[NI];
-    T z[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        const int sj = sl + S * min(i, jl);
-        idx[i] = P.lb_idx[sj];
-        z[i] = P.lb_z[sj];
-    }
-    V4<T> X[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-#ifdef BOS_JH_DIAG_NOGATHER
-        X[i] = V4<T>{(T)(idx[i] & 1023), (T)(idx[i] & 511), (T)0.5, (T)0.5};
-#else
-        X[i] = load4(P.pc + 4 * idx[i]);
-#endif
-    }
-    stamp(P.diag_stamps, st, 1);
-    T hl[3] = {0, 0, 0}, gl[2] = {0, 0};
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-        if (i < n) {
-#ifdef BOS_JH_DIAG_NOCOMPUTE
-            hl[0] += X[i].x + z[i]; hl[1] += X[i].y; hl[2] += X[i].z + Lm.x; gl[0] += X[i].w + Lm.y;
-#else
-            landmark_bearing<T>(P, X[i], Lm, z[i], (T)1, hl, gl);
-#endif
-        }
-    for (int j0 = NI; j0 < n; j0 += NI) {   // lists longer than NI
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int sj = sl + S * min(j0 + i, jl);
-            idx[i] = P.lb_idx[sj];
-            z[i] = P.lb_z[sj];
-        }
-#pragma unroll
-        for (int i = 0; i < NI; ++i) X[i] = load4(P.pc + 4 * idx[i]);
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-            if (j0 + i < n) landmark_bearing<T>(P, X[i], Lm, z[i], (T)1, hl, gl);
-    }
-    stamp(P.diag_stamps, st, 2);
-    T* hp = P.hval + P.off_ldiag + 3 * l;
-    hp[0] = hl[0] + P.lambda; hp[1] = hl[1]; hp[2] = hl[2] + P.lambda;
-    T* bl = P.b + 3 * P.NP + 2 * l;
-    bl[0] = gl[0]; bl[1] = gl[1];
-}
-
 // XCD-aware block order: blocks b and b + 8 share an XCD (and its L2), so a segment [s0, s1) of
 // the grid is renumbered to give each XCD a contiguous run of it; the pose (landmark) blocks an
 // XCD runs then cover a stretch of the trajectory, and the landmark (pose) cache lines their
@@ -617,29 +386,16 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t s0, int64_t
 
 // Launch order of the J+H units (kJhWg lanes each; kJhSub per block of lanes): pose units first,
 // then landmark units, each range XCD-contiguous (above). Pose waves are the longer chains (~12.7 us
-// against ~8.5 us per wave cold at config 3), so they get the head start; one-wave units spread
-// them evenly over the CUs (tools/jh_timeline.py, per-CU section: with 256-lane workgroups, 135 of
-// 256 CUs held two pose blocks and ended 2.7 us after the others). BOS_JH_ORDER=1 (measurement
-// builds) interleaves the two kinds in proportion instead: every CU the same mix, but the pose
-// waves lose their head start (measured slower). Returns true for a pose unit; u = the unit's
-// index in its range.
-#ifndef BOS_JH_ORDER
-#define BOS_JH_ORDER 0
-#endif
+// against ~8.5 us per wave cold at config 3), so they get the head start (measured: interleaving
+// the two kinds in proportion, or one-wave units spreading the pose waves over every CU, is no
+// faster). Returns true for a pose unit; u = the unit's index in its range.
 __device__ __forceinline__ bool jh_unit(int64_t i, int64_t n_units, int64_t n_pose_units, int64_t& u) {
-#if BOS_JH_ORDER == 1
-    const int64_t j = xcd_contiguous(i, 0, n_units);
-    const int64_t cp = j * n_pose_units / n_units, cp1 = (j + 1) * n_pose_units / n_units;
-    u = cp1 > cp ? cp : j - cp;
-    return cp1 > cp;
-#else
     if (i < n_pose_units) {
         u = xcd_contiguous(i, 0, n_pose_units);
         return true;
     }
     u = xcd_contiguous(i, n_pose_units, n_units) - n_pose_units;
     return false;
-#endif
 }
 
 // chi^2 / robust count of a pose workgroup, its waves summed in order (deterministic), one partial
@@ -675,31 +431,7 @@ __global__ __launch_bounds__(kJhWg, MINW) void linearize_kernel(const LinParams<
     const int g = (int)(((int64_t)P.pose_b0 * kJhSub + u) * kJhWg + threadIdx.x);
     double chi = 0.0;
     int nrob = 0;
-#ifdef BOS_JH_PRIO   // (experiment) pose waves, the longer chains, issue first
-    __builtin_amdgcn_s_setprio(BOS_JH_PRIO);
-#endif
     pose_lanes<T, HAS_W, HAS_DUPS, LPP>(P, g, chi, nrob, st);
-    stamp_flush(P.diag_stamps, st, 0);
-    pose_wg_partials(P.chi2_part, P.nrob_part, g, chi, nrob);
-}
-
-// The J+H launch of the common case (unit weights, no duplicate pairs): the ILP lanes above.
-template <typename T, int LPP, int NIP, int NIL, int MINW>
-__global__ __launch_bounds__(kJhWg, MINW) void linearize_ilp_kernel(const LinParams<T> P) {
-    int64_t u;
-    const bool pose = jh_unit(blockIdx.x, gridDim.x, (int64_t)P.n_pose_run * kJhSub, u);
-    unsigned long long st[3] = {0, 0, 0};
-    if (P.t_start && blockIdx.x == 0 && threadIdx.x == 0) *P.t_start = __builtin_amdgcn_s_memrealtime();
-    stamp(P.diag_stamps, st, 0);
-    if (!pose) {
-        landmark_lane_ilp<T, NIL>(P, (int)(((int64_t)P.lm_b0 * kJhSub + u) * kJhWg + threadIdx.x), st);
-        stamp_flush(P.diag_stamps, st, 1);
-        return;
-    }
-    const int g = (int)(((int64_t)P.pose_b0 * kJhSub + u) * kJhWg + threadIdx.x);
-    double chi = 0.0;
-    int nrob = 0;
-    pose_lanes_ilp<T, LPP, NIP>(P, g, chi, nrob, st);
     stamp_flush(P.diag_stamps, st, 0);
     pose_wg_partials(P.chi2_part, P.nrob_part, g, chi, nrob);
 }
@@ -1132,32 +864,8 @@ hipError_t launch_lin_k(LinParams<T> p, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <typename T, int LPP, int MINW>
-hipError_t launch_lin_ilp(LinParams<T> p, hipStream_t s) {
-    const int lm_blocks = (p.n_lm_lanes + kBlock - 1) / kBlock;
-    if (p.pose_b0 < 0 || p.n_pose_run < 0 || p.pose_b0 + p.n_pose_run > p.pose_blocks || p.lm_b0 < 0 || p.n_lm_run < 0 ||
-        p.lm_b0 + p.n_lm_run > lm_blocks)
-        return hipErrorInvalidValue;
-    const int grid = (p.n_pose_run + p.n_lm_run) * kJhSub;
-    if (grid == 0) return hipSuccess;
-    // items read per chunk: 12 pose / 8 landmark items (fp32), 8 / 8 (fp64: twice the registers)
-    constexpr int NIP = sizeof(T) == 4 ? BOS_JH_NIP : 8, NIL = 8;
-    hipLaunchKernelGGL((linearize_ilp_kernel<T, LPP, NIP, NIL, MINW>), dim3(grid), dim3(kJhWg), 0, s, p);
-    return hipGetLastError();
-}
-
 template <typename T, bool W, bool D, int MINW>
 hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, hipStream_t s) {
-#ifdef BOS_JH_ILP
-    if (!W && !D) {   // every load of a lane up front (measurement builds: DESIGN.md §4)
-        switch (lpp) {
-            case 1: return launch_lin_ilp<T, 1, BOS_JH_MINW>(p, s);
-            case 2: return launch_lin_ilp<T, 2, BOS_JH_MINW>(p, s);
-            case 4: return launch_lin_ilp<T, 4, BOS_JH_MINW>(p, s);
-            default: return hipErrorInvalidValue;
-        }
-    }
-#endif
     switch (lpp) {
         case 1: return launch_lin_k<T, W, D, 1, MINW>(p, s);
         case 2: return launch_lin_k<T, W, D, 2, MINW>(p, s);
@@ -1167,14 +875,11 @@ hipError_t launch_lin_lpp(const LinParams<T>& p, int lpp, hipStream_t s) {
 }
 
 // Minimum waves per SIMD the kernel is compiled for (register budget): 4 (<= 128 VGPRs); 5 (<= 102)
-// makes the fp64 variant spill, measured slower (36 vs 31 us on config 3).
-// BOS_JH_MINW_ALL (measurement builds): another register budget for every variant
-#ifndef BOS_JH_MINW_ALL
-#define BOS_JH_MINW_ALL 4
-#endif
+// makes the fp64 variant spill, measured slower (36 vs 31 us on config 3), and 80 VGPRs for every
+// variant (all two-lane waves resident) spill in fp32 too.
 template <typename T, bool W, bool D>
 hipError_t launch_lin_w(const LinParams<T>& p, int lpp, hipStream_t s) {
-    return launch_lin_lpp<T, W, D, BOS_JH_MINW_ALL>(p, lpp, s);
+    return launch_lin_lpp<T, W, D, 4>(p, lpp, s);
 }
 
 template <typename T>

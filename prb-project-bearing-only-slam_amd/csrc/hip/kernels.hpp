@@ -7,16 +7,10 @@
 namespace bos {
 namespace dev {
 
-#ifndef BOS_JH_BLOCK
-#define BOS_JH_BLOCK 256
-#endif
-constexpr int kBlock = BOS_JH_BLOCK;   // J+H block of lanes (host/plan.hpp kJhBlock)
+constexpr int kBlock = 256;   // J+H block of lanes (host/plan.hpp kJhBlock)
 // J+H launch: workgroups of kJhWg threads, kJhSub of them per block of lanes (linearize_kernel,
 // jh_unit); chi^2 partials: one per pose workgroup
-#ifndef BOS_JH_WG
-#define BOS_JH_WG 256
-#endif
-constexpr int kJhWg = BOS_JH_WG;
+constexpr int kJhWg = 256;
 constexpr int kJhSub = kBlock / kJhWg;
 static_assert(kJhSub * kJhWg == kBlock && kJhWg % 64 == 0, "J+H workgroup");
 // padding records after each lane-list array: the J+H kernel reads records up to five items past a

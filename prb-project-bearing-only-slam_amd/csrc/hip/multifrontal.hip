@@ -460,9 +460,6 @@ __device__ __forceinline__ void fold_chunk(const MfArgs& a, double* W, FoldBuf* 
             W[pos * WS + 2 * lml + 1] = lt1;
         }
     }
-#ifdef BOS_MF_FOLD_STAMPS   // measurement builds: the first chunk's values have arrived (slot 6)
-    if (first) fstamp(a.stamps_f, s, 6);
-#endif
     wave_sync();
     const int kc = 2 * nl;
     if (lane < m) {   // u-vector part: -(W y) at this lane's position
@@ -540,9 +537,6 @@ __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W,
         nn = n2;
     }
     if (nbad) atomicAdd(a.info, nbad);
-#ifdef BOS_MF_FOLD_STAMPS   // slot 7: the front's chunk count
-    if (a.stamps_f && lane == 0) a.stamps_f[8 * (int64_t)s + 7] = (unsigned long long)(ch1 - ch0);
-#endif
 }
 
 // The front before its assembly: every lower entry of F and of wv set to minus the folded
@@ -595,18 +589,12 @@ struct Flow {
                             // per-level launches, the other program, or another rank's exchange)
     int id;
     unsigned long long* stamps;   // diagnostics (bos_debug_solver_stamps): 8 realtime stamps per front, or null
-    // the top launch (one workgroup, mf_factor_top / mf_backward_top): its fronts' completion flags in
-    // LDS (by position in `order`), the position of the front a wave works on, and each position's
-    // dependencies inside the launch (children for the factorization, the parent backward)
-    int* lds_done;
-    int pos;
-    const int32_t* dep_ptr;   // [n + 1]
-    const int32_t* dep_pos;
 };
 
 // Front-processing modes: per-level launch (no waits), dataflow launch (flags in global memory,
-// coherent hand-off), top launch (one workgroup: flags in LDS, hand-off through the CU's caches)
-constexpr int kModeLevel = 0, kModeFlow = 1, kModeTop = 2;
+// coherent hand-off). (A third, the tree's top as one workgroup with flags in LDS, measured slower
+// than the flows: DESIGN.md §4.)
+constexpr int kModeLevel = 0, kModeFlow = 1;
 
 constexpr int kStall = kMfStall;               // or-ed into info when a dependency wait times out
 constexpr uint64_t kWaitTicks = 5000000;        // 50 ms of the 100 MHz realtime clock
@@ -638,7 +626,7 @@ __device__ __forceinline__ int next_ticket(int* ticket) {
 // ancestor further up (a backward front reads x rows of its parent's ancestors) is covered by the
 // chain: each ancestor drained its sc1 stores before its flag, which its child observed before
 // publishing its own. The formal agent-scope acquire (buffer_inv sc1 after the poll) measured
-// costlier and bit-identical: DESIGN.md §4 (build flag BOS_MF_AGENT_ACQUIRE).
+// costlier and bit-identical: DESIGN.md §4.
 __device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
     if (threadIdx.x == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -651,11 +639,7 @@ __device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
             __builtin_amdgcn_s_sleep(2);
         }
     }
-#ifdef BOS_MF_AGENT_ACQUIRE
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the formal form (measurement builds only)
-#else
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
     wave_sync();
 }
 
@@ -665,35 +649,6 @@ __device__ __forceinline__ void leave_flow(const Flow& f) {
         __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(f.exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-}
-
-// The top launch's hand-off (one workgroup, so workgroup scope): the dependency's LDS flag, then an
-// acquire fence at workgroup scope (no cache invalidation: every wave of the workgroup shares the CU's
-// caches); bounded like wait_done.
-__device__ __forceinline__ void wait_lds(const Flow& f, int pos, int32_t* info) {
-    if ((threadIdx.x & 63) == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f.lds_done + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
-            if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStall) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) {
-                atomicOr(info, kStall);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    wave_sync();
-}
-
-__device__ __forceinline__ void wait_deps_lds(const Flow& f, int32_t* info) {
-    for (int q = f.dep_ptr[f.pos]; q < f.dep_ptr[f.pos + 1]; ++q) wait_lds(f, f.dep_pos[q], info);
-}
-
-// release at workgroup scope (the front's stores complete before the flag), then the LDS flag
-__device__ __forceinline__ void publish_lds(const Flow& f) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if ((threadIdx.x & 63) == 0) __hip_atomic_store(f.lds_done + f.pos, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 __device__ __forceinline__ void publish_done(const Flow& f, int s) {
@@ -824,8 +779,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     if constexpr (MODE == kModeFlow) {
         for (int ci = a.child_ptr[s]; ci < ce; ++ci)
             if (f->fid[a.child[ci]] == f->id) wait_done(*f, a.child[ci], a.info);
-    } else if constexpr (MODE == kModeTop) {
-        wait_deps_lds(*f, a.info);
     }
     fstamp(stp, s, 3);
     // extend-add, children in list order (deterministic)
@@ -972,12 +925,9 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     wave_sync();
 }
 
-// BOS_MF_C48_WAVES (measurement builds): waves per SIMD the class-48 launch is compiled for
-#ifndef BOS_MF_C48_WAVES
-#define BOS_MF_C48_WAVES 1
-#endif
+// (class 48 bounded to 4 waves per SIMD spills and measured slower)
 template <int MAXM, bool F32>
-__global__ __launch_bounds__(64, (MAXM == 48 ? BOS_MF_C48_WAVES : 1)) void mf_factor_reg(const MfArgs a) {
+__global__ __launch_bounds__(64, 1) void mf_factor_reg(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * MAXM];
     __shared__ __attribute__((aligned(16))) double wv[MAXM];
@@ -1022,11 +972,7 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
         for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
         fstamp(stp, s, 1);
-        if constexpr (MODE == kModeFlow) {
-            if (parent[s] >= 0 && f->fid[parent[s]] == f->id) wait_done(*f, parent[s], a.info);
-        } else {
-            wait_deps_lds(*f, a.info);
-        }
+        if (parent[s] >= 0 && f->fid[parent[s]] == f->id) wait_done(*f, parent[s], a.info);
         fstamp(stp, s, 2);
         if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
         for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
@@ -1100,14 +1046,8 @@ __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
 // the landmark's own values are loaded before them: the launch is latency bound (few dependent
 // hops per landmark, 200k landmarks), so fewer lanes per landmark with more loads in flight each
 // beat one row per lane.
-// BOS_MF_FOLD_LANES (measurement builds): 1, 2 or 4 lanes per landmark, bit-identical (rows go to
-// the partial of their index mod 4, combined as the four-lane butterfly does: (p0 + p2) + (p1 + p3))
-#ifndef BOS_MF_FOLD_LANES
-#define BOS_MF_FOLD_LANES 4
-#endif
-constexpr int kFoldLanes = BOS_MF_FOLD_LANES;   // measured: 22 us at 4 lanes, 23 at 8, 34 at 16 (config 3)
-constexpr int kFoldParts = 4 / kFoldLanes;
-static_assert(kFoldParts * kFoldLanes == 4, "1, 2 or 4 lanes per folded landmark");
+// (one lane per landmark from a packed record measured slower: DESIGN.md §4)
+constexpr int kFoldLanes = 4;   // measured: 22 us at 4 lanes, 23 at 8, 34 at 16 (config 3)
 __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const int g = (blockIdx.x * kMfBlock + threadIdx.x) / kFoldLanes;
     const int q0 = threadIdx.x % kFoldLanes;
@@ -1123,9 +1063,7 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const double y0v = a.x[c0], y1v = a.x[c0 + 1], L00v = Ls[0], L10v = Ls[1], L11v = Ls[m + 1];
     const double y0 = head ? y0v : 0.0, y1 = head ? y1v : 0.0;
     const double L00 = head ? L00v : 1.0, L10 = head ? L10v : 0.0, L11 = head ? L11v : 1.0;
-    double t0p[kFoldParts], t1p[kFoldParts];
-#pragma unroll
-    for (int k = 0; k < kFoldParts; ++k) t0p[k] = t1p[k] = 0.0;
+    double t0 = 0.0, t1 = 0.0;
     const int rl = r > 0 ? r - 1 : 0;   // reads of rows past r are clamped (and their products dropped)
     for (int q = q0; q < r; q += 4 * kFoldLanes) {
         int idx[4];
@@ -1142,17 +1080,9 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const bool ok = q + u * kFoldLanes < r;
-            t0p[u % kFoldParts] += ok ? la[u] * xv[u] : 0.0;
-            t1p[u % kFoldParts] += ok ? lb[u] * xv[u] : 0.0;
+            t0 += ok ? la[u] * xv[u] : 0.0;
+            t1 += ok ? lb[u] * xv[u] : 0.0;
         }
-    }
-    double t0 = t0p[0], t1 = t1p[0];
-    if constexpr (kFoldParts == 2) {
-        t0 += t0p[1];
-        t1 += t1p[1];
-    } else if constexpr (kFoldParts == 4) {
-        t0 = (t0p[0] + t0p[2]) + (t0p[1] + t0p[3]);
-        t1 = (t1p[0] + t1p[2]) + (t1p[1] + t1p[3]);
     }
 #pragma unroll
     for (int o = kFoldLanes / 2; o > 0; o >>= 1) {
@@ -1217,70 +1147,6 @@ __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flo
     leave_flow(f);
 }
 
-// The top of the tree as one workgroup of kTopWaves waves (levels with at most that many fronts,
-// mf_create): a wave takes the next front from an LDS ticket, waits for its children of this launch
-// on LDS flags, and hands its update matrix / u-vector over through plain stores and loads (the
-// workgroup's waves share the CU's caches), ordered by release / acquire fences at workgroup scope.
-// Fronts further down finished in earlier launches.
-constexpr int kTopWaves = kMfTopWaves;
-constexpr int kTopMax = 256;   // fronts of a top launch (mf_create keeps the top within this)
-
-__device__ __forceinline__ int lds_ticket(int* ticket) {
-    int t = 0;
-    if ((threadIdx.x & 63) == 0) t = atomicAdd(ticket, 1);
-    return __builtin_amdgcn_readfirstlane(t);
-}
-
-template <bool F32>
-__global__ __launch_bounds__(64 * kTopWaves) void mf_factor_top(const MfArgs a, const Flow f_in) {
-    __shared__ __attribute__((aligned(16))) double F[kTopWaves][kFlowMaxM * (kFlowMaxM + 1) / 2];
-    __shared__ __attribute__((aligned(16))) double colbuf[kTopWaves][2 * kFlowMaxM];
-    __shared__ __attribute__((aligned(16))) double wv[kTopWaves][kFlowMaxM];
-    __shared__ FoldBuf fb[kTopWaves];
-    __shared__ int done[kTopMax];
-    __shared__ int ticket;
-    for (int i = threadIdx.x; i < kTopMax; i += blockDim.x) done[i] = 0;
-    if (threadIdx.x == 0) ticket = 0;
-    __syncthreads();
-    const int wv_id = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    Flow f = f_in;
-    f.lds_done = done;
-    for (int it = 0; it <= f.n; ++it) {   // bounded (see factor_flow_body)
-        const int t = lds_ticket(&ticket);
-        if (t >= f.n) break;
-        f.pos = t;
-        const int s = f.order[t];
-        factor_front_reg<kFlowMaxM, kModeTop, F32>(a, s, F[wv_id], colbuf[wv_id], wv[wv_id], &fb[wv_id], lane, &f);
-        fstamp(f.stamps, s, 6);
-        publish_lds(f);
-        fstamp(f.stamps, s, 7);
-    }
-}
-
-// Backward substitution of the top, top-down in the same form (dependency: the parent); LDS per wave:
-// lds_bwd bytes (dynamic, kTopWaves slices)
-__global__ __launch_bounds__(64 * kTopWaves) void mf_backward_top(const MfArgs a, const Flow f_in, int slice) {
-    extern __shared__ __attribute__((aligned(16))) double wl[];
-    __shared__ int done[kTopMax];
-    __shared__ int ticket;
-    for (int i = threadIdx.x; i < kTopMax; i += blockDim.x) done[i] = 0;
-    if (threadIdx.x == 0) ticket = 0;
-    __syncthreads();
-    const int wv_id = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    Flow f = f_in;
-    f.lds_done = done;
-    double* w = wl + (int64_t)wv_id * slice;
-    for (int it = 0; it <= f.n; ++it) {
-        const int t = lds_ticket(&ticket);
-        if (t >= f.n) break;
-        f.pos = t;
-        const int s = f.order[t];
-        backward_front<kModeTop>(a, s, w, lane, &f, nullptr);
-        publish_lds(f);
-        fstamp(f.stamps, s, 4);
-    }
-}
-
 // Structure arrays carry kMfPad zeroed elements after their end: the kernels read clamped indices
 // unconditionally (branch-free loads, see assemble_wave) and may touch up to one chunk / 64 lanes past
 // a range's last element.
@@ -1327,16 +1193,11 @@ struct Prog {
     int32_t* order_bwd = nullptr;
     int32_t* fold_list = nullptr;   // folded landmarks whose parent is in this program
     int n_fold = 0;
-    // the top launches (mf_factor_top / mf_backward_top): levels >= top_lev0 (factorization) and >=
-    // top_b0 (backward), at most kTopWaves fronts each; flow id id + 2; dependencies by position
-    int top_lev0 = 0, top_b0 = 0, n_top_f = 0, n_top_b = 0, top_slice = 0;
-    // per-level backward launches of the wave fronts (classes 0-3) split by their LDS need
-    // (kBwdSplit): level l's buckets are blist[bptr[l][b] .. bptr[l][b + 1]) with blds[l][b] bytes each
-    std::vector<std::vector<int32_t>> bptr;
-    std::vector<std::vector<int>> blds;
+    // per-level backward launches of the wave fronts (classes 0-3, one launch per level, the LDS of
+    // the level's largest panel): level l's fronts are blist[bptr[l] .. bptr[l + 1]), blds[l] bytes each
+    std::vector<int32_t> bptr;
+    std::vector<int> blds;
     int32_t* blist = nullptr;
-    int32_t *order_top_f = nullptr, *dep_ptr_f = nullptr, *dep_pos_f = nullptr;
-    int32_t *order_top_b = nullptr, *dep_ptr_b = nullptr, *dep_pos_b = nullptr;
     int count(int lev, int c0, int c1) const { return ptr[lev * kClasses + c1] - ptr[lev * kClasses + c0]; }
     int count(int lev, int c) const { return count(lev, c, c + 1); }
     int lds_max(const std::vector<int>& v, int lev, int c0, int c1) const {
@@ -1356,18 +1217,9 @@ struct Prog {
 // factorization of levels with >= kFactorWideLevel fronts before its flow starts (config 3: levels
 // 0-2, 564 -> 556 us; also level 3: 567).
 constexpr int kFlowWavesFactor = 6;
-#ifndef BOS_MF_TOP   // measurement builds: 1 = the one-workgroup top launches (mf_factor_top /
-#define BOS_MF_TOP 0   // mf_backward_top); measured slower than the flows taking the top
-#endif
-constexpr bool kTopLaunch = BOS_MF_TOP != 0;
 // The per-level backward launch of a level's wave fronts gives every wave the LDS of the level's
 // largest panel (m k doubles): class-64 fronts (up to ~16 KB) then hold a level-0 launch to 8-10
-// waves per CU. Fronts needing more than kBwdSplit bytes go to a launch of their own, before the rest.
-#ifndef BOS_MF_BWD_SPLIT   // bytes; 0 = one launch per level (measurement builds)
-#define BOS_MF_BWD_SPLIT 0
-#endif
-constexpr int kBwdSplit = BOS_MF_BWD_SPLIT;
-constexpr int kTopMinLevels = 2;
+// waves per CU; splitting the big panels into a launch of their own measured no faster.
 constexpr int kFlowWavesBackward = 4;
 constexpr int kSolveWideLevel = 256;
 constexpr int kFactorWideLevel = 2048;
@@ -1458,23 +1310,17 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
         return c;
     };
     std::vector<int32_t> blst;
-    P.bptr.assign(L, {});
-    P.blds.assign(L, {});
+    P.bptr.assign(L + 1, 0);
+    P.blds.assign(L, 0);
     for (int l = 0; l < L; ++l) {
-        // the level's wave fronts (classes 0-3, in list order: longest first), big panels first
+        // the level's wave fronts (classes 0-3, in list order: longest first)
         const int q0 = P.ptr[l * kClasses], q1 = P.ptr[l * kClasses + 4];
-        auto need = [&](int s2) { const int k = F.k[s2], m = k + F.r[s2]; return (2 * k + (m - k) + m * k) * 8; };
-        std::vector<int32_t> big, small;
-        for (int q = q0; q < q1; ++q) (kBwdSplit > 0 && need(lst[q]) > kBwdSplit ? big : small).push_back(lst[q]);
-        for (auto* part : {&big, &small}) {
-            if (part->empty()) continue;
-            int mx = 0;
-            for (int s2 : *part) mx = std::max(mx, need(s2));
-            P.bptr[l].push_back((int32_t)blst.size());
-            P.blds[l].push_back(mx);
-            blst.insert(blst.end(), part->begin(), part->end());
+        for (int q = q0; q < q1; ++q) {
+            const int s2 = lst[q], k = F.k[s2], m = k + F.r[s2];
+            P.blds[l] = std::max(P.blds[l], (2 * k + (m - k) + m * k) * 8);
+            blst.push_back(s2);
         }
-        P.bptr[l].push_back((int32_t)blst.size());
+        P.bptr[l + 1] = (int32_t)blst.size();
     }
     // dataflow ranges: the factor flow starts at the lowest level (>= 2) from which every front of
     // the program is <= kFlowMaxM, and above the wide levels
@@ -1491,37 +1337,17 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
         while (wide < L && mine_in_level(wide) >= kFactorWideLevel) ++wide;
         P.flow_lev0 = std::max(P.flow_lev0, wide);
     }
-    // the top: the highest levels of the flow range with at most kTopWaves fronts each (at least
-    // kTopMinLevels of them, at most kTopMax fronts)
-    P.top_lev0 = L;
-    if (kTopLaunch && P.flow_lev0 < L) {
-        int t0 = L, nt = 0;
-        while (t0 > P.flow_lev0 && mine_in_level(t0 - 1) <= kTopWaves && nt + mine_in_level(t0 - 1) <= kTopMax)
-            nt += mine_in_level(--t0);
-        if (L - t0 >= kTopMinLevels) P.top_lev0 = t0;
-    }
-    const int8_t top_id = (int8_t)(id + 2);
-    std::vector<int32_t> ofac, ofwd, otop;
+    std::vector<int32_t> ofac, ofwd;
     for (int q = F.level_ptr[std::min(P.flow_lev0, L)]; q < F.level_ptr[L]; ++q) {
         const int s = F.level[q];
         if (!mine(s)) continue;
-        if (q < F.level_ptr[P.top_lev0]) { ofac.push_back(s); fid_f[s] = (int8_t)id; }
-        else { otop.push_back(s); fid_f[s] = top_id; }
+        ofac.push_back(s);
+        fid_f[s] = (int8_t)id;
     }
     P.n_flow_factor = (int)ofac.size();
-    P.n_top_f = (int)otop.size();
-    std::vector<int32_t> pos_of(F.nsuper, -1), dptr_f(1, 0), dpos_f;
-    for (int t = 0; t < P.n_top_f; ++t) pos_of[otop[t]] = t;
-    for (int t = 0; t < P.n_top_f; ++t) {   // children of this launch (lower positions: level order)
-        const int s = otop[t];
-        for (int ci = F.child_ptr[s]; ci < F.child_ptr[s + 1]; ++ci)
-            if (fid_f[F.child[ci]] == top_id) dpos_f.push_back(pos_of[F.child[ci]]);
-        dptr_f.push_back((int32_t)dpos_f.size());
-    }
     P.solve_lev0 = std::min(2, L);
     while (P.solve_lev0 < L && mine_in_level(P.solve_lev0) >= kSolveWideLevel) ++P.solve_lev0;
-    P.top_b0 = P.top_lev0 < L ? std::max(P.top_lev0, P.solve_lev0) : L;
-    for (int q = F.level_ptr[P.solve_lev0]; q < F.level_ptr[P.top_b0]; ++q) {
+    for (int q = F.level_ptr[P.solve_lev0]; q < F.level_ptr[L]; ++q) {
         const int s = F.level[q], k = F.k[s], m = k + F.r[s];
         if (!mine(s)) continue;
         ofwd.push_back(s);
@@ -1530,38 +1356,22 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
     std::vector<int32_t> obwd(ofwd.rbegin(), ofwd.rend());
     P.n_flow_solve = (int)ofwd.size();
     P.flow_solve = P.n_flow_solve > 0 && P.lds_bwd_flow <= 48 * 1024;
-    if (!P.flow_solve) P.solve_lev0 = P.top_b0;
+    if (!P.flow_solve) P.solve_lev0 = L;
     else
         for (int s : obwd) fid_b[s] = (int8_t)id;
-    // backward top: top-down, each front after its parent (lower positions)
-    std::vector<int32_t> otopb, dptr_b(1, 0), dpos_b;
-    for (int q = F.level_ptr[L] - 1; q >= F.level_ptr[P.top_b0]; --q)
-        if (mine(F.level[q])) otopb.push_back(F.level[q]);
-    P.n_top_b = (int)otopb.size();
-    std::fill(pos_of.begin(), pos_of.end(), -1);
-    for (int t = 0; t < P.n_top_b; ++t) { pos_of[otopb[t]] = t; fid_b[otopb[t]] = top_id; }
-    for (int t = 0; t < P.n_top_b; ++t) {
-        const int s = otopb[t], k = F.k[s], m = k + F.r[s];
-        if (F.parent[s] >= 0 && pos_of[F.parent[s]] >= 0) dpos_b.push_back(pos_of[F.parent[s]]);
-        dptr_b.push_back((int32_t)dpos_b.size());
-        P.top_slice = std::max(P.top_slice, 2 * k + (m - k) + m * k);   // doubles per wave
-    }
     std::vector<int32_t> folds;
     for (int s : F.fold_list)
         if (mine(F.parent[s])) folds.push_back(s);
     P.n_fold = (int)folds.size();
     int rc;
     if ((rc = up(&P.list, lst, err)) || (rc = up(&P.order_factor, ofac, err)) || (rc = up(&P.order_bwd, obwd, err)) ||
-        (rc = up(&P.fold_list, folds, err)) || (rc = up(&P.order_top_f, otop, err)) || (rc = up(&P.dep_ptr_f, dptr_f, err)) ||
-        (rc = up(&P.dep_pos_f, dpos_f, err)) || (rc = up(&P.order_top_b, otopb, err)) ||
-        (rc = up(&P.dep_ptr_b, dptr_b, err)) || (rc = up(&P.dep_pos_b, dpos_b, err)) || (rc = up(&P.blist, blst, err)))
+        (rc = up(&P.fold_list, folds, err)) || (rc = up(&P.blist, blst, err)))
         return rc;
     return 0;
 }
 
 void free_prog(Prog& P) {
-    void* bufs[] = {P.list, P.order_factor, P.order_bwd, P.fold_list, P.order_top_f, P.dep_ptr_f, P.dep_pos_f,
-                    P.order_top_b, P.dep_ptr_b, P.dep_pos_b, P.blist};
+    void* bufs[] = {P.list, P.order_factor, P.order_bwd, P.fold_list, P.blist};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
 }
@@ -1642,19 +1452,12 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         (rc = up(&d->fold_cnt, F.fold_cnt, err)) || (rc = up(&d->fold_cptr, F.fold_cptr, err)) ||
         (rc = up(&d->fold_chunk, F.fold_chunk, err)) || (rc = up(&d->fold_rec, F.fold_rec, err)))
         return rc;
-#ifndef BOS_MF_EVENT_FLAGS   // (measurement builds: other fence scopes for the fork / join events)
-#define BOS_MF_EVENT_FLAGS 0
-#endif
     if (hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming | BOS_MF_EVENT_FLAGS) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming | BOS_MF_EVENT_FLAGS) != hipSuccess) {
+        hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) {
         err = "side stream creation failed (multifrontal)";
         return -2;
     }
-#ifdef BOS_MF_NO_SIDE   // measurement builds: every class of a level on the main stream
-    (void)hipStreamDestroy(d->side);
-    d->side = nullptr;
-#endif
     auto alloc = [&](double** p, int64_t n) -> int {   // + kMfPad: clamped reads (up())
         if (n <= 0) n = 1;
         if (hipMalloc((void**)p, (n + kMfPad) * sizeof(double)) != hipSuccess) { err = "hipMalloc failed (multifrontal buffers)"; return -2; }
@@ -1729,13 +1532,6 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
         hipLaunchKernelGGL((mf_factor_flow<F32>), dim3(grid), dim3(64), 0, s, d->args(P, 0, 0, A, x), f);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (P.n_top_f > 0) {
-        Flow f{P.order_top_f, P.n_top_f, nullptr, nullptr, nullptr, nullptr, 0u, d->fid_f, P.id + 2, d->stamps};
-        f.dep_ptr = P.dep_ptr_f;
-        f.dep_pos = P.dep_pos_f;
-        hipLaunchKernelGGL((mf_factor_top<F32>), dim3(1), dim3(64 * kTopWaves), 0, s, d->args(P, 0, 0, A, x), f);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     return hipSuccess;
 }
 
@@ -1754,15 +1550,6 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
     hipError_t e;
     const Prog& P = d->prog[which];
     if (P.ptr.empty()) return hipSuccess;
-    if (P.n_top_b > 0) {   // the top first (top-down)
-        Flow f{P.order_top_b, P.n_top_b, nullptr, nullptr, nullptr, nullptr, 0u, d->fid_b, P.id + 2,
-               d->stamps ? d->stamps + 8 * (int64_t)d->nsuper : nullptr};
-        f.dep_ptr = P.dep_ptr_b;
-        f.dep_pos = P.dep_pos_b;
-        hipLaunchKernelGGL(mf_backward_top, dim3(1), dim3(64 * kTopWaves), kTopWaves * P.top_slice * sizeof(double), s,
-                           d->args(P, 0, 0, nullptr, x), f, P.top_slice);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     if (P.flow_solve) {
         const Flow fb{P.order_bwd, P.n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1, d->done + d->nsuper,
                       d->epoch, 0u, d->fid_b, P.id, d->stamps ? d->stamps + 8 * (int64_t)d->nsuper : nullptr};
@@ -1773,11 +1560,11 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
     }
     for (int l = std::min(P.solve_lev0, d->nlevels) - 1; l >= 0; --l) {
         int n;
-        for (size_t b = 0; b + 1 < P.bptr[l].size(); ++b) {
+        if (P.bptr[l + 1] > P.bptr[l]) {
             MfArgs g = d->args(P, l, 0, nullptr, x);
-            g.level = P.blist + P.bptr[l][b];
-            g.count = P.bptr[l][b + 1] - P.bptr[l][b];
-            hipLaunchKernelGGL(mf_backward_wave, dim3(g.count), dim3(64), P.blds[l][b], s, g);
+            g.level = P.blist + P.bptr[l];
+            g.count = P.bptr[l + 1] - P.bptr[l];
+            hipLaunchKernelGGL(mf_backward_wave, dim3(g.count), dim3(64), P.blds[l], s, g);
         }
         if ((n = P.count(l, 4)))
             hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), P.lds_bwd[l * kClasses + 4], s, d->args(P, l, 4, nullptr, x));

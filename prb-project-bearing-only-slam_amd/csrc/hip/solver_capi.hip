@@ -953,9 +953,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
     if (pb->bearing_omega)
         for (int k = 0; k < s->Mb; ++k)
             if (pb->bearing_omega[k] != 1.0) { s->has_w = true; break; }
-#ifndef BOS_JH_NO_FACTOR   // (measurement builds: the unfactored layout for comparison)
     s->pl_factored = s->precision == BOS_FP32 && uses_mf(s) && !s->has_w && !s->has_dups;
-#endif
 
     // ---- streams / events / libraries
     if (opt.stream) {
@@ -1147,9 +1145,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         std::string merr;
         if (bos::dev::mf_create(P.mf, s->sharded ? P.shard.sn_owner.data() : nullptr, s->rank, &s->mf, merr))
             return bail(fail(BOS_ERR_DEVICE, merr));
-#ifndef BOS_MF_NO_FOLD32   // (measurement builds: the folds read the fp64 copy)
         s->fold32 = s->pl_factored && bos::mf_fold_reads_fp32(P);
-#endif
         if (s->fold32) bos::dev::mf_set_fold_source(s->mf, (const float*)s->sys_val, P.blk.off_pl);
     } else if (s->solver_kind == BOS_SOLVER_ROCSOLVER_RF) {
         std::vector<int32_t> piv(P.n);

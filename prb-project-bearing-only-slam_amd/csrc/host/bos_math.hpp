@@ -34,7 +34,13 @@ template <typename T> BOS_HD T normalized_angle(T a) {
     // from a diverged iteration) is first brought near [-pi, pi) by subtracting the nearest multiple
     // of 2 pi (a few instructions, unlike fmod, which costs registers in every kernel that inlines
     // this); a non-finite one becomes NaN. Every |a| <= 1e6 takes exactly the reference's path.
-    if (!(std::fabs((double)a) <= 1e6)) a = (T)((double)a - k2Pi * std::rint((double)a / k2Pi));
+    // Past |a| ~ 1e15 the quotient a / 2 pi is no longer exact and the remainder can be anything
+    // (and a float of that size does not move by +-2 pi), so a remainder outside [-4 pi, 4 pi]
+    // carries no angle: NaN, which the loops below pass through unchanged.
+    if (!(std::fabs((double)a) <= 1e6)) {
+        a = (T)((double)a - k2Pi * std::rint((double)a / k2Pi));
+        if (!(std::fabs((double)a) <= 2.0 * k2Pi)) return (T)__builtin_nan("");
+    }
     while ((double)a < -kPi) a = (T)((double)a + k2Pi);
     while ((double)a >= kPi) a = (T)((double)a - k2Pi);
     return a;

@@ -131,6 +131,9 @@ int bos_dataset_load_g2o(const char* path, int triangulate, int verbose, bos_dat
     return BOS_OK;
 }
 
+double bos_normalized_angle_f64(double a) { return bos::normalized_angle<double>(a); }
+float bos_normalized_angle_f32(float a) { return bos::normalized_angle<float>(a); }
+
 int bos_dataset_synthetic(int32_t num_poses, int32_t num_landmarks, int32_t bearings_per_pose, uint64_t seed,
                           bos_dataset** out) {
     if (!out) return hfail(BOS_ERR_INVALID, "null argument");

@@ -31,10 +31,7 @@ struct ProblemIndex {
 };
 
 // J+H launch geometry shared by the host plan and the kernel (hip/kernels.hpp kBlock)
-#ifndef BOS_JH_BLOCK   // (measurement builds: other J+H workgroup sizes, tools/build_full_variant.sh)
-#define BOS_JH_BLOCK 256
-#endif
-constexpr int kJhBlock = BOS_JH_BLOCK;
+constexpr int kJhBlock = 256;
 // Contiguous share [a, b) of n items for rank r of W (BOS_PARTITION_OBSERVATIONS: each rank runs a
 // range of the J+H's pose blocks and one of its landmark blocks, i.e. of the observations in
 // measurement order)
@@ -127,7 +124,6 @@ struct OrderingReport {
 //  - L panels are m x k column-major (entries above the diagonal unused).
 constexpr int kMfWaveMaxM = 64;
 constexpr int kMfFlowMaxM = 48;   // fronts of the dataflow factor launch (hip/multifrontal.hip kFlowMaxM)
-constexpr int kMfTopWaves = 8;    // waves of the one-workgroup top launches (hip/multifrontal.hip kTopWaves)
 constexpr int kFoldChunk = 64;   // folded rows per chunk (one per lane)
 constexpr int kFoldRec = 8;      // ints per folded row
 // landmarks per fold chunk for a parent front of size m: the device forms the chunk's

@@ -92,36 +92,66 @@ bool make_synthetic(const SyntheticParams& p, SyntheticWorld& out) {
         return a.first != b.first ? a.first < b.first : a.lane < b.lane;
     });
 
+    // ---- landmark placement with parallax (">= 2 observations per landmark with
+    // parallax"). A candidate is drawn from the window's last pose (bearing 20-82 deg to the window's
+    // side, range 0.7-4.5 m; wider after 128 attempts) and kept if every pose of the window sees it in
+    // front (|bearing| < 85 deg, range > 0.5 m and <= max(5.5 m, window span + 2 m)) and the rays
+    // from the window's poses span >= kMinParallax. With information 1 per bearing and the
+    // reference's constant damping 0.01 (slam/solver.cpp:16-17), a landmark's along-ray curvature is
+    // about (1 - cos parallax) / range^2: at 4 deg and 7 m (the old generator's tail) it is 1e-4, a
+    // hundredth of the damping, and such landmarks crept along their rays for hundreds of GN
+    // iterations and crossed poses (bearing errors of pi); at >= 20 deg and <= 5 m it is >= 2.4e-3.
+    // If no candidate qualifies, the one with the widest parallax among the visible ones is kept
+    // (`min_parallax` of the world reports the minimum reached).
+    constexpr double kMinParallax = 20.0 * bos::kPi / 180.0;
+    const double cos_front = std::cos(85.0 * bos::kPi / 180.0);
     std::vector<double> lx(NL), ly(NL);
     std::vector<std::vector<int>> seen_by(NP);
+    double min_par = 1e300;
     for (int j = 0; j < NL; ++j) {
         const Win& w = wins[j];
         const int L = w.last;
         const double side = (w.lane % 2) ? 1.0 : -1.0;
-        double bx = 0, by = 0;
-        for (int attempt = 0; attempt < 64; ++attempt) {
-            const double f = rng.uniform(0.8, attempt < 32 ? 3.0 : 6.0);
-            const double lat = side * rng.uniform(0.4, attempt < 32 ? 4.0 : 6.0);
-            bx = gx[L] + std::cos(gth[L]) * f - std::sin(gth[L]) * lat;
-            by = gy[L] + std::sin(gth[L]) * f + std::cos(gth[L]) * lat;
+        const double span = std::hypot(gx[L] - gx[w.first], gy[L] - gy[w.first]);
+        const double r_cap = std::max(5.5, span + 2.0);
+        double best_x = 0, best_y = 0, best_par = -1;
+        bool have_visible = false;
+        for (int attempt = 0; attempt < 256; ++attempt) {
+            const bool wide = attempt >= 128;
+            const double beta = side * rng.uniform(20.0, 82.0) * (bos::kPi / 180.0);
+            const double rho = rng.uniform(0.7, wide ? 7.0 : 4.5);
+            const double bx = gx[L] + rho * std::cos(gth[L] + beta);
+            const double by = gy[L] + rho * std::sin(gth[L] + beta);
             bool ok = true;
+            double a0 = 0, amin = 0, amax = 0;
             for (int i = w.first; i <= L && ok; ++i) {
+                const double dx = bx - gx[i], dy = by - gy[i];
                 const double c = std::cos(gth[i]), s = std::sin(gth[i]);
-                const double qx = c * (bx - gx[i]) + s * (by - gy[i]);
-                const double qy = -s * (bx - gx[i]) + c * (by - gy[i]);
-                const double r = std::hypot(qx, qy);
-                ok = r > 0.5 && qx > 0.08 * r;
+                const double qx = c * dx + s * dy;
+                const double r = std::hypot(dx, dy);
+                ok = r > 0.5 && r <= r_cap && qx > cos_front * r;
+                const double a = std::atan2(dy, dx);
+                if (i == w.first) a0 = a;
+                const double d = bos::normalized_angle<double>(a - a0);
+                amin = std::min(amin, d);
+                amax = std::max(amax, d);
             }
-            if (ok) break;
+            if (!ok) continue;
+            const double par = amax - amin;
+            if (!have_visible || par > best_par) { best_x = bx; best_y = by; best_par = par; have_visible = true; }
+            if (par >= kMinParallax) break;
         }
-        lx[j] = bx;
-        ly[j] = by;
+        if (!have_visible) return false;
+        lx[j] = best_x;
+        ly[j] = best_y;
+        min_par = std::min(min_par, best_par);
         for (int i = w.first; i <= L; ++i) seen_by[i].push_back(j);
     }
 
     // ---- assemble the two states and the measurements (bearings listed per pose, like the dataset)
     out = SyntheticWorld();
     out.fixed_pose_id = 0;
+    out.min_parallax = min_par;
     const int lm_id0 = NP;   // ids unique across poses and landmarks (g2o convention)
     double ix = gx[0], iy = gy[0], ith = gth[0];
     for (int i = 0; i < NP; ++i) {

@@ -26,13 +26,16 @@ struct SyntheticWorld {
     BearingObservationVector bearings;
     OdometryObservationVector odometry;
     int fixed_pose_id = 0;
+    double min_parallax = 0;          // smallest ray spread of any landmark (rad, ground truth)
 };
 
 // Trajectory: a bounded random walk (step 0.75-1 m, smooth heading changes, steered back inside
 // the world). Landmarks: K "lanes"; lane k cuts the pose sequence into windows of >= 2 consecutive
-// poses, one landmark per window, placed ahead of the window's last pose so every pose of the
-// window sees it with |bearing| < pi/2. Each pose therefore observes exactly K landmarks, each
-// landmark is observed >= 2 times with parallax, and (pose, landmark) pairs are unique.
+// poses, one landmark per window, placed beside the window's last pose so every pose of the
+// window sees it in front (|bearing| < 85 deg) and the window's rays span >= 20 deg wherever the
+// geometry allows it (min_parallax reports what was reached). Each pose therefore observes exactly
+// K landmarks, each landmark is observed >= 2 times with parallax, and (pose, landmark) pairs are
+// unique.
 // Returns false if the counts are infeasible (num_poses * K < 2 * num_landmarks, or
 // num_landmarks < K).
 bool make_synthetic(const SyntheticParams& p, SyntheticWorld& out);

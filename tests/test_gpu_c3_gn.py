@@ -1,7 +1,7 @@
 """GN-step parity at full config 3 on the benchmark's own world (bench.py CONFIG3: 100k poses /
-200k landmarks / 1M bearings / 99 999 odometry edges, seed 0xB05EED01 + 3), for the configuration
-bench.py times and for the fp64 path, over the iterations the bench times (it restarts from the
-initial guess for every timed run: iterations 1..K of the solve, the reference UI's batch of 50 at
+200k landmarks / 1M bearings / 99 999 odometry edges, seed 0xB05EED01 + 3), for the configurations
+bench.py times and for the fp64 path, over the iterations the bench times (iterations 1..50 of the
+solve from the initial guess, the reference UI's batch of 50 at
 /root/reference/executables/bearing_only_slam.cpp:93-99). Reference: Solver::step,
 slam/solver.cpp:27-97.
 
@@ -9,19 +9,27 @@ Oracle per iteration: the C++ oracle's J+H build (oracle/bos_oracle.cpp, referen
 order) + SciPy sparse direct solve of H_nf dx = -b_nf + box-plus, in the precisions the HIP path
 uses (fp64 J+H or fp32 J+H; the solve and the master state fp64).
 
+The world gives every landmark >= 20 deg of parallax (csrc/host/synthetic.cpp), so
+GN converges on it as on the reference dataset (README.md:22-24): chi^2 is flat to 1e-4 relative
+from iteration ~8 on (test_c3_fp32_converges_without_pivot_failures).
+
 Tolerances (stated here, measured margins in DESIGN.md §5):
   * fp64 J+H + fp64 Schur solve, 20 iterations: chi^2 of every iteration within 1e-9 relative, dx
     of iteration 1 within 1e-8 of max |dx| (two direct factorizations of one SPD system, as on C1),
     the state after 20 iterations within 1e-6 relative + 1e-9 absolute (the C1 50-iteration bound).
-  * fp32 J+H + fp64 Schur solve (the benchmarked path), 10 iterations, against the oracle's fp32 J+H
-    + fp64 solve/state: the two fp32 builds sum each pose's terms in different orders, so H and b
-    differ by fp32 rounding (2e-2 max-relative / 5e-4 p99.9 per entry at config 3, see
-    tests/test_gpu_parity.py). dx inherits that times the conditioning of H_nf; the bounds (poses
-    absolute, landmarks through the bearings they predict, chi^2 1e-3 relative) and their
-    calibration against the oracle's own fp32-vs-fp64 spread are in the test's docstring.
-  * Every step reports solver_info == 0 (no non-positive pivot, no dataflow stall); a system forced
-    to lose positive definiteness reports its non-positive pivots instead (slam/solver.cpp:82-84).
+  * fp32 J+H + fp64 Schur solve (the benchmarked path), 50 iterations, with one lane per pose (the
+    one-GPU bench) and two (the N > 1 bench), against the oracle's fp32 J+H + fp64 solve/state: the
+    two fp32 builds sum each pose's terms in different orders, so H and b differ by fp32 rounding
+    (2e-2 max-relative / 5e-4 p99.9 per entry at config 3, tests/test_gpu_parity.py). Bounds:
+    chi^2 of every iteration 1e-4 relative, poses 1e-4 absolute (SURVEY.md §8(c)'s fp32 row; the
+    world's coordinates reach ~1 km, where one fp32 ulp is 6e-5), landmarks through the bearings
+    they predict (p99.9 1e-5, max 1e-4 rad).
+  * Every step reports solver_info == 0 (no non-positive pivot, no dataflow stall), for 200
+    iterations of the fp32 path; a system forced to lose positive definiteness reports its
+    non-positive pivots instead (slam/solver.cpp:82-84).
 """
+import sys
+
 import numpy as np
 import pytest
 import scipy.sparse.linalg as spla
@@ -33,6 +41,7 @@ from helpers import close_state, to_oracle
 pytestmark = pytest.mark.gpu
 
 BENCH_SEED = 0xB05EED01 + 3   # bench.py CONFIG3
+FP32_ITERS = 50               # bench.py's batch
 
 
 @pytest.fixture(scope="module")
@@ -43,43 +52,58 @@ def world():
 def oracle_step(Q, pose, lm, jh_precision):
     """One GN iteration with the oracle's J+H in jh_precision and fp64 solve and state."""
     lin = O.linearize(Q, pose, lm, precision=jh_precision)
-    H = O.assemble_H(Q, lin)
-    Hnf, bnf, idx = O.reduced_system(Q, H, lin.b)
+    Hnf, bnf, idx = O.reduced_system_csc(Q, lin)
     dx = np.zeros(Q.N)
-    dx[idx] = spla.spsolve(Hnf.tocsc(), -bnf)
+    dx[idx] = spla.spsolve(Hnf, -bnf)
     O.apply_boxplus(Q, pose, lm, dx, 64)
     return lin.chi2, dx
 
 
-def run_pair(P, precision, iters):
+def oracle_run(P, jh_precision, iters):
+    """(chi^2 per iteration, dx of iteration 1, final pose, final landmarks)."""
     Q = to_oracle(P)
-    S = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR)
+    po, lo = Q.copy_state()
+    chis, dx1 = [], None
+    for i in range(iters):
+        c, dx = oracle_step(Q, po, lo, jh_precision)
+        chis.append(c)
+        if i == 0:
+            dx1 = dx
+        if i % 10 == 9:   # progress past pytest's capture (a silent minute reads as a hang)
+            print(f"oracle fp{jh_precision} iteration {i + 1}/{iters}: chi2 {c:.9g}", file=sys.__stderr__, flush=True)
+    return np.array(chis), dx1, po, lo
+
+
+@pytest.fixture(scope="module")
+def oracle_fp32(world):
+    return oracle_run(world, 32, FP32_ITERS)
+
+
+def hip_run(P, precision, iters, lanes_per_pose=0):
+    S = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=lanes_per_pose)
     # the benchmarked path: fp32 J+H with factored pose-landmark blocks that the folds read directly
     info = S.system_info()
     assert (info["pl_factored"], info["fold_fp32"]) == ((1, 1) if precision == bos.BOS_FP32 else (0, 0)), info
-    po, lo = Q.copy_state()
-    out = []
+    chis, dx1 = [], None
     for i in range(iters):
         st = S.step()
-        assert st["solver_info"] == 0, st
-        dxg = S.last_dx()
-        chio, dxo = oracle_step(Q, po, lo, 32 if precision == bos.BOS_FP32 else 64)
-        out.append((st["chi2"], chio, dxg, dxo))
+        assert st["solver_info"] == 0, (i, st)
+        chis.append(st["chi2"])
+        if i == 0:
+            dx1 = S.last_dx()
     pg, lg = S.get_state()
     S.close()
-    return out, (pg, lg), (po, lo), Q
+    return np.array(chis), dx1, pg, lg
 
 
 @pytest.mark.timeout(900)
 def test_c3_gn_fp64_schur_matches_oracle(world):
-    out, (pg, lg), (po, lo), _ = run_pair(world, bos.BOS_FP64, 20)
-    worst = 0.0
-    for chig, chio, dxg, dxo in out:
-        worst = max(worst, abs(chig - chio) / chio)
-        assert abs(chig - chio) <= 1e-9 * chio, (chig, chio)
-    _, _, dxg, dxo = out[0]
+    chio, dxo, po, lo = oracle_run(world, 64, 20)
+    chig, dxg, pg, lg = hip_run(world, bos.BOS_FP64, 20)
+    worst = float(np.max(np.abs(chig - chio) / chio))
     e = np.abs(dxg - dxo).max() / np.abs(dxo).max()
     print(f"c3 fp64: chi2 worst rel err over 20 iterations {worst:.3g}; dx(1) rel err {e:.3g}")
+    assert worst <= 1e-9
     assert e <= 1e-8
     ok, ep, el = close_state(pg, lg, po, lo, rtol=1e-6, atol=1e-9)
     print(f"c3 fp64 after 20 iterations: state max abs err poses {ep:.3g} landmarks {el:.3g}")
@@ -105,36 +129,46 @@ def fp32_state_errors(P, pg, lg, po, lo):
     return np.abs(dp).max(), np.quantile(db, 0.999), db.max()
 
 
-@pytest.mark.timeout(900)
-def test_c3_gn_fp32_jh_schur_matches_oracle(world):
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("lpp", [1, 2])
+def test_c3_gn_fp32_jh_schur_matches_oracle(world, oracle_fp32, lpp):
     """The benchmarked configuration (fp32 J+H, fp64 Schur multifrontal solve, fp64 state) against
-    the oracle's fp32 J+H + fp64 solve and state, 10 iterations. Poses are compared in absolute
-    terms, landmarks through the bearing each observation predicts (a
-    landmark seen twice from a short baseline is weakly determined along its ray).
-
-    The tolerance is calibrated by fp32 itself: the oracle's fp32 path and its fp64 path differ by
-    1.2e-2 in the poses and 1.4e-4 rad (p99.9) in the predicted bearings on this world after 2
-    iterations (one 2-observation landmark flips sides of its poses: 3 rad at the worst bearing).
-    The HIP fp32 path must stay closer to the oracle's fp32 path than that in the poses, within twice
-    that spread in the bearings' p99.9, below that spread's maximum bearing difference, and within
-    fixed bounds: poses 5e-4, bearings p99.9 1e-4 and max 1e-2 rad (the maximum is one weakly
-    determined landmark whose fp32 rounding drifts along its ray). Measured after 10 iterations: HIP
-    vs oracle fp32 poses 1.2e-4 - 2.3e-4, bearings p99.9 5.2e-5 - 5.5e-5, max 2.9e-3 - 7.2e-3; oracle
-    fp32 vs fp64 poses 3.8e-3, bearings p99.9 4.1e-5, max 1.3e-2."""
-    iters = 10
-    out, (pg, lg), (po, lo), Q = run_pair(world, bos.BOS_FP32, iters)
-    for chig, chio, _, _ in out:
-        assert abs(chig - chio) <= 1e-3 * chio, (chig, chio)
+    the oracle's fp32 J+H + fp64 solve and state over the bench's 50 iterations, with lanes_per_pose
+    1 (bench.py at N = 1) and 2 (bench.py at N > 1). Poses are compared in absolute terms, landmarks
+    through the bearing each observation predicts."""
+    chio, dxo, po, lo = oracle_fp32
+    chig, dxg, pg, lg = hip_run(world, bos.BOS_FP32, FP32_ITERS, lanes_per_pose=lpp)
+    worst = float(np.max(np.abs(chig - chio) / chio))
+    e1 = np.abs(dxg - dxo).max() / np.abs(dxo).max()
     ep, eq, eb = fp32_state_errors(world, pg, lg, po, lo)
-    Q64 = to_oracle(world)
-    p64, l64 = Q64.copy_state()
-    for _ in range(iters):
-        oracle_step(Q64, p64, l64, 64)
-    rp, rq, rb = fp32_state_errors(world, po, lo, p64, l64)
-    print(f"c3 fp32 after {iters} iterations, HIP vs oracle fp32 J+H: pose {ep:.3g}, bearing p99.9 {eq:.3g} "
-          f"max {eb:.3g} rad; oracle fp32 vs fp64: pose {rp:.3g}, bearing p99.9 {rq:.3g} max {rb:.3g}")
-    assert ep <= 5e-4 and eq <= 1e-4 and eb <= 1e-2
-    assert ep < rp and eq < 2 * rq and eb < rb
+    print(f"c3 fp32 lpp={lpp} after {FP32_ITERS} iterations, HIP vs oracle fp32 J+H: chi2 worst rel {worst:.3g}, "
+          f"dx(1) rel {e1:.3g}, pose {ep:.3g}, bearing p99.9 {eq:.3g} max {eb:.3g} rad")
+    assert worst <= 1e-4
+    assert ep <= 1e-4 and eq <= 1e-5 and eb <= 1e-4
+    assert np.array_equal(pg[world.fixed], world.pose_xyt[world.fixed])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("lpp", [1, 2])
+def test_c3_fp32_converges_without_pivot_failures(world, lpp):
+    """200 GN iterations of the benchmarked fp32 path from the initial guess (four times the bench's
+    batch): every step positive definite (solver_info == 0), the state finite, and chi^2 flat, as GN
+    on the reference dataset is by iteration 20 (README.md:22-24): from iteration 20 on every chi^2
+    within 1e-4 relative of the last one."""
+    S = bos.Solver(world, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=lpp)
+    chis = []
+    for i in range(200):
+        st = S.step()
+        assert st["solver_info"] == 0, (i, st)
+        chis.append(st["chi2"])
+    pg, lg = S.get_state()
+    S.close()
+    chis = np.array(chis)
+    assert np.all(np.isfinite(pg)) and np.all(np.isfinite(lg))
+    spread = np.abs(chis[19:] - chis[-1]).max() / chis[-1]
+    print(f"lpp={lpp}: chi2 {chis[0]:.6g} -> {chis[9]:.6g} (10) -> {chis[19]:.6g} (20) -> {chis[-1]:.6g} (200); "
+          f"spread from 20 on {spread:.3g}")
+    assert spread <= 1e-4
 
 
 def test_c3_fp32_reports_non_positive_pivots():

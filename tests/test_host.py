@@ -129,6 +129,41 @@ def test_synthetic_world_properties():
         bos.synthetic(10, 100, 2)
 
 
+def ray_parallax(P):
+    """Per landmark: the spread (rad) of the world-frame ray angles from its observing poses, at
+    ground truth."""
+    gp, gl = P.gt_pose_xyt, P.gt_lm_xy
+    bp, bl = P.b_pose, P.b_lm
+    ang = np.arctan2(gl[bl, 1] - gp[bp, 1], gl[bl, 0] - gp[bp, 0])
+    ref = np.zeros(P.NL)
+    ref[bl[::-1]] = ang[::-1]   # the first observation's ray
+    d = (ang - ref[bl] + np.pi) % (2 * np.pi) - np.pi
+    lo = np.zeros(P.NL)
+    hi = np.zeros(P.NL)
+    np.minimum.at(lo, bl, d)
+    np.maximum.at(hi, bl, d)
+    return hi - lo
+
+
+@pytest.mark.parametrize("size", [(1000, 2000, 20, 0xB05EED01 + 2), (100000, 200000, 10, 0xB05EED01 + 3)])
+def test_synthetic_world_parallax(size):
+    """every landmark observed >= 2 times with parallax. The generator guarantees a
+    ray spread >= 20 deg (csrc/host/synthetic.cpp), and every bearing is in front of its pose
+    (|bearing| < 85 deg) — the property that makes GN converge on the benchmark world (the old
+    generator's 0.8 deg tail never did)."""
+    P = bos.synthetic(*size)
+    par = ray_parallax(P)
+    assert np.bincount(P.b_lm, minlength=P.NL).min() >= 2
+    assert par.min() >= np.radians(20.0) * (1 - 1e-12), np.degrees(par.min())
+    g = P.gt_pose_xyt[P.b_pose]
+    l = P.gt_lm_xy[P.b_lm]
+    c, s = np.cos(g[:, 2]), np.sin(g[:, 2])
+    dx, dy = l[:, 0] - g[:, 0], l[:, 1] - g[:, 1]
+    bearing = np.arctan2(-s * dx + c * dy, c * dx + s * dy)
+    assert np.abs(bearing).max() < np.radians(85.0)
+    assert np.hypot(dx, dy).min() > 0.5
+
+
 @pytest.mark.parametrize("which", ["mini", "c1", "c2"])
 def test_plan_pattern_matches_oracle(which):
     P = {"mini": lambda: bos.load_g2o(MINI), "c1": lambda: bos.load_g2o(C1),

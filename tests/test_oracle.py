@@ -43,6 +43,37 @@ def test_normalized_angle_half_open():
     assert O.normalized_angle(float(f_pi), 32) < 0
 
 
+@pytest.mark.parametrize("precision", [32, 64])
+def test_normalized_angle_huge_and_non_finite(precision):
+    """the reference's while loops (slam/solver_jacobians.cpp:325-333) never end for an
+    infinite angle or one whose ulp exceeds 2 pi; a diverged iteration (dx ~ 1e150 from a clamped
+    non-positive pivot) reaches them through the box-plus. The product (bos_math.hpp, exported as
+    bos_normalized_angle_*) and the oracle return NaN there, and land in [-pi, pi) for every angle
+    whose remainder is still defined (a NaN or an in-range value past that); |a| <= 1e6 is the
+    reference's loop exactly, and the two agree there."""
+    import bos
+    L = bos.lib()
+    prod = L.bos_normalized_angle_f32 if precision == 32 else L.bos_normalized_angle_f64
+    cast = (lambda v: float(np.float32(v))) if precision == 32 else float
+    for a in (1e30, -1e30, 1e150, -1e150, 3e38, 1e17, math.inf, -math.inf, math.nan):
+        if precision == 32 and abs(a) > 3.4e38 and math.isfinite(a):
+            continue
+        for f in (prod, lambda v: O.normalized_angle(v, precision)):
+            r = f(cast(a))
+            # no angle is left in such an a: NaN, or a value in range (the loops ended)
+            assert math.isnan(r) or (math.isfinite(a) and -PI <= r < PI), (a, r)
+            if not math.isfinite(a):
+                assert math.isnan(r), (a, r)
+    for a in (7.0, -7.0, 123456.7, 1e6, -1e6, 1.5e6, 1e9, -3.3e12, 1e14):
+        a = cast(a)
+        r, o = prod(a), O.normalized_angle(a, precision)
+        assert -PI <= r < PI and -PI <= o < PI, (a, r, o)
+        if precision == 64:   # (fp32: the reference's loop rounds every +-2 pi step to float)
+            assert abs(math.remainder(r - a, 2 * PI)) <= 1e-6 * max(1.0, abs(a)), (a, r)
+        if abs(a) <= 1e6:
+            assert r == o, (a, r, o)
+
+
 def test_smallest_angle():
     assert O.smallest_angle(0.5) == 0.5
     assert O.smallest_angle(7.0) == pytest.approx(7.0 - 2 * PI)
@@ -183,6 +214,18 @@ def test_golden_crosscheck(golden):
         for it in (50,):
             assert np.abs(X - g[f"X{it}"]).max() < 1e-8
             assert np.abs(L - g[f"L{it}"]).max() < 1e-8
+
+
+def test_reduced_system_csc_equals_reduced_system():
+    """The cached scatter assembly the C3 GN tests use equals assemble_H + reduced_system (C1)."""
+    P = O.load(C1)
+    for it in range(2):
+        lin = O.linearize(P)
+        A, b, idx = O.reduced_system(P, O.assemble_H(P, lin), lin.b)
+        B, b2, idx2 = O.reduced_system_csc(P, lin)
+        assert np.array_equal(idx, idx2) and np.array_equal(b, b2)
+        assert abs(A.tocsc() - B).max() <= 1e-15 * abs(A).max()
+        O.apply_boxplus(P, P.pose_xyt, P.lm_xy, O.solve_dx(P, O.assemble_H(P, lin), lin.b))
 
 
 def test_convergence_pins(c1):

@@ -1,4 +1,4 @@
-# A/B of libbos.so build variants (tools/build_jh_variants.sh) with tools/jh_variant_timing.py, in
+# A/B of libbos.so build variants (tools/build_full_variant.sh) with tools/jh_variant_timing.py, in
 # alternating processes, two rounds; results appended to gpurun_out/$1.txt.
 # Usage: tools/gpu_ab_jh.sh <out-name> variant1 variant2 ...
 set -o pipefail
