@@ -192,10 +192,13 @@ def free_port():
         return sk.getsockname()[1]
 
 
-def launch_ranks(n):
+def launch_ranks(n, deadline_s=1800.0):
     """No launcher but --gpus N > 1: start N rank processes of this script (one per GPU, env as
     torch.distributed.run sets it), relay rank 0's JSON line, exit with the worst exit code. Runs
-    before anything in this process touches HIP."""
+    before anything in this process touches HIP. Every rank is polled against one deadline: as soon
+    as any rank exits non-zero (or the deadline passes) the others are killed, so a rank that dies
+    before the rendezvous cannot leave the rest waiting forever."""
+    import threading
     port = free_port()
     procs = []
     for r in range(n):
@@ -203,22 +206,34 @@ def launch_ranks(n):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out = procs[0].communicate()[0]
-    rcs = [procs[0].returncode]
-    for p in procs[1:]:
-        try:
-            rcs.append(p.wait(timeout=600))
-        except subprocess.TimeoutExpired:
-            p.kill()
-            rcs.append(p.wait())
-    for ln in (out or b"").decode(errors="replace").splitlines():
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    t_end = time.monotonic() + deadline_s
+    failed = False
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        if any(rc not in (None, 0) for rc in rcs) or time.monotonic() > t_end:
+            failed = True
+            break
+        time.sleep(0.2)
+    own = [rc for rc in rcs if rc not in (None, 0)]   # ranks that failed by themselves
+    if failed:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    rcs = [p.wait() for p in procs]
+    reader.join(timeout=10)
+    for ln in (out[0] if out else b"").decode(errors="replace").splitlines():
         # the JSON line to stdout; anything else rank 0's libraries printed there (gloo's connection
         # notice) to stderr
         (sys.stdout if ln.startswith("{") else sys.stderr).write(ln + "\n")
     sys.stdout.flush()
-    bad = [rc for rc in rcs if rc != 0]
+    bad = own + [rc for rc in rcs if rc != 0]
     if bad:
-        log(f"launcher: rank exit codes {rcs}")
+        log(f"launcher: rank exit codes {rcs}" + (" (killed after a failure or the deadline)" if failed else ""))
     return bad[0] if bad else 0
 
 
@@ -242,6 +257,8 @@ def main():
     ap.add_argument("--check-launch", action="store_true",
                     help="launch / rendezvous check only (no GPU): every rank joins the gloo group, rank 0 prints "
                          "the ranks seen")
+    ap.add_argument("--check-launch-fail-rank", type=int, default=-1,
+                    help="with --check-launch: this rank exits 5 before the rendezvous (tests the launcher)")
     ap.add_argument("--solver", choices=["supernodal", "schur"], default="schur",
                     help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
                          "nested-dissection multifrontal; the other one is timed too (gn_other)")
@@ -265,6 +282,8 @@ def main():
 
     if args.check_launch:   # the rank processes and their rendezvous, nothing else (tests/test_bench.py)
         seen = 1
+        if rank == args.check_launch_fail_rank:
+            sys.exit(5)
         if world > 1:
             import torch
             import torch.distributed as dist

@@ -742,6 +742,10 @@ __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const doub
     if (mirror) *mirror = *out;
 }
 
+// a J+H launch with no blocks (a rank with an empty share of the observations partition) still
+// stamps its start, so the phase times of that rank read 0 rather than a stale stamp
+__global__ void stamp_kernel(unsigned long long* t) { *t = __builtin_amdgcn_s_memrealtime(); }
+
 __global__ __launch_bounds__(256) void cache_scrub_kernel(const double* buf, int64_t n, double* sink) {
     double acc = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -859,7 +863,10 @@ hipError_t launch_lin_k(LinParams<T> p, hipStream_t s) {
         p.lm_b0 + p.n_lm_run > lm_blocks)
         return hipErrorInvalidValue;   // a block range outside the build (checked before any launch)
     const int grid = (p.n_pose_run + p.n_lm_run) * kJhSub;
-    if (grid == 0) return hipSuccess;
+    if (grid == 0) {
+        if (p.t_start) hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, s, p.t_start);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((linearize_kernel<T, W, D, LPP, MINW>), dim3(grid), dim3(kJhWg), 0, s, p);
     return hipGetLastError();
 }

@@ -660,9 +660,7 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     }
     // lanes per pose and their bearing segments (lane 0 also takes the odometry entries; a run of
     // duplicate observations of one pair never straddles two lanes)
-    const double avg = NP ? (double)Mb / NP : 0.0;
-    // measured on config 3 (K = 10): 1 lane per pose beats 2 and 4 (bos_options.lanes_per_pose forces it)
-    B.lpp = pi.lpp > 0 ? pi.lpp : avg >= 32 ? 2 : 1;
+    B.lpp = plan_lanes_per_pose(pi);
     if (B.lpp != 1 && B.lpp != 2 && B.lpp != 4) { err = "lanes per pose must be 1, 2 or 4"; return BOS_ERR_INVALID; }
     const int L = B.lpp;
     auto same_lm = [&](int i, int j) { return pi.b_lm[pb_obs[i]] == pi.b_lm[pb_obs[j]]; };

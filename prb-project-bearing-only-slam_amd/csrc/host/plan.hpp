@@ -32,6 +32,13 @@ struct ProblemIndex {
 
 // J+H launch geometry shared by the host plan and the kernel (hip/kernels.hpp kBlock)
 constexpr int kJhBlock = 256;
+// J+H lanes per pose: bos_options.lanes_per_pose when set, else 2 from 32 bearings per pose on and
+// 1 below (measured on config 3, K = 10: 1 lane per pose beats 2 and 4). build_layout and
+// build_shard both use this.
+inline int plan_lanes_per_pose(const ProblemIndex& pi) {
+    const double avg = pi.NP ? (double)pi.Mb / pi.NP : 0.0;
+    return pi.lpp > 0 ? pi.lpp : avg >= 32 ? 2 : 1;
+}
 // Contiguous share [a, b) of n items for rank r of W (BOS_PARTITION_OBSERVATIONS: each rank runs a
 // range of the J+H's pose blocks and one of its landmark blocks, i.e. of the observations in
 // measurement order)

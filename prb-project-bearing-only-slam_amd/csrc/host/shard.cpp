@@ -120,13 +120,17 @@ int build_shard(const ProblemIndex& pi, Plan& P, int rank, int world, std::strin
     }
     // J+H lanes: own poses, padded to a whole J+H block (chi^2 partials of own lanes and of top
     // lanes fall in different blocks), then the top poses and the fixed pose
-    const int lpp = (NP && (double)pi.Mb / NP >= 32) ? 2 : 1;   // as build_layout
+    const int lpp = plan_lanes_per_pose(pi);   // as build_layout
     const int poses_per_block = kJhBlock / lpp;
     for (int p = 0; p < NP; ++p)
         if (S.node_owner[p] == rank) S.lane_poses.push_back(p);
     if (world > 1)
         while (S.lane_poses.size() % poses_per_block) S.lane_poses.push_back(-1);
     S.own_pose_lanes = (int)S.lane_poses.size();
+    if (world > 1 && ((int64_t)S.own_pose_lanes * lpp) % kJhBlock) {   // ranks != 0 count whole own blocks
+        err = "shard: own pose lanes not a whole number of J+H blocks";
+        return BOS_ERR_INVALID;
+    }
     for (int p = 0; p < NP; ++p)
         if (S.node_owner[p] < 0) S.lane_poses.push_back(p);
     for (int l = 0; l < NL; ++l)

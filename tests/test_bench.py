@@ -34,3 +34,14 @@ def test_bench_refuses_a_wrong_world_size():
                                              MASTER_PORT="29512"))
     assert r.returncode == 2
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_launcher_stops_when_a_rank_dies():
+    """a rank that dies before the rendezvous must not leave rank 0 waiting for it; the
+    launcher kills the others and exits with the failed rank's code."""
+    import time
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--check-launch", "--check-launch-fail-rank", "1"],
+                       capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 5, (r.returncode, r.stderr[-2000:])
+    assert time.monotonic() - t0 < 200

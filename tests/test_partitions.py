@@ -50,6 +50,18 @@ def test_observation_ranges_cover_every_entry_once(world, which):
     assert info["nnz_lower"] == one["nnz_lower"] and info["n"] == one["n"]
 
 
+@pytest.mark.parametrize("lpp", [1, 2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_subtree_shard_own_lanes_fill_whole_blocks(world, lpp):
+    """every rank's own pose lanes (lanes per pose forced, on a world whose default
+    would be two) are a whole number of J+H blocks, so ranks != 0 count every own block's chi^2."""
+    P = bos.synthetic(300, 3000, 40, seed=11)
+    for r in range(world):
+        info = bos.plan_inspect(P, r, world, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=lpp)
+        assert info["lanes_per_pose"] == lpp
+        assert info["shard_own_pose_lanes"] * lpp % 256 == 0, (r, info["shard_own_pose_lanes"])
+
+
 def _obs_plan_worker(rank, world, port, q):
     try:
         import sys

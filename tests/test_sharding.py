@@ -199,6 +199,26 @@ def test_sharded_step_two_lanes_per_pose(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lpp", [1, 4])
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_dense_world_forced_lanes(world, lpp):
+    """a world with >= 32 bearings per pose (the plan's default is then two lanes per
+    pose) with the lanes forced to 1 or 4: the shard's own pose lanes must still fill whole J+H
+    blocks, or the block mixing a rank's last own poses with top poses loses their chi^2 on ranks
+    != 0. chi^2 and robust counts equal the one-GPU step's."""
+    import bos
+    P = bos.synthetic(300, 3000, 40, seed=11)
+    (pm, lm_), stats, states, owner, info = _run_local_shards(P, world, 3, bos.BOS_FP64, lpp=lpp)
+    (p1, l1), st1 = _run_one(P, 3, bos.BOS_FP64, lpp=lpp)
+    assert all(i["lanes_per_pose"] == lpp for i in info)
+    assert np.array_equal(pm, p1) and np.array_equal(lm_, l1)
+    for it in range(3):
+        for r in range(world):
+            assert abs(stats[it][r]["chi2"] - st1[it]["chi2"]) <= 1e-12 * st1[it]["chi2"], (it, r)
+            assert stats[it][r]["n_robust"] == st1[it]["n_robust"]
+
+
+@pytest.mark.gpu
 def test_rccl_one_rank_sharded_path():
     """world 1 with a communicator: the sharded phases and their RCCL all-gathers (one rank) equal
     the plain step bit for bit."""
