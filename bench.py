@@ -3,9 +3,9 @@
 
 A *step* is one Gauss-Newton iteration of the reference's Solver::step (slam/solver.cpp:27-97) over
 the whole synthetic config-3 world (100k poses / 200k landmarks / 1M bearings / 99 999 odometry
-edges), inputs resident in HBM. The timed region is K such steps (synchronous bos_step calls,
-restarting from the initial guess every 50 steps outside the timed region: each run times iterations
-1..50 of the solve, the reference UI's batch). ``value`` = observations (bearings + odometry edges)
+edges), inputs resident in HBM. The timed region is K such steps (synchronous bos_step calls) from the
+initial guess, iterations 1..K of the solve (default 50, the reference UI's batch; the world converges,
+so any K runs positive definite). ``value`` = observations (bearings + odometry edges)
 per second of the J+H build *as it runs inside those steps* (device realtime stamps written by the
 step's own kernels, median over the K steps, the slowest rank); ``ms_per_step`` is that J+H time
 (= roofline.kernel_ms). The steps' wall rate is ``gn_iters_per_s``.
@@ -167,23 +167,39 @@ def solver_model(P, phase, world):
             "frac_of_chain_bound": t_chain / t_solve_us, "frac_of_bytes_bound": t_bytes / t_solve_us}
 
 
-PROFILE_TAG = "r03"   # profiles/<tag>_pmc_linearize_<prec>_<mode>.json, written by tools/pmc_summary.py
+PROFILE_TAG = "r04"   # profiles/<tag>_pmc_linearize_<prec>_<mode>.json, written by tools/pmc_summary.py
 
 
-def traffic_from_profile(precision):
+def lib_sha256():
+    import hashlib
+    with open(bos.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def traffic_from_profile(precision, profiles_dir=None):
     """Fabric bytes per launch of the J+H kernel from the committed rocprofv3 PMC summaries
     (L2 <-> fabric requests by size, tools/gpu_profile.sh): the in-step launches of the timed GN steps
-    ("instep") and back-to-back builds ("warm")."""
-    out = {}
+    ("instep") and back-to-back builds ("warm"). A summary counts only if it was taken with the very
+    libbos.so this process loaded (its libbos_sha256): counters of another build are not this line's
+    traffic, so the value is then None and the reason is returned beside it."""
+    out, why = {}, {}
+    mine = lib_sha256()
     for label in ("instep", "warm"):
         name = f"{PROFILE_TAG}_pmc_linearize_" + ("fp32" if precision == bos.BOS_FP32 else "fp64") + f"_{label}.json"
-        path = os.path.join(ROOT, "profiles", name)
+        path = os.path.join(profiles_dir or os.path.join(ROOT, "profiles"), name)
+        out[label] = None
         try:
             with open(path) as f:
-                out[label] = float(json.load(f)["hbm_bytes_per_launch"])
-        except (OSError, ValueError, KeyError):
-            out[label] = None
-    return out
+                d = json.load(f)
+        except (OSError, ValueError):
+            why[label] = f"no profiles/{name}"
+            continue
+        if d.get("libbos_sha256") != mine:
+            why[label] = f"profiles/{name} was taken with another libbos.so build"
+            continue
+        out[label] = float(d["hbm_bytes_per_launch"])
+        why[label] = f"profiles/{name} (rocprofv3 --pmc of this libbos.so build)"
+    return out, why
 
 
 def free_port():
@@ -240,7 +256,7 @@ def launch_ranks(n, deadline_s=1800.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50, help="GN iterations timed (restart from the initial guess every 50)")
+    ap.add_argument("--steps", type=int, default=50, help="GN iterations timed (from the initial guess)")
     ap.add_argument("--warmup", type=int, default=5, help="untimed GN iterations before the timed ones")
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--replay-steps", type=int, default=200, help="J+H builds back to back (warm-replay roofline)")
@@ -263,11 +279,8 @@ def main():
                     help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
                          "nested-dissection multifrontal; the other one is timed too (gn_other)")
     ap.add_argument("--lanes-per-pose", type=int, default=0, choices=[0, 1, 2, 4],
-                    help="J+H lanes per pose (bos_options.lanes_per_pose); 0 = by the ranks: 1 on one GPU, 2 for "
-                         "N > 1 (a rank's share of the lanes leaves the GPU room for shorter lanes: per-rank J+H at "
-                         "N = 4 / 8 11 us with 2 lanes against 13 us with 1; 4 lanes, 9 us at N = 8, make this fp32 "
-                         "trajectory hit a non-positive pivot at iteration 44, inside the timed window; "
-                         "profiles/r03_shard_lanes_per_pose.txt)")
+                    help="J+H lanes per pose (bos_options.lanes_per_pose); 0 = the plan's rule (1 at config 3), "
+                         "the same at every N so that the scaling curve compares the same arithmetic")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -335,7 +348,7 @@ def main():
     device = 0 if args.same_device else local_rank
     solver = bos.BOS_SOLVER_SCHUR if args.solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
 
-    lpp = args.lanes_per_pose or (1 if world == 1 else 2)
+    lpp = args.lanes_per_pose
 
     def make_handle(partition):
         nccl_id = None
@@ -385,28 +398,26 @@ def main():
         return h.step_phase(2)
 
     def timed_steps(h, partition, k, warmup):
-        """k GN iterations in chunks of <= 50 from the initial guess (restart outside the timed
-        region), after `warmup` untimed ones: (wall seconds of the timed steps, max over ranks;
-        per-step stats)."""
+        """`warmup` untimed GN iterations, then the state reset to the initial guess (outside the
+        timed region) and k GN iterations from it, timed as one region: iterations 1..k of the solve
+        (the world converges; tests/test_gpu_c3_gn.py checks 200 fp32 iterations positive definite).
+        Returns (wall seconds of the timed steps, max over ranks; per-step stats)."""
         init = h.get_state()
         for _ in range(warmup):
             gn_step(h, partition)
-        stats, wall, done = [], 0.0, 0
-        while done < k:
-            n = min(50, k - done)
-            h.set_state(*init)
-            h.synchronize()
-            barrier()
-            h.synchronize()
-            t0 = time.perf_counter()
-            stats += [gn_step(h, partition) for _ in range(n)]
-            h.synchronize()
-            barrier()
-            h.synchronize()
-            wall += max_over_ranks(time.perf_counter() - t0)
-            done += n
         h.set_state(*init)
-        assert all(g["solver_info"] == 0 for g in stats), "non-positive pivot in a benchmarked GN step"
+        h.synchronize()
+        barrier()
+        h.synchronize()
+        t0 = time.perf_counter()
+        stats = [gn_step(h, partition) for _ in range(k)]
+        h.synchronize()
+        barrier()
+        h.synchronize()
+        wall = max_over_ranks(time.perf_counter() - t0)
+        h.set_state(*init)
+        bad = [i + 1 for i, g in enumerate(stats) if g["solver_info"] != 0]
+        assert not bad, f"non-positive pivot or stall in benchmarked GN iterations {bad[:5]}"
         return wall, stats
 
     def phases(stats):
@@ -491,12 +502,14 @@ def main():
     if rank == 0:
         algo = info["algorithmic_bytes"]
         layout = info["layout_bytes"]
-        traffic = traffic_from_profile(precision) if world == 1 else None
+        traffic, traffic_src = traffic_from_profile(precision) if world == 1 else (None, None)
 
         def roof(ms, label, timing):
             a = algo / (ms * 1e-3) / 1e9
             return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
                     "traffic": traffic.get("warm" if label == "warm" else "instep") if traffic else None,
+                    "traffic_source": traffic_src.get("warm" if label == "warm" else "instep") if traffic_src else
+                    "not collected for N > 1",
                     "algorithmic_bytes_per_launch": algo, "kernel_ms": ms, "caches": label, "timing": timing,
                     # the bytes this layout moves at minimum (pose-landmark blocks stored as 3 factors
                     # when pl_factored) and the fraction of the roofline on those
@@ -549,6 +562,7 @@ def main():
             "roofline": r_instep or r_warm,
             "roofline_cold_events": r_cold,
             "roofline_warm_replay": r_warm,
+            "libbos_sha256": lib_sha256(),
         }
         if world == 1 and not args.no_cpu_baseline:
             cpus = host_cpus()

@@ -45,3 +45,21 @@ def test_bench_launcher_stops_when_a_rank_dies():
                        capture_output=True, text=True, timeout=240, env=_env())
     assert r.returncode == 5, (r.returncode, r.stderr[-2000:])
     assert time.monotonic() - t0 < 200
+
+
+def test_traffic_only_from_a_profile_of_this_build(tmp_path):
+    """roofline.traffic is read from a committed PMC summary only when that summary was
+    taken with the libbos.so this process loaded (its sha256); otherwise it is null."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import bos
+    bench.bos = bos
+    mine = bench.lib_sha256()
+    for label, sha in (("instep", mine), ("warm", "0" * 64)):
+        with open(tmp_path / f"{bench.PROFILE_TAG}_pmc_linearize_fp32_{label}.json", "w") as f:
+            json.dump({"hbm_bytes_per_launch": 123.0, "libbos_sha256": sha}, f)
+    t, why = bench.traffic_from_profile(bos.BOS_FP32, str(tmp_path))
+    assert t == {"instep": 123.0, "warm": None}
+    assert "another libbos.so" in why["warm"]
+    t, why = bench.traffic_from_profile(bos.BOS_FP64, str(tmp_path))
+    assert t == {"instep": None, "warm": None}

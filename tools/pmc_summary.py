@@ -10,10 +10,21 @@ sum(size x count) -- this sidesteps FETCH_SIZE's 64-B tally of 128-B requests on
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import statistics
 import sys
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "prb-project-bearing-only-slam_amd",
+                   "lib", "libbos.so")
+
+
+def lib_sha256(path=LIB):
+    """Hash of the libbos.so the profiled runs loaded (bench.py reports a profile's traffic only for
+    the same build)."""
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 
 def load(d, regex="linearize"):
@@ -69,6 +80,7 @@ def main():
                   "SQ cycle counters in quad-cycles summed over waves",
         "algorithmic_bytes_per_launch": algo,
         "traffic_over_algorithmic": (read_bytes + write_bytes) / algo,
+        "libbos_sha256": lib_sha256(),
     })
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
