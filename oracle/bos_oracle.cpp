@@ -31,8 +31,10 @@
 // The one libm substitute shared with the product: a portable atan2 (fdlibm-style reduction,
 // plain IEEE operations; <= 1 ulp vs glibc, tests/test_oracle.py). Bearings whose error sits on
 // the +-pi wrap (the reference's single-observation landmarks) flip sign on a last-ulp difference
-// of atan2, so the oracle and the GPU path must round identically there. This file is compiled
-// with -ffp-contract=off for the same reason.
+// of atan2, so for the reference dataset the oracle and the GPU path must round identically. It is
+// used only in the bit-reproducing form (bearing_g below); the literal form (oracle_set_literal)
+// uses libm's atan2 and Eigen's product sums and shares no code with the product — the synthetic
+// worlds' parity tests run in it. This file is compiled with -ffp-contract=off.
 #include "../prb-project-bearing-only-slam_amd/csrc/host/det_atan2.hpp"
 
 namespace {
@@ -71,22 +73,41 @@ template <typename T> inline T smallest_angle(T a) {
 
 template <typename T> struct PoseT { T x, y, th; };
 
-// Solver::predict_bearing — slam/solver_jacobians.cpp:301-305: g = X^-1 * l,
-// Isometry inverse = (R^T, -R^T t) so g = R^T l + (-R^T t); bearing = atan2(g.y, g.x).
+// Two evaluations of the bearing prediction g = X^-1 l and its atan2:
+//  * literal (oracle_set_literal(1)): Eigen's `pose.inverse() * lm` as the reference writes it
+//    (slam/solver_jacobians.cpp:32, :302): Isometry inverse (R^T, -R^T t), each row a plain
+//    product sum (this file is compiled without FP contraction), and libm atan2 (:15, :304). It
+//    shares nothing with the product's code, so the C2/C3 parity tests use it: their bearings are
+//    all in front of their poses (|bearing| < 85 deg), far from the +-pi wrap.
+//  * bit-reproducing (default): the rounding sequence of the GPU kernels (bos_math.hpp
+//    bearing_error, products summed with one explicit fma each) and the portable atan2 shared with
+//    them. The reference dataset's single-observation landmarks sit exactly on the +-pi wrap after
+//    triangulation, where the sign of e (and so b) flips on the last ulp of atan2: C1 and the mini
+//    dataset are compared in this mode.
+int g_literal = 0;
+
 template <typename T> inline void bearing_g(const PoseT<T>& p, T lx, T ly, T& gx, T& gy) {
     const T c = std::cos(p.th), s = std::sin(p.th);
-    // the same rounding sequence as the GPU kernels (bos_math.hpp bearing_error): products
-    // summed with one explicit fma each
+    if (g_literal) {
+        const T itx = -(c * p.x + s * p.y), ity = -(-s * p.x + c * p.y);   // -R^T t
+        gx = (c * lx + s * ly) + itx;                                          // R^T l + (-R^T t)
+        gy = (-s * lx + c * ly) + ity;
+        return;
+    }
     const T itx = -std::fma(c, p.x, s * p.y);
     const T ity = -std::fma(-s, p.x, c * p.y);
     gx = std::fma(c, lx, s * ly) + itx;
     gy = std::fma(-s, lx, c * ly) + ity;
 }
 
+template <typename T> inline T bearing_atan2(T gy, T gx) {
+    return g_literal ? std::atan2(gy, gx) : bos::det_atan2(gy, gx);
+}
+
 template <typename T> inline T predict_bearing(const PoseT<T>& p, T lx, T ly) {
     T gx, gy;
     bearing_g(p, lx, ly, gx, gy);
-    return bos::det_atan2(gy, gx);
+    return bearing_atan2(gy, gx);
 }
 
 // Bearing error_and_jacobian — slam/solver_jacobians.cpp:9-95.
@@ -95,7 +116,7 @@ template <typename T> inline T bearing_error_and_jacobian(const PoseT<T>& p, T l
     const T c = std::cos(p.th), s = std::sin(p.th);
     T gx, gy;
     bearing_g(p, lx, ly, gx, gy);
-    const T pred = bos::det_atan2(gy, gx);                             // :15, :301-305
+    const T pred = bearing_atan2(gy, gx);                              // :15, :301-305
     const T e = normalized_angle<T>(pred - z);                         // :18 (z already smallestAngle)
     const T f = (T)1 / (gx * gx + gy * gy);                            // :35
     const T a0 = f * (-gy), a1 = f * gx;                               // :47-48
@@ -515,6 +536,8 @@ extern "C" {
 // ABI version of this oracle, checked by oracle/oracle.py.
 int oracle_version(void) { return 4; }
 
+void oracle_set_literal(int on) { g_literal = on != 0; }
+int oracle_get_literal() { return g_literal; }
 double oracle_normalized_angle_f64(double a) { return normalized_angle<double>(a); }
 float oracle_normalized_angle_f32(float a) { return normalized_angle<float>(a); }
 double oracle_smallest_angle_f64(double a) { return smallest_angle<double>(a); }

@@ -58,6 +58,9 @@ def lib():
         fp = ctypes.POINTER(ctypes.c_float)
         ip = ctypes.POINTER(ctypes.c_int32)
         L.oracle_version.restype = ctypes.c_int
+        L.oracle_set_literal.restype = None
+        L.oracle_set_literal.argtypes = [ctypes.c_int]
+        L.oracle_get_literal.restype = ctypes.c_int
         L.oracle_normalized_angle_f64.restype = ctypes.c_double
         L.oracle_normalized_angle_f64.argtypes = [ctypes.c_double]
         L.oracle_normalized_angle_f32.restype = ctypes.c_float
@@ -118,6 +121,27 @@ def _pi(a):
 
 
 # ----------------------------------------------------------------------------------- angles
+def set_literal(on: bool) -> None:
+    """Bearing prediction evaluated as the reference writes it (Eigen's ``pose.inverse() * lm`` as
+    plain product sums, libm atan2; shares no code with the product) instead of the GPU kernels'
+    rounding sequence and portable atan2 (bos_oracle.cpp bearing_g). Use for worlds without
+    bearings on the +-pi wrap (the synthetic ones)."""
+    lib().oracle_set_literal(1 if on else 0)
+
+
+class literal:
+    """``with O.literal(): ...`` — set_literal(True) for the block, restored after."""
+
+    def __enter__(self):
+        self._was = lib().oracle_get_literal()
+        set_literal(True)
+        return self
+
+    def __exit__(self, *exc):
+        set_literal(bool(self._was))
+        return False
+
+
 def normalized_angle(a: float, precision: int = 64) -> float:
     """``Solver::normalized_angle`` (slam/solver_jacobians.cpp:325-333)."""
     if precision == 32:

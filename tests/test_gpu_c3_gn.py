@@ -60,7 +60,14 @@ def oracle_step(Q, pose, lm, jh_precision):
 
 
 def oracle_run(P, jh_precision, iters):
-    """(chi^2 per iteration, dx of iteration 1, final pose, final landmarks)."""
+    """(chi^2 per iteration, dx of iteration 1, final pose, final landmarks), with the oracle's
+    literal bearing evaluation (oracle.set_literal: Eigen's product sums and libm atan2, no code
+    shared with the product; every bearing of this world is in front of its pose)."""
+    with O.literal():
+        return _oracle_run(P, jh_precision, iters)
+
+
+def _oracle_run(P, jh_precision, iters):
     Q = to_oracle(P)
     po, lo = Q.copy_state()
     chis, dx1 = [], None

@@ -228,6 +228,22 @@ def test_reduced_system_csc_equals_reduced_system():
         O.apply_boxplus(P, P.pose_xyt, P.lm_xy, O.solve_dx(P, O.assemble_H(P, lin), lin.b))
 
 
+def test_literal_and_bit_reproducing_forms_agree():
+    """The oracle's two bearing evaluations (set_literal: Eigen's product sums + libm atan2, vs the
+    kernels' fma sequence + portable atan2) on a synthetic world with no bearing near the +-pi wrap:
+    fp64 H and b within 1e-13 relative, chi^2 within 1e-13."""
+    import bos
+    from helpers import to_oracle
+    P = to_oracle(bos.synthetic(1000, 2000, 20, 0xB05EED01 + 2))
+    a = O.linearize(P)
+    with O.literal():
+        b = O.linearize(P)
+    assert O.lib().oracle_get_literal() == 0
+    for x, y in ((a.b, b.b), (a.pose_diag, b.pose_diag), (a.lm_diag, b.lm_diag), (a.hpl, b.hpl)):
+        assert np.abs(x - y).max() <= 1e-13 * np.abs(x).max()
+    assert abs(a.chi2 - b.chi2) <= 1e-13 * a.chi2
+
+
 def test_convergence_pins(c1):
     """chi^2 before the robust kernel: 96.864254 at iteration 0 and 5.882761 at 49 (an
     independent survey-time restatement); ~20 iterations to converge (README)."""
