@@ -451,7 +451,9 @@ template <typename T> __global__ __launch_bounds__(kUpdateBlock) void boxplus_ke
     // solution, follows); nothing is written when the solver aborted
     const bool is_pose = i >= 0 && i < U.NP && i != U.fixed, is_lm = i >= U.NP && i < U.NP + U.NL;
     const int d = is_pose || is_lm ? U.node_dof[i] : 0;
-    const int32_t inf = U.info ? *U.info : 0;
+    int32_t inf = U.info ? *U.info : 0;
+    if (U.ex_hdr)
+        for (int q = 0; q < U.ex_world; ++q) inf |= (int32_t)U.ex_hdr[q * U.ex_stride] & kStepAbort;
     if (is_pose) {
         double x = U.pose[3 * i], y = U.pose[3 * i + 1], th = U.pose[3 * i + 2];
         const double dx = -U.x[d], dy = -U.x[d + 1], dth = -U.x[d + 2];
@@ -562,7 +564,7 @@ __global__ void reduce_stats_kernel(const double* chi_part, const int32_t* nrob_
             mirror->n_robust = v.n_robust;
             mirror->info = v.info;
             mirror->aborted = v.aborted;
-            for (int k = 0; k < 6; ++k) mirror->stamp[k] = v.stamp[k];
+            for (int k = 0; k < 8; ++k) mirror->stamp[k] = v.stamp[k];
             __threadfence_system();
             __hip_atomic_store(&mirror->seq, v.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -651,7 +653,8 @@ template <typename T> __global__ __launch_bounds__(256) void triangulate_kernel(
 
 // one segment per blockIdx.y, its elements grid-strided over blockIdx.x
 template <typename T>
-__global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* segs) {
+__global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* segs, unsigned long long* stamp) {
+    if (stamp && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
     const ExSeg g = segs[blockIdx.y];
     T* const base[4] = {val, b, send, recv};
     const T* src = base[g.src_kind] + g.src;
@@ -702,9 +705,11 @@ __global__ __launch_bounds__(256) void node_absmax_kernel(const double* x, const
 // block 0 thread 0: header (max of the partials, the solver word, which is then zeroed); every
 // thread: the boundary payload
 __global__ __launch_bounds__(256) void shard_pack2_kernel(const double* x, const double* part, int n_part, int32_t* info,
-                                                          const int32_t* bnd, int n_bnd, double* send2) {
+                                                          const int32_t* bnd, int n_bnd, double* send2,
+                                                          unsigned long long* stamp) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) {
+        if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
         double m = 0.0;
         for (int i = 0; i < n_part; ++i) m = nan_max(m, part[i]);
         send2[0] = m;
@@ -714,7 +719,9 @@ __global__ __launch_bounds__(256) void shard_pack2_kernel(const double* x, const
     for (int i = t; i < n_bnd; i += gridDim.x * blockDim.x) send2[2 + i] = x[bnd[i]];
 }
 
-__global__ void index_copy_kernel(const double* src, const int32_t* si, double* dst, const int32_t* di, int64_t n) {
+__global__ void index_copy_kernel(const double* src, const int32_t* si, double* dst, const int32_t* di, int64_t n,
+                                  unsigned long long* stamp) {
+    if (stamp && blockIdx.x == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         dst[di ? di[i] : i] = src[si ? si[i] : i];
 }
@@ -903,10 +910,15 @@ template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStr
 }
 
 template <typename T>
-hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s) {
-    if (nseg == 0 || max_len == 0) return hipSuccess;
+hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s,
+                           unsigned long long* stamp) {
+    if (nseg == 0 || max_len == 0) {
+        if (stamp) hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, s, stamp);
+        return hipGetLastError();
+    }
     const int64_t bx = std::min<int64_t>((max_len + 255) / 256, 256);
-    hipLaunchKernelGGL((seg_copy_kernel<T>), dim3((unsigned)bx, (unsigned)nseg), dim3(256), 0, s, val, b, send, recv, segs);
+    hipLaunchKernelGGL((seg_copy_kernel<T>), dim3((unsigned)bx, (unsigned)nseg), dim3(256), 0, s, val, b, send, recv, segs,
+                       stamp);
     return hipGetLastError();
 }
 
@@ -932,19 +944,22 @@ hipError_t launch_shard_header1(const double* chi_part, const int32_t* nrob_part
 
 hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes, const int32_t* node_dof, int NP,
                               int32_t* info, const int32_t* bnd, int n_bnd, double* part, double* send2,
-                              hipStream_t s) {
+                              hipStream_t s, unsigned long long* stamp) {
     const int nb = std::max(1, (n_nodes + 255) / 256);
     hipLaunchKernelGGL(node_absmax_kernel, dim3(nb), dim3(256), 0, s, x, nodes, n_nodes, node_dof, NP, part);
     const int pb = std::max(1, std::min(256, (n_bnd + 255) / 256));
-    hipLaunchKernelGGL(shard_pack2_kernel, dim3(pb), dim3(256), 0, s, x, part, nb, info, bnd, n_bnd, send2);
+    hipLaunchKernelGGL(shard_pack2_kernel, dim3(pb), dim3(256), 0, s, x, part, nb, info, bnd, n_bnd, send2, stamp);
     return hipGetLastError();
 }
 
 hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* dst, const int32_t* dst_idx, int64_t n,
-                             hipStream_t s) {
-    if (n == 0) return hipSuccess;
+                             hipStream_t s, unsigned long long* stamp) {
+    if (n == 0) {
+        if (stamp) hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, s, stamp);
+        return hipGetLastError();
+    }
     const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
-    hipLaunchKernelGGL(index_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, src_idx, dst, dst_idx, n);
+    hipLaunchKernelGGL(index_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, src_idx, dst, dst_idx, n, stamp);
     return hipGetLastError();
 }
 
@@ -1032,8 +1047,10 @@ template hipError_t launch_linearize<float>(const LinParams<float>&, int, bool, 
 template hipError_t launch_boxplus<double>(const UpdateParams<double>&, hipStream_t);
 template hipError_t launch_boxplus<float>(const UpdateParams<float>&, hipStream_t);
 template hipError_t launch_triangulate<double>(const TriParams<double>&, hipStream_t);
-template hipError_t launch_seg_copy<double>(double*, double*, double*, double*, const ExSeg*, int, int64_t, hipStream_t);
-template hipError_t launch_seg_copy<float>(float*, float*, float*, float*, const ExSeg*, int, int64_t, hipStream_t);
+template hipError_t launch_seg_copy<double>(double*, double*, double*, double*, const ExSeg*, int, int64_t, hipStream_t,
+                                            unsigned long long*);
+template hipError_t launch_seg_copy<float>(float*, float*, float*, float*, const ExSeg*, int, int64_t, hipStream_t,
+                                           unsigned long long*);
 template hipError_t launch_triangulate<float>(const TriParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);

@@ -92,6 +92,11 @@ template <typename T> struct UpdateParams {
     T* lc;
     double* max_part;         // [update blocks] max |dx| of each block (reduced by reduce_stats)
     const int32_t* info;      // solver status word or null; | kStepAbort => the update is skipped
+    // sharded step: every rank's exchange-2 header [max |x|, solver word] (ex_hdr[q * ex_stride],
+    // q < ex_world; null otherwise): any rank's abort bit skips the update
+    const double* ex_hdr;
+    int64_t ex_stride;
+    int ex_world;
     const int32_t* nodes;     // nodes to update (sharded: own, top, boundary), null = all NP + NL
     int n_nodes;
     unsigned long long* t_start;   // phase timing: block 0 writes the realtime clock at its start, or null
@@ -109,10 +114,12 @@ struct StepStatus {
     int32_t info;     // solver status: count of non-positive pivots, | kStepAbort (see above)
     int32_t aborted;  // sticky: kStepAbort once any step aborted; the host clears it when it reports it
     int32_t seq;      // steps summarised so far (reduce_stats); written to the host mirror last
-    // phase boundaries of the last step, realtime clock (100 MHz): J+H start, J+H end / solve start,
-    // solve end / update start, step end (written by the step's own kernels: no events in the step);
-    // BOS_PARTITION_OBSERVATIONS: [1] = J+H end (before the all-reduce), [4] = solve start (after it)
-    unsigned long long stamp[6];
+    // phase boundaries of the last step, realtime clock (100 MHz), written by the step's own kernels
+    // (no events in the step): [0] J+H start, [1] J+H end / solve start, [2] solve end / update
+    // start, [3] step end. BOS_PARTITION_OBSERVATIONS: [1] = J+H end (before the all-reduce), [4] =
+    // solve start (after it). BOS_PARTITION_SUBTREE: [4] exchange 1 start (phase 0 done), [5]
+    // exchange 1 end (phase 1 starts), [6] exchange 2 start, [7] exchange 2 end (phase 2 starts).
+    unsigned long long stamp[8];
 };
 constexpr double kStampMs = 1e-5;   // one realtime tick in ms
 
@@ -140,8 +147,10 @@ struct ExSeg {
     int32_t src_kind, dst_kind;
 };
 
+// *stamp (if set) gets the realtime clock at the launch's start
 template <typename T>
-hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s);
+hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s,
+                           unsigned long long* stamp = nullptr);
 
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);
@@ -160,10 +169,10 @@ template <typename T> hipError_t launch_from_f64(const double* in, T* out, int64
 // and the solver word *info (then zeroed for the next iteration); payload = x[bnd[i]].
 hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes, const int32_t* node_dof, int NP,
                               int32_t* info, const int32_t* bnd, int n_bnd, double* part, double* send2,
-                              hipStream_t s);
-// dst[dst_idx[i]] = src[src_idx[i]], i < n
+                              hipStream_t s, unsigned long long* stamp = nullptr);
+// dst[dst_idx[i]] = src[src_idx[i]], i < n; *stamp (if set) gets the realtime clock at the start
 hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* dst, const int32_t* dst_idx, int64_t n,
-                             hipStream_t s);
+                             hipStream_t s, unsigned long long* stamp = nullptr);
 // All ranks' headers -> *out (chi^2 and robust count summed in rank order plus the self-loop
 // terms, max |dx| the max, info: non-positive pivots summed, abort bits or-ed; `aborted` sticky
 // sticky), identical on every rank.

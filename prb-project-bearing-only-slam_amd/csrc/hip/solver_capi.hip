@@ -169,8 +169,13 @@ struct bos_solver {
     hipGraphExec_t graph_exec = nullptr;
     hipGraph_t graph_full = nullptr;     // the whole step (the steps of a batch before its last)
     hipGraphExec_t exec_full = nullptr;
-    hipGraph_t pgraph[3] = {};          // sharded step: one graph per phase
+    hipGraph_t pgraph[3] = {};          // sharded step, external exchanges: one graph per phase
     hipGraphExec_t pexec[3] = {};
+    // sharded step with a communicator: the whole iteration (phases and their RCCL collectives) as
+    // one graph; rccl_capture_failed: RCCL could not be captured, the phase graphs run instead
+    hipGraph_t sgraph = nullptr;
+    hipGraphExec_t sexec = nullptr;
+    bool rccl_capture_failed = false;
     bool graph_failed = false;   // capture not possible on this stream (e.g. the legacy null stream)
     // one GPU: the status sequence number last seen, and the status launches enqueued since (each
     // bumps the device counter once; wait_status polls for seq_seen + seq_pending)
@@ -230,7 +235,11 @@ template <typename T> bos::dev::UpdateParams<T> upd_params(const bos_solver* s) 
     u.pose = s->d_pose; u.lm = s->d_lm;
     u.pc = (T*)s->d_pc; u.pth = (T*)s->d_pth; u.lc = (T*)s->d_lc;
     u.max_part = s->d_maxpart;
-    u.info = s->sharded ? &s->d_status->info : uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : nullptr;
+    // sharded: the abort bits of every rank's exchange-2 header (the local word was moved into it)
+    u.info = s->sharded ? nullptr : uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : nullptr;
+    u.ex_hdr = s->sharded ? s->ex2_recv + 1 : nullptr;
+    u.ex_stride = s->ex2_count;
+    u.ex_world = s->world;
     u.nodes = s->sharded ? s->upd_nodes : nullptr;
     u.n_nodes = s->n_upd;
     u.t_start = nullptr;
@@ -549,15 +558,17 @@ int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr, bo
     return BOS_OK;
 }
 
-// ---- sharded GN iteration in three phases (exchanges between them). Each phase's launches are
-// captured once into a graph (like the one-GPU step) and replayed; the exchanges run between the
-// graphs (RCCL on the handle's stream, or the caller's buffer moves in external mode).
+// ---- sharded GN iteration in three phases (exchanges between them). With a communicator the
+// whole iteration — the phases and the two ncclAllGather calls between them — is captured once into
+// one graph and replayed (do_step_sharded); in external mode (the caller moves the buffers) each
+// phase is a graph of its own. Phase boundaries are stamped by the phases' own kernels (StepStatus
+// stamp slots 0-7), not by events.
 // phase 0: J+H (own + top lanes), solver inputs, own subtrees factored (and forward-solved),
 // exchange-1 buffer packed (roots' U / u, this rank's chi^2 partials)
 // phase 1: the other ranks' roots in place, the top factored and solved, own subtrees solved
 // backward, exchange-2 buffer packed (max |x| of own + top, solver word, boundary solution)
-// phase 2: boundary solution in place, step status combined from every rank's headers, box-plus of
-// own + top + boundary nodes (skipped when any rank's factorization aborted)
+// phase 2: boundary solution in place, box-plus of own + top + boundary nodes (skipped when any
+// rank's factorization aborted: every rank's header), step status combined from every rank's headers
 int shard_enqueue(bos_solver* s, int phase) {
     int rc;
     double* U = bos::dev::mf_update_ptr(s->mf);
@@ -567,22 +578,25 @@ int shard_enqueue(bos_solver* s, int phase) {
         if ((rc = enqueue_solver_inputs(s))) return rc;   // opens this step's flow epoch
         HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
         HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_pack, s->n1p, s->maxlen1p, s->stream));
-        HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream));
+        HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream,
+                                               s->d_status->stamp + 4));
     } else if (phase == 1) {
-        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_unpack, s->n1u, s->maxlen1u, s->stream));
+        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_unpack, s->n1u, s->maxlen1u, s->stream,
+                                                  s->d_status->stamp + 5));
         HIP_TRY(bos::dev::mf_factor(s->mf, 1, mf_matrix(s), s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, 1, s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, 0, s->d_rhs, s->stream));
         HIP_TRY(bos::dev::launch_shard_pack2(s->d_rhs, s->upd_nodes, s->n_upd_local, s->node_dof, s->NP,
                                              bos::dev::mf_info_ptr(s->mf), s->ex2_bnd, s->n_bnd, s->abs_part, s->ex2_send,
-                                             s->stream));
+                                             s->stream, s->d_status->stamp + 6));
     } else {
-        HIP_TRY(bos::dev::launch_index_copy(s->ex2_recv, s->ex2_usrc, s->d_rhs, s->ex2_udst, s->n_bnd_remote, s->stream));
+        HIP_TRY(bos::dev::launch_index_copy(s->ex2_recv, s->ex2_usrc, s->d_rhs, s->ex2_udst, s->n_bnd_remote, s->stream,
+                                            s->d_status->stamp + 7));
+        if ((rc = enqueue_update(s))) return rc;
         int32_t nrob_c = 0;
         const double chi_c = self_loop_chi(s, nrob_c);
         HIP_TRY(bos::dev::launch_shard_combine(s->ex1_recv, s->ex1_count, s->ex2_recv, s->ex2_count, s->world, chi_c,
                                                nrob_c, s->d_status, s->m_status, s->stream));
-        if ((rc = enqueue_update(s))) return rc;
     }
     return BOS_OK;
 }
@@ -614,6 +628,8 @@ int obs_enqueue(bos_solver* s, int phase) {
     return enqueue_step_tail(s);
 }
 
+int rccl_allreduce_obs(bos_solver* s);
+
 int obs_phase(bos_solver* s, int phase) {
     int rc;
     if (!s->pexec[phase] && !s->graph_failed && (rc = capture(s, 10 + phase, &s->pgraph[phase], &s->pexec[phase]))) return rc;
@@ -634,15 +650,12 @@ int rccl_allreduce_obs(bos_solver* s) {
     return BOS_OK;
 }
 
-// one phase: its graph (captured on first use), bracketed by the phase events
+// one phase: its graph (captured on first use)
 int shard_phase(bos_solver* s, int phase) {
-    static const int evb[3] = {0, 3, 5}, eve[3] = {2, 4, 6};
     int rc;
-    HIP_TRY(hipEventRecord(s->ev[evb[phase]], s->stream));
     if (!s->pexec[phase] && !s->graph_failed && (rc = capture(s, phase, &s->pgraph[phase], &s->pexec[phase]))) return rc;
     if (s->pexec[phase]) HIP_TRY(hipGraphLaunch(s->pexec[phase], s->stream));
     else if ((rc = shard_enqueue(s, phase))) return rc;
-    HIP_TRY(hipEventRecord(s->ev[eve[phase]], s->stream));
     return BOS_OK;
 }
 int shard_phase0(bos_solver* s) { return shard_phase(s, 0); }
@@ -656,13 +669,63 @@ int rccl_allgather(bos_solver* s, const double* send, double* recv, int64_t coun
 
 int finish_step(bos_solver* s, bos_step_stats* st);
 
+// the whole sharded iteration with its collectives (RCCL on the handle's stream)
+int enqueue_sharded_step(bos_solver* s) {
+    int rc;
+    if ((rc = shard_enqueue(s, 0)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
+        (rc = shard_enqueue(s, 1)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)))
+        return rc;
+    return shard_enqueue(s, 2);
+}
+
+// the whole observations-partition iteration with its all-reduce
+int enqueue_obs_step(bos_solver* s) {
+    int rc;
+    if ((rc = obs_enqueue(s, 0)) || (rc = rccl_allreduce_obs(s))) return rc;
+    return obs_enqueue(s, 1);
+}
+
+// One graph for a multi-rank iteration with its RCCL collectives (captured on first use). If the
+// collectives cannot be captured, rccl_capture_failed is set and the caller runs the phase graphs
+// with the collectives between them instead (the same launches in the same order).
+int capture_rccl_step(bos_solver* s) {
+    if (s->sexec || s->graph_failed || s->rccl_capture_failed) return BOS_OK;
+    if (hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        s->graph_failed = true;
+        return BOS_OK;
+    }
+    const int rc = s->obs ? enqueue_obs_step(s) : enqueue_sharded_step(s);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s->stream, &g);
+    if (rc || e != hipSuccess || !g) {
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        s->rccl_capture_failed = true;   // (a launch error reappears on the eager path)
+        return BOS_OK;
+    }
+    if (hipGraphInstantiate(&s->sexec, g, nullptr, nullptr, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipGraphDestroy(g);
+        s->sexec = nullptr;
+        s->rccl_capture_failed = true;
+        return BOS_OK;
+    }
+    s->sgraph = g;
+    return BOS_OK;
+}
+
 int do_step_sharded(bos_solver* s, bos_step_stats* st, bool sync) {
     if (!s->comm) return fail(BOS_ERR_INVALID, "sharded handle without a communicator: drive bos_step_phase");
     int rc;
-    if ((rc = shard_phase0(s)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
-        (rc = shard_phase1(s)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)) ||
-        (rc = shard_phase2(s)))
+    if ((rc = capture_rccl_step(s))) return rc;
+    if (s->sexec) {
+        HIP_TRY(hipGraphLaunch(s->sexec, s->stream));
+    } else if ((rc = shard_phase0(s)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
+               (rc = shard_phase1(s)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)) ||
+               (rc = shard_phase2(s))) {
         return rc;
+    }
     s->have_dx = true;
     if (!sync) return BOS_OK;
     return finish_step(s, st);
@@ -678,13 +741,14 @@ int finish_step(bos_solver* s, bos_step_stats* st) {
         return fail(BOS_ERR_SOLVER, "sparse factorization aborted: a dataflow dependency wait timed out (state "
                                     "left unchanged by the failed iteration)");
     }
-    if (st && s->sharded) {   // J+H from the device stamps, the rest from the phase events
+    if (st && s->sharded) {   // phase boundaries stamped by the phases' kernels (StepStatus::stamp)
         bos::dev::StepStatus h;
         std::memcpy(&h, (const void*)s->h_status, sizeof(h));
-        st->t_linearize_ms = h.stamp[1] > h.stamp[0] ? (double)(h.stamp[1] - h.stamp[0]) * bos::dev::kStampMs : 0.0;
-        st->t_exchange_ms = elapsed(s->ev[2], s->ev[3]) + elapsed(s->ev[4], s->ev[5]);
-        st->t_solve_ms = std::max(0.0, elapsed(s->ev[0], s->ev[2]) - st->t_linearize_ms) + elapsed(s->ev[3], s->ev[4]);
-        st->t_update_ms = elapsed(s->ev[5], s->ev[6]);
+        auto d = [](unsigned long long a, unsigned long long b) { return b > a ? (double)(b - a) * bos::dev::kStampMs : 0.0; };
+        st->t_linearize_ms = d(h.stamp[0], h.stamp[1]);
+        st->t_solve_ms = d(h.stamp[1], h.stamp[4]) + d(h.stamp[5], h.stamp[6]);
+        st->t_exchange_ms = d(h.stamp[4], h.stamp[5]) + d(h.stamp[6], h.stamp[7]);
+        st->t_update_ms = d(h.stamp[7], h.stamp[3]);
     }
     return BOS_OK;
 }
@@ -726,6 +790,10 @@ void drop_graph(bos_solver* s) {
         s->pexec[i] = nullptr;
         s->pgraph[i] = nullptr;
     }
+    if (s->sexec) (void)hipGraphExecDestroy(s->sexec);
+    if (s->sgraph) (void)hipGraphDestroy(s->sgraph);
+    s->sexec = nullptr;
+    s->sgraph = nullptr;
 }
 
 // Capture the launches of one GN step (phase -1: the one-GPU step after its J+H build,
@@ -765,7 +833,9 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     int rc;
     if (s->obs) {
         if (!s->comm) return fail(BOS_ERR_INVALID, "observations-partition handle without a communicator: drive bos_step_phase");
-        if ((rc = obs_phase(s, 0)) || (rc = rccl_allreduce_obs(s)) || (rc = obs_phase(s, 1))) return rc;
+        if ((rc = capture_rccl_step(s))) return rc;
+        if (s->sexec) HIP_TRY(hipGraphLaunch(s->sexec, s->stream));
+        else if ((rc = obs_phase(s, 0)) || (rc = rccl_allreduce_obs(s)) || (rc = obs_phase(s, 1))) return rc;
     } else if ((rc = launch_step(s, sync))) {
         return rc;
     }

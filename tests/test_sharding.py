@@ -283,3 +283,50 @@ def test_two_processes_share_one_gpu():
     assert np.array_equal(pm, p1) and np.array_equal(lm_, l1)
     assert res[0][4] == res[1][4]
     assert np.allclose(res[0][4], [s["chi2"] for s in st1], rtol=1e-12, atol=0)
+
+
+def _gpu_obs_worker(rank, world, port, q, iters):
+    try:
+        _paths()
+        import bos
+        bos.lib()
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        P = bos.synthetic(1000, 2000, 20)
+        S = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR, device=0, rank=rank, world_size=world,
+                       partition=bos.BOS_PARTITION_OBSERVATIONS)
+        stats = []
+        for _ in range(iters):
+            S.step_phase(0)
+            t = torch.from_numpy(S.exchange_download(1))
+            dist.all_reduce(t)   # the north star's all-reduce of (H, b) and the chi^2 header
+            S.exchange_upload(1, t.numpy())
+            stats.append(S.step_phase(1))
+        pose, lm = S.get_state()
+        S.close()
+        dist.destroy_process_group()
+        q.put((rank, pose, lm, stats, None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, None, None, None, repr(e)))
+
+
+@pytest.mark.gpu
+def test_two_processes_observations_partition():
+    """BOS_PARTITION_OBSERVATIONS across two processes on the one GPU, the all-reduce of (H, b) over
+    gloo: both ranks' states after 3 GN iterations equal the one-GPU run bit for bit, with the same
+    chi^2 and robust counts (the multi-process counterpart of
+    tests/test_partitions.py's in-process W-handle test)."""
+    import bos
+    world, iters = 2, 3
+    res = _spawn(_gpu_obs_worker, world, (iters,), timeout=300)
+    P = bos.synthetic(1000, 2000, 20)
+    (p1, l1), st1 = _run_one(P, iters, bos.BOS_FP64)
+    for r in res:
+        assert np.array_equal(r[1], p1) and np.array_equal(r[2], l1)
+        for it in range(iters):
+            assert abs(r[3][it]["chi2"] - st1[it]["chi2"]) <= 1e-12 * st1[it]["chi2"]
+            assert r[3][it]["n_robust"] == st1[it]["n_robust"]
+            assert r[3][it]["solver_info"] == 0

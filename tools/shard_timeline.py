@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Per-rank phase times of the sharded GN step on ONE GPU (ranks run one after another, each alone
 on the device, exchanges by host copies): what each rank's GPU would spend per iteration on an
-N-GPU node, minus the two RCCL all-gathers. Config 3, fp32 J+H, Schur solver.
+N-GPU node, minus the two RCCL all-gathers. The phase times are the device stamps the phases'
+kernels write (StepStatus stamp slots), so the host's exchange copies between phases are not in
+them. W = 1 runs the RCCL path with a one-rank communicator (the whole iteration, collectives
+included, one graph) and is also timed on the host clock beside the plain one-GPU step.
+Config 3, fp32 J+H, Schur solver.
 
     python tools/shard_timeline.py [worlds...]      (default 1 2 4 8)
     BOS_LPP=2|4: J+H lanes per pose (bos_options.lanes_per_pose; default: the plan's choice)
@@ -51,10 +55,27 @@ for W in worlds:
             rows.append([[s["t_linearize_ms"], s["t_solve_ms"], s["t_update_ms"]] for s in st])
     a = np.median(np.array(rows), axis=0)   # [rank][phase]
     per_rank = a.sum(axis=1)
+    wall = {}
+    if W == 1:   # host-clock rate of the one-rank RCCL path against the plain one-GPU step
+        S1 = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=LPP)
+        for name, h in (("rccl_one_rank", S[0]), ("one_gpu", S1)):
+            init = h.get_state()
+            h.step()
+            h.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(20):
+                h.step()
+            h.synchronize()
+            wall[name] = (time.perf_counter() - t0) / 20 * 1e3
+            h.set_state(*init)
+        S1.close()
+        print(f"W=1 wall ms/step: RCCL one-rank path {wall['rccl_one_rank']:.3f}, one GPU {wall['one_gpu']:.3f}",
+              flush=True)
     info = [h.system_info() for h in S]
     out[W] = {"create_s": t_create, "jh_ms": a[:, 0].tolist(), "solve_ms": a[:, 1].tolist(), "update_ms": a[:, 2].tolist(),
               "max_rank_ms": float(per_rank.max()), "own_fronts": [i["own_fronts"] for i in info],
-              "top_fronts": info[0]["top_fronts"], "pose_lane_groups": [i["pose_lane_groups"] for i in info]}
+              "top_fronts": info[0]["top_fronts"], "pose_lane_groups": [i["pose_lane_groups"] for i in info],
+              "wall_ms_per_step": wall}
     print(f"W={W}: per-rank compute (J+H + solve + update) max {per_rank.max():.3f} ms "
           f"(J+H {a[:, 0].max():.3f}, solve {a[:, 1].max():.3f}, update {a[:, 2].max():.3f}); top fronts "
           f"{info[0]['top_fronts']}; create {t_create:.1f} s", flush=True)
