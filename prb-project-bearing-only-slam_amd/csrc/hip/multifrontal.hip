@@ -304,42 +304,46 @@ __device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
 }
 
 // Folded landmark children (Schur ordering) of front s, eliminated by its wave: per chunk (whole
-// children, <= 64 rows, <= fold_chunk_landmarks(m) landmarks) lane q takes row t of landmark c
-// (one 32-byte record: sources of its two entries, of the landmark's 2 x 2 block, the landmark's
-// col0 / r / L offset, the row's position in this front and c's index in the chunk), factors the
-// 2 x 2 block, forms L[t, 0..1], the landmark's forward step y, and writes the landmark's L panel
-// and y. The rows also form the chunk's W (front position x 2 columns per landmark, in LDS that
-// the front's F uses later) and its y; W W^T accumulates in f64 MFMA registers (the landmarks'
-// update matrices -L21 L21^T, summed) and -W y in the position lanes (their u-vectors). The
-// caller subtracts both once the front is assembled. Nothing goes through global memory and the
-// result is deterministic.
+// children, <= 64 row groups, <= fold_chunk_landmarks(m) landmarks) lane q takes one observing pose
+// of landmark c — its 3 rows t, t + 1, t + 2 (one 32-byte record: sources of the pose-landmark
+// block and of the landmark's 2 x 2 block, the landmark's col0 / r / L offset, the rows' first
+// position in this front and c's index in the chunk), factors the 2 x 2 block, forms L[t + g,
+// 0..1], the landmark's forward step y, and writes the landmark's L panel and y. The rows also form
+// the chunk's W (front position x 2 columns per landmark, in LDS that the front's F uses later) and
+// its y; W W^T accumulates in f64 MFMA registers (the landmarks' update matrices -L21 L21^T,
+// summed) and -W y in the position lanes (their u-vectors). The caller subtracts both once the
+// front is assembled. Nothing goes through global memory and the result is deterministic.
 __device__ __forceinline__ int4 fold_rec_load(const MfArgs& a, int q, int half) {
     return reinterpret_cast<const int4*>(a.fold_rec + (int64_t)kFoldRec * q)[half];
 }
 
-// The values one chunk's rows need (H entries of the row and of its landmark's 2 x 2 block, the
-// landmark's right-hand side), gathered for chunk c + 1 while chunk c is processed.
+// The values one chunk's row groups need (the pose-landmark block, 3 x 2, the landmark's 2 x 2
+// block and right-hand side), gathered for chunk c + 1 while chunk c is processed.
 struct FoldVals {
-    double ht0, ht1, a00, a10, a11, x0, x1;
+    double h[6];   // (row g, column j) at 2 g + j
+    double a00, a10, a11, x0, x1;
 };
 // The same from the fp32 build (F32: mf_set_fold_source): the bearing's factored block (J_theta,
-// J_lx, J_ly) and the landmark's 2 x 2 block as loaded, the row's pose dof and the entries' presence
-// in flags; fold_decode forms the doubles the fp64 copy would hold (products in fp32, as
+// J_lx, J_ly) and the landmark's 2 x 2 block as loaded, and the entries' presence in flags;
+// fold_decode forms the doubles the fp64 copy would hold (products in fp32, as
 // gather_f64_factored_kernel expands them), so the result is bit-identical.
 struct FoldVals32 {
     float jt, jx, jy, a00, a10, a11;
-    int flags;   // pose dof of the row (0..2; 3: no entry) | a00, a10, a11 present << 2, 3, 4
+    int flags;   // block present << 0 | a00, a10, a11 present << 2, 3, 4
     double x0, x1;
 };
 template <bool F32> using FoldValsT = typename std::conditional<F32, FoldVals32, FoldVals>::type;
 
 __device__ __forceinline__ FoldVals fold_decode(const FoldVals& v) { return v; }
 __device__ __forceinline__ FoldVals fold_decode(const FoldVals32& v) {
-    const int row = v.flags & 3;
-    const float p = row == 0 ? -v.jx : row == 1 ? -v.jy : v.jt;
     FoldVals d;
-    d.ht0 = row == 3 ? 0.0 : (double)(p * v.jx);
-    d.ht1 = row == 3 ? 0.0 : (double)(p * v.jy);
+    const bool blk = v.flags & 1;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        const float p = g == 0 ? -v.jx : g == 1 ? -v.jy : v.jt;   // J_p = (-J_lx, -J_ly, J_theta)
+        d.h[2 * g] = blk ? (double)(p * v.jx) : 0.0;
+        d.h[2 * g + 1] = blk ? (double)(p * v.jy) : 0.0;
+    }
     d.a00 = (v.flags & 4) ? (double)v.a00 : 0.0;
     d.a10 = (v.flags & 8) ? (double)v.a10 : 0.0;
     d.a11 = (v.flags & 16) ? (double)v.a11 : 0.0;
@@ -351,10 +355,9 @@ __device__ __forceinline__ FoldVals fold_decode(const FoldVals32& v) {
 template <bool F32>
 __device__ __forceinline__ FoldValsT<F32> fold_vals(const MfArgs& a, const int4& r0, const int4& r1, bool mine) {
     if constexpr (F32) {
-        // records index the fp64 layout: pose-landmark entry (t, j) of slot q at pl_lo + 6 q + 2 t + j,
-        // held factored at pl_lo + 3 q of the fp32 array (mf_set_fold_source checked the records)
-        const int e = max(r0.x - (int)a.pl_lo, 0);
-        const int q = e / 6, row = (e - 6 * q) >> 1;
+        // records index the fp64 layout: the block of slot q at pl_lo + 6 q, held factored at
+        // pl_lo + 3 q of the fp32 array (mf_set_fold_source checked the records)
+        const int q = max(r0.x - (int)a.pl_lo, 0) / 6;
         const float* f = a.A32 + a.pl_lo + 3 * (int64_t)q;
         FoldVals32 v;
         v.jt = f[0];
@@ -363,20 +366,24 @@ __device__ __forceinline__ FoldValsT<F32> fold_vals(const MfArgs& a, const int4&
         v.a00 = a.A32[max(r0.z, 0)];
         v.a10 = a.A32[max(r0.w, 0)];
         v.a11 = a.A32[max(r1.x, 0)];
-        v.x0 = a.x[r1.y];   // (a lane past the chunk's rows reads its last row's: see fold_chunk)
+        v.x0 = a.x[r1.y];   // (a lane past the chunk's groups reads its last group's: see fold_chunk)
         v.x1 = a.x[r1.y + 1];
-        v.flags = (r0.x >= 0 ? row : 3) | (r0.z >= 0 ? 4 : 0) | (r0.w >= 0 ? 8 : 0) | (r1.x >= 0 ? 16 : 0);
+        v.flags = (r0.x >= 0 ? 1 : 0) | (r0.z >= 0 ? 4 : 0) | (r0.w >= 0 ? 8 : 0) | (r1.x >= 0 ? 16 : 0);
         return v;
     } else {
     // every load unconditional (indices clamped to valid ones), the value selected afterwards: a
     // predicated load would be a branch with its wait inside, and the next chunk's values must stay
     // in flight while the current chunk is processed
-    const double ht0 = a.A[max(r0.x, 0)], ht1 = a.A[max(r0.y, 0)], a00 = a.A[max(r0.z, 0)], a10 = a.A[max(r0.w, 0)];
+    const int b = max(r0.x, 0);
+    double h[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) h[e] = a.A[b + e];
+    const double a00 = a.A[max(r0.z, 0)], a10 = a.A[max(r0.w, 0)];
     const double a11 = a.A[max(r1.x, 0)];
-    const double x0 = a.x[r1.y], x1 = a.x[r1.y + 1];   // (lanes past the rows: their last row's)
+    const double x0 = a.x[r1.y], x1 = a.x[r1.y + 1];   // (lanes past the groups: their last group's)
     FoldVals v;
-    v.ht0 = r0.x >= 0 ? ht0 : 0.0;
-    v.ht1 = r0.y >= 0 ? ht1 : 0.0;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) v.h[e] = r0.x >= 0 ? h[e] : 0.0;
     v.a00 = r0.z >= 0 ? a00 : 0.0;
     v.a10 = r0.w >= 0 ? a10 : 0.0;
     v.a11 = r1.x >= 0 ? a11 : 0.0;
@@ -438,13 +445,18 @@ __device__ __forceinline__ void fold_chunk(const MfArgs& a, double* W, FoldBuf* 
         const bool bad1 = !(d1 > 0.0);
         d1 = bad1 ? 1e-300 : d1;
         const double i1 = rsqrt_nr(d1), l11 = d1 * i1;
-        const double lt0 = v.ht0 * i0, lt1 = (v.ht1 - lt0 * l10) * i1;
         const double y0 = v.x0 * i0, y1 = (v.x1 - l10 * y0) * i1;
         const int mc = 2 + rc;
         double* Lc = a.L + loff;
         const bool head = mine && t == 0;
-        Lc[2 + t] = lt0;
-        Lc[mc + 2 + t] = lt1;
+        double lt0[3], lt1[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            lt0[g] = v.h[2 * g] * i0;
+            lt1[g] = (v.h[2 * g + 1] - lt0[g] * l10) * i1;
+            Lc[2 + t + g] = lt0[g];
+            Lc[mc + 2 + t + g] = lt1[g];
+        }
         Lc[0] = l00;
         Lc[1] = l10;
         Lc[mc + 1] = l11;
@@ -456,8 +468,11 @@ __device__ __forceinline__ void fold_chunk(const MfArgs& a, double* W, FoldBuf* 
             fb->y[2 * lml + 1] = y1;
         }
         if (mine) {
-            W[pos * WS + 2 * lml] = lt0;
-            W[pos * WS + 2 * lml + 1] = lt1;
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                W[(pos + g) * WS + 2 * lml] = lt0[g];
+                W[(pos + g) * WS + 2 * lml + 1] = lt1[g];
+            }
         }
     }
     wave_sync();
@@ -482,8 +497,11 @@ __device__ __forceinline__ void fold_chunk(const MfArgs& a, double* W, FoldBuf* 
     }
     wave_sync();
     if (mine) {   // clear this chunk's W entries for the next chunk
-        W[pos * WS + 2 * lml] = 0.0;
-        W[pos * WS + 2 * lml + 1] = 0.0;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            W[(pos + g) * WS + 2 * lml] = 0.0;
+            W[(pos + g) * WS + 2 * lml + 1] = 0.0;
+        }
     }
     wave_sync();
 }
@@ -492,6 +510,8 @@ template <int MAXM, bool F32>
 __device__ __forceinline__ void fold_children(const MfArgs& a, int s, double* W, FoldBuf* fb, int m, int lane,
                                               FoldAcc<MAXM>& acc) {
     constexpr int WS = 2 * fold_chunk_landmarks(MAXM) + 1;
+    static_assert(MAXM * WS <= MAXM * (MAXM + 1) / 2, "W fits the front's LDS triangle");
+    static_assert(fold_chunk_landmarks(MAXM) % 2 == 0, "the W W^T steps (4 columns) stay inside W's rows");
 #pragma unroll
     for (int q = 0; q < FoldAcc<MAXM>::NP; ++q) acc.d[q] = dbl4{0.0, 0.0, 0.0, 0.0};
     acc.w = 0.0;

@@ -120,31 +120,34 @@ struct HostMf {
         }
     }
 
-    // folded landmark children (Schur ordering): the fold records, as fold_children reads them;
-    // their u entries accumulate per parent in fwv
+    // folded landmark children (Schur ordering): the fold records (one per observing pose: rows t,
+    // t + 1, t + 2), as fold_children reads them; their u entries accumulate per parent in fwv
     void fold(int s, std::vector<double>& W, int m) {
         fwv[s].assign(m, 0.0);
         for (int ch = F.fold_cptr[s]; ch < F.fold_cptr[s + 1]; ++ch) {
             const int q0 = F.fold_chunk[ch], nq = F.fold_chunk[ch + 1] - q0;
-            std::vector<double> l0(nq), l1(nq);
-            std::vector<int> pos(nq), rcs(nq);
+            std::vector<double> l0(3 * nq), l1(3 * nq);
+            std::vector<int> pos(3 * nq), cl(3 * nq);
             for (int q = 0; q < nq; ++q) {
                 const int32_t* rec = F.fold_rec.data() + (size_t)kFoldRec * (q0 + q);
                 auto v = [&](int32_t src) { return src >= 0 ? hval[src] : 0.0; };
                 const int col0 = rec[5], t = rec[6] & 63, rc = (rec[6] >> 6) & 63;
                 const double l00 = std::sqrt(std::max(v(rec[2]), 1e-300)), l10 = v(rec[3]) / l00;
                 const double l11 = std::sqrt(std::max(v(rec[4]) - l10 * l10, 1e-300));
-                l0[q] = v(rec[0]) / l00;
-                l1[q] = (v(rec[1]) - l0[q] * l10) / l11;
                 const double y0 = x[col0] / l00, y1 = (x[col0 + 1] - l10 * y0) / l11;
                 double* Lc = L.data() + rec[7];
                 const int mc = 2 + rc;
-                Lc[2 + t] = l0[q];
-                Lc[mc + 2 + t] = l1[q];
+                for (int g = 0; g < 3; ++g) {
+                    const int i = 3 * q + g;
+                    l0[i] = v(rec[0] >= 0 ? rec[0] + 2 * g : rec[0]) / l00;
+                    l1[i] = (v(rec[0] >= 0 ? rec[0] + 2 * g + 1 : rec[0]) - l0[i] * l10) / l11;
+                    Lc[2 + t + g] = l0[i];
+                    Lc[mc + 2 + t + g] = l1[i];
+                    pos[i] = ((rec[6] >> 12) & 63) + g;
+                    cl[i] = rec[7];   // the landmark (its L offset)
+                    fwv[s][pos[i]] -= l0[i] * y0 + l1[i] * y1;
+                }
                 if (t == 0) { Lc[0] = l00; Lc[1] = l10; Lc[mc + 1] = l11; }
-                pos[q] = (rec[6] >> 12) & 63;
-                rcs[q] = rc;
-                fwv[s][pos[q]] -= l0[q] * y0 + l1[q] * y1;
             }
             for (int q = 0; q < nq; ++q) {   // the landmarks' forward results, after every row used them
                 const int32_t* rec = F.fold_rec.data() + (size_t)kFoldRec * (q0 + q);
@@ -156,10 +159,9 @@ struct HostMf {
                     x[col0] = y0;
                 }
             }
-            for (int c0 = 0; c0 < nq; c0 += rcs[c0])
-                for (int j = c0; j < c0 + rcs[c0]; ++j)
-                    for (int i = j; i < c0 + rcs[c0]; ++i)
-                        W[pos[i] + (size_t)pos[j] * m] -= l0[i] * l0[j] + l1[i] * l1[j];
+            for (int j = 0; j < 3 * nq; ++j)   // W W^T within each landmark
+                for (int i = j; i < 3 * nq && cl[i] == cl[j]; ++i)
+                    W[pos[i] + (size_t)pos[j] * m] -= l0[i] * l0[j] + l1[i] * l1[j];
         }
     }
 

@@ -918,7 +918,7 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
         for (int ci = F.child_ptr[p]; ci < F.child_ptr[p + 1]; ++ci) {
             const int c = F.child[ci];
             if (c >= n_fold_cand) break;
-            ok = ok && F.k[c] == 2 && F.k[c] + F.r[c] <= kMfWaveMaxM && F.r[c] <= kFoldChunk &&
+            ok = ok && F.k[c] == 2 && F.k[c] + F.r[c] <= kMfWaveMaxM && F.r[c] <= 3 * kFoldChunk &&
                  F.child_ptr[c] == F.child_ptr[c + 1];
             ++nf;
         }
@@ -994,11 +994,13 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
             F.amap_dst[q] = dst[e];
         }
     }
-    // fold records, one per row t of a folded child c (parents in id order, their folded children
-    // in child-list order): {src (t, 0), src (t, 1), src (0, 0), src (1, 0), src (1, 1), col0[c],
-    // t | r[c] << 6 | (row t's position in the parent front) << 12 | (c's index in the chunk) << 18,
-    // L_off[c]}; src = block-array
-    // index of the front entry (-1: structurally zero)
+    // fold records, one per observing pose of a folded child c — a group of 3 consecutive rows
+    // t, t + 1, t + 2 (the pose's x, y, theta dofs) at consecutive positions of the parent front —
+    // (parents in id order, their folded children in child-list order): {src (t, 0), src (t, 1),
+    // src (0, 0), src (1, 0), src (1, 1), col0[c], t | r[c] << 6 | (row t's position in the parent
+    // front) << 12 | (c's index in the chunk) << 18, L_off[c]}; src = block-array index of the front
+    // entry (-1: structurally zero, -2: another rank's); the group's 6 entries (t + g, j) are the
+    // pose-landmark block's values src (t, 0) + 2 g + j
     F.fold_cptr.assign(ns + 1, 0);
     F.fold_chunk.clear();
     F.fold_rec.clear();
@@ -1009,8 +1011,9 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
         int32_t chunk_rows = kFoldChunk, chunk_lms = 0;   // forces a new chunk at the parent's first child
         const int cap = fold_chunk_landmarks(F.k[p] + F.r[p]);
         for (int ci = F.child_ptr[p]; ci < F.child_ptr[p] + F.fold_cnt[p]; ++ci) {
-            const int c = F.child[ci], rc = F.r[c], mc = 2 + rc;
-            if (chunk_rows + rc > kFoldChunk || chunk_lms >= cap) {
+            const int c = F.child[ci], rc = F.r[c], mc = 2 + rc, ng = rc / 3;
+            if (rc % 3) { err = "multifrontal: folded landmark rows not whole poses"; return BOS_ERR_INVALID; }
+            if (chunk_rows + ng > kFoldChunk || chunk_lms >= cap) {
                 F.fold_chunk.push_back(nrows);
                 chunk_rows = 0;
                 chunk_lms = 0;
@@ -1021,15 +1024,22 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
                 while (d >= mc - j) { d -= mc - j; ++j; }
                 src[(j + d) + j * mc] = F.amap_src[q];
             }
-            for (int t = 0; t < rc; ++t) {
-                const int32_t rec[kFoldRec] = {src[2 + t], src[2 + t + mc], src[0], src[1], src[1 + mc], F.col0[c],
-                                               t | rc << 6 | F.rmap[F.rmap_off[c] + t] << 12 | chunk_lms << 18,
-                                               (int32_t)F.L_off[c]};
+            const int32_t* rm = F.rmap.data() + F.rmap_off[c];
+            for (int t = 0; t < rc; t += 3) {
+                const int32_t b0 = src[2 + t];
+                for (int g = 0; g < 3; ++g) {
+                    const bool pos_ok = rm[t + g] == rm[t] + g;
+                    const bool src_ok = b0 >= 0 ? src[2 + t + g] == b0 + 2 * g && src[2 + t + g + mc] == b0 + 2 * g + 1
+                                                : src[2 + t + g] == b0 && src[2 + t + g + mc] == b0;
+                    if (!pos_ok || !src_ok) { err = "multifrontal: folded pose rows not one block"; return BOS_ERR_INVALID; }
+                }
+                const int32_t rec[kFoldRec] = {b0, src[2 + t + mc], src[0], src[1], src[1 + mc], F.col0[c],
+                                               t | rc << 6 | rm[t] << 12 | chunk_lms << 18, (int32_t)F.L_off[c]};
                 F.fold_rec.insert(F.fold_rec.end(), rec, rec + kFoldRec);
             }
-            chunk_rows += rc;
+            chunk_rows += ng;
             ++chunk_lms;
-            nrows += rc;
+            nrows += ng;
         }
     }
     F.fold_cptr[ns] = (int32_t)F.fold_chunk.size();
@@ -1054,8 +1064,8 @@ bool mf_fold_reads_fp32(const Plan& P) {
     const size_t nrec = F.fold_rec.size() / kFoldRec;
     for (size_t q = 0; q < nrec; ++q) {
         const int32_t* r = &F.fold_rec[kFoldRec * q];
-        if (r[0] >= 0 || r[1] >= 0) {
-            if (r[0] < pl || r[0] >= hi || ((r[0] - pl) & 1) || r[1] != r[0] + 1) return false;
+        if (r[0] >= 0 || r[1] >= 0) {   // a group's block: 6 values from slot (r[0] - pl) / 6
+            if (r[0] < pl || r[0] + 6 > hi || (r[0] - pl) % 6 || r[1] != r[0] + 1) return false;
         }
         for (int j = 2; j < 5; ++j)
             if (r[j] >= 0 && (r[j] < lo || r[j] >= pl)) return false;

@@ -131,11 +131,13 @@ struct OrderingReport {
 //  - L panels are m x k column-major (entries above the diagonal unused).
 constexpr int kMfWaveMaxM = 64;
 constexpr int kMfFlowMaxM = 48;   // fronts of the dataflow factor launch (hip/multifrontal.hip kFlowMaxM)
-constexpr int kFoldChunk = 64;   // folded rows per chunk (one per lane)
-constexpr int kFoldRec = 8;      // ints per folded row
-// landmarks per fold chunk for a parent front of size m: the device forms the chunk's
-// W (m x 2 landmarks, aliasing the front's LDS) whose W W^T it accumulates with f64 MFMA
-constexpr int fold_chunk_landmarks(int m) { return m <= 16 ? 2 : m <= 32 ? 4 : 8; }
+constexpr int kFoldChunk = 64;   // folded row groups per chunk (one per lane)
+constexpr int kFoldRec = 8;      // ints per folded row group (the 3 rows of one observing pose)
+// landmarks per fold chunk for a parent front of size m: the device forms the chunk's W (m x 2
+// landmarks, row stride 2 cap + 1, aliasing the front's packed LDS triangle of m (m + 1) / 2
+// values) whose W W^T it accumulates with f64 MFMA, 4 columns per step (cap even: the steps read
+// no column past 2 cap)
+constexpr int fold_chunk_landmarks(int m) { return m <= 16 ? 2 : m <= 32 ? 6 : m <= 48 ? 10 : 14; }
 inline int64_t mf_packed(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }   // i >= j
 
 struct Multifrontal {
@@ -159,9 +161,9 @@ struct Multifrontal {
     // level ignores them); fold_list holds them for the backward substitution.
     std::vector<int32_t> fold_cnt;          // per supernode: #folded children (the first of its child list)
     std::vector<int32_t> fold_cptr;         // per supernode: its chunks [fold_cptr[s], fold_cptr[s + 1])
-    std::vector<int32_t> fold_chunk;        // chunk c = folded rows [fold_chunk[c], fold_chunk[c + 1]):
-                                            // whole children, <= kFoldChunk rows
-    std::vector<int32_t> fold_rec;          // kFoldRec ints per folded row (layout: build_multifrontal)
+    std::vector<int32_t> fold_chunk;        // chunk c = folded row groups [fold_chunk[c], fold_chunk[c + 1]):
+                                            // whole children, <= kFoldChunk groups
+    std::vector<int32_t> fold_rec;          // kFoldRec ints per folded row group (layout: build_multifrontal)
     std::vector<int32_t> fold_list;         // folded supernodes
     int64_t L_size = 0, U_size = 0, u_size = 0;
     double flops = 0;
