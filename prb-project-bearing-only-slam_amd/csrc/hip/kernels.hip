@@ -746,7 +746,18 @@ __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const doub
     out->info = (int32_t)min(piv, (long long)(kStepAbort - 1)) | abort_bits;
     out->aborted |= abort_bits;
     out->stamp[3] = __builtin_amdgcn_s_memrealtime();
-    if (mirror) *mirror = *out;
+    out->seq += 1;
+    if (mirror) {   // the summary, then (after a system-scope release) its sequence number (read_stats)
+        const StepStatus v = *out;
+        mirror->chi2 = v.chi2;
+        mirror->max_dx = v.max_dx;
+        mirror->n_robust = v.n_robust;
+        mirror->info = v.info;
+        mirror->aborted = v.aborted;
+        for (int k = 0; k < 8; ++k) mirror->stamp[k] = v.stamp[k];
+        __threadfence_system();
+        __hip_atomic_store(&mirror->seq, v.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // a J+H launch with no blocks (a rank with an empty share of the observations partition) still

@@ -173,8 +173,8 @@ struct bos_solver {
     hipGraphExec_t pexec[3] = {};
     // sharded step with a communicator: the whole iteration (phases and their RCCL collectives) as
     // one graph; rccl_capture_failed: RCCL could not be captured, the phase graphs run instead
-    hipGraph_t sgraph = nullptr;
-    hipGraphExec_t sexec = nullptr;
+    hipGraph_t sgraph = nullptr, stail = nullptr;   // the whole iteration; the iteration after its J+H build
+    hipGraphExec_t sexec = nullptr, stail_exec = nullptr;
     bool rccl_capture_failed = false;
     bool graph_failed = false;   // capture not possible on this stream (e.g. the legacy null stream)
     // one GPU: the status sequence number last seen, and the status launches enqueued since (each
@@ -500,7 +500,7 @@ int enqueue_triangulate(bos_solver* s) {
 // the stream is not synchronised (every later call that reads device memory synchronises it, and
 // launches are stream ordered). A fault or an unexpected state falls back to the stream wait.
 int wait_status(bos_solver* s, bool sync) {
-    if (!sync && !s->sharded && s->seq_pending > 0) {
+    if (!sync && s->seq_pending > 0) {
         const int32_t target = s->seq_seen + s->seq_pending;
         s->seq_seen = target;
         s->seq_pending = 0;
@@ -569,12 +569,12 @@ int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr, bo
 // backward, exchange-2 buffer packed (max |x| of own + top, solver word, boundary solution)
 // phase 2: boundary solution in place, box-plus of own + top + boundary nodes (skipped when any
 // rank's factorization aborted: every rank's header), step status combined from every rank's headers
-int shard_enqueue(bos_solver* s, int phase) {
+int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
     int rc;
     double* U = bos::dev::mf_update_ptr(s->mf);
     double* u = bos::dev::mf_uvec_ptr(s->mf);
     if (phase == 0) {
-        if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
+        if (with_jh && (rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
         if ((rc = enqueue_solver_inputs(s))) return rc;   // opens this step's flow epoch
         HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
         HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_pack, s->n1p, s->maxlen1p, s->stream));
@@ -610,11 +610,11 @@ int enqueue_step_tail(bos_solver* s);
 // summed buffer back into T) the one-GPU solve, box-plus of every node and stats. Every value of H and
 // b is written by exactly one rank's lanes and is zero on the others, so the sum is exact and every
 // rank solves the one-GPU system bit for bit.
-int obs_enqueue(bos_solver* s, int phase) {
+int obs_enqueue(bos_solver* s, int phase, bool with_jh = true) {
     int rc;
     const bool f32 = s->precision == BOS_FP32;
     if (phase == 0) {
-        if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
+        if (with_jh && (rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
         HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream,
                                                s->d_status->stamp + 1));
         if (s->external)
@@ -669,33 +669,34 @@ int rccl_allgather(bos_solver* s, const double* send, double* recv, int64_t coun
 
 int finish_step(bos_solver* s, bos_step_stats* st);
 
-// the whole sharded iteration with its collectives (RCCL on the handle's stream)
-int enqueue_sharded_step(bos_solver* s) {
+// the whole sharded iteration with its collectives (RCCL on the handle's stream); with_jh false:
+// everything after the J+H build
+int enqueue_sharded_step(bos_solver* s, bool with_jh = true) {
     int rc;
-    if ((rc = shard_enqueue(s, 0)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
+    if ((rc = shard_enqueue(s, 0, with_jh)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
         (rc = shard_enqueue(s, 1)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)))
         return rc;
     return shard_enqueue(s, 2);
 }
 
-// the whole observations-partition iteration with its all-reduce
-int enqueue_obs_step(bos_solver* s) {
+// the whole observations-partition iteration with its all-reduce (with_jh false: after the J+H build)
+int enqueue_obs_step(bos_solver* s, bool with_jh = true) {
     int rc;
-    if ((rc = obs_enqueue(s, 0)) || (rc = rccl_allreduce_obs(s))) return rc;
+    if ((rc = obs_enqueue(s, 0, with_jh)) || (rc = rccl_allreduce_obs(s))) return rc;
     return obs_enqueue(s, 1);
 }
 
-// One graph for a multi-rank iteration with its RCCL collectives (captured on first use). If the
-// collectives cannot be captured, rccl_capture_failed is set and the caller runs the phase graphs
-// with the collectives between them instead (the same launches in the same order).
-int capture_rccl_step(bos_solver* s) {
-    if (s->sexec || s->graph_failed || s->rccl_capture_failed) return BOS_OK;
+// One graph for a multi-rank iteration with its RCCL collectives, and one of the iteration after
+// its J+H build (captured on first use). If the collectives cannot be captured,
+// rccl_capture_failed is set and the caller runs the phase graphs with the collectives between them
+// instead (the same launches in the same order).
+int capture_rccl_graph(bos_solver* s, bool with_jh, hipGraph_t* graph, hipGraphExec_t* exec) {
     if (hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
         (void)hipGetLastError();
         s->graph_failed = true;
         return BOS_OK;
     }
-    const int rc = s->obs ? enqueue_obs_step(s) : enqueue_sharded_step(s);
+    const int rc = s->obs ? enqueue_obs_step(s, with_jh) : enqueue_sharded_step(s, with_jh);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s->stream, &g);
     if (rc || e != hipSuccess || !g) {
@@ -704,28 +705,51 @@ int capture_rccl_step(bos_solver* s) {
         s->rccl_capture_failed = true;   // (a launch error reappears on the eager path)
         return BOS_OK;
     }
-    if (hipGraphInstantiate(&s->sexec, g, nullptr, nullptr, 0) != hipSuccess) {
+    if (hipGraphInstantiate(exec, g, nullptr, nullptr, 0) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipGraphDestroy(g);
-        s->sexec = nullptr;
+        *exec = nullptr;
         s->rccl_capture_failed = true;
         return BOS_OK;
     }
-    s->sgraph = g;
+    *graph = g;
+    return BOS_OK;
+}
+
+int capture_rccl_step(bos_solver* s) {
+    int rc;
+    if (s->graph_failed || s->rccl_capture_failed) return BOS_OK;
+    if (!s->sexec && (rc = capture_rccl_graph(s, true, &s->sgraph, &s->sexec))) return rc;
+    if (s->sexec && !s->stail_exec && (rc = capture_rccl_graph(s, false, &s->stail, &s->stail_exec))) return rc;
+    return BOS_OK;
+}
+
+// A multi-rank iteration on RCCL (sharded or observations partition): a batch's steps before its
+// last replay the whole iteration's graph; a synchronous step launches its J+H build directly and
+// the rest as a graph submitted while the build runs (as the one-GPU step, launch_step).
+int launch_rccl_step(bos_solver* s, bool sync) {
+    int rc;
+    if ((rc = capture_rccl_step(s))) return rc;
+    if (!sync && s->sexec) {
+        HIP_TRY(hipGraphLaunch(s->sexec, s->stream));
+    } else if (s->stail_exec) {
+        if ((rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
+        HIP_TRY(hipGraphLaunch(s->stail_exec, s->stream));
+    } else if (s->obs) {
+        if ((rc = obs_phase(s, 0)) || (rc = rccl_allreduce_obs(s)) || (rc = obs_phase(s, 1))) return rc;
+    } else if ((rc = shard_phase0(s)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
+               (rc = shard_phase1(s)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)) ||
+               (rc = shard_phase2(s))) {
+        return rc;
+    }
+    ++s->seq_pending;   // the iteration's status launch bumps the device counter once
     return BOS_OK;
 }
 
 int do_step_sharded(bos_solver* s, bos_step_stats* st, bool sync) {
     if (!s->comm) return fail(BOS_ERR_INVALID, "sharded handle without a communicator: drive bos_step_phase");
     int rc;
-    if ((rc = capture_rccl_step(s))) return rc;
-    if (s->sexec) {
-        HIP_TRY(hipGraphLaunch(s->sexec, s->stream));
-    } else if ((rc = shard_phase0(s)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
-               (rc = shard_phase1(s)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)) ||
-               (rc = shard_phase2(s))) {
-        return rc;
-    }
+    if ((rc = launch_rccl_step(s, sync))) return rc;
     s->have_dx = true;
     if (!sync) return BOS_OK;
     return finish_step(s, st);
@@ -792,8 +816,10 @@ void drop_graph(bos_solver* s) {
     }
     if (s->sexec) (void)hipGraphExecDestroy(s->sexec);
     if (s->sgraph) (void)hipGraphDestroy(s->sgraph);
-    s->sexec = nullptr;
-    s->sgraph = nullptr;
+    if (s->stail_exec) (void)hipGraphExecDestroy(s->stail_exec);
+    if (s->stail) (void)hipGraphDestroy(s->stail);
+    s->sexec = s->stail_exec = nullptr;
+    s->sgraph = s->stail = nullptr;
 }
 
 // Capture the launches of one GN step (phase -1: the one-GPU step after its J+H build,
@@ -833,13 +859,12 @@ int do_step(bos_solver* s, bos_step_stats* st, bool sync) {
     int rc;
     if (s->obs) {
         if (!s->comm) return fail(BOS_ERR_INVALID, "observations-partition handle without a communicator: drive bos_step_phase");
-        if ((rc = capture_rccl_step(s))) return rc;
-        if (s->sexec) HIP_TRY(hipGraphLaunch(s->sexec, s->stream));
-        else if ((rc = obs_phase(s, 0)) || (rc = rccl_allreduce_obs(s)) || (rc = obs_phase(s, 1))) return rc;
+        if ((rc = launch_rccl_step(s, sync))) return rc;
     } else if ((rc = launch_step(s, sync))) {
         return rc;
+    } else {
+        ++s->seq_pending;   // the step's status launch (now enqueued) bumps the device counter once
     }
-    ++s->seq_pending;   // the step's status launch (now enqueued) bumps the device counter once
     s->have_dx = true;
     if (!sync) return BOS_OK;
     int32_t aborted = 0;
@@ -1404,6 +1429,7 @@ int bos_step_phase(bos_solver* s, int32_t phase, bos_step_stats* st) {
     if (rc) { s->phase = 0; return rc; }
     s->phase = (phase + 1) % 3;
     if (phase < 2) return BOS_OK;
+    ++s->seq_pending;   // phase 2's status launch bumps the device counter
     s->have_dx = true;
     return finish_step(s, st);
 }

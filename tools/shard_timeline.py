@@ -52,9 +52,9 @@ for W in worlds:
                 h.exchange_upload(2, recv)
             st = [h.step_phase(2) for h in S]
         if it >= 1:
-            rows.append([[s["t_linearize_ms"], s["t_solve_ms"], s["t_update_ms"]] for s in st])
+            rows.append([[s["t_linearize_ms"], s["t_solve_ms"], s["t_update_ms"], s["t_exchange_ms"]] for s in st])
     a = np.median(np.array(rows), axis=0)   # [rank][phase]
-    per_rank = a.sum(axis=1)
+    per_rank = a[:, :3].sum(axis=1)
     wall = {}
     if W == 1:   # host-clock rate of the one-rank RCCL path against the plain one-GPU step
         S1 = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=LPP)
@@ -73,11 +73,13 @@ for W in worlds:
               flush=True)
     info = [h.system_info() for h in S]
     out[W] = {"create_s": t_create, "jh_ms": a[:, 0].tolist(), "solve_ms": a[:, 1].tolist(), "update_ms": a[:, 2].tolist(),
+              "exchange_ms": a[:, 3].tolist(),
               "max_rank_ms": float(per_rank.max()), "own_fronts": [i["own_fronts"] for i in info],
               "top_fronts": info[0]["top_fronts"], "pose_lane_groups": [i["pose_lane_groups"] for i in info],
               "wall_ms_per_step": wall}
     print(f"W={W}: per-rank compute (J+H + solve + update) max {per_rank.max():.3f} ms "
-          f"(J+H {a[:, 0].max():.3f}, solve {a[:, 1].max():.3f}, update {a[:, 2].max():.3f}); top fronts "
+          f"(J+H {a[:, 0].max():.3f}, solve {a[:, 1].max():.3f}, update {a[:, 2].max():.3f}; between the phases "
+          f"{a[:, 3].max():.3f}); top fronts "
           f"{info[0]['top_fronts']}; create {t_create:.1f} s", flush=True)
     for h in S:
         h.close()
