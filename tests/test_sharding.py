@@ -220,8 +220,10 @@ def test_sharded_dense_world_forced_lanes(world, lpp):
 
 @pytest.mark.gpu
 def test_rccl_one_rank_sharded_path():
-    """world 1 with a communicator: the sharded phases and their RCCL all-gathers (one rank) equal
-    the plain step bit for bit."""
+    """world 1 with a communicator: the sharded iteration (one graph: phases and their RCCL
+    all-gathers, one rank) equals the plain step bit for bit, in synchronous steps (J+H launched
+    directly, the rest replayed) and in bos_step_n batches (the whole iteration replayed); its phase
+    times come from the phases' device stamps (the collectives between the phases included)."""
     import bos
     P = bos.synthetic(1000, 2000, 20)
     A = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR)
@@ -229,6 +231,10 @@ def test_rccl_one_rank_sharded_path():
     for _ in range(3):
         a, b = A.step(), B.step()
         assert abs(a["chi2"] - b["chi2"]) <= 1e-12 * a["chi2"] and a["max_abs_dx"] == b["max_abs_dx"]
+        assert b["t_linearize_ms"] > 0 and b["t_solve_ms"] > 0 and b["t_update_ms"] > 0 and b["t_exchange_ms"] > 0
+        assert b["solver_info"] == 0
+    a, b = A.step_n(4), B.step_n(4)
+    assert abs(a["chi2"] - b["chi2"]) <= 1e-12 * a["chi2"] and b["solver_info"] == 0
     pa, la = A.get_state()
     pb, lb = B.get_state()
     assert np.array_equal(pa, pb) and np.array_equal(la, lb)
