@@ -266,9 +266,11 @@ def main():
     ap.add_argument("--no-gn-other", action="store_true", help="skip timing the other solver ordering")
     ap.add_argument("--no-partition-other", action="store_true", help="N > 1: skip the observations partition")
     ap.add_argument("--tri-steps", type=int, default=20, help="device triangulations timed (0: skip)")
-    ap.add_argument("--exchange", choices=["rccl", "gloo"], default="rccl",
-                    help="N > 1: the exchanges on RCCL (default), or through host memory and gloo (rehearsal of "
-                         "the N-rank path on fewer GPUs, with --same-device)")
+    ap.add_argument("--exchange", choices=["p2p", "rccl", "gloo"], default="p2p",
+                    help="N > 1, subtree partition: the two exchanges per iteration written directly into the other "
+                         "ranks' mailboxes over xGMI (p2p, default; falls back to RCCL if a rank cannot map the "
+                         "others'), RCCL all-gathers, or host memory and gloo (rehearsal of the N-rank path on fewer "
+                         "GPUs, with --same-device)")
     ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (rehearsal only)")
     ap.add_argument("--check-launch", action="store_true",
                     help="launch / rendezvous check only (no GPU): every rank joins the gloo group, rank 0 prints "
@@ -350,9 +352,9 @@ def main():
 
     lpp = args.lanes_per_pose
 
-    def make_handle(partition):
+    def make_handle(partition, rccl=None):
         nccl_id = None
-        if world > 1 and args.exchange == "rccl":
+        if world > 1 and (args.exchange != "gloo" if rccl is None else rccl):
             obj = [bos.nccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             nccl_id = obj[0]
@@ -370,7 +372,36 @@ def main():
             sys.exit(3)
         return h, inf, seen
 
-    S, info, ranks_seen = make_handle(bos.BOS_PARTITION_SUBTREE)
+    S, info, ranks_seen = make_handle(bos.BOS_PARTITION_SUBTREE, rccl=args.exchange == "rccl")
+    exchange = "single GPU" if world == 1 else ("gloo rehearsal" if args.exchange == "gloo" else "rccl")
+    if world > 1 and args.exchange == "p2p":
+        # Every rank maps every other rank's mailbox (HIP IPC), then three GN steps from the initial
+        # guess must give every rank the same chi^2 (each rank combines all ranks' headers, so a
+        # payload that did not arrive intact shows as a difference). All ranks, or none, keep it;
+        # otherwise the handle is rebuilt on RCCL all-gathers.
+        ok, why = 1, ""
+        try:
+            handles = [None] * world
+            dist.all_gather_object(handles, S.p2p_handle())
+            S.p2p_connect(handles)
+            init = S.get_state()
+            chk = [S.step()["chi2"] for _ in range(3)]
+            S.set_state(*init)
+        except bos.BosError as e:
+            ok, why, chk = 0, str(e), [float("nan")] * 3
+        lo, hi = torch.tensor(chk, dtype=torch.float64), torch.tensor(chk, dtype=torch.float64)
+        flag = torch.tensor([ok], dtype=torch.int64)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        if int(flag.item()) == 1 and bool(torch.equal(lo, hi)):
+            exchange = "p2p"
+        else:
+            why = why or ("on another rank" if int(flag.item()) != 1 else "the ranks' chi^2 differ")
+            log(f"rank {rank}: direct exchange unusable ({why}); RCCL all-gathers instead")
+            S.close()
+            S, info, ranks_seen = make_handle(bos.BOS_PARTITION_SUBTREE, rccl=True)
+            exchange = "rccl (direct exchange failed its check)"
 
     # ---- one GN iteration, per exchange mode
     def gloo_allgather(h, which):
@@ -385,7 +416,7 @@ def main():
         h.exchange_upload(1, t.numpy())
 
     def gn_step(h, partition):
-        if world == 1 or args.exchange == "rccl":
+        if world == 1 or args.exchange != "gloo":
             return h.step()
         if partition == bos.BOS_PARTITION_OBSERVATIONS:
             h.step_phase(0)
@@ -427,9 +458,19 @@ def main():
     # ---- the timed region: K GN iterations; the J+H inside them is the headline (K = 0: no GN steps,
     # the J+H builds alone, for profiling runs)
     wall, stats, phase, jh_ms, gn_it_s = 0.0, [], None, None, None
+    ranks_consistent = None
     if args.steps > 0:
         wall, stats = timed_steps(S, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup)
         phase = phases(stats)
+        if world > 1:   # every rank combines the same headers: the chi^2 of every step must agree bit for bit
+            mine = torch.tensor([g["chi2"] for g in stats], dtype=torch.float64)
+            lo, hi = mine.clone(), mine.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            ranks_consistent = bool(torch.equal(lo, hi))
+            if not ranks_consistent:
+                log(f"error: rank {rank}: the ranks' per-step chi^2 differ (exchange {exchange})")
+                sys.exit(3)
         jh_ms = max_over_ranks(phase["t_linearize_ms"])      # the slowest rank's in-step J+H
         gn_it_s = args.steps / wall
         log(f"rank {rank}: {args.steps} GN steps in {wall * 1e3:.1f} ms ({gn_it_s:.0f} it/s); phases {phase}")
@@ -437,7 +478,7 @@ def main():
     # ---- other GN loops (the headline's timed region above is the reference for value)
     gn_c_loop, gn_batched = None, None
     init = S.get_state()
-    if args.steps > 0 and (world == 1 or args.exchange == "rccl"):
+    if args.steps > 0 and (world == 1 or args.exchange != "gloo"):
         gn_c_loop = 1e3 / max_over_ranks(S.time_steps(min(args.steps, 50)))   # bos_step in a C loop
         S.set_state(*init)
         barrier()
@@ -540,11 +581,13 @@ def main():
                             "edges; J+H build " + ("fp32" if precision == bos.BOS_FP32 else "fp64") +
                             " inside full GN iterations (solve fp64, " + args.solver + ")",
                 "poses": P.NP, "landmarks": P.NL, "bearings": int(len(P.b_z)), "odometry": int(len(P.o_z)),
-                "parallelism": (f"subtree-sharded x{world} ({'RCCL' if args.exchange == 'rccl' else 'gloo rehearsal'} "
-                                f"all-gathers; top fronts replicated: {info['top_fronts']})") if world > 1 else "single GPU",
+                "parallelism": (f"subtree-sharded x{world} ({exchange} exchanges; top fronts replicated: "
+                                f"{info['top_fronts']})") if world > 1 else "single GPU",
+                "exchange": exchange,
                 "lanes_per_pose": info["lanes_per_pose"],
             },
             "ranks_seen": ranks_seen,
+            "ranks_consistent": ranks_consistent,
             "devices": 1 if (args.same_device or world == 1) else world,
             "timed_region_ms": wall * 1e3,
             "gn_iters_per_s": gn_it_s,

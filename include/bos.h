@@ -211,6 +211,23 @@ int bos_exchange_size(const struct bos_solver* s, int32_t which, int64_t* double
 int bos_exchange_download(struct bos_solver* s, int32_t which, double* send);
 int bos_exchange_upload(struct bos_solver* s, int32_t which, const double* recv_all_ranks);
 int bos_node_owner(const struct bos_solver* s, int32_t* owner);
+/*
+ * Direct peer exchange (BOS_PARTITION_SUBTREE, round 4): instead of the two ncclAllGather calls,
+ * every rank writes its exchange buffers straight into every rank's receive mailbox (uncached device
+ * memory, mapped into the other ranks' processes by HIP IPC: over xGMI between GPUs) and raises a
+ * per-sender flag there; the receiving rank's next kernel waits for every sender's flag of the
+ * current iteration (bounded: a missing peer aborts the step with BOS_ERR_SOLVER instead of
+ * hanging). Two small launches per exchange, no collective library, and the whole iteration stays
+ * one graph. bos_exchange_p2p_handle writes this rank's mailbox handle (BOS_P2P_HANDLE_BYTES bytes);
+ * the caller gathers every rank's (rank order, e.g. torch.distributed.all_gather_object) and passes
+ * them to bos_exchange_p2p_connect, after which bos_step uses the direct exchange (a communicator
+ * is then not needed; world_size 1 exchanges with itself). All ranks must step in lockstep (each
+ * bos_step / bos_step_n iteration on every rank). BOS_ERR_UNSUPPORTED if the mailbox cannot be
+ * exported (no uncached IPC memory) or on other partitions; callers then keep RCCL.
+ */
+#define BOS_P2P_HANDLE_BYTES 64
+int bos_exchange_p2p_handle(struct bos_solver* s, void* handle);
+int bos_exchange_p2p_connect(struct bos_solver* s, const void* handles);
 
 /* State read/write in stix order (State::poses / landmarks, framework/state.hpp:47-48) */
 int bos_get_state(const struct bos_solver* s, double* pose_xyt, double* landmark_xy);

@@ -74,6 +74,8 @@ typedef struct bos_plan_info {
     int64_t mf_fold_fp32;           /* the folds alone read the pose-landmark / landmark-diagonal
                                        region (mf_fold_reads_fp32): an fp32 build's folds read it
                                        from the fp32 array (bos_system_info.fold_fp32)             */
+    int64_t lm_lanes_consecutive;   /* J+H landmark lanes whose poses are consecutive (p0, p0 + 1,
+                                       ...): they read no pose-index records                      */
 } bos_plan_info;
 
 /* Build the static plan on the host (what bos_create does before touching the GPU) with the

@@ -21,6 +21,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libbos.so")
+# diagnostics tools that load an older build (tools/gn_ab.py) set this: its missing entry points
+# are then left unbound instead of failing the load
+ALLOW_MISSING_SYMBOLS = False
 
 BOS_OK = 0
 BOS_FP64 = 64
@@ -48,8 +51,11 @@ EXPORTED_SYMBOLS = [
     "bos_node_owner",
     "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph", "bos_debug_solver_stamps",
     "bos_time_linearize", "bos_time_triangulate", "bos_time_steps", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
-    "bos_cpu_gn_destroy", "bos_normalized_angle_f64", "bos_normalized_angle_f32",
+    "bos_cpu_gn_destroy", "bos_normalized_angle_f64", "bos_normalized_angle_f32", "bos_exchange_p2p_handle",
+    "bos_exchange_p2p_connect",
 ]
+
+P2P_HANDLE_BYTES = 64   # include/bos.h BOS_P2P_HANDLE_BYTES
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)
@@ -104,7 +110,8 @@ class bos_plan_info(ctypes.Structure):
                 ("shard_roots", ctypes.c_int64), ("shard_ex1_doubles", ctypes.c_int64),
                 ("shard_ex2_doubles", ctypes.c_int64), ("shard_pose_lanes", ctypes.c_int64),
                 ("shard_own_pose_lanes", ctypes.c_int64), ("shard_lm_lanes", ctypes.c_int64),
-                ("shard_update_nodes", ctypes.c_int64), ("mf_fold_fp32", ctypes.c_int64)]
+                ("shard_update_nodes", ctypes.c_int64), ("mf_fold_fp32", ctypes.c_int64),
+                ("lm_lanes_consecutive", ctypes.c_int64)]
 
 
 _lib = None
@@ -179,10 +186,14 @@ def lib():
         "bos_cpu_gn_step": (ctypes.c_int, [vp, _dp]),
         "bos_cpu_gn_get_state": (ctypes.c_int, [vp, _dp, _dp]),
         "bos_cpu_gn_destroy": (None, [vp]),
+        "bos_exchange_p2p_handle": (ctypes.c_int, [vp, ctypes.c_void_p]),
+        "bos_exchange_p2p_connect": (ctypes.c_int, [vp, ctypes.c_void_p]),
         "bos_normalized_angle_f64": (ctypes.c_double, [ctypes.c_double]),
         "bos_normalized_angle_f32": (ctypes.c_float, [ctypes.c_float]),
     }
     for name, (res, args) in sig.items():
+        if ALLOW_MISSING_SYMBOLS and not hasattr(L, name):   # A/B tools loading an older build
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -345,7 +356,7 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
            "mf_levels": info.mf_levels, "mf_max_front": info.mf_max_front, "mf_flops": info.mf_flops,
            "mf_update_bytes": info.mf_update_bytes, "mf_fits": bool(info.mf_fits),
            "mf_max_front_upper": info.mf_max_front_upper, "mf_balance_pct": info.mf_balance_pct,
-           "mf_fold_fp32": bool(info.mf_fold_fp32)}
+           "mf_fold_fp32": bool(info.mf_fold_fp32), "lm_lanes_consecutive": info.lm_lanes_consecutive}
     out.update({k: getattr(info, k) for k, _ in bos_plan_info._fields_ if k.startswith("shard_")})
     if entries:
         nnz = info.nnz_lower
@@ -542,6 +553,19 @@ class Solver:
         observations partition: the element-wise sum over the ranks (all-reduce)."""
         a = np.ascontiguousarray(all_ranks, dtype=np.float64)
         _check(lib().bos_exchange_upload(self._h, which, _ptr(a, ctypes.c_double)), "bos_exchange_upload")
+
+    def p2p_handle(self) -> bytes:
+        """This rank's direct-exchange mailbox handle (bos_exchange_p2p_handle)."""
+        buf = ctypes.create_string_buffer(P2P_HANDLE_BYTES)
+        _check(lib().bos_exchange_p2p_handle(self._h, buf), "bos_exchange_p2p_handle")
+        return buf.raw
+
+    def p2p_connect(self, handles) -> None:
+        """Every rank's handle in rank order (bos_exchange_p2p_connect): bos_step then exchanges
+        directly between the ranks' mailboxes."""
+        blob = b"".join(handles)
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        _check(lib().bos_exchange_p2p_connect(self._h, buf), "bos_exchange_p2p_connect")
 
     def node_owner(self) -> np.ndarray:
         o = np.zeros(self.P.NP + self.P.NL, dtype=np.int32)

@@ -346,9 +346,36 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int g, unsi
     auto at = [&](int j) { return sl + S * min(j, jl); };
     const V2<T> Lm = load2(P.lc + 2 * l);
     T hl[3] = {0, 0, 0}, gl[2] = {0, 0};
+    const T* zp = P.lb_z;
+    const int p0 = P.ll_run ? P.ll_run[g] : -1;
+    if (p0 >= 0) {
+        // consecutive poses p0 + j: every load of the lane is independent of the others (one latency
+        // per pair instead of the index -> pose chain). Paired registers, one pair ahead.
+        const T* xp = P.pc + 4 * (int64_t)p0;
+        auto xat = [&](int j) { return xp + 4 * min(j, jl); };
+        V4<T> XA = load4(xat(0)), XB = load4(xat(1));
+        T zA = zp[at(0)], zB = zp[at(1)];
+        T wA = HAS_W ? P.lb_w[at(0)] : (T)1, wB = HAS_W ? P.lb_w[at(1)] : (T)1;
+        stamp(P.diag_stamps, st, 1);
+        for (int j = 0; j < n; j += 2) {
+            landmark_bearing<T>(P, XA, Lm, zA, wA, hl, gl);
+            XA = load4(xat(j + 2));
+            zA = zp[at(j + 2)];
+            if (HAS_W) wA = P.lb_w[at(j + 2)];
+            if (j + 1 < n) landmark_bearing<T>(P, XB, Lm, zB, wB, hl, gl);
+            XB = load4(xat(j + 3));
+            zB = zp[at(j + 3)];
+            if (HAS_W) wB = P.lb_w[at(j + 3)];
+        }
+        stamp(P.diag_stamps, st, 2);
+        T* hp = P.hval + P.off_ldiag + 3 * l;
+        hp[0] = hl[0] + P.lambda; hp[1] = hl[1]; hp[2] = hl[2] + P.lambda;
+        T* bl = P.b + 3 * P.NP + 2 * l;
+        bl[0] = gl[0]; bl[1] = gl[1];
+        return;
+    }
     // paired register sets as in pose_lanes (reads past the last item clamped to it)
     const int32_t* ip = P.lb_idx;
-    const T* zp = P.lb_z;
     int iA = ip[at(0)], iB = ip[at(1)];
     V4<T> XA = load4(P.pc + 4 * iA), XB = load4(P.pc + 4 * iB);
     T zA = zp[at(0)], zB = zp[at(1)];
@@ -727,11 +754,16 @@ __global__ void index_copy_kernel(const double* src, const int32_t* si, double* 
 }
 
 __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                     double chi_const, int32_t nrob_const, StepStatus* out, StepStatus* mirror) {
+                                     double chi_const, int32_t nrob_const, int32_t* local_info, StepStatus* out,
+                                     StepStatus* mirror) {
     if (threadIdx.x != 0) return;
     double chi = 0.0, m = 0.0;
     long long nr = 0, piv = 0;
     int32_t abort_bits = 0;
+    if (local_info) {   // an exchange-2 wait that timed out (its abort bit arrived after exchange 2's packing)
+        abort_bits |= *local_info & kStepAbort;
+        *local_info &= ~kStepAbort;
+    }
     for (int q = 0; q < world; ++q) {
         chi += recv1[q * c1];
         nr += (long long)recv1[q * c1 + 1];
@@ -763,6 +795,44 @@ __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const doub
 // a J+H launch with no blocks (a rank with an empty share of the observations partition) still
 // stamps its start, so the phase times of that rank read 0 rather than a stale stamp
 __global__ void stamp_kernel(unsigned long long* t) { *t = __builtin_amdgcn_s_memrealtime(); }
+
+// Direct peer exchange (launch_p2p_push / launch_p2p_wait). The mailboxes are uncached device
+// memory, so remote stores land in the receiver's HBM and its reads never see a stale cached line;
+// the pushing wave drains its payload stores (vmcnt) and releases at system scope before the flag.
+__global__ __launch_bounds__(64) void p2p_push_kernel(const double* send, int64_t count, double* const* peers,
+                                                      int64_t data_off, int64_t flag_off, int rank,
+                                                      const uint32_t* epoch) {
+    char* base = reinterpret_cast<char*>(peers[blockIdx.x]);
+    double* dst = reinterpret_cast<double*>(base + data_off) + (int64_t)rank * count;
+    for (int64_t i = threadIdx.x; i < count; i += 64) dst[i] = send[i];
+    const uint32_t e = *epoch;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __threadfence_system();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(base + flag_off + 64 * (int64_t)rank), e, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void p2p_wait_kernel(const char* mailbox, int64_t flag_off, int world,
+                                                      const uint32_t* epoch, int32_t* info, unsigned long long* stamp) {
+    const uint32_t e = *epoch;
+    const int q = threadIdx.x;
+    bool ok = true;
+    if (q < world) {
+        const uint32_t* f = reinterpret_cast<const uint32_t*>(mailbox + flag_off + 64 * (int64_t)q);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {   // 50 ms of the 100 MHz clock
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __threadfence_system();
+    if (!ok) atomicOr(info, kStepAbort);
+    if (stamp && q == 0) *stamp = __builtin_amdgcn_s_memrealtime();
+}
 
 __global__ __launch_bounds__(256) void cache_scrub_kernel(const double* buf, int64_t n, double* sink) {
     double acc = 0.0;
@@ -975,10 +1045,24 @@ hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* 
 }
 
 hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                double chi_const, int32_t nrob_const, StepStatus* out, StepStatus* mirror,
-                                hipStream_t s) {
+                                double chi_const, int32_t nrob_const, int32_t* local_info, StepStatus* out,
+                                StepStatus* mirror, hipStream_t s) {
     hipLaunchKernelGGL(shard_combine_kernel, dim3(1), dim3(64), 0, s, recv1, c1, recv2, c2, world, chi_const, nrob_const,
-                       out, mirror);
+                       local_info, out, mirror);
+    return hipGetLastError();
+}
+
+hipError_t launch_p2p_push(const double* send, int64_t count, double* const* peers, int64_t data_off, int64_t flag_off,
+                           int rank, int world, const uint32_t* epoch, hipStream_t s) {
+    if (world <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(p2p_push_kernel, dim3(world), dim3(64), 0, s, send, count, peers, data_off, flag_off, rank, epoch);
+    return hipGetLastError();
+}
+
+hipError_t launch_p2p_wait(const char* mailbox, int64_t flag_off, int world, const uint32_t* epoch, int32_t* info,
+                           unsigned long long* stamp, hipStream_t s) {
+    if (world <= 0 || world > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(p2p_wait_kernel, dim3(1), dim3(64), 0, s, mailbox, flag_off, world, epoch, info, stamp);
     return hipGetLastError();
 }
 

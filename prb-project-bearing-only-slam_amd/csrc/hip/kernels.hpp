@@ -61,6 +61,10 @@ template <typename T> struct LinParams {
     const int32_t* ll_cnt;    // [NL] per lane
     const int32_t* ll_lm;     // [NL] landmark of each lane (degree-sorted inside 256-lane windows)
     const int32_t* lb_idx;    // [slots] pose
+    // [NL] per lane: the first pose when the lane's poses are consecutive (p0, p0 + 1, ..., no
+    // repeats; BlockLayout::lm_lane_run), else -1. Such a lane reads no index records: its pose
+    // gathers depend on no load. Null: every lane reads its records.
+    const int32_t* ll_run;
     const T* lb_z;            // [slots] measured bearing
     const T* lb_w;
     // outputs
@@ -177,9 +181,19 @@ hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* 
 // terms, max |dx| the max, info: non-positive pivots summed, abort bits or-ed; `aborted` sticky
 // sticky), identical on every rank.
 hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
-                                double chi_const, int32_t nrob_const, StepStatus* out, StepStatus* mirror,
-                                hipStream_t s);
+                                double chi_const, int32_t nrob_const, int32_t* local_info, StepStatus* out,
+                                StepStatus* mirror, hipStream_t s);
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
+// Direct peer exchange (bos_exchange_p2p_connect): push = one wave per receiving rank q copies the
+// `count` doubles of `send` to peers[q] + data_off (bytes) + rank * count doubles, drains its stores,
+// releases at system scope and stores the iteration's epoch (*epoch) into its flag slot there
+// (peers[q] + flag_off + 64 * rank). wait = one wave polls the flags of every sender in its own
+// mailbox (mailbox + flag_off + 64 q, q < world) until they equal *epoch, or marks the step aborted
+// (*info |= kStepAbort) after ~50 ms; *stamp (if set) gets the clock when the last flag is seen.
+hipError_t launch_p2p_push(const double* send, int64_t count, double* const* peers, int64_t data_off, int64_t flag_off,
+                           int rank, int world, const uint32_t* epoch, hipStream_t s);
+hipError_t launch_p2p_wait(const char* mailbox, int64_t flag_off, int world, const uint32_t* epoch, int32_t* info,
+                           unsigned long long* stamp, hipStream_t s);
 // Reduces the J+H kernel's chi^2 / robust-count partials (nrob_part null: chi_part is an
 // all-reduced header [chi^2, robust count], n ignored) (plus the constant terms of odometry
 // self-loops, chi_const / nrob_const) and the box-plus max |dx| partials (when max_part is set; a NaN

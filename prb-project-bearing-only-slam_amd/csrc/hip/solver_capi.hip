@@ -98,7 +98,7 @@ struct bos_solver {
     // J+H work lists (host/plan.hpp BlockLayout)
     int32_t *pw_base = nullptr, *pw_stride = nullptr, *pl_cnt = nullptr, *lw_base = nullptr, *lw_stride = nullptr, *ll_cnt = nullptr, *ll_lm = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_oth = nullptr, *po_blk = nullptr, *csr_src = nullptr,
             *elim_ref = nullptr;
-    int32_t *pb_idx = nullptr, *lb_idx = nullptr;
+    int32_t *pb_idx = nullptr, *lb_idx = nullptr, *ll_run = nullptr;
     void *pb_z = nullptr, *pb_w = nullptr, *lb_z = nullptr, *lb_w = nullptr;
     int pose_blocks = 0;
     // odometry
@@ -136,6 +136,14 @@ struct bos_solver {
     bool lane_identity = false;              // group i runs pose i (one GPU): the kernel skips the table
     int chi_parts = 0;                       // J+H chi^2 partial blocks this rank counts
     double *ex1_send = nullptr, *ex1_recv = nullptr, *ex2_send = nullptr, *ex2_recv = nullptr;
+    // sharded: the receive buffers of both exchanges and the direct exchange's flags live in one
+    // mailbox, uncached device memory (bos_exchange_p2p_connect maps every rank's into the others)
+    char* mailbox = nullptr;
+    bool mailbox_uncached = false;
+    int64_t mb_ex1 = 0, mb_ex2 = 0, mb_flag1 = 0, mb_flag2 = 0;   // byte offsets
+    bool p2p = false;                          // direct peer exchange connected
+    double** d_peers = nullptr;                // [world] every rank's mailbox (own included)
+    std::vector<void*> peer_maps;              // opened IPC mappings (closed at destroy)
     int64_t ex1_count = 0, ex2_count = 0;
     bos::dev::ExSeg *ex1_pack = nullptr, *ex1_unpack = nullptr;
     int n1p = 0, n1u = 0;
@@ -213,7 +221,7 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_oth = s->po_oth; p.po_blk = s->po_blk;
     p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
     p.lw_base = s->lw_base; p.lw_stride = s->lw_stride; p.ll_cnt = s->ll_cnt; p.ll_lm = s->ll_lm;
-    p.lb_idx = s->lb_idx; p.lb_z = (const T*)s->lb_z; p.lb_w = (const T*)s->lb_w;
+    p.lb_idx = s->lb_idx; p.lb_z = (const T*)s->lb_z; p.lb_w = (const T*)s->lb_w; p.ll_run = s->ll_run;
     p.hval = (T*)s->d_val;
     p.b = (T*)s->d_b;
     p.off_ldiag = (int)P.blk.off_ldiag; p.off_pl = (int)P.blk.off_pl; p.off_pp = (int)P.blk.off_pp;
@@ -236,7 +244,9 @@ template <typename T> bos::dev::UpdateParams<T> upd_params(const bos_solver* s) 
     u.pc = (T*)s->d_pc; u.pth = (T*)s->d_pth; u.lc = (T*)s->d_lc;
     u.max_part = s->d_maxpart;
     // sharded: the abort bits of every rank's exchange-2 header (the local word was moved into it)
-    u.info = s->sharded ? nullptr : uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : nullptr;
+    // (sharded: the local word is zeroed by exchange 2's packing; it can then only carry the abort bit
+    // of a direct-exchange wait that timed out)
+    u.info = uses_mf(s) ? bos::dev::mf_info_ptr(s->mf) : nullptr;
     u.ex_hdr = s->sharded ? s->ex2_recv + 1 : nullptr;
     u.ex_stride = s->ex2_count;
     u.ex_world = s->world;
@@ -306,10 +316,26 @@ int setup_shard(bos_solver* s) {
     s->n_upd_local = S.n_upd_local;
     if ((rc = upload(&s->ex1_pack, pack)) || (rc = upload(&s->ex1_unpack, unpack)) || (rc = upload(&s->ex2_bnd, bnd)) ||
         (rc = upload(&s->ex2_usrc, usrc)) || (rc = upload(&s->ex2_udst, udst)) || (rc = upload(&s->upd_nodes, S.upd_nodes)) ||
-        (rc = dalloc(&s->ex1_send, (size_t)s->ex1_count)) || (rc = dalloc(&s->ex1_recv, (size_t)s->ex1_count * W)) ||
-        (rc = dalloc(&s->ex2_send, (size_t)s->ex2_count)) || (rc = dalloc(&s->ex2_recv, (size_t)s->ex2_count * W)) ||
+        (rc = dalloc(&s->ex1_send, (size_t)s->ex1_count)) || (rc = dalloc(&s->ex2_send, (size_t)s->ex2_count)) ||
         (rc = dalloc(&s->abs_part, (size_t)std::max(1, (S.n_upd_local + 255) / 256))))
         return rc;
+    {   // the mailbox: [exchange 1: W x ex1_count][exchange 2: W x ex2_count][flags: 2 x W x 64 B]
+        auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+        s->mb_ex1 = 0;
+        s->mb_ex2 = al((int64_t)W * s->ex1_count * (int64_t)sizeof(double));
+        s->mb_flag1 = s->mb_ex2 + al((int64_t)W * s->ex2_count * (int64_t)sizeof(double));
+        s->mb_flag2 = s->mb_flag1 + 64 * (int64_t)W;
+        const size_t bytes = (size_t)(s->mb_flag2 + 64 * (int64_t)W);
+        if (hipExtMallocWithFlags((void**)&s->mailbox, bytes, hipDeviceMallocUncached) == hipSuccess) {
+            s->mailbox_uncached = true;
+        } else {
+            (void)hipGetLastError();
+            HIP_TRY(hipMalloc((void**)&s->mailbox, bytes));
+        }
+        HIP_TRY(hipMemset(s->mailbox, 0, bytes));
+        s->ex1_recv = reinterpret_cast<double*>(s->mailbox + s->mb_ex1);
+        s->ex2_recv = reinterpret_cast<double*>(s->mailbox + s->mb_ex2);
+    }
     HIP_TRY(hipMemset(s->ex1_send, 0, s->ex1_count * sizeof(double)));
     HIP_TRY(hipMemset(s->ex2_send, 0, s->ex2_count * sizeof(double)));
     return BOS_OK;
@@ -596,7 +622,7 @@ int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
         int32_t nrob_c = 0;
         const double chi_c = self_loop_chi(s, nrob_c);
         HIP_TRY(bos::dev::launch_shard_combine(s->ex1_recv, s->ex1_count, s->ex2_recv, s->ex2_count, s->world, chi_c,
-                                               nrob_c, s->d_status, s->m_status, s->stream));
+                                               nrob_c, bos::dev::mf_info_ptr(s->mf), s->d_status, s->m_status, s->stream));
     }
     return BOS_OK;
 }
@@ -669,12 +695,26 @@ int rccl_allgather(bos_solver* s, const double* send, double* recv, int64_t coun
 
 int finish_step(bos_solver* s, bos_step_stats* st);
 
-// the whole sharded iteration with its collectives (RCCL on the handle's stream); with_jh false:
+// one all-gather of the sharded step: RCCL, or the direct peer exchange (push to every rank's
+// mailbox, then wait for every rank's flag in this rank's)
+int exchange(bos_solver* s, int which) {
+    const double* send = which == 1 ? s->ex1_send : s->ex2_send;
+    double* recv = which == 1 ? s->ex1_recv : s->ex2_recv;
+    const int64_t count = which == 1 ? s->ex1_count : s->ex2_count;
+    if (!s->p2p) return rccl_allgather(s, send, recv, count);
+    const int64_t data = which == 1 ? s->mb_ex1 : s->mb_ex2, flag = which == 1 ? s->mb_flag1 : s->mb_flag2;
+    const uint32_t* epoch = bos::dev::mf_epoch_ptr(s->mf);
+    HIP_TRY(bos::dev::launch_p2p_push(send, count, s->d_peers, data, flag, s->rank, s->world, epoch, s->stream));
+    HIP_TRY(bos::dev::launch_p2p_wait(s->mailbox, flag, s->world, epoch, bos::dev::mf_info_ptr(s->mf), nullptr, s->stream));
+    return BOS_OK;
+}
+
+// the whole sharded iteration with its exchanges (on the handle's stream); with_jh false:
 // everything after the J+H build
 int enqueue_sharded_step(bos_solver* s, bool with_jh = true) {
     int rc;
-    if ((rc = shard_enqueue(s, 0, with_jh)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
-        (rc = shard_enqueue(s, 1)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)))
+    if ((rc = shard_enqueue(s, 0, with_jh)) || (rc = exchange(s, 1)) || (rc = shard_enqueue(s, 1)) ||
+        (rc = exchange(s, 2)))
         return rc;
     return shard_enqueue(s, 2);
 }
@@ -737,8 +777,7 @@ int launch_rccl_step(bos_solver* s, bool sync) {
         HIP_TRY(hipGraphLaunch(s->stail_exec, s->stream));
     } else if (s->obs) {
         if ((rc = obs_phase(s, 0)) || (rc = rccl_allreduce_obs(s)) || (rc = obs_phase(s, 1))) return rc;
-    } else if ((rc = shard_phase0(s)) || (rc = rccl_allgather(s, s->ex1_send, s->ex1_recv, s->ex1_count)) ||
-               (rc = shard_phase1(s)) || (rc = rccl_allgather(s, s->ex2_send, s->ex2_recv, s->ex2_count)) ||
+    } else if ((rc = shard_phase0(s)) || (rc = exchange(s, 1)) || (rc = shard_phase1(s)) || (rc = exchange(s, 2)) ||
                (rc = shard_phase2(s))) {
         return rc;
     }
@@ -747,7 +786,8 @@ int launch_rccl_step(bos_solver* s, bool sync) {
 }
 
 int do_step_sharded(bos_solver* s, bos_step_stats* st, bool sync) {
-    if (!s->comm) return fail(BOS_ERR_INVALID, "sharded handle without a communicator: drive bos_step_phase");
+    if (!s->comm && !s->p2p)
+        return fail(BOS_ERR_INVALID, "sharded handle without a communicator or direct exchange: drive bos_step_phase");
     int rc;
     if ((rc = launch_rccl_step(s, sync))) return rc;
     s->have_dx = true;
@@ -952,17 +992,19 @@ int bos_destroy(bos_solver* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     drop_graph(s);
     void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pw_stride, s->pl_cnt, s->lw_base, s->lw_stride, s->ll_cnt, s->ll_lm,
-                    s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w,
+                    s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w, s->ll_run,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->obs ? nullptr : s->d_b, s->d_sys,
                     s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_status,
                     s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr,
-                    s->scrub, s->lane_pose, s->ex1_send, s->ex1_recv, s->ex2_send, s->ex2_recv, s->ex1_pack,
+                    s->scrub, s->lane_pose, s->ex1_send, s->obs ? s->ex1_recv : nullptr, s->ex2_send, s->mailbox,
+                    s->d_peers, s->ex1_pack,
                     s->ex1_unpack, s->ex2_bnd, s->ex2_usrc, s->ex2_udst, s->upd_nodes, s->abs_part};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (s->h_status) (void)hipHostFree(s->h_status);
+    for (void* m : s->peer_maps) (void)hipIpcCloseMemHandle(m);
     if (s->rf) rocsolver_destroy_rfinfo(s->rf);
     if (s->mf) bos::dev::mf_destroy(s->mf);
     if (s->rb) rocblas_destroy_handle(s->rb);
@@ -1142,7 +1184,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         if ((rc = upload(&s->pw_base, B.pose_lanes.w_base)) || (rc = upload(&s->pl_cnt, B.pose_lanes.cnt)) ||
             (rc = upload(&s->pw_stride, B.pose_lanes.w_stride)) || (rc = upload(&s->lw_stride, B.lm_lanes.w_stride)) ||
             (rc = upload(&s->lw_base, B.lm_lanes.w_base)) || (rc = upload(&s->ll_cnt, B.lm_lanes.cnt)) ||
-            (rc = upload(&s->ll_lm, B.lm_lane_lm)) ||
+            (rc = upload(&s->ll_lm, B.lm_lane_lm)) || (rc = upload(&s->ll_run, B.lm_lane_run)) ||
             (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, po_ent)) ||
             (rc = upload(&s->po_oth, po_oth)) ||
             (rc = upload(&s->po_blk, po_blk)) || (rc = upload(&s->pb_idx, pbi)) || (rc = upload_Tv(&s->pb_z, pbz)) ||
@@ -1459,6 +1501,53 @@ int bos_exchange_upload(bos_solver* s, int32_t which, const double* recv_all) {
     // subtree partition: every rank's buffer (all-gather); observations partition: their sum
     const int64_t c = s->obs ? s->ex1_count : (which == 1 ? s->ex1_count : s->ex2_count) * s->world;
     HIP_TRY(hipMemcpy(which == 1 ? s->ex1_recv : s->ex2_recv, recv_all, c * sizeof(double), hipMemcpyHostToDevice));
+    return BOS_OK;
+}
+
+int bos_exchange_p2p_handle(bos_solver* s, void* handle) {
+    if (!s || !handle) return fail(BOS_ERR_INVALID, "null argument");
+    if (!s->sharded) return fail(BOS_ERR_UNSUPPORTED, "direct exchange: subtree-sharded handles only");
+    if (!s->mailbox_uncached) return fail(BOS_ERR_UNSUPPORTED, "direct exchange: no uncached device memory for the mailbox");
+    HIP_TRY(hipSetDevice(s->device));
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, s->mailbox);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(BOS_ERR_UNSUPPORTED, std::string("direct exchange: hipIpcGetMemHandle: ") + hipGetErrorString(e));
+    }
+    static_assert(sizeof(h) == BOS_P2P_HANDLE_BYTES, "IPC handle size");
+    std::memcpy(handle, &h, sizeof(h));
+    return BOS_OK;
+}
+
+int bos_exchange_p2p_connect(bos_solver* s, const void* handles) {
+    if (!s || !handles) return fail(BOS_ERR_INVALID, "null argument");
+    if (!s->sharded || !s->mailbox_uncached) return fail(BOS_ERR_UNSUPPORTED, "direct exchange: not available on this handle");
+    if (s->p2p) return fail(BOS_ERR_INVALID, "direct exchange: already connected");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    std::vector<double*> peers(s->world, nullptr);
+    for (int q = 0; q < s->world; ++q) {
+        if (q == s->rank) { peers[q] = reinterpret_cast<double*>(s->mailbox); continue; }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, static_cast<const char*>(handles) + (size_t)q * BOS_P2P_HANDLE_BYTES, sizeof(h));
+        void* p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess || !p) {
+            (void)hipGetLastError();
+            for (void* m : s->peer_maps) (void)hipIpcCloseMemHandle(m);
+            s->peer_maps.clear();
+            return fail(BOS_ERR_UNSUPPORTED, std::string("direct exchange: hipIpcOpenMemHandle (rank ") + std::to_string(q) +
+                                                 "): " + hipGetErrorString(e));
+        }
+        s->peer_maps.push_back(p);
+        peers[q] = reinterpret_cast<double*>(p);
+    }
+    int rc;
+    if ((rc = upload(&s->d_peers, peers))) return rc;
+    drop_graph(s);   // the next step captures the iteration with the direct exchange
+    s->rccl_capture_failed = false;
+    s->p2p = true;
     return BOS_OK;
 }
 

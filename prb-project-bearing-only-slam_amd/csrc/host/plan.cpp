@@ -701,18 +701,32 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
         }
     }
     make_lane_lists(G * L, lane_ptr, pitems, B.pose_lanes, true);
-    {   // landmark lanes in the shard's order, degree-sorted inside each window (ties by id: deterministic)
+    {   // landmark lanes in the shard's order; inside each window consecutive-pose lanes first, then
+        // by degree (ties by the shard's order: deterministic)
         B.lm_lane_lm = P.shard.lane_lms;
         const int NLL = (int)B.lm_lane_lm.size();
         auto deg = [&](int l) { return lb_ptr[l + 1] - lb_ptr[l]; };
+        auto run0 = [&](int l) -> int32_t {   // poses p0, p0 + 1, ... (sorted by pose above)
+            if (deg(l) < 1) return -1;
+            const int32_t p0 = pi.b_pose[lb_obs[lb_ptr[l]]];
+            for (int i = lb_ptr[l] + 1; i < lb_ptr[l + 1]; ++i)
+                if (pi.b_pose[lb_obs[i]] != p0 + (i - lb_ptr[l])) return -1;
+            return p0;
+        };
         for (int w0 = 0; w0 < NLL; w0 += kLmWindow)
             std::stable_sort(B.lm_lane_lm.begin() + w0, B.lm_lane_lm.begin() + std::min(NLL, w0 + kLmWindow),
-                             [&](int a, int b) { return deg(a) > deg(b); });
+                             [&](int a, int b) {
+                                 const bool ra = run0(a) >= 0, rb = run0(b) >= 0;
+                                 if (ra != rb) return ra;
+                                 return deg(a) > deg(b);
+                             });
         std::vector<int32_t> lptr(NLL + 1, 0), litems;
+        B.lm_lane_run.assign(NLL, -1);
         for (int g = 0; g < NLL; ++g) {
             const int l = B.lm_lane_lm[g];
             litems.insert(litems.end(), lb_obs.begin() + lb_ptr[l], lb_obs.begin() + lb_ptr[l + 1]);
             lptr[g + 1] = (int32_t)litems.size();
+            B.lm_lane_run[g] = run0(l);
         }
         make_lane_lists(NLL, lptr, litems, B.lm_lanes, false);
     }

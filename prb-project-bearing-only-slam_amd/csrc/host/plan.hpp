@@ -91,9 +91,12 @@ struct BlockLayout {
     LaneLists pose_lanes;               // lanes = lane_pose.size() * lpp
     LaneLists lm_lanes;                 // lane g -> landmark lm_lane_lm[g]
     // landmark of each landmark lane (Shard::lane_lms): inside each window of kLmWindow lanes the
-    // window's landmarks sorted by degree (descending), so the lanes of a wave walk lists of similar
-    // length
+    // window's landmarks sorted by consecutive-pose lanes first, then degree (descending), so the
+    // lanes of a wave take one path and walk lists of similar length
     std::vector<int32_t> lm_lane_lm;
+    // [lanes] the landmark lane's first pose when its poses are consecutive stix (p0, p0 + 1, ...,
+    // no repeated pose), else -1 (LinParams::ll_run)
+    std::vector<int32_t> lm_lane_run;
     std::vector<int32_t> ub_ptr;        // [NP + 1] pose-landmark blocks of each pose
     std::vector<int32_t> ub_lm;         // [nub] landmark of each pose-landmark block (ascending per pose)
     std::vector<int32_t> ub_slot;       // [nub] bearing slot holding the block

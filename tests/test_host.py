@@ -180,6 +180,22 @@ def test_plan_pattern_matches_oracle(which):
     assert set(perm[info["n"]:].tolist()) == {3 * P.fixed, 3 * P.fixed + 1, 3 * P.fixed + 2}
 
 
+@pytest.mark.parametrize("which", ["mini", "c1", "c2"])
+def test_consecutive_pose_landmark_lanes(which):
+    """A landmark lane whose poses are consecutive (p0, p0 + 1, ..., no repeat) reads no pose
+    records (LinParams::ll_run); the plan's count equals a direct count over the bearings."""
+    P = {"mini": lambda: bos.load_g2o(MINI), "c1": lambda: bos.load_g2o(C1),
+         "c2": lambda: bos.synthetic(1000, 2000, 20)}[which]()
+    want = 0
+    for lm in range(P.lm_xy.shape[0]):
+        poses = np.sort(P.b_pose[P.b_lm == lm])
+        want += poses.size > 0 and bool(np.all(poses == poses[0] + np.arange(poses.size)))
+    got = bos.plan_inspect(P, solver=bos.BOS_SOLVER_SCHUR)["lm_lanes_consecutive"]
+    assert got == want
+    if which == "c2":   # the synthetic generator's windows are consecutive poses
+        assert got == P.lm_xy.shape[0]
+
+
 @pytest.mark.parametrize("solver", ["supernodal", "schur"])
 @pytest.mark.parametrize("which", ["c1", "c2"])
 def test_multifrontal_structure_solves_like_scipy(which, solver):

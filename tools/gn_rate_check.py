@@ -16,6 +16,7 @@ if sys.argv[1] != "--child":
         subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib], check=True, timeout=120)
     sys.exit(0)
 bos.LIB_PATH = os.path.abspath(sys.argv[2])
+bos.ALLOW_MISSING_SYMBOLS = True
 P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
 S = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, device=0)
 init = S.get_state()

@@ -10,6 +10,7 @@ if sys.argv[1] == "--child":
     import numpy as np
     import bos
     bos.LIB_PATH = os.path.abspath(sys.argv[2])
+    bos.ALLOW_MISSING_SYMBOLS = True
     P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
     S = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, device=0)
     st = S.linearize()

@@ -10,6 +10,7 @@ import numpy as np  # noqa: E402
 import bos  # noqa: E402
 
 bos.LIB_PATH = os.path.abspath(sys.argv[1])
+bos.ALLOW_MISSING_SYMBOLS = True
 prec = bos.BOS_FP64 if len(sys.argv) > 2 and sys.argv[2] == "fp64" else bos.BOS_FP32
 P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
 S = bos.Solver(P, precision=prec, device=0, lanes_per_pose=int(os.environ.get("BOS_LPP", "0")))

@@ -58,7 +58,10 @@ for W in worlds:
     wall = {}
     if W == 1:   # host-clock rate of the one-rank RCCL path against the plain one-GPU step
         S1 = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=LPP)
-        for name, h in (("rccl_one_rank", S[0]), ("one_gpu", S1)):
+        S2 = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, rank=0, world_size=1,
+                        nccl_id=bos.nccl_unique_id(), lanes_per_pose=LPP)
+        S2.p2p_connect([S2.p2p_handle()])
+        for name, h in (("rccl_one_rank", S[0]), ("p2p_one_rank", S2), ("one_gpu", S1)):
             init = h.get_state()
             h.step()
             h.synchronize()
@@ -68,9 +71,13 @@ for W in worlds:
             h.synchronize()
             wall[name] = (time.perf_counter() - t0) / 20 * 1e3
             h.set_state(*init)
+        st2 = [S2.step() for _ in range(5)]
+        wall["p2p_one_rank_exchange_ms"] = float(np.median([g["t_exchange_ms"] for g in st2]))
         S1.close()
-        print(f"W=1 wall ms/step: RCCL one-rank path {wall['rccl_one_rank']:.3f}, one GPU {wall['one_gpu']:.3f}",
-              flush=True)
+        S2.close()
+        print(f"W=1 wall ms/step: RCCL one-rank path {wall['rccl_one_rank']:.3f}, direct-exchange one-rank path "
+              f"{wall['p2p_one_rank']:.3f} (exchanges {wall['p2p_one_rank_exchange_ms']:.3f}), one GPU "
+              f"{wall['one_gpu']:.3f}", flush=True)
     info = [h.system_info() for h in S]
     out[W] = {"create_s": t_create, "jh_ms": a[:, 0].tolist(), "solve_ms": a[:, 1].tolist(), "update_ms": a[:, 2].tolist(),
               "exchange_ms": a[:, 3].tolist(),

@@ -39,6 +39,7 @@ import bos  # noqa: E402
 
 if os.environ.get("BOS_LIB"):   # a library variant (experiments)
     bos.LIB_PATH = os.path.abspath(os.environ["BOS_LIB"])
+    bos.ALLOW_MISSING_SYMBOLS = True
 
 P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
 S = bos.Solver(P, precision=bos.BOS_FP32, device=0)
