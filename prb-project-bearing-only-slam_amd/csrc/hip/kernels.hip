@@ -678,9 +678,33 @@ template <typename T> __global__ __launch_bounds__(256) void triangulate_kernel(
     P.lc[2 * (int64_t)l + 1] = (T)oy;
 }
 
+// lanes q < world of the block poll sender q's flag in this rank's mailbox until it equals the
+// iteration's epoch (or mark the step aborted after ~50 ms); then the whole block acquires
+__device__ __forceinline__ void p2p_wait_block(const P2PWait& w) {
+    const int q = threadIdx.x;
+    if (q < w.world) {
+        const uint32_t e = *w.epoch;
+        const uint32_t* f = reinterpret_cast<const uint32_t*>(w.mailbox + w.flag_off + 64 * (int64_t)q);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {   // 50 ms of the 100 MHz clock
+                atomicOr(w.info, kStepAbort);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    __threadfence_system();
+}
+
 // one segment per blockIdx.y, its elements grid-strided over blockIdx.x
+// (w.mailbox set: every block first waits for the direct exchange's flags, and the stamp marks the
+// end of that wait)
 template <typename T>
-__global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* segs, unsigned long long* stamp) {
+__global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* segs, unsigned long long* stamp,
+                                const P2PWait w) {
+    if (w.mailbox) p2p_wait_block(w);
     if (stamp && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
     const ExSeg g = segs[blockIdx.y];
     T* const base[4] = {val, b, send, recv};
@@ -690,8 +714,10 @@ __global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* seg
         dst[i] = src[i];
 }
 
-__global__ __launch_bounds__(256) void shard_header1_kernel(const double* chi_part, const int32_t* nrob_part, int n,
-                                                           double* send1, unsigned long long* stamp) {
+// the exchange-1 header of a 256-thread block: this rank's chi^2 and robust count, summed in a fixed
+// order (valid in thread 0)
+__device__ __forceinline__ void header1_block(const double* chi_part, const int32_t* nrob_part, int n, double& chi,
+                                              long long& nrob) {
     __shared__ double sc[256];
     __shared__ long long sr[256];
     double c = 0.0;
@@ -704,9 +730,18 @@ __global__ __launch_bounds__(256) void shard_header1_kernel(const double* chi_pa
         if ((int)threadIdx.x < o) { sc[threadIdx.x] += sc[threadIdx.x + o]; sr[threadIdx.x] += sr[threadIdx.x + o]; }
         __syncthreads();
     }
+    chi = sc[0];
+    nrob = sr[0];
+}
+
+__global__ __launch_bounds__(256) void shard_header1_kernel(const double* chi_part, const int32_t* nrob_part, int n,
+                                                           double* send1, unsigned long long* stamp) {
+    double c;
+    long long r;
+    header1_block(chi_part, nrob_part, n, c, r);
     if (threadIdx.x == 0) {
-        send1[0] = sc[0];
-        send1[1] = (double)sr[0];
+        send1[0] = c;
+        send1[1] = (double)r;
         if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
     }
 }
@@ -729,25 +764,34 @@ __global__ __launch_bounds__(256) void node_absmax_kernel(const double* x, const
     if (threadIdx.x == 0) part[blockIdx.x] = nan_max(nan_max(sm[0], sm[1]), nan_max(sm[2], sm[3]));
 }
 
-// block 0 thread 0: header (max of the partials, the solver word, which is then zeroed); every
+// block 0: header (max of the partials, reduced by the whole block — one thread walking ~1 200
+// partials serially took 109 us at config 3 — and the solver word, which is then zeroed); every
 // thread: the boundary payload
 __global__ __launch_bounds__(256) void shard_pack2_kernel(const double* x, const double* part, int n_part, int32_t* info,
                                                           const int32_t* bnd, int n_bnd, double* send2,
                                                           unsigned long long* stamp) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t == 0) {
-        if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x == 0) {   // block-uniform branch
+        if (stamp && t == 0) *stamp = __builtin_amdgcn_s_memrealtime();
         double m = 0.0;
-        for (int i = 0; i < n_part; ++i) m = nan_max(m, part[i]);
-        send2[0] = m;
-        send2[1] = (double)*info;
-        *info = 0;
+        for (int i = threadIdx.x; i < n_part; i += 256) m = nan_max(m, part[i]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o));
+        __shared__ double sm[4];
+        if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (t == 0) {
+            send2[0] = nan_max(nan_max(sm[0], sm[1]), nan_max(sm[2], sm[3]));
+            send2[1] = (double)*info;
+            *info = 0;
+        }
     }
     for (int i = t; i < n_bnd; i += gridDim.x * blockDim.x) send2[2 + i] = x[bnd[i]];
 }
 
 __global__ void index_copy_kernel(const double* src, const int32_t* si, double* dst, const int32_t* di, int64_t n,
-                                  unsigned long long* stamp) {
+                                  unsigned long long* stamp, const P2PWait w) {
+    if (w.mailbox) p2p_wait_block(w);
     if (stamp && blockIdx.x == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         dst[di ? di[i] : i] = src[si ? si[i] : i];
@@ -796,42 +840,38 @@ __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const doub
 // stamps its start, so the phase times of that rank read 0 rather than a stale stamp
 __global__ void stamp_kernel(unsigned long long* t) { *t = __builtin_amdgcn_s_memrealtime(); }
 
-// Direct peer exchange (launch_p2p_push / launch_p2p_wait). The mailboxes are uncached device
-// memory, so remote stores land in the receiver's HBM and its reads never see a stale cached line;
-// the pushing wave drains its payload stores (vmcnt) and releases at system scope before the flag.
-__global__ __launch_bounds__(64) void p2p_push_kernel(const double* send, int64_t count, double* const* peers,
-                                                      int64_t data_off, int64_t flag_off, int rank,
-                                                      const uint32_t* epoch) {
+// Direct peer exchange (launch_p2p_push, P2PWait). The mailboxes are uncached device memory, so
+// remote stores land in the receiver's HBM and its reads never see a stale cached line; the pushing
+// block drains its payload stores (vmcnt) and releases at system scope before its flag.
+__global__ __launch_bounds__(256) void p2p_push_kernel(const double* send, int64_t count, double* const* peers,
+                                                       int64_t data_off, int64_t flag_off, int rank,
+                                                       const uint32_t* epoch, const double* chi_part,
+                                                       const int32_t* nrob_part, int n_parts,
+                                                       unsigned long long* stamp) {
+    if (stamp && blockIdx.x == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
     char* base = reinterpret_cast<char*>(peers[blockIdx.x]);
     double* dst = reinterpret_cast<double*>(base + data_off) + (int64_t)rank * count;
-    for (int64_t i = threadIdx.x; i < count; i += 64) dst[i] = send[i];
+    int64_t i0 = 0;
+    if (chi_part) {   // exchange 1: the header computed here (every block the same sums), then the payload
+        double c;
+        long long r;
+        header1_block(chi_part, nrob_part, n_parts, c, r);
+        if (threadIdx.x == 0) { dst[0] = c; dst[1] = (double)r; }
+        i0 = kExHeader;
+    }
+    for (int64_t i = i0 + threadIdx.x; i < count; i += 256) dst[i] = send[i];
     const uint32_t e = *epoch;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __threadfence_system();
+    __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_store(reinterpret_cast<uint32_t*>(base + flag_off + 64 * (int64_t)rank), e, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(64) void p2p_wait_kernel(const char* mailbox, int64_t flag_off, int world,
-                                                      const uint32_t* epoch, int32_t* info, unsigned long long* stamp) {
-    const uint32_t e = *epoch;
-    const int q = threadIdx.x;
-    bool ok = true;
-    if (q < world) {
-        const uint32_t* f = reinterpret_cast<const uint32_t*>(mailbox + flag_off + 64 * (int64_t)q);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {   // 50 ms of the 100 MHz clock
-                ok = false;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __threadfence_system();
-    if (!ok) atomicOr(info, kStepAbort);
-    if (stamp && q == 0) *stamp = __builtin_amdgcn_s_memrealtime();
+__global__ __launch_bounds__(64) void p2p_wait_kernel(const P2PWait w, unsigned long long* stamp) {
+    p2p_wait_block(w);
+    if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ __launch_bounds__(256) void cache_scrub_kernel(const double* buf, int64_t n, double* sink) {
@@ -992,14 +1032,16 @@ template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStr
 
 template <typename T>
 hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s,
-                           unsigned long long* stamp) {
+                           unsigned long long* stamp, const P2PWait& w) {
+    if (w.mailbox && (w.world <= 0 || w.world > 64)) return hipErrorInvalidValue;
     if (nseg == 0 || max_len == 0) {
-        if (stamp) hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, s, stamp);
+        if (w.mailbox) hipLaunchKernelGGL(p2p_wait_kernel, dim3(1), dim3(64), 0, s, w, stamp);
+        else if (stamp) hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, s, stamp);
         return hipGetLastError();
     }
     const int64_t bx = std::min<int64_t>((max_len + 255) / 256, 256);
     hipLaunchKernelGGL((seg_copy_kernel<T>), dim3((unsigned)bx, (unsigned)nseg), dim3(256), 0, s, val, b, send, recv, segs,
-                       stamp);
+                       stamp, w);
     return hipGetLastError();
 }
 
@@ -1034,13 +1076,15 @@ hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes
 }
 
 hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* dst, const int32_t* dst_idx, int64_t n,
-                             hipStream_t s, unsigned long long* stamp) {
+                             hipStream_t s, unsigned long long* stamp, const P2PWait& w) {
+    if (w.mailbox && (w.world <= 0 || w.world > 64)) return hipErrorInvalidValue;
     if (n == 0) {
-        if (stamp) hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, s, stamp);
+        if (w.mailbox) hipLaunchKernelGGL(p2p_wait_kernel, dim3(1), dim3(64), 0, s, w, stamp);
+        else if (stamp) hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, s, stamp);
         return hipGetLastError();
     }
     const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
-    hipLaunchKernelGGL(index_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, src_idx, dst, dst_idx, n, stamp);
+    hipLaunchKernelGGL(index_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, src_idx, dst, dst_idx, n, stamp, w);
     return hipGetLastError();
 }
 
@@ -1053,16 +1097,11 @@ hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* r
 }
 
 hipError_t launch_p2p_push(const double* send, int64_t count, double* const* peers, int64_t data_off, int64_t flag_off,
-                           int rank, int world, const uint32_t* epoch, hipStream_t s) {
-    if (world <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(p2p_push_kernel, dim3(world), dim3(64), 0, s, send, count, peers, data_off, flag_off, rank, epoch);
-    return hipGetLastError();
-}
-
-hipError_t launch_p2p_wait(const char* mailbox, int64_t flag_off, int world, const uint32_t* epoch, int32_t* info,
-                           unsigned long long* stamp, hipStream_t s) {
-    if (world <= 0 || world > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(p2p_wait_kernel, dim3(1), dim3(64), 0, s, mailbox, flag_off, world, epoch, info, stamp);
+                           int rank, int world, const uint32_t* epoch, const double* chi_part, const int32_t* nrob_part,
+                           int n_parts, unsigned long long* stamp, hipStream_t s) {
+    if (world <= 0 || (chi_part && count < kExHeader)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(p2p_push_kernel, dim3(world), dim3(256), 0, s, send, count, peers, data_off, flag_off, rank, epoch,
+                       chi_part, nrob_part, n_parts, stamp);
     return hipGetLastError();
 }
 
@@ -1143,9 +1182,9 @@ template hipError_t launch_boxplus<double>(const UpdateParams<double>&, hipStrea
 template hipError_t launch_boxplus<float>(const UpdateParams<float>&, hipStream_t);
 template hipError_t launch_triangulate<double>(const TriParams<double>&, hipStream_t);
 template hipError_t launch_seg_copy<double>(double*, double*, double*, double*, const ExSeg*, int, int64_t, hipStream_t,
-                                            unsigned long long*);
+                                            unsigned long long*, const P2PWait&);
 template hipError_t launch_seg_copy<float>(float*, float*, float*, float*, const ExSeg*, int, int64_t, hipStream_t,
-                                           unsigned long long*);
+                                           unsigned long long*, const P2PWait&);
 template hipError_t launch_triangulate<float>(const TriParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);

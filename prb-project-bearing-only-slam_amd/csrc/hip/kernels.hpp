@@ -151,10 +151,23 @@ struct ExSeg {
     int32_t src_kind, dst_kind;
 };
 
-// *stamp (if set) gets the realtime clock at the launch's start
+// A wait for the direct exchange's flags (bos_exchange_p2p_connect), fused into the launch that
+// reads the received data: in every block, lanes q < world poll sender q's flag (mailbox + flag_off
+// + 64 q) until it equals the iteration's epoch (*epoch), or mark the step aborted (*info |=
+// kStepAbort) after ~50 ms; then the block reads. mailbox null: no wait.
+struct P2PWait {
+    const char* mailbox = nullptr;
+    int64_t flag_off = 0;
+    int world = 0;
+    const uint32_t* epoch = nullptr;
+    int32_t* info = nullptr;
+};
+
+// *stamp (if set) gets the realtime clock at the launch's start (after the wait, with one); with
+// nothing to copy, a wait (or the stamp) still runs
 template <typename T>
 hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s,
-                           unsigned long long* stamp = nullptr);
+                           unsigned long long* stamp = nullptr, const P2PWait& w = P2PWait());
 
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);
@@ -162,6 +175,7 @@ template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStr
 
 // Sharded GN step (host/plan.hpp Shard, hip/solver_capi.hip). Exchange buffers are doubles with a
 // kExHeader-double header per rank.
+constexpr int kExHeader = 2;   // = bos::kExHeader (host/plan.hpp)
 // Exchange 1 header: this rank's chi^2 and robust count (sums of the J+H partials [0, n_parts));
 // *stamp (if set) gets the realtime clock at its end.
 hipError_t launch_shard_header1(const double* chi_part, const int32_t* nrob_part, int n_parts, double* send1,
@@ -175,8 +189,9 @@ hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes
                               int32_t* info, const int32_t* bnd, int n_bnd, double* part, double* send2,
                               hipStream_t s, unsigned long long* stamp = nullptr);
 // dst[dst_idx[i]] = src[src_idx[i]], i < n; *stamp (if set) gets the realtime clock at the start
+// (after the wait, with one)
 hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* dst, const int32_t* dst_idx, int64_t n,
-                             hipStream_t s, unsigned long long* stamp = nullptr);
+                             hipStream_t s, unsigned long long* stamp = nullptr, const P2PWait& w = P2PWait());
 // All ranks' headers -> *out (chi^2 and robust count summed in rank order plus the self-loop
 // terms, max |dx| the max, info: non-positive pivots summed, abort bits or-ed; `aborted` sticky
 // sticky), identical on every rank.
@@ -184,16 +199,15 @@ hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* r
                                 double chi_const, int32_t nrob_const, int32_t* local_info, StepStatus* out,
                                 StepStatus* mirror, hipStream_t s);
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
-// Direct peer exchange (bos_exchange_p2p_connect): push = one wave per receiving rank q copies the
+// Direct peer exchange (bos_exchange_p2p_connect): one block per receiving rank q copies the
 // `count` doubles of `send` to peers[q] + data_off (bytes) + rank * count doubles, drains its stores,
 // releases at system scope and stores the iteration's epoch (*epoch) into its flag slot there
-// (peers[q] + flag_off + 64 * rank). wait = one wave polls the flags of every sender in its own
-// mailbox (mailbox + flag_off + 64 q, q < world) until they equal *epoch, or marks the step aborted
-// (*info |= kStepAbort) after ~50 ms; *stamp (if set) gets the clock when the last flag is seen.
+// (peers[q] + flag_off + 64 * rank); the receiver waits with a P2PWait. chi_part set (exchange 1):
+// the first kExHeader doubles are the header of launch_shard_header1, computed by the push itself
+// (no header launch). *stamp (if set) gets the realtime clock at the start.
 hipError_t launch_p2p_push(const double* send, int64_t count, double* const* peers, int64_t data_off, int64_t flag_off,
-                           int rank, int world, const uint32_t* epoch, hipStream_t s);
-hipError_t launch_p2p_wait(const char* mailbox, int64_t flag_off, int world, const uint32_t* epoch, int32_t* info,
-                           unsigned long long* stamp, hipStream_t s);
+                           int rank, int world, const uint32_t* epoch, const double* chi_part, const int32_t* nrob_part,
+                           int n_parts, unsigned long long* stamp, hipStream_t s);
 // Reduces the J+H kernel's chi^2 / robust-count partials (nrob_part null: chi_part is an
 // all-reduced header [chi^2, robust count], n ignored) (plus the constant terms of odometry
 // self-loops, chi_const / nrob_const) and the box-plus max |dx| partials (when max_part is set; a NaN

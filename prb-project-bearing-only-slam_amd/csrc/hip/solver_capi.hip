@@ -191,6 +191,7 @@ struct bos_solver {
 };
 
 static_assert(bos::dev::kStepAbort == bos::dev::kMfStall, "solver abort bit");
+static_assert(bos::dev::kExHeader == bos::kExHeader, "exchange header size");
 
 namespace {
 // both multifrontal orderings (nested dissection / landmarks-first Schur) share the GPU engine
@@ -595,6 +596,19 @@ int read_stats(bos_solver* s, bos_step_stats* st, int32_t* aborted = nullptr, bo
 // backward, exchange-2 buffer packed (max |x| of own + top, solver word, boundary solution)
 // phase 2: boundary solution in place, box-plus of own + top + boundary nodes (skipped when any
 // rank's factorization aborted: every rank's header), step status combined from every rank's headers
+// the wait for exchange `which` of the direct exchange, fused into the launch that reads it (none
+// without the direct exchange)
+bos::dev::P2PWait p2p_wait(const bos_solver* s, int which) {
+    bos::dev::P2PWait w;
+    if (!s->p2p) return w;
+    w.mailbox = s->mailbox;
+    w.flag_off = which == 1 ? s->mb_flag1 : s->mb_flag2;
+    w.world = s->world;
+    w.epoch = bos::dev::mf_epoch_ptr(s->mf);
+    w.info = bos::dev::mf_info_ptr(s->mf);
+    return w;
+}
+
 int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
     int rc;
     double* U = bos::dev::mf_update_ptr(s->mf);
@@ -604,11 +618,12 @@ int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
         if ((rc = enqueue_solver_inputs(s))) return rc;   // opens this step's flow epoch
         HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
         HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_pack, s->n1p, s->maxlen1p, s->stream));
-        HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream,
-                                               s->d_status->stamp + 4));
+        if (!s->p2p)   // (the direct exchange's push computes the header itself)
+            HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream,
+                                                   s->d_status->stamp + 4));
     } else if (phase == 1) {
         HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_unpack, s->n1u, s->maxlen1u, s->stream,
-                                                  s->d_status->stamp + 5));
+                                                  s->d_status->stamp + 5, p2p_wait(s, 1)));
         HIP_TRY(bos::dev::mf_factor(s->mf, 1, mf_matrix(s), s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, 1, s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, 0, s->d_rhs, s->stream));
@@ -617,7 +632,7 @@ int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
                                              s->stream, s->d_status->stamp + 6));
     } else {
         HIP_TRY(bos::dev::launch_index_copy(s->ex2_recv, s->ex2_usrc, s->d_rhs, s->ex2_udst, s->n_bnd_remote, s->stream,
-                                            s->d_status->stamp + 7));
+                                            s->d_status->stamp + 7, p2p_wait(s, 2)));
         if ((rc = enqueue_update(s))) return rc;
         int32_t nrob_c = 0;
         const double chi_c = self_loop_chi(s, nrob_c);
@@ -695,8 +710,9 @@ int rccl_allgather(bos_solver* s, const double* send, double* recv, int64_t coun
 
 int finish_step(bos_solver* s, bos_step_stats* st);
 
-// one all-gather of the sharded step: RCCL, or the direct peer exchange (push to every rank's
-// mailbox, then wait for every rank's flag in this rank's)
+// one all-gather of the sharded step: RCCL, or the direct peer exchange's push to every rank's
+// mailbox (exchange 1's push also computes the header; the receiving side's wait is fused into the
+// launch that reads the data, p2p_wait)
 int exchange(bos_solver* s, int which) {
     const double* send = which == 1 ? s->ex1_send : s->ex2_send;
     double* recv = which == 1 ? s->ex1_recv : s->ex2_recv;
@@ -704,8 +720,12 @@ int exchange(bos_solver* s, int which) {
     if (!s->p2p) return rccl_allgather(s, send, recv, count);
     const int64_t data = which == 1 ? s->mb_ex1 : s->mb_ex2, flag = which == 1 ? s->mb_flag1 : s->mb_flag2;
     const uint32_t* epoch = bos::dev::mf_epoch_ptr(s->mf);
-    HIP_TRY(bos::dev::launch_p2p_push(send, count, s->d_peers, data, flag, s->rank, s->world, epoch, s->stream));
-    HIP_TRY(bos::dev::launch_p2p_wait(s->mailbox, flag, s->world, epoch, bos::dev::mf_info_ptr(s->mf), nullptr, s->stream));
+    if (which == 1)
+        HIP_TRY(bos::dev::launch_p2p_push(send, count, s->d_peers, data, flag, s->rank, s->world, epoch, s->d_chi_part,
+                                          s->d_nrob_part, s->chi_parts, s->d_status->stamp + 4, s->stream));
+    else
+        HIP_TRY(bos::dev::launch_p2p_push(send, count, s->d_peers, data, flag, s->rank, s->world, epoch, nullptr, nullptr, 0,
+                                          nullptr, s->stream));
     return BOS_OK;
 }
 
