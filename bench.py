@@ -509,7 +509,12 @@ def main():
     # ---- N > 1: the north star's partition (observations by measurement order, all-reduce of H, b)
     part_obs = None
     if world > 1 and not args.no_partition_other and args.steps > 0:
-        S3, _, seen3 = make_handle(bos.BOS_PARTITION_OBSERVATIONS)
+        try:   # (a secondary leg: an RCCL failure here is reported in the line, not fatal to it)
+            S3, _, seen3 = make_handle(bos.BOS_PARTITION_OBSERVATIONS)
+        except bos.BosError as e:
+            log(f"rank {rank}: observations partition unavailable: {e}")
+            S3, part_obs = None, {"error": str(e)}
+    if world > 1 and not args.no_partition_other and args.steps > 0 and S3 is not None:
         w3, st3 = timed_steps(S3, bos.BOS_PARTITION_OBSERVATIONS, args.steps, args.warmup)
         ph3 = phases(st3)
         jh3 = max_over_ranks(ph3["t_linearize_ms"])
