@@ -76,6 +76,8 @@ typedef struct bos_plan_info {
                                        from the fp32 array (bos_system_info.fold_fp32)             */
     int64_t lm_lanes_consecutive;   /* J+H landmark lanes whose poses are consecutive (p0, p0 + 1,
                                        ...): they read no pose-index records                      */
+    int64_t pose_odometry_chain;    /* poses whose odometry entries are exactly edges p - 1 = (p - 1,
+                                       p) and p = (p, p + 1): the J+H derives them from p          */
 } bos_plan_info;
 
 /* Build the static plan on the host (what bos_create does before touching the GPU) with the

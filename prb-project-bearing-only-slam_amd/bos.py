@@ -111,7 +111,7 @@ class bos_plan_info(ctypes.Structure):
                 ("shard_ex2_doubles", ctypes.c_int64), ("shard_pose_lanes", ctypes.c_int64),
                 ("shard_own_pose_lanes", ctypes.c_int64), ("shard_lm_lanes", ctypes.c_int64),
                 ("shard_update_nodes", ctypes.c_int64), ("mf_fold_fp32", ctypes.c_int64),
-                ("lm_lanes_consecutive", ctypes.c_int64)]
+                ("lm_lanes_consecutive", ctypes.c_int64), ("pose_odometry_chain", ctypes.c_int64)]
 
 
 _lib = None
@@ -356,7 +356,8 @@ def plan_inspect(P: Problem, rank: int = 0, world: int = 1, entries: bool = Fals
            "mf_levels": info.mf_levels, "mf_max_front": info.mf_max_front, "mf_flops": info.mf_flops,
            "mf_update_bytes": info.mf_update_bytes, "mf_fits": bool(info.mf_fits),
            "mf_max_front_upper": info.mf_max_front_upper, "mf_balance_pct": info.mf_balance_pct,
-           "mf_fold_fp32": bool(info.mf_fold_fp32), "lm_lanes_consecutive": info.lm_lanes_consecutive}
+           "mf_fold_fp32": bool(info.mf_fold_fp32), "lm_lanes_consecutive": info.lm_lanes_consecutive,
+           "pose_odometry_chain": info.pose_odometry_chain}
     out.update({k: getattr(info, k) for k, _ in bos_plan_info._fields_ if k.startswith("shard_")})
     if entries:
         nnz = info.nnz_lower

@@ -231,7 +231,9 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
         // Dependent load stages, the bearing chain (count/base -> records -> landmarks) and the
         // odometry chain (entry range -> entry ids -> other pose + edge data) issued side by side.
         const V4<T> X = load4(P.pc + 4 * p);
-        const int n = P.pl_cnt[g];
+        const int cnt = P.pl_cnt[g];
+        const int n = cnt & ~kOdoChain;
+        const bool chain = cnt & kOdoChain;   // (first lane of the group only)
         const int sl = P.pw_base[g >> 6] + t;   // slot of item j: sl + S j
         const int S = P.pw_stride[g >> 6];
         const int jl = n > 0 ? n - 1 : 0;       // record reads past the lane's last item: clamped to it
@@ -240,6 +242,18 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
         int x0 = 0, x1 = 0;
         T th = (T)0;
         if (odo) { x0 = P.po_ptr[p]; x1 = P.po_ptr[p + 1]; th = P.pth[p]; }
+        // a chain pose's two entries follow from p (edge p - 1 from its destination side, edge p from
+        // its source side): its edge and other-pose loads wait for no index load; only the pair
+        // block's index (a store address) is loaded
+        auto ids = [&](int i, OdoIn<T>& o, int& oth) {
+            if (chain) {
+                o.ent = i == 0 ? ((p - 1) << 1) | 1 : p << 1;
+                oth = i == 0 ? p - 1 : p + 1;
+                o.blk = i == 0 ? -1 : P.po_blk[x0 + 1];
+            } else {
+                odo_fetch_ids(P, x0 + i, o, oth);
+            }
+        };
         // Bearing items run in pairs with two register sets (A: even items, B: odd items). Per set,
         // the record index is loaded two pairs ahead, the full record and the landmark gather one
         // pair ahead; every register is refilled by a load right after its last use, so no loaded
@@ -250,8 +264,8 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
         int iA = ip[at(0)], iB = ip[at(1)];
         OdoIn<T> oa, ob;
         int otha = 0, othb = 0;
-        if (x0 < x1) odo_fetch_ids(P, x0, oa, otha);
-        if (x0 + 1 < x1) odo_fetch_ids(P, x0 + 1, ob, othb);
+        if (chain || x0 < x1) ids(0, oa, otha);
+        if (chain || x0 + 1 < x1) ids(1, ob, othb);
         V2<T> LA = load2(P.lc + 2 * (iA & kIdxMask)), LB = load2(P.lc + 2 * (iB & kIdxMask));
         T zA = zp[at(0)], zB = zp[at(1)];
         bool lastA = !(iA & kRunCont), lastB = !(iB & kRunCont);

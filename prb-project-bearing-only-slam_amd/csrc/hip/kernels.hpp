@@ -21,6 +21,9 @@ constexpr int kRecPad = 512;
 // summed into the run's last slot) carry kRunCont in their index.
 constexpr int32_t kRunCont = (int32_t)0x80000000u;
 constexpr int32_t kIdxMask = 0x7fffffff;
+// A pose lane count (pl_cnt, the group's first lane) with kOdoChain set: the pose is an odometry
+// chain pose (BlockLayout::po_chain; never with duplicate pairs), its entries derived from p
+constexpr int32_t kOdoChain = 0x40000000;
 
 // A lane list item is the other endpoint (landmark for the pose lists, pose for the landmark lists)
 // and the measured bearing, stored as two arrays (index, z) so each is read exactly once.
@@ -43,7 +46,7 @@ template <typename T> struct LinParams {
     // pose lanes
     const int32_t* pw_base;   // [waves + 1]
     const int32_t* pw_stride; // [waves]
-    const int32_t* pl_cnt;    // [NP * lpp]
+    const int32_t* pl_cnt;    // [NP * lpp] items per lane (| kOdoChain)
     const int32_t* pb_idx;    // [slots] landmark (| kRunCont); the pose-landmark block of a slot is at off_pl + 6 slot
     const T* pb_z;            // [slots] measured bearing
     const T* pb_w;            // [slots] information, null => 1

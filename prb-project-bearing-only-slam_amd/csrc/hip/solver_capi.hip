@@ -1201,7 +1201,11 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             const int32_t e = B.po_ent[x];
             po_oth[x] = (e & 1) ? pb->odom_src[e >> 1] : pb->odom_dst[e >> 1];
         }
-        if ((rc = upload(&s->pw_base, B.pose_lanes.w_base)) || (rc = upload(&s->pl_cnt, B.pose_lanes.cnt)) ||
+        std::vector<int32_t> plc(B.pose_lanes.cnt);   // chain poses flagged in their first lane's count
+        if (!B.has_dups)
+            for (size_t i = 0; i < B.lane_pose.size(); ++i)
+                if (B.lane_pose[i] >= 0 && B.po_chain[B.lane_pose[i]]) plc[i * B.lpp] |= bos::dev::kOdoChain;
+        if ((rc = upload(&s->pw_base, B.pose_lanes.w_base)) || (rc = upload(&s->pl_cnt, plc)) ||
             (rc = upload(&s->pw_stride, B.pose_lanes.w_stride)) || (rc = upload(&s->lw_stride, B.lm_lanes.w_stride)) ||
             (rc = upload(&s->lw_base, B.lm_lanes.w_base)) || (rc = upload(&s->ll_cnt, B.lm_lanes.cnt)) ||
             (rc = upload(&s->ll_lm, B.lm_lane_lm)) || (rc = upload(&s->ll_run, B.lm_lane_run)) ||

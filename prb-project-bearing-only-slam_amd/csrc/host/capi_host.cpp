@@ -297,6 +297,7 @@ int bos_plan_inspect(const bos_problem* pb, const bos_options* options, int32_t 
         info->mf_supernodes = P.mf.nsuper;
         info->mf_fold_fp32 = bos::mf_fold_reads_fp32(P) ? 1 : 0;
         for (int32_t p0 : P.blk.lm_lane_run) info->lm_lanes_consecutive += p0 >= 0;
+        for (uint8_t c : P.blk.po_chain) info->pose_odometry_chain += c;
         info->mf_levels = P.mf.nlevels;
         info->mf_max_front = P.mf.max_m;
         info->mf_flops = P.mf.flops;

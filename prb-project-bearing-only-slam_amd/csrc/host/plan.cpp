@@ -658,6 +658,16 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
         }
         B.uo_ptr[p + 1] = (int32_t)B.uo_dst.size();
     }
+    // odometry chain poses: exactly the entries (edge p - 1 from its destination side, edge p from its
+    // source side) of edges p - 1 = (p - 1, p) and p = (p, p + 1) (LinParams / kOdoChain)
+    B.po_chain.assign(NP, 0);
+    for (int p = 1; p + 1 < NP; ++p) {
+        const int x0 = B.po_ptr[p];
+        if (B.po_ptr[p + 1] - x0 != 2 || p >= Mo) continue;
+        if (B.po_ent[x0] != (((p - 1) << 1) | 1) || B.po_ent[x0 + 1] != (p << 1)) continue;
+        if (pi.o_src[p - 1] != p - 1 || pi.o_dst[p] != p + 1) continue;
+        B.po_chain[p] = 1;
+    }
     // lanes per pose and their bearing segments (lane 0 also takes the odometry entries; a run of
     // duplicate observations of one pair never straddles two lanes)
     B.lpp = plan_lanes_per_pose(pi);

@@ -105,6 +105,9 @@ struct BlockLayout {
                                         // sorted by (other pose, edge)
     std::vector<int32_t> po_blk;        // pose-pose block an entry adds to when the other pose is the
                                         // higher one (this pose stores it), else -1
+    // [NP] 1: the pose's odometry entries are exactly edge p - 1 = (p - 1, p) seen from its
+    // destination and edge p = (p, p + 1) from its source (a chain pose: the J+H derives them from p)
+    std::vector<uint8_t> po_chain;
     std::vector<int32_t> uo_ptr;        // [NP + 1] pose-pose blocks stored by each pose (the lower one)
     std::vector<int32_t> uo_dst;        // [nuo] the higher pose of each pose-pose block
     std::vector<int32_t> csr_src;       // [nnzA] block value of each stored entry of P^T H_nf P; -2 when

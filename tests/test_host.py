@@ -190,10 +190,20 @@ def test_consecutive_pose_landmark_lanes(which):
     for lm in range(P.lm_xy.shape[0]):
         poses = np.sort(P.b_pose[P.b_lm == lm])
         want += poses.size > 0 and bool(np.all(poses == poses[0] + np.arange(poses.size)))
-    got = bos.plan_inspect(P, solver=bos.BOS_SOLVER_SCHUR)["lm_lanes_consecutive"]
-    assert got == want
+    info = bos.plan_inspect(P, solver=bos.BOS_SOLVER_SCHUR)
+    assert info["lm_lanes_consecutive"] == want
     if which == "c2":   # the synthetic generator's windows are consecutive poses
-        assert got == P.lm_xy.shape[0]
+        assert want == P.lm_xy.shape[0]
+    # odometry chain poses (BlockLayout::po_chain): exactly edges p - 1 = (p - 1, p), p = (p, p + 1)
+    NP, Mo = P.pose_xyt.shape[0], len(P.o_src)
+    chain = 0
+    for p in range(1, NP - 1):
+        mine = np.nonzero(((P.o_src == p) | (P.o_dst == p)) & (P.o_src != P.o_dst))[0]
+        chain += (p < Mo and sorted(mine.tolist()) == [p - 1, p] and P.o_src[p - 1] == p - 1 and P.o_dst[p - 1] == p
+                  and P.o_src[p] == p and P.o_dst[p] == p + 1)
+    assert info["pose_odometry_chain"] == chain
+    if which == "c2":   # the synthetic trajectory is one chain
+        assert chain == NP - 2
 
 
 @pytest.mark.parametrize("solver", ["supernodal", "schur"])
