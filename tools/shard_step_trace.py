@@ -13,6 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "prb-project-bearing-only-slam_amd"))
 import bos  # noqa: E402
 
+if os.environ.get("BOS_LIB"):   # a library build variant (diagnostics)
+    bos.LIB_PATH = os.path.abspath(os.environ["BOS_LIB"])
+    bos.ALLOW_MISSING_SYMBOLS = True
+
 mode = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 P = bos.synthetic(100000, 200000, 10, seed=0xB05EED01 + 3)
