@@ -166,26 +166,50 @@ __device__ __forceinline__ void odometry_entry(const LinParams<T>& P, int x, int
     }
 }
 
-// One bearing seen from its pose (solver_jacobians.cpp:9-95, solver.cpp:37-45): accumulates the
-// pose's diagonal block h and b, returns the pose-landmark block o (J_p^T w J_l).
+// One bearing seen from its pose (solver_jacobians.cpp:9-95, solver.cpp:37-45), in two parts: the
+// evaluation (error, Jacobian, robust kernel; the pose-landmark block o = J_p^T w J_l and its factors
+// jf) and the accumulation of the pose's diagonal block h, b, chi^2 and robust count from the terms
+// (interleaved lane groups accumulate another lane's terms: pose_lanes).
+template <typename T> struct BearingTerms {
+    T j0, j1, j2, e, w, rho;   // pose Jacobian, robust-scaled error, information, e w e before scaling
+    int rob;                   // the robust kernel scaled e
+};
+
 template <typename T>
-__device__ __forceinline__ void pose_bearing(const LinParams<T>& P, const V4<T>& X, const V2<T>& Lm, T z, T w,
-                                             T h[6], T gb[3], T o[6], double& chi, int& nrob, T jf[3]) {
+__device__ __forceinline__ BearingTerms<T> pose_bearing_eval(const LinParams<T>& P, const V4<T>& X, const V2<T>& Lm,
+                                                             T z, T w, T o[6], T jf[3]) {
     T J[5];
     T e = bos::bearing_error_jacobian<T>(X.x, X.y, X.z, X.w, Lm.x, Lm.y, z, J);   // :9-95
     const T rho = e * w * e;                                                       // solver.cpp:37
-    chi += (double)rho;
+    int rob = 0;
     if (rho > P.kt) {                                                              // :38-40
         e *= sqrt(P.kt / rho);
-        ++nrob;
+        rob = 1;
     }
-    // H += (J^T w) J, b += (J^T w) e (:44-45)
     const T w0 = J[0] * w, w1 = J[1] * w, w2 = J[2] * w;
-    h[0] += w0 * J[0]; h[1] += w1 * J[0]; h[2] += w1 * J[1];
-    h[3] += w2 * J[0]; h[4] += w2 * J[1]; h[5] += w2 * J[2];
-    gb[0] += w0 * e; gb[1] += w1 * e; gb[2] += w2 * e;
     o[0] = w0 * J[3]; o[1] = w0 * J[4]; o[2] = w1 * J[3]; o[3] = w1 * J[4]; o[4] = w2 * J[3]; o[5] = w2 * J[4];
     jf[0] = J[2]; jf[1] = J[3]; jf[2] = J[4];
+    return BearingTerms<T>{J[0], J[1], J[2], e, w, rho, rob};
+}
+
+// H += (J^T w) J, b += (J^T w) e (:44-45), each term one explicit fused multiply-add: the
+// instruction sequence must not depend on where the terms come from (this lane's registers, with w
+// a compile-time 1 when the problem has no bearing information, or another lane's shuffle), or
+// the compiler's contraction and packing choices would round the two differently
+template <typename T>
+__device__ __forceinline__ void pose_bearing_acc(const BearingTerms<T>& b, T h[6], T gb[3], double& chi, int& nrob) {
+    chi += (double)b.rho;
+    nrob += b.rob;
+    const T w0 = b.j0 * b.w, w1 = b.j1 * b.w, w2 = b.j2 * b.w;
+    h[0] = fma(w0, b.j0, h[0]); h[1] = fma(w1, b.j0, h[1]); h[2] = fma(w1, b.j1, h[2]);
+    h[3] = fma(w2, b.j0, h[3]); h[4] = fma(w2, b.j1, h[4]); h[5] = fma(w2, b.j2, h[5]);
+    gb[0] = fma(w0, b.e, gb[0]); gb[1] = fma(w1, b.e, gb[1]); gb[2] = fma(w2, b.e, gb[2]);
+}
+
+// lane src's terms (a bearing of the same pose evaluated by another lane of the group)
+template <typename T> __device__ __forceinline__ BearingTerms<T> shfl_terms(const BearingTerms<T>& b, int src) {
+    return BearingTerms<T>{__shfl(b.j0, src), __shfl(b.j1, src), __shfl(b.j2, src), __shfl(b.e, src),
+                           __shfl(b.w, src), __shfl(b.rho, src), __shfl(b.rob, src)};
 }
 
 // The pose-landmark block of a bearing: stored at its slot, or (duplicate pairs) summed over the
@@ -218,9 +242,17 @@ __device__ __forceinline__ void put_pl(T* plbase, int64_t slot, const T o[6], T 
     }
 }
 
+// Interleaved lane groups (LPP > 1 without duplicate pairs, plan.cpp build_layout): item i of a pose
+// goes to lane i % LPP of its group, and the group's first lane accumulates every item in pose order
+// (its own, then each other lane's of the same round, shuffled to it) after the odometry entries —
+// the operations and order of one lane per pose, so H, b and the blocks are bit-identical to LPP = 1;
+// the other lanes evaluate their bearings (gathers, atan2, Jacobians) side by side and store their
+// blocks. A lane's count word then holds its own count (bits 0-15) and the group's round count
+// (its first lane's count, bits 16-29).
 template <typename T, bool HAS_W, bool HAS_DUPS, int LPP>
 __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double& chi, int& nrob,
                                            unsigned long long* st) {
+    constexpr bool ILV = LPP > 1 && !HAS_DUPS;
     const int grp = g / LPP, sub = g % LPP, t = g & 63;
     // group i runs pose i unless a table says otherwise (sharded ranks): one dependent load fewer
     // at the head of both of the lane's load chains
@@ -232,7 +264,8 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
         // odometry chain (entry range -> entry ids -> other pose + edge data) issued side by side.
         const V4<T> X = load4(P.pc + 4 * p);
         const int cnt = P.pl_cnt[g];
-        const int n = cnt & ~kOdoChain;
+        const int n = ILV ? cnt & 0xffff : cnt & ~kOdoChain;
+        const int nloop = ILV ? (cnt >> 16) & 0x3fff : n;   // the group's rounds (interleaved) or own items
         const bool chain = cnt & kOdoChain;   // (first lane of the group only)
         const int sl = P.pw_base[g >> 6] + t;   // slot of item j: sl + S j
         const int S = P.pw_stride[g >> 6];
@@ -292,9 +325,33 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
         const bool factored = P.pl_factored != 0;
         T* const plbase = P.hval + P.off_pl;
         stamp(P.diag_stamps, st, 1);
-        for (int j = 0; j < n; j += 2) {
+        const int src0 = (threadIdx.x & 63 & ~(LPP - 1));   // the group's first lane in the wave
+        // (interleaved) the other lanes' terms of this round, after this lane's own, in lane order
+        auto peers = [&](const BearingTerms<T>& mine, bool valid) {
+#pragma unroll
+            for (int k = 1; k < LPP; ++k) {
+                const BearingTerms<T> q = shfl_terms(mine, src0 + k);
+                if (__shfl((int)valid, src0 + k)) pose_bearing_acc<T>(q, h, gb, chi, nrob);
+            }
+        };
+        for (int j = 0; j < nloop; j += 2) {
             // item j (set A), then refill A: item j + 2's gather and z, item j + 4's index
-            pose_bearing<T>(P, X, LA, zA, wA, h, gb, o, chi, nrob, jf);
+            {
+                // (interleaved: every lane of the group evaluates, valid or not — a round past a
+                // lane's last item reads clamped records and stores zeros to a padding slot of its
+                // wave — so the shuffles run with the whole group active)
+                const bool vA = !ILV || j < n;
+                const BearingTerms<T> bA = pose_bearing_eval<T>(P, X, LA, zA, wA, o, jf);
+                if (vA) pose_bearing_acc<T>(bA, h, gb, chi, nrob);
+                if constexpr (ILV) {
+                    peers(bA, vA);
+                    if (!vA) {
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) o[q] = (T)0;
+                        jf[0] = jf[1] = jf[2] = (T)0;
+                    }
+                }
+            }
             put_pl<T, HAS_DUPS>(plbase, sl + (int64_t)S * j, o, acc, lastA, factored, jf);
             lastA = !(iA & kRunCont);
             LA = load2(P.lc + 2 * (iA & kIdxMask));
@@ -304,8 +361,18 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
             // item j + 1 (set B). Its block is stored even past the lane's last item (a padding slot
             // of the lane's wave: pose-lane waves have an even number of slots per lane), so both
             // paths issue the same memory operations and the loop's waits stay exact.
-            if (j + 1 < n) {
-                pose_bearing<T>(P, X, LB, zB, wB, h, gb, o, chi, nrob, jf);
+            if constexpr (ILV) {
+                const bool vB = j + 1 < n;
+                const BearingTerms<T> bB = pose_bearing_eval<T>(P, X, LB, zB, wB, o, jf);
+                if (vB) pose_bearing_acc<T>(bB, h, gb, chi, nrob);
+                peers(bB, vB);
+                if (!vB) {
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) o[q] = (T)0;
+                    jf[0] = jf[1] = jf[2] = (T)0;
+                }
+            } else if (j + 1 < n) {
+                pose_bearing_acc<T>(pose_bearing_eval<T>(P, X, LB, zB, wB, o, jf), h, gb, chi, nrob);
             } else {
 #pragma unroll
                 for (int q = 0; q < 6; ++q) o[q] = (T)0;
@@ -320,13 +387,17 @@ __device__ __forceinline__ void pose_lanes(const LinParams<T>& P, int g, double&
         }
         stamp(P.diag_stamps, st, 2);
     }
-    // combine the lane group's partial sums (fixed butterfly: deterministic)
+    if constexpr (ILV) {   // the first lane holds the pose's sums; the others' chi^2 / counts are not theirs
+        if (sub != 0) { chi = 0.0; nrob = 0; }
+    } else {
+        // combine the lane group's partial sums (fixed butterfly: deterministic)
 #pragma unroll
-    for (int o = 1; o < LPP; o <<= 1) {
+        for (int o = 1; o < LPP; o <<= 1) {
 #pragma unroll
-        for (int v = 0; v < 6; ++v) h[v] += __shfl_xor(h[v], o);
+            for (int v = 0; v < 6; ++v) h[v] += __shfl_xor(h[v], o);
 #pragma unroll
-        for (int v = 0; v < 3; ++v) gb[v] += __shfl_xor(gb[v], o);
+            for (int v = 0; v < 3; ++v) gb[v] += __shfl_xor(gb[v], o);
+        }
     }
     if (active && sub == 0) {
         const T lam = P.lambda;

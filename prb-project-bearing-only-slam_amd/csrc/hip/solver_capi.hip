@@ -1201,7 +1201,11 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             const int32_t e = B.po_ent[x];
             po_oth[x] = (e & 1) ? pb->odom_src[e >> 1] : pb->odom_dst[e >> 1];
         }
-        std::vector<int32_t> plc(B.pose_lanes.cnt);   // chain poses flagged in their first lane's count
+        // chain poses flagged in their first lane's count; interleaved groups: each lane's count with
+        // the group's round count (its first lane's) in bits 16-29 (kernels.hip pose_lanes)
+        std::vector<int32_t> plc(B.pose_lanes.cnt);
+        if (B.interleaved)
+            for (size_t g = 0; g < plc.size(); ++g) plc[g] |= B.pose_lanes.cnt[g - g % B.lpp] << 16;
         if (!B.has_dups)
             for (size_t i = 0; i < B.lane_pose.size(); ++i)
                 if (B.lane_pose[i] >= 0 && B.po_chain[B.lane_pose[i]]) plc[i * B.lpp] |= bos::dev::kOdoChain;

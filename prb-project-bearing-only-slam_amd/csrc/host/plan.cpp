@@ -600,6 +600,20 @@ void make_lane_lists(int lanes, const std::vector<int32_t>& lane_ptr, const std:
 
 inline int32_t lane_slot(const LaneLists& L, int g, int j) { return L.slot(g, j); }
 
+bool duplicate_pairs(const ProblemIndex& pi) {
+    std::vector<int64_t> key;
+    key.reserve(std::max(pi.Mb, pi.Mo));
+    for (int k = 0; k < pi.Mb; ++k) key.push_back((int64_t)pi.b_pose[k] * pi.NL + pi.b_lm[k]);
+    std::sort(key.begin(), key.end());
+    if (std::adjacent_find(key.begin(), key.end()) != key.end()) return true;
+    key.clear();
+    for (int k = 0; k < pi.Mo; ++k)
+        if (pi.o_src[k] != pi.o_dst[k])
+            key.push_back((int64_t)std::min(pi.o_src[k], pi.o_dst[k]) * pi.NP + std::max(pi.o_src[k], pi.o_dst[k]));
+    std::sort(key.begin(), key.end());
+    return std::adjacent_find(key.begin(), key.end()) != key.end();
+}
+
 // Block layout of H and the J+H work split (see BlockLayout in plan.hpp).
 int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     const int NP = pi.NP, NL = pi.NL, Mb = pi.Mb, Mo = pi.Mo;
@@ -670,21 +684,38 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     }
     // lanes per pose and their bearing segments (lane 0 also takes the odometry entries; a run of
     // duplicate observations of one pair never straddles two lanes)
-    B.lpp = plan_lanes_per_pose(pi);
+    B.lpp = plan_lanes_per_pose(pi, P.shard.world);
     if (B.lpp != 1 && B.lpp != 2 && B.lpp != 4) { err = "lanes per pose must be 1, 2 or 4"; return BOS_ERR_INVALID; }
     const int L = B.lpp;
     auto same_lm = [&](int i, int j) { return pi.b_lm[pb_obs[i]] == pi.b_lm[pb_obs[j]]; };
     for (int p = 0; p < NP; ++p)
         for (int i = pb_ptr[p] + 1; i < pb_ptr[p + 1]; ++i)
             if (same_lm(i, i - 1)) B.has_dups = true;
-    // pose lane groups in the shard's order (every pose in stix order on one GPU); lane g's items
-    // are pb_obs[lane_b0[g], lane_b0[g] + count)
+    // pose lane groups in the shard's order (every pose in stix order on one GPU). Without duplicate
+    // pairs the items are dealt round robin (item i of a pose to lane i % L, LinParams: interleaved
+    // groups accumulate in pose order, bit-identical to one lane per pose); with them each lane takes
+    // a contiguous range pb_obs[cut[j], cut[j + 1]) (runs never straddle lanes; partial sums combined).
+    // lane_item[g]: the pb_obs offsets of lane g's items, in lane order.
     B.lane_pose = P.shard.lane_poses;
     const int G = (int)B.lane_pose.size();
-    std::vector<int32_t> lane_ptr((size_t)G * L + 1, 0), lane_b0((size_t)G * L, 0), pitems;
+    B.interleaved = L > 1 && !B.has_dups;
+    std::vector<int32_t> lane_ptr((size_t)G * L + 1, 0), pitems, lane_item;
     pitems.reserve(Mb);
+    lane_item.reserve(Mb);
     for (int i = 0; i < G; ++i) {
         const int p = B.lane_pose[i];
+        if (B.interleaved) {
+            for (int j = 0; j < L; ++j) {
+                const size_t g = (size_t)i * L + j;
+                if (p >= 0)
+                    for (int q = pb_ptr[p] + j; q < pb_ptr[p + 1]; q += L) {
+                        pitems.push_back(pb_obs[q]);
+                        lane_item.push_back(q);
+                    }
+                lane_ptr[g + 1] = (int32_t)pitems.size();
+            }
+            continue;
+        }
         int cut[5] = {0, 0, 0, 0, 0};   // bearing range of each lane (as pb_obs offsets)
         if (p >= 0) {
             const int b0 = pb_ptr[p], b1 = pb_ptr[p + 1], nb = b1 - b0;
@@ -705,12 +736,15 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
         }
         for (int j = 0; j < L; ++j) {
             const size_t g = (size_t)i * L + j;
-            lane_b0[g] = cut[j];
             pitems.insert(pitems.end(), pb_obs.begin() + cut[j], pb_obs.begin() + cut[j + 1]);
+            for (int q = cut[j]; q < cut[j + 1]; ++q) lane_item.push_back(q);
             lane_ptr[g + 1] = (int32_t)pitems.size();
         }
     }
     make_lane_lists(G * L, lane_ptr, pitems, B.pose_lanes, true);
+    if (B.interleaved)
+        for (int c : B.pose_lanes.cnt)
+            if (c > 0x3fff) { err = "interleaved pose lanes: more than 16383 bearings per lane"; return BOS_ERR_UNSUPPORTED; }
     {   // landmark lanes in the shard's order; inside each window consecutive-pose lanes first, then
         // by degree (ties by the shard's order: deterministic)
         B.lm_lane_lm = P.shard.lane_lms;
@@ -744,19 +778,23 @@ int build_layout(const ProblemIndex& pi, Plan& P, std::string& err) {
     std::vector<int32_t> group_of(NP, -1);
     for (int i = 0; i < G; ++i)
         if (B.lane_pose[i] >= 0) group_of[B.lane_pose[i]] = i;
+    // (in pose order: an item is its run's last when the pose's next item observes another
+    // landmark; a contiguous split never cuts a run, an interleaved one has none)
     B.ub_ptr.assign(NP + 1, 0);
-    for (int p = 0; p < NP; ++p) {
-        if (group_of[p] >= 0)
-            for (int sub = 0; sub < L; ++sub) {
-                const int g = group_of[p] * L + sub;
-                const int n = B.pose_lanes.cnt[g], i0 = lane_b0[g];
-                for (int j = 0; j < n; ++j)
-                    if (j + 1 == n || !same_lm(i0 + j + 1, i0 + j)) {
-                        B.ub_lm.push_back(pi.b_lm[pb_obs[i0 + j]]);
-                        B.ub_slot.push_back(lane_slot(B.pose_lanes, g, j));
+    {
+        std::vector<int32_t> item_slot(Mb, -1);   // pb_obs offset -> the slot holding it
+        for (size_t g = 0; g < B.pose_lanes.cnt.size(); ++g)
+            for (int j = 0; j < B.pose_lanes.cnt[g]; ++j) item_slot[lane_item[lane_ptr[g] + j]] = lane_slot(B.pose_lanes, (int)g, j);
+        for (int p = 0; p < NP; ++p) {
+            if (group_of[p] >= 0)
+                for (int q = pb_ptr[p]; q < pb_ptr[p + 1]; ++q)
+                    if (q + 1 == pb_ptr[p + 1] || !same_lm(q + 1, q)) {
+                        if (item_slot[q] < 0) { err = "pose lane item without a slot"; return BOS_ERR_INVALID; }
+                        B.ub_lm.push_back(pi.b_lm[pb_obs[q]]);
+                        B.ub_slot.push_back(item_slot[q]);
                     }
-            }
-        B.ub_ptr[p + 1] = (int32_t)B.ub_lm.size();
+            B.ub_ptr[p + 1] = (int32_t)B.ub_lm.size();
+        }
     }
     B.off_ldiag = 6 * (int64_t)NP;
     B.off_pl = (B.off_ldiag + 3 * (int64_t)NL + 1) & ~(int64_t)1;   // even: 2-value vector stores stay aligned

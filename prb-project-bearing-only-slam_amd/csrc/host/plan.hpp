@@ -32,12 +32,20 @@ struct ProblemIndex {
 
 // J+H launch geometry shared by the host plan and the kernel (hip/kernels.hpp kBlock)
 constexpr int kJhBlock = 256;
-// J+H lanes per pose: bos_options.lanes_per_pose when set, else 2 from 32 bearings per pose on and
-// 1 below (measured on config 3, K = 10: 1 lane per pose beats 2 and 4). build_layout and
-// build_shard both use this.
-inline int plan_lanes_per_pose(const ProblemIndex& pi) {
+// some (pose, landmark) bearing pair or (pose, pose) odometry pair occurs twice (plan.cpp)
+bool duplicate_pairs(const ProblemIndex& pi);
+// J+H lanes per pose: bos_options.lanes_per_pose when set, else 2 from 32 bearings per pose on, 2 on
+// a sharded rank (world > 1) when there are no duplicate pairs, and 1 otherwise. Without duplicate
+// pairs two or four lanes per pose interleave a pose's bearings and compute H and b bit for bit as
+// one lane does (kernels.hip pose_lanes); a rank's share leaves the GPU with few waves, where two
+// lanes halve each pose's chain (config 3, per rank in-step J+H: W = 2 15 -> 13 us, W = 8 14 -> 11
+// us), while on one GPU one lane is fastest (17 against 20 and 25 us with two and four). build_layout
+// and build_shard both use this.
+inline int plan_lanes_per_pose(const ProblemIndex& pi, int world) {
     const double avg = pi.NP ? (double)pi.Mb / pi.NP : 0.0;
-    return pi.lpp > 0 ? pi.lpp : avg >= 32 ? 2 : 1;
+    if (pi.lpp > 0) return pi.lpp;
+    if (avg >= 32) return 2;
+    return world > 1 && !duplicate_pairs(pi) ? 2 : 1;
 }
 // Contiguous share [a, b) of n items for rank r of W (BOS_PARTITION_OBSERVATIONS: each rank runs a
 // range of the J+H's pose blocks and one of its landmark blocks, i.e. of the observations in
@@ -84,6 +92,7 @@ constexpr int kLmWindow = 256;   // landmark lanes are permuted only inside alig
 struct BlockLayout {
     int64_t off_ldiag = 0, off_pl = 0, off_pp = 0, size = 0;
     int lpp = 1;                        // lanes per pose: 1, 2 or 4
+    bool interleaved = false;           // lpp > 1 without duplicate pairs: items dealt round robin
     bool has_dups = false;              // some (pose, landmark) or (src, dst) pair repeats
     // pose lane groups: group i (lanes i * lpp ... + lpp - 1) runs pose lane_pose[i] (-1: padding);
     // one rank runs the poses of Shard::lane_poses (all poses in stix order on one GPU)

@@ -120,7 +120,7 @@ int build_shard(const ProblemIndex& pi, Plan& P, int rank, int world, std::strin
     }
     // J+H lanes: own poses, padded to a whole J+H block (chi^2 partials of own lanes and of top
     // lanes fall in different blocks), then the top poses and the fixed pose
-    const int lpp = plan_lanes_per_pose(pi);   // as build_layout
+    const int lpp = plan_lanes_per_pose(pi, world);   // as build_layout
     const int poses_per_block = kJhBlock / lpp;
     for (int p = 0; p < NP; ++p)
         if (S.node_owner[p] == rank) S.lane_poses.push_back(p);

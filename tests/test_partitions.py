@@ -277,11 +277,39 @@ def test_subtree_sharded_handle_refuses_partial_answers():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+@pytest.mark.parametrize("which", ["c1", "c2"])
+def test_interleaved_lane_groups_bit_identical(which, precision):
+    """lanes_per_pose 2 and 4 without duplicate pairs deal a pose's bearings round robin and the
+    group's first lane accumulates them in pose order (kernels.hip pose_lanes, plan.cpp
+    build_layout): H, b and the states after GN steps equal one lane per pose bit for bit."""
+    P = bos.load_g2o(C1) if which == "c1" else bos.synthetic(1000, 2000, 20)
+    prec = bos.BOS_FP64 if precision == "fp64" else bos.BOS_FP32
+    ref = None
+    for lpp in (1, 2, 4):
+        S = bos.Solver(P, precision=prec, solver=bos.BOS_SOLVER_SCHUR, lanes_per_pose=lpp)
+        assert S.system_info()["lanes_per_pose"] == lpp
+        S.linearize()
+        rows, cols, vals, b = S.export_system()
+        for _ in range(3):
+            assert S.step()["solver_info"] == 0
+        pose, lm = S.get_state()
+        S.close()
+        got = (rows, cols, vals, b, pose, lm)
+        if ref is None:
+            ref = got
+            continue
+        for a, r in zip(got, ref):
+            assert np.array_equal(a, r), f"lanes_per_pose {lpp} differs from 1"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("lpp", [2, 4])
 @pytest.mark.parametrize("which", ["c1", "c2"])
 def test_lanes_per_pose_matches_oracle(lpp, which):
-    """lanes_per_pose 2 and 4 (bearing segments per pose, the lane group's butterfly combine):
-    H and b against the oracle at the fp64 bounds, and 3 GN steps against the oracle's."""
+    """lanes_per_pose 2 and 4 (interleaved groups without duplicate pairs; bearing segments per
+    pose and the group's butterfly combine with them): H and b against the oracle at the fp64
+    bounds, and 3 GN steps against the oracle's."""
     P = bos.load_g2o(C1) if which == "c1" else bos.synthetic(1000, 2000, 20)
     lin_parity(P, lanes_per_pose=lpp)
     Q = to_oracle(P)
