@@ -288,6 +288,19 @@ def test_shard_partition(world):
     assert np.all(b_cov[keep] >= 1)
 
 
+def test_lanes_per_pose_rule():
+    """plan_lanes_per_pose: one lane per pose on one GPU, two on sharded ranks when no (pose,
+    landmark) or odometry pair repeats (interleaved groups, bit-identical to one lane), one with a
+    repeated pair (a split would change the summation order); an explicit option wins."""
+    P = bos.synthetic(2000, 4000, 10, seed=5)
+    lpp = lambda Q, world, opt=0: bos.plan_inspect(Q, 0, world, solver=bos.BOS_SOLVER_SCHUR,
+                                                    lanes_per_pose=opt)["lanes_per_pose"]
+    assert lpp(P, 1) == 1 and lpp(P, 2) == 2 and lpp(P, 8) == 2 and lpp(P, 2, 1) == 1 and lpp(P, 1, 4) == 4
+    D = bos.Problem(P.pose_xyt, P.lm_xy, np.append(P.b_pose, P.b_pose[0]), np.append(P.b_lm, P.b_lm[0]),
+                    np.append(P.b_z, P.b_z[0]), P.o_src, P.o_dst, P.o_z, P.o_omega, P.fixed)
+    assert lpp(D, 1) == 1 and lpp(D, 2) == 1
+
+
 def test_shard_world1_is_the_unsharded_plan():
     P = bos.load_g2o(C1)
     a = bos.plan_inspect(P, 0, 1, solver=bos.BOS_SOLVER_SCHUR)
