@@ -1554,6 +1554,18 @@ int bos_exchange_p2p_connect(bos_solver* s, const void* handles) {
     if (s->p2p) return fail(BOS_ERR_INVALID, "direct exchange: already connected");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    // the peers' mailboxes are written by this device's kernels: every other visible device must be
+    // reachable (xGMI), or the caller keeps the RCCL exchange
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    for (int d = 0; d < ndev; ++d) {
+        int ok = 0;
+        if (d != s->device && (hipDeviceCanAccessPeer(&ok, s->device, d) != hipSuccess || !ok)) {
+            (void)hipGetLastError();
+            return fail(BOS_ERR_UNSUPPORTED, "direct exchange: device " + std::to_string(s->device) +
+                                                 " has no peer access to device " + std::to_string(d));
+        }
+    }
     std::vector<double*> peers(s->world, nullptr);
     for (int q = 0; q < s->world; ++q) {
         if (q == s->rank) { peers[q] = reinterpret_cast<double*>(s->mailbox); continue; }

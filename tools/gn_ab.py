@@ -4,6 +4,8 @@ median device-stamped phases of 50 synchronous steps, synchronous GN it/s (bos_t
 3 x 50) and a checksum of the state after 50 iterations (equal for variants that compute the same).
 
     python tools/gn_ab.py <libA.so> <libB.so> [<libC.so> ...] [rounds]
+
+A variant may carry environment settings for its process: <lib.so>@NAME=VALUE[@NAME=VALUE...].
 """
 import os
 import subprocess
@@ -12,7 +14,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(lib):
+def child(lib, label):
     sys.path.insert(0, os.path.join(ROOT, "prb-project-bearing-only-slam_amd"))
     import numpy as np
     import bos
@@ -32,20 +34,23 @@ def child(lib):
     for _ in range(3):
         S.set_state(*init)
         best = max(best, 1e3 / S.time_steps(50))
-    print(f"{os.path.basename(lib)}: J+H {ph['t_linearize_ms']:.2f} us  solve {ph['t_solve_ms']:.1f} us  "
+    print(f"{label}: J+H {ph['t_linearize_ms']:.2f} us  solve {ph['t_solve_ms']:.1f} us  "
           f"update {ph['t_update_ms']:.1f} us  GN {best:.0f} it/s  state {ck!r}", flush=True)
 
 
 def main():
     if sys.argv[1] == "--child":
-        child(sys.argv[2])
+        child(sys.argv[2], sys.argv[3])
         return
-    libs = [a for a in sys.argv[1:] if a.endswith(".so")]
-    rest = [a for a in sys.argv[1:] if not a.endswith(".so")]
+    libs = [a for a in sys.argv[1:] if a.split("@")[0].endswith(".so")]
+    rest = [a for a in sys.argv[1:] if a not in libs]
     rounds = int(rest[0]) if rest else 2
     for _ in range(rounds):
-        for lib in libs:
-            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib], timeout=120)
+        for spec in libs:
+            lib, *env = spec.split("@")
+            label = os.path.basename(spec)
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib, label], timeout=120,
+                               env=dict(os.environ, **dict(e.split("=", 1) for e in env)))
             if r.returncode != 0:
                 sys.exit(r.returncode)
 
