@@ -159,6 +159,10 @@ struct bos_solver {
     int32_t *tri_ptr = nullptr, *tri_obs = nullptr, *tri_pose = nullptr;
     double *tri_z = nullptr, *tri_scr = nullptr;
     double* d_maxpart = nullptr;                 // box-plus max |dx| per update block
+    // the J+H build's static inputs (work lists, records, odometry) carved from one allocation
+    // (JhStage): the fields below point into it and are not freed one by one
+    char* jh_arena = nullptr;
+    std::vector<void**> jh_fields;
     rocblas_handle rb = nullptr;
     rocsolver_rfinfo rf = nullptr;
     bos::dev::MfDevice* mf = nullptr;
@@ -257,12 +261,35 @@ template <typename T> bos::dev::UpdateParams<T> upd_params(const bos_solver* s) 
     return u;
 }
 
-template <typename T> int upload_T(void** p, const std::vector<double>& v) {
-    std::vector<T> t(v.begin(), v.end());
-    T* d = nullptr;
-    int rc = upload(&d, t);
-    *p = d;
-    return rc;
+// Host staging of device arrays that are uploaded together into one allocation (each at a 256-byte
+// aligned offset; an empty array stays null, as with upload)
+struct JhStage {
+    std::vector<char> host;
+    std::vector<std::pair<void**, size_t>> fields;
+    template <typename X> void add(X** p, const std::vector<X>& v) {
+        *p = nullptr;
+        if (v.empty()) return;
+        const size_t off = (host.size() + 255) & ~(size_t)255;
+        host.resize(off + v.size() * sizeof(X));
+        std::memcpy(host.data() + off, v.data(), v.size() * sizeof(X));
+        fields.push_back({reinterpret_cast<void**>(p), off});
+    }
+    template <typename T> void add_T(void** p, const std::vector<double>& v) {
+        std::vector<T> t(v.begin(), v.end());
+        add(reinterpret_cast<T**>(p), t);
+    }
+};
+
+int flush_stage(bos_solver* s, JhStage& st) {
+    if (st.host.empty()) return BOS_OK;
+    HIP_TRY(hipMalloc((void**)&s->jh_arena, st.host.size()));
+    HIP_TRY(hipMemcpy(s->jh_arena, st.host.data(), st.host.size(), hipMemcpyHostToDevice));
+    for (auto& f : st.fields) {
+        *f.first = s->jh_arena + f.second;
+        s->jh_fields.push_back(f.first);
+    }
+    st = JhStage{};
+    return BOS_OK;
 }
 
 int enqueue_linearize(bos_solver* s, unsigned long long* t_start = nullptr) {
@@ -1011,6 +1038,7 @@ int bos_destroy(bos_solver* s) {
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     drop_graph(s);
+    for (void** f : s->jh_fields) *f = nullptr;   // inside jh_arena
     void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pw_stride, s->pl_cnt, s->lw_base, s->lw_stride, s->ll_cnt, s->ll_lm,
                     s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w, s->ll_run,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->obs ? nullptr : s->d_b, s->d_sys,
@@ -1020,7 +1048,7 @@ int bos_destroy(bos_solver* s) {
                     s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr,
                     s->scrub, s->lane_pose, s->ex1_send, s->obs ? s->ex1_recv : nullptr, s->ex2_send, s->mailbox,
                     s->d_peers, s->ex1_pack,
-                    s->ex1_unpack, s->ex2_bnd, s->ex2_usrc, s->ex2_udst, s->upd_nodes, s->abs_part};
+                    s->ex1_unpack, s->ex2_bnd, s->ex2_usrc, s->ex2_udst, s->upd_nodes, s->abs_part, s->jh_arena};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (s->h_status) (void)hipHostFree(s->h_status);
@@ -1164,11 +1192,14 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         if (f32) return dalloc((float**)p, count);
         return dalloc((double**)p, count);
     };
-    auto upload_Tv = [&](void** p, const std::vector<double>& v) -> int {
-        return f32 ? upload_T<float>(p, v) : upload_T<double>(p, v);
-    };
     if ((rc = alloc_T(&s->d_pc, 4 * (size_t)NP)) || (rc = alloc_T(&s->d_pth, NP)) || (rc = alloc_T(&s->d_lc, 2 * (size_t)NL)))
         return bail(rc);
+    // the J+H's static inputs: one allocation (flush_stage)
+    JhStage stage;
+    auto stage_Tv = [&](void** p, const std::vector<double>& v) {
+        if (f32) stage.add_T<float>(p, v);
+        else stage.add_T<double>(p, v);
+    };
 
     {
         const bos::BlockLayout& B = P.blk;
@@ -1209,20 +1240,18 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         if (!B.has_dups)
             for (size_t i = 0; i < B.lane_pose.size(); ++i)
                 if (B.lane_pose[i] >= 0 && B.po_chain[B.lane_pose[i]]) plc[i * B.lpp] |= bos::dev::kOdoChain;
-        if ((rc = upload(&s->pw_base, B.pose_lanes.w_base)) || (rc = upload(&s->pl_cnt, plc)) ||
-            (rc = upload(&s->pw_stride, B.pose_lanes.w_stride)) || (rc = upload(&s->lw_stride, B.lm_lanes.w_stride)) ||
-            (rc = upload(&s->lw_base, B.lm_lanes.w_base)) || (rc = upload(&s->ll_cnt, B.lm_lanes.cnt)) ||
-            (rc = upload(&s->ll_lm, B.lm_lane_lm)) || (rc = upload(&s->ll_run, B.lm_lane_run)) ||
-            (rc = upload(&s->po_ptr, B.po_ptr)) || (rc = upload(&s->po_ent, po_ent)) ||
-            (rc = upload(&s->po_oth, po_oth)) ||
-            (rc = upload(&s->po_blk, po_blk)) || (rc = upload(&s->pb_idx, pbi)) || (rc = upload_Tv(&s->pb_z, pbz)) ||
-            (rc = upload(&s->lb_idx, lbi)) || (rc = upload_Tv(&s->lb_z, lbz)))
-            return bail(rc);
+        stage.add(&s->pw_base, B.pose_lanes.w_base); stage.add(&s->pl_cnt, plc);
+        stage.add(&s->pw_stride, B.pose_lanes.w_stride); stage.add(&s->lw_stride, B.lm_lanes.w_stride);
+        stage.add(&s->lw_base, B.lm_lanes.w_base); stage.add(&s->ll_cnt, B.lm_lanes.cnt);
+        stage.add(&s->ll_lm, B.lm_lane_lm); stage.add(&s->ll_run, B.lm_lane_run);
+        stage.add(&s->po_ptr, B.po_ptr); stage.add(&s->po_ent, po_ent); stage.add(&s->po_oth, po_oth);
+        stage.add(&s->po_blk, po_blk); stage.add(&s->pb_idx, pbi); stage_Tv(&s->pb_z, pbz);
+        stage.add(&s->lb_idx, lbi); stage_Tv(&s->lb_z, lbz);
         if (s->has_w) {
             pbw.assign(po.size() + pad, 0.0); lbw.assign(lo.size() + pad, 0.0);
             for (size_t i = 0; i < po.size(); ++i) if (po[i] >= 0) pbw[i] = pb->bearing_omega[po[i]];
             for (size_t i = 0; i < lo.size(); ++i) if (lo[i] >= 0) lbw[i] = pb->bearing_omega[lo[i]];
-            if ((rc = upload_Tv(&s->pb_w, pbw)) || (rc = upload_Tv(&s->lb_w, lbw))) return bail(rc);
+            stage_Tv(&s->pb_w, pbw); stage_Tv(&s->lb_w, lbw);
         }
         static_assert(bos::kJhBlock == bos::dev::kBlock, "J+H block size");
         s->pose_blocks = (int)B.pose_blocks();
@@ -1240,7 +1269,7 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         // observations partition: every block (the others' partials stay 0)
         s->chi_parts = bos::dev::kJhSub *
                        (s->rank == 0 || s->obs ? s->pose_blocks : (int)((int64_t)P.shard.own_pose_lanes * B.lpp / bos::dev::kBlock));
-        if ((rc = upload(&s->lane_pose, B.lane_pose))) return bail(rc);
+        stage.add(&s->lane_pose, B.lane_pose);
         s->lane_identity = true;
         for (size_t i = 0; i < B.lane_pose.size() && s->lane_identity; ++i) s->lane_identity = B.lane_pose[i] == (int32_t)i;
     }
@@ -1260,10 +1289,9 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
             const double u[6] = {m[0], m[1], m[2], m[4], m[5], m[8]};
             for (int q = 0; q < 6; ++q) om[6 * (size_t)k + q] = u[q];
         }
-        if ((rc = upload(&s->o_src, os)) || (rc = upload(&s->o_dst, od)) || (rc = upload_Tv(&s->o_z, oz)) ||
-            (rc = upload_Tv(&s->o_om, om)))
-            return bail(rc);
+        stage.add(&s->o_src, os); stage.add(&s->o_dst, od); stage_Tv(&s->o_z, oz); stage_Tv(&s->o_om, om);
     }
+    if ((rc = flush_stage(s, stage))) return bail(rc);
     // permuted dof -> reference dof
     s->ref_dof.assign(P.n + 3, 0);
     for (int u = 0; u < NP + NL; ++u) {
