@@ -1192,14 +1192,16 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         if (f32) return dalloc((float**)p, count);
         return dalloc((double**)p, count);
     };
-    if ((rc = alloc_T(&s->d_pc, 4 * (size_t)NP)) || (rc = alloc_T(&s->d_pth, NP)) || (rc = alloc_T(&s->d_lc, 2 * (size_t)NL)))
-        return bail(rc);
-    // the J+H's static inputs: one allocation (flush_stage)
+    // the J+H's inputs: the state caches (filled by upload_cache, then by the box-plus) and the
+    // static work lists, records and odometry, in one allocation (flush_stage)
     JhStage stage;
     auto stage_Tv = [&](void** p, const std::vector<double>& v) {
         if (f32) stage.add_T<float>(p, v);
         else stage.add_T<double>(p, v);
     };
+    stage_Tv(&s->d_pc, std::vector<double>(4 * (size_t)NP, 0.0));
+    stage_Tv(&s->d_pth, std::vector<double>((size_t)NP, 0.0));
+    stage_Tv(&s->d_lc, std::vector<double>(2 * (size_t)NL, 0.0));
 
     {
         const bos::BlockLayout& B = P.blk;
