@@ -258,6 +258,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50, help="GN iterations timed (from the initial guess)")
     ap.add_argument("--warmup", type=int, default=5, help="untimed GN iterations before the timed ones")
+    ap.add_argument("--device-warmup", type=int, default=1000,
+                    help="untimed GN iterations (bos_step_n batches of 100, about 0.5 s on one GPU) before the "
+                         "headline's warmup: brings the GPU to its steady clocks (tools/jh_placement_probe.py); "
+                         "0 = off")
     ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
     ap.add_argument("--replay-steps", type=int, default=200, help="J+H builds back to back (warm-replay roofline)")
     ap.add_argument("--cold-steps", type=int, default=20, help="J+H builds timed from cold caches by events")
@@ -428,12 +432,17 @@ def main():
         gloo_allgather(h, 2)
         return h.step_phase(2)
 
-    def timed_steps(h, partition, k, warmup):
-        """`warmup` untimed GN iterations, then the state reset to the initial guess (outside the
+    def timed_steps(h, partition, k, warmup, device_warmup=0):
+        """`device_warmup` untimed GN iterations as one batch (not with the gloo exchange), `warmup`
+        untimed GN iterations, then the state reset to the initial guess (outside the
         timed region) and k GN iterations from it, timed as one region: iterations 1..k of the solve
         (the world converges; tests/test_gpu_c3_gn.py checks 200 fp32 iterations positive definite).
         Returns (wall seconds of the timed steps, max over ranks; per-step stats)."""
         init = h.get_state()
+        if device_warmup > 0 and (world == 1 or args.exchange != "gloo"):
+            for b in range(0, device_warmup, 100):   # batches of <= 100 from the initial guess (the
+                h.step_n(min(100, device_warmup - b))  # trajectory tests/test_gpu_c3_gn.py checks)
+                h.set_state(*init)
         for _ in range(warmup):
             gn_step(h, partition)
         h.set_state(*init)
@@ -460,7 +469,7 @@ def main():
     wall, stats, phase, jh_ms, gn_it_s = 0.0, [], None, None, None
     ranks_consistent = None
     if args.steps > 0:
-        wall, stats = timed_steps(S, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup)
+        wall, stats = timed_steps(S, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup, args.device_warmup)
         phase = phases(stats)
         if world > 1:   # every rank combines the same headers: the chi^2 of every step must agree bit for bit
             mine = torch.tensor([g["chi2"] for g in stats], dtype=torch.float64)
@@ -575,6 +584,7 @@ def main():
             "n_gpus": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
+            "device_warmup": args.device_warmup if args.steps > 0 else 0,
             "ms_per_step": head_ms,
             "higher_is_better": True,
             "scaling": "strong",
