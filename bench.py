@@ -499,6 +499,20 @@ def main():
         assert last["solver_info"] == 0, "non-positive pivot in a benchmarked GN step"
         S.set_state(*init)
 
+    # ---- the drop-in caller's loop: proj02::Solver::step() through the C++ façade, as the reference's
+    # executable calls it (executables/bearing_only_slam.cpp:93-99), then one read of solver.state
+    facade = None
+    if world == 1 and args.steps > 0:
+        nf = min(args.steps, 50)
+        f = bos.time_facade_steps(P, nf, bos.options(solver=solver, precision=precision, lanes_per_pose=lpp))
+        facade = {"steps": nf, "ms_per_step": f["ms_per_step"], "ms_state_read": f["ms_state_read"],
+                  "gn_iters_per_s_incl_state_read": nf / ((nf * f["ms_per_step"] + f["ms_state_read"]) * 1e-3),
+                  "gn_iters_per_s_c_loop_same_handle": 1e3 / f["ms_per_step_capi"],
+                  "state_mismatches_vs_device": f["state_mismatches"]}
+        assert f["state_mismatches"] == 0, "solver.state differs from the device state"
+        log(f"facade: {1e3 / f['ms_per_step']:.0f} it/s, state read {f['ms_state_read']:.2f} ms, C loop on the same "
+            f"handle {1e3 / f['ms_per_step_capi']:.0f} it/s")
+
     # ---- the J+H alone: back to back (warm replay) and from cold caches (events)
     barrier()
     replay_ms = S.time_linearize(args.replay_steps) if args.replay_steps > 0 else None
@@ -608,6 +622,9 @@ def main():
             "gn_iters_per_s": gn_it_s,
             "gn_iters_per_s_c_loop": gn_c_loop,
             "gn_iters_per_s_batched": gn_batched,
+            # proj02::Solver::step() through the C++ façade (solver.state lazily downloaded on read)
+            "gn_iters_per_s_facade": 1e3 / facade["ms_per_step"] if facade else None,
+            "facade": facade,
             "gn_phase_ms": phase,
             "solver_model": solver_model(P, phase, world),
             "gn_solver": args.solver,

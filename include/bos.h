@@ -228,6 +228,19 @@ int bos_node_owner(const struct bos_solver* s, int32_t* owner);
 #define BOS_P2P_HANDLE_BYTES 64
 int bos_exchange_p2p_handle(struct bos_solver* s, void* handle);
 int bos_exchange_p2p_connect(struct bos_solver* s, const void* handles);
+/* Timing contract of the direct exchange. A rank's step waits on the device for the other ranks'
+ * pushes (two waits per iteration); a wait gives up after `seconds` (default 2 s, so host-side gaps
+ * of one rank between its bos_step calls — the first step's graph captures, logging, a pause —
+ * stay far inside it) and then marks the step aborted: every later wait of that step returns at
+ * once, the box-plus is skipped and bos_step returns BOS_ERR_SOLVER. An abort raised before
+ * exchange 2 travels in exchange 2's header, so every rank skips that update together; a wait on
+ * exchange 2 itself that times out skips the update on the ranks that timed out only, so after any
+ * BOS_ERR_SOLVER from a sharded step the caller must bring all ranks back to one state
+ * (bos_set_state on every rank) or destroy the handles. Once connected, bos_step_phase and
+ * bos_exchange_download / _upload return BOS_ERR_INVALID (the exchange is the handle's own). Every
+ * rank must finish stepping (its last bos_step returned on every rank, e.g. a barrier) before any
+ * rank calls bos_destroy: the peers' pushes write into this rank's mailbox. */
+int bos_set_exchange_timeout(struct bos_solver* s, double seconds);
 
 /* State read/write in stix order (State::poses / landmarks, framework/state.hpp:47-48) */
 int bos_get_state(const struct bos_solver* s, double* pose_xyt, double* landmark_xy);

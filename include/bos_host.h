@@ -133,6 +133,23 @@ int bos_time_linearize(struct bos_solver* s, int32_t n, int32_t flush_caches, do
 int bos_time_triangulate(struct bos_solver* s, int32_t n, double* ms_per_call);
 int bos_time_steps(struct bos_solver* s, int32_t n, double* ms_per_step);
 
+/* The C++ façade proj02::Solver (prb-project-bearing-only-slam_amd/csrc/host/solver.hpp, the
+ * reference's class API, slam/solver.hpp:21-92) driven as the reference's executable drives it
+ * (executables/bearing_only_slam.cpp:93-99: solver.step() in a loop, then one read of solver.state
+ * to draw it). The façade is built from `problem` (ids = stix); one untimed step, then n
+ * Solver::step() calls timed on the host clock: *ms_per_step. *ms_state_read: the one read of
+ * solver.state after them (its lazy download of the device state). *mismatches: doubles of
+ * solver.state whose bits differ from bos_get_state of the façade's handle. *ms_per_step_capi: n
+ * bos_step calls on the same handle right after (bos_time_steps). Optional outputs may be NULL. */
+int bos_time_facade_steps(const bos_problem* problem, const bos_options* options, int32_t n, double* ms_per_step,
+                          double* ms_state_read, double* ms_per_step_capi, int64_t* mismatches);
+/* Test hook: n steps of the façade beside n bos_step calls of a second handle created from the same
+ * problem, solver.state read every 7 steps and written once (a landmark moved, a pose turned:
+ * through the façade's public state, by bos_get_state / bos_set_state on the other handle) at n / 2.
+ * *mismatches = doubles of solver.state that differ in their bits from the device states at the
+ * reads and at the end (0 expected). */
+int bos_debug_facade_selftest(const bos_problem* problem, const bos_options* options, int32_t n, int64_t* mismatches);
+
 /* Test hook (process-wide, default 0 = product behaviour; not part of the drop-in boundary): the
  * line-by-line g2o parser instead of the chunked one (the tests prove them identical). */
 void bos_debug_set_g2o_parser(int32_t line_by_line);

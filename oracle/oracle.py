@@ -61,6 +61,10 @@ def lib():
         L.oracle_set_literal.restype = None
         L.oracle_set_literal.argtypes = [ctypes.c_int]
         L.oracle_get_literal.restype = ctypes.c_int
+        L.oracle_bearing_errors.restype = None
+        L.oracle_bearing_errors.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 6
+        L.oracle_set_wrap_signs.restype = None
+        L.oracle_set_wrap_signs.argtypes = [ctypes.c_int, ctypes.c_void_p]
         L.oracle_normalized_angle_f64.restype = ctypes.c_double
         L.oracle_normalized_angle_f64.argtypes = [ctypes.c_double]
         L.oracle_normalized_angle_f32.restype = ctypes.c_float
@@ -103,7 +107,7 @@ def lib():
         L.oracle_triangulate.restype = ctypes.c_int
         L.oracle_triangulate.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, dp,
                                          ctypes.c_int, ip, dp]
-        assert L.oracle_version() == 4
+        assert L.oracle_version() == 5
         _lib = L
     return _lib
 
@@ -129,16 +133,38 @@ def set_literal(on: bool) -> None:
     lib().oracle_set_literal(1 if on else 0)
 
 
+_wrap_signs_keep = None
+
+
+def set_wrap_signs(signs) -> None:
+    """Knife-edge bearings (bos_oracle.cpp knife_edge): ``signs[k]`` in {-1, 0, +1} fixes the sign
+    of bearing k's error when it lies on the +-pi wrap (within 1e-9 of pi in fp64); None clears."""
+    global _wrap_signs_keep
+    if signs is None:
+        _wrap_signs_keep = None
+        lib().oracle_set_wrap_signs(0, None)
+        return
+    _wrap_signs_keep = np.ascontiguousarray(signs, dtype=np.int8)
+    lib().oracle_set_wrap_signs(len(_wrap_signs_keep), _wrap_signs_keep.ctypes.data)
+
+
 class literal:
-    """``with O.literal(): ...`` — set_literal(True) for the block, restored after."""
+    """``with O.literal(wrap_signs=None): ...`` — set_literal(True) and the knife-edge bearings'
+    signs (set_wrap_signs; None = none) for the block, both restored after (blocks nest)."""
+
+    def __init__(self, wrap_signs=None):
+        self._signs = wrap_signs
 
     def __enter__(self):
         self._was = lib().oracle_get_literal()
+        self._was_signs = _wrap_signs_keep
         set_literal(True)
+        set_wrap_signs(self._signs)
         return self
 
     def __exit__(self, *exc):
         set_literal(bool(self._was))
+        set_wrap_signs(self._was_signs)
         return False
 
 
@@ -194,6 +220,19 @@ def bearing_error_and_jacobian(pose, lm, z, precision: int = 64):
     J = np.zeros(5)
     e = lib().oracle_bearing_ej_f64(_pd(p), _pd(l), float(z), _pd(J))
     return e, J
+
+
+def bearing_errors(P: "Problem", pose_xyt=None, lm_xy=None) -> np.ndarray:
+    """e_k of every bearing at a state (fp64, the current evaluation form, no knife-edge override)."""
+    pose = np.ascontiguousarray(P.pose_xyt if pose_xyt is None else pose_xyt, dtype=np.float64)
+    lm = np.ascontiguousarray(P.lm_xy if lm_xy is None else lm_xy, dtype=np.float64)
+    bp = np.ascontiguousarray(P.b_pose, dtype=np.int32)
+    bl = np.ascontiguousarray(P.b_lm, dtype=np.int32)
+    bz = np.ascontiguousarray(P.b_z, dtype=np.float64)
+    e = np.zeros(len(bz))
+    lib().oracle_bearing_errors(len(bz), pose.ctypes.data, lm.ctypes.data, bp.ctypes.data, bl.ctypes.data,
+                                bz.ctypes.data, e.ctypes.data)
+    return e
 
 
 def odometry_error_and_jacobian(src, dst, z, precision: int = 64):

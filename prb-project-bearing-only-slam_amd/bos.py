@@ -52,7 +52,7 @@ EXPORTED_SYMBOLS = [
     "bos_debug_set_g2o_parser", "bos_debug_inject_stall", "bos_debug_set_step_graph", "bos_debug_solver_stamps",
     "bos_time_linearize", "bos_time_triangulate", "bos_time_steps", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
     "bos_cpu_gn_destroy", "bos_normalized_angle_f64", "bos_normalized_angle_f32", "bos_exchange_p2p_handle",
-    "bos_exchange_p2p_connect",
+    "bos_exchange_p2p_connect", "bos_time_facade_steps", "bos_debug_facade_selftest", "bos_set_exchange_timeout",
 ]
 
 P2P_HANDLE_BYTES = 64   # include/bos.h BOS_P2P_HANDLE_BYTES
@@ -188,8 +188,13 @@ def lib():
         "bos_cpu_gn_destroy": (None, [vp]),
         "bos_exchange_p2p_handle": (ctypes.c_int, [vp, ctypes.c_void_p]),
         "bos_exchange_p2p_connect": (ctypes.c_int, [vp, ctypes.c_void_p]),
+        "bos_set_exchange_timeout": (ctypes.c_int, [vp, ctypes.c_double]),
         "bos_normalized_angle_f64": (ctypes.c_double, [ctypes.c_double]),
         "bos_normalized_angle_f32": (ctypes.c_float, [ctypes.c_float]),
+        "bos_time_facade_steps": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options), ctypes.c_int32,
+                                                 _dp, _dp, _dp, ctypes.POINTER(ctypes.c_int64)]),
+        "bos_debug_facade_selftest": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options),
+                                                     ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     }
     for name, (res, args) in sig.items():
         if ALLOW_MISSING_SYMBOLS and not hasattr(L, name):   # A/B tools loading an older build
@@ -328,6 +333,27 @@ def write_g2o(P: Problem, path: str, pose_xyt=None, lm_xy=None, with_landmarks=T
                                        int(with_landmarks)), "write_g2o")
     finally:
         L.bos_dataset_free(h)
+
+
+def time_facade_steps(P: Problem, n: int, opts=None) -> dict:
+    """n x proj02::Solver::step() through the C++ façade, then one read of solver.state
+    (bos_time_facade_steps; the reference's loop, executables/bearing_only_slam.cpp:93-99)."""
+    ms, rd, capi, bad = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    pb = P.c_struct()
+    _check(lib().bos_time_facade_steps(ctypes.byref(pb), None if opts is None else ctypes.byref(opts), n,
+                                       ctypes.byref(ms), ctypes.byref(rd), ctypes.byref(capi), ctypes.byref(bad)),
+           "bos_time_facade_steps")
+    return {"ms_per_step": ms.value, "ms_state_read": rd.value, "ms_per_step_capi": capi.value,
+            "state_mismatches": bad.value}
+
+
+def facade_selftest(P: Problem, n: int, opts=None) -> int:
+    """Doubles of the façade's solver.state that differ from the device state (bos_debug_facade_selftest)."""
+    bad = ctypes.c_int64()
+    pb = P.c_struct()
+    _check(lib().bos_debug_facade_selftest(ctypes.byref(pb), None if opts is None else ctypes.byref(opts), n,
+                                           ctypes.byref(bad)), "bos_debug_facade_selftest")
+    return bad.value
 
 
 def options(solver: int = BOS_SOLVER_SUPERNODAL, partition: int = BOS_PARTITION_SUBTREE, lanes_per_pose: int = 0,
@@ -567,6 +593,10 @@ class Solver:
         blob = b"".join(handles)
         buf = ctypes.create_string_buffer(blob, len(blob))
         _check(lib().bos_exchange_p2p_connect(self._h, buf), "bos_exchange_p2p_connect")
+
+    def set_exchange_timeout(self, seconds: float) -> None:
+        """Bound of the direct exchange's device-side flag waits (bos_set_exchange_timeout, 2 s default)."""
+        _check(lib().bos_set_exchange_timeout(self._h, float(seconds)), "bos_set_exchange_timeout")
 
     def node_owner(self) -> np.ndarray:
         o = np.zeros(self.P.NP + self.P.NL, dtype=np.int32)

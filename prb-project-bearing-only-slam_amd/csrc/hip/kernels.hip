@@ -764,18 +764,23 @@ template <typename T> __global__ __launch_bounds__(256) void triangulate_kernel(
 }
 
 // lanes q < world of the block poll sender q's flag in this rank's mailbox until it equals the
-// iteration's epoch (or mark the step aborted after ~50 ms); then the whole block acquires
+// iteration's epoch (or mark the step aborted after w.timeout_ticks, or give up at once when the
+// step is already marked aborted: a launch's blocks, and the step's later waits, then drain in one
+// timeout); then the whole block acquires
 __device__ __forceinline__ void p2p_wait_block(const P2PWait& w) {
     const int q = threadIdx.x;
     if (q < w.world) {
         const uint32_t e = *w.epoch;
         const uint32_t* f = reinterpret_cast<const uint32_t*>(w.mailbox + w.flag_off + 64 * (int64_t)q);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {   // 50 ms of the 100 MHz clock
+        for (uint32_t it = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++it) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > w.timeout_ticks) {
                 atomicOr(w.info, kStepAbort);
                 break;
             }
+            if ((it & 63) == 63 &&
+                (__hip_atomic_load(w.info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStepAbort))
+                break;
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -787,12 +792,12 @@ __device__ __forceinline__ void p2p_wait_block(const P2PWait& w) {
 // (w.mailbox set: every block first waits for the direct exchange's flags, and the stamp marks the
 // end of that wait)
 template <typename T>
-__global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, const ExSeg* segs, unsigned long long* stamp,
+__global__ void seg_copy_kernel(T* val, T* b, T* send, T* recv, T* aux, const ExSeg* segs, unsigned long long* stamp,
                                 const P2PWait w) {
     if (w.mailbox) p2p_wait_block(w);
     if (stamp && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
     const ExSeg g = segs[blockIdx.y];
-    T* const base[4] = {val, b, send, recv};
+    T* const base[5] = {val, b, send, recv, aux};
     const T* src = base[g.src_kind] + g.src;
     T* dst = base[g.dst_kind] + g.dst;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < g.len; i += (int64_t)gridDim.x * blockDim.x)
@@ -1116,8 +1121,8 @@ template <typename T> hipError_t launch_boxplus(const UpdateParams<T>& p, hipStr
 }
 
 template <typename T>
-hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s,
-                           unsigned long long* stamp, const P2PWait& w) {
+hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, T* aux, const ExSeg* segs, int nseg, int64_t max_len,
+                           hipStream_t s, unsigned long long* stamp, const P2PWait& w) {
     if (w.mailbox && (w.world <= 0 || w.world > 64)) return hipErrorInvalidValue;
     if (nseg == 0 || max_len == 0) {
         if (w.mailbox) hipLaunchKernelGGL(p2p_wait_kernel, dim3(1), dim3(64), 0, s, w, stamp);
@@ -1125,8 +1130,8 @@ hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, in
         return hipGetLastError();
     }
     const int64_t bx = std::min<int64_t>((max_len + 255) / 256, 256);
-    hipLaunchKernelGGL((seg_copy_kernel<T>), dim3((unsigned)bx, (unsigned)nseg), dim3(256), 0, s, val, b, send, recv, segs,
-                       stamp, w);
+    hipLaunchKernelGGL((seg_copy_kernel<T>), dim3((unsigned)bx, (unsigned)nseg), dim3(256), 0, s, val, b, send, recv, aux,
+                       segs, stamp, w);
     return hipGetLastError();
 }
 
@@ -1266,10 +1271,10 @@ template hipError_t launch_linearize<float>(const LinParams<float>&, int, bool, 
 template hipError_t launch_boxplus<double>(const UpdateParams<double>&, hipStream_t);
 template hipError_t launch_boxplus<float>(const UpdateParams<float>&, hipStream_t);
 template hipError_t launch_triangulate<double>(const TriParams<double>&, hipStream_t);
-template hipError_t launch_seg_copy<double>(double*, double*, double*, double*, const ExSeg*, int, int64_t, hipStream_t,
-                                            unsigned long long*, const P2PWait&);
-template hipError_t launch_seg_copy<float>(float*, float*, float*, float*, const ExSeg*, int, int64_t, hipStream_t,
-                                           unsigned long long*, const P2PWait&);
+template hipError_t launch_seg_copy<double>(double*, double*, double*, double*, double*, const ExSeg*, int, int64_t,
+                                            hipStream_t, unsigned long long*, const P2PWait&);
+template hipError_t launch_seg_copy<float>(float*, float*, float*, float*, float*, const ExSeg*, int, int64_t,
+                                           hipStream_t, unsigned long long*, const P2PWait&);
 template hipError_t launch_triangulate<float>(const TriParams<float>&, hipStream_t);
 template hipError_t launch_to_f64<double>(const double*, double*, int64_t, hipStream_t);
 template hipError_t launch_to_f64<float>(const float*, double*, int64_t, hipStream_t);

@@ -157,20 +157,24 @@ struct ExSeg {
 // A wait for the direct exchange's flags (bos_exchange_p2p_connect), fused into the launch that
 // reads the received data: in every block, lanes q < world poll sender q's flag (mailbox + flag_off
 // + 64 q) until it equals the iteration's epoch (*epoch), or mark the step aborted (*info |=
-// kStepAbort) after ~50 ms; then the block reads. mailbox null: no wait.
+// kStepAbort) after timeout_ticks of the 100 MHz realtime clock (bos_set_exchange_timeout, 2 s by
+// default), or stop at once when another block already did; then the block reads. mailbox null:
+// no wait.
 struct P2PWait {
     const char* mailbox = nullptr;
     int64_t flag_off = 0;
     int world = 0;
     const uint32_t* epoch = nullptr;
     int32_t* info = nullptr;
+    uint64_t timeout_ticks = 200000000ull;
 };
 
-// *stamp (if set) gets the realtime clock at the launch's start (after the wait, with one); with
-// nothing to copy, a wait (or the stamp) still runs
+// Segment kinds (ExSeg src_kind / dst_kind): 0 val, 1 b, 2 send, 3 recv, 4 aux (the received
+// exchange-1 headers' local copy). *stamp (if set) gets the realtime clock at the launch's start
+// (after the wait, with one); with nothing to copy, a wait (or the stamp) still runs
 template <typename T>
-hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, const ExSeg* segs, int nseg, int64_t max_len, hipStream_t s,
-                           unsigned long long* stamp = nullptr, const P2PWait& w = P2PWait());
+hipError_t launch_seg_copy(T* val, T* b, T* send, T* recv, T* aux, const ExSeg* segs, int nseg, int64_t max_len,
+                           hipStream_t s, unsigned long long* stamp = nullptr, const P2PWait& w = P2PWait());
 
 template <typename T>
 hipError_t launch_linearize(const LinParams<T>& p, int lpp, bool has_w, bool has_dups, hipStream_t s);

@@ -136,6 +136,11 @@ struct bos_solver {
     bool lane_identity = false;              // group i runs pose i (one GPU): the kernel skips the table
     int chi_parts = 0;                       // J+H chi^2 partial blocks this rank counts
     double *ex1_send = nullptr, *ex1_recv = nullptr, *ex2_send = nullptr, *ex2_recv = nullptr;
+    // every rank's exchange-1 header (chi^2, robust count), copied out of the mailbox by phase 1's
+    // unpack right after its wait: a faster rank may push the next iteration's exchange 1 into the
+    // mailbox before this rank's phase 2 combines the headers
+    double* hdr1 = nullptr;
+    uint64_t ex_timeout_ticks = 200000000ull;  // direct-exchange flag waits: 2 s (bos_set_exchange_timeout)
     // sharded: the receive buffers of both exchanges and the direct exchange's flags live in one
     // mailbox, uncached device memory (bos_exchange_p2p_connect maps every rank's into the others)
     char* mailbox = nullptr;
@@ -326,7 +331,11 @@ int setup_shard(bos_solver* s) {
         }
         return o;
     };
-    const std::vector<bos::dev::ExSeg> pack = conv(hp, s->maxlen1p), unpack = conv(hu, s->maxlen1u);
+    const std::vector<bos::dev::ExSeg> pack = conv(hp, s->maxlen1p);
+    std::vector<bos::dev::ExSeg> unpack = conv(hu, s->maxlen1u);
+    for (int q = 0; q < W; ++q)   // rank q's header -> hdr1[q * kExHeader] (kind 4), after the wait
+        unpack.push_back({(int64_t)q * S.ex1_count, (int64_t)q * bos::kExHeader, bos::kExHeader, 3, 4});
+    s->maxlen1u = std::max<int64_t>(s->maxlen1u, bos::kExHeader);
     s->n1p = (int)pack.size();
     s->n1u = (int)unpack.size();
     std::vector<int32_t> bnd(S.bnd_dof.begin() + S.bnd_ptr[s->rank], S.bnd_dof.begin() + S.bnd_ptr[s->rank + 1]);
@@ -345,6 +354,7 @@ int setup_shard(bos_solver* s) {
     if ((rc = upload(&s->ex1_pack, pack)) || (rc = upload(&s->ex1_unpack, unpack)) || (rc = upload(&s->ex2_bnd, bnd)) ||
         (rc = upload(&s->ex2_usrc, usrc)) || (rc = upload(&s->ex2_udst, udst)) || (rc = upload(&s->upd_nodes, S.upd_nodes)) ||
         (rc = dalloc(&s->ex1_send, (size_t)s->ex1_count)) || (rc = dalloc(&s->ex2_send, (size_t)s->ex2_count)) ||
+        (rc = dalloc(&s->hdr1, (size_t)W * bos::kExHeader)) ||
         (rc = dalloc(&s->abs_part, (size_t)std::max(1, (S.n_upd_local + 255) / 256))))
         return rc;
     {   // the mailbox: [exchange 1: W x ex1_count][exchange 2: W x ex2_count][flags: 2 x W x 64 B]
@@ -366,6 +376,7 @@ int setup_shard(bos_solver* s) {
     }
     HIP_TRY(hipMemset(s->ex1_send, 0, s->ex1_count * sizeof(double)));
     HIP_TRY(hipMemset(s->ex2_send, 0, s->ex2_count * sizeof(double)));
+    HIP_TRY(hipMemset(s->hdr1, 0, (size_t)W * bos::kExHeader * sizeof(double)));
     return BOS_OK;
 }
 
@@ -633,6 +644,7 @@ bos::dev::P2PWait p2p_wait(const bos_solver* s, int which) {
     w.world = s->world;
     w.epoch = bos::dev::mf_epoch_ptr(s->mf);
     w.info = bos::dev::mf_info_ptr(s->mf);
+    w.timeout_ticks = s->ex_timeout_ticks;
     return w;
 }
 
@@ -644,13 +656,14 @@ int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
         if (with_jh && (rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
         if ((rc = enqueue_solver_inputs(s))) return rc;   // opens this step's flow epoch
         HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
-        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_pack, s->n1p, s->maxlen1p, s->stream));
+        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->hdr1, s->ex1_pack, s->n1p, s->maxlen1p,
+                                                  s->stream));
         if (!s->p2p)   // (the direct exchange's push computes the header itself)
             HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream,
                                                    s->d_status->stamp + 4));
     } else if (phase == 1) {
-        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->ex1_unpack, s->n1u, s->maxlen1u, s->stream,
-                                                  s->d_status->stamp + 5, p2p_wait(s, 1)));
+        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->hdr1, s->ex1_unpack, s->n1u, s->maxlen1u,
+                                                  s->stream, s->d_status->stamp + 5, p2p_wait(s, 1)));
         HIP_TRY(bos::dev::mf_factor(s->mf, 1, mf_matrix(s), s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, 1, s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, 0, s->d_rhs, s->stream));
@@ -663,7 +676,9 @@ int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
         if ((rc = enqueue_update(s))) return rc;
         int32_t nrob_c = 0;
         const double chi_c = self_loop_chi(s, nrob_c);
-        HIP_TRY(bos::dev::launch_shard_combine(s->ex1_recv, s->ex1_count, s->ex2_recv, s->ex2_count, s->world, chi_c,
+        // exchange-1 headers from phase 1's local copy (the mailbox may already hold the next
+        // iteration's); exchange 2's are still current (no rank pushes again before this rank does)
+        HIP_TRY(bos::dev::launch_shard_combine(s->hdr1, bos::kExHeader, s->ex2_recv, s->ex2_count, s->world, chi_c,
                                                nrob_c, bos::dev::mf_info_ptr(s->mf), s->d_status, s->m_status, s->stream));
     }
     return BOS_OK;
@@ -1047,7 +1062,7 @@ int bos_destroy(bos_solver* s) {
                     s->d_Lval, s->d_dense, s->d_info, s->d_chi_part, s->d_nrob_part, s->d_status,
                     s->d_maxpart, s->tri_ptr, s->tri_obs, s->tri_pose, s->tri_z, s->tri_scr,
                     s->scrub, s->lane_pose, s->ex1_send, s->obs ? s->ex1_recv : nullptr, s->ex2_send, s->mailbox,
-                    s->d_peers, s->ex1_pack,
+                    s->d_peers, s->ex1_pack, s->hdr1,
                     s->ex1_unpack, s->ex2_bnd, s->ex2_usrc, s->ex2_udst, s->upd_nodes, s->abs_part, s->jh_arena};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1523,6 +1538,7 @@ int bos_step_phase(bos_solver* s, int32_t phase, bos_step_stats* st) {
         return finish_step(s, st);
     }
     if (!s->sharded) return fail(BOS_ERR_INVALID, "bos_step_phase needs a sharded handle (world_size > 1)");
+    if (s->p2p) return fail(BOS_ERR_INVALID, "bos_step_phase: the handle exchanges directly (bos_exchange_p2p_connect); use bos_step");
     if (phase != s->phase) return fail(BOS_ERR_INVALID, "bos_step_phase: phases run 0, 1, 2 in order");
     HIP_TRY(hipSetDevice(s->device));
     int rc = phase == 0 ? shard_phase0(s) : phase == 1 ? shard_phase1(s) : shard_phase2(s);
@@ -1543,6 +1559,7 @@ int bos_exchange_size(const bos_solver* s, int32_t which, int64_t* doubles_per_r
 
 int bos_exchange_download(bos_solver* s, int32_t which, double* send) {
     if (!s || !send || (which != 1 && which != 2)) return fail(BOS_ERR_INVALID, "bad argument");
+    if (s->p2p) return fail(BOS_ERR_INVALID, "bos_exchange_download: the handle exchanges directly (bos_exchange_p2p_connect)");
     if (!s->sharded && !(s->obs && which == 1)) return fail(BOS_ERR_INVALID, "not a sharded handle / no such exchange");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1553,12 +1570,21 @@ int bos_exchange_download(bos_solver* s, int32_t which, double* send) {
 
 int bos_exchange_upload(bos_solver* s, int32_t which, const double* recv_all) {
     if (!s || !recv_all || (which != 1 && which != 2)) return fail(BOS_ERR_INVALID, "bad argument");
+    if (s->p2p) return fail(BOS_ERR_INVALID, "bos_exchange_upload: the handle exchanges directly (bos_exchange_p2p_connect)");
     if (!s->sharded && !(s->obs && which == 1)) return fail(BOS_ERR_INVALID, "not a sharded handle / no such exchange");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
     // subtree partition: every rank's buffer (all-gather); observations partition: their sum
     const int64_t c = s->obs ? s->ex1_count : (which == 1 ? s->ex1_count : s->ex2_count) * s->world;
     HIP_TRY(hipMemcpy(which == 1 ? s->ex1_recv : s->ex2_recv, recv_all, c * sizeof(double), hipMemcpyHostToDevice));
+    return BOS_OK;
+}
+
+int bos_set_exchange_timeout(bos_solver* s, double seconds) {
+    if (!s || !(seconds > 0.0) || seconds > 3600.0) return fail(BOS_ERR_INVALID, "bad argument");
+    const uint64_t t = (uint64_t)(seconds * 1e8);   // 100 MHz realtime clock
+    if (t != s->ex_timeout_ticks) drop_graph(s);     // a launch argument of the captured step
+    s->ex_timeout_ticks = t;
     return BOS_OK;
 }
 

@@ -33,11 +33,6 @@ Solver::Solver(const State& st, const BearingObservationVector& bear_obs, const 
     const int NP = state.number_of_poses(), NL = state.number_of_landmarks();
     pose_.resize(3 * (size_t)NP);
     lm_.resize(2 * (size_t)NL);
-    for (int i = 0; i < NP; ++i) {
-        const NEPose& p = state.poses_vec()[i];
-        pose_[3 * i] = p.x; pose_[3 * i + 1] = p.y; pose_[3 * i + 2] = p.theta;
-    }
-    for (int j = 0; j < NL; ++j) { lm_[2 * j] = state.landmarks_vec()[j].x; lm_[2 * j + 1] = state.landmarks_vec()[j].y; }
     const size_t Mb = bearing_observations.size(), Mo = odometry_observations.size();
     bp_.resize(Mb); bl_.resize(Mb); os_.resize(Mo); od_.resize(Mo);
     bz_.resize(Mb); bw_.resize(Mb); oz_.resize(3 * Mo); om_.resize(9 * Mo);
@@ -64,17 +59,22 @@ Solver::Solver(const State& st, const BearingObservationVector& bear_obs, const 
     if (options) opt_ = *options;
 }
 
+namespace {
+// the host state in the C ABI's SoA form (const accessors: reading is not a write)
+void stage_state(const State& st, std::vector<double>& pose, std::vector<double>& lm) {
+    const NEPoseVector& P = st.poses_vec();
+    const LMPosVector& L = st.landmarks_vec();
+    if (pose.size() != 3 * P.size() || lm.size() != 2 * L.size())
+        throw std::runtime_error("proj02::Solver: poses or landmarks were added to solver.state after construction");
+    for (size_t i = 0; i < P.size(); ++i) { pose[3 * i] = P[i].x; pose[3 * i + 1] = P[i].y; pose[3 * i + 2] = P[i].theta; }
+    for (size_t j = 0; j < L.size(); ++j) { lm[2 * j] = L[j].x; lm[2 * j + 1] = L[j].y; }
+}
+}  // namespace
+
 bos_solver* Solver::ensure() {
     if (h_) return h_;
     // the public state as it is now (the reference's step() reads its member state)
-    for (int i = 0; i < state.number_of_poses(); ++i) {
-        const NEPose& p = state.poses_vec()[i];
-        pose_[3 * i] = p.x; pose_[3 * i + 1] = p.y; pose_[3 * i + 2] = p.theta;
-    }
-    for (int j = 0; j < state.number_of_landmarks(); ++j) {
-        lm_[2 * j] = state.landmarks_vec()[j].x;
-        lm_[2 * j + 1] = state.landmarks_vec()[j].y;
-    }
+    stage_state(state, pose_, lm_);
     bos_problem pb;
     pb.num_poses = state.number_of_poses(); pb.num_landmarks = state.number_of_landmarks();
     pb.num_bearings = (int32_t)bz_.size(); pb.num_odometry = (int32_t)os_.size();
@@ -84,6 +84,7 @@ bos_solver* Solver::ensure() {
     pb.odom_src = os_.data(); pb.odom_dst = od_.data(); pb.odom_z = oz_.data(); pb.odom_omega = om_.data();
     pb.fixed_pose = state.pose_stix(fixed_pose_id_);
     check(bos_create(&pb, &opt_, &h_), "bos_create");
+    state.attach_source(this);   // from here on the device holds the current values
     return h_;
 }
 
@@ -98,22 +99,43 @@ void Solver::set_damping_factor(float df) {
     if (h_) check(bos_set_damping_factor(h_, df), "set_damping_factor");
 }
 
-void Solver::sync_state() {
-    const int NP = state.number_of_poses(), NL = state.number_of_landmarks();
-    std::vector<double> pose(3 * (size_t)NP), lm(2 * (size_t)NL);
-    check(bos_get_state(h_, pose.data(), lm.data()), "bos_get_state");
-    for (int i = 0; i < NP; ++i) state.poses_vec()[i] = NEPose(pose[3 * i], pose[3 * i + 1], pose[3 * i + 2]);
-    for (int j = 0; j < NL; ++j) state.landmarks_vec()[j] = LMPos(lm[2 * j], lm[2 * j + 1]);
+// StateSource: the device's fp64 state, copied as is (bit for bit bos_get_state)
+void Solver::pull_state(NEPoseVector& poses, LMPosVector& landmarks) {
+    check(bos_get_state(h_, pose_.data(), lm_.data()), "bos_get_state");
+    for (size_t i = 0; i < poses.size(); ++i) poses[i] = NEPose(pose_[3 * i], pose_[3 * i + 1], pose_[3 * i + 2]);
+    for (size_t j = 0; j < landmarks.size(); ++j) landmarks[j] = LMPos(lm_[2 * j], lm_[2 * j + 1]);
+}
+
+void Solver::push_state() {
+    stage_state(state, pose_, lm_);
+    check(bos_set_state(h_, pose_.data(), lm_.data()), "bos_set_state");
+}
+
+void Solver::before_step() {
+    const bool fresh = h_ == nullptr;
+    ensure();
+    // a write to `state` since the last step (or, for a fresh handle, since bos_create copied it)
+    if (state.take_host_writes() && !fresh) push_state();
+}
+
+bos_solver* Solver::handle() {
+    before_step();
+    state.mark_stale();
+    return h_;
 }
 
 void Solver::step() {
-    check(bos_step(ensure(), &stats_), "bos_step");
-    sync_state();
+    before_step();
+    const int rc = bos_step(h_, &stats_);
+    state.mark_stale();   // even a failed step may have moved nothing or everything: re-read
+    check(rc, "bos_step");
 }
 
 void Solver::step_n(int n) {
-    check(bos_step_n(ensure(), n, &stats_), "bos_step_n");
-    sync_state();
+    before_step();
+    const int rc = bos_step_n(h_, n, &stats_);
+    state.mark_stale();
+    check(rc, "bos_step_n");
 }
 
 double Solver::normalized_angle(double a) { return bos::normalized_angle<double>(a); }

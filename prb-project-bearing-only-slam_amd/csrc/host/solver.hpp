@@ -36,7 +36,11 @@ struct Jacobian3 {
     double coeff(int row, int col) const;
 };
 
-class Solver {
+// The public `state` follows the device lazily (State / StateSource, state.hpp): step() leaves the
+// new values on the device and the first read of `state` afterwards downloads them (fp64, bit for
+// bit bos_get_state); a write to `state` between steps (non-const accessor, assignment,
+// apply_boxplus) is uploaded before the next step, as the reference's step() reads its member.
+class Solver final : private StateSource {
   public:
     State state;
     BearingObservationVector bearing_observations;
@@ -54,7 +58,9 @@ class Solver {
     void step();                           // :36 — one GN iteration, state updated on return
     void step_n(int n);                    // n iterations, one state download at the end
     const bos_step_stats& last_stats() const { return stats_; }
-    bos_solver* handle() { return ensure(); }
+    // The device handle (created on first use). The caller may step it directly: the public state
+    // re-reads the device afterwards (host writes pending at this call are uploaded first).
+    bos_solver* handle();
 
     // :38-44
     void error_and_jacobian(const State& state, const BearingObservation& obs, double& error, JacobianRow& J);
@@ -69,13 +75,15 @@ class Solver {
     double normalized_angle(double angle);
 
   private:
-    void sync_state();
+    void pull_state(NEPoseVector& poses, LMPosVector& landmarks) override;
+    void push_state();
+    void before_step();
     bos_solver* ensure();   // creates the device handle on first use
     bos_solver* h_ = nullptr;
     int fixed_pose_id_;
     bos_step_stats stats_ = {};
     // the problem in the C ABI's SoA form (bos_create copies it)
-    std::vector<double> pose_, lm_, bz_, bw_, oz_, om_;
+    std::vector<double> pose_, lm_, bz_, bw_, oz_, om_;   // pose_ / lm_ also stage state transfers
     std::vector<int32_t> bp_, bl_, os_, od_;
     bool w1_ = true;
     bos_options opt_;

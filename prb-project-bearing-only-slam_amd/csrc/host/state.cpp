@@ -13,7 +13,24 @@ State::State(int expected_states, int expected_landmarks) {
     lm_stix_to_id.reserve(expected_landmarks > 0 ? expected_landmarks : 0);
 }
 
+State::State(const State& o)
+    : poses(o.poses_vec()), landmarks(o.landmarks_vec()), pose_id_to_stix(o.pose_id_to_stix),
+      pose_stix_to_id(o.pose_stix_to_id), lm_id_to_stix(o.lm_id_to_stix), lm_stix_to_id(o.lm_stix_to_id) {}
+
+State& State::operator=(const State& o) {
+    if (this == &o) return *this;
+    touch();   // replaced on the host: a source's next step uploads it
+    poses = o.poses_vec();
+    landmarks = o.landmarks_vec();
+    pose_id_to_stix = o.pose_id_to_stix;
+    pose_stix_to_id = o.pose_stix_to_id;
+    lm_id_to_stix = o.lm_id_to_stix;
+    lm_stix_to_id = o.lm_stix_to_id;
+    return *this;
+}
+
 void State::add_pose(const NEPose& pose, const int& id) {
+    touch();
     poses.push_back(pose);
     pose_id_to_stix[id] = (int)poses.size() - 1;   // a repeated id re-points the map (state.cpp:23)
     pose_stix_to_id.push_back(id);
@@ -24,6 +41,7 @@ void State::add_pose(const double& x, const double& y, const double& theta, cons
 }
 
 void State::add_landmark(const LMPos& lm, const int& id) {
+    touch();
     landmarks.push_back(lm);
     lm_id_to_stix[id] = (int)landmarks.size() - 1;
     lm_stix_to_id.push_back(id);
@@ -31,8 +49,8 @@ void State::add_landmark(const LMPos& lm, const int& id) {
 
 void State::add_landmark(const double& x, const double& y, const int& id) { add_landmark(LMPos(x, y), id); }
 
-NEPose State::get_pose_by_id(const int& id) const { return poses[pose_id_to_stix.at(id)]; }
-LMPos State::get_landmark_by_id(const int& id) const { return landmarks[lm_id_to_stix.at(id)]; }
+NEPose State::get_pose_by_id(const int& id) const { return poses_vec()[pose_id_to_stix.at(id)]; }
+LMPos State::get_landmark_by_id(const int& id) const { return landmarks_vec()[lm_id_to_stix.at(id)]; }
 
 int State::number_of_poses() const { return (int)poses.size(); }
 int State::number_of_landmarks() const { return (int)landmarks.size(); }
@@ -46,6 +64,7 @@ int State::default_pose_id() {
 }
 
 void State::apply_boxplus(const std::vector<double>& dx) {
+    touch();
     const size_t NP = poses.size(), NL = landmarks.size();
     if (dx.size() < 3 * NP + 2 * NL) throw std::invalid_argument("State::apply_boxplus: dx too short");
     for (size_t i = 0; i < NP; ++i) poses[i] = boxplus(poses[i], EPose(dx[3 * i], dx[3 * i + 1], dx[3 * i + 2]));
@@ -53,6 +72,7 @@ void State::apply_boxplus(const std::vector<double>& dx) {
 }
 
 void State::print_full_vector() {
+    materialize();
     std::cout << "State:";
     for (const NEPose& p : poses) {
         const EPose e = t2v(p);

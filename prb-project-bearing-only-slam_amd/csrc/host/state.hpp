@@ -15,9 +15,28 @@ inline NEPose boxplus(const NEPose& X, const EPose& dx) {
     return r;
 }
 
+class State;
+
+// Where a State's current values live when it is not the host vectors: proj02::Solver registers
+// itself for its public `state` member, whose values after a step are on the device. The State
+// then refreshes its vectors from the source on the first read after a step (lazy: a caller that
+// steps 50 times and reads once pays one download, not 50), and remembers a write through a
+// non-const accessor so that the next step uploads the host values first (the reference's step()
+// reads its member state, slam/solver.cpp:27-97).
+class StateSource {
+  public:
+    virtual void pull_state(NEPoseVector& poses, LMPosVector& landmarks) = 0;
+
+  protected:
+    ~StateSource() = default;
+};
+
 class State {
   public:
     State(int expected_states = 300, int expected_landmarks = 200);
+    // A copy is a plain host State: the source's current values, no source attached.
+    State(const State& o);
+    State& operator=(const State& o);
 
     void add_pose(const NEPose& pose, const int& id);                          // state.cpp:20-25
     void add_pose(const double& x, const double& y, const double& theta, const int& id);  // :27-30
@@ -39,17 +58,36 @@ class State {
     void apply_boxplus(const std::vector<double>& delta_x);
     void print_full_vector();                                                   // :82-93
 
-    // direct stix-order access (the reference keeps these private; the C ABI needs them)
-    const NEPoseVector& poses_vec() const { return poses; }
-    const LMPosVector& landmarks_vec() const { return landmarks; }
-    NEPoseVector& poses_vec() { return poses; }
-    LMPosVector& landmarks_vec() { return landmarks; }
+    // direct stix-order access (the reference keeps these private; the C ABI needs them). A
+    // reference from the non-const overloads counts as a write and is valid until the next step.
+    const NEPoseVector& poses_vec() const { materialize(); return poses; }
+    const LMPosVector& landmarks_vec() const { materialize(); return landmarks; }
+    NEPoseVector& poses_vec() { touch(); return poses; }
+    LMPosVector& landmarks_vec() { touch(); return landmarks; }
     const AssociationVec& pose_ids() const { return pose_stix_to_id; }
     const AssociationVec& landmark_ids() const { return lm_stix_to_id; }
 
+    // Source protocol (proj02::Solver): attach once; mark_stale after every step; take_host_writes
+    // before a step returns (and clears) whether the host values were written since.
+    void attach_source(StateSource* src) { source_ = src; stale_ = false; host_written_ = false; }
+    void mark_stale() { stale_ = source_ != nullptr; }
+    bool take_host_writes() { const bool w = host_written_; host_written_ = false; return w; }
+
   private:
-    NEPoseVector poses;
-    LMPosVector landmarks;
+    void materialize() const {
+        if (stale_) {
+            stale_ = false;
+            source_->pull_state(poses, landmarks);
+        }
+    }
+    void touch() { materialize(); host_written_ = true; }
+
+    StateSource* source_ = nullptr;
+    mutable bool stale_ = false;
+    bool host_written_ = false;
+    // mutable: a const read may refresh them from the source
+    mutable NEPoseVector poses;
+    mutable LMPosVector landmarks;
     AssociationMap pose_id_to_stix;
     AssociationVec pose_stix_to_id;
     AssociationMap lm_id_to_stix;

@@ -1,5 +1,8 @@
 """Shared helpers for the parity tests: convert between the product's problem (bos.Problem)
 and the oracle's (oracle.Problem), and bring both H's into one comparable form."""
+import contextlib
+import itertools
+
 import numpy as np
 import scipy.sparse as sp
 
@@ -52,12 +55,83 @@ def close_state(pa, la, pb, lb, rtol=1e-6, atol=1e-9):
     return ok_p and ok_l, float(np.abs(dp).max()), float(np.abs(la - lb).max() if len(lb) else 0.0)
 
 
+def knife_edge_bearings(P, tol=1e-9):
+    """Bearings whose error (the oracle's literal evaluation, at P's state) lies on the +-pi wrap:
+    their sign is decided by the last ulp of atan2 and g (the reference dataset's single-observation
+    landmarks after triangulation)."""
+    with O.literal():
+        e = O.bearing_errors(P)
+    return np.nonzero(np.abs(e) >= np.pi - tol)[0], e
+
+
+def wrap_signs_from_gpu(P, b_gpu, kt=1.0):
+    """The sign the GPU path gave each knife-edge bearing's error, read off its exported b (fp64,
+    P's state): flipping bearing k's error changes b by -2 J_k^T w e_k (robust-scaled e_k) on its
+    pose's and landmark's dofs; the combination of flips that reproduces the GPU's b (to 1e-9 of
+    max |b|) gives the signs. None when P has no such bearing. The oracle then evaluates every
+    bearing literally (Eigen's product sums, libm atan2: no code shared with the product) and only
+    takes these signs from the GPU (bos_oracle.cpp knife_edge)."""
+    ks, e = knife_edge_bearings(P)
+    if len(ks) == 0:
+        return None
+    assert len(ks) <= 10, len(ks)
+    Q = to_oracle(P)
+    with O.literal():
+        lin = O.linearize(Q, kernel_threshold=kt)
+        contrib = []
+        for k in ks:
+            ek, J = O.bearing_error_and_jacobian(P.pose_xyt[P.b_pose[k]], P.lm_xy[P.b_lm[k]], P.b_z[k])
+            w = 1.0 if P.b_omega is None else float(P.b_omega[k])
+            rho = ek * w * ek
+            es = ek * np.sqrt(kt / rho) if rho > kt else ek
+            d = np.zeros(P.N)
+            d[3 * P.b_pose[k]:3 * P.b_pose[k] + 3] = J[:3] * w * es
+            d[3 * P.NP + 2 * P.b_lm[k]:3 * P.NP + 2 * P.b_lm[k] + 2] = J[3:] * w * es
+            contrib.append(d)
+    keep = np.ones(P.N, dtype=bool)
+    keep[3 * P.fixed:3 * P.fixed + 3] = False
+    best, best_flip = None, None
+    for flips in itertools.product((False, True), repeat=len(ks)):
+        alt = lin.b - sum(2 * c for c, f in zip(contrib, flips) if f)
+        err = np.abs(b_gpu - alt)[keep].max()
+        if best is None or err < best:
+            best, best_flip = err, flips
+    assert best <= 1e-9 * np.abs(lin.b[keep]).max(), f"no sign combination of the knife-edge bearings reproduces b ({best})"
+    signs = np.zeros(len(P.b_z), dtype=np.int8)
+    for k, f in zip(ks, best_flip):
+        signs[k] = -int(np.sign(e[k])) if f else int(np.sign(e[k]))
+    return signs
+
+
+@contextlib.contextmanager
+def literal_oracle(P, b_gpu=None, kt=1.0):
+    """The oracle in its literal form for the block, with the knife-edge bearings' signs taken from
+    the GPU path's b at P's initial state (b_gpu, or one fp64 GPU linearization made here)."""
+    if b_gpu is None and len(knife_edge_bearings(P)[0]):
+        S = bos.Solver(P, kernel_threshold=kt)
+        S.linearize()
+        b_gpu = S.export_system()[3]
+        S.close()
+    signs = None if b_gpu is None else wrap_signs_from_gpu(P, b_gpu, kt)
+    with O.literal(wrap_signs=signs):
+        yield signs
+
+
 def lin_parity(P, precision=bos.BOS_FP64, kt=1.0, damping=0.01, tol=1e-12, p999=None, btol=None, **solver_kw):
+    """H, b, chi^2 of one GPU J+H build against the oracle's literal evaluation (knife-edge
+    bearings' signs from the GPU's fp64 b, literal_oracle)."""
     Q = to_oracle(P)
     S = bos.Solver(P, precision=precision, kernel_threshold=kt, damping=damping, **solver_kw)
     st = S.linearize()
     rows, cols, vals, b = S.export_system()
-    lin = O.linearize(Q, kernel_threshold=kt, damping=damping, precision=32 if precision == bos.BOS_FP32 else 64)
+    b64 = b
+    if precision != bos.BOS_FP64 and len(knife_edge_bearings(P)[0]):
+        S64 = bos.Solver(P, kernel_threshold=kt, damping=damping, **solver_kw)
+        S64.linearize()
+        b64 = S64.export_system()[3]
+        S64.close()
+    with literal_oracle(P, b64, kt):
+        lin = O.linearize(Q, kernel_threshold=kt, damping=damping, precision=32 if precision == bos.BOS_FP32 else 64)
     Hg = gpu_lower(rows, cols, vals, P.N)
     Ho = oracle_lower_nf(Q, lin)
     eh = rel_err(Hg, Ho)

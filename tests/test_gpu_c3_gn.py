@@ -18,18 +18,16 @@ Tolerances (stated here, measured margins in DESIGN.md §5):
     of iteration 1 within 1e-8 of max |dx| (two direct factorizations of one SPD system, as on C1),
     the state after 50 iterations within 1e-6 relative + 1e-9 absolute (the C1 50-iteration bound).
   * fp32 J+H + fp64 Schur solve (the benchmarked path), 50 iterations, with one lane per pose (the
-    one-GPU bench) and two (the N > 1 bench), against the oracle's fp32 J+H + fp64 solve/state: the
-    two fp32 builds sum each pose's terms in different orders, so H and b differ by fp32 rounding
-    (2e-2 max-relative / 5e-4 p99.9 per entry at config 3, tests/test_gpu_parity.py), and the
-    world's coordinates reach ~1 km, where one fp32 ulp of the state caches is 6e-5 m: every fp32
-    trajectory carries that noise, which the constant damping lets accumulate along the chain's
-    slow modes. Bounds, calibrated by the oracle's own fp32 path against its fp64 path (a single
-    fp32 path's deviation; two independent fp32 paths differ by about sqrt(2) of it): each of the
-    pose, bearing-p99.9 and bearing-max differences within 3x the oracle's fp32-vs-fp64 spread,
-    and absolutely poses <= 2e-4 (SURVEY.md §8(c)'s fp32 row, ~1e-4), bearings p99.9 <= 2e-4 and
-    max <= 1e-3 rad, chi^2 of every iteration 1e-4 relative. Measured: oracle fp32
-    vs fp64 6.4e-5 / 8.8e-5 / 3.4e-4 after 50 iterations; HIP fp32 vs oracle fp32 1.2e-4 / 1.1e-4 /
-    4.4e-4, chi^2 8.6e-6.
+    one-GPU bench) and two (the N > 1 bench), judged on ACCURACY against the fp64 answer (the
+    oracle's fp64 J+H + fp64 solve), not on agreement between two fp32 paths: the reference is fp32
+    end to end (framework/definitions.hpp:17-37), so the yardstick is how far reference-style fp32
+    arithmetic (the oracle's literal fp32 J+H: Eigen's product sums, libm atan2, no code shared
+    with the product) lands from the fp64 answer. For each of pose max |difference|, predicted
+    bearing p99.9 and max (landmarks through the bearings they predict),
+    the HIP fp32 path's distance to the fp64 answer must be <= 1.25x the oracle fp32 path's, and
+    poses <= 1.5e-4 absolutely (~1e-4). chi^2 of every iteration within 1e-4
+    relative of the oracle's fp32 chi^2. All figures are printed (the committed -s log:
+    profiles/r05_c3_fp32_accuracy.log).
   * Every step reports solver_info == 0 (no non-positive pivot, no dataflow stall), for 200
     iterations of the fp32 path; a system forced to lose positive definiteness reports its
     non-positive pivots instead (slam/solver.cpp:82-84).
@@ -124,7 +122,8 @@ def test_c3_gn_fp64_schur_matches_oracle(world, oracle_fp64):
     assert worst <= 1e-9
     assert e <= 1e-8
     ok, ep, el = close_state(pg, lg, po, lo, rtol=1e-6, atol=1e-9)
-    print(f"c3 fp64 after {FP32_ITERS} iterations: state max abs err poses {ep:.3g} landmarks {el:.3g}")
+    print(f"c3 fp64 after {FP32_ITERS} iterations: state max abs err poses {ep:.3g} landmarks {el:.3g}; "
+          f"chi2 worst rel {worst:.3g}, dx(1) rel {e:.3g}")
     assert ok, (ep, el)
     assert np.array_equal(pg[world.fixed], world.pose_xyt[world.fixed])
 
@@ -150,23 +149,27 @@ def fp32_state_errors(P, pg, lg, po, lo):
 @pytest.mark.timeout(1200)
 @pytest.mark.parametrize("lpp", [1, 2])
 def test_c3_gn_fp32_jh_schur_matches_oracle(world, oracle_fp32, oracle_fp64, lpp):
-    """The benchmarked configuration (fp32 J+H, fp64 Schur multifrontal solve, fp64 state) against
-    the oracle's fp32 J+H + fp64 solve and state over the bench's 50 iterations, with lanes_per_pose
-    1 (bench.py at N = 1) and 2 (bench.py at N > 1). Poses are compared in absolute terms, landmarks
-    through the bearing each observation predicts."""
+    """The benchmarked configuration (fp32 J+H, fp64 Schur multifrontal solve, fp64 state) over the
+    bench's 50 iterations, with lanes_per_pose 1 (bench.py at N = 1) and 2 (bench.py at N > 1),
+    measured against the oracle's fp64 answer beside reference-style fp32 (the oracle's literal fp32
+    J+H + fp64 solve and state): the HIP path must be at least as accurate, within 25 %."""
     chio, dxo, po, lo = oracle_fp32
     _, _, p64, l64 = oracle_fp64
     chig, dxg, pg, lg = hip_run(world, bos.BOS_FP32, FP32_ITERS, lanes_per_pose=lpp)
     worst = float(np.max(np.abs(chig - chio) / chio))
     e1 = np.abs(dxg - dxo).max() / np.abs(dxo).max()
-    ep, eq, eb = fp32_state_errors(world, pg, lg, po, lo)
-    rp, rq, rb = fp32_state_errors(world, po, lo, p64, l64)
-    print(f"c3 fp32 lpp={lpp} after {FP32_ITERS} iterations, HIP vs oracle fp32 J+H: chi2 worst rel {worst:.3g}, "
-          f"dx(1) rel {e1:.3g}, pose {ep:.3g}, bearing p99.9 {eq:.3g} max {eb:.3g} rad; oracle fp32 vs fp64: "
-          f"pose {rp:.3g}, bearing p99.9 {rq:.3g} max {rb:.3g}")
+    hp, hq, hb = fp32_state_errors(world, pg, lg, p64, l64)    # HIP fp32 vs the fp64 answer
+    rp, rq, rb = fp32_state_errors(world, po, lo, p64, l64)    # reference-style fp32 vs the fp64 answer
+    ep, eq, eb = fp32_state_errors(world, pg, lg, po, lo)      # the two fp32 paths (information only)
+    print(f"c3 fp32 lpp={lpp} after {FP32_ITERS} iterations vs the oracle's fp64 answer: "
+          f"HIP fp32 pose {hp:.3g} bearing p99.9 {hq:.3g} max {hb:.3g} rad; "
+          f"oracle (reference-style) fp32 pose {rp:.3g} bearing p99.9 {rq:.3g} max {rb:.3g}; "
+          f"ratios {hp / rp:.3f} / {hq / rq:.3f} / {hb / rb:.3f}. "
+          f"HIP fp32 vs oracle fp32: pose {ep:.3g} bearing p99.9 {eq:.3g} max {eb:.3g}, "
+          f"chi2 worst rel {worst:.3g}, dx(1) rel {e1:.3g}")
     assert worst <= 1e-4
-    assert ep <= 3 * rp and eq <= 3 * rq and eb <= 3 * rb
-    assert ep <= 2e-4 and eq <= 2e-4 and eb <= 1e-3
+    assert hp <= 1.25 * rp and hq <= 1.25 * rq and hb <= 1.25 * rb, (hp / rp, hq / rq, hb / rb)
+    assert hp <= 1.5e-4
     assert np.array_equal(pg[world.fixed], world.pose_xyt[world.fixed])
 
 

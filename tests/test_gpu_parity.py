@@ -21,7 +21,8 @@ import pytest
 import bos
 import oracle as O
 from conftest import C1, MINI
-from helpers import close_state as _close_state, gpu_lower, lin_parity as _lin_parity, oracle_lower_nf, rel_err, to_oracle
+from helpers import (close_state as _close_state, gpu_lower, lin_parity as _lin_parity, literal_oracle, oracle_lower_nf,
+                     rel_err, to_oracle)
 
 pytestmark = pytest.mark.gpu
 
@@ -71,7 +72,8 @@ def test_step_c1_50_iterations(c1, golden):
         assert st["solver_info"] == 0
         chis.append(st["chi2"])
     pg, lg = S.get_state()
-    po, lo, chio = O.run(Q, 50)
+    with literal_oracle(c1):
+        po, lo, chio = O.run(Q, 50)
     ok, ep, el = _close_state(pg, lg, po, lo)
     assert ok, (ep, el)
     assert np.allclose(chis, chio, rtol=1e-9, atol=1e-12)
@@ -88,7 +90,8 @@ def test_step_dx_matches_oracle(c1):
     assert S.step()["solver_info"] == 0
     dxg = S.last_dx()
     po, lo = Q.copy_state()
-    _, _, dxo = O.step(Q, po, lo)
+    with literal_oracle(c1):
+        _, _, dxo = O.step(Q, po, lo)
     # two different direct factorizations (supernodal multifrontal vs SciPy SuperLU) of the same
     # system: normwise agreement to ~cond(H_nf) * eps (host re-run of the same tree: 1.1e-10)
     assert np.abs(dxg - dxo).max() <= 1e-8 * np.abs(dxo).max()
@@ -133,15 +136,16 @@ def test_settings_changed_between_replayed_steps(c1):
     Q = to_oracle(c1)
     S = bos.Solver(c1)
     po, lo = Q.copy_state()
-    for it in range(6):
-        kt, damping = (1.0, 0.01) if it < 2 else (1e-3, 0.5) if it < 4 else (1.0, 0.01)
-        if it in (2, 4):
-            S.set_kernel_threshold(kt)
-            S.set_damping_factor(damping)
-        st = S.step()
-        assert st["solver_info"] == 0
-        chi, _, _ = O.step(Q, po, lo, kernel_threshold=kt, damping=damping)
-        assert abs(st["chi2"] - chi) <= 1e-9 * max(1.0, chi)
+    with literal_oracle(c1):
+        for it in range(6):
+            kt, damping = (1.0, 0.01) if it < 2 else (1e-3, 0.5) if it < 4 else (1.0, 0.01)
+            if it in (2, 4):
+                S.set_kernel_threshold(kt)
+                S.set_damping_factor(damping)
+            st = S.step()
+            assert st["solver_info"] == 0
+            chi, _, _ = O.step(Q, po, lo, kernel_threshold=kt, damping=damping)
+            assert abs(st["chi2"] - chi) <= 1e-9 * max(1.0, chi)
     pg, lg = S.get_state()
     ok, ep, el = _close_state(pg, lg, po, lo)
     assert ok, (ep, el)
@@ -203,7 +207,8 @@ def test_fp32_converges_like_fp64(c1):
     S = bos.Solver(c1, precision=bos.BOS_FP32)
     assert S.step_n(50)["solver_info"] == 0
     pg, lg = S.get_state()
-    po, lo, _ = O.run(to_oracle(c1), 50)
+    with literal_oracle(c1):
+        po, lo, _ = O.run(to_oracle(c1), 50)
     # landmarks with < 2 observations are unobservable along their ray (SURVEY.md §7 hard part 1)
     cnt = np.bincount(c1.b_lm, minlength=c1.NL)
     good = cnt >= 3
@@ -217,20 +222,19 @@ def c2():
 
 
 @pytest.fixture
-def literal_oracle():
+def literal_form():
     """The synthetic worlds are compared with the oracle's literal evaluation (Eigen's product sums,
     libm atan2; oracle.set_literal): no code shared with the product. Their bearings are all in
-    front of their poses, so no error sits on the +-pi wrap that made C1 need the bit-reproducing
-    form."""
+    front of their poses, so no error sits on the +-pi wrap (no knife-edge sign to take from the GPU)."""
     with O.literal():
         yield
 
 
-def test_linearize_c2_fp64(c2, literal_oracle):
+def test_linearize_c2_fp64(c2, literal_form):
     _lin_parity(c2)
 
 
-def test_step_c2_10_iterations(c2, literal_oracle):
+def test_step_c2_10_iterations(c2, literal_form):
     Q = to_oracle(c2)
     S = bos.Solver(c2)
     assert S.step_n(10)["solver_info"] == 0
@@ -260,12 +264,12 @@ def c3():
     return bos.synthetic(100000, 200000, 10)
 
 
-def test_linearize_c3_fp64_full(c3, literal_oracle):
+def test_linearize_c3_fp64_full(c3, literal_form):
     """Full-size (config 3) J+H build against the oracle's, entry by entry."""
     _lin_parity(c3, tol=5e-11, p999=1e-12)
 
 
-def test_linearize_c3_fp32_full(c3, literal_oracle):
+def test_linearize_c3_fp32_full(c3, literal_form):
     _lin_parity(c3, precision=bos.BOS_FP32, tol=2e-2, p999=5e-4)
 
 
@@ -366,6 +370,7 @@ def test_headless_driver_50_iterations_matches_oracle(c1, tmp_path):
     assert res.returncode == 0, res.stdout + res.stderr
     D = bos.load_g2o(str(out), triangulate=False)
     assert np.array_equal(D.pose_ids, c1.pose_ids) and np.array_equal(D.lm_ids, c1.lm_ids)
-    po, lo, _ = O.run(to_oracle(c1), 50)
+    with literal_oracle(c1):
+        po, lo, _ = O.run(to_oracle(c1), 50)
     ok, ep, el = _close_state(D.pose_xyt, D.lm_xy, po, lo)
     assert ok, (ep, el)

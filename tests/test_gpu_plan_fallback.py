@@ -9,7 +9,7 @@ import pytest
 import bos
 import oracle as O
 from conftest import C1
-from helpers import close_state, to_oracle
+from helpers import close_state, literal_oracle, to_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -28,6 +28,7 @@ def test_schur_plan_with_large_fronts_matches_oracle(which, iters):
     for _ in range(iters):
         assert S.step()["solver_info"] == 0
     pg, lg = S.get_state()
-    po, lo, _ = O.run(to_oracle(P), iters)
+    with literal_oracle(P):
+        po, lo, _ = O.run(to_oracle(P), iters)
     ok, ep, el = close_state(pg, lg, po, lo)
     assert ok, (ep, el)

@@ -19,7 +19,7 @@ import pytest
 import bos
 import oracle as O
 from conftest import C1, C1_GT
-from helpers import close_state, to_oracle
+from helpers import close_state, literal_oracle, to_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -65,7 +65,8 @@ def _run(noiseless):
     S.close()
     P.lm_xy[:] = xy
     Q = to_oracle(P)
-    po, lo, chis = O.run(Q, 50)
+    with literal_oracle(P):
+        po, lo, chis = O.run(Q, 50)
     ok, ep, el = close_state(pg, lg, po, lo, rtol=1e-6, atol=1e-9)
     assert ok, (ep, el)
     return P, pg, lg, gtp, gtl, cnt, chis, st

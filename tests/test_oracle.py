@@ -64,14 +64,24 @@ def test_normalized_angle_huge_and_non_finite(precision):
             assert math.isnan(r) or (math.isfinite(a) and -PI <= r < PI), (a, r)
             if not math.isfinite(a):
                 assert math.isnan(r), (a, r)
-    for a in (7.0, -7.0, 123456.7, 1e6, -1e6, 1.5e6, 1e9, -3.3e12, 1e14):
+    for a in (7.0, -7.0, 123456.7, 1e6, -1e6, 1.5e6, -2.5e7, 1e8, 1e9, -3.3e12, 1e14):
         a = cast(a)
         r, o = prod(a), O.normalized_angle(a, precision)
+        if math.isnan(o):   # the reference's loop never ends: a step of 2 pi rounds back to a (float)
+            assert precision == 32 and float(np.float32(a - 2 * PI)) == a, (a, o)
+            o = r
         assert -PI <= r < PI and -PI <= o < PI, (a, r, o)
         if precision == 64:   # (fp32: the reference's loop rounds every +-2 pi step to float)
             assert abs(math.remainder(r - a, 2 * PI)) <= 1e-6 * max(1.0, abs(a)), (a, r)
         if abs(a) <= 1e6:
             assert r == o, (a, r, o)
+        elif precision == 64 and abs(a) <= 1e9:
+            # the oracle runs the reference's loop: it rounds each of its |a| / 2 pi
+            # steps, the product subtracts the nearest multiple of 2 pi once; they agree to the
+            # loop's accumulated rounding (half an ulp of a per step). Past 1e9 (and for fp32,
+            # where a step rounds to float) the range is parity-unpinned: both in [-pi, pi) only.
+            steps = abs(a) / (2 * PI) + 1
+            assert abs(math.remainder(r - o, 2 * PI)) <= steps * 0.5 * math.ulp(a), (a, r, o)
 
 
 def test_smallest_angle():
@@ -242,6 +252,39 @@ def test_literal_and_bit_reproducing_forms_agree():
     for x, y in ((a.b, b.b), (a.pose_diag, b.pose_diag), (a.lm_diag, b.lm_diag), (a.hpl, b.hpl)):
         assert np.abs(x - y).max() <= 1e-13 * np.abs(x).max()
     assert abs(a.chi2 - b.chi2) <= 1e-13 * a.chi2
+
+
+def test_knife_edge_signs_literal_oracle_reference_dataset():
+    """The reference dataset in the literal form (no code shared with the product). Three bearings
+    sit exactly on the +-pi wrap after triangulation (landmarks 69, 112 and 114, one observation
+    each); their error's sign is the last ulp's choice, and the two forms disagree on
+    landmark 112's. tests/helpers.wrap_signs_from_gpu reads the signs off a GPU b; here the
+    bit-reproducing form's b stands in for it. With those signs the literal form's b equals it to
+    1e-13 relative (|e| and b up to sign: the flips are exact) and 50 GN iterations agree to the C1
+    state bound (1e-6 relative + 1e-9); without them landmark 112 ends 0.8 m away."""
+    import bos
+    from helpers import close_state, knife_edge_bearings, to_oracle, wrap_signs_from_gpu
+    P = bos.load_g2o(C1)
+    ks, e = knife_edge_bearings(P)
+    assert sorted(int(P.lm_ids[P.b_lm[k]]) for k in ks) == [69, 112, 114]
+    assert np.all(np.abs(np.abs(e[ks]) - np.pi) < 1e-12)
+    Q = to_oracle(P)
+    stand_in = O.linearize(Q).b                       # bit-reproducing form (what the GPU computes)
+    signs = wrap_signs_from_gpu(P, stand_in)
+    assert np.count_nonzero(signs) == 3
+    keep = np.ones(P.N, dtype=bool)
+    keep[3 * P.fixed:3 * P.fixed + 3] = False
+    with O.literal(wrap_signs=signs):
+        lit = O.linearize(Q).b
+        po, lo, _ = O.run(Q, 50)
+    assert np.abs(lit - stand_in)[keep].max() <= 1e-13 * np.abs(stand_in[keep]).max()
+    with O.literal():                                  # the literal form's own sign for 112 differs
+        plain = O.linearize(Q).b
+    assert np.abs(plain - stand_in)[keep].max() > 1e-3
+    pb, lb, _ = O.run(Q, 50)
+    ok, ep, el = close_state(po, lo, pb, lb)
+    assert ok, (ep, el)
+    assert O.lib().oracle_get_literal() == 0
 
 
 def test_convergence_pins(c1):

@@ -18,6 +18,7 @@ sharded iteration must reproduce the single-GPU iteration bit for bit.
 The 8-GPU RCCL run itself is the driver's scaling bench (bench.py --gpus 8)."""
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -375,11 +376,24 @@ def _gpu_p2p_worker(rank, world, port, q, iters):
         S.p2p_connect(handles)
         dist.barrier()
         stats = [S.step() for _ in range(iters)]
+        # bos_step_n batches (the ranks run ahead of each other inside a batch: the exchange-1 headers
+        # must be read from phase 1's local copy), rank 1 starting each batch 0.3 s late
+        # (a host-side gap longer than the old 50 ms wait bound, well inside the 2 s default)
+        for _ in range(3):
+            if rank == 1:
+                time.sleep(0.3)
+            stats.append(S.step_n(5))
+        with_phase_api = None
+        try:
+            S.step_phase(0)
+        except bos.BosError as e:
+            with_phase_api = str(e)
         pose, lm = S.get_state()
         owner = S.node_owner()
         dist.barrier()
         S.close()
         dist.destroy_process_group()
+        assert with_phase_api and "exchanges directly" in with_phase_api, with_phase_api
         q.put((rank, pose, lm, owner, stats, None))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, None, None, None, None, repr(e)))
@@ -390,16 +404,20 @@ def test_two_processes_p2p_exchange():
     """Two ranks in two processes on the one GPU exchanging directly (each writes into the other's
     mailbox through a HIP IPC mapping and raises its flag there; no collective library, no host
     copies): the merged state after 3 iterations equals the single-process run bit for bit, and
-    both ranks report the same chi^2 (combined from both ranks' headers)."""
+    both ranks report the same chi^2 (combined from both ranks' headers). Then three bos_step_n
+    batches of 5, rank 1 starting each 0.3 s late: every batch's chi^2 equal on both ranks and to the
+    single-process run's iteration, the merged state after all 18 iterations equal to it bit for bit;
+    once connected, the external phase API refuses the handle."""
     import bos
     world, iters = 2, 3
     res = _spawn(_gpu_p2p_worker, world, (iters,), timeout=300)
     P = bos.synthetic(1000, 2000, 20)
     owner = res[0][3]
     pm, lm_ = _merge(P, [(r[1], r[2]) for r in res], owner)
-    (p1, l1), st1 = _run_one(P, iters, bos.BOS_FP64)
+    (p1, l1), st1 = _run_one(P, iters + 15, bos.BOS_FP64)
     assert np.array_equal(pm, p1) and np.array_equal(lm_, l1)
-    for it in range(iters):
-        assert res[0][4][it]["chi2"] == res[1][4][it]["chi2"]
-        assert abs(res[0][4][it]["chi2"] - st1[it]["chi2"]) <= 1e-12 * st1[it]["chi2"]
+    one = [st1[i] for i in range(iters)] + [st1[iters + 5 * b + 4] for b in range(3)]
+    for it in range(iters + 3):
+        assert res[0][4][it]["chi2"] == res[1][4][it]["chi2"], it
+        assert abs(res[0][4][it]["chi2"] - one[it]["chi2"]) <= 1e-12 * one[it]["chi2"], it
         assert res[0][4][it]["solver_info"] == 0 and res[1][4][it]["solver_info"] == 0
