@@ -378,6 +378,8 @@ def main():
 
     S, info, ranks_seen = make_handle(bos.BOS_PARTITION_SUBTREE, rccl=args.exchange == "rccl")
     exchange = "single GPU" if world == 1 else ("gloo rehearsal" if args.exchange == "gloo" else "rccl")
+    exchange_reason = {"p2p": None, "rccl": "--exchange rccl", "gloo": "--exchange gloo (rehearsal)"}[args.exchange] \
+        if world > 1 else None
     if world > 1 and args.exchange == "p2p":
         # Every rank maps every other rank's mailbox (HIP IPC), then three GN steps from the initial
         # guess must give every rank the same chi^2 (each rank combines all ranks' headers, so a
@@ -400,12 +402,15 @@ def main():
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         if int(flag.item()) == 1 and bool(torch.equal(lo, hi)):
             exchange = "p2p"
+            exchange_reason = ("every rank mapped every other rank's mailbox (HIP IPC, peer access) and three GN steps "
+                               "gave every rank the same chi^2")
         else:
             why = why or ("on another rank" if int(flag.item()) != 1 else "the ranks' chi^2 differ")
             log(f"rank {rank}: direct exchange unusable ({why}); RCCL all-gathers instead")
             S.close()
             S, info, ranks_seen = make_handle(bos.BOS_PARTITION_SUBTREE, rccl=True)
             exchange = "rccl (direct exchange failed its check)"
+            exchange_reason = f"direct exchange unusable: {why}"
 
     # ---- one GN iteration, per exchange mode
     def gloo_allgather(h, which):
@@ -464,10 +469,32 @@ def main():
         return {k: float(np.median([g[k] for g in stats])) for k in
                 ("t_linearize_ms", "t_exchange_ms", "t_solve_ms", "t_update_ms")}
 
+    def rank_breakdown(h, partition, steps=20):
+        """Per-rank phase times (device stamps of the step's own kernels, bos_last_step_stamps), the
+        median over `steps` untimed GN iterations after the timed region, gathered to every rank:
+        J+H, own subtrees (solver inputs, factorization and forward of this rank's subtrees, exchange-1
+        pack), exchange-1 wait, replicated top (its factorization and solves) + own backward + pack,
+        exchange-2 wait, box-plus + status. Lists in rank order."""
+        init = h.get_state()
+        rows = []
+        for _ in range(steps):
+            gn_step(h, partition)
+            t = h.last_step_stamps().astype(np.int64)
+            d = lambda a, b: max(0.0, float(t[b] - t[a]) * 1e-5)   # ms (100 MHz ticks)
+            rows.append([d(0, 1), d(1, 4), d(4, 5), d(5, 6), d(6, 7), d(7, 3), d(0, 3)])
+        h.set_state(*init)
+        med = [float(x) for x in np.median(np.array(rows), axis=0)]
+        allr = [None] * world
+        dist.all_gather_object(allr, med)
+        keys = ("jh_ms", "own_subtrees_ms", "exchange1_wait_ms", "top_and_backward_ms", "exchange2_wait_ms",
+                "update_ms", "step_device_ms")
+        return {k: [r[i] for r in allr] for i, k in enumerate(keys)}
+
     # ---- the timed region: K GN iterations; the J+H inside them is the headline (K = 0: no GN steps,
     # the J+H builds alone, for profiling runs)
     wall, stats, phase, jh_ms, gn_it_s = 0.0, [], None, None, None
     ranks_consistent = None
+    per_rank = None
     if args.steps > 0:
         wall, stats = timed_steps(S, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup, args.device_warmup)
         phase = phases(stats)
@@ -481,6 +508,8 @@ def main():
                 log(f"error: rank {rank}: the ranks' per-step chi^2 differ (exchange {exchange})")
                 sys.exit(3)
         jh_ms = max_over_ranks(phase["t_linearize_ms"])      # the slowest rank's in-step J+H
+        if world > 1:
+            per_rank = rank_breakdown(S, partition=bos.BOS_PARTITION_SUBTREE)
         gn_it_s = args.steps / wall
         log(f"rank {rank}: {args.steps} GN steps in {wall * 1e3:.1f} ms ({gn_it_s:.0f} it/s); phases {phase}")
 
@@ -617,6 +646,9 @@ def main():
             },
             "ranks_seen": ranks_seen,
             "ranks_consistent": ranks_consistent,
+            "exchange_decision": {"mode": exchange, "reason": exchange_reason} if world > 1 else None,
+            # N > 1: per-rank phase medians (device stamps), rank order (rank_breakdown)
+            "per_rank": per_rank,
             "devices": 1 if (args.same_device or world == 1) else world,
             "timed_region_ms": wall * 1e3,
             "gn_iters_per_s": gn_it_s,

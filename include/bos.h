@@ -247,6 +247,13 @@ int bos_get_state(const struct bos_solver* s, double* pose_xyt, double* landmark
 int bos_set_state(struct bos_solver* s, const double* pose_xyt, const double* landmark_xy);
 /* The dx of the last bos_step in the reference's dof order (slam/solver.cpp:88-94) */
 int bos_get_last_dx(const struct bos_solver* s, double* dx);
+/* Diagnostics: the phase boundaries of the last completed step, realtime clock (100 MHz ticks),
+ * as the step's own kernels stamped them: [0] J+H start, [1] J+H end / solve start, [2] solve end,
+ * [3] step end; subtree-sharded handles: [4] phase 0 done (own subtrees factored, exchange 1
+ * starts), [5] exchange 1 received (replicated top starts), [6] phase 1 done (top factored and
+ * solved, own subtrees solved backward; exchange 2 starts), [7] exchange 2 received (box-plus
+ * starts). bench.py reports them per rank. */
+int bos_last_step_stamps(const struct bos_solver* s, uint64_t stamps[8]);
 
 #ifdef __cplusplus
 }

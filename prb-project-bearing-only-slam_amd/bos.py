@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = [
     "bos_time_linearize", "bos_time_triangulate", "bos_time_steps", "bos_cpu_gn_create", "bos_cpu_gn_step", "bos_cpu_gn_get_state",
     "bos_cpu_gn_destroy", "bos_normalized_angle_f64", "bos_normalized_angle_f32", "bos_exchange_p2p_handle",
     "bos_exchange_p2p_connect", "bos_time_facade_steps", "bos_debug_facade_selftest", "bos_set_exchange_timeout",
+    "bos_last_step_stamps",
 ]
 
 P2P_HANDLE_BYTES = 64   # include/bos.h BOS_P2P_HANDLE_BYTES
@@ -189,6 +190,7 @@ def lib():
         "bos_exchange_p2p_handle": (ctypes.c_int, [vp, ctypes.c_void_p]),
         "bos_exchange_p2p_connect": (ctypes.c_int, [vp, ctypes.c_void_p]),
         "bos_set_exchange_timeout": (ctypes.c_int, [vp, ctypes.c_double]),
+        "bos_last_step_stamps": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "bos_normalized_angle_f64": (ctypes.c_double, [ctypes.c_double]),
         "bos_normalized_angle_f32": (ctypes.c_float, [ctypes.c_float]),
         "bos_time_facade_steps": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options), ctypes.c_int32,
@@ -593,6 +595,13 @@ class Solver:
         blob = b"".join(handles)
         buf = ctypes.create_string_buffer(blob, len(blob))
         _check(lib().bos_exchange_p2p_connect(self._h, buf), "bos_exchange_p2p_connect")
+
+    def last_step_stamps(self) -> np.ndarray:
+        """Phase stamps of the last step (bos_last_step_stamps; 100 MHz realtime ticks)."""
+        st = np.zeros(8, dtype=np.uint64)
+        _check(lib().bos_last_step_stamps(self._h, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))),
+               "bos_last_step_stamps")
+        return st
 
     def set_exchange_timeout(self, seconds: float) -> None:
         """Bound of the direct exchange's device-side flag waits (bos_set_exchange_timeout, 2 s default)."""

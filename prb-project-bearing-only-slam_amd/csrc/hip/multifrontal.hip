@@ -35,6 +35,9 @@ namespace dev {
 namespace {
 
 constexpr int kMfBlock = 256;
+#ifdef BOS_MF_PIVOT_CYCLES
+__device__ unsigned long long* g_pivot_bwd;   // diagnostic build: the stamp buffer's backward half
+#endif
 constexpr int kLdsCapM = 90;   // larger fronts up to 90 x 90 doubles (64.8 KB) are factored in LDS
 
 __device__ __forceinline__ int64_t pk(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }
@@ -300,8 +303,22 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 
 // phase stamp k of front s (lane 0; the product launches pass no stamp buffer)
 __device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
+#ifdef BOS_MF_PIVOT_CYCLES
+    if (stp && stp == g_pivot_bwd) return;   // the backward half holds the pivot-loop cycle stamps
+#endif
     if (stp && (threadIdx.x & 63) == 0) stp[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
 }
+#ifdef BOS_MF_PIVOT_CYCLES
+// Diagnostic build only (tools/pivot_cycles.py): core-clock stamps of the pivot loop of every front
+// in the backward half of the stamp buffer: [0] loop start, [1..6] after two-pivot step i, [7] end.
+__device__ __forceinline__ void cstamp(unsigned long long* stpb, int s, int k) {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (stpb && (threadIdx.x & 63) == 0) stpb[8 * (int64_t)s + k] = t;
+}
+#endif
 
 // Folded landmark children (Schur ordering) of front s, eliminated by its wave: per chunk (whole
 // children, <= 64 row groups, <= fold_chunk_landmarks(m) landmarks) lane q takes one observing pose
@@ -813,10 +830,19 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         extend_child<COH>(a, pq, F, wv, m, lane);
     }
     const bool live = lane < m;
+#ifdef BOS_MF_BLOCKED
+    // Blocked: the pivot loop factors the k panel columns only (rows >= k become L21 as they go);
+    // the trailing r x r block stays in F and receives -L21 L21^T from f64 MFMA after the loop.
+    const int ncol = k;
+    double* const L21s = F;   // L21 column-major, row stride RS (odd), over F's panel columns (read by now)
+    const int RS = r | 1;
+#else
+    const int ncol = m;
+#endif
     double row[MAXM];
 #pragma unroll
-    for (int c0 = 0; c0 < MAXM; c0 += 8) {   // whole groups of 8 past m skipped by a scalar branch
-        if (c0 < m) {
+    for (int c0 = 0; c0 < MAXM; c0 += 8) {   // whole groups of 8 past ncol skipped by a scalar branch
+        if (c0 < ncol) {
 #pragma unroll
             for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk32(lane, c, m)] : 0.0;
         } else {
@@ -836,6 +862,10 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     int nbad = 0;   // non-positive pivots (uniform), reported once per front
     double* Lj = Ls + lane;
     int j = 0;
+#ifdef BOS_MF_PIVOT_CYCLES
+    unsigned long long* const cst = stp ? g_pivot_bwd : nullptr;
+    cstamp(cst, s, 0);
+#endif
     // Two pivots per step: column j + 1 is brought up to date in registers (L(j+1, j) by readlane),
     // both columns go through ONE LDS broadcast as pairs, and the trailing columns take a rank-2
     // update; the window rotates by two.
@@ -869,8 +899,14 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             const double y1 = readlane_d(wi, j + 1) * inv1;
             if (lane == j + 1) wi = y1;
             else if (lane > j + 1) wi -= l1 * y1;
+#ifdef BOS_MF_BLOCKED
+            if (lane >= k && live) {
+                L21s[j * RS + (lane - k)] = l0;
+                L21s[(j + 1) * RS + (lane - k)] = l1;
+            }
+#endif
             wave_sync();
-            const int nt = m - j - 2;                            // live columns after this step
+            const int nt = ncol - j - 2;                         // live columns after this step
 #pragma unroll
             for (int t0 = 0; t0 < MAXM - 2; t0 += 8) {
                 if (t0 < nt) {
@@ -885,6 +921,9 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
                 }
             }
             __builtin_amdgcn_wave_barrier();   // the next step's pair stores stay after these reads
+#ifdef BOS_MF_PIVOT_CYCLES
+            if (j / 2 < 6) cstamp(cst, s, 1 + j / 2);
+#endif
         }
     }
 #pragma nounroll
@@ -912,7 +951,10 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         if (lane == j) wi = yj;
         else if (lane > j) wi -= lij * yj;
         const double g = lij * inv;                          // L[i, j] / L[j, j]
-        const int nt = m - j - 1;                            // live columns after this step (uniform)
+        const int nt = ncol - j - 1;                         // live columns after this step (uniform)
+#ifdef BOS_MF_BLOCKED
+        if (lane >= k && live) L21s[j * RS + (lane - k)] = lij;
+#endif
 #pragma unroll
         for (int u = 0; u < 8; ++u)
             if (u < MAXM - 1) row[u] = fma(-g, c0v[u], row[u + 1]);   // -= L[i,j] L[l,j], l = j + 1 + t
@@ -927,7 +969,67 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             }
         }
     }
+#ifdef BOS_MF_PIVOT_CYCLES
+    cstamp(cst, s, 7);
+#endif
     if (nbad && lane == 0) atomicAdd(a.info, nbad);
+#ifdef BOS_MF_BLOCKED
+    // S = A22 - L21 L21^T on f64 MFMA (16 x 16 blocks, 4 panel columns per step; lane l feeds row
+    // 16 b + (l & 15), column 4 st + (l >> 4) of L21, as in the fold's W W^T), then in place into F
+    wave_sync();
+    if (r > 0) {
+        constexpr int NB = (MAXM + 15) / 16, NPB = NB * (NB + 1) / 2;
+        const int nbr = (r + 15) >> 4;
+        dbl4 acc[NPB];
+#pragma unroll
+        for (int q = 0; q < NPB; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+        for (int st = 0; 4 * st < k; ++st) {
+            const int jc = 4 * st + (lane >> 4);
+            double av[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int i = 16 * b + (lane & 15);
+                const double v = L21s[min(jc, k - 1) * RS + min(i, r - 1)];
+                av[b] = (b < nbr && i < r && jc < k) ? v : 0.0;
+            }
+            int q = 0;
+#pragma unroll
+            for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+                for (int bj = 0; bj <= bi; ++bj, ++q)
+                    if (bi < nbr) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], av[bj], acc[q], 0, 0, 0);
+        }
+        int q = 0;
+#pragma unroll
+        for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+            for (int bj = 0; bj <= bi; ++bj, ++q) {
+                if (bi < nbr) {
+                    const int jj = 16 * bj + (lane & 15);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int ii = 16 * bi + (lane >> 4) + 4 * e;
+                        if (ii < r && jj <= ii) F[pk32(k + ii, k + jj, m)] -= acc[q][e];
+                    }
+                }
+            }
+        wave_sync();
+    }
+    fstamp(stp, s, 5);
+    // the update matrix: the trailing block of F, row by row (lane k + i stores row i)
+#pragma unroll
+    for (int t0 = 0; t0 < MAXM; t0 += 8) {
+        if (t0 < r) {
+            double uv[8];
+#pragma unroll
+            for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
+                uv[t - t0] = (live && lane >= k && t <= lane - k) ? F[pk32(lane, k + min(t, max(lane - k, 0)), m)] : 0.0;
+#pragma unroll
+            for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
+                if (live && lane >= k && t <= lane - k) stc<COH>(Us + pk(lane - k, t, r), uv[t - t0]);
+        }
+    }
+#else
     fstamp(stp, s, 5);
     // the update matrix: row[t] holds column k + t
 #pragma unroll
@@ -938,6 +1040,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
                 if (live && lane >= k && t <= lane - k) stc<COH>(Us + pk(lane - k, t, r), row[t]);
         }
     }
+#endif
     if (live) {
         if (lane < k) a.x[c0 + lane] = wi;
         else stc<COH>(us + (lane - k), wi);
@@ -1602,7 +1705,13 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
 
 int32_t* mf_info_ptr(const MfDevice* d) { return d->info; }
 uint32_t* mf_epoch_ptr(const MfDevice* d) { return d->epoch; }
-void mf_debug_set_stamps(MfDevice* d, unsigned long long* stamps) { d->stamps = stamps; }
+void mf_debug_set_stamps(MfDevice* d, unsigned long long* stamps) {
+    d->stamps = stamps;
+#ifdef BOS_MF_PIVOT_CYCLES
+    unsigned long long* b = stamps ? stamps + 8 * (int64_t)d->nsuper : nullptr;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pivot_bwd), &b, sizeof(b));
+#endif
+}
 int32_t* mf_tickets_ptr(const MfDevice* d) { return d->tickets; }
 double* mf_update_ptr(const MfDevice* d) { return d->U; }
 double* mf_uvec_ptr(const MfDevice* d) { return d->u; }

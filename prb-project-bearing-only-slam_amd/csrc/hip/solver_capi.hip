@@ -1848,6 +1848,14 @@ int bos_set_state(bos_solver* s, const double* pose_xyt, const double* landmark_
     return BOS_OK;
 }
 
+int bos_last_step_stamps(const bos_solver* s, uint64_t stamps[8]) {
+    if (!s || !stamps) return fail(BOS_ERR_INVALID, "null argument");
+    bos::dev::StepStatus h;
+    std::memcpy(&h, (const void*)s->h_status, sizeof(h));   // the last step's summary (host-mapped)
+    for (int i = 0; i < 8; ++i) stamps[i] = h.stamp[i];
+    return BOS_OK;
+}
+
 int bos_get_last_dx(const bos_solver* s, double* dx) {
     if (!s || !dx) return fail(BOS_ERR_INVALID, "null argument");
     if (s->sharded) return fail(BOS_ERR_UNSUPPORTED, "bos_get_last_dx on a subtree-sharded handle (a rank holds part of x)");
