@@ -43,14 +43,26 @@ constexpr int kLdsCapM = 90;   // larger fronts up to 90 x 90 doubles (64.8 KB) 
 __device__ __forceinline__ int64_t pk(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }
 __device__ __forceinline__ int pk32(int i, int j, int m) { return j * m - j * (j - 1) / 2 + (i - j); }   // LDS fronts
 
+// L panel traffic (written by the factorization, read once by the backward substitution) as
+// non-temporal accesses: the solve's ~300 MB of L then streams past the caches instead of evicting
+// the next J+H build's inputs (in-step J+H 16.0-16.5 -> 14.2-14.5 us, solve -6 us).
+// -DBOS_MF_CACHED_L (A/B only) restores plain accesses.
+#ifndef BOS_MF_CACHED_L
+#define ST_L(p, i, v) __builtin_nontemporal_store((v), (p) + (i))
+#define LD_L(p, i) __builtin_nontemporal_load((p) + (i))
+#else
+#define ST_L(p, i, v) ((p)[i] = (v))
+#define LD_L(p, i) ((p)[i])
+#endif
+
 // Copy n doubles global -> LDS by one wavefront, 8 independent loads in flight per lane.
-template <int U = 8> __device__ __forceinline__ void stage_lds(double* dst, const double* src, int n, int lane) {
+template <int U = 8, bool NTL = false> __device__ __forceinline__ void stage_lds(double* dst, const double* src, int n, int lane) {
     for (int e0 = 0; e0 < n; e0 += 64 * U) {
         double v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int e = e0 + 64 * u + lane;
-            v[u] = e < n ? src[e] : 0.0;
+            v[u] = e < n ? (NTL ? LD_L(src, e) : src[e]) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -76,6 +88,25 @@ template <bool COH> __device__ __forceinline__ double ldc(const double* p) {
 template <bool COH> __device__ __forceinline__ void stc(double* p, double v) {
     if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = v;
+}
+
+// Tagged granules (cdna_hip_programming.md §6 Guideline 16, R2: the data is the flag). A double
+// travels as two 8-byte granules {epoch, 32 bits of it}, each written by one relaxed agent-scope
+// atomic store (sc1, write-through) and read by relaxed agent-scope atomic loads (sc1): a consumer
+// that sees the step's epoch in both tags holds the value, with no flag, no drain of the producer's
+// stores and no second load round trip. The epoch is the GN step's (never 0, bumped per step), so
+// granules of earlier steps never match.
+__device__ __forceinline__ void tag_pair(unsigned long long* g, double v, uint32_t epoch) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v), t = (unsigned long long)epoch << 32;
+    __hip_atomic_store(g, t | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 1, t | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one read of a tagged pair: *ok &= both tags current; the value assembled from the halves
+__device__ __forceinline__ double untag_pair(const unsigned long long* g, uint32_t epoch, bool& ok) {
+    const unsigned long long lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ok = ok && (uint32_t)(lo >> 32) == epoch && (uint32_t)(hi >> 32) == epoch;
+    return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
 }
 
 struct MfArgs {
@@ -114,6 +145,14 @@ struct MfArgs {
     const int64_t* emap_off;        // packed position emap[emap_off[c] + e] of its parent's front (wave fronts)
     unsigned long long* stamps_f;   // diagnostics (mf_debug_set_stamps): factor / backward stamps, or null
     unsigned long long* stamps_b;
+    // tagged hand-offs inside a dataflow launch (tag_pair / sweep): a flow front whose parent is in
+    // the same flow publishes its update matrix and u-vector as tagged granules at Ug + ug_off[s]
+    // (-1: plain U / u); every backward front publishes its solved x as tagged granules xg[2 dof]
+    unsigned long long* Ug;
+    const int64_t* ug_off;
+    unsigned long long* xg;
+    const int8_t* xtag;             // per supernode: its x is read by a backward flow front (write xg)
+    const uint32_t* epoch;          // the GN step's epoch (device word, mf_epoch_ptr)
 };
 
 // LDS of one wave's fold chunk: the y (forward-step) values of its landmarks, two per landmark
@@ -150,9 +189,17 @@ __device__ __forceinline__ void assemble_wave(const MfArgs& a, int q0_, int q1, 
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = a.A[src[u]];
+        if (add) {   // (uniform) the four front entries read at once, as in extend_child
+            double f[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) f[u] = F[dst[u]];
+            asm volatile("" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += f[u];
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (q0 + 64 * u + lane < q1) F[dst[u]] = add ? F[dst[u]] + v[u] : v[u];
+            if (q0 + 64 * u + lane < q1) F[dst[u]] = v[u];
     }
 }
 
@@ -278,6 +325,10 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
         __syncthreads();
     }
     for (int j = tid; j < k; j += kMfBlock) a.x[c0 + j] = w[j];
+    if (a.xtag[s]) {
+        const uint32_t ep = *a.epoch;
+        for (int j = tid; j < k; j += kMfBlock) tag_pair(a.xg + 2 * (int64_t)(c0 + j), w[j], ep);
+    }
 }
 
 // One wavefront per front with m <= MAXM, the factorization in registers: lane i holds row i of
@@ -309,8 +360,9 @@ __device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
     if (stp && (threadIdx.x & 63) == 0) stp[8 * (int64_t)s + k] = __builtin_amdgcn_s_memrealtime();
 }
 #ifdef BOS_MF_PIVOT_CYCLES
-// Diagnostic build only (tools/pivot_cycles.py): core-clock stamps of the pivot loop of every front
-// in the backward half of the stamp buffer: [0] loop start, [1..6] after two-pivot step i, [7] end.
+// Diagnostic build only (tools/pivot_cycles.py): core-clock stamps of every front in the backward
+// half of the stamp buffer: [1] children ready, [2] their values loaded, [3] extend-added, [0] pivot
+// loop start (rows in registers), [4..6] after two-pivot steps 1-3, [7] pivot loop end.
 __device__ __forceinline__ void cstamp(unsigned long long* stpb, int s, int k) {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -471,12 +523,12 @@ __device__ __forceinline__ void fold_chunk(const MfArgs& a, double* W, FoldBuf* 
         for (int g = 0; g < 3; ++g) {
             lt0[g] = v.h[2 * g] * i0;
             lt1[g] = (v.h[2 * g + 1] - lt0[g] * l10) * i1;
-            Lc[2 + t + g] = lt0[g];
-            Lc[mc + 2 + t + g] = lt1[g];
+            ST_L(Lc, 2 + t + g, lt0[g]);
+            ST_L(Lc, mc + 2 + t + g, lt1[g]);
         }
-        Lc[0] = l00;
-        Lc[1] = l10;
-        Lc[mc + 1] = l11;
+        ST_L(Lc, 0, l00);
+        ST_L(Lc, 1, l10);
+        ST_L(Lc, mc + 1, l11);
         a.x[col0] = y0;
         a.x[col0 + 1] = y1;
         nbad += head ? (int)bad0 + (int)bad1 : 0;
@@ -708,6 +760,7 @@ struct ChildPre {
     const double* Uc;
     const double* uc;
     const int16_t* ec;
+    const unsigned long long* G;    // tagged update matrix + u-vector (a child in the same flow), or null
 };
 
 // (Every structure and value array is padded by kMfPad elements, so the clamped reads below stay in
@@ -719,6 +772,8 @@ __device__ __forceinline__ void child_meta(const MfArgs& a, int c, int lane, Chi
     p.Uc = a.U + a.U_off[c];
     p.uc = a.u + a.u_off[c];
     p.ec = a.emap + a.emap_off[c];
+    const int64_t go = a.ug_off[c];
+    p.G = go >= 0 ? a.Ug + go : nullptr;
     const int sv = a.rmap[roff + min(lane, max(rc - 1, 0))];
     p.smap_v = lane < rc ? sv : 0;
     const int ne = rc * (rc + 1) / 2;
@@ -744,10 +799,43 @@ __device__ __forceinline__ void child_vals(int lane, ChildPre& p) {
     }
 }
 
+// A child of the same flow (p.G): poll its tagged update matrix and u-vector until every granule
+// carries this step's epoch (the data is the flag: no completion flag, no second load round trip),
+// keeping the u-vector entry and the first 256 entries. Bounded like wait_done: a stall marks info
+// and returns (the launch then drains, the step fails).
+__device__ __forceinline__ void child_sweep(ChildPre& p, uint32_t epoch, int lane, int32_t* info) {
+    const int rc = p.rc, ne = rc * (rc + 1) / 2;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t it = 0;; ++it) {
+        bool ok = true;
+        const double uv = untag_pair(p.G + 2 * (int64_t)(ne + min(lane, max(rc - 1, 0))), epoch, ok);
+        p.uval = lane < rc ? uv : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = 64 * u + lane;
+            const double v = untag_pair(p.G + 2 * (int64_t)min(e, max(ne - 1, 0)), epoch, ok);
+            p.v[u] = e < ne ? v : 0.0;
+        }
+        for (int e0 = 256; e0 < ne; e0 += 256)   // later entries: checked here, read in extend_child
+#pragma unroll
+            for (int u = 0; u < 4; ++u) (void)untag_pair(p.G + 2 * (int64_t)min(e0 + 64 * u + lane, ne - 1), epoch, ok);
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) return;
+        if ((it & 15) == 15) {
+            const bool stalled = (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kMfStall) != 0;
+            if (stalled || __builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {   // 50 ms, as wait_done
+                if (lane == 0) atomicOr(info, kMfStall);
+                return;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 // Extend-add of one child: every entry of its packed update matrix added at its precomputed position
 // in the parent's packed front (positions of one child are distinct), then its u-vector.
 template <bool COH>
-__device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p, double* F, double* wv, int m, int lane) {
+__device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p, double* F, double* wv, int m, int lane,
+                                             uint32_t epoch = 0) {
     const int rc = p.rc;
     const int ne = rc * (rc + 1) / 2;
     for (int e0 = 0; e0 < ne; e0 += 256) {
@@ -756,12 +844,20 @@ __device__ __forceinline__ void extend_child(const MfArgs& a, const ChildPre& p,
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int e = min(e0 + 64 * u + lane, ne - 1);   // clamped (see assemble_wave)
-            v[u] = e0 == 0 ? p.v[u] : ldc<COH>(p.Uc + e);
+            bool ok = true;   // (tagged: child_sweep has seen every tag current)
+            v[u] = e0 == 0 ? p.v[u] : p.G ? untag_pair(p.G + 2 * (int64_t)e, epoch, ok) : ldc<COH>(p.Uc + e);
             pos[u] = e0 == 0 ? p.pos[u] : p.ec[e];
         }
+        // the four front entries read at once (positions of one child are distinct; a lane past the
+        // child's entries reads a valid position and writes nothing), then added and written back: a
+        // read-modify-write per entry under its own branch waited for each read separately
+        double f[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) f[u] = F[pos[u]];
+        asm volatile("" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (e0 + 64 * u + lane < ne) F[pos[u]] += v[u];
+            if (e0 + 64 * u + lane < ne) F[pos[u]] = f[u] + v[u];
     }
     if (lane < rc) wv[p.smap_v] += p.uval;
     wave_sync();
@@ -813,38 +909,57 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     assemble_wave(a, aq0, aq1, F, lane, fold);
     wave_sync();
     fstamp(stp, s, 2);
-    if constexpr (MODE == kModeFlow) {
-        for (int ci = a.child_ptr[s]; ci < ce; ++ci)
-            if (f->fid[a.child[ci]] == f->id) wait_done(*f, a.child[ci], a.info);
-    }
+    // children of this flow hand over tagged granules (child_sweep polls the data itself); children of
+    // earlier launches are final (kernel boundary): plain reads
+    uint32_t ep = 0;
+    if constexpr (MODE == kModeFlow) ep = f->epoch;
     fstamp(stp, s, 3);
+#ifdef BOS_MF_PIVOT_CYCLES
+    unsigned long long* const cst = stp ? g_pivot_bwd : nullptr;
+    cstamp(cst, s, 1);
+#endif
     // extend-add, children in list order (deterministic)
-    if (cb < ce) child_vals<COH>(lane, p0);
-    if (cb + 1 < ce) child_vals<COH>(lane, p1);
-    if (cb < ce) extend_child<COH>(a, p0, F, wv, m, lane);
-    if (cb + 1 < ce) extend_child<COH>(a, p1, F, wv, m, lane);
+    if (cb < ce) {
+        if (MODE == kModeFlow && p0.G) child_sweep(p0, ep, lane, a.info);
+        else child_vals<COH>(lane, p0);
+    }
+    if (cb + 1 < ce) {
+        if (MODE == kModeFlow && p1.G) child_sweep(p1, ep, lane, a.info);
+        else child_vals<COH>(lane, p1);
+    }
+#ifdef BOS_MF_PIVOT_CYCLES
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the children's values have arrived
+    cstamp(cst, s, 2);
+#endif
+    if (cb < ce) extend_child<COH>(a, p0, F, wv, m, lane, ep);
+    if (cb + 1 < ce) extend_child<COH>(a, p1, F, wv, m, lane, ep);
     for (int ci = cb + 2; ci < ce; ++ci) {
         ChildPre pq;
         child_meta(a, a.child[ci], lane, pq);
-        child_vals<COH>(lane, pq);
-        extend_child<COH>(a, pq, F, wv, m, lane);
+        if (MODE == kModeFlow && pq.G) child_sweep(pq, ep, lane, a.info);
+        else child_vals<COH>(lane, pq);
+        extend_child<COH>(a, pq, F, wv, m, lane, ep);
     }
-    const bool live = lane < m;
-#ifdef BOS_MF_BLOCKED
-    // Blocked: the pivot loop factors the k panel columns only (rows >= k become L21 as they go);
-    // the trailing r x r block stays in F and receives -L21 L21^T from f64 MFMA after the loop.
-    const int ncol = k;
-    double* const L21s = F;   // L21 column-major, row stride RS (odd), over F's panel columns (read by now)
-    const int RS = r | 1;
-#else
-    const int ncol = m;
+#ifdef BOS_MF_PIVOT_CYCLES
+    cstamp(cst, s, 3);
 #endif
+    const bool live = lane < m;
+    const int lrow = min(lane, m - 1);
     double row[MAXM];
 #pragma unroll
-    for (int c0 = 0; c0 < MAXM; c0 += 8) {   // whole groups of 8 past ncol skipped by a scalar branch
-        if (c0 < ncol) {
+    for (int c0 = 0; c0 < MAXM; c0 += 8) {   // whole groups of 8 past m skipped by a scalar branch
+        if (c0 < m) {
+            // branch-free: every lane reads an in-range entry (for a row i < m, pk32(i, c, m) < np for
+            // every c < m + 8), the group's eight reads under one wait, then selects. A predicated read
+            // per entry compiled to an exec-mask branch with its own wait each (~2 500 cycles for the
+            // rows of a 24-row front); the empty asm keeps the reads out of such branches.
+            double v[8];
 #pragma unroll
-            for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = (live && c <= lane) ? F[pk32(lane, c, m)] : 0.0;
+            for (int c = c0; c < c0 + 8; ++c) v[c - c0] = c < MAXM ? F[pk32(lrow, c, m)] : 0.0;
+            asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                         "+v"(v[7]));
+#pragma unroll
+            for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = (live && c <= lane) ? v[c - c0] : 0.0;
         } else {
 #pragma unroll
             for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = 0.0;
@@ -863,7 +978,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     double* Lj = Ls + lane;
     int j = 0;
 #ifdef BOS_MF_PIVOT_CYCLES
-    unsigned long long* const cst = stp ? g_pivot_bwd : nullptr;
     cstamp(cst, s, 0);
 #endif
     // Two pivots per step: column j + 1 is brought up to date in registers (L(j+1, j) by readlane),
@@ -889,8 +1003,8 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             double2* cp = reinterpret_cast<double2*>(colbuf);   // (L[l, j], L[l, j+1]), l = j + 2 + t
             if (lane > j + 1 && lane < m) cp[lane - j - 2] = make_double2(l0, l1);
             if (live) {
-                if (lane >= j) Lj[0] = l0;
-                if (lane >= j + 1) Lj[m] = l1;
+                if (lane >= j) ST_L(Lj, 0, l0);
+                if (lane >= j + 1) ST_L(Lj, m, l1);
             }
             Lj += 2 * m;
             const double y0 = readlane_d(wi, j) * inv0;          // forward steps j, j + 1
@@ -899,14 +1013,8 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             const double y1 = readlane_d(wi, j + 1) * inv1;
             if (lane == j + 1) wi = y1;
             else if (lane > j + 1) wi -= l1 * y1;
-#ifdef BOS_MF_BLOCKED
-            if (lane >= k && live) {
-                L21s[j * RS + (lane - k)] = l0;
-                L21s[(j + 1) * RS + (lane - k)] = l1;
-            }
-#endif
             wave_sync();
-            const int nt = ncol - j - 2;                         // live columns after this step
+            const int nt = m - j - 2;                            // live columns after this step
 #pragma unroll
             for (int t0 = 0; t0 < MAXM - 2; t0 += 8) {
                 if (t0 < nt) {
@@ -922,7 +1030,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             }
             __builtin_amdgcn_wave_barrier();   // the next step's pair stores stay after these reads
 #ifdef BOS_MF_PIVOT_CYCLES
-            if (j / 2 < 6) cstamp(cst, s, 1 + j / 2);
+            if (j / 2 < 3) cstamp(cst, s, 4 + j / 2);
 #endif
         }
     }
@@ -944,17 +1052,15 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         d = bad ? 1e-300 : d;
         const double inv = rsqrt_nr(d), ljj = d * inv;
         const double lij = lane == j ? ljj : row[0] * inv;   // L[i, j]
-        if (live && lane >= j) *Lj = lij;
+        if (live && lane >= j) ST_L(Lj, 0, lij);
         Lj += m;
         // forward step: y_j = w_j / L_jj, w_i -= L_ij y_j
         const double yj = readlane_d(wi, j) * inv;
         if (lane == j) wi = yj;
         else if (lane > j) wi -= lij * yj;
         const double g = lij * inv;                          // L[i, j] / L[j, j]
-        const int nt = ncol - j - 1;                         // live columns after this step (uniform)
-#ifdef BOS_MF_BLOCKED
-        if (lane >= k && live) L21s[j * RS + (lane - k)] = lij;
-#endif
+        const int nt = m - j - 1;                            // live columns after this step (uniform)
+
 #pragma unroll
         for (int u = 0; u < 8; ++u)
             if (u < MAXM - 1) row[u] = fma(-g, c0v[u], row[u + 1]);   // -= L[i,j] L[l,j], l = j + 1 + t
@@ -973,76 +1079,32 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     cstamp(cst, s, 7);
 #endif
     if (nbad && lane == 0) atomicAdd(a.info, nbad);
-#ifdef BOS_MF_BLOCKED
-    // S = A22 - L21 L21^T on f64 MFMA (16 x 16 blocks, 4 panel columns per step; lane l feeds row
-    // 16 b + (l & 15), column 4 st + (l >> 4) of L21, as in the fold's W W^T), then in place into F
-    wave_sync();
-    if (r > 0) {
-        constexpr int NB = (MAXM + 15) / 16, NPB = NB * (NB + 1) / 2;
-        const int nbr = (r + 15) >> 4;
-        dbl4 acc[NPB];
-#pragma unroll
-        for (int q = 0; q < NPB; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
-        for (int st = 0; 4 * st < k; ++st) {
-            const int jc = 4 * st + (lane >> 4);
-            double av[NB];
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const int i = 16 * b + (lane & 15);
-                const double v = L21s[min(jc, k - 1) * RS + min(i, r - 1)];
-                av[b] = (b < nbr && i < r && jc < k) ? v : 0.0;
-            }
-            int q = 0;
-#pragma unroll
-            for (int bi = 0; bi < NB; ++bi)
-#pragma unroll
-                for (int bj = 0; bj <= bi; ++bj, ++q)
-                    if (bi < nbr) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], av[bj], acc[q], 0, 0, 0);
-        }
-        int q = 0;
-#pragma unroll
-        for (int bi = 0; bi < NB; ++bi)
-#pragma unroll
-            for (int bj = 0; bj <= bi; ++bj, ++q) {
-                if (bi < nbr) {
-                    const int jj = 16 * bj + (lane & 15);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int ii = 16 * bi + (lane >> 4) + 4 * e;
-                        if (ii < r && jj <= ii) F[pk32(k + ii, k + jj, m)] -= acc[q][e];
-                    }
-                }
-            }
-        wave_sync();
-    }
     fstamp(stp, s, 5);
-    // the update matrix: the trailing block of F, row by row (lane k + i stores row i)
+    // the update matrix: row[t] holds column k + t; for a parent in this flow as tagged granules
+    // (update matrix, then u-vector), else plain (coherent) stores
+    unsigned long long* const G = (MODE == kModeFlow && a.ug_off[s] >= 0) ? a.Ug + a.ug_off[s] : nullptr;
+    if (G) {
 #pragma unroll
-    for (int t0 = 0; t0 < MAXM; t0 += 8) {
-        if (t0 < r) {
-            double uv[8];
+        for (int t0 = 0; t0 < MAXM; t0 += 8) {
+            if (t0 < r) {
 #pragma unroll
-            for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
-                uv[t - t0] = (live && lane >= k && t <= lane - k) ? F[pk32(lane, k + min(t, max(lane - k, 0)), m)] : 0.0;
+                for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
+                    if (live && lane >= k && t <= lane - k) tag_pair(G + 2 * pk(lane - k, t, r), row[t], ep);
+            }
+        }
+    } else {
 #pragma unroll
-            for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
-                if (live && lane >= k && t <= lane - k) stc<COH>(Us + pk(lane - k, t, r), uv[t - t0]);
+        for (int t0 = 0; t0 < MAXM; t0 += 8) {
+            if (t0 < r) {
+#pragma unroll
+                for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
+                    if (live && lane >= k && t <= lane - k) stc<COH>(Us + pk(lane - k, t, r), row[t]);
+            }
         }
     }
-#else
-    fstamp(stp, s, 5);
-    // the update matrix: row[t] holds column k + t
-#pragma unroll
-    for (int t0 = 0; t0 < MAXM; t0 += 8) {
-        if (t0 < r) {
-#pragma unroll
-            for (int t = t0; t < t0 + 8 && t < MAXM; ++t)
-                if (live && lane >= k && t <= lane - k) stc<COH>(Us + pk(lane - k, t, r), row[t]);
-        }
-    }
-#endif
     if (live) {
         if (lane < k) a.x[c0 + lane] = wi;
+        else if (G) tag_pair(G + 2 * ((int64_t)r * (r + 1) / 2 + (lane - k)), wi, ep);
         else stc<COH>(us + (lane - k), wi);
     }
     wave_sync();
@@ -1084,7 +1146,7 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         const double y0v = a.x[c0 + min(lane, k - 1)], xr0v = a.x[xi0];
         const double y0 = lane < k ? y0v : 0.0;
         const double xr0 = lane < r ? xr0v : 0.0;
-        stage_lds<16>(Lw, a.L + a.L_off[s], m * k, lane);
+        stage_lds<16, true>(Lw, a.L + a.L_off[s], m * k, lane);
         if (lane < k) w[lane] = y0;
         for (int j = 64 + lane; j < k; j += 64) w[j] = a.x[c0 + j];
         fstamp(stp, s, 1);
@@ -1092,13 +1154,33 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         if (lane < r) xs[lane] = xr0;
         for (int i = 64 + lane; i < r; i += 64) xs[i] = a.x[fi[k + i]];
     } else {
-        stage_lds(Lw, a.L + a.L_off[s], m * k, lane);
+        stage_lds<8, true>(Lw, a.L + a.L_off[s], m * k, lane);
         for (int j = lane; j < k; j += 64) w[j] = a.x[c0 + j];
         fstamp(stp, s, 1);
-        if (parent[s] >= 0 && f->fid[parent[s]] == f->id) wait_done(*f, parent[s], a.info);
+        if (parent[s] >= 0 && f->fid[parent[s]] == f->id) {
+            // the rows are dofs of ancestors, whose x every backward front publishes as tagged
+            // granules (xg): poll them until every tag is this step's epoch (no completion flag)
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t it = 0;; ++it) {
+                bool ok = true;
+                const double v0 = untag_pair(a.xg + 2 * (int64_t)xi0, f->epoch, ok);
+                if (lane < r) xs[lane] = v0;
+                for (int i = 64 + lane; i < r; i += 64) xs[i] = untag_pair(a.xg + 2 * (int64_t)fi[k + i], f->epoch, ok);
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+                if ((it & 15) == 15) {
+                    const bool stalled = (__hip_atomic_load(a.info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStall) != 0;
+                    if (stalled || __builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) {
+                        if (lane == 0) atomicOr(a.info, kStall);
+                        break;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        } else {   // the parent finished in an earlier launch (or none): final x
+            if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
+            for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
+        }
         fstamp(stp, s, 2);
-        if (lane < r) xs[lane] = ldc<COH>(a.x + xi0);
-        for (int i = 64 + lane; i < r; i += 64) xs[i] = ldc<COH>(a.x + fi[k + i]);
     }
     wave_sync();
     if (k <= 64) {
@@ -1133,6 +1215,7 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
             }
         }
         if (own) stc<COH>(a.x + c0 + lane, xv);
+        if (a.xtag[s] && own) tag_pair(a.xg + 2 * (int64_t)(c0 + lane), xv, *a.epoch);
         wave_sync();
         fstamp(stp, s, 3);
         return;
@@ -1154,6 +1237,10 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         wave_sync();
     }
     for (int j = lane; j < k; j += 64) stc<COH>(a.x + c0 + j, w[j]);
+    if (a.xtag[s]) {
+        const uint32_t ep = *a.epoch;
+        for (int j = lane; j < k; j += 64) tag_pair(a.xg + 2 * (int64_t)(c0 + j), w[j], ep);
+    }
     wave_sync();
 }
 
@@ -1183,7 +1270,7 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const bool head = valid && q0 == 0;
     // the landmark's own values, read by all its lanes (one address: no extra traffic) so no branch
     // holds a wait; only the head lane uses them
-    const double y0v = a.x[c0], y1v = a.x[c0 + 1], L00v = Ls[0], L10v = Ls[1], L11v = Ls[m + 1];
+    const double y0v = a.x[c0], y1v = a.x[c0 + 1], L00v = LD_L(Ls, 0), L10v = LD_L(Ls, 1), L11v = LD_L(Ls, m + 1);
     const double y0 = head ? y0v : 0.0, y1 = head ? y1v : 0.0;
     const double L00 = head ? L00v : 1.0, L10 = head ? L10v : 0.0, L11 = head ? L11v : 1.0;
     double t0 = 0.0, t1 = 0.0;
@@ -1195,8 +1282,8 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
         for (int u = 0; u < 4; ++u) {
             const int qq = min(q + u * kFoldLanes, rl);
             idx[u] = fi[qq];
-            la[u] = Ls[2 + qq];
-            lb[u] = Ls[m + 2 + qq];
+            la[u] = LD_L(Ls, 2 + qq);
+            lb[u] = LD_L(Ls, m + 2 + qq);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) xv[u] = a.x[idx[u]];
@@ -1241,8 +1328,8 @@ __device__ __forceinline__ void factor_flow_body(const MfArgs& a, const Flow& f)
         if (t >= f.n) break;
         const int s = f.order[t];
         factor_front_reg<kFlowMaxM, kModeFlow, F32>(a, s, F, colbuf, wv, &fb, lane, &f);   // m <= kFlowMaxM
+        // (no completion flag: a parent in this flow polls the tagged granules themselves)
         fstamp(f.stamps, s, 6);
-        publish_done(f, s);
         fstamp(f.stamps, s, 7);
     }
     leave_flow(f);
@@ -1264,7 +1351,7 @@ __global__ __launch_bounds__(64) void mf_backward_flow(const MfArgs a, const Flo
         if (t >= f.n) break;
         const int s = f.order[t];
         backward_front<kModeFlow>(a, s, w, threadIdx.x, &f, parent);
-        publish_done(f, s);
+        // (no completion flag: the children poll the tagged x granules themselves)
         fstamp(f.stamps, s, 4);
     }
     leave_flow(f);
@@ -1371,6 +1458,11 @@ struct MfDevice {
     double *L = nullptr, *U = nullptr, *u = nullptr, *scratch = nullptr;
     const float* A32 = nullptr;   // mf_set_fold_source
     int64_t pl_lo = 0;
+    // tagged hand-offs (MfArgs): update-matrix granules of flow fronts whose parent is in the same
+    // flow, their offsets, x granules per dof and the fronts whose x a backward flow reads
+    unsigned long long *Ug = nullptr, *xg = nullptr;
+    int64_t* ug_off = nullptr;
+    int8_t* xtag = nullptr;
 
     MfArgs args(const Prog& P, int lev, int c, const double* A, double* x) const {
         MfArgs g;
@@ -1382,6 +1474,7 @@ struct MfDevice {
         g.findex = findex; g.A = A; g.A32 = A32; g.pl_lo = pl_lo; g.L = L; g.U = U; g.u = u; g.scratch = scratch; g.x = x; g.info = info;
         g.fold_cnt = fold_cnt; g.fold_cptr = fold_cptr; g.fold_chunk = fold_chunk; g.fold_rec = fold_rec;
         g.emap = emap; g.emap_off = emap_off;
+        g.Ug = Ug; g.ug_off = ug_off; g.xg = xg; g.xtag = xtag; g.epoch = epoch;
         g.stamps_f = stamps;
         g.stamps_b = stamps ? stamps + 8 * (int64_t)nsuper : nullptr;
         return g;
@@ -1527,6 +1620,34 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         return rc;
     if ((rc = up(&d->fid_f, fid_f, err)) || (rc = up(&d->fid_b, fid_b, err)) || (rc = up(&d->parent, F.parent, err)))
         return rc;
+    {   // tagged hand-offs: a flow front whose parent is in the same flow publishes its update matrix
+        // and u-vector as granule pairs; every ancestor of a backward-flow front publishes its x so
+        std::vector<int64_t> ugo(F.nsuper, -1);
+        int64_t ug_size = 0, ndof = 0;
+        for (int c = 0; c < F.nsuper; ++c) {
+            ndof = std::max<int64_t>(ndof, (int64_t)F.col0[c] + F.k[c]);
+            const int p = F.parent[c];
+            if (p < 0 || fid_f[c] == 0 || fid_f[p] != fid_f[c]) continue;
+            const int64_t rc2 = F.r[c];
+            ugo[c] = ug_size;
+            ug_size += 2 * (rc2 * (rc2 + 1) / 2 + rc2);
+        }
+        std::vector<int8_t> xt(F.nsuper, 0);
+        for (int c = 0; c < F.nsuper; ++c)
+            if (fid_b[c] != 0)
+                for (int q = c; q >= 0 && !xt[q]; q = F.parent[q]) xt[q] = 1;
+        if ((rc = up(&d->ug_off, ugo, err)) || (rc = up(&d->xtag, xt, err))) return rc;
+        auto alloc0 = [&](unsigned long long** p, int64_t n) -> int {
+            n = std::max<int64_t>(n, 1) + 2 * kMfPad;
+            if (hipMalloc((void**)p, n * sizeof(unsigned long long)) != hipSuccess ||
+                hipMemset(*p, 0, n * sizeof(unsigned long long)) != hipSuccess) {
+                err = "hipMalloc failed (multifrontal granules)";
+                return -2;
+            }
+            return 0;
+        };
+        if ((rc = alloc0(&d->Ug, ug_size)) || (rc = alloc0(&d->xg, 2 * ndof))) return rc;
+    }
     if (hipMalloc((void**)&d->done, 2 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(d->done, 0, 2 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void**)&d->tickets, 2 * kMfTickets * sizeof(int)) != hipSuccess ||
@@ -1602,7 +1723,7 @@ void mf_destroy(MfDevice* d) {
     void* bufs[] = {d->emap, d->emap_off, d->epoch, d->fid_f, d->fid_b, d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->parent, d->done,
                     d->tickets, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
-                    d->findex_off, d->L, d->U, d->u, d->scratch};
+                    d->findex_off, d->L, d->U, d->u, d->scratch, d->Ug, d->xg, d->ug_off, d->xtag};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);

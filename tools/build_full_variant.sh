@@ -4,7 +4,7 @@
 set -e
 cd "$(dirname "$0")/../prb-project-bearing-only-slam_amd"
 name=$1; flags=$2
-HIPFLAGS="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wall -Wno-unused-parameter -Wno-unused-result -mllvm -pragma-unroll-threshold=1000000 -mllvm -amdgpu-mfma-vgpr-form=1"
+HIPFLAGS="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wall -Wno-unused-parameter -Wno-unused-result -mllvm -pragma-unroll-threshold=1000000 -mllvm -amdgpu-mfma-vgpr-form=1 -fno-slp-vectorize"
 CXXFLAGS="-O2 -pthread -fPIC -std=c++17 -Wno-unused-parameter -I/opt/rocm/include"
 LD="-pthread -L/opt/rocm/lib -lrocsolver -lrocblas -lrccl -Wl,--no-as-needed -lrocsparse -Wl,--as-needed -lamdhip64 -Wl,-rpath,/opt/rocm/lib"
 D=/tmp/fv_$name

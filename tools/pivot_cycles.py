@@ -1,9 +1,10 @@
-"""Core-clock cycles of the multifrontal pivot loop per tree level (diagnostics; a library built
+"""Core-clock cycles of the multifrontal front phases per tree level (diagnostics; a library built
 with -DBOS_MF_PIVOT_CYCLES, tools/build_full_variant.sh): one config-3 GN step with
-bos_debug_solver_stamps, whose backward half then holds s_memtime stamps of every front's pivot loop
-([0] start, [1..6] after two-pivot step i, [7] end). Prints per level the median k, cycles of the
-whole loop, cycles per two-pivot step (first step and the rest), and the core clock measured
-against the factor stamps' realtime clock (loop start .. end).
+bos_debug_solver_stamps, whose backward half then holds s_memtime stamps of every front: [1]
+children ready, [2] their update matrices loaded (coherent loads), [3] extend-added, [0] pivot loop
+start (rows in registers), [4..6] after two-pivot steps 1-3, [7] pivot loop end. Prints per level the
+median k and m, cycles of: child value loads, LDS extend-add, row loads, the whole pivot loop, one
+two-pivot step; and the core clock (GHz) from the factor stamps' realtime clock over the pivot loop.
 Usage: python tools/pivot_cycles.py gpurun_exp/libbos_pivcyc.so"""
 import os
 import sys
@@ -27,20 +28,26 @@ C = st[1].astype(np.int64)   # core cycles
 lev = meta[:, 0]
 ok = (C[:, 0] > 0) & (C[:, 7] > 0) & (F[:, 4] > 0) & (F[:, 5] > 0)
 print(f"fronts with cycle stamps: {ok.sum()} of {nsuper}")
-print(f"{'lvl':>3} {'fronts':>6} {'k':>4} {'m':>4} {'loop cyc':>9} {'step1':>7} {'step2+':>7} {'cyc/pivot':>9} "
-      f"{'loop us':>8} {'GHz':>6}")
+print(f"{'lvl':>3} {'fronts':>6} {'k':>4} {'m':>4} {'Uload':>7} {'extend':>7} {'rows':>6} {'loop':>7} {'step':>6} "
+      f"{'cyc/piv':>7} {'loop us':>8} {'GHz':>5}")
+
+
+def med(x):
+    x = x[np.isfinite(x)]
+    return float(np.median(x)) if len(x) else float("nan")
+
+
 for l in sorted(set(lev[ok])):
     sel = ok & (lev == l)
-    k = meta[sel, 1]
-    m = meta[sel, 1] + meta[sel, 2]
-    loop = C[sel, 7] - C[sel, 0]
-    s1 = C[sel, 1] - C[sel, 0]
-    steps = []
-    for i in range(1, 6):
-        good = C[sel, i + 1] > 0
-        steps.extend((C[sel, i + 1] - C[sel, i])[good & (k >= 2 * (i + 1))])
+    k = meta[sel, 1].astype(float)
+    m = k + meta[sel, 2]
+    c = C[sel].astype(float)
+    c[c == 0] = np.nan
+    uload, ext, rows = c[:, 2] - c[:, 1], c[:, 3] - c[:, 2], c[:, 0] - c[:, 3]
+    loop = c[:, 7] - c[:, 0]
+    step = np.concatenate([c[:, 4] - c[:, 0], c[:, 5] - c[:, 4], c[:, 6] - c[:, 5]])
     us = (F[sel, 5] - F[sel, 4]) / 100.0
-    ghz = np.median(loop / np.maximum(us * 1e3, 1e-9))
-    print(f"{l:3d} {sel.sum():6d} {np.median(k):4.0f} {np.median(m):4.0f} {np.median(loop):9.0f} {np.median(s1):7.0f} "
-          f"{np.median(steps) if steps else float('nan'):7.0f} {np.median(loop / np.maximum(k, 1)):9.0f} "
-          f"{np.median(us):8.2f} {ghz:6.2f}")
+    ghz = med(loop / np.maximum(us * 1e3, 1e-9))
+    print(f"{l:3d} {sel.sum():6d} {np.median(k):4.0f} {np.median(m):4.0f} {med(uload):7.0f} {med(ext):7.0f} "
+          f"{med(rows):6.0f} {med(loop):7.0f} {med(step):6.0f} {med(loop / np.maximum(k, 1)):7.0f} "
+          f"{np.median(us):8.2f} {ghz:5.2f}")
