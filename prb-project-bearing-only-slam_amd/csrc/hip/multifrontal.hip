@@ -352,6 +352,13 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
     return y;
 }
 
+// 1 / d for d > 0 in the normal range: hardware estimate refined by two Newton steps
+__device__ __forceinline__ double rcp_nr(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    y = fma(fma(-d, y, 1.0), y, y);
+    return fma(fma(-d, y, 1.0), y, y);
+}
+
 // phase stamp k of front s (lane 0; the product launches pass no stamp buffer)
 __device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
 #ifdef BOS_MF_PIVOT_CYCLES
@@ -803,9 +810,28 @@ __device__ __forceinline__ void child_vals(int lane, ChildPre& p) {
 // carries this step's epoch (the data is the flag: no completion flag, no second load round trip),
 // keeping the u-vector entry and the first 256 entries. Bounded like wait_done: a stall marks info
 // and returns (the launch then drains, the step fails).
+// Waiting is done by ONE lane probing ONE granule (the child's last u-vector entry, its last store),
+// the full sweep follows once it matches: a wave sweeping all its granules on every poll multiplied
+// the polling traffic by ~600 loads per poll.
+__device__ __forceinline__ bool probe_granule(const unsigned long long* g, uint32_t epoch, uint64_t t0, int32_t* info) {
+    if (threadIdx.x % 64 == 0) {
+        for (uint32_t it = 0;; ++it) {
+            if ((uint32_t)(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == epoch) break;
+            if ((it & 15) == 15) {
+                const bool stalled = (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kMfStall) != 0;
+                if (stalled || __builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) break;   // 50 ms, as wait_done
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
 __device__ __forceinline__ void child_sweep(ChildPre& p, uint32_t epoch, int lane, int32_t* info) {
     const int rc = p.rc, ne = rc * (rc + 1) / 2;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    probe_granule(p.G + 2 * (int64_t)(ne + max(rc - 1, 0)) + 1, epoch, t0, info);
     for (uint32_t it = 0;; ++it) {
         bool ok = true;
         const double uv = untag_pair(p.G + 2 * (int64_t)(ne + min(lane, max(rc - 1, 0))), epoch, ok);
@@ -877,7 +903,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     const int c0 = a.col0[s];
     const int aq0 = a.amap_ptr[s], aq1 = a.amap_ptr[s + 1];   // the assembly's range, loaded up front
     const int np = m * (m + 1) / 2;
-    const double xo = lane < k ? a.x[c0 + lane] : 0.0;   // right-hand side of the own dofs (k < 64)
+    double xo = a.x[c0 + min(lane, k - 1)];   // right-hand side of the own dofs (k < 64; unconditional read)
     // output offsets up front: their loads complete during the assembly instead of before the pivots
     double* Ls = a.L + a.L_off[s];
     double* Us = a.U + a.U_off[s];
@@ -908,6 +934,10 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     fstamp(stp, s, 1);
     assemble_wave(a, aq0, aq1, F, lane, fold);
     wave_sync();
+    // the own right-hand side has arrived by now (the assembly waited for its loads): pin it here,
+    // so that the compiler does not leave its wait (one memory latency) in front of the pivots
+    asm volatile("" : "+v"(xo));
+    xo = lane < k ? xo : 0.0;
     fstamp(stp, s, 2);
     // children of this flow hand over tagged granules (child_sweep polls the data itself); children of
     // earlier launches are final (kernel boundary): plain reads
@@ -986,6 +1016,56 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     {
 #pragma nounroll
         for (; j + 1 < kf; j += 2) {
+#ifdef BOS_MF_UNSCALED
+            // Unscaled columns (experiment): the trailing update needs L(i,j) L(l,j) = g0_i c0_l with
+            // g0 = c0 / d0, so the columns broadcast unscaled — column j at once, before any pivot
+            // arithmetic — and the chain is rcp, not rsqrt (the L panel's 1/sqrt scaling runs beside it)
+            const double c0 = row[0], c1 = row[1];
+            double* const cq = colbuf;            // column j (unscaled), rows l = j + 2 + t
+            double* const cr = colbuf + MAXM;     // column j + 1 after pivot j, same rows
+            if (lane > j + 1 && lane < m) cq[lane - j - 2] = c0;
+            double d0 = readlane_d(c0, j);
+            const double a10 = readlane_d(c0, j + 1);            // A(j+1, j)
+            const bool bad0 = !(d0 > 0.0);
+            nbad += bad0;
+            d0 = bad0 ? 1e-300 : d0;
+            const double r0 = rcp_nr(d0);
+            const double g0 = c0 * r0;                           // L[i, j] / L[j, j]
+            const double f1 = fma(-g0, a10, c1);                 // column j+1 after pivot j
+            if (lane > j + 1 && lane < m) cr[lane - j - 2] = f1;
+            double d1 = readlane_d(f1, j + 1);
+            const bool bad1 = !(d1 > 0.0);
+            nbad += bad1;
+            d1 = bad1 ? 1e-300 : d1;
+            const double r1 = rcp_nr(d1);
+            const double g1 = f1 * r1;
+            const double inv0 = rsqrt_nr(d0), inv1 = rsqrt_nr(d1);   // the panel's scaling (off the chain)
+            const double l0 = lane == j ? d0 * inv0 : c0 * inv0;     // L[i, j]
+            const double l1 = lane == j + 1 ? d1 * inv1 : f1 * inv1; // L[i, j+1]
+            if (live) {
+                if (lane >= j) ST_L(Lj, 0, l0);
+                if (lane >= j + 1) ST_L(Lj, m, l1);
+            }
+            Lj += 2 * m;
+            const double w0 = readlane_d(wi, j);                 // forward steps j, j + 1
+            if (lane == j) wi = w0 * inv0;
+            else if (lane > j) wi = fma(-g0, w0, wi);
+            const double w1 = readlane_d(wi, j + 1);
+            if (lane == j + 1) wi = w1 * inv1;
+            else if (lane > j + 1) wi = fma(-g1, w1, wi);
+            wave_sync();
+            const int nt = m - j - 2;                            // live columns after this step
+#pragma unroll
+            for (int t0 = 0; t0 < MAXM - 2; t0 += 8) {
+                if (t0 < nt) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int t = t0 + u;
+                        if (t < MAXM - 2) row[t] = fma(-g1, cr[t], fma(-g0, cq[t], row[t + 2]));
+                    }
+                }
+            }
+#else
             double d0 = readlane_d(row[0], j);
             const bool bad0 = !(d0 > 0.0);
             nbad += bad0;
@@ -1028,6 +1108,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
                     }
                 }
             }
+#endif
             __builtin_amdgcn_wave_barrier();   // the next step's pair stores stay after these reads
 #ifdef BOS_MF_PIVOT_CYCLES
             if (j / 2 < 3) cstamp(cst, s, 4 + j / 2);
@@ -1159,8 +1240,10 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         fstamp(stp, s, 1);
         if (parent[s] >= 0 && f->fid[parent[s]] == f->id) {
             // the rows are dofs of ancestors, whose x every backward front publishes as tagged
-            // granules (xg): poll them until every tag is this step's epoch (no completion flag)
+            // granules (xg): one lane probes the parent's first dof, then the rows are swept until
+            // every tag is this step's epoch (no completion flag)
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            probe_granule(a.xg + 2 * (int64_t)a.col0[parent[s]] + 1, f->epoch, t0, a.info);
             for (uint32_t it = 0;; ++it) {
                 bool ok = true;
                 const double v0 = untag_pair(a.xg + 2 * (int64_t)xi0, f->epoch, ok);
@@ -1431,8 +1514,14 @@ constexpr int kFlowWavesFactor = 6;
 // largest panel (m k doubles): class-64 fronts (up to ~16 KB) then hold a level-0 launch to 8-10
 // waves per CU; splitting the big panels into a launch of their own measured no faster.
 constexpr int kFlowWavesBackward = 4;
-constexpr int kSolveWideLevel = 256;
-constexpr int kFactorWideLevel = 2048;
+#ifndef BOS_MF_SOLVE_WIDE   // (A/B builds may override the two thresholds)
+#define BOS_MF_SOLVE_WIDE 256
+#endif
+#ifndef BOS_MF_FACTOR_WIDE
+#define BOS_MF_FACTOR_WIDE 2048
+#endif
+constexpr int kSolveWideLevel = BOS_MF_SOLVE_WIDE;
+constexpr int kFactorWideLevel = BOS_MF_FACTOR_WIDE;
 struct MfDevice {
     int nlevels = 0, nsuper = 0, ncu = 256;
     // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside

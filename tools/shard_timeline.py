@@ -34,7 +34,7 @@ for W in worlds:
         S = [bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, rank=r, world_size=W,
                         lanes_per_pose=LPP) for r in range(W)]
     t_create = time.perf_counter() - t0
-    rows = []
+    rows, split = [], []
     for it in range(6):
         if W == 1:
             st = [S[0].step()]
@@ -53,7 +53,11 @@ for W in worlds:
             st = [h.step_phase(2) for h in S]
         if it >= 1:
             rows.append([[s["t_linearize_ms"], s["t_solve_ms"], s["t_update_ms"], s["t_exchange_ms"]] for s in st])
+            if W > 1:   # own subtrees (J+H end -> phase 0 done) and top + backward (exchange 1 in -> phase 1 done)
+                stp = [h.last_step_stamps().astype(np.int64) for h in S]
+                split.append([[(t[4] - t[1]) * 1e-5, (t[6] - t[5]) * 1e-5] for t in stp])
     a = np.median(np.array(rows), axis=0)   # [rank][phase]
+    sp = np.median(np.array(split), axis=0) if split else None   # [rank][own, top + backward]
     per_rank = a[:, :3].sum(axis=1)
     wall = {}
     if W == 1:   # host-clock rate of the one-rank RCCL path against the plain one-GPU step
@@ -83,11 +87,15 @@ for W in worlds:
               "exchange_ms": a[:, 3].tolist(),
               "max_rank_ms": float(per_rank.max()), "own_fronts": [i["own_fronts"] for i in info],
               "top_fronts": info[0]["top_fronts"], "pose_lane_groups": [i["pose_lane_groups"] for i in info],
-              "wall_ms_per_step": wall}
+              "wall_ms_per_step": wall,
+              "own_subtrees_ms": sp[:, 0].tolist() if sp is not None else None,
+              "top_and_backward_ms": sp[:, 1].tolist() if sp is not None else None}
     print(f"W={W}: per-rank compute (J+H + solve + update) max {per_rank.max():.3f} ms "
           f"(J+H {a[:, 0].max():.3f}, solve {a[:, 1].max():.3f}, update {a[:, 2].max():.3f}; between the phases "
           f"{a[:, 3].max():.3f}); top fronts "
-          f"{info[0]['top_fronts']}; create {t_create:.1f} s", flush=True)
+          f"{info[0]['top_fronts']}; create {t_create:.1f} s" +
+          (f"; slowest rank: own subtrees {sp[:, 0].max():.3f}, top + backward {sp[:, 1].max():.3f} ms"
+           if sp is not None else ""), flush=True)
     for h in S:
         h.close()
 print(json.dumps(out))
