@@ -352,13 +352,6 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
     return y;
 }
 
-// 1 / d for d > 0 in the normal range: hardware estimate refined by two Newton steps
-__device__ __forceinline__ double rcp_nr(double d) {
-    double y = __builtin_amdgcn_rcp(d);
-    y = fma(fma(-d, y, 1.0), y, y);
-    return fma(fma(-d, y, 1.0), y, y);
-}
-
 // phase stamp k of front s (lane 0; the product launches pass no stamp buffer)
 __device__ __forceinline__ void fstamp(unsigned long long* stp, int s, int k) {
 #ifdef BOS_MF_PIVOT_CYCLES
@@ -659,15 +652,15 @@ __device__ __forceinline__ void fold_store(const FoldAcc<MAXM>& acc, double* F, 
 }
 
 // ---- dataflow (work-queue) kernels: one launch walks a whole tree range. A wavefront takes the
-// next front from an atomic ticket (fronts listed in topological order), waits for the fronts it
-// depends on (children bottom-up, the parent top-down) through per-supernode completion flags,
-// processes the front and publishes its flag. Hand-off data goes through coherent (sc1) accesses
-// (ldc / stc), drained by s_waitcnt before the flag store: no L2 writeback / invalidate per front.
+// next front from an atomic ticket (fronts listed in topological order), prepares what does not
+// depend on other fronts (the fold and the assembly of H), waits for the fronts it depends on
+// (children bottom-up, the parent top-down) by polling their tagged hand-off data (tag_pair /
+// untag_pair: the data is the flag), processes the front and writes its own hand-off data tagged.
 // A wave only ever waits for tickets already taken by running waves, so any grid size is
-// deadlock-free. Every wait is bounded in time: a dependency that has not completed within
-// kWaitTicks marks the launch stalled (kStall in info), and from then on every wait of every wave
-// returns at once, so a stalled launch drains in about one timeout and is reported as an error
-// (bos_step returns BOS_ERR_SOLVER and the box-plus is skipped), never a hang.
+// deadlock-free. Every wait is bounded in time: a dependency that has not arrived within 50 ms marks
+// the launch stalled (kStall in info), and from then on every wait of every wave returns at once, so
+// a stalled launch drains in about one timeout and is reported as an error (bos_step returns
+// BOS_ERR_SOLVER and the box-plus is skipped), never a hang.
 // The ticket is reset by the launch itself: the last wave to leave zeroes it (and its exit
 // counter), so no host-side reset is needed between launches and no error path can leave a
 // partly consumed ticket behind (a launch that never started never took one).
@@ -676,7 +669,6 @@ struct Flow {
     int n;
     int* ticket;            // zero at launch; zeroed again by the launch's last wave
     int* exits;             // waves that have left the launch (same life cycle)
-    uint32_t* done;         // per supernode: epoch of its last completion
     const uint32_t* epoch_src;   // device word: this step's epoch (bumped once per GN step by the
                                  // step_mark kernel before the first flow launch, mf_epoch_ptr)
     uint32_t epoch;              // *epoch_src, read by the launch itself (graph-replayable)
@@ -702,57 +694,22 @@ __device__ __forceinline__ int next_ticket(int* ticket) {
 }
 
 // Memory ordering of the in-launch hand-off (the form cdna_hip_programming.md §6 Guideline 16 and
-// MI355X_MICROARCH.md § visibility, "Valid forms", allow without an agent-scope acquire; gfx950 has
-// 8 XCDs with private L2s and per-CU L1s that other CUs' stores never refresh):
-//  (1) every handed-off byte (update matrices U, u-vectors, backward x rows) is stored sc1
-//      (stc<true>: a relaxed agent-scope atomic store = global_store ... sc1, write-through: the line
-//      leaves the XCD's L2 for the memory-side coherence point and is dropped from it);
-//  (2) every storing wave drains them (s_waitcnt vmcnt(0), publish_done) before its flag store, and
-//      the wave that stores is the wave that signals (one wave per front);
-//  (3) the flag is an agent-scope atomic store (sc1) and is polled with agent-scope atomic loads;
-//  (4) every load of handed-off bytes is an sc1 vector load to registers (ldc<true>: a relaxed
-//      agent-scope atomic load = global_load ... sc1, which bypasses the CU's L1 and reads the
-//      coherence point, never a stale L1/L2 copy), issued after the poll has seen the flag; every
-//      other load in the flow launches reads bytes no workgroup of the same launch writes (static
-//      structure, H, and L / y of earlier launches, made visible by the kernel boundary).
-// Checked in the disassembly (hipcc -S of this file): the flow kernels' loads and stores of handed-off
-// data are global_load/store_dwordx2 sc1 and global_load/store_dword sc1 (flags), no flat_ access,
-// no scalar load of handed-off data. Under (1)-(4) the acquire reduces to a compiler barrier that
-// keeps the payload loads below the poll: fence(acquire, "wavefront") (no instruction). Data of an
-// ancestor further up (a backward front reads x rows of its parent's ancestors) is covered by the
-// chain: each ancestor drained its sc1 stores before its flag, which its child observed before
-// publishing its own. The formal agent-scope acquire (buffer_inv sc1 after the poll) measured
-// costlier and bit-identical: DESIGN.md §4.
-__device__ __forceinline__ void wait_done(const Flow& f, int c, int32_t* info) {
-    if (threadIdx.x == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f.done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != f.epoch) {
-            if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStall) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) {
-                atomicOr(info, kStall);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    wave_sync();
-}
-
+// MI355X_MICROARCH.md § visibility allow without an agent-scope acquire; gfx950 has 8 XCDs with
+// private L2s and per-CU L1s that other CUs' stores never refresh): every handed-off double (update
+// matrices and u-vectors of a child in the same flow, x of a backward front whose children wait for
+// it) is written as a tagged pair by relaxed agent-scope atomic stores (global_store ... sc1,
+// write-through to the memory-side coherence point) and read by relaxed agent-scope atomic loads
+// (global_load ... sc1, which bypass the CU's L1 and the XCD's L2 copy); a consumer accepts a value
+// only when both of its halves carry this step's epoch, so it can never take a stale or torn value,
+// and no drain, flag or fence is needed on either side. Data from earlier launches (kernel boundary)
+// is read with plain loads. Checked in the disassembly: the granule loads and stores are
+// global_load/store_dwordx2 sc1, no flat_ access, no scalar load of handed-off data.
 // Called by every wave once it has taken its last ticket.
 __device__ __forceinline__ void leave_flow(const Flow& f) {
     if (threadIdx.x == 0 && atomicAdd(f.exits, 1) == (int)gridDim.x - 1) {
         __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(f.exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-}
-
-__device__ __forceinline__ void publish_done(const Flow& f, int s) {
-    // drain this wave's sc1 stores before the flag (see wait_done: condition (2)); the fence only
-    // keeps the compiler from sinking stores below the wait
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // A child's extend-add inputs: its r, row map entry (lane < rc) and where its update matrix and
@@ -808,7 +765,7 @@ __device__ __forceinline__ void child_vals(int lane, ChildPre& p) {
 
 // A child of the same flow (p.G): poll its tagged update matrix and u-vector until every granule
 // carries this step's epoch (the data is the flag: no completion flag, no second load round trip),
-// keeping the u-vector entry and the first 256 entries. Bounded like wait_done: a stall marks info
+// keeping the u-vector entry and the first 256 entries. Bounded (kWaitTicks): a stall marks info
 // and returns (the launch then drains, the step fails).
 // Waiting is done by ONE lane probing ONE granule (the child's last u-vector entry, its last store),
 // the full sweep follows once it matches: a wave sweeping all its granules on every poll multiplied
@@ -819,7 +776,7 @@ __device__ __forceinline__ bool probe_granule(const unsigned long long* g, uint3
             if ((uint32_t)(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == epoch) break;
             if ((it & 15) == 15) {
                 const bool stalled = (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kMfStall) != 0;
-                if (stalled || __builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) break;   // 50 ms, as wait_done
+                if (stalled || __builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
@@ -848,7 +805,7 @@ __device__ __forceinline__ void child_sweep(ChildPre& p, uint32_t epoch, int lan
         if (__builtin_amdgcn_ballot_w64(!ok) == 0) return;
         if ((it & 15) == 15) {
             const bool stalled = (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kMfStall) != 0;
-            if (stalled || __builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {   // 50 ms, as wait_done
+            if (stalled || __builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) {
                 if (lane == 0) atomicOr(info, kMfStall);
                 return;
             }
@@ -1016,56 +973,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     {
 #pragma nounroll
         for (; j + 1 < kf; j += 2) {
-#ifdef BOS_MF_UNSCALED
-            // Unscaled columns (experiment): the trailing update needs L(i,j) L(l,j) = g0_i c0_l with
-            // g0 = c0 / d0, so the columns broadcast unscaled — column j at once, before any pivot
-            // arithmetic — and the chain is rcp, not rsqrt (the L panel's 1/sqrt scaling runs beside it)
-            const double c0 = row[0], c1 = row[1];
-            double* const cq = colbuf;            // column j (unscaled), rows l = j + 2 + t
-            double* const cr = colbuf + MAXM;     // column j + 1 after pivot j, same rows
-            if (lane > j + 1 && lane < m) cq[lane - j - 2] = c0;
-            double d0 = readlane_d(c0, j);
-            const double a10 = readlane_d(c0, j + 1);            // A(j+1, j)
-            const bool bad0 = !(d0 > 0.0);
-            nbad += bad0;
-            d0 = bad0 ? 1e-300 : d0;
-            const double r0 = rcp_nr(d0);
-            const double g0 = c0 * r0;                           // L[i, j] / L[j, j]
-            const double f1 = fma(-g0, a10, c1);                 // column j+1 after pivot j
-            if (lane > j + 1 && lane < m) cr[lane - j - 2] = f1;
-            double d1 = readlane_d(f1, j + 1);
-            const bool bad1 = !(d1 > 0.0);
-            nbad += bad1;
-            d1 = bad1 ? 1e-300 : d1;
-            const double r1 = rcp_nr(d1);
-            const double g1 = f1 * r1;
-            const double inv0 = rsqrt_nr(d0), inv1 = rsqrt_nr(d1);   // the panel's scaling (off the chain)
-            const double l0 = lane == j ? d0 * inv0 : c0 * inv0;     // L[i, j]
-            const double l1 = lane == j + 1 ? d1 * inv1 : f1 * inv1; // L[i, j+1]
-            if (live) {
-                if (lane >= j) ST_L(Lj, 0, l0);
-                if (lane >= j + 1) ST_L(Lj, m, l1);
-            }
-            Lj += 2 * m;
-            const double w0 = readlane_d(wi, j);                 // forward steps j, j + 1
-            if (lane == j) wi = w0 * inv0;
-            else if (lane > j) wi = fma(-g0, w0, wi);
-            const double w1 = readlane_d(wi, j + 1);
-            if (lane == j + 1) wi = w1 * inv1;
-            else if (lane > j + 1) wi = fma(-g1, w1, wi);
-            wave_sync();
-            const int nt = m - j - 2;                            // live columns after this step
-#pragma unroll
-            for (int t0 = 0; t0 < MAXM - 2; t0 += 8) {
-                if (t0 < nt) {
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int t = t0 + u;
-                        if (t < MAXM - 2) row[t] = fma(-g1, cr[t], fma(-g0, cq[t], row[t + 2]));
-                    }
-                }
-            }
-#else
             double d0 = readlane_d(row[0], j);
             const bool bad0 = !(d0 > 0.0);
             nbad += bad0;
@@ -1108,7 +1015,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
                     }
                 }
             }
-#endif
             __builtin_amdgcn_wave_barrier();   // the next step's pair stores stay after these reads
 #ifdef BOS_MF_PIVOT_CYCLES
             if (j / 2 < 3) cstamp(cst, s, 4 + j / 2);
@@ -1532,9 +1438,8 @@ struct MfDevice {
     Prog prog[2];                 // [0]: own (or every front), [1]: the replicated top (sharded only)
     int8_t *fid_f = nullptr, *fid_b = nullptr;   // flow membership: factor, backward
     int32_t* parent = nullptr;
-    uint32_t* done = nullptr;     // [2][nsuper]: factor, backward
     int* tickets = nullptr;       // [2 * kMfTickets]: work-queue tickets, then the launches' exit counters
-    uint32_t* epoch = nullptr;    // device word, 1 at creation (done[] starts at 0), bumped per GN step
+    uint32_t* epoch = nullptr;    // device word, 1 at creation (granule tags start at 0), bumped per GN step
     unsigned long long* stamps = nullptr;   // diagnostics: [2][nsuper][8] flow stamps (factor, backward), or null
     int32_t *fold_cnt = nullptr, *fold_cptr = nullptr, *fold_chunk = nullptr, *fold_rec = nullptr;
     int16_t* emap = nullptr;
@@ -1737,9 +1642,7 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         };
         if ((rc = alloc0(&d->Ug, ug_size)) || (rc = alloc0(&d->xg, 2 * ndof))) return rc;
     }
-    if (hipMalloc((void**)&d->done, 2 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(d->done, 0, 2 * (size_t)std::max(1, F.nsuper) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void**)&d->tickets, 2 * kMfTickets * sizeof(int)) != hipSuccess ||
+    if (hipMalloc((void**)&d->tickets, 2 * kMfTickets * sizeof(int)) != hipSuccess ||
         hipMemset(d->tickets, 0, 2 * kMfTickets * sizeof(int)) != hipSuccess ||
         hipMalloc((void**)&d->epoch, sizeof(uint32_t)) != hipSuccess) {
         err = "hipMalloc failed (multifrontal flow)";
@@ -1809,7 +1712,7 @@ void mf_destroy(MfDevice* d) {
     if (!d) return;
     free_prog(d->prog[0]);
     free_prog(d->prog[1]);
-    void* bufs[] = {d->emap, d->emap_off, d->epoch, d->fid_f, d->fid_b, d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->parent, d->done,
+    void* bufs[] = {d->emap, d->emap_off, d->epoch, d->fid_f, d->fid_b, d->fold_cnt, d->fold_cptr, d->fold_chunk, d->fold_rec, d->parent,
                     d->tickets, d->col0, d->k, d->r, d->child_ptr, d->child, d->rmap, d->amap_ptr, d->amap_src,
                     d->amap_dst, d->findex, d->info, d->L_off, d->U_off, d->u_off, d->scratch_off, d->rmap_off,
                     d->findex_off, d->L, d->U, d->u, d->scratch, d->Ug, d->xg, d->ug_off, d->xtag};
@@ -1859,7 +1762,7 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (P.n_flow_factor > 0) {
-        const Flow f{P.order_factor, P.n_flow_factor, d->tickets, d->tickets + kMfTickets, d->done, d->epoch, 0u,
+        const Flow f{P.order_factor, P.n_flow_factor, d->tickets, d->tickets + kMfTickets, d->epoch, 0u,
                      d->fid_f, P.id, d->stamps};
         const int grid = std::min(P.n_flow_factor, d->ncu * kFlowWavesFactor);
         hipLaunchKernelGGL((mf_factor_flow<F32>), dim3(grid), dim3(64), 0, s, d->args(P, 0, 0, A, x), f);
@@ -1884,7 +1787,7 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
     const Prog& P = d->prog[which];
     if (P.ptr.empty()) return hipSuccess;
     if (P.flow_solve) {
-        const Flow fb{P.order_bwd, P.n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1, d->done + d->nsuper,
+        const Flow fb{P.order_bwd, P.n_flow_solve, d->tickets + 1, d->tickets + kMfTickets + 1,
                       d->epoch, 0u, d->fid_b, P.id, d->stamps ? d->stamps + 8 * (int64_t)d->nsuper : nullptr};
         const int grid = std::min(P.n_flow_solve, d->ncu * kFlowWavesBackward);
         hipLaunchKernelGGL(mf_backward_flow, dim3(grid), dim3(64), P.lds_bwd_flow, s, d->args(P, 0, 0, nullptr, x), fb,
