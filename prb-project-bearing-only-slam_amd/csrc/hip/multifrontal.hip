@@ -43,17 +43,25 @@ constexpr int kLdsCapM = 90;   // larger fronts up to 90 x 90 doubles (64.8 KB) 
 __device__ __forceinline__ int64_t pk(int64_t i, int64_t j, int64_t m) { return j * m - j * (j - 1) / 2 + (i - j); }
 __device__ __forceinline__ int pk32(int i, int j, int m) { return j * m - j * (j - 1) / 2 + (i - j); }   // LDS fronts
 
-// L panel traffic (written by the factorization, read once by the backward substitution) as
-// non-temporal accesses: the solve's ~300 MB of L then streams past the caches instead of evicting
-// the next J+H build's inputs (in-step J+H 16.0-16.5 -> 14.2-14.5 us, solve -6 us).
-// -DBOS_MF_CACHED_L (A/B only) restores plain accesses.
+// L panel traffic (written by the factorization, read once by the backward substitution): the
+// stores are non-temporal, so the solve's ~300 MB of L stream past the caches instead of evicting the
+// next J+H build's inputs (in-step J+H 16.0-16.5 -> 13.2-14.5 us, solve -14 us). The
+// folded landmarks' backward launch reads its L columns with plain loads (non-temporal loads there:
+// solve +13 us, profiles/r05_fold_l_policy_ab.txt). -DBOS_MF_CACHED_L (A/B only) restores plain stores
+// and loads everywhere, -DBOS_MF_L_LD_PLAIN plain loads everywhere.
 #ifndef BOS_MF_CACHED_L
 #define ST_L(p, i, v) __builtin_nontemporal_store((v), (p) + (i))
+#ifndef BOS_MF_L_LD_PLAIN
 #define LD_L(p, i) __builtin_nontemporal_load((p) + (i))
+#else
+#define LD_L(p, i) ((p)[i])
+#endif
 #else
 #define ST_L(p, i, v) ((p)[i] = (v))
 #define LD_L(p, i) ((p)[i])
 #endif
+#define ST_LF(p, i, v) ST_L(p, i, v)
+#define LD_LF(p, i) ((p)[i])
 
 // Copy n doubles global -> LDS by one wavefront, 8 independent loads in flight per lane.
 template <int U = 8, bool NTL = false> __device__ __forceinline__ void stage_lds(double* dst, const double* src, int n, int lane) {
@@ -523,12 +531,12 @@ __device__ __forceinline__ void fold_chunk(const MfArgs& a, double* W, FoldBuf* 
         for (int g = 0; g < 3; ++g) {
             lt0[g] = v.h[2 * g] * i0;
             lt1[g] = (v.h[2 * g + 1] - lt0[g] * l10) * i1;
-            ST_L(Lc, 2 + t + g, lt0[g]);
-            ST_L(Lc, mc + 2 + t + g, lt1[g]);
+            ST_LF(Lc, 2 + t + g, lt0[g]);
+            ST_LF(Lc, mc + 2 + t + g, lt1[g]);
         }
-        ST_L(Lc, 0, l00);
-        ST_L(Lc, 1, l10);
-        ST_L(Lc, mc + 1, l11);
+        ST_LF(Lc, 0, l00);
+        ST_LF(Lc, 1, l10);
+        ST_LF(Lc, mc + 1, l11);
         a.x[col0] = y0;
         a.x[col0 + 1] = y1;
         nbad += head ? (int)bad0 + (int)bad1 : 0;
@@ -1005,6 +1013,20 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
 #pragma unroll
             for (int t0 = 0; t0 < MAXM - 2; t0 += 8) {
                 if (t0 < nt) {
+#ifndef BOS_MF_PAIRS_ONE_BY_ONE
+                    // the group's eight pairs read at once (one LDS latency per group; pairs past the
+                    // live columns are scratch), the empty asm keeps the compiler from interleaving a
+                    // wait per pair: two-pivot step 1 269 -> 1 037 cycles at m = 18, 1 818 -> 1 554 at
+                    // m = 42 (tools/pivot_probe2.hip, profiles/r05_pivot_step_anatomy.txt)
+                    double2 c[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) c[u] = t0 + u < MAXM - 2 ? cp[t0 + u] : make_double2(0.0, 0.0);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(c[u].x), "+v"(c[u].y));
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (t0 + u < MAXM - 2) row[t0 + u] = fma(-l1, c[u].y, fma(-l0, c[u].x, row[t0 + u + 2]));
+#else
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         const int t = t0 + u;
@@ -1013,6 +1035,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
                             row[t] = fma(-l1, c.y, fma(-l0, c.x, row[t + 2]));
                         }
                     }
+#endif
                 }
             }
             __builtin_amdgcn_wave_barrier();   // the next step's pair stores stay after these reads
@@ -1182,7 +1205,9 @@ __device__ __forceinline__ void backward_front(const MfArgs& a, int s, double* w
         // 1 / L_jj by every lane at once, off the sequential chain below
         const double yv = own ? w[lane] : 0.0, rjj = own ? 1.0 / Lw[lane + lane * m] : 1.0;
         double xv = 0.0;
-        if (MODE == kModeLevel && k <= kBwdRegK) {   // per-level launches only (the flow keeps its registers)
+        // per-level launches only: in the backward flow the register form measured slower (solve +6 us,
+        // profiles/r05_backward_flow_registers_ab.txt)
+        if (MODE == kModeLevel && k <= kBwdRegK) {
             // the lane's column of the k x k block in registers, read from LDS before the chain, so
             // each step of the sequential chain is arithmetic and a lane read only
             double lr[kBwdRegK];
@@ -1259,7 +1284,7 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const bool head = valid && q0 == 0;
     // the landmark's own values, read by all its lanes (one address: no extra traffic) so no branch
     // holds a wait; only the head lane uses them
-    const double y0v = a.x[c0], y1v = a.x[c0 + 1], L00v = LD_L(Ls, 0), L10v = LD_L(Ls, 1), L11v = LD_L(Ls, m + 1);
+    const double y0v = a.x[c0], y1v = a.x[c0 + 1], L00v = LD_LF(Ls, 0), L10v = LD_LF(Ls, 1), L11v = LD_LF(Ls, m + 1);
     const double y0 = head ? y0v : 0.0, y1 = head ? y1v : 0.0;
     const double L00 = head ? L00v : 1.0, L10 = head ? L10v : 0.0, L11 = head ? L11v : 1.0;
     double t0 = 0.0, t1 = 0.0;
@@ -1271,8 +1296,8 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
         for (int u = 0; u < 4; ++u) {
             const int qq = min(q + u * kFoldLanes, rl);
             idx[u] = fi[qq];
-            la[u] = LD_L(Ls, 2 + qq);
-            lb[u] = LD_L(Ls, m + 2 + qq);
+            la[u] = LD_LF(Ls, 2 + qq);
+            lb[u] = LD_LF(Ls, m + 2 + qq);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) xv[u] = a.x[idx[u]];
