@@ -944,17 +944,21 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
 #pragma unroll
     for (int c0 = 0; c0 < MAXM; c0 += 8) {   // whole groups of 8 past m skipped by a scalar branch
         if (c0 < m) {
-            // branch-free: every lane reads an in-range entry (for a row i < m, pk32(i, c, m) < np for
-            // every c < m + 8), the group's eight reads under one wait, then selects. A predicated read
-            // per entry compiled to an exec-mask branch with its own wait each (~2 500 cycles for the
-            // rows of a 24-row front); the empty asm keeps the reads out of such branches.
+            // branch-free: every lane reads a position of the LDS front (for a row i < m, pk32(i, c, m)
+            // < np for every c < m + 8), the group's eight reads under one wait. A predicated read per
+            // entry compiled to an exec-mask branch with its own wait each (~2 500 cycles for the rows
+            // of a 24-row front); the empty asm keeps the reads out of such branches. Entries above
+            // the diagonal, of rows >= m (copies of row m - 1) and of columns >= m are scratch that no
+            // stored or broadcast value ever reads, so they are taken as read: selecting zeros there
+            // held 48 loop-invariant lane masks that the compiler spilled to VGPR lanes and read back
+            // per column.
             double v[8];
 #pragma unroll
             for (int c = c0; c < c0 + 8; ++c) v[c - c0] = c < MAXM ? F[pk32(lrow, c, m)] : 0.0;
             asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
                          "+v"(v[7]));
 #pragma unroll
-            for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = (live && c <= lane) ? v[c - c0] : 0.0;
+            for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = v[c - c0];
         } else {
 #pragma unroll
             for (int c = c0; c < c0 + 8 && c < MAXM; ++c) row[c] = 0.0;
