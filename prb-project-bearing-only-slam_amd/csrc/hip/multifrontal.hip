@@ -1275,7 +1275,11 @@ __global__ __launch_bounds__(64) void mf_backward_wave(const MfArgs a) {
 // hops per landmark, 200k landmarks), so fewer lanes per landmark with more loads in flight each
 // beat one row per lane.
 // (one lane per landmark from a packed record measured slower: DESIGN.md §4)
-constexpr int kFoldLanes = 4;   // measured: 22 us at 4 lanes, 23 at 8, 34 at 16 (config 3)
+#ifndef BOS_MF_FOLD_LANES
+#define BOS_MF_FOLD_LANES 4
+#endif
+// measured: 22 us at 4 lanes, 23 at 8, 34 at 16 (config 3); round 5: 2 / 8 lanes +10 / +3 us of solve
+constexpr int kFoldLanes = BOS_MF_FOLD_LANES;
 __global__ __launch_bounds__(kMfBlock) void mf_backward_fold(const MfArgs a) {
     const int g = (blockIdx.x * kMfBlock + threadIdx.x) / kFoldLanes;
     const int q0 = threadIdx.x % kFoldLanes;
@@ -1444,11 +1448,17 @@ struct Prog {
 // fronts before the flow reaches them (config 3: levels 0-5, solve 659 -> 582 us), the
 // factorization of levels with >= kFactorWideLevel fronts before its flow starts (config 3: levels
 // 0-2, 564 -> 556 us; also level 3: 567).
-constexpr int kFlowWavesFactor = 6;
+#ifndef BOS_MF_FLOW_WAVES_F   // (A/B builds may override the flow geometry)
+#define BOS_MF_FLOW_WAVES_F 6
+#endif
+constexpr int kFlowWavesFactor = BOS_MF_FLOW_WAVES_F;
 // The per-level backward launch of a level's wave fronts gives every wave the LDS of the level's
 // largest panel (m k doubles): class-64 fronts (up to ~16 KB) then hold a level-0 launch to 8-10
 // waves per CU; splitting the big panels into a launch of their own measured no faster.
-constexpr int kFlowWavesBackward = 4;
+#ifndef BOS_MF_FLOW_WAVES_B
+#define BOS_MF_FLOW_WAVES_B 4
+#endif
+constexpr int kFlowWavesBackward = BOS_MF_FLOW_WAVES_B;
 #ifndef BOS_MF_SOLVE_WIDE   // (A/B builds may override the two thresholds)
 #define BOS_MF_SOLVE_WIDE 256
 #endif
