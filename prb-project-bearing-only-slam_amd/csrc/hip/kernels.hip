@@ -889,14 +889,16 @@ __global__ void index_copy_kernel(const double* src, const int32_t* si, double* 
 
 __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
                                      double chi_const, int32_t nrob_const, int32_t* local_info, StepStatus* out,
-                                     StepStatus* mirror) {
+                                     StepStatus* mirror, bool zero_info) {
     if (threadIdx.x != 0) return;
     double chi = 0.0, m = 0.0;
     long long nr = 0, piv = 0;
     int32_t abort_bits = 0;
     if (local_info) {   // an exchange-2 wait that timed out (its abort bit arrived after exchange 2's packing)
         abort_bits |= *local_info & kStepAbort;
-        *local_info &= ~kStepAbort;
+        // zero_info: the gathering exchange-2 push sent the whole word without zeroing it (its blocks
+        // read it concurrently), so it is zeroed here, after every block has read it
+        *local_info = zero_info ? 0 : (*local_info & ~kStepAbort);
     }
     for (int q = 0; q < world; ++q) {
         chi += recv1[q * c1];
@@ -956,6 +958,44 @@ __global__ __launch_bounds__(256) void p2p_push_kernel(const double* send, int64
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_store(reinterpret_cast<uint32_t*>(base + flag_off + 64 * (int64_t)rank), e, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// launch_p2p_push_gather: one block per receiving rank, the payload read from its sources
+__global__ __launch_bounds__(256) void p2p_push_gather_kernel(const P2PPush p) {
+    if (p.stamp && blockIdx.x == 0 && threadIdx.x == 0) *p.stamp = __builtin_amdgcn_s_memrealtime();
+    char* base = reinterpret_cast<char*>(p.peers[blockIdx.x]);
+    double* dst = reinterpret_cast<double*>(base + p.data_off) + (int64_t)p.rank * p.count;
+    if (p.which == 1) {   // exchange 1: header, then the pack segments
+        double c;
+        long long r;
+        header1_block(p.chi_part, p.nrob_part, p.n_parts, c, r);
+        if (threadIdx.x == 0) { dst[0] = c; dst[1] = (double)r; }
+        for (int g = 0; g < p.nseg; ++g) {
+            const ExSeg e = p.segs[g];
+            const double* src = (e.src_kind == 0 ? p.U : p.u) + e.src;
+            for (int64_t i = threadIdx.x; i < e.len; i += 256) dst[e.dst + i] = src[i];
+        }
+    } else {        // exchange 2: header [max |x|, solver word], then the boundary solution
+        double m = 0.0;
+        for (int i = threadIdx.x; i < p.n_abs; i += 256) m = nan_max(m, p.abs_part[i]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o));
+        __shared__ double sm[4];
+        if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            dst[0] = nan_max(nan_max(sm[0], sm[1]), nan_max(sm[2], sm[3]));
+            dst[1] = (double)*p.info;
+        }
+        for (int i = threadIdx.x; i < p.n_bnd; i += 256) dst[2 + i] = p.x[p.bnd[i]];
+    }
+    const uint32_t e = *p.epoch;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(base + p.flag_off + 64 * (int64_t)p.rank), e, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -1165,6 +1205,14 @@ hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes
     return hipGetLastError();
 }
 
+int launch_node_absmax(const double* x, const int32_t* nodes, int n_nodes, const int32_t* node_dof, int NP, double* part,
+                       hipStream_t s, hipError_t* err) {
+    const int nb = std::max(1, (n_nodes + 255) / 256);
+    hipLaunchKernelGGL(node_absmax_kernel, dim3(nb), dim3(256), 0, s, x, nodes, n_nodes, node_dof, NP, part);
+    *err = hipGetLastError();
+    return nb;
+}
+
 hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* dst, const int32_t* dst_idx, int64_t n,
                              hipStream_t s, unsigned long long* stamp, const P2PWait& w) {
     if (w.mailbox && (w.world <= 0 || w.world > 64)) return hipErrorInvalidValue;
@@ -1180,9 +1228,9 @@ hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* 
 
 hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
                                 double chi_const, int32_t nrob_const, int32_t* local_info, StepStatus* out,
-                                StepStatus* mirror, hipStream_t s) {
+                                StepStatus* mirror, hipStream_t s, bool zero_info) {
     hipLaunchKernelGGL(shard_combine_kernel, dim3(1), dim3(64), 0, s, recv1, c1, recv2, c2, world, chi_const, nrob_const,
-                       local_info, out, mirror);
+                       local_info, out, mirror, zero_info);
     return hipGetLastError();
 }
 
@@ -1192,6 +1240,16 @@ hipError_t launch_p2p_push(const double* send, int64_t count, double* const* pee
     if (world <= 0 || (chi_part && count < kExHeader)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(p2p_push_kernel, dim3(world), dim3(256), 0, s, send, count, peers, data_off, flag_off, rank, epoch,
                        chi_part, nrob_part, n_parts, stamp);
+    return hipGetLastError();
+}
+
+hipError_t launch_p2p_push_gather(const P2PPush& p, hipStream_t s) {
+    const bool bad1 = p.which == 1 && (!p.chi_part || (p.nseg > 0 && (!p.segs || !p.U || !p.u)));
+    const bool bad2 = p.which == 2 && (!p.info || !p.x || (p.n_abs > 0 && !p.abs_part) || (p.n_bnd > 0 && !p.bnd) ||
+                                       p.count < 2 + (int64_t)p.n_bnd);
+    if (p.world <= 0 || (p.which != 1 && p.which != 2) || p.count < kExHeader || bad1 || bad2)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(p2p_push_gather_kernel, dim3(p.world), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -195,6 +195,10 @@ template <typename T> hipError_t launch_from_f64(const double* in, T* out, int64
 hipError_t launch_shard_pack2(const double* x, const int32_t* nodes, int n_nodes, const int32_t* node_dof, int NP,
                               int32_t* info, const int32_t* bnd, int n_bnd, double* part, double* send2,
                               hipStream_t s, unsigned long long* stamp = nullptr);
+// the first launch of launch_shard_pack2 alone: per-block max |x| partials into part; returns the
+// number of partials (for launch_p2p_push_gather's exchange 2)
+int launch_node_absmax(const double* x, const int32_t* nodes, int n_nodes, const int32_t* node_dof, int NP, double* part,
+                       hipStream_t s, hipError_t* err);
 // dst[dst_idx[i]] = src[src_idx[i]], i < n; *stamp (if set) gets the realtime clock at the start
 // (after the wait, with one)
 hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* dst, const int32_t* dst_idx, int64_t n,
@@ -204,7 +208,7 @@ hipError_t launch_index_copy(const double* src, const int32_t* src_idx, double* 
 // sticky), identical on every rank.
 hipError_t launch_shard_combine(const double* recv1, int64_t c1, const double* recv2, int64_t c2, int world,
                                 double chi_const, int32_t nrob_const, int32_t* local_info, StepStatus* out,
-                                StepStatus* mirror, hipStream_t s);
+                                StepStatus* mirror, hipStream_t s, bool zero_info = false);
 template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipStream_t s);
 // Direct peer exchange (bos_exchange_p2p_connect): one block per receiving rank q copies the
 // `count` doubles of `send` to peers[q] + data_off (bytes) + rank * count doubles, drains its stores,
@@ -215,6 +219,33 @@ template <typename T> hipError_t launch_triangulate(const TriParams<T>& p, hipSt
 hipError_t launch_p2p_push(const double* send, int64_t count, double* const* peers, int64_t data_off, int64_t flag_off,
                            int rank, int world, const uint32_t* epoch, const double* chi_part, const int32_t* nrob_part,
                            int n_parts, unsigned long long* stamp, hipStream_t s);
+// The direct exchange's push with the payload gathered from where it lives instead of from a packed
+// send buffer (one launch less per exchange). Exchange 1: the header of
+// launch_shard_header1, then every pack segment (src_kind 0: U, 1: u; dst: offset in the slot).
+// Exchange 2: the header [max of abs_part, *info] (launch_shard_pack2's, without zeroing
+// *info: the combine launch zeroes it after the step, zero_info), then x[bnd[i]] at 2 + i.
+struct P2PPush {
+    int which = 1;                      // exchange 1 or 2
+    double* const* peers = nullptr;
+    int64_t data_off = 0, flag_off = 0, count = 0;
+    int rank = 0, world = 0;
+    const uint32_t* epoch = nullptr;
+    unsigned long long* stamp = nullptr;
+    const double* chi_part = nullptr;   // exchange 1
+    const int32_t* nrob_part = nullptr;
+    int n_parts = 0;
+    const double* U = nullptr;
+    const double* u = nullptr;
+    const ExSeg* segs = nullptr;
+    int nseg = 0;
+    const double* x = nullptr;          // exchange 2
+    const double* abs_part = nullptr;
+    int n_abs = 0;
+    const int32_t* info = nullptr;
+    const int32_t* bnd = nullptr;
+    int n_bnd = 0;
+};
+hipError_t launch_p2p_push_gather(const P2PPush& p, hipStream_t s);
 // Reduces the J+H kernel's chi^2 / robust-count partials (nrob_part null: chi_part is an
 // all-reduced header [chi^2, robust count], n ignored) (plus the constant terms of odometry
 // self-loops, chi_const / nrob_const) and the box-plus max |dx| partials (when max_part is set; a NaN

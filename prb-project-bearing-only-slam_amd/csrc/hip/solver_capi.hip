@@ -151,6 +151,7 @@ struct bos_solver {
     std::vector<void*> peer_maps;              // opened IPC mappings (closed at destroy)
     int64_t ex1_count = 0, ex2_count = 0;
     bos::dev::ExSeg *ex1_pack = nullptr, *ex1_unpack = nullptr;
+    int n_abs = 1;                          // max |x| partials of exchange 2 (direct exchange)
     int n1p = 0, n1u = 0;
     int64_t maxlen1p = 0, maxlen1u = 0;
     int32_t *ex2_bnd = nullptr, *ex2_usrc = nullptr, *ex2_udst = nullptr;   // pack / unpack index lists
@@ -656,20 +657,28 @@ int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
         if (with_jh && (rc = enqueue_linearize(s, s->d_status->stamp))) return rc;
         if ((rc = enqueue_solver_inputs(s))) return rc;   // opens this step's flow epoch
         HIP_TRY(bos::dev::mf_factor(s->mf, 0, mf_matrix(s), s->d_rhs, s->stream));
-        HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->hdr1, s->ex1_pack, s->n1p, s->maxlen1p,
-                                                  s->stream));
-        if (!s->p2p)   // (the direct exchange's push computes the header itself)
+        if (!s->p2p) {   // (the direct exchange's push gathers the payload and computes the header itself)
+            HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->hdr1, s->ex1_pack, s->n1p,
+                                                      s->maxlen1p, s->stream));
             HIP_TRY(bos::dev::launch_shard_header1(s->d_chi_part, s->d_nrob_part, s->chi_parts, s->ex1_send, s->stream,
                                                    s->d_status->stamp + 4));
+        }
     } else if (phase == 1) {
         HIP_TRY(bos::dev::launch_seg_copy<double>(U, u, s->ex1_send, s->ex1_recv, s->hdr1, s->ex1_unpack, s->n1u, s->maxlen1u,
                                                   s->stream, s->d_status->stamp + 5, p2p_wait(s, 1)));
         HIP_TRY(bos::dev::mf_factor(s->mf, 1, mf_matrix(s), s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, 1, s->d_rhs, s->stream));
         HIP_TRY(bos::dev::mf_solve(s->mf, 0, s->d_rhs, s->stream));
-        HIP_TRY(bos::dev::launch_shard_pack2(s->d_rhs, s->upd_nodes, s->n_upd_local, s->node_dof, s->NP,
-                                             bos::dev::mf_info_ptr(s->mf), s->ex2_bnd, s->n_bnd, s->abs_part, s->ex2_send,
-                                             s->stream, s->d_status->stamp + 6));
+        if (s->p2p) {   // the push packs exchange 2 itself (exchange()); the max |x| partials first
+            hipError_t e = hipSuccess;
+            s->n_abs = bos::dev::launch_node_absmax(s->d_rhs, s->upd_nodes, s->n_upd_local, s->node_dof, s->NP,
+                                                    s->abs_part, s->stream, &e);
+            HIP_TRY(e);
+        } else {
+            HIP_TRY(bos::dev::launch_shard_pack2(s->d_rhs, s->upd_nodes, s->n_upd_local, s->node_dof, s->NP,
+                                                 bos::dev::mf_info_ptr(s->mf), s->ex2_bnd, s->n_bnd, s->abs_part,
+                                                 s->ex2_send, s->stream, s->d_status->stamp + 6));
+        }
     } else {
         HIP_TRY(bos::dev::launch_index_copy(s->ex2_recv, s->ex2_usrc, s->d_rhs, s->ex2_udst, s->n_bnd_remote, s->stream,
                                             s->d_status->stamp + 7, p2p_wait(s, 2)));
@@ -679,7 +688,8 @@ int shard_enqueue(bos_solver* s, int phase, bool with_jh = true) {
         // exchange-1 headers from phase 1's local copy (the mailbox may already hold the next
         // iteration's); exchange 2's are still current (no rank pushes again before this rank does)
         HIP_TRY(bos::dev::launch_shard_combine(s->hdr1, bos::kExHeader, s->ex2_recv, s->ex2_count, s->world, chi_c,
-                                               nrob_c, bos::dev::mf_info_ptr(s->mf), s->d_status, s->m_status, s->stream));
+                                               nrob_c, bos::dev::mf_info_ptr(s->mf), s->d_status, s->m_status, s->stream,
+                                               s->p2p));
     }
     return BOS_OK;
 }
@@ -753,21 +763,45 @@ int rccl_allgather(bos_solver* s, const double* send, double* recv, int64_t coun
 int finish_step(bos_solver* s, bos_step_stats* st);
 
 // one all-gather of the sharded step: RCCL, or the direct peer exchange's push to every rank's
-// mailbox (exchange 1's push also computes the header; the receiving side's wait is fused into the
-// launch that reads the data, p2p_wait)
+// mailbox (the push gathers its payload and computes the header; the receiving side's wait is fused
+// into the launch that reads the data, p2p_wait)
 int exchange(bos_solver* s, int which) {
     const double* send = which == 1 ? s->ex1_send : s->ex2_send;
     double* recv = which == 1 ? s->ex1_recv : s->ex2_recv;
     const int64_t count = which == 1 ? s->ex1_count : s->ex2_count;
     if (!s->p2p) return rccl_allgather(s, send, recv, count);
     const int64_t data = which == 1 ? s->mb_ex1 : s->mb_ex2, flag = which == 1 ? s->mb_flag1 : s->mb_flag2;
-    const uint32_t* epoch = bos::dev::mf_epoch_ptr(s->mf);
-    if (which == 1)
-        HIP_TRY(bos::dev::launch_p2p_push(send, count, s->d_peers, data, flag, s->rank, s->world, epoch, s->d_chi_part,
-                                          s->d_nrob_part, s->chi_parts, s->d_status->stamp + 4, s->stream));
-    else
-        HIP_TRY(bos::dev::launch_p2p_push(send, count, s->d_peers, data, flag, s->rank, s->world, epoch, nullptr, nullptr, 0,
-                                          nullptr, s->stream));
+    // the push gathers its payload where it lives (exchange 1: the subtree roots' U / u by the pack
+    // segments, with the chi^2 header; exchange 2: the boundary solution with the max |x| / solver-word
+    // header): no pack launch before it
+    bos::dev::P2PPush p;
+    p.which = which;
+    p.peers = s->d_peers;
+    p.data_off = data;
+    p.flag_off = flag;
+    p.count = count;
+    p.rank = s->rank;
+    p.world = s->world;
+    p.epoch = bos::dev::mf_epoch_ptr(s->mf);
+    if (which == 1) {
+        p.stamp = s->d_status->stamp + 4;
+        p.chi_part = s->d_chi_part;
+        p.nrob_part = s->d_nrob_part;
+        p.n_parts = s->chi_parts;
+        p.U = bos::dev::mf_update_ptr(s->mf);
+        p.u = bos::dev::mf_uvec_ptr(s->mf);
+        p.segs = s->ex1_pack;
+        p.nseg = s->n1p;
+    } else {
+        p.stamp = s->d_status->stamp + 6;
+        p.x = s->d_rhs;
+        p.abs_part = s->abs_part;
+        p.n_abs = s->n_abs;
+        p.info = bos::dev::mf_info_ptr(s->mf);
+        p.bnd = s->ex2_bnd;
+        p.n_bnd = s->n_bnd;
+    }
+    HIP_TRY(bos::dev::launch_p2p_push_gather(p, s->stream));
     return BOS_OK;
 }
 

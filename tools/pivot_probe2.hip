@@ -32,6 +32,10 @@ __device__ __forceinline__ void wave_sync() {
 // MODE 2: chain only (pivots, L columns; no LDS broadcast, no trailing update, no stores)
 // MODE 3: trailing update only (fixed L columns through the LDS broadcast)
 // MODE 4: full step branch-free, no forward step
+// MODE 5: full step (predicated stores), the pivot pair of each trailing column read by readlane
+//         into scalar registers instead of the LDS broadcast
+// MODE 6: trailing update only, readlane form
+// MODE 7: full step (predicated stores), LDS broadcast with each group of 8 pairs read at once
 template <int M, int K, int MODE>
 __global__ __launch_bounds__(64) void step(const double* A, double* L, double* wout, unsigned long long* cyc,
                                            double* rows_out) {
@@ -50,7 +54,7 @@ __global__ __launch_bounds__(64) void step(const double* A, double* L, double* w
 #pragma nounroll
     for (int j = 0; j + 1 < K; j += 2) {
         double l0, l1, inv0, inv1;
-        if (MODE == 3) {
+        if (MODE == 3 || MODE == 6) {
             l0 = 0.01 * (lane + j);
             l1 = 0.02 * (lane + j);
             inv0 = inv1 = 1.0;
@@ -81,13 +85,13 @@ __global__ __launch_bounds__(64) void step(const double* A, double* L, double* w
             continue;
         }
         double2* cp = reinterpret_cast<double2*>(colbuf);
-        if (MODE == 0) {
-            if (lane > j + 1 && lane < M) cp[lane - j - 2] = make_double2(l0, l1);
+        if (MODE == 0 || MODE == 5 || MODE == 7) {
+            if (MODE != 5 && lane > j + 1 && lane < M) cp[lane - j - 2] = make_double2(l0, l1);
             if (live) {
                 if (lane >= j) __builtin_nontemporal_store(l0, Lj);
                 if (lane >= j + 1) __builtin_nontemporal_store(l1, Lj + M);
             }
-        } else if (MODE != 3) {
+        } else if (MODE != 3 && MODE != 6) {
             const bool wc = lane > j + 1 && lane < M;
             cp[wc ? lane - j - 2 : M + 1] = make_double2(l0, l1);   // slot M + 1: scratch
             __builtin_nontemporal_store(l0, (live && lane >= j) ? Lj : Lsink);
@@ -96,7 +100,7 @@ __global__ __launch_bounds__(64) void step(const double* A, double* L, double* w
             if (lane > j + 1 && lane < M) cp[lane - j - 2] = make_double2(l0, l1);
         }
         Lj += 2 * M;
-        if (MODE != 4 && MODE != 3) {
+        if (MODE != 4 && MODE != 3 && MODE != 6) {
             const double y0 = readlane_d(wi, j) * inv0;
             if (lane == j) wi = y0;
             else if (lane > j) wi -= l0 * y0;
@@ -104,11 +108,32 @@ __global__ __launch_bounds__(64) void step(const double* A, double* L, double* w
             if (lane == j + 1) wi = y1;
             else if (lane > j + 1) wi -= l1 * y1;
         }
-        wave_sync();
+        if (MODE == 5 || MODE == 6) {
 #pragma unroll
-        for (int t = 0; t < M - 2; ++t) {
-            const double2 c = cp[t];
-            row[t] = fma(-l1, c.y, fma(-l0, c.x, row[t + 2]));
+            for (int t = 0; t < M - 2; ++t) {
+                const double cx = readlane_d(l0, j + 2 + t), cy = readlane_d(l1, j + 2 + t);
+                row[t] = fma(-l1, cy, fma(-l0, cx, row[t + 2]));
+            }
+        } else if (MODE == 7) {
+            wave_sync();
+#pragma unroll
+            for (int t0 = 0; t0 < M - 2; t0 += 8) {
+                double2 c[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) c[u] = t0 + u < M - 2 ? cp[t0 + u] : make_double2(0.0, 0.0);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(c[u].x), "+v"(c[u].y));
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (t0 + u < M - 2) row[t0 + u] = fma(-l1, c[u].y, fma(-l0, c[u].x, row[t0 + u + 2]));
+            }
+        } else {
+            wave_sync();
+#pragma unroll
+            for (int t = 0; t < M - 2; ++t) {
+                const double2 c = cp[t];
+                row[t] = fma(-l1, c.y, fma(-l0, c.x, row[t + 2]));
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -146,6 +171,9 @@ void suite(double* dA, double* dL, double* dw, unsigned long long* dc, double* d
     run<M, K, 4>("static m, branch-free, no forward step", dA, dL, dw, dc, dr);
     run<M, K, 2>("chain only (pivots + L columns)", dA, dL, dw, dc, dr);
     run<M, K, 3>("trailing update only (LDS broadcast + FMAs)", dA, dL, dw, dc, dr);
+    run<M, K, 5>("static m, readlane broadcast", dA, dL, dw, dc, dr);
+    run<M, K, 6>("trailing update only, readlane broadcast", dA, dL, dw, dc, dr);
+    run<M, K, 7>("static m, LDS pairs read 8 at once", dA, dL, dw, dc, dr);
 }
 
 int main() {
