@@ -941,8 +941,14 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
     const bool live = lane < m;
     const int lrow = min(lane, m - 1);
     double row[MAXM];
+#if defined(BOS_MF_PIVOT_CYCLES) && defined(BOS_MF_ROWS_STAMPS)
+    cstamp(cst, s, 5);   // (diagnostic: slots 5 / 6 split the row loads instead of timing pivot steps)
+#endif
 #pragma unroll
     for (int c0 = 0; c0 < MAXM; c0 += 8) {   // whole groups of 8 past m skipped by a scalar branch
+#if defined(BOS_MF_PIVOT_CYCLES) && defined(BOS_MF_ROWS_STAMPS)
+        if (c0 == 8) cstamp(cst, s, 6);
+#endif
         if (c0 < m) {
             // branch-free: every lane reads a position of the LDS front (for a row i < m, pk32(i, c, m)
             // < np for every c < m + 8), the group's eight reads under one wait. A predicated read per
@@ -951,7 +957,9 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             // the diagonal, of rows >= m (copies of row m - 1) and of columns >= m are scratch that no
             // stored or broadcast value ever reads, so they are taken as read: selecting zeros there
             // held 48 loop-invariant lane masks that the compiler spilled to VGPR lanes and read back
-            // per column.
+            // per column. (All columns read at once, without the groups' waits and zero fills: rows
+            // 1 500 -> 1 260 cycles at the top, 3 430 -> 2 830 at level 0, solve unchanged,
+            // profiles/r05_rows_all_at_once_ab.txt.)
             double v[8];
 #pragma unroll
             for (int c = c0; c < c0 + 8; ++c) v[c - c0] = c < MAXM ? F[pk32(lrow, c, m)] : 0.0;
@@ -1044,7 +1052,11 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             }
             __builtin_amdgcn_wave_barrier();   // the next step's pair stores stay after these reads
 #ifdef BOS_MF_PIVOT_CYCLES
+#ifdef BOS_MF_ROWS_STAMPS
+            if (j / 2 < 1) cstamp(cst, s, 4 + j / 2);
+#else
             if (j / 2 < 3) cstamp(cst, s, 4 + j / 2);
+#endif
 #endif
         }
     }

@@ -5,7 +5,10 @@ children ready, [2] their update matrices loaded (coherent loads), [3] extend-ad
 start (rows in registers), [4..6] after two-pivot steps 1-3, [7] pivot loop end. Prints per level the
 median k and m, cycles of: child value loads, LDS extend-add, row loads, the whole pivot loop, one
 two-pivot step; and the core clock (GHz) from the factor stamps' realtime clock over the pivot loop.
-Usage: python tools/pivot_cycles.py gpurun_exp/libbos_pivcyc.so"""
+Usage: python tools/pivot_cycles.py gpurun_exp/libbos_pivcyc.so [--rows]
+--rows: a build with -DBOS_MF_ROWS_STAMPS, whose stamps [5] / [6] mark the row loads' start and the
+end of their first group of 8: prints the row loads split as (extend end -> start), first group,
+the rest (up to the pivot loop)."""
 import os
 import sys
 
@@ -14,8 +17,10 @@ sys.path.insert(0, os.path.join(ROOT, "prb-project-bearing-only-slam_amd"))
 import numpy as np  # noqa: E402
 import bos  # noqa: E402
 
-if len(sys.argv) > 1:
-    bos.LIB_PATH = os.path.abspath(sys.argv[1])
+ROWS = "--rows" in sys.argv
+args = [a for a in sys.argv[1:] if a != "--rows"]
+if args:
+    bos.LIB_PATH = os.path.abspath(args[0])
     bos.ALLOW_MISSING_SYMBOLS = True
 P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
 S = bos.Solver(P, precision=bos.BOS_FP32, device=0, solver=bos.BOS_SOLVER_SCHUR)
@@ -37,6 +42,16 @@ def med(x):
     return float(np.median(x)) if len(x) else float("nan")
 
 
+if ROWS:
+    print(f"{'lvl':>3} {'fronts':>6} {'k':>4} {'m':>4} {'pre':>6} {'group0':>7} {'rest':>6} {'rows':>6}")
+    for l in sorted(set(lev[ok])):
+        sel = ok & (lev == l)
+        c = C[sel].astype(float)
+        k = meta[sel, 1].astype(float)
+        m = k + meta[sel, 2]
+        print(f"{l:3d} {sel.sum():6d} {np.median(k):4.0f} {np.median(m):4.0f} {med(c[:, 5] - c[:, 3]):6.0f} "
+              f"{med(c[:, 6] - c[:, 5]):7.0f} {med(c[:, 0] - c[:, 6]):6.0f} {med(c[:, 0] - c[:, 3]):6.0f}")
+    sys.exit(0)
 for l in sorted(set(lev[ok])):
     sel = ok & (lev == l)
     k = meta[sel, 1].astype(float)
