@@ -45,21 +45,12 @@ __device__ __forceinline__ int pk32(int i, int j, int m) { return j * m - j * (j
 
 // L panel traffic (written by the factorization, read once by the backward substitution): the
 // stores are non-temporal, so the solve's ~300 MB of L stream past the caches instead of evicting the
-// next J+H build's inputs (in-step J+H 16.0-16.5 -> 13.2-14.5 us, solve -14 us). The
-// folded landmarks' backward launch reads its L columns with plain loads (non-temporal loads there:
-// solve +13 us, profiles/r05_fold_l_policy_ab.txt). -DBOS_MF_CACHED_L (A/B only) restores plain stores
-// and loads everywhere, -DBOS_MF_L_LD_PLAIN plain loads everywhere.
-#ifndef BOS_MF_CACHED_L
+// next J+H build's inputs (in-step J+H 16.0-16.5 -> 13.2-14.5 us, solve -14 us; plain stores and
+// loads: profiles/r05_ntl_lds_ab.txt). The backward launches' panel loads are non-temporal too (plain
+// loads measured slower), except the folded landmarks' backward launch, which reads its L columns
+// with plain loads (non-temporal there: solve +13 us, profiles/r05_fold_l_policy_ab.txt).
 #define ST_L(p, i, v) __builtin_nontemporal_store((v), (p) + (i))
-#ifndef BOS_MF_L_LD_PLAIN
 #define LD_L(p, i) __builtin_nontemporal_load((p) + (i))
-#else
-#define LD_L(p, i) ((p)[i])
-#endif
-#else
-#define ST_L(p, i, v) ((p)[i] = (v))
-#define LD_L(p, i) ((p)[i])
-#endif
 #define ST_LF(p, i, v) ST_L(p, i, v)
 #define LD_LF(p, i) ((p)[i])
 
@@ -1025,7 +1016,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
 #pragma unroll
             for (int t0 = 0; t0 < MAXM - 2; t0 += 8) {
                 if (t0 < nt) {
-#ifndef BOS_MF_PAIRS_ONE_BY_ONE
                     // the group's eight pairs read at once (one LDS latency per group; pairs past the
                     // live columns are scratch), the empty asm keeps the compiler from interleaving a
                     // wait per pair: two-pivot step 1 269 -> 1 037 cycles at m = 18, 1 818 -> 1 554 at
@@ -1038,16 +1028,6 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
 #pragma unroll
                     for (int u = 0; u < 8; ++u)
                         if (t0 + u < MAXM - 2) row[t0 + u] = fma(-l1, c[u].y, fma(-l0, c[u].x, row[t0 + u + 2]));
-#else
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int t = t0 + u;
-                        if (t < MAXM - 2) {
-                            const double2 c = cp[t];
-                            row[t] = fma(-l1, c.y, fma(-l0, c.x, row[t + 2]));
-                        }
-                    }
-#endif
                 }
             }
             __builtin_amdgcn_wave_barrier();   // the next step's pair stores stay after these reads
