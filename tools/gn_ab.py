@@ -1,7 +1,7 @@
 """A/B timing of libbos.so build variants on the bench's config-3 world (fp32 J+H, fp64 Schur
 solve; experiments). Each variant runs in its own process, alternating A B A B ...; per run: the
 median device-stamped phases of 50 synchronous steps, synchronous GN it/s (bos_time_steps, best of
-3 x 50) and a checksum of the state after 50 iterations (equal for variants that compute the same).
+3 x 50), batched GN it/s (bos_step_n of 50, best of 3) and a checksum of the state after 50 iterations (equal for variants that compute the same).
 
     python tools/gn_ab.py <libA.so> <libB.so> [<libC.so> ...] [rounds]
 
@@ -34,8 +34,17 @@ def child(lib, label):
     for _ in range(3):
         S.set_state(*init)
         best = max(best, 1e3 / S.time_steps(50))
+    import time
+    batched = 0.0
+    for _ in range(3):   # bos_step_n batches of 50 (the host ahead of the device)
+        S.set_state(*init)
+        S.synchronize()
+        t0 = time.perf_counter()
+        S.step_n(50)
+        S.synchronize()
+        batched = max(batched, 50 / (time.perf_counter() - t0))
     print(f"{label}: J+H {ph['t_linearize_ms']:.2f} us  solve {ph['t_solve_ms']:.1f} us  "
-          f"update {ph['t_update_ms']:.1f} us  GN {best:.0f} it/s  state {ck!r}", flush=True)
+          f"update {ph['t_update_ms']:.1f} us  GN {best:.0f} it/s  batched {batched:.0f} it/s  state {ck!r}", flush=True)
 
 
 def main():
