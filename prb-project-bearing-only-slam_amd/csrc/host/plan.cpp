@@ -233,7 +233,7 @@ void nested_dissection(const Graph& g, const std::vector<char>& active, std::vec
         int bestk = -1;
         // balanced splits keep the assembly tree shallow (its depth is the solver's critical path):
         // each side must hold >= minpct % of the nodes (40: 17 levels at config 3 instead of 27
-        // with 20, for 6 % more flops); BOS_ND_MINPCT overrides (diagnostics)
+        // with 20, for 6 % more flops; build_plan tries other balances when a front does not fit)
         const int minpct = nd_minpct();
         for (int k = 1; k + 1 < h; ++k) {
             const int64_t below = cum[k - 1], above = tot - cum[k];

@@ -43,8 +43,11 @@ def child(lib, label):
         S.step_n(50)
         S.synchronize()
         batched = max(batched, 50 / (time.perf_counter() - t0))
+    info = bos.plan_inspect(P, solver=bos.BOS_SOLVER_SCHUR)
+    plan = f"levels {info['mf_levels']} balance {info['mf_balance_pct']} fits {info['mf_fits']}"
     print(f"{label}: J+H {ph['t_linearize_ms']:.2f} us  solve {ph['t_solve_ms']:.1f} us  "
-          f"update {ph['t_update_ms']:.1f} us  GN {best:.0f} it/s  batched {batched:.0f} it/s  state {ck!r}", flush=True)
+          f"update {ph['t_update_ms']:.1f} us  GN {best:.0f} it/s  batched {batched:.0f} it/s  state {ck!r}  {plan}",
+          flush=True)
 
 
 def main():
