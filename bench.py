@@ -253,6 +253,219 @@ def launch_ranks(n, deadline_s=1800.0):
     return bad[0] if bad else 0
 
 
+LADDER = {"p2p": ("p2p", "rccl", "gloo"), "rccl": ("rccl", "gloo"), "gloo": ("gloo",)}
+
+
+def agree_all(dist, torch, ok, why=None):
+    """Every rank's verdict on one step of the exchange ladder: (True only if every rank is ok, every
+    rank's reason in rank order). Without a process group: (ok, [why])."""
+    if dist is None:
+        return ok, [why]
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    whys = [None] * dist.get_world_size()
+    dist.all_gather_object(whys, why)
+    return bool(int(t.item()) == 1), whys
+
+
+def run_ladder(modes, setup, run, agree, close, log):
+    """The N > 1 exchange ladder: try each mode in order — set it up on every rank
+    (setup(mode), local apart from its own collective calls), agree, run it (run(mode, handle): the
+    consistency check and the timed steps, collective-safe), agree — and keep the first mode every
+    rank completed. A mode that fails on any rank is closed on every rank and the next one is tried,
+    so all ranks always take the same decision. Returns (mode or None, handle, run's result, attempts:
+    one record per mode tried, with each failing rank's reason)."""
+    attempts = []
+    for mode in modes:
+        h, why = None, None
+        try:
+            h = setup(mode)
+        except Exception as e:
+            why = f"setup: {type(e).__name__}: {e}"
+        ok, whys = agree(why is None, why)
+        if not ok:
+            attempts.append({"mode": mode, "ok": False, "stage": "setup",
+                             "why": {r: w for r, w in enumerate(whys) if w}})
+            log(f"exchange {mode}: setup failed {attempts[-1]['why']}")
+            close(h)
+            continue
+        res, why = None, None
+        try:
+            res = run(mode, h)
+        except Exception as e:
+            why = f"{type(e).__name__}: {e}"
+        ok, whys = agree(why is None, why)
+        if ok:
+            attempts.append({"mode": mode, "ok": True})
+            return mode, h, res, attempts
+        attempts.append({"mode": mode, "ok": False, "stage": "run", "why": {r: w for r, w in enumerate(whys) if w}})
+        log(f"exchange {mode}: run failed {attempts[-1]['why']}")
+        close(h)
+    return None, None, None, attempts
+
+
+def topology(rank, world, local_rank, device, ndev, dist):
+    """Where the ranks run: every rank's (rank, local rank, device, visible devices, visibility
+    variables), and rank 0's peer-access matrix of the visible devices (hipDeviceCanAccessPeer)."""
+    mine = {"rank": rank, "local_rank": local_rank, "device": device, "visible_devices": ndev,
+            "host": socket.gethostname(),
+            "HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES"),
+            "ROCR_VISIBLE_DEVICES": os.environ.get("ROCR_VISIBLE_DEVICES")}
+    peer = None
+    if rank == 0:
+        try:
+            peer = bos.device_peer_access()
+        except Exception as e:
+            peer = f"unavailable: {e}"
+    ranks = [mine]
+    if dist is not None and world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    return {"ranks": ranks, "peer_access": peer}
+
+
+def fail_line(args, world, attempts, topo=None):
+    """No exchange mode (or the one-GPU run) completed: rank 0 still prints one line saying so."""
+    if int(os.environ.get("RANK", "0")) != 0:
+        return
+    print(json.dumps({"metric": METRIC, "value": None, "unit": "obs/s", "n_gpus": world, "steps": args.steps,
+                      "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
+                      "vs_baseline": None, "dtype": args.precision.replace("fp", "f"), "data": "synthetic",
+                      "config": {"workload": "config 3 (no run completed)"},
+                      "error": "no exchange mode completed" if world > 1 else "the GN run failed",
+                      "exchange_decision": {"mode": None, "attempts": attempts}, "topology": topo}), flush=True)
+
+
+def check_ladder(args, rank, dist, torch):
+    """--check-launch --check-ladder: the exchange ladder of main() with stand-in modes (no GPU) that
+    fail where the spec says; each stand-in run makes the real run's kinds of collective calls after
+    its failure point too (a barrier, a chi^2 reduction), as check_and_time does."""
+    fails = set()
+    for item in filter(None, (args.check_ladder or "").split(",")):
+        mode_stage, _, r = item.partition("@")
+        fails.add((mode_stage, r or "*"))
+
+    def failing(mode, stage):
+        return (f"{mode}:{stage}", "*") in fails or (f"{mode}:{stage}", str(rank)) in fails
+
+    def setup(mode):
+        if failing(mode, "setup"):
+            raise RuntimeError(f"stand-in {mode} setup failure")
+        return mode
+
+    def run(mode, h):
+        err = "stand-in run failure" if failing(mode, "run") else None
+        dist.barrier()
+        t = torch.tensor([float("nan") if err else 1.0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if err:
+            raise RuntimeError(err)
+        return mode
+
+    mode, _, _, attempts = run_ladder(LADDER[args.exchange], setup, run,
+                                      lambda ok, why: agree_all(dist, torch, ok, why), lambda h: None,
+                                      lambda *a: None)
+    return {"mode": mode, "attempts": attempts}
+
+
+def bench_c2(args):
+    """BASELINE config 2 on one GPU: the synthetic 1k-pose / 2k-landmark / 20k-bearing
+    world the GPU parity tests check (bos.synthetic(1000, 2000, 20)), fp64 J+H and solve. At this size the
+    step is launch- and latency-bound (1.7 MB of J+H traffic), so the line reports microseconds: per GN
+    iteration (synchronous bos_step, the Python loop and the C loop; bos_step_n batches), the in-step
+    phases (device stamps) and the J+H build back to back, beside the build's C++ CPU backend (full GN
+    iterations on 1 thread and on every usable CPU) and the oracle's J+H on the same host."""
+    global bos
+    import bos as _bos
+    bos = _bos
+    bos.lib()
+    precision = bos.BOS_FP64 if args.precision == "fp64" else bos.BOS_FP32
+    P = bos.synthetic(1000, 2000, 20)
+    nobs = len(P.b_z) + len(P.o_z)
+    S = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SCHUR, device=0)
+    init = S.get_state()
+    for _ in range(max(args.warmup, 20)):
+        S.step()
+    S.set_state(*init)
+    S.synchronize()
+    k = args.steps
+    t0 = time.perf_counter()
+    stats = [S.step() for _ in range(k)]
+    S.synchronize()
+    wall = time.perf_counter() - t0
+    assert all(g["solver_info"] == 0 for g in stats), "non-positive pivot in a timed C2 step"
+    S.set_state(*init)
+    ph = {key: float(np.median([g[key] for g in stats])) for key in ("t_linearize_ms", "t_solve_ms", "t_update_ms")}
+    c_loop_ms = S.time_steps(k)
+    S.set_state(*init)
+    tb = time.perf_counter()
+    last = S.step_n(args.batch)
+    S.synchronize()
+    batched_ms = (time.perf_counter() - tb) * 1e3 / args.batch
+    assert last["solver_info"] == 0
+    S.set_state(*init)
+    warm_ms = S.time_linearize(max(args.replay_steps, 200))
+    S.close()
+    # the other multifrontal ordering (nested dissection, landmarks not folded) on the same world
+    S2 = bos.Solver(P, precision=precision, solver=bos.BOS_SOLVER_SUPERNODAL, device=0)
+    for _ in range(5):
+        S2.step()
+    t2 = time.perf_counter()
+    st2 = [S2.step() for _ in range(k)]
+    S2.synchronize()
+    other = {"solver": "supernodal", "gn_us_per_iteration": (time.perf_counter() - t2) * 1e6 / k,
+             "t_solve_us": float(np.median([g["t_solve_ms"] for g in st2])) * 1e3}
+    S2.close()
+    cpus = host_cpus()
+    cpu = {}
+    for th in sorted({1, cpus["usable"]}):
+        c = bos.CpuGN(P, th)
+        c.step()
+        n, tc = 0, time.perf_counter()
+        while time.perf_counter() - tc < 3.0 or n < 5:
+            c.step()
+            n += 1
+        cpu[f"{th} threads"] = (time.perf_counter() - tc) * 1e6 / n
+        c.close()
+    cpu_best = min(cpu.values())
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    from helpers import to_oracle
+    Q = to_oracle(P)
+    O.linearize(Q, precision=64 if precision == bos.BOS_FP64 else 32)
+    n, tc = 0, time.perf_counter()
+    while time.perf_counter() - tc < 2.0 or n < 5:
+        O.linearize(Q, precision=64 if precision == bos.BOS_FP64 else 32)
+        n += 1
+    oracle_jh_us = (time.perf_counter() - tc) * 1e6 / n
+    gn_us = wall * 1e6 / k
+    line = {
+        "metric": METRIC, "value": nobs / (ph["t_linearize_ms"] * 1e-3), "unit": "obs/s", "n_gpus": 1, "steps": k,
+        "warmup": max(args.warmup, 20), "ms_per_step": ph["t_linearize_ms"], "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64" if precision == bos.BOS_FP64 else "f32",
+        "data": "synthetic",
+        "config": {"workload": "config 2: synthetic 1k poses / 2k landmarks / 20k bearings / 999 odometry edges "
+                               "(bos.synthetic(1000, 2000, 20), the GPU parity tests' world); J+H and solve "
+                               + args.precision + ", schur", "poses": P.NP, "landmarks": P.NL,
+                   "bearings": int(len(P.b_z)), "odometry": int(len(P.o_z)), "parallelism": "single GPU"},
+        "note": "launch-bound size (SURVEY.md §8(d)): microseconds per iteration, no roofline",
+        "gn_us_per_iteration": gn_us, "gn_iters_per_s": 1e6 / gn_us,
+        "gn_us_per_iteration_c_loop": c_loop_ms * 1e3, "gn_us_per_iteration_batched": batched_ms * 1e3,
+        "gn_phase_us": {key.replace("_ms", "_us"): v * 1e3 for key, v in ph.items()}, "gn_other": other,
+        "jh_us_in_step": ph["t_linearize_ms"] * 1e3, "jh_us_back_to_back": warm_ms * 1e3,
+        "cpu_baseline_gn": {"us_per_iteration": cpu_best, "forms_us_per_iteration": cpu, "kind": "port",
+                            "sample": "full GN iterations of config 2 by the build's C++ CPU backend (fp64 J+H, host "
+                                      "multifrontal Cholesky, box-plus), >= 3 s per thread count", "host": cpus},
+        "cpu_baseline_jh": {"us_per_build": oracle_jh_us, "cores": 1, "kind": "port",
+                            "sample": "the C++ oracle's J+H of config 2 in reference order, >= 2 s"},
+        "gn_speedup_vs_cpu": cpu_best / gn_us, "jh_speedup_vs_cpu": oracle_jh_us / (ph["t_linearize_ms"] * 1e3),
+        "libbos_sha256": lib_sha256(),
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -262,7 +475,12 @@ def main():
                     help="untimed GN iterations (bos_step_n batches of 100, about 0.5 s on one GPU) before the "
                          "headline's warmup: brings the GPU to its steady clocks (tools/jh_placement_probe.py); "
                          "0 = off")
-    ap.add_argument("--precision", choices=["fp32", "fp64"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "fp64"], default=None,
+                    help="J+H precision (default fp32 for config 3, fp64 for config 2)")
+    ap.add_argument("--config", choices=["c3", "c2"], default="c3",
+                    help="c3: the headline (100k / 200k / 1M, fp32 J+H); c2: BASELINE config 2 (synthetic 1k poses / "
+                         "2k landmarks / 20k bearings, fp64, one GPU), launch-bound: microseconds per GN iteration "
+                         "and per J+H build beside the CPU backend's (SURVEY.md §8(d))")
     ap.add_argument("--replay-steps", type=int, default=200, help="J+H builds back to back (warm-replay roofline)")
     ap.add_argument("--cold-steps", type=int, default=20, help="J+H builds timed from cold caches by events")
     ap.add_argument("--batch", type=int, default=50, help="GN iterations per bos_step_n batch (the reference UI's 50)")
@@ -281,6 +499,10 @@ def main():
                          "the ranks seen")
     ap.add_argument("--check-launch-fail-rank", type=int, default=-1,
                     help="with --check-launch: this rank exits 5 before the rendezvous (tests the launcher)")
+    ap.add_argument("--check-ladder", default=None,
+                    help="with --check-launch: run the exchange ladder with stand-in modes that fail as listed "
+                         "(comma-separated MODE:STAGE@RANK, STAGE setup|run, RANK a rank or *), print the decision "
+                         "(tests/test_bench.py; no GPU)")
     ap.add_argument("--solver", choices=["supernodal", "schur"], default="schur",
                     help="GN linear solver: landmarks-first Schur multifrontal (config 5, default) or "
                          "nested-dissection multifrontal; the other one is timed too (gn_other)")
@@ -289,6 +511,13 @@ def main():
                          "the same at every N so that the scaling curve compares the same arithmetic")
     args = ap.parse_args()
 
+    if args.precision is None:
+        args.precision = "fp64" if args.config == "c2" else "fp32"
+    if args.config == "c2":
+        if args.gpus != 1:
+            log("error: --config c2 runs on one GPU")
+            sys.exit(2)
+        sys.exit(bench_c2(args))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
 
@@ -311,9 +540,19 @@ def main():
             parts = [torch.zeros_like(t) for _ in range(world)]
             dist.all_gather(parts, t)
             seen = len({int(x) for x in parts})
+            decision = None
+            if args.check_ladder is not None:
+                decision = check_ladder(args, rank, dist, torch)
             dist.destroy_process_group()
+        else:
+            decision = None
         if rank == 0:
-            print(json.dumps({"check_launch": True, "ranks_seen": seen, "world": world}), flush=True)
+            out = {"check_launch": True, "ranks_seen": seen, "world": world}
+            if decision is not None:
+                out["exchange_decision"] = decision
+            print(json.dumps(out), flush=True)
+        if decision is not None and decision["mode"] is None:
+            sys.exit(4)
         sys.exit(0 if seen == args.gpus else 3)
 
     global bos
@@ -327,7 +566,7 @@ def main():
 
     # torch only for the rendezvous and the gloo rehearsal (host memory): the GPU work and its timing
     # go through libbos.so, and the exchanges run on RCCL inside it
-    dist = None
+    dist, torch = None, None
     if world > 1:
         import torch
         import torch.distributed as dist
@@ -351,66 +590,48 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    device = 0 if args.same_device else local_rank
+    # the rank's device: LOCAL_RANK among the visible devices; a launcher that shows each rank only
+    # its own GPU (one visible device) gets device 0
+    ndev = bos.device_count()
+    device = 0 if (args.same_device or (ndev == 1 and local_rank > 0)) else local_rank
+    topo = topology(rank, world, local_rank, device, ndev, dist)
     solver = bos.BOS_SOLVER_SCHUR if args.solver == "schur" else bos.BOS_SOLVER_SUPERNODAL
 
     lpp = args.lanes_per_pose
 
-    def make_handle(partition, rccl=None):
+    def make_handle(partition, mode):
+        """A handle for `mode` (world 1: "single"; N > 1: "p2p", "rccl" or "gloo"). Collective-safe:
+        every rank makes the same collective calls whatever fails locally (the RCCL id broadcast),
+        then creates its handle locally; raises on a local failure."""
         nccl_id = None
-        if world > 1 and (args.exchange != "gloo" if rccl is None else rccl):
-            obj = [bos.nccl_unique_id() if rank == 0 else None]
+        if mode == "rccl":
+            uid = None
+            if rank == 0:
+                try:
+                    uid = bos.nccl_unique_id()
+                except Exception as e:   # broadcast None: every rank then fails this mode alike
+                    log(f"rank 0: ncclGetUniqueId failed: {e}")
+            obj = [uid]
             dist.broadcast_object_list(obj, src=0)
             nccl_id = obj[0]
+            if nccl_id is None:
+                raise RuntimeError("no RCCL unique id (ncclGetUniqueId failed on rank 0)")
         t0 = time.perf_counter()
         h = bos.Solver(P, precision=precision, solver=solver, device=device, rank=rank, world_size=world,
                        nccl_id=nccl_id, partition=partition, lanes_per_pose=lpp)
-        inf = h.system_info()
-        # the ranks the exchange actually spans: the communicator's count (RCCL), or gloo's
-        seen = inf["comm_ranks"] if nccl_id is not None else (dist.get_world_size() if world > 1 else 1)
-        log(f"rank {rank}: bos_create ({'observations' if partition else 'subtree'} partition) "
-            f"{time.perf_counter() - t0:.1f} s, n={inf['n']} nnz(H lower)={inf['nnz_lower']} "
-            f"nnz(L)={inf['nnz_factor']}, ranks seen {seen}")
-        if seen != args.gpus:
-            log(f"error: rank {rank}: the exchange spans {seen} ranks, --gpus {args.gpus}")
-            sys.exit(3)
-        return h, inf, seen
-
-    S, info, ranks_seen = make_handle(bos.BOS_PARTITION_SUBTREE, rccl=args.exchange == "rccl")
-    exchange = "single GPU" if world == 1 else ("gloo rehearsal" if args.exchange == "gloo" else "rccl")
-    exchange_reason = {"p2p": None, "rccl": "--exchange rccl", "gloo": "--exchange gloo (rehearsal)"}[args.exchange] \
-        if world > 1 else None
-    if world > 1 and args.exchange == "p2p":
-        # Every rank maps every other rank's mailbox (HIP IPC), then three GN steps from the initial
-        # guess must give every rank the same chi^2 (each rank combines all ranks' headers, so a
-        # payload that did not arrive intact shows as a difference). All ranks, or none, keep it;
-        # otherwise the handle is rebuilt on RCCL all-gathers.
-        ok, why = 1, ""
         try:
-            handles = [None] * world
-            dist.all_gather_object(handles, S.p2p_handle())
-            S.p2p_connect(handles)
-            init = S.get_state()
-            chk = [S.step()["chi2"] for _ in range(3)]
-            S.set_state(*init)
-        except bos.BosError as e:
-            ok, why, chk = 0, str(e), [float("nan")] * 3
-        lo, hi = torch.tensor(chk, dtype=torch.float64), torch.tensor(chk, dtype=torch.float64)
-        flag = torch.tensor([ok], dtype=torch.int64)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-        if int(flag.item()) == 1 and bool(torch.equal(lo, hi)):
-            exchange = "p2p"
-            exchange_reason = ("every rank mapped every other rank's mailbox (HIP IPC, peer access) and three GN steps "
-                               "gave every rank the same chi^2")
-        else:
-            why = why or ("on another rank" if int(flag.item()) != 1 else "the ranks' chi^2 differ")
-            log(f"rank {rank}: direct exchange unusable ({why}); RCCL all-gathers instead")
-            S.close()
-            S, info, ranks_seen = make_handle(bos.BOS_PARTITION_SUBTREE, rccl=True)
-            exchange = "rccl (direct exchange failed its check)"
-            exchange_reason = f"direct exchange unusable: {why}"
+            inf = h.system_info()
+            # the ranks the exchange actually spans: the communicator's count (RCCL), or the process group's
+            seen = inf["comm_ranks"] if nccl_id is not None else (dist.get_world_size() if world > 1 else 1)
+            log(f"rank {rank}: bos_create ({'observations' if partition else 'subtree'} partition, {mode}) "
+                f"{time.perf_counter() - t0:.1f} s, n={inf['n']} nnz(H lower)={inf['nnz_lower']} "
+                f"nnz(L)={inf['nnz_factor']}, ranks seen {seen}")
+            if seen != args.gpus:
+                raise RuntimeError(f"the exchange spans {seen} ranks, --gpus {args.gpus}")
+        except Exception:
+            h.close()
+            raise
+        return h, inf, seen
 
     # ---- one GN iteration, per exchange mode
     def gloo_allgather(h, which):
@@ -424,8 +645,8 @@ def main():
         dist.all_reduce(t)
         h.exchange_upload(1, t.numpy())
 
-    def gn_step(h, partition):
-        if world == 1 or args.exchange != "gloo":
+    def gn_step(h, partition, mode):
+        if mode != "gloo":
             return h.step()
         if partition == bos.BOS_PARTITION_OBSERVATIONS:
             h.step_phase(0)
@@ -437,33 +658,143 @@ def main():
         gloo_allgather(h, 2)
         return h.step_phase(2)
 
-    def timed_steps(h, partition, k, warmup, device_warmup=0):
+    def quiet(fn, *a):
+        try:
+            fn(*a)
+        except Exception as e:
+            log(f"rank {rank}: {getattr(fn, '__name__', fn)}: {e}")
+
+    def timed_steps(h, partition, k, warmup, mode, device_warmup=0):
         """`device_warmup` untimed GN iterations as one batch (not with the gloo exchange), `warmup`
         untimed GN iterations, then the state reset to the initial guess (outside the
         timed region) and k GN iterations from it, timed as one region: iterations 1..k of the solve
         (the world converges; tests/test_gpu_c3_gn.py checks 200 fp32 iterations positive definite).
-        Returns (wall seconds of the timed steps, max over ranks; per-step stats)."""
-        init = h.get_state()
-        if device_warmup > 0 and (world == 1 or args.exchange != "gloo"):
-            for b in range(0, device_warmup, 100):   # batches of <= 100 from the initial guess (the
-                h.step_n(min(100, device_warmup - b))  # trajectory tests/test_gpu_c3_gn.py checks)
-                h.set_state(*init)
-        for _ in range(warmup):
-            gn_step(h, partition)
-        h.set_state(*init)
-        h.synchronize()
+        Collective-safe (N > 1): a local failure stops this rank's stepping but not its barriers and
+        reductions, so every rank leaves together. Returns (wall seconds of the timed steps, max over
+        ranks; per-step stats; the local error or None)."""
+        err, init, stats = None, None, []
+        try:
+            init = h.get_state()
+            if device_warmup > 0 and mode != "gloo":
+                for b in range(0, device_warmup, 100):   # batches of <= 100 from the initial guess (the
+                    h.step_n(min(100, device_warmup - b))  # trajectory tests/test_gpu_c3_gn.py checks)
+                    h.set_state(*init)
+            for _ in range(warmup):
+                gn_step(h, partition, mode)
+            h.set_state(*init)
+            h.synchronize()
+        except Exception as e:
+            err = f"warm-up: {type(e).__name__}: {e}"
         barrier()
-        h.synchronize()
+        quiet(h.synchronize)
         t0 = time.perf_counter()
-        stats = [gn_step(h, partition) for _ in range(k)]
-        h.synchronize()
+        if err is None:
+            try:
+                for _ in range(k):
+                    stats.append(gn_step(h, partition, mode))
+                h.synchronize()
+            except Exception as e:
+                err = f"timed GN step {len(stats) + 1}: {type(e).__name__}: {e}"
         barrier()
-        h.synchronize()
+        quiet(h.synchronize)
         wall = max_over_ranks(time.perf_counter() - t0)
-        h.set_state(*init)
+        if init is not None:
+            quiet(h.set_state, *init)
         bad = [i + 1 for i, g in enumerate(stats) if g["solver_info"] != 0]
-        assert not bad, f"non-positive pivot or stall in benchmarked GN iterations {bad[:5]}"
+        if err is None and bad:
+            err = f"non-positive pivot or stall in benchmarked GN iterations {bad[:5]}"
+        return wall, stats, err
+
+    def chi2_agree(vals):
+        """Every rank's chi^2 sequence equal bit for bit (NaN, a failed rank's placeholder, never is)."""
+        if world == 1:
+            return True
+        mine = torch.tensor(vals, dtype=torch.float64)
+        lo, hi = mine.clone(), mine.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        return bool(torch.equal(lo, hi))
+
+    def check_and_time(mode, hinf, partition, k, warmup, device_warmup):
+        """One exchange mode's run (collective-safe; raises at the end on a local or global failure):
+        the direct exchange connected (every rank maps every other rank's mailbox), three GN steps from
+        the initial guess giving every rank the same chi^2 (each rank combines all ranks' headers, so a
+        payload that did not arrive intact shows as a difference), then the timed steps, whose per-step
+        chi^2 must agree on every rank too."""
+        h = hinf[0]
+        err = None
+        if mode == "p2p":
+            mine = None
+            try:
+                mine = h.p2p_handle()
+            except Exception as e:
+                err = f"p2p handle: {e}"
+            handles = [None] * world
+            dist.all_gather_object(handles, mine)
+            if err is None:
+                try:
+                    if any(x is None for x in handles):
+                        raise RuntimeError("another rank has no mailbox handle")
+                    h.p2p_connect(handles)
+                except Exception as e:
+                    err = f"p2p connect: {e}"
+        if not agree_all(dist, torch, err is None)[0]:
+            raise RuntimeError(err or "the direct exchange failed on another rank")
+        chk = [float("nan")] * 3
+        if world > 1:
+            try:
+                init = h.get_state()
+                chk = [gn_step(h, partition, mode)["chi2"] for _ in range(3)]
+                h.set_state(*init)
+            except Exception as e:
+                err = f"check steps: {type(e).__name__}: {e}"
+                chk = [float("nan")] * 3
+        same = chi2_agree(chk)
+        if err is None and not same:
+            err = "the ranks' chi^2 differ over three GN steps"
+        if not agree_all(dist, torch, err is None)[0]:
+            raise RuntimeError(err or "the check failed on another rank")
+        wall, stats, err = timed_steps(h, partition, k, warmup, mode, device_warmup)
+        vals = [g["chi2"] for g in stats] if err is None and len(stats) == k else [float("nan")] * k
+        same = chi2_agree(vals)
+        if err is None and not same:
+            err = f"the ranks' per-step chi^2 differ (exchange {mode})"
+        if err is not None:
+            raise RuntimeError(err)
         return wall, stats
+
+    def close_handle(hinf):
+        if hinf is not None:
+            quiet(hinf[0].close)
+
+    # ---- the timed region: K GN iterations; the J+H inside them is the headline (K = 0: no GN steps,
+    # the J+H builds alone, for profiling runs). N > 1: the exchange ladder (p2p -> RCCL -> gloo host
+    # exchange, from --exchange on) — every rank takes the same decision, the line records why.
+    modes = ("single",) if world == 1 else LADDER[args.exchange]
+    mode, hinf, res, attempts = run_ladder(
+        modes,
+        setup=lambda m: make_handle(bos.BOS_PARTITION_SUBTREE, m),
+        run=lambda m, hi: check_and_time(m, hi, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup,
+                                         args.device_warmup) if args.steps > 0 or world > 1 else (0.0, []),
+        agree=lambda ok, why: agree_all(dist, torch, ok, why),
+        close=close_handle, log=log)
+    if mode is None:
+        fail_line(args, world, attempts, topo)
+        sys.exit(4)
+    S, info, ranks_seen = hinf
+    exchange = {"single": "single GPU", "p2p": "p2p", "rccl": "rccl", "gloo": "gloo"}[mode]
+    exchange_reason = None
+    if world > 1:
+        exchange_reason = {"p2p": "every rank mapped every other rank's mailbox (HIP IPC, peer access) and three GN "
+                                  "steps gave every rank the same chi^2",
+                           "rccl": "RCCL all-gathers; three GN steps gave every rank the same chi^2",
+                           "gloo": "host exchange over the gloo process group (no device-to-device path)"}[mode]
+        if args.exchange != mode:
+            exchange_reason += f" (--exchange {args.exchange} failed, see attempts)"
+    wall, stats = res
+    phase, jh_ms, gn_it_s = None, None, None
+    ranks_consistent = True if world > 1 and args.steps > 0 else None
+    per_rank = None
 
     def phases(stats):
         return {k: float(np.median([g[k] for g in stats])) for k in
@@ -474,59 +805,70 @@ def main():
         median over `steps` untimed GN iterations after the timed region, gathered to every rank:
         J+H, own subtrees (solver inputs, factorization and forward of this rank's subtrees, exchange-1
         pack), exchange-1 wait, replicated top (its factorization and solves) + own backward + pack,
-        exchange-2 wait, box-plus + status. Lists in rank order."""
-        init = h.get_state()
-        rows = []
-        for _ in range(steps):
-            gn_step(h, partition)
-            t = h.last_step_stamps().astype(np.int64)
-            d = lambda a, b: max(0.0, float(t[b] - t[a]) * 1e-5)   # ms (100 MHz ticks)
-            rows.append([d(0, 1), d(1, 4), d(4, 5), d(5, 6), d(6, 7), d(7, 3), d(0, 3)])
-        h.set_state(*init)
-        med = [float(x) for x in np.median(np.array(rows), axis=0)]
+        exchange-2 wait, box-plus + status. Lists in rank order; None on any rank's failure."""
+        med = None
+        try:
+            init = h.get_state()
+            rows = []
+            for _ in range(steps):
+                gn_step(h, partition, mode)
+                t = h.last_step_stamps().astype(np.int64)
+                d = lambda a, b: max(0.0, float(t[b] - t[a]) * 1e-5)   # ms (100 MHz ticks)
+                rows.append([d(0, 1), d(1, 4), d(4, 5), d(5, 6), d(6, 7), d(7, 3), d(0, 3)])
+            h.set_state(*init)
+            med = [float(x) for x in np.median(np.array(rows), axis=0)]
+        except Exception as e:
+            log(f"rank {rank}: per-rank breakdown: {e}")
         allr = [None] * world
         dist.all_gather_object(allr, med)
+        if any(r is None for r in allr):
+            return None
         keys = ("jh_ms", "own_subtrees_ms", "exchange1_wait_ms", "top_and_backward_ms", "exchange2_wait_ms",
                 "update_ms", "step_device_ms")
         return {k: [r[i] for r in allr] for i, k in enumerate(keys)}
 
-    # ---- the timed region: K GN iterations; the J+H inside them is the headline (K = 0: no GN steps,
-    # the J+H builds alone, for profiling runs)
-    wall, stats, phase, jh_ms, gn_it_s = 0.0, [], None, None, None
-    ranks_consistent = None
-    per_rank = None
     if args.steps > 0:
-        wall, stats = timed_steps(S, bos.BOS_PARTITION_SUBTREE, args.steps, args.warmup, args.device_warmup)
         phase = phases(stats)
-        if world > 1:   # every rank combines the same headers: the chi^2 of every step must agree bit for bit
-            mine = torch.tensor([g["chi2"] for g in stats], dtype=torch.float64)
-            lo, hi = mine.clone(), mine.clone()
-            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-            ranks_consistent = bool(torch.equal(lo, hi))
-            if not ranks_consistent:
-                log(f"error: rank {rank}: the ranks' per-step chi^2 differ (exchange {exchange})")
-                sys.exit(3)
         jh_ms = max_over_ranks(phase["t_linearize_ms"])      # the slowest rank's in-step J+H
         if world > 1:
             per_rank = rank_breakdown(S, partition=bos.BOS_PARTITION_SUBTREE)
         gn_it_s = args.steps / wall
         log(f"rank {rank}: {args.steps} GN steps in {wall * 1e3:.1f} ms ({gn_it_s:.0f} it/s); phases {phase}")
 
+    def local(fn, what):
+        """A secondary measurement on this rank: its value, or None (logged) if it raised."""
+        try:
+            return fn()
+        except Exception as e:
+            log(f"rank {rank}: {what}: {type(e).__name__}: {e}")
+            return None
+
+    def max_or_none(v):
+        """Max over ranks of a secondary measurement; None if any rank has none (collective-safe)."""
+        m = max_over_ranks(float("nan") if v is None else float(v))
+        return None if m != m else m
+
     # ---- other GN loops (the headline's timed region above is the reference for value)
     gn_c_loop, gn_batched = None, None
     init = S.get_state()
-    if args.steps > 0 and (world == 1 or args.exchange != "gloo"):
-        gn_c_loop = 1e3 / max_over_ranks(S.time_steps(min(args.steps, 50)))   # bos_step in a C loop
-        S.set_state(*init)
+    if args.steps > 0 and mode != "gloo":
+        c_ms = max_or_none(local(lambda: S.time_steps(min(args.steps, 50)), "C-loop steps"))   # bos_step in a C loop
+        gn_c_loop = 1e3 / c_ms if c_ms else None
+        local(lambda: S.set_state(*init), "state reset")
         barrier()
         tg = time.perf_counter()
-        last = S.step_n(args.batch)                       # executables/bearing_only_slam.cpp:95-98
-        S.synchronize()
+
+        def batch():
+            last = S.step_n(args.batch)                       # executables/bearing_only_slam.cpp:95-98
+            S.synchronize()
+            if last["solver_info"] != 0:
+                raise RuntimeError("non-positive pivot in a benchmarked GN step")
+            return True
+        ok = local(batch, "batched steps")
         barrier()
-        gn_batched = args.batch / max_over_ranks(time.perf_counter() - tg)
-        assert last["solver_info"] == 0, "non-positive pivot in a benchmarked GN step"
-        S.set_state(*init)
+        dt = max_or_none(time.perf_counter() - tg if ok else None)
+        gn_batched = args.batch / dt if dt else None
+        local(lambda: S.set_state(*init), "state reset")
 
     # ---- the drop-in caller's loop: proj02::Solver::step() through the C++ façade, as the reference's
     # executable calls it (executables/bearing_only_slam.cpp:93-99), then one read of solver.state
@@ -544,41 +886,51 @@ def main():
 
     # ---- the J+H alone: back to back (warm replay) and from cold caches (events)
     barrier()
-    replay_ms = S.time_linearize(args.replay_steps) if args.replay_steps > 0 else None
-    cold_ms = S.time_linearize(args.cold_steps, flush_caches=True) if args.cold_steps > 0 else None
-    replay_ms = max_over_ranks(replay_ms) if replay_ms else None
-    cold_ms = max_over_ranks(cold_ms) if cold_ms else None
+    replay_ms = max_or_none(local(lambda: S.time_linearize(args.replay_steps), "warm J+H")) \
+        if args.replay_steps > 0 else None
+    cold_ms = max_or_none(local(lambda: S.time_linearize(args.cold_steps, flush_caches=True), "cold J+H")) \
+        if args.cold_steps > 0 else None
 
     gn_other = None
     if world == 1 and not args.no_gn_other and args.steps > 0:   # the other multifrontal ordering
         other = "supernodal" if args.solver == "schur" else "schur"
-        S2 = bos.Solver(P, precision=precision, device=local_rank,
+        S2 = bos.Solver(P, precision=precision, device=device,
                         solver=bos.BOS_SOLVER_SUPERNODAL if other == "supernodal" else bos.BOS_SOLVER_SCHUR)
-        w2, st2 = timed_steps(S2, bos.BOS_PARTITION_SUBTREE, min(args.steps, 50), 1)
-        gn_other = {"solver": other, "gn_iters_per_s": min(args.steps, 50) / w2, "t_solve_ms": phases(st2)["t_solve_ms"]}
+        w2, st2, err2 = timed_steps(S2, bos.BOS_PARTITION_SUBTREE, min(args.steps, 50), 1, "single")
+        gn_other = {"solver": other, "gn_iters_per_s": min(args.steps, 50) / w2,
+                    "t_solve_ms": phases(st2)["t_solve_ms"]} if err2 is None else {"solver": other, "error": err2}
         S2.close()
 
-    # ---- N > 1: the north star's partition (observations by measurement order, all-reduce of H, b)
+    # ---- N > 1: the north star's partition (observations by measurement order, all-reduce of (H, b)),
+    # a secondary leg through its own ladder (RCCL all-reduce, else gloo on the host with fewer steps;
+    # a failure is reported in the line, never fatal to it)
     part_obs = None
     if world > 1 and not args.no_partition_other and args.steps > 0:
-        try:   # (a secondary leg: an RCCL failure here is reported in the line, not fatal to it)
-            S3, _, seen3 = make_handle(bos.BOS_PARTITION_OBSERVATIONS)
-        except bos.BosError as e:
-            log(f"rank {rank}: observations partition unavailable: {e}")
-            S3, part_obs = None, {"error": str(e)}
-    if world > 1 and not args.no_partition_other and args.steps > 0 and S3 is not None:
-        w3, st3 = timed_steps(S3, bos.BOS_PARTITION_OBSERVATIONS, args.steps, args.warmup)
-        ph3 = phases(st3)
-        jh3 = max_over_ranks(ph3["t_linearize_ms"])
-        ex3 = max_over_ranks(ph3["t_exchange_ms"])
-        part_obs = {"partition": "observations (measurement-order lane ranges, one all-reduce of (H, b) per "
-                                 "iteration, solve replicated)",
-                    "ranks_seen": seen3, "gn_iters_per_s": args.steps / w3, "gn_phase_ms": ph3,
-                    "jh_ms_max_rank": jh3, "jh_obs_per_s": nobs / (jh3 * 1e-3) if jh3 > 0 else None,
-                    "jh_plus_allreduce_obs_per_s": nobs / ((jh3 + ex3) * 1e-3) if jh3 + ex3 > 0 else None,
-                    "allreduce_bytes": int(info["num_block_values"] + 3 * P.NP + 2 * P.NL) *
-                    (4 if precision == bos.BOS_FP32 else 8)}
-        S3.close()
+        obs_modes = tuple(m for m in ("rccl", "gloo") if not any(t["mode"] == m and not t["ok"] for t in attempts))
+        obs_steps = lambda m: args.steps if m == "rccl" else min(args.steps, 5)
+        mode3, h3, res3, att3 = run_ladder(
+            obs_modes,
+            setup=lambda m: make_handle(bos.BOS_PARTITION_OBSERVATIONS, m),
+            run=lambda m, hi: check_and_time(m, hi, bos.BOS_PARTITION_OBSERVATIONS, obs_steps(m),
+                                             min(args.warmup, 2), 0),
+            agree=lambda ok, why: agree_all(dist, torch, ok, why),
+            close=close_handle, log=log)
+        if mode3 is None:
+            part_obs = {"error": "no exchange mode worked", "attempts": att3}
+        else:
+            w3, st3 = res3
+            ph3 = phases(st3)
+            jh3 = max_over_ranks(ph3["t_linearize_ms"])
+            ex3 = max_over_ranks(ph3["t_exchange_ms"])
+            part_obs = {"partition": "observations (measurement-order lane ranges, one all-reduce of (H, b) per "
+                                     "iteration, solve replicated)",
+                        "exchange": mode3, "attempts": att3, "steps": obs_steps(mode3),
+                        "ranks_seen": h3[2], "gn_iters_per_s": obs_steps(mode3) / w3, "gn_phase_ms": ph3,
+                        "jh_ms_max_rank": jh3, "jh_obs_per_s": nobs / (jh3 * 1e-3) if jh3 > 0 else None,
+                        "jh_plus_allreduce_obs_per_s": nobs / ((jh3 + ex3) * 1e-3) if jh3 + ex3 > 0 else None,
+                        "allreduce_bytes": int(info["num_block_values"] + 3 * P.NP + 2 * P.NL) *
+                        (4 if precision == bos.BOS_FP32 else 8)}
+            close_handle(h3)
 
     # ---- landmark triangulation on the device (slam/triangulation.cpp:65-74), config 3 (run last:
     # it re-estimates the landmarks of S)
@@ -646,7 +998,10 @@ def main():
             },
             "ranks_seen": ranks_seen,
             "ranks_consistent": ranks_consistent,
-            "exchange_decision": {"mode": exchange, "reason": exchange_reason} if world > 1 else None,
+            "exchange_decision": {"mode": exchange, "reason": exchange_reason, "attempts": attempts}
+            if world > 1 else None,
+            # every rank's device and visibility, rank 0's peer-access matrix (hipDeviceCanAccessPeer)
+            "topology": topo if world > 1 else None,
             # N > 1: per-rank phase medians (device stamps), rank order (rank_breakdown)
             "per_rank": per_rank,
             "devices": 1 if (args.same_device or world == 1) else world,

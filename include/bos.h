@@ -143,6 +143,11 @@ void bos_default_options(bos_options* opt);
 const char* bos_last_error(void);
 int bos_abi_version(void);
 int bos_device_count(void);
+/* Peer access between the visible devices (no reference counterpart: the multi-GPU bench records it
+ * beside its exchange decision). out[i * n + j] = 1 if device i can access device j's memory
+ * (hipDeviceCanAccessPeer; 1 on the diagonal), for n = min(capacity, bos_device_count()) devices;
+ * *n_out = that n. */
+int bos_device_peer_access(int32_t capacity, int32_t* out, int32_t* n_out);
 /* ncclGetUniqueId for world_size > 1: rank 0 creates it, the caller distributes the bytes */
 int bos_nccl_unique_id(void* out, int64_t len);
 
@@ -231,12 +236,14 @@ int bos_exchange_p2p_connect(struct bos_solver* s, const void* handles);
 /* Timing contract of the direct exchange. A rank's step waits on the device for the other ranks'
  * pushes (two waits per iteration); a wait gives up after `seconds` (default 2 s, so host-side gaps
  * of one rank between its bos_step calls — the first step's graph captures, logging, a pause —
- * stay far inside it) and then marks the step aborted: every later wait of that step returns at
- * once, the box-plus is skipped and bos_step returns BOS_ERR_SOLVER. An abort raised before
- * exchange 2 travels in exchange 2's header, so every rank skips that update together; a wait on
- * exchange 2 itself that times out skips the update on the ranks that timed out only, so after any
- * BOS_ERR_SOLVER from a sharded step the caller must bring all ranks back to one state
- * (bos_set_state on every rank) or destroy the handles. Once connected, bos_step_phase and
+ * stay far inside it) and then marks the step aborted: every later exchange wait of that step
+ * returns at once, the box-plus is skipped and bos_step returns BOS_ERR_SOLVER. A local solver
+ * stall (a dataflow dependency wait that timed out) aborts the step too but does not shorten the
+ * exchange waits, so that rank still receives its peers' current exchange 2. An abort raised before
+ * exchange 2 travels in exchange 2's header, so every rank skips that update together and reports
+ * BOS_ERR_SOLVER for the same step; a wait on exchange 2 itself that times out skips the update on
+ * the ranks that timed out only, so after any BOS_ERR_SOLVER from a sharded step the caller must
+ * bring all ranks back to one state (bos_set_state on every rank) or destroy the handles. Once connected, bos_step_phase and
  * bos_exchange_download / _upload return BOS_ERR_INVALID (the exchange is the handle's own). Every
  * rank must finish stepping (its last bos_step returned on every rank, e.g. a barrier) before any
  * rank calls bos_destroy: the peers' pushes write into this rank's mailbox. */

@@ -39,7 +39,8 @@ ABI_VERSION = 3
 
 # every symbol declared in include/bos.h and include/bos_host.h
 EXPORTED_SYMBOLS = [
-    "bos_default_options", "bos_last_error", "bos_abi_version", "bos_device_count", "bos_nccl_unique_id",
+    "bos_default_options", "bos_last_error", "bos_abi_version", "bos_device_count", "bos_device_peer_access",
+    "bos_nccl_unique_id",
     "bos_create", "bos_destroy", "bos_set_kernel_threshold", "bos_set_damping_factor", "bos_step", "bos_step_n",
     "bos_linearize", "bos_linearize_async", "bos_synchronize", "bos_system_info_get", "bos_export_system",
     "bos_get_state", "bos_set_state", "bos_get_last_dx",
@@ -132,6 +133,7 @@ def lib():
         "bos_last_error": (ctypes.c_char_p, []),
         "bos_abi_version": (ctypes.c_int, []),
         "bos_device_count": (ctypes.c_int, []),
+        "bos_device_peer_access": (ctypes.c_int, [ctypes.c_int32, _ip, _ip]),
         "bos_nccl_unique_id": (ctypes.c_int, [vp, ctypes.c_int64]),
         "bos_create": (ctypes.c_int, [ctypes.POINTER(bos_problem), ctypes.POINTER(bos_options), ctypes.POINTER(vp)]),
         "bos_destroy": (ctypes.c_int, [vp]),
@@ -219,6 +221,16 @@ def _ptr(a, ct):
 
 def device_count() -> int:
     return lib().bos_device_count()
+
+
+def device_peer_access(capacity: int = 64) -> list:
+    """Peer-access matrix of the visible devices (hipDeviceCanAccessPeer; 1 on the diagonal)."""
+    out = np.zeros(capacity * capacity, dtype=np.int32)
+    n = np.zeros(1, dtype=np.int32)
+    _check(lib().bos_device_peer_access(capacity, _ptr(out, ctypes.c_int32), _ptr(n, ctypes.c_int32)),
+           "bos_device_peer_access")
+    k = int(n[0])
+    return out[:k * k].reshape(k, k).tolist()
 
 
 class Problem:

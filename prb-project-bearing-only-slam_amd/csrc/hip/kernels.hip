@@ -764,9 +764,10 @@ template <typename T> __global__ __launch_bounds__(256) void triangulate_kernel(
 }
 
 // lanes q < world of the block poll sender q's flag in this rank's mailbox until it equals the
-// iteration's epoch (or mark the step aborted after w.timeout_ticks, or give up at once when the
-// step is already marked aborted: a launch's blocks, and the step's later waits, then drain in one
-// timeout); then the whole block acquires
+// iteration's epoch (or mark the step aborted, kStepAbort | kExTimeout, after w.timeout_ticks, or give
+// up at once when an exchange wait of this step already timed out: a launch's blocks, and the step's
+// later waits, then drain in one timeout; a local solver stall alone does not end the wait, so the
+// rank still receives its peers' current headers); then the whole block acquires
 __device__ __forceinline__ void p2p_wait_block(const P2PWait& w) {
     const int q = threadIdx.x;
     if (q < w.world) {
@@ -775,11 +776,11 @@ __device__ __forceinline__ void p2p_wait_block(const P2PWait& w) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (uint32_t it = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++it) {
             if (__builtin_amdgcn_s_memrealtime() - t0 > w.timeout_ticks) {
-                atomicOr(w.info, kStepAbort);
+                atomicOr(w.info, kStepAbort | kExTimeout);
                 break;
             }
             if ((it & 63) == 63 &&
-                (__hip_atomic_load(w.info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStepAbort))
+                (__hip_atomic_load(w.info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kExTimeout))
                 break;
             __builtin_amdgcn_s_sleep(1);
         }
@@ -898,20 +899,20 @@ __global__ void shard_combine_kernel(const double* recv1, int64_t c1, const doub
         abort_bits |= *local_info & kStepAbort;
         // zero_info: the gathering exchange-2 push sent the whole word without zeroing it (its blocks
         // read it concurrently), so it is zeroed here, after every block has read it
-        *local_info = zero_info ? 0 : (*local_info & ~kStepAbort);
+        *local_info = zero_info ? 0 : (*local_info & ~(kStepAbort | kExTimeout));
     }
     for (int q = 0; q < world; ++q) {
         chi += recv1[q * c1];
         nr += (long long)recv1[q * c1 + 1];
         m = nan_max(m, recv2[q * c2]);
         const int32_t inf = (int32_t)recv2[q * c2 + 1];
-        piv += inf & ~kStepAbort;
+        piv += inf & ~(kStepAbort | kExTimeout);
         abort_bits |= inf & kStepAbort;
     }
     out->chi2 = chi + chi_const;
     out->n_robust = (int32_t)nr + nrob_const;
     out->max_dx = m;
-    out->info = (int32_t)min(piv, (long long)(kStepAbort - 1)) | abort_bits;
+    out->info = (int32_t)min(piv, (long long)(kExTimeout - 1)) | abort_bits;
     out->aborted |= abort_bits;
     out->stamp[3] = __builtin_amdgcn_s_memrealtime();
     out->seq += 1;

@@ -112,6 +112,11 @@ template <typename T> struct UpdateParams {
 // Solver status bit: the factorization's results are invalid (a dataflow launch timed out,
 // multifrontal.hpp kMfStall); the box-plus then leaves the state untouched and bos_step fails.
 constexpr int32_t kStepAbort = 1 << 30;
+// Set with kStepAbort by a direct-exchange wait that timed out (a peer's data never arrived): the
+// step's later exchange waits then give up at once. A local solver stall (kStepAbort alone) does not
+// shorten them: the rank still waits (bounded) for its peers' exchange 2, so every rank combines the
+// same, current headers and reports the failed step alike.
+constexpr int32_t kExTimeout = 1 << 29;
 
 // End-of-iteration summary, read back by the host in one copy.
 struct StepStatus {

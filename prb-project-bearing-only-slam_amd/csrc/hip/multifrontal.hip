@@ -294,6 +294,145 @@ __global__ __launch_bounds__(kMfBlock) void mf_forward_level(const MfArgs a) {
     }
 }
 
+__device__ __forceinline__ double readlane_d(double x, int l);
+__device__ __forceinline__ double rsqrt_nr(double d);
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// Larger fronts (kMfWaveMaxM < m <= kBlkMaxM: config 2's separators, m ~ 60-100): one 256-thread
+// workgroup per front, the whole m x m front in LDS (column-major, leading dimension m, as the plan's
+// amap_dst), a blocked right-looking partial Cholesky of its k columns fused with the forward step.
+// Per panel of kBlkNb columns: wave 0 factors the panel with its rows in registers (two rows per lane,
+// pivots broadcast by v_readlane, no barrier inside the panel) and carries the forward elimination
+// along; then all four waves update the trailing lower triangle, A22 -= L21 L21^T, in 16 x 16 tiles
+// on f64 MFMA (v_mfma_f64_16x16x4f64, the fold's W W^T pattern). The children's u-vectors are
+// extend-added with their update matrices (no separate forward launch). mf_factor_level (with
+// mf_forward_level) kept the front in global scratch above 90 rows and took ~140 us per level launch
+// at config 2; it remains for m > kBlkMaxM (fallback plans).
+constexpr int kBlkMaxM = 128, kBlkNb = 16;
+
+__global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int s = a.level[blockIdx.x];
+    const int k = a.k[s], r = a.r[s], m = k + r;   // m <= kBlkMaxM (mf_create / the launch check it)
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    double* F = lds;                  // m x m, column-major
+    double* w = lds + m * m;          // right-hand side, then the forward step's results
+    const int c0 = a.col0[s];
+    for (int e = tid; e < m * m; e += kMfBlock) F[e] = 0.0;
+    for (int i = tid; i < m; i += kMfBlock) w[i] = i < k ? a.x[c0 + i] : 0.0;
+    __syncthreads();
+    for (int q = a.amap_ptr[s] + tid; q < a.amap_ptr[s + 1]; q += kMfBlock) F[a.amap_dst[q]] = a.A[a.amap_src[q]];
+    __syncthreads();
+    // children one at a time (deterministic): update matrix into F, u-vector into w
+    for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {
+        const int c = a.child[ci];
+        const int rc = a.r[c];
+        const int32_t* map = a.rmap + a.rmap_off[c];
+        const double* Uc = a.U + a.U_off[c];
+        for (int j = wave; j < rc; j += kMfBlock / 64) {
+            const int pj = map[j] * m;
+            const double* uj = Uc + pk(j, j, rc) - j;
+            for (int i = j + lane; i < rc; i += 64) F[map[i] + pj] += uj[i];
+        }
+        const double* uc = a.u + a.u_off[c];
+        for (int t = tid; t < rc; t += kMfBlock) w[map[t]] += uc[t];
+        __syncthreads();
+    }
+    double* Ls = a.L + a.L_off[s];
+    int nbad = 0;
+    for (int p0 = 0; p0 < k; p0 += kBlkNb) {
+        const int nb = min(kBlkNb, k - p0);
+        if (wave == 0) {
+            // lane l holds rows p0 + l and p0 + 64 + l of the panel's columns (m - p0 <= 128 rows)
+            const int ia = p0 + lane, ib = p0 + 64 + lane;
+            const bool va = ia < m, vb = ib < m;
+            double pa[kBlkNb], pb[kBlkNb];
+#pragma unroll
+            for (int c = 0; c < kBlkNb; ++c) {
+                pa[c] = va && c < nb ? F[ia + (p0 + c) * m] : 0.0;
+                pb[c] = vb && c < nb ? F[ib + (p0 + c) * m] : 0.0;
+            }
+            double wa = va ? w[ia] : 0.0, wb = vb ? w[ib] : 0.0;
+#pragma unroll
+            for (int j = 0; j < kBlkNb; ++j) {
+                if (j < nb) {   // uniform
+                    double d = readlane_d(pa[j], j);
+                    const bool bad = !(d > 0.0);
+                    nbad += bad;
+                    d = bad ? 1e-300 : d;
+                    const double inv = rsqrt_nr(d), ljj = d * inv;
+                    // L[i, p0 + j]; rows above the pivot (lanes < j) hold upper entries: zero
+                    const double la = lane < j ? 0.0 : lane == j ? ljj : pa[j] * inv;
+                    const double lb = pb[j] * inv;
+                    pa[j] = la;
+                    pb[j] = lb;
+                    const double y = readlane_d(wa, j) * inv;   // forward step: y_j = w_j / L_jj
+                    wa = lane == j ? y : lane > j ? fma(-la, y, wa) : wa;
+                    wb = fma(-lb, y, wb);
+#pragma unroll
+                    for (int c = j + 1; c < kBlkNb; ++c) {
+                        if (c < nb) {
+                            const double lc = readlane_d(la, c);   // L[p0 + c, p0 + j]
+                            pa[c] = fma(-la, lc, pa[c]);
+                            pb[c] = fma(-lb, lc, pb[c]);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kBlkNb; ++c) {
+                if (c < nb) {
+                    if (va) {
+                        F[ia + (p0 + c) * m] = pa[c];
+                        ST_L(Ls, ia + (p0 + c) * m, pa[c]);
+                    }
+                    if (vb) {
+                        F[ib + (p0 + c) * m] = pb[c];
+                        ST_L(Ls, ib + (p0 + c) * m, pb[c]);
+                    }
+                }
+            }
+            if (va) w[ia] = wa;
+            if (vb) w[ib] = wb;
+        }
+        __syncthreads();
+        // trailing lower triangle, rows / columns [t0, m): 16 x 16 tiles (bi >= bj) over the waves
+        const int t0 = p0 + nb, nbt = (m - t0 + 15) >> 4, ntiles = nbt * (nbt + 1) / 2;
+        for (int q = wave; q < ntiles; q += kMfBlock / 64) {
+            int bi = 0;
+            while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+            const int bj = q - bi * (bi + 1) / 2;
+            const int ra = t0 + 16 * bi + (lane & 15), rb = t0 + 16 * bj + (lane & 15);
+            dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+            for (int kk = 0; kk < nb; kk += 4) {
+                const int cc = kk + (lane >> 4);
+                const double av = cc < nb && ra < m ? F[ra + (p0 + cc) * m] : 0.0;
+                const double bv = cc < nb && rb < m ? F[rb + (p0 + cc) * m] : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+            const int col = t0 + 16 * bj + (lane & 15);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = t0 + 16 * bi + (lane >> 4) + 4 * e;
+                if (row < m && row >= col) F[row + col * m] -= acc[e];
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && nbad) atomicAdd(a.info, nbad);
+    // the update matrix (packed lower r x r), the forward results: own dofs to x, the rest to u
+    double* Us = a.U + a.U_off[s];
+    for (int j = wave; j < r; j += kMfBlock / 64) {
+        double* uj = Us + pk(j, j, r) - j;
+        const double* fj = F + (k + (k + j) * m);
+        for (int i = j + lane; i < r; i += 64) uj[i] = fj[i];
+    }
+    for (int i = tid; i < m; i += kMfBlock) {
+        if (i < k) a.x[c0 + i] = w[i];
+        else a.u[a.u_off[s] + (i - k)] = w[i];
+    }
+}
+
 // backward substitution L^T x = y for one level (top-down): the rows below the supernode are
 // ancestors' dofs whose solution is already final in x
 __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
@@ -941,8 +1080,10 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
         if (c0 == 8) cstamp(cst, s, 6);
 #endif
         if (c0 < m) {
-            // branch-free: every lane reads a position of the LDS front (for a row i < m, pk32(i, c, m)
-            // < np for every c < m + 8), the group's eight reads under one wait. A predicated read per
+            // branch-free: every lane reads a position of the LDS front (the column clamped to m - 1:
+            // for a row i < m and a column c' < m, 0 <= pk32(i, c', m) < np, also above the diagonal;
+            // unclamped, m <= 3 would give negative positions), the group's eight reads
+            // under one wait. A predicated read per
             // entry compiled to an exec-mask branch with its own wait each (~2 500 cycles for the rows
             // of a 24-row front); the empty asm keeps the reads out of such branches. Entries above
             // the diagonal, of rows >= m (copies of row m - 1) and of columns >= m are scratch that no
@@ -953,7 +1094,7 @@ __device__ __forceinline__ void factor_front_reg(const MfArgs& a, int s, double*
             // profiles/r05_rows_all_at_once_ab.txt.)
             double v[8];
 #pragma unroll
-            for (int c = c0; c < c0 + 8; ++c) v[c - c0] = c < MAXM ? F[pk32(lrow, c, m)] : 0.0;
+            for (int c = c0; c < c0 + 8; ++c) v[c - c0] = c < MAXM ? F[pk32(lrow, min(c, m - 1), m)] : 0.0;
             asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
                          "+v"(v[7]));
 #pragma unroll
@@ -1409,8 +1550,10 @@ struct Prog {
     int id = 0;                     // flow id (1: own / everything, 2: top)
     std::vector<int32_t> ptr;       // (level l, class c) = list[ptr[l * kClasses + c], ...)
     std::vector<int> lds_factor, lds_fwd, lds_bwd;   // per (level, class): dynamic LDS bytes
+    std::vector<int> lds_blk;       // per level: mf_factor_blk's LDS for its class-4 fronts, 0 if one is > kBlkMaxM
     int32_t* list = nullptr;
     int flow_lev0 = 0, n_flow_factor = 0;
+    bool first_waited = false;      // the factor flow's first front has its parent in the same flow
     int32_t* order_factor = nullptr;
     bool flow_solve = false;
     int solve_lev0 = 0, n_flow_solve = 0, lds_bwd_flow = 0;
@@ -1461,6 +1604,7 @@ constexpr int kSolveWideLevel = BOS_MF_SOLVE_WIDE;
 constexpr int kFactorWideLevel = BOS_MF_FACTOR_WIDE;
 struct MfDevice {
     int nlevels = 0, nsuper = 0, ncu = 256;
+    bool blk = false;             // mf_factor_blk may take its (up to 132 KB of) dynamic LDS
     // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
     // the level's other classes
     hipStream_t side = nullptr;
@@ -1514,6 +1658,7 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
     const int L = F.nlevels;
     P.lds_factor.assign(L * kClasses, 0); P.lds_fwd.assign(L * kClasses, 0); P.lds_bwd.assign(L * kClasses, 0);
     P.ptr.assign(L * kClasses + 1, 0);
+    P.lds_blk.assign(L, 0);
     auto mine = [&](int s) { return sel[s] == id; };
     std::vector<int32_t> lst;
     for (int l = 0; l < L; ++l)
@@ -1528,6 +1673,7 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
                     P.lds_bwd[lc] = std::max(P.lds_bwd[lc], (2 * k + (m - k) + m * k) * 8);
                 } else {
                     if (m <= kLdsCapM) P.lds_factor[lc] = std::max(P.lds_factor[lc], m * m * 8);
+                    P.lds_blk[l] = P.lds_blk[l] < 0 || m > kBlkMaxM ? -1 : std::max(P.lds_blk[l], (m * m + m) * 8);
                     P.lds_fwd[lc] = std::max(P.lds_fwd[lc], m * 8);
                     P.lds_bwd[lc] = std::max(P.lds_bwd[lc], 2 * k * 8);
                 }
@@ -1545,6 +1691,7 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
             std::stable_sort(lst.begin() + P.ptr[lc], lst.end(), [&](int x, int y) { return cost(x) > cost(y); });
             P.ptr[lc + 1] = (int32_t)lst.size();
         }
+    for (int l = 0; l < L; ++l) P.lds_blk[l] = std::max(P.lds_blk[l], 0);
     auto mine_in_level = [&](int l) {
         int c = 0;
         for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) c += mine(F.level[q]);
@@ -1586,6 +1733,7 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
         fid_f[s] = (int8_t)id;
     }
     P.n_flow_factor = (int)ofac.size();
+    P.first_waited = !ofac.empty() && F.parent[ofac[0]] >= 0 && fid_f[F.parent[ofac[0]]] == id;
     P.solve_lev0 = std::min(2, L);
     while (P.solve_lev0 < L && mine_in_level(P.solve_lev0) >= kSolveWideLevel) ++P.solve_lev0;
     for (int q = F.level_ptr[P.solve_lev0]; q < F.level_ptr[L]; ++q) {
@@ -1634,6 +1782,11 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         int dev = 0, ncu = 0;
         if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
             d->ncu = ncu;
+        // a front of kBlkMaxM rows takes 129 KB of LDS (160 KB per CU on gfx950)
+        const int blk_lds = (kBlkMaxM * kBlkMaxM + kBlkMaxM) * 8;
+        d->blk = hipFuncSetAttribute((const void*)mf_factor_blk, hipFuncAttributeMaxDynamicSharedMemorySize, blk_lds) ==
+                 hipSuccess;
+        if (!d->blk) (void)hipGetLastError();
     }
     // program of every supernode: 1 = own (everything on one GPU), 2 = top, 0 = another rank's
     std::vector<int8_t> sel(F.nsuper, 1), fid_f(F.nsuper, 0), fid_b(F.nsuper, 0);
@@ -1784,11 +1937,15 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
         if ((n = P.count(l, 3)) && !fork)
             hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
         if (fork && (e = hipStreamWaitEvent(s, d->ev_join, 0)) != hipSuccess) return e;
-        if ((n = P.count(l, 4))) {   // large fronts: workgroup factorization, then their forward step
-            hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), P.lds_factor[l * kClasses + 4], s,
-                               d->args(P, l, 4, A, x));
-            hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), P.lds_fwd[l * kClasses + 4], s,
-                               d->args(P, l, 4, A, x));
+        if ((n = P.count(l, 4))) {   // large fronts: workgroup factorization (blocked, MFMA; fused forward step)
+            if (d->blk && P.lds_blk[l] > 0) {
+                hipLaunchKernelGGL(mf_factor_blk, dim3(n), dim3(kMfBlock), P.lds_blk[l], s, d->args(P, l, 4, A, x));
+            } else {   // a front above kBlkMaxM rows in the level: the unblocked kernels, then the forward step
+                hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), P.lds_factor[l * kClasses + 4], s,
+                                   d->args(P, l, 4, A, x));
+                hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), P.lds_fwd[l * kClasses + 4], s,
+                                   d->args(P, l, 4, A, x));
+            }
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
@@ -1861,7 +2018,9 @@ double* mf_update_ptr(const MfDevice* d) { return d->U; }
 double* mf_uvec_ptr(const MfDevice* d) { return d->u; }
 
 hipError_t mf_debug_skip_next_front(MfDevice* d, hipStream_t s) {
-    if (d->prog[0].n_flow_factor == 0) return hipErrorInvalidValue;
+    // only where a front of the same launch waits for the skipped one (otherwise nothing would notice
+    // the skip and the step would use the front's previous outputs)
+    if (d->prog[0].n_flow_factor == 0 || !d->prog[0].first_waited) return hipErrorInvalidValue;
     static const int one = 1;
     return hipMemcpyAsync(d->tickets, &one, sizeof(int), hipMemcpyHostToDevice, s);
 }

@@ -1062,6 +1062,27 @@ int bos_device_count(void) {
     return n;
 }
 
+int bos_device_peer_access(int32_t capacity, int32_t* out, int32_t* n_out) {
+    if (!out || !n_out || capacity < 0) return fail(BOS_ERR_INVALID, "bad argument");
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess) {
+        (void)hipGetLastError();
+        nd = 0;
+    }
+    const int n = std::min<int>(nd, capacity);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            int ok = i == j;
+            if (i != j && hipDeviceCanAccessPeer(&ok, i, j) != hipSuccess) {
+                (void)hipGetLastError();
+                ok = 0;
+            }
+            out[(int64_t)i * n + j] = ok ? 1 : 0;
+        }
+    *n_out = n;
+    return BOS_OK;
+}
+
 void bos_default_options(bos_options* o) {
     if (!o) return;
     std::memset(o, 0, sizeof(*o));
@@ -1695,7 +1716,8 @@ int bos_debug_inject_stall(bos_solver* s) {
     if (!uses_mf(s)) return fail(BOS_ERR_UNSUPPORTED, "no dataflow launch in this solver");
     HIP_TRY(hipSetDevice(s->device));
     const hipError_t e = bos::dev::mf_debug_skip_next_front(s->mf, s->stream);
-    if (e == hipErrorInvalidValue) return fail(BOS_ERR_UNSUPPORTED, "no dataflow launch in this plan");
+    if (e == hipErrorInvalidValue)
+        return fail(BOS_ERR_UNSUPPORTED, "no dataflow launch in this plan whose first front another front of it waits for");
     HIP_TRY(e);
     return BOS_OK;
 }

@@ -56,6 +56,24 @@ int64_t count_mismatches(const proj02::State& st, const std::vector<double>& pos
     return bad;
 }
 
+// the façade's state as read (a copy: a later solver.handle() marks the state stale and the next
+// read would download it again)
+void snapshot(const proj02::State& st, std::vector<double>& pose, std::vector<double>& lm) {
+    const proj02::NEPoseVector& P = st.poses_vec();
+    const proj02::LMPosVector& L = st.landmarks_vec();
+    pose.resize(3 * P.size());
+    lm.resize(2 * L.size());
+    for (size_t i = 0; i < P.size(); ++i) {
+        pose[3 * i] = P[i].x;
+        pose[3 * i + 1] = P[i].y;
+        pose[3 * i + 2] = P[i].theta;
+    }
+    for (size_t j = 0; j < L.size(); ++j) {
+        lm[2 * j] = L[j].x;
+        lm[2 * j + 1] = L[j].y;
+    }
+}
+
 bool valid(const bos_problem* pb) {
     return pb && pb->num_poses > 0 && pb->num_landmarks > 0 && pb->pose_xyt && pb->landmark_xy &&
            (pb->num_bearings == 0 || (pb->bearing_pose && pb->bearing_landmark && pb->bearing_z)) &&
@@ -85,12 +103,20 @@ int bos_time_facade_steps(const bos_problem* pb, const bos_options* options, int
         *ms_per_step = std::chrono::duration<double, std::milli>(t1 - t0).count() / n;
         if (ms_state_read) *ms_state_read = std::chrono::duration<double, std::milli>(t2 - t1).count() + 0 * sum;
         if (mismatches) {
+            // the values that timed read produced, copied before solver.handle() (which marks the
+            // façade's state stale, so reading it afterwards would download the device state again and
+            // compare it with itself), against the device state
+            std::vector<double> fpose, flm;
+            snapshot(shown, fpose, flm);
             const size_t NP = (size_t)pb->num_poses, NL = (size_t)pb->num_landmarks;
             std::vector<double> pose(3 * NP), lm(2 * NL);
-            const proj02::State& st = solver.state;
-            bos_solver* h = solver.handle();            // (marks the façade's state stale: re-read below)
+            if (fpose.size() != pose.size() || flm.size() != lm.size()) return ffail(BOS_ERR_INVALID, "facade state size");
+            bos_solver* h = solver.handle();
             if (bos_get_state(h, pose.data(), lm.data()) != BOS_OK) return BOS_ERR_DEVICE;
-            *mismatches = count_mismatches(st, pose, lm);
+            int64_t bad = 0;
+            for (size_t i = 0; i < pose.size(); ++i) bad += std::memcmp(&fpose[i], &pose[i], sizeof(double)) != 0;
+            for (size_t i = 0; i < lm.size(); ++i) bad += std::memcmp(&flm[i], &lm[i], sizeof(double)) != 0;
+            *mismatches = bad;
         }
         if (ms_per_step_capi) {                         // the same handle, bos_step in a C loop
             const int rc = bos_time_steps(solver.handle(), n, ms_per_step_capi);

@@ -1,6 +1,8 @@
 // proj02::State — mirror of framework/state.hpp:15-54 (no drawing; OpenCV is out of scope).
 #pragma once
 
+#include <atomic>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -74,16 +76,31 @@ class State {
     bool take_host_writes() { const bool w = host_written_; host_written_ = false; return w; }
 
   private:
+    // The first read after a step downloads the values. Const reads from several threads are safe
+    // (one of them downloads under the lock; the others wait for it), and stale_ is cleared only
+    // once the download succeeded, so a read whose download throws leaves the next read to retry
+    // instead of returning the pre-step values. A write (non-const accessor) while
+    // another thread reads is a data race, as on any std::vector.
     void materialize() const {
+        if (!stale_) return;
+        std::lock_guard<std::mutex> g(pull_lock_.m);
         if (stale_) {
-            stale_ = false;
             source_->pull_state(poses, landmarks);
+            stale_ = false;
         }
     }
     void touch() { materialize(); host_written_ = true; }
 
+    // a mutex that copies and assigns as a fresh one (State itself is copyable, as the reference's)
+    struct PullLock {
+        std::mutex m;
+        PullLock() = default;
+        PullLock(const PullLock&) {}
+        PullLock& operator=(const PullLock&) { return *this; }
+    };
+    mutable PullLock pull_lock_;
     StateSource* source_ = nullptr;
-    mutable bool stale_ = false;
+    mutable std::atomic<bool> stale_{false};
     bool host_written_ = false;
     // mutable: a const read may refresh them from the source
     mutable NEPoseVector poses;

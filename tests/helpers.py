@@ -74,7 +74,14 @@ def wrap_signs_from_gpu(P, b_gpu, kt=1.0):
     ks, e = knife_edge_bearings(P)
     if len(ks) == 0:
         return None
-    assert len(ks) <= 10, len(ks)
+    # The only bearings whose sign may be taken from the GPU are the sole observations of their
+    # landmark (triangulated onto their own ray); on the reference dataset exactly
+    # the three on landmarks 69, 112 and 114 (the set cannot grow silently). Their sign
+    # is parity-unpinned.
+    counts = np.bincount(P.b_lm, minlength=P.NL)
+    assert np.all(counts[P.b_lm[ks]] == 1), [int(k) for k in ks if counts[P.b_lm[k]] != 1]
+    if getattr(P, "lm_ids", None) is not None and P.NP == 301 and P.NL == 141:
+        assert sorted(int(P.lm_ids[P.b_lm[k]]) for k in ks) == [69, 112, 114], ks
     Q = to_oracle(P)
     with O.literal():
         lin = O.linearize(Q, kernel_threshold=kt)

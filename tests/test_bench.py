@@ -63,3 +63,36 @@ def test_traffic_only_from_a_profile_of_this_build(tmp_path):
     assert "another libbos.so" in why["warm"]
     t, why = bench.traffic_from_profile(bos.BOS_FP64, str(tmp_path))
     assert t == {"instep": None, "warm": None}
+
+
+LADDER_CASES = [
+    # (world, failures, expected mode, expected failed attempts)
+    (2, "", "p2p", []),
+    (2, "p2p:setup@1", "rccl", ["p2p"]),
+    (2, "p2p:run@0,rccl:setup@*", "gloo", ["p2p", "rccl"]),
+    (8, "p2p:run@5", "rccl", ["p2p"]),
+    (8, "p2p:setup@3,rccl:run@7", "gloo", ["p2p", "rccl"]),
+    (8, "p2p:setup@*,rccl:run@1,gloo:run@6", None, ["p2p", "rccl", "gloo"]),
+]
+
+
+@pytest.mark.parametrize("world,fails,mode,failed", LADDER_CASES)
+def test_exchange_ladder_every_rank_takes_the_same_decision(world, fails, mode, failed):
+    """the N > 1 bench falls back p2p -> RCCL -> gloo host exchange when a mode
+    fails on any rank (at setup or in its run), every rank agreeing on each step (gloo collectives),
+    and rank 0 prints a line whatever fails, naming the failing ranks' reasons. The stand-in modes
+    fail at the listed rank and stage and make the real run's collective calls after the failure."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(world), "--check-launch", "--check-ladder", fails],
+                       capture_output=True, text=True, timeout=600, env=_env())
+    assert r.returncode == (0 if mode else 4), r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["ranks_seen"] == world
+    d = line["exchange_decision"]
+    assert d["mode"] == mode
+    assert [a["mode"] for a in d["attempts"] if not a["ok"]] == failed
+    for a in d["attempts"]:
+        if not a["ok"]:   # the reason of every rank that failed, and only of those
+            spec = [f for f in fails.split(",") if f.startswith(a["mode"] + ":")][0]
+            who = spec.split("@")[1]
+            assert set(a["why"]) == ({str(q) for q in range(world)} if who == "*" else {who}), a
+            assert a["stage"] == spec.split(":")[1].split("@")[0]

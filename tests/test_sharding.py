@@ -421,3 +421,90 @@ def test_two_processes_p2p_exchange():
         assert res[0][4][it]["chi2"] == res[1][4][it]["chi2"], it
         assert abs(res[0][4][it]["chi2"] - one[it]["chi2"]) <= 1e-12 * one[it]["chi2"], it
         assert res[0][4][it]["solver_info"] == 0 and res[1][4][it]["solver_info"] == 0
+
+
+def _abort_world(case):
+    import bos
+    # the stall hook skips the first front of the rank's own factor flow: on the config-3 world that
+    # front's parent is in the same flow and waits for it (at config 2 a rank's flow holds only its
+    # subtree roots, whose parents are in the replicated top, and nothing would wait)
+    if case == "stall":
+        return bos.synthetic(100000, 200000, 10, seed=0xB05EED01 + 3)
+    return bos.synthetic(1000, 2000, 20)
+
+
+def _gpu_p2p_abort_worker(rank, world, port, q, case):
+    try:
+        _paths()
+        import bos
+        bos.lib()
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        P = _abort_world(case)
+        S = bos.Solver(P, solver=bos.BOS_SOLVER_SCHUR, device=0, rank=rank, world_size=world)
+        handles = [None] * world
+        dist.all_gather_object(handles, S.p2p_handle())
+        S.p2p_connect(handles)
+        init = S.get_state()
+        S.step()   # first step: the graph is captured outside the short timeout below
+        S.set_state(*init)
+        S.synchronize()
+        dist.barrier()
+        before = S.get_state()
+        if case == "timeout":
+            # rank 1 starts its step 0.5 s late against a 0.1 s wait bound: rank 0's exchange-1 wait
+            # times out; rank 1's step then finds rank 0's abort in exchange 2's header
+            S.set_exchange_timeout(0.1)
+            if rank == 1:
+                time.sleep(0.5)
+        elif rank == 1:   # a local solver stall on rank 1 (a dataflow front skipped)
+            S.debug_inject_stall()
+        err = None
+        try:
+            S.step()
+        except bos.BosError as e:
+            err = str(e)
+        S.synchronize()
+        after = S.get_state()
+        untouched = bool(np.array_equal(before[0], after[0]) and np.array_equal(before[1], after[1]))
+        dist.barrier()
+        # back to one state on every rank, the default wait bound, then 3 steps as the one-GPU run
+        S.set_exchange_timeout(2.0)
+        S.set_state(*init)
+        S.synchronize()
+        dist.barrier()
+        stats = [S.step() for _ in range(3)]
+        pose, lm = S.get_state()
+        owner = S.node_owner()
+        dist.barrier()
+        S.close()
+        dist.destroy_process_group()
+        q.put((rank, pose, lm, owner, stats, err, untouched, None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, None, None, None, None, None, None, repr(e)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["timeout", "stall"])
+def test_two_processes_p2p_abort_contract(case):
+    """the direct exchange's abort contract (include/bos.h, bos_set_exchange_timeout).
+    Two ranks on the one GPU; one step fails — rank 1 starts 0.5 s late against a 0.1 s wait bound
+    (rank 0's exchange wait times out), or rank 1's factorization stalls (bos_debug_inject_stall).
+    Both ranks must report BOS_ERR_SOLVER for that step with their state untouched (a local stall no
+    longer ends the exchange-2 wait early, so the stalled rank combines its peer's current header),
+    and after bos_set_state on every rank the next 3 steps equal the one-GPU run bit for bit."""
+    import bos
+    world, iters = 2, 3
+    res = _spawn(_gpu_p2p_abort_worker, world, (case,), timeout=300)
+    for r in res:
+        assert r[5] is not None and "aborted" in r[5], (case, r[0], r[5])
+        assert r[6], (case, r[0], "state changed by the failed step")
+    P = _abort_world(case)
+    pm, lm_ = _merge(P, [(r[1], r[2]) for r in res], res[0][3])
+    (p1, l1), st1 = _run_one(P, iters, bos.BOS_FP64)
+    assert np.array_equal(pm, p1) and np.array_equal(lm_, l1)
+    for it in range(iters):
+        assert res[0][4][it]["chi2"] == res[1][4][it]["chi2"], it
+        assert res[0][4][it]["solver_info"] == 0 and res[1][4][it]["solver_info"] == 0

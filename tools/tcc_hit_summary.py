@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """L2 (TCC) hit rate of the J+H kernel in the GN step against back-to-back builds (diagnostics;
 VERDICT r04 item 4: where the in-step build's extra time comes from). Reads two rocprofv3 --pmc
-passes of TCC_HIT_sum TCC_MISS_sum (tools/gpu_r05_tcc.sh) and prints per-launch hits, misses and the
+passes of TCC_HIT_sum TCC_MISS_sum (tools/gpu_run.sh l2hit) and prints per-launch hits, misses and the
 hit rate, median over the profiled launches.
 
     python tools/tcc_hit_summary.py DIR_INSTEP DIR_WARM
