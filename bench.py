@@ -12,8 +12,13 @@ step's own kernels, median over the K steps, the slowest rank); ``ms_per_step`` 
 
 With ``--gpus N > 1`` the same world is split over N ranks (strong scaling), one process per GPU:
 under torch.distributed.run (RANK / WORLD_SIZE set), or — without a launcher — this script starts the N
-rank processes itself before anything touches the GPU. Every rank checks that its RCCL communicator
-holds N ranks (``ranks_seen``, ncclCommCount) and exits non-zero otherwise. The default partition
+rank processes itself before anything touches the GPU. The exchanges go through a ladder (DESIGN.md
+§7): the direct peer exchange (p2p), else RCCL all-gathers, else the gloo host exchange — a mode that
+fails on any rank (set-up, the three-step chi^2 check or the timed steps) is dropped on every rank
+together and the next one runs; the line records each attempt with every failing rank's reason
+(``exchange_decision``), every rank's device and rank 0's peer-access matrix (``topology``), and if no
+mode completes rank 0 still prints a line (``value`` null, ``error``). The exchange must span N ranks
+(``ranks_seen``: the RCCL communicator's count or the process group's). The default partition
 (BOS_PARTITION_SUBTREE) gives each rank the subtrees of the Schur assembly tree below a
 replicated top: its J+H builds only the H its fronts read, two all-gathers per iteration. The north
 star's partition (BOS_PARTITION_OBSERVATIONS: the J+H lanes split by measurement order, one
@@ -23,7 +28,10 @@ Also reported: the J+H kernel's HBM roofline fraction (in-step; from cold caches
 back), GN iterations/s, and the CPU baselines (the oracle, oracle/bos_oracle.cpp, and the build's
 C++ CPU backend, timed on this host's usable cores).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|fp64]
+``--config c2`` times BASELINE config 2 instead (synthetic 1k / 2k / 20k, fp64, one GPU): microseconds
+per GN iteration and per J+H build beside the CPU backend's (the size is launch-bound: no roofline).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|fp64] [--config c3|c2]
 """
 import argparse
 import json

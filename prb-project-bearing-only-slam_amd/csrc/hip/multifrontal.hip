@@ -294,145 +294,6 @@ __global__ __launch_bounds__(kMfBlock) void mf_forward_level(const MfArgs a) {
     }
 }
 
-__device__ __forceinline__ double readlane_d(double x, int l);
-__device__ __forceinline__ double rsqrt_nr(double d);
-typedef double dbl4 __attribute__((ext_vector_type(4)));
-
-// Larger fronts (kMfWaveMaxM < m <= kBlkMaxM: config 2's separators, m ~ 60-100): one 256-thread
-// workgroup per front, the whole m x m front in LDS (column-major, leading dimension m, as the plan's
-// amap_dst), a blocked right-looking partial Cholesky of its k columns fused with the forward step.
-// Per panel of kBlkNb columns: wave 0 factors the panel with its rows in registers (two rows per lane,
-// pivots broadcast by v_readlane, no barrier inside the panel) and carries the forward elimination
-// along; then all four waves update the trailing lower triangle, A22 -= L21 L21^T, in 16 x 16 tiles
-// on f64 MFMA (v_mfma_f64_16x16x4f64, the fold's W W^T pattern). The children's u-vectors are
-// extend-added with their update matrices (no separate forward launch). mf_factor_level (with
-// mf_forward_level) kept the front in global scratch above 90 rows and took ~140 us per level launch
-// at config 2; it remains for m > kBlkMaxM (fallback plans).
-constexpr int kBlkMaxM = 128, kBlkNb = 16;
-
-__global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int s = a.level[blockIdx.x];
-    const int k = a.k[s], r = a.r[s], m = k + r;   // m <= kBlkMaxM (mf_create / the launch check it)
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    double* F = lds;                  // m x m, column-major
-    double* w = lds + m * m;          // right-hand side, then the forward step's results
-    const int c0 = a.col0[s];
-    for (int e = tid; e < m * m; e += kMfBlock) F[e] = 0.0;
-    for (int i = tid; i < m; i += kMfBlock) w[i] = i < k ? a.x[c0 + i] : 0.0;
-    __syncthreads();
-    for (int q = a.amap_ptr[s] + tid; q < a.amap_ptr[s + 1]; q += kMfBlock) F[a.amap_dst[q]] = a.A[a.amap_src[q]];
-    __syncthreads();
-    // children one at a time (deterministic): update matrix into F, u-vector into w
-    for (int ci = a.child_ptr[s]; ci < a.child_ptr[s + 1]; ++ci) {
-        const int c = a.child[ci];
-        const int rc = a.r[c];
-        const int32_t* map = a.rmap + a.rmap_off[c];
-        const double* Uc = a.U + a.U_off[c];
-        for (int j = wave; j < rc; j += kMfBlock / 64) {
-            const int pj = map[j] * m;
-            const double* uj = Uc + pk(j, j, rc) - j;
-            for (int i = j + lane; i < rc; i += 64) F[map[i] + pj] += uj[i];
-        }
-        const double* uc = a.u + a.u_off[c];
-        for (int t = tid; t < rc; t += kMfBlock) w[map[t]] += uc[t];
-        __syncthreads();
-    }
-    double* Ls = a.L + a.L_off[s];
-    int nbad = 0;
-    for (int p0 = 0; p0 < k; p0 += kBlkNb) {
-        const int nb = min(kBlkNb, k - p0);
-        if (wave == 0) {
-            // lane l holds rows p0 + l and p0 + 64 + l of the panel's columns (m - p0 <= 128 rows)
-            const int ia = p0 + lane, ib = p0 + 64 + lane;
-            const bool va = ia < m, vb = ib < m;
-            double pa[kBlkNb], pb[kBlkNb];
-#pragma unroll
-            for (int c = 0; c < kBlkNb; ++c) {
-                pa[c] = va && c < nb ? F[ia + (p0 + c) * m] : 0.0;
-                pb[c] = vb && c < nb ? F[ib + (p0 + c) * m] : 0.0;
-            }
-            double wa = va ? w[ia] : 0.0, wb = vb ? w[ib] : 0.0;
-#pragma unroll
-            for (int j = 0; j < kBlkNb; ++j) {
-                if (j < nb) {   // uniform
-                    double d = readlane_d(pa[j], j);
-                    const bool bad = !(d > 0.0);
-                    nbad += bad;
-                    d = bad ? 1e-300 : d;
-                    const double inv = rsqrt_nr(d), ljj = d * inv;
-                    // L[i, p0 + j]; rows above the pivot (lanes < j) hold upper entries: zero
-                    const double la = lane < j ? 0.0 : lane == j ? ljj : pa[j] * inv;
-                    const double lb = pb[j] * inv;
-                    pa[j] = la;
-                    pb[j] = lb;
-                    const double y = readlane_d(wa, j) * inv;   // forward step: y_j = w_j / L_jj
-                    wa = lane == j ? y : lane > j ? fma(-la, y, wa) : wa;
-                    wb = fma(-lb, y, wb);
-#pragma unroll
-                    for (int c = j + 1; c < kBlkNb; ++c) {
-                        if (c < nb) {
-                            const double lc = readlane_d(la, c);   // L[p0 + c, p0 + j]
-                            pa[c] = fma(-la, lc, pa[c]);
-                            pb[c] = fma(-lb, lc, pb[c]);
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < kBlkNb; ++c) {
-                if (c < nb) {
-                    if (va) {
-                        F[ia + (p0 + c) * m] = pa[c];
-                        ST_L(Ls, ia + (p0 + c) * m, pa[c]);
-                    }
-                    if (vb) {
-                        F[ib + (p0 + c) * m] = pb[c];
-                        ST_L(Ls, ib + (p0 + c) * m, pb[c]);
-                    }
-                }
-            }
-            if (va) w[ia] = wa;
-            if (vb) w[ib] = wb;
-        }
-        __syncthreads();
-        // trailing lower triangle, rows / columns [t0, m): 16 x 16 tiles (bi >= bj) over the waves
-        const int t0 = p0 + nb, nbt = (m - t0 + 15) >> 4, ntiles = nbt * (nbt + 1) / 2;
-        for (int q = wave; q < ntiles; q += kMfBlock / 64) {
-            int bi = 0;
-            while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
-            const int bj = q - bi * (bi + 1) / 2;
-            const int ra = t0 + 16 * bi + (lane & 15), rb = t0 + 16 * bj + (lane & 15);
-            dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-            for (int kk = 0; kk < nb; kk += 4) {
-                const int cc = kk + (lane >> 4);
-                const double av = cc < nb && ra < m ? F[ra + (p0 + cc) * m] : 0.0;
-                const double bv = cc < nb && rb < m ? F[rb + (p0 + cc) * m] : 0.0;
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
-            const int col = t0 + 16 * bj + (lane & 15);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int row = t0 + 16 * bi + (lane >> 4) + 4 * e;
-                if (row < m && row >= col) F[row + col * m] -= acc[e];
-            }
-        }
-        __syncthreads();
-    }
-    if (tid == 0 && nbad) atomicAdd(a.info, nbad);
-    // the update matrix (packed lower r x r), the forward results: own dofs to x, the rest to u
-    double* Us = a.U + a.U_off[s];
-    for (int j = wave; j < r; j += kMfBlock / 64) {
-        double* uj = Us + pk(j, j, r) - j;
-        const double* fj = F + (k + (k + j) * m);
-        for (int i = j + lane; i < r; i += 64) uj[i] = fj[i];
-    }
-    for (int i = tid; i < m; i += kMfBlock) {
-        if (i < k) a.x[c0 + i] = w[i];
-        else a.u[a.u_off[s] + (i - k)] = w[i];
-    }
-}
-
 // backward substitution L^T x = y for one level (top-down): the rows below the supernode are
 // ancestors' dofs whose solution is already final in x
 __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
@@ -630,7 +491,8 @@ __device__ __forceinline__ void fold_chunk(const MfArgs& a, double* W, FoldBuf* 
     constexpr int NB = FoldAcc<MAXM>::NB;
     constexpr int WS = 2 * fold_chunk_landmarks(MAXM) + 1;   // W row stride (odd: no bank conflicts)
     const int nbm = (m + 15) >> 4;
-    const int t = q1.z & 63, rc = (q1.z >> 6) & 63, pos = (q1.z >> 12) & 63, lml = (q1.z >> 18) & 63;
+    const int t = q1.z & 63, rc = (q1.z >> 6) & 63, pos = (q1.z >> kFoldPosShift) & kFoldPosMask,
+              lml = (q1.z >> kFoldLmShift) & 63;
     const bool mine = lane < n;
     const int nl = __builtin_amdgcn_readlane(lml, n - 1) + 1;   // landmarks of this chunk
     const int col0 = q1.y;
@@ -787,6 +649,381 @@ __device__ __forceinline__ void fold_store(const FoldAcc<MAXM>& acc, double* F, 
             }
         }
     if (lane < m) wv[lane] = acc.w;
+}
+
+// Larger fronts (kMfWaveMaxM < m <= kBlkMaxM: config 2's separators, m ~ 60-100): one 256-thread
+// workgroup per front, the whole m x m front in LDS (column-major, leading dimension m, as the plan's
+// amap_dst), a blocked right-looking partial Cholesky of its k columns fused with the forward step.
+// Per panel of kBlkNb columns: wave 0 factors the panel with its rows in registers (two rows per lane,
+// pivots broadcast by v_readlane, no barrier inside the panel) and carries the forward elimination
+// along; then all four waves update the trailing lower triangle, A22 -= L21 L21^T, in 16 x 16 tiles
+// on f64 MFMA (v_mfma_f64_16x16x4f64, the fold's W W^T pattern). The children's u-vectors are
+// extend-added with their update matrices (no separate forward launch). mf_factor_level (with
+// mf_forward_level) kept the front in global scratch above 90 rows and took ~140 us per level launch
+// at config 2; it remains for m > kBlkMaxM (fallback plans).
+constexpr int kBlkMaxM = kMfBlkMaxM, kBlkNb = 16;
+constexpr int kBlkTiles = 9;   // 16 x 16 lower tiles per wave: (8 * 9 / 2 = 36 for 128 rows) / 4 waves
+// dynamic LDS of a front of m rows: F (m x m), w (kBlkMaxM), the fold's chunk y and landmark count,
+// the panel's column broadcast (kBlkNb)
+inline int blk_lds_bytes(int m) { return (m * m + kBlkMaxM + 2 * fold_chunk_landmarks(kBlkMaxM) + 2 + kBlkNb) * 8; }
+// children whose update matrices the blocked kernel prefetches (values and front positions, kBlkXU per
+// thread: r <= 63), issued before the fold; more (or larger) children take the plain loop
+constexpr int kBlkXCh = 4, kBlkXU = 8;
+
+// The folded landmark children of a workgroup front (Schur ordering), the workgroup form of
+// fold_children: per chunk (<= kFoldChunk observing poses, <= fold_chunk_landmarks(m) landmarks)
+// wave 0's lanes take the chunk's records — the landmarks' 2 x 2 factors, L panels and forward steps,
+// the chunk's W (front position x 2 columns per landmark, LDS aliasing F) and y — with the next
+// chunk's records and values in flight; then every wave accumulates its 16 x 16 tiles of W W^T on f64
+// MFMA (registers, acc[u]: tile wave + 4 u) and each row's thread -W y (wacc). The caller stores
+// minus both into the front before its assembly.
+template <bool F32>
+__device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double* W, double* ybuf, int* nlb, int m,
+                                                 int tid, dbl4 acc[kBlkTiles], double& wacc) {
+    constexpr int cap = fold_chunk_landmarks(kBlkMaxM);
+    constexpr int WS = 2 * cap + 1;   // W row stride (odd: no bank conflicts)
+    const int wave = tid >> 6, lane = tid & 63;
+    const int nbt = (m + 15) >> 4, ntiles = nbt * (nbt + 1) / 2;
+#pragma unroll
+    for (int u = 0; u < kBlkTiles; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+    wacc = 0.0;
+    for (int e = tid; e < m * WS; e += kMfBlock) W[e] = 0.0;
+    const int ch0 = a.fold_cptr[s], ch1 = a.fold_cptr[s + 1];
+    int nbad = 0;
+    ChunkTable tb;
+    int n = 0, nn = 0;
+    int4 r0, r1, n0, n1;
+    FoldValsT<F32> v;
+    auto rec = [&](int c, int cnt, int4& q0, int4& q1) {
+        const int q = tb.at(c) + min(lane, max(cnt - 1, 0));
+        q0 = fold_rec_load(a, q, 0);
+        q1 = fold_rec_load(a, q, 1);
+    };
+    auto len = [&](int c) { return c < ch1 ? tb.at(c + 1) - tb.at(c) : 0; };
+    if (wave == 0) {
+        tb.load(a, ch0, lane);
+        n = len(ch0);
+        rec(ch0, n, r0, r1);
+        v = fold_vals<F32>(a, r0, r1, lane < n);
+        nn = len(ch0 + 1);
+        rec(ch0 + 1, nn, n0, n1);
+    }
+    __syncthreads();   // (W cleared)
+    for (int ch = ch0; ch < ch1; ++ch) {   // (uniform over the workgroup)
+        int pos = 0, lml = 0, ncur = 0;
+        if (wave == 0) {
+            if (ch + 3 - tb.base > 63) tb.reload(a, ch, lane);
+            const FoldVals d = fold_decode(v);
+            const int4 q1 = r1;
+            ncur = n;
+            // the next chunk: values now (its records arrived during this one), records of ch + 2
+            v = fold_vals<F32>(a, n0, n1, lane < nn);
+            r0 = n0;
+            r1 = n1;
+            const int n2 = len(ch + 2);
+            rec(ch + 2, n2, n0, n1);
+            n = nn;
+            nn = n2;
+            const int t = q1.z & 63, rc = (q1.z >> 6) & 63;
+            pos = (q1.z >> kFoldPosShift) & kFoldPosMask;
+            lml = (q1.z >> kFoldLmShift) & 63;
+            const bool mine = lane < ncur;
+            // as fold_chunk: every lane issues the same stores (a lane past the chunk's rows holds its
+            // last row's record and values: the owners' bits to the owners' addresses)
+            double d0 = d.a00;
+            const bool bad0 = !(d0 > 0.0);
+            d0 = bad0 ? 1e-300 : d0;
+            const double i0 = rsqrt_nr(d0), l00 = d0 * i0;
+            const double l10 = d.a10 * i0;
+            double d1 = d.a11 - l10 * l10;
+            const bool bad1 = !(d1 > 0.0);
+            d1 = bad1 ? 1e-300 : d1;
+            const double i1 = rsqrt_nr(d1), l11 = d1 * i1;
+            const double y0 = d.x0 * i0, y1 = (d.x1 - l10 * y0) * i1;
+            const int mc = 2 + rc;
+            double* Lc = a.L + q1.w;
+            const bool head = mine && t == 0;
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                const double lt0 = d.h[2 * g] * i0;
+                const double lt1 = (d.h[2 * g + 1] - lt0 * l10) * i1;
+                ST_LF(Lc, 2 + t + g, lt0);
+                ST_LF(Lc, mc + 2 + t + g, lt1);
+                if (mine) {
+                    W[(pos + g) * WS + 2 * lml] = lt0;
+                    W[(pos + g) * WS + 2 * lml + 1] = lt1;
+                }
+            }
+            ST_LF(Lc, 0, l00);
+            ST_LF(Lc, 1, l10);
+            ST_LF(Lc, mc + 1, l11);
+            a.x[q1.y] = y0;
+            a.x[q1.y + 1] = y1;
+            nbad += head ? (int)bad0 + (int)bad1 : 0;
+            if (head) {
+                ybuf[2 * lml] = y0;
+                ybuf[2 * lml + 1] = y1;
+            }
+            const int nl = __builtin_amdgcn_readlane(lml, ncur - 1) + 1;   // landmarks of this chunk
+            if (lane == 0) *nlb = nl;
+        }
+        __syncthreads();
+        const int kc = 2 * *nlb;
+        if (tid < m) {   // u-vector part: -(W y) at this thread's row
+            double wsum = 0.0;
+            for (int q = 0; q < kc; ++q) wsum += W[tid * WS + q] * ybuf[q];
+            wacc -= wsum;
+        }
+        // W W^T, 4 columns per MFMA step: tile (bi, bj) of wave + 4 u; lane l feeds row 16 b + (l & 15),
+        // column 4 st + (l >> 4) of W as A (block row bi) and as B (block row bj)
+#pragma unroll
+        for (int u = 0; u < kBlkTiles; ++u) {
+            const int q = wave + 4 * u;
+            if (q < ntiles) {
+                int bi = 0;
+                while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+                const int bj = q - bi * (bi + 1) / 2;
+                const int ra = 16 * bi + (lane & 15), rb = 16 * bj + (lane & 15);
+                for (int st = 0; 4 * st < kc; ++st) {
+                    const int cc = 4 * st + (lane >> 4);
+                    const double av = ra < m ? W[ra * WS + cc] : 0.0;
+                    const double bv = rb < m ? W[rb * WS + cc] : 0.0;
+                    acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[u], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+        if (wave == 0 && lane < ncur) {   // clear this chunk's W entries (wave 0 writes the next chunk's after)
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                W[(pos + g) * WS + 2 * lml] = 0.0;
+                W[(pos + g) * WS + 2 * lml + 1] = 0.0;
+            }
+        }
+    }
+    if (wave == 0 && nbad) atomicAdd(a.info, nbad);
+}
+
+template <bool F32>
+__global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int s = a.level[blockIdx.x];
+    const int k = a.k[s], r = a.r[s], m = k + r;   // m <= kBlkMaxM (mf_create / the launch check it)
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    double* F = lds;                  // m x m, column-major
+    double* w = lds + m * m;          // right-hand side, then the forward step's results
+    double* ybuf = w + kBlkMaxM;      // the fold's y of one chunk (2 per landmark)
+    int* nlb = reinterpret_cast<int*>(ybuf + 2 * fold_chunk_landmarks(kBlkMaxM));
+    double* colbuf = ybuf + 2 * fold_chunk_landmarks(kBlkMaxM) + 2;
+    const int c0 = a.col0[s];
+    const int nfold = a.fold_cnt[s];
+    // the non-folded children (pose separators, typically 2): their update matrices and u-vectors,
+    // with their positions in this front (emap), loaded now and in flight during the fold
+    const int cb = a.child_ptr[s] + nfold, ce = a.child_ptr[s + 1];
+    const int nx = min(ce - cb, kBlkXCh);
+    double xv[kBlkXCh][kBlkXU], xuv[kBlkXCh];
+    int xp[kBlkXCh][kBlkXU], xum[kBlkXCh], xne[kBlkXCh];
+#pragma unroll
+    for (int i = 0; i < kBlkXCh; ++i) {
+        xne[i] = 0;
+        if (i < nx) {   // uniform
+            const int c = a.child[cb + i];
+            const int rc = a.r[c], ne = rc * (rc + 1) / 2;
+            xne[i] = ne;
+            const double* Uc = a.U + a.U_off[c];
+            const int16_t* ec = a.emap + a.emap_off[c];
+#pragma unroll
+            for (int u = 0; u < kBlkXU; ++u) {
+                const int e = min(tid + kMfBlock * u, ne - 1);   // clamped (see assemble_wave)
+                xv[i][u] = Uc[e];
+                xp[i][u] = ec[e];
+            }
+            const int t = min(tid, rc - 1);
+            xuv[i] = a.u[a.u_off[c] + t];
+            xum[i] = tid < rc ? a.rmap[a.rmap_off[c] + t] : -1;
+        }
+    }
+    // diagnostics (bos_debug_solver_stamps): the per-front phases of tools/solver_stamps.py
+    auto stamp = [&](int q) {
+        if (a.stamps_f && tid == 0) a.stamps_f[8 * (int64_t)s + q] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
+    double wacc = 0.0;
+    if (nfold > 0) {
+        // the folded landmarks first (their W uses F's LDS); F and w then start from minus their
+        // contribution, each lower entry written once by the wave holding its tile
+        dbl4 acc[kBlkTiles];
+        fold_children_wg<F32>(a, s, F, ybuf, nlb, m, tid, acc, wacc);
+        for (int e = tid; e < m * m; e += kMfBlock) F[e] = 0.0;
+        __syncthreads();
+        const int nbt = (m + 15) >> 4, ntiles = nbt * (nbt + 1) / 2;
+#pragma unroll
+        for (int u = 0; u < kBlkTiles; ++u) {
+            const int q = wave + 4 * u;
+            if (q < ntiles) {
+                int bi = 0;
+                while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+                const int bj = q - bi * (bi + 1) / 2;
+                const int j = 16 * bj + (lane & 15);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int i = 16 * bi + (lane >> 4) + 4 * e;
+                    if (i < m && j <= i) F[i + j * m] = -acc[u][e];
+                }
+            }
+        }
+    } else {
+        for (int e = tid; e < m * m; e += kMfBlock) F[e] = 0.0;
+    }
+    if (tid < m) w[tid] = (tid < k ? a.x[c0 + tid] : 0.0) + wacc;   // (m <= kBlkMaxM < kMfBlock)
+    __syncthreads();
+    stamp(1);
+    for (int q = a.amap_ptr[s] + tid; q < a.amap_ptr[s + 1]; q += kMfBlock) F[a.amap_dst[q]] += a.A[a.amap_src[q]];
+    __syncthreads();
+    stamp(2);
+    stamp(3);
+    // the other children one at a time (deterministic): update matrix into F, u-vector into w
+#pragma unroll
+    for (int i = 0; i < kBlkXCh; ++i) {
+        if (i < nx) {   // uniform
+#pragma unroll
+            for (int u = 0; u < kBlkXU; ++u)
+                if (tid + kMfBlock * u < xne[i]) F[xp[i][u]] += xv[i][u];
+            if (xum[i] >= 0) w[xum[i]] += xuv[i];
+            if (xne[i] > kMfBlock * kBlkXU) {   // entries past the prefetched ones (r > 63)
+                const int c = a.child[cb + i];
+                const double* Uc = a.U + a.U_off[c];
+                const int16_t* ec = a.emap + a.emap_off[c];
+                for (int e = kMfBlock * kBlkXU + tid; e < xne[i]; e += kMfBlock) F[ec[e]] += Uc[e];
+            }
+            __syncthreads();
+        }
+    }
+    for (int ci = cb + nx; ci < ce; ++ci) {
+        const int c = a.child[ci];
+        const int rc = a.r[c];
+        const int32_t* map = a.rmap + a.rmap_off[c];
+        const double* Uc = a.U + a.U_off[c];
+        for (int j = wave; j < rc; j += kMfBlock / 64) {
+            const int pj = map[j] * m;
+            const double* uj = Uc + pk(j, j, rc) - j;
+            for (int i = j + lane; i < rc; i += 64) F[map[i] + pj] += uj[i];
+        }
+        const double* uc = a.u + a.u_off[c];
+        for (int t = tid; t < rc; t += kMfBlock) w[map[t]] += uc[t];
+        __syncthreads();
+    }
+    stamp(4);
+    double* Ls = a.L + a.L_off[s];
+    int nbad = 0;
+    for (int p0 = 0; p0 < k; p0 += kBlkNb) {
+        const int nb = min(kBlkNb, k - p0);
+        if (wave == 0) {
+            // lane l holds rows p0 + l and p0 + 64 + l of the panel's columns (m - p0 <= 128 rows); the
+            // reads are clamped to valid positions (one wait for all), the values past the front zero.
+            // Columns past nb hold copies of column nb - 1: updated like the others, never a pivot,
+            // never stored.
+            const int ia = p0 + lane, ib = p0 + 64 + lane;
+            const bool va = ia < m, vb = ib < m;
+            const int ra = min(ia, m - 1), rb = min(ib, m - 1);
+            double pa[kBlkNb], pb[kBlkNb];
+#pragma unroll
+            for (int c = 0; c < kBlkNb; ++c) {
+                const int cc = p0 + min(c, nb - 1);
+                pa[c] = F[ra + cc * m];
+                pb[c] = F[rb + cc * m];
+            }
+            asm volatile("" : "+v"(pa[0]), "+v"(pb[0]));
+#pragma unroll
+            for (int c = 0; c < kBlkNb; ++c) {
+                pa[c] = va ? pa[c] : 0.0;
+                pb[c] = vb ? pb[c] : 0.0;
+            }
+            double wa = va ? w[ia] : 0.0, wb = vb ? w[ib] : 0.0;
+#pragma unroll
+            for (int j = 0; j < kBlkNb; ++j) {
+                if (j < nb) {   // uniform
+                    double d = readlane_d(pa[j], j);
+                    const bool bad = !(d > 0.0);
+                    nbad += bad;
+                    d = bad ? 1e-300 : d;
+                    const double inv = rsqrt_nr(d), ljj = d * inv;
+                    // L[i, p0 + j]; rows above the pivot (lanes < j) hold upper entries: zero
+                    const double la = lane < j ? 0.0 : lane == j ? ljj : pa[j] * inv;
+                    const double lb = pb[j] * inv;
+                    pa[j] = la;
+                    pb[j] = lb;
+                    // the column's panel rows broadcast through LDS (one write, independent reads)
+                    if (lane < kBlkNb) colbuf[lane] = la;
+                    const double y = readlane_d(wa, j) * inv;   // forward step: y_j = w_j / L_jj
+                    wa = lane == j ? y : lane > j ? fma(-la, y, wa) : wa;
+                    wb = fma(-lb, y, wb);
+                    wave_sync();
+                    double cbv[kBlkNb];
+#pragma unroll
+                    for (int c = j + 1; c < kBlkNb; ++c) cbv[c] = colbuf[c];   // L[p0 + c, p0 + j]
+#pragma unroll
+                    for (int c = j + 1; c < kBlkNb; ++c) {
+                        pa[c] = fma(-la, cbv[c], pa[c]);
+                        pb[c] = fma(-lb, cbv[c], pb[c]);
+                    }
+                    __builtin_amdgcn_wave_barrier();   // the next pivot's broadcast stays after these reads
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kBlkNb; ++c) {
+                if (c < nb) {
+                    if (va) {
+                        F[ia + (p0 + c) * m] = pa[c];
+                        ST_L(Ls, ia + (p0 + c) * m, pa[c]);
+                    }
+                    if (vb) {
+                        F[ib + (p0 + c) * m] = pb[c];
+                        ST_L(Ls, ib + (p0 + c) * m, pb[c]);
+                    }
+                }
+            }
+            if (va) w[ia] = wa;
+            if (vb) w[ib] = wb;
+        }
+        __syncthreads();
+        // trailing lower triangle, rows / columns [t0, m): 16 x 16 tiles (bi >= bj) over the waves
+        const int t0 = p0 + nb, nbt = (m - t0 + 15) >> 4, ntiles = nbt * (nbt + 1) / 2;
+        for (int q = wave; q < ntiles; q += kMfBlock / 64) {
+            int bi = 0;
+            while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+            const int bj = q - bi * (bi + 1) / 2;
+            const int ra = t0 + 16 * bi + (lane & 15), rb = t0 + 16 * bj + (lane & 15);
+            dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+            for (int kk = 0; kk < nb; kk += 4) {
+                const int cc = kk + (lane >> 4);
+                const double av = cc < nb && ra < m ? F[ra + (p0 + cc) * m] : 0.0;
+                const double bv = cc < nb && rb < m ? F[rb + (p0 + cc) * m] : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+            const int col = t0 + 16 * bj + (lane & 15);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = t0 + 16 * bi + (lane >> 4) + 4 * e;
+                if (row < m && row >= col) F[row + col * m] -= acc[e];
+            }
+        }
+        __syncthreads();
+    }
+    stamp(5);
+    if (tid == 0 && nbad) atomicAdd(a.info, nbad);
+    // the update matrix (packed lower r x r), the forward results: own dofs to x, the rest to u
+    double* Us = a.U + a.U_off[s];
+    for (int j = wave; j < r; j += kMfBlock / 64) {
+        double* uj = Us + pk(j, j, r) - j;
+        const double* fj = F + (k + (k + j) * m);
+        for (int i = j + lane; i < r; i += 64) uj[i] = fj[i];
+    }
+    for (int i = tid; i < m; i += kMfBlock) {
+        if (i < k) a.x[c0 + i] = w[i];
+        else a.u[a.u_off[s] + (i - k)] = w[i];
+    }
+    stamp(6);
 }
 
 // ---- dataflow (work-queue) kernels: one launch walks a whole tree range. A wavefront takes the
@@ -1267,6 +1504,220 @@ __global__ __launch_bounds__(64, 1) void mf_factor_reg(const MfArgs a) {
     factor_front_reg<MAXM, kModeLevel, F32>(a, a.level[blockIdx.x], F, colbuf, wv, &fb, threadIdx.x, nullptr);
 }
 
+// Level-launch wave fronts with the pivots on register panels and the trailing update on f64 MFMA
+// (VERDICT r05 next 1). factor_front_reg holds a lane's whole front row in registers (row[MAXM]): at
+// class 48 that is 96 of the kernel's 147 VGPRs and caps level 0 (10 350 fronts, k ~ 18, m ~ 42) at 3
+// waves per SIMD. Here a lane holds only the KP columns of the current panel: the pivot loop (the
+// same two-pivot steps, LDS pair broadcast) runs over the panel's columns, the L columns go to global
+// memory as before and into the front's LDS triangle in place of the columns they replace, and the
+// rest of the front, still in LDS, takes A22 -= L21 L21^T in 16 x 16 tiles on v_mfma_f64_16x16x4f64
+// (the fold's W W^T pattern); the last panel's tiles go straight to the update matrix. The prologue
+// (fold, assembly, children) is factor_front_reg's, with the children's structure read after the
+// fold instead of before it (its registers would be live across the fold).
+template <int MAXM, int KP, bool F32>
+__device__ __forceinline__ void factor_front_pan(const MfArgs& a, int s, double* F, double* colbuf, double* wv,
+                                                 FoldBuf* fb, int lane) {
+    const int k = a.k[s], r = a.r[s], m = k + r;
+    const int nfold = a.fold_cnt[s];
+    const int c0 = a.col0[s];
+    const int aq0 = a.amap_ptr[s], aq1 = a.amap_ptr[s + 1];
+    const int np = m * (m + 1) / 2;
+    double xo = a.x[c0 + min(lane, k - 1)];
+    double* Ls = a.L + a.L_off[s];
+    double* Us = a.U + a.U_off[s];
+    double* us = a.u + a.u_off[s];
+    const int cb = a.child_ptr[s] + nfold, ce = a.child_ptr[s + 1];
+    unsigned long long* const stp = a.stamps_f;
+    fstamp(stp, s, 0);
+    if (nfold > 0) {
+        FoldAcc<MAXM> facc;
+        fold_children<MAXM, F32>(a, s, F, fb, m, lane, facc);
+        wave_sync();
+        fold_store<MAXM>(facc, F, wv, m, lane);
+    } else {
+        for (int e = lane; e < np; e += 64) F[e] = 0.0;
+        for (int i = lane; i < m; i += 64) wv[i] = 0.0;
+    }
+    wave_sync();
+    fstamp(stp, s, 1);
+    ChildPre p0c, p1c;   // (structure in flight during the assembly)
+    if (cb < ce) child_meta(a, a.child[cb], lane, p0c);
+    if (cb + 1 < ce) child_meta(a, a.child[cb + 1], lane, p1c);
+    assemble_wave(a, aq0, aq1, F, lane, nfold > 0);
+    wave_sync();
+    asm volatile("" : "+v"(xo));
+    xo = lane < k ? xo : 0.0;
+    fstamp(stp, s, 2);
+    fstamp(stp, s, 3);
+    if (cb < ce) child_vals<false>(lane, p0c);
+    if (cb + 1 < ce) child_vals<false>(lane, p1c);
+    if (cb < ce) extend_child<false>(a, p0c, F, wv, m, lane);
+    if (cb + 1 < ce) extend_child<false>(a, p1c, F, wv, m, lane);
+    for (int ci = cb + 2; ci < ce; ++ci) {
+        ChildPre pq;
+        child_meta(a, a.child[ci], lane, pq);
+        child_vals<false>(lane, pq);
+        extend_child<false>(a, pq, F, wv, m, lane);
+    }
+    fstamp(stp, s, 4);
+    const bool live = lane < m;
+    const int lrow = min(lane, m - 1);
+    double wi = live ? wv[lane] + xo : 0.0;   // forward elimination, fused into the pivot loop
+    int nbad = 0;
+    double2* cp = reinterpret_cast<double2*>(colbuf);
+    for (int p0 = 0; p0 < k; p0 += KP) {
+        const int nb = min(KP, k - p0);
+        // row[t] = F(lane, p0 + t) (column clamped to m - 1: branch-free reads, one wait; entries
+        // above the diagonal, of rows >= m and columns past the panel are scratch)
+        double row[KP];
+#pragma unroll
+        for (int t0 = 0; t0 < KP; t0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int t = t0; t < t0 + 8; ++t) v[t - t0] = F[pk32(lrow, min(p0 + t, m - 1), m)];
+            asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                         "+v"(v[7]));
+#pragma unroll
+            for (int t = t0; t < t0 + 8; ++t) row[t] = v[t - t0];
+        }
+        double* Lj = Ls + lane + (int64_t)p0 * m;
+        int j = 0;   // pivot p0 + j; before step j, row[t] holds column p0 + j + t
+#pragma nounroll
+        for (; j + 1 < nb; j += 2) {
+            const int J = p0 + j;
+            double d0 = readlane_d(row[0], J);
+            const bool bad0 = !(d0 > 0.0);
+            nbad += bad0;
+            d0 = bad0 ? 1e-300 : d0;
+            const double inv0 = rsqrt_nr(d0), l00 = d0 * inv0;
+            const double l0 = lane == J ? l00 : row[0] * inv0;   // L[i, J]
+            const double lj1 = readlane_d(l0, J + 1);
+            const double f1 = fma(-l0, lj1, row[1]);
+            double d1 = readlane_d(f1, J + 1);
+            const bool bad1 = !(d1 > 0.0);
+            nbad += bad1;
+            d1 = bad1 ? 1e-300 : d1;
+            const double inv1 = rsqrt_nr(d1), l11 = d1 * inv1;
+            const double l1 = lane == J + 1 ? l11 : f1 * inv1;   // L[i, J + 1]
+            // pairs of the panel's later rows (the rank-2 update of its remaining columns)
+            if (lane > J + 1 && lane < p0 + nb) cp[lane - J - 2] = make_double2(l0, l1);
+            if (live) {
+                if (lane >= J) {
+                    ST_L(Lj, 0, l0);
+                    F[pk32(lane, J, m)] = l0;   // L21 for the trailing update (column J is consumed)
+                }
+                if (lane >= J + 1) {
+                    ST_L(Lj, m, l1);
+                    F[pk32(lane, J + 1, m)] = l1;
+                }
+            }
+            Lj += 2 * m;
+            const double y0 = readlane_d(wi, J) * inv0;          // forward steps J, J + 1
+            if (lane == J) wi = y0;
+            else if (lane > J) wi -= l0 * y0;
+            const double y1 = readlane_d(wi, J + 1) * inv1;
+            if (lane == J + 1) wi = y1;
+            else if (lane > J + 1) wi -= l1 * y1;
+            wave_sync();
+            const int nt = nb - j - 2;                           // panel columns left after this step
+#pragma unroll
+            for (int t0 = 0; t0 < KP - 2; t0 += 8) {
+                if (t0 < nt) {
+                    double2 c[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) c[u] = t0 + u < KP - 2 ? cp[t0 + u] : make_double2(0.0, 0.0);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(c[u].x), "+v"(c[u].y));
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (t0 + u < KP - 2) row[t0 + u] = fma(-l1, c[u].y, fma(-l0, c[u].x, row[t0 + u + 2]));
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (j < nb) {   // the panel's last column (odd nb)
+            const int J = p0 + j;
+            double d = readlane_d(row[0], J);
+            const bool bad = !(d > 0.0);
+            nbad += bad;
+            d = bad ? 1e-300 : d;
+            const double inv = rsqrt_nr(d), ljj = d * inv;
+            const double lij = lane == J ? ljj : row[0] * inv;
+            if (live && lane >= J) {
+                ST_L(Lj, 0, lij);
+                F[pk32(lane, J, m)] = lij;
+            }
+            const double yj = readlane_d(wi, J) * inv;
+            if (lane == J) wi = yj;
+            else if (lane > J) wi -= lij * yj;
+        }
+        wave_sync();
+        // trailing block, rows / columns [t0, m): A22 -= L21 L21^T (L21 = rows >= t0 of the panel's L
+        // columns, now in F) in 16 x 16 tiles; the last panel's result is the update matrix
+        const int t0 = p0 + nb, T = m - t0;
+        if (T > 0) {
+            const bool last = t0 == k;
+            const int nbt = (T + 15) >> 4;
+            for (int bi = 0; bi < nbt; ++bi)
+                for (int bj = 0; bj <= bi; ++bj) {
+                    const int ra = t0 + 16 * bi + (lane & 15), rb = t0 + 16 * bj + (lane & 15);
+                    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+                    for (int kk = 0; kk < nb; kk += 4) {
+                        const int cc = kk + (lane >> 4);
+                        const int col = p0 + min(cc, nb - 1);
+                        const double av = F[pk32(min(ra, m - 1), col, m)];
+                        const double bv = F[pk32(min(rb, m - 1), col, m)];
+                        const bool ok = cc < nb;
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ok && ra < m ? av : 0.0, ok && rb < m ? bv : 0.0,
+                                                                   acc, 0, 0, 0);
+                    }
+                    const int jj = t0 + 16 * bj + (lane & 15);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int ii = t0 + 16 * bi + (lane >> 4) + 4 * e;
+                        if (ii < m && jj <= ii) {
+                            const double v = F[pk32(ii, jj, m)] - acc[e];
+                            if (last) Us[pk(ii - k, jj - k, r)] = v;
+                            else F[pk32(ii, jj, m)] = v;
+                        }
+                    }
+                }
+            wave_sync();
+        }
+    }
+    if (nbad && lane == 0) atomicAdd(a.info, nbad);
+    fstamp(stp, s, 5);
+    if (live) {
+        if (lane < k) a.x[c0 + lane] = wi;
+        else us[lane - k] = wi;
+    }
+    wave_sync();
+}
+
+// the class-48 level launches take the panel kernel (A/B builds: -DBOS_MF_PAN=0 keeps mf_factor_reg)
+#ifndef BOS_MF_PAN
+#define BOS_MF_PAN 1
+#endif
+constexpr bool kPanel48 = BOS_MF_PAN != 0;
+#ifndef BOS_MF_PAN_KP
+#define BOS_MF_PAN_KP 16
+#endif
+constexpr int kPanelKP = BOS_MF_PAN_KP;
+// waves per SIMD the panel kernel is compiled for: 4 (<= 128 VGPRs; its LDS, ~10 KB per wave, allows 15
+// waves per CU) against mf_factor_reg<48>'s 3 (147 VGPRs)
+#ifndef BOS_MF_PAN_WAVES
+#define BOS_MF_PAN_WAVES 4
+#endif
+
+template <int MAXM, int KP, bool F32>
+__global__ __launch_bounds__(64, BOS_MF_PAN_WAVES) void mf_factor_pan(const MfArgs a) {
+    __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * KP];
+    __shared__ __attribute__((aligned(16))) double wv[MAXM];
+    __shared__ FoldBuf fb;
+    factor_front_pan<MAXM, KP, F32>(a, a.level[blockIdx.x], F, colbuf, wv, &fb, threadIdx.x);
+}
+
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
 // L panel (m x k). The rows below the supernode are ancestors' dofs, already final in x.
 // The L panel and the front's own forward results do not depend on the ancestors, so the flow
@@ -1531,9 +1982,10 @@ template <typename X> int up(X** p, const std::vector<X>& v, std::string& err) {
 
 }  // namespace
 
-// front size classes: m <= 16, 32, 48, 64 (one wavefront, registers / LDS) and larger (workgroup)
-constexpr int kClasses = 5;
-inline int front_class(int m) { return m <= kMfWaveMaxM ? (m - 1) / 16 : 4; }
+// front size classes: m <= 16, 32, 48, 64 (one wavefront, registers / LDS), m <= kBlkMaxM (workgroup,
+// blocked, folds landmarks: mf_factor_blk) and larger (workgroup, global scratch: mf_factor_level)
+constexpr int kClasses = 6;
+inline int front_class(int m) { return m <= kMfWaveMaxM ? (m - 1) / 16 : m <= kBlkMaxM ? 4 : 5; }
 // The launch a front goes to: fronts with 16 < m <= 32 run in the class-48 launch of their level (one
 // launch packs the level's waves better than two in a row on one stream: solve 589 -> 564 us on
 // config 3; moving the m <= 16 fronts too measured 570)
@@ -1550,7 +2002,7 @@ struct Prog {
     int id = 0;                     // flow id (1: own / everything, 2: top)
     std::vector<int32_t> ptr;       // (level l, class c) = list[ptr[l * kClasses + c], ...)
     std::vector<int> lds_factor, lds_fwd, lds_bwd;   // per (level, class): dynamic LDS bytes
-    std::vector<int> lds_blk;       // per level: mf_factor_blk's LDS for its class-4 fronts, 0 if one is > kBlkMaxM
+    std::vector<int> lds_blk;       // per level: mf_factor_blk's LDS for its class-4 fronts
     int32_t* list = nullptr;
     int flow_lev0 = 0, n_flow_factor = 0;
     bool first_waited = false;      // the factor flow's first front has its parent in the same flow
@@ -1673,7 +2125,7 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
                     P.lds_bwd[lc] = std::max(P.lds_bwd[lc], (2 * k + (m - k) + m * k) * 8);
                 } else {
                     if (m <= kLdsCapM) P.lds_factor[lc] = std::max(P.lds_factor[lc], m * m * 8);
-                    P.lds_blk[l] = P.lds_blk[l] < 0 || m > kBlkMaxM ? -1 : std::max(P.lds_blk[l], (m * m + m) * 8);
+                    if (c == 4) P.lds_blk[l] = std::max(P.lds_blk[l], blk_lds_bytes(m));
                     P.lds_fwd[lc] = std::max(P.lds_fwd[lc], m * 8);
                     P.lds_bwd[lc] = std::max(P.lds_bwd[lc], 2 * k * 8);
                 }
@@ -1691,7 +2143,6 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
             std::stable_sort(lst.begin() + P.ptr[lc], lst.end(), [&](int x, int y) { return cost(x) > cost(y); });
             P.ptr[lc + 1] = (int32_t)lst.size();
         }
-    for (int l = 0; l < L; ++l) P.lds_blk[l] = std::max(P.lds_blk[l], 0);
     auto mine_in_level = [&](int l) {
         int c = 0;
         for (int q = F.level_ptr[l]; q < F.level_ptr[l + 1]; ++q) c += mine(F.level[q]);
@@ -1783,10 +2234,20 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
             d->ncu = ncu;
         // a front of kBlkMaxM rows takes 129 KB of LDS (160 KB per CU on gfx950)
-        const int blk_lds = (kBlkMaxM * kBlkMaxM + kBlkMaxM) * 8;
-        d->blk = hipFuncSetAttribute((const void*)mf_factor_blk, hipFuncAttributeMaxDynamicSharedMemorySize, blk_lds) ==
-                 hipSuccess;
-        if (!d->blk) (void)hipGetLastError();
+        const int blk_lds = blk_lds_bytes(kBlkMaxM);
+        d->blk = hipFuncSetAttribute((const void*)mf_factor_blk<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     blk_lds) == hipSuccess &&
+                 hipFuncSetAttribute((const void*)mf_factor_blk<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     blk_lds) == hipSuccess;
+        if (!d->blk) {
+            (void)hipGetLastError();
+            // the plan folds landmarks into fronts of up to kMfBlkMaxM rows, which only mf_factor_blk eliminates
+            for (int s = 0; s < F.nsuper; ++s)
+                if (F.k[s] + F.r[s] > kMfWaveMaxM && !F.fold_cnt.empty() && F.fold_cnt[s] > 0) {
+                    err = "multifrontal: the blocked front kernel cannot get its LDS (needed by this plan's folds)";
+                    return -2;
+                }
+        }
     }
     // program of every supernode: 1 = own (everything on one GPU), 2 = top, 0 = another rank's
     std::vector<int8_t> sel(F.nsuper, 1), fid_f(F.nsuper, 0), fid_b(F.nsuper, 0);
@@ -1839,14 +2300,14 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
             return -2;
         }
     }
-    {   // extend-add positions of every child whose parent is a wave front (m <= kMfWaveMaxM)
+    {   // extend-add positions of every child whose parent is a wave or blocked front (m <= kBlkMaxM)
         std::vector<int64_t> eoff(F.nsuper, 0);
         std::vector<int16_t> em;
         for (int c = 0; c < F.nsuper; ++c) {
             const int p = F.parent[c];
             if (p < 0) continue;
             const int mp = F.k[p] + F.r[p], rc = F.r[c];
-            if (mp > kMfWaveMaxM || rc == 0) continue;
+            if (mp > kBlkMaxM || rc == 0) continue;
             bool folded = false;
             for (int ci = F.child_ptr[p]; ci < F.child_ptr[p] + (F.fold_cnt.empty() ? 0 : F.fold_cnt[p]); ++ci)
                 folded = folded || F.child[ci] == c;
@@ -1857,7 +2318,8 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
                 for (int i = j; i < rc; ++i) {
                     const int I = rm[i], J = rm[j];
                     if (I < J || I >= mp) { err = "multifrontal: child row map not increasing"; return -1; }
-                    em.push_back((int16_t)(J * mp - J * (J - 1) / 2 + (I - J)));
+                    // wave fronts: packed lower column-major; blocked fronts: full m x m column-major
+                    em.push_back((int16_t)(mp <= kMfWaveMaxM ? J * mp - J * (J - 1) / 2 + (I - J) : I + J * mp));
                 }
         }
         if ((rc = up(&d->emap, em, err)) || (rc = up(&d->emap_off, eoff, err))) return rc;
@@ -1933,18 +2395,26 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
         if ((n = P.count(l, 0)) && !tiny16)
             hipLaunchKernelGGL((mf_factor_reg<16, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 0, A, x));
         if ((n = P.count(l, 1))) hipLaunchKernelGGL((mf_factor_reg<32, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 1, A, x));
-        if ((n = P.count(l, 2))) hipLaunchKernelGGL((mf_factor_reg<48, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 2, A, x));
+        if ((n = P.count(l, 2))) {
+            if (kPanel48)
+                hipLaunchKernelGGL((mf_factor_pan<48, kPanelKP, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 2, A, x));
+            else
+                hipLaunchKernelGGL((mf_factor_reg<48, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 2, A, x));
+        }
         if ((n = P.count(l, 3)) && !fork)
             hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
         if (fork && (e = hipStreamWaitEvent(s, d->ev_join, 0)) != hipSuccess) return e;
-        if ((n = P.count(l, 4))) {   // large fronts: workgroup factorization (blocked, MFMA; fused forward step)
-            if (d->blk && P.lds_blk[l] > 0) {
-                hipLaunchKernelGGL(mf_factor_blk, dim3(n), dim3(kMfBlock), P.lds_blk[l], s, d->args(P, l, 4, A, x));
-            } else {   // a front above kBlkMaxM rows in the level: the unblocked kernels, then the forward step
-                hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), P.lds_factor[l * kClasses + 4], s,
-                                   d->args(P, l, 4, A, x));
-                hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), P.lds_fwd[l * kClasses + 4], s,
-                                   d->args(P, l, 4, A, x));
+        // larger fronts: up to kBlkMaxM rows the blocked workgroup kernel (MFMA; folds; forward step fused),
+        // above it (fallback plans) the unblocked workgroup kernel in global scratch and its forward step
+        for (int c = 4; c < kClasses; ++c) {
+            if (!(n = P.count(l, c))) continue;
+            if (c == 4 && d->blk) {
+                hipLaunchKernelGGL((mf_factor_blk<F32>), dim3(n), dim3(kMfBlock), P.lds_blk[l], s, d->args(P, l, 4, A, x));
+            } else {
+                hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), P.lds_factor[l * kClasses + c], s,
+                                   d->args(P, l, c, A, x));
+                hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), P.lds_fwd[l * kClasses + c], s,
+                                   d->args(P, l, c, A, x));
             }
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1990,8 +2460,11 @@ hipError_t mf_solve(MfDevice* d, int which, double* x, hipStream_t s) {
             g.count = P.bptr[l + 1] - P.bptr[l];
             hipLaunchKernelGGL(mf_backward_wave, dim3(g.count), dim3(64), P.blds[l], s, g);
         }
-        if ((n = P.count(l, 4)))
-            hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), P.lds_bwd[l * kClasses + 4], s, d->args(P, l, 4, nullptr, x));
+        if ((n = P.count(l, 4, kClasses))) {   // the workgroup fronts (classes 4 and 5, one list)
+            MfArgs g = d->args(P, l, 4, nullptr, x);
+            g.count = n;
+            hipLaunchKernelGGL(mf_backward_level, dim3(n), dim3(kMfBlock), P.lds_max(P.lds_bwd, l, 4, kClasses), s, g);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (P.n_fold > 0) {   // folded landmarks last: their rows are poses, final by now

@@ -143,7 +143,7 @@ struct HostMf {
                     l1[i] = (v(rec[0] >= 0 ? rec[0] + 2 * g + 1 : rec[0]) - l0[i] * l10) / l11;
                     Lc[2 + t + g] = l0[i];
                     Lc[mc + 2 + t + g] = l1[i];
-                    pos[i] = ((rec[6] >> 12) & 63) + g;
+                    pos[i] = ((rec[6] >> kFoldPosShift) & kFoldPosMask) + g;
                     cl[i] = rec[7];   // the landmark (its L offset)
                     fwv[s][pos[i]] -= l0[i] * y0 + l1[i] * y1;
                 }

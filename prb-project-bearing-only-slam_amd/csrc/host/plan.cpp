@@ -968,13 +968,14 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
         std::vector<int32_t> w(F.child_ptr.begin(), F.child_ptr.end() - 1);
         for (int s = 0; s < ns; ++s) if (F.parent[s] >= 0) F.child[w[F.parent[s]]++] = s;
     }
-    // folding (Schur ordering): a parent factored by one wavefront takes all its landmark children
-    // (2-column leaves with m <= kMfWaveMaxM) into its own front; children lists are ascending, so
-    // the landmark supernodes (ids < n_fold_cand) come first
+    // folding (Schur ordering): a parent factored by one wavefront or one blocked workgroup
+    // (m <= kMfBlkMaxM) takes all its landmark children (2-column leaves with m <= kMfWaveMaxM) into
+    // its own front; children lists are ascending, so the landmark supernodes (ids < n_fold_cand)
+    // come first
     F.fold_cnt.assign(ns, 0);
     std::vector<char> folded(ns, 0);
     for (int p = 0; p < ns && n_fold_cand > 0; ++p) {
-        if (F.k[p] + F.r[p] > kMfWaveMaxM) continue;
+        if (F.k[p] + F.r[p] > kMfBlkMaxM) continue;
         int nf = 0;
         bool ok = true;
         for (int ci = F.child_ptr[p]; ci < F.child_ptr[p + 1]; ++ci) {
@@ -1060,7 +1061,7 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
     // t, t + 1, t + 2 (the pose's x, y, theta dofs) at consecutive positions of the parent front —
     // (parents in id order, their folded children in child-list order): {src (t, 0), src (t, 1),
     // src (0, 0), src (1, 0), src (1, 1), col0[c], t | r[c] << 6 | (row t's position in the parent
-    // front) << 12 | (c's index in the chunk) << 18, L_off[c]}; src = block-array index of the front
+    // front) << kFoldPosShift | (c's index in the chunk) << kFoldLmShift, L_off[c]}; src = block-array index of the front
     // entry (-1: structurally zero, -2: another rank's); the group's 6 entries (t + g, j) are the
     // pose-landmark block's values src (t, 0) + 2 g + j
     F.fold_cptr.assign(ns + 1, 0);
@@ -1096,7 +1097,8 @@ int build_multifrontal(const Graph& g, int NP, Plan& P, const std::vector<int32_
                     if (!pos_ok || !src_ok) { err = "multifrontal: folded pose rows not one block"; return BOS_ERR_INVALID; }
                 }
                 const int32_t rec[kFoldRec] = {b0, src[2 + t + mc], src[0], src[1], src[1 + mc], F.col0[c],
-                                               t | rc << 6 | rm[t] << 12 | chunk_lms << 18, (int32_t)F.L_off[c]};
+                                               t | rc << 6 | rm[t] << kFoldPosShift | chunk_lms << kFoldLmShift,
+                                               (int32_t)F.L_off[c]};
                 F.fold_rec.insert(F.fold_rec.end(), rec, rec + kFoldRec);
             }
             chunk_rows += ng;

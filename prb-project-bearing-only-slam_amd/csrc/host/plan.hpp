@@ -146,8 +146,14 @@ struct OrderingReport {
 //  - L panels are m x k column-major (entries above the diagonal unused).
 constexpr int kMfWaveMaxM = 64;
 constexpr int kMfFlowMaxM = 48;   // fronts of the dataflow factor launch (hip/multifrontal.hip kFlowMaxM)
+constexpr int kMfBlkMaxM = 128;   // fronts of 65-128 rows: one workgroup, the front in LDS, blocked on MFMA
+                                  // (hip/multifrontal.hip mf_factor_blk); landmarks fold into them too
 constexpr int kFoldChunk = 64;   // folded row groups per chunk (one per lane)
 constexpr int kFoldRec = 8;      // ints per folded row group (the 3 rows of one observing pose)
+// fold record word 6: t (row of the landmark's update rows, 6 bits) | r[c] << 6 (6 bits) | the row's
+// position in the parent front << kFoldPosShift (7 bits: parents up to kMfBlkMaxM rows) | the
+// landmark's index in its chunk << kFoldLmShift (6 bits)
+constexpr int kFoldPosShift = 12, kFoldPosMask = 127, kFoldLmShift = 19;
 // landmarks per fold chunk for a parent front of size m: the device forms the chunk's W (m x 2
 // landmarks, row stride 2 cap + 1, aliasing the front's packed LDS triangle of m (m + 1) / 2
 // values) whose W W^T it accumulates with f64 MFMA, 4 columns per step (cap even: the steps read
@@ -171,7 +177,8 @@ struct Multifrontal {
     std::vector<int32_t> amap_src, amap_dst;// block-array value (BlockLayout) -> front position (see above)
     std::vector<int32_t> level_ptr, level;  // supernodes grouped by tree level (leaves first)
     // Schur ordering: landmark supernodes (k = 2, leaves) are folded into their parent's front when
-    // the parent is factored by one wavefront (m <= kMfWaveMaxM): the parent's wave eliminates them
+    // the parent is factored by one wavefront (m <= kMfWaveMaxM) or one blocked workgroup
+    // (m <= kMfBlkMaxM): the parent's wave(s) eliminate them
     // itself (no launch, no update matrix). Folded supernodes are in no level list (the parent's
     // level ignores them); fold_list holds them for the backward substitution.
     std::vector<int32_t> fold_cnt;          // per supernode: #folded children (the first of its child list)
