@@ -665,7 +665,7 @@ constexpr int kBlkMaxM = kMfBlkMaxM, kBlkNb = 16;
 constexpr int kBlkTiles = 9;   // 16 x 16 lower tiles per wave: (8 * 9 / 2 = 36 for 128 rows) / 4 waves
 // dynamic LDS of a front of m rows: F (m x m), w (kBlkMaxM), the fold's chunk y and landmark count,
 // the panel's column broadcast (kBlkNb)
-inline int blk_lds_bytes(int m) { return (m * m + kBlkMaxM + 2 * fold_chunk_landmarks(kBlkMaxM) + 2 + kBlkNb) * 8; }
+inline int blk_lds_bytes(int m) { return (m * m + kBlkMaxM + 2 * fold_chunk_landmarks(kBlkMaxM) + 2 + 2 * kBlkNb) * 8; }
 // children whose update matrices the blocked kernel prefetches (values and front positions, kBlkXU per
 // thread: r <= 63), issued before the fold; more (or larger) children take the plain loop
 constexpr int kBlkXCh = 4, kBlkXU = 8;
@@ -688,6 +688,7 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
     for (int u = 0; u < kBlkTiles; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
     wacc = 0.0;
     for (int e = tid; e < m * WS; e += kMfBlock) W[e] = 0.0;
+    if (tid < 2 * cap) ybuf[tid] = 0.0;
     const int ch0 = a.fold_cptr[s], ch1 = a.fold_cptr[s + 1];
     int nbad = 0;
     ChunkTable tb;
@@ -765,13 +766,36 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
                 ybuf[2 * lml + 1] = y1;
             }
             const int nl = __builtin_amdgcn_readlane(lml, ncur - 1) + 1;   // landmarks of this chunk
-            if (lane == 0) *nlb = nl;
+            // the 16-row blocks the chunk's W rows span (its poses are a band of the front's rows):
+            // W W^T is zero outside them
+            int lo = mine ? pos : 1 << 20, hi = mine ? pos + 2 : -1;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                lo = min(lo, __shfl_xor(lo, o));
+                hi = max(hi, __shfl_xor(hi, o));
+            }
+            if (lane == 0) {
+                nlb[0] = nl;
+                nlb[1] = lo >> 4;
+                nlb[2] = hi >> 4;
+            }
         }
         __syncthreads();
-        const int kc = 2 * *nlb;
-        if (tid < m) {   // u-vector part: -(W y) at this thread's row
+        const int kc = 2 * nlb[0], blo = nlb[1], bhi = nlb[2];
+        // The chunk's W columns past kc are zero (never written in this chunk, cleared after the last)
+        // and y is finite there (zeroed before the first chunk), so both loops run over all 2 cap
+        // columns with every LDS read issued up front: the same sums in the same order (the extra
+        // terms add exact zeros), one LDS latency instead of one per column.
+        if (tid < m && (tid >> 4) >= blo && (tid >> 4) <= bhi) {   // u-vector part: -(W y) at this thread's row
+            double wr[2 * cap], yr[2 * cap];
+#pragma unroll
+            for (int q = 0; q < 2 * cap; ++q) {
+                wr[q] = W[tid * WS + q];
+                yr[q] = ybuf[q];
+            }
             double wsum = 0.0;
-            for (int q = 0; q < kc; ++q) wsum += W[tid * WS + q] * ybuf[q];
+#pragma unroll
+            for (int q = 0; q < 2 * cap; ++q) wsum += wr[q] * yr[q];
             wacc -= wsum;
         }
         // W W^T, 4 columns per MFMA step: tile (bi, bj) of wave + 4 u; lane l feeds row 16 b + (l & 15),
@@ -779,17 +803,23 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
 #pragma unroll
         for (int u = 0; u < kBlkTiles; ++u) {
             const int q = wave + 4 * u;
-            if (q < ntiles) {
-                int bi = 0;
-                while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
-                const int bj = q - bi * (bi + 1) / 2;
-                const int ra = 16 * bi + (lane & 15), rb = 16 * bj + (lane & 15);
-                for (int st = 0; 4 * st < kc; ++st) {
+            int bi = 0;
+            while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+            const int bj = q - bi * (bi + 1) / 2;
+            if (q < ntiles && bi <= bhi && bj >= blo) {   // (uniform) tiles the chunk's W rows reach
+                const int ra = min(16 * bi + (lane & 15), m - 1), rb = min(16 * bj + (lane & 15), m - 1);
+                const bool oka = 16 * bi + (lane & 15) < m, okb = 16 * bj + (lane & 15) < m;
+                double av[cap / 2], bv[cap / 2];
+#pragma unroll
+                for (int st = 0; st < cap / 2; ++st) {
                     const int cc = 4 * st + (lane >> 4);
-                    const double av = ra < m ? W[ra * WS + cc] : 0.0;
-                    const double bv = rb < m ? W[rb * WS + cc] : 0.0;
-                    acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[u], 0, 0, 0);
+                    av[st] = W[ra * WS + cc];
+                    bv[st] = W[rb * WS + cc];
                 }
+#pragma unroll
+                for (int st = 0; st < cap / 2; ++st)
+                    if (4 * st < kc)   // (uniform)
+                        acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(oka ? av[st] : 0.0, okb ? bv[st] : 0.0, acc[u], 0, 0, 0);
             }
         }
         __syncthreads();
@@ -810,11 +840,13 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
     const int s = a.level[blockIdx.x];
     const int k = a.k[s], r = a.r[s], m = k + r;   // m <= kBlkMaxM (mf_create / the launch check it)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    double* F = lds;                  // m x m, column-major
-    double* w = lds + m * m;          // right-hand side, then the forward step's results
-    double* ybuf = w + kBlkMaxM;      // the fold's y of one chunk (2 per landmark)
-    int* nlb = reinterpret_cast<int*>(ybuf + 2 * fold_chunk_landmarks(kBlkMaxM));
-    double* colbuf = ybuf + 2 * fold_chunk_landmarks(kBlkMaxM) + 2;
+    // LDS: the small buffers first (fixed, 16-byte aligned offsets), then the front
+    double* colbuf = lds;                                             // panel pair broadcast (kBlkNb pairs)
+    double* ybuf = colbuf + 2 * kBlkNb;                               // the fold's y of one chunk
+    int* nlb = reinterpret_cast<int*>(ybuf + 2 * fold_chunk_landmarks(kBlkMaxM));   // chunk: landmarks, row blocks
+    double* w = ybuf + 2 * fold_chunk_landmarks(kBlkMaxM) + 2;        // right-hand side, then the forward results
+    double* F = w + kBlkMaxM;                                         // m x m, column-major
+    static_assert((2 * kBlkNb + 2 * fold_chunk_landmarks(kBlkMaxM) + 2 + kBlkMaxM) % 2 == 0, "F 16-byte aligned");
     const int c0 = a.col0[s];
     const int nfold = a.fold_cnt[s];
     // the non-folded children (pose separators, typically 2): their update matrices and u-vectors,
@@ -940,34 +972,61 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
                 pb[c] = vb ? pb[c] : 0.0;
             }
             double wa = va ? w[ia] : 0.0, wb = vb ? w[ib] : 0.0;
+            // two pivots per step (as factor_front_reg): column j + 1 brought up to date in registers,
+            // both columns' panel rows through ONE LDS broadcast as pairs, then a rank-2 update
 #pragma unroll
-            for (int j = 0; j < kBlkNb; ++j) {
-                if (j < nb) {   // uniform
+            for (int j = 0; j < kBlkNb; j += 2) {
+                if (j + 1 < nb) {   // uniform
+                    double d0 = readlane_d(pa[j], j);
+                    const bool bad0 = !(d0 > 0.0);
+                    nbad += bad0;
+                    d0 = bad0 ? 1e-300 : d0;
+                    const double inv0 = rsqrt_nr(d0), l00 = d0 * inv0;
+                    const double la0 = lane < j ? 0.0 : lane == j ? l00 : pa[j] * inv0;   // L[i, p0 + j]
+                    const double lb0 = pb[j] * inv0;
+                    const double lj1 = readlane_d(la0, j + 1);                           // L[p0 + j + 1, p0 + j]
+                    const double fa = fma(-la0, lj1, pa[j + 1]), fb = fma(-lb0, lj1, pb[j + 1]);
+                    double d1 = readlane_d(fa, j + 1);
+                    const bool bad1 = !(d1 > 0.0);
+                    nbad += bad1;
+                    d1 = bad1 ? 1e-300 : d1;
+                    const double inv1 = rsqrt_nr(d1), l11 = d1 * inv1;
+                    const double la1 = lane < j + 1 ? 0.0 : lane == j + 1 ? l11 : fa * inv1;
+                    const double lb1 = fb * inv1;
+                    pa[j] = la0;
+                    pb[j] = lb0;
+                    pa[j + 1] = la1;
+                    pb[j + 1] = lb1;
+                    if (lane < kBlkNb) reinterpret_cast<double2*>(colbuf)[lane] = make_double2(la0, la1);
+                    const double y0 = readlane_d(wa, j) * inv0;   // forward steps
+                    wa = lane == j ? y0 : lane > j ? fma(-la0, y0, wa) : wa;
+                    wb = fma(-lb0, y0, wb);
+                    const double y1 = readlane_d(wa, j + 1) * inv1;
+                    wa = lane == j + 1 ? y1 : lane > j + 1 ? fma(-la1, y1, wa) : wa;
+                    wb = fma(-lb1, y1, wb);
+                    wave_sync();
+                    double2 cbv[kBlkNb];
+#pragma unroll
+                    for (int c = j + 2; c < kBlkNb; ++c) cbv[c] = reinterpret_cast<const double2*>(colbuf)[c];
+#pragma unroll
+                    for (int c = j + 2; c < kBlkNb; ++c) {
+                        pa[c] = fma(-la1, cbv[c].y, fma(-la0, cbv[c].x, pa[c]));
+                        pb[c] = fma(-lb1, cbv[c].y, fma(-lb0, cbv[c].x, pb[c]));
+                    }
+                    __builtin_amdgcn_wave_barrier();   // the next step's broadcast stays after these reads
+                } else if (j < nb) {   // the panel's last column (odd nb): nothing left to update
                     double d = readlane_d(pa[j], j);
                     const bool bad = !(d > 0.0);
                     nbad += bad;
                     d = bad ? 1e-300 : d;
                     const double inv = rsqrt_nr(d), ljj = d * inv;
-                    // L[i, p0 + j]; rows above the pivot (lanes < j) hold upper entries: zero
                     const double la = lane < j ? 0.0 : lane == j ? ljj : pa[j] * inv;
                     const double lb = pb[j] * inv;
                     pa[j] = la;
                     pb[j] = lb;
-                    // the column's panel rows broadcast through LDS (one write, independent reads)
-                    if (lane < kBlkNb) colbuf[lane] = la;
-                    const double y = readlane_d(wa, j) * inv;   // forward step: y_j = w_j / L_jj
+                    const double y = readlane_d(wa, j) * inv;
                     wa = lane == j ? y : lane > j ? fma(-la, y, wa) : wa;
                     wb = fma(-lb, y, wb);
-                    wave_sync();
-                    double cbv[kBlkNb];
-#pragma unroll
-                    for (int c = j + 1; c < kBlkNb; ++c) cbv[c] = colbuf[c];   // L[p0 + c, p0 + j]
-#pragma unroll
-                    for (int c = j + 1; c < kBlkNb; ++c) {
-                        pa[c] = fma(-la, cbv[c], pa[c]);
-                        pb[c] = fma(-lb, cbv[c], pb[c]);
-                    }
-                    __builtin_amdgcn_wave_barrier();   // the next pivot's broadcast stays after these reads
                 }
             }
 #pragma unroll
@@ -995,11 +1054,21 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
             const int bj = q - bi * (bi + 1) / 2;
             const int ra = t0 + 16 * bi + (lane & 15), rb = t0 + 16 * bj + (lane & 15);
             dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-            for (int kk = 0; kk < nb; kk += 4) {
-                const int cc = kk + (lane >> 4);
-                const double av = cc < nb && ra < m ? F[ra + (p0 + cc) * m] : 0.0;
-                const double bv = cc < nb && rb < m ? F[rb + (p0 + cc) * m] : 0.0;
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            // every operand read issued up front (clamped positions, masked values), then the MFMAs
+            double av[kBlkNb / 4], bv[kBlkNb / 4];
+#pragma unroll
+            for (int st = 0; st < kBlkNb / 4; ++st) {
+                const int cc = min(4 * st + (lane >> 4), nb - 1);
+                av[st] = F[min(ra, m - 1) + (p0 + cc) * m];
+                bv[st] = F[min(rb, m - 1) + (p0 + cc) * m];
+            }
+#pragma unroll
+            for (int st = 0; st < kBlkNb / 4; ++st) {
+                if (4 * st < nb) {   // (uniform)
+                    const bool okc = 4 * st + (lane >> 4) < nb;
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(okc && ra < m ? av[st] : 0.0, okc && rb < m ? bv[st] : 0.0,
+                                                               acc, 0, 0, 0);
+                }
             }
             const int col = t0 + 16 * bj + (lane & 15);
 #pragma unroll
@@ -1700,13 +1769,17 @@ __device__ __forceinline__ void factor_front_pan(const MfArgs& a, int s, double*
 #endif
 constexpr bool kPanel48 = BOS_MF_PAN != 0;
 #ifndef BOS_MF_PAN_KP
-#define BOS_MF_PAN_KP 16
+#define BOS_MF_PAN_KP 24
 #endif
 constexpr int kPanelKP = BOS_MF_PAN_KP;
-// waves per SIMD the panel kernel is compiled for: 4 (<= 128 VGPRs; its LDS, ~10 KB per wave, allows 15
-// waves per CU) against mf_factor_reg<48>'s 3 (147 VGPRs)
+// waves per SIMD the panel kernel is compiled for. Its register peak is the fold (the panel's rows
+// alone take 92 VGPRs, the fold 132), so it stays at mf_factor_reg<48>'s 3 waves per SIMD; bounded to 4
+// it spills 3 registers (14 in fp64) and measured no faster. Measured (config 3, tools/gn_ab.py, two
+// rounds, profiles/r06_panel_ab.txt): solve 439.6 / 442.8 us with mf_factor_reg, 439.0 / 439.8 with
+// 16-column panels at 4 waves, 433.7 / 432.0 with 24 columns at 3 waves (one panel for most level-0
+// fronts, k ~ 18), 433.6 / 434.4 with 32.
 #ifndef BOS_MF_PAN_WAVES
-#define BOS_MF_PAN_WAVES 4
+#define BOS_MF_PAN_WAVES 3
 #endif
 
 template <int MAXM, int KP, bool F32>
@@ -2059,8 +2132,8 @@ struct MfDevice {
     bool blk = false;             // mf_factor_blk may take its (up to 132 KB of) dynamic LDS
     // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
     // the level's other classes
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t side = nullptr, side2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
     static constexpr int tiny16 = 256;   // class-16 launches of at most this many fronts go to the side stream too
     Prog prog[2];                 // [0]: own (or every front), [1]: the replicated top (sharded only)
     int8_t *fid_f = nullptr, *fid_b = nullptr;   // flow membership: factor, backward
@@ -2335,8 +2408,10 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
         (rc = up(&d->fold_chunk, F.fold_chunk, err)) || (rc = up(&d->fold_rec, F.fold_rec, err)))
         return rc;
     if (hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&d->side2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_join2, hipEventDisableTiming) != hipSuccess) {
         err = "side stream creation failed (multifrontal)";
         return -2;
     }
@@ -2366,7 +2441,9 @@ void mf_destroy(MfDevice* d) {
         if (b) (void)hipFree(b);
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
     if (d->ev_join) (void)hipEventDestroy(d->ev_join);
+    if (d->ev_join2) (void)hipEventDestroy(d->ev_join2);
     if (d->side) (void)hipStreamDestroy(d->side);
+    if (d->side2) (void)hipStreamDestroy(d->side2);
     delete d;
 }
 
@@ -2382,11 +2459,22 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
     for (int l = 0; l < std::min(P.flow_lev0, d->nlevels); ++l) {
         int n;
         const bool fork = d->side && P.count(l, 3) > 0;
+        // the level's blocked fronts (config 2's separators: a few workgroups, each one latency-bound
+        // front) on a second side stream, beside the wave fronts instead of after them
+        const bool fork2 = d->side2 && d->blk && P.count(l, 4) > 0;
         // a handful of class-16 fronts (one latency-bound round, negligible load) follow them there
         const bool tiny16 = fork && P.count(l, 0) <= d->tiny16;
+        if (fork || fork2) {
+            if ((e = hipEventRecord(d->ev_fork, s)) != hipSuccess) return e;
+        }
+        if (fork2) {
+            if ((e = hipStreamWaitEvent(d->side2, d->ev_fork, 0)) != hipSuccess) return e;
+            hipLaunchKernelGGL((mf_factor_blk<F32>), dim3(P.count(l, 4)), dim3(kMfBlock), P.lds_blk[l], d->side2,
+                               d->args(P, l, 4, A, x));
+            if ((e = hipEventRecord(d->ev_join2, d->side2)) != hipSuccess) return e;
+        }
         if (fork) {
-            if ((e = hipEventRecord(d->ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(d->side, d->ev_fork, 0)) != hipSuccess)
-                return e;
+            if ((e = hipStreamWaitEvent(d->side, d->ev_fork, 0)) != hipSuccess) return e;
             hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(P.count(l, 3)), dim3(64), 0, d->side, d->args(P, l, 3, A, x));
             if (tiny16 && (n = P.count(l, 0)))
                 hipLaunchKernelGGL((mf_factor_reg<16, F32>), dim3(n), dim3(64), 0, d->side, d->args(P, l, 0, A, x));
@@ -2404,9 +2492,10 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
         if ((n = P.count(l, 3)) && !fork)
             hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
         if (fork && (e = hipStreamWaitEvent(s, d->ev_join, 0)) != hipSuccess) return e;
+        if (fork2 && (e = hipStreamWaitEvent(s, d->ev_join2, 0)) != hipSuccess) return e;
         // larger fronts: up to kBlkMaxM rows the blocked workgroup kernel (MFMA; folds; forward step fused),
         // above it (fallback plans) the unblocked workgroup kernel in global scratch and its forward step
-        for (int c = 4; c < kClasses; ++c) {
+        for (int c = fork2 ? 5 : 4; c < kClasses; ++c) {
             if (!(n = P.count(l, c))) continue;
             if (c == 4 && d->blk) {
                 hipLaunchKernelGGL((mf_factor_blk<F32>), dim3(n), dim3(kMfBlock), P.lds_blk[l], s, d->args(P, l, 4, A, x));

@@ -31,12 +31,17 @@ for name, A, labels in (("factor", st[0], ["fold", "assemble", "wait", "extend",
     t0 = A[ok, 0].min()
     print(f"{name}: fronts {ok.sum()}, span {(end[ok].max() - t0) / 100:.1f} us")
     print(f"{'lvl':>3} {'fronts':>6} {'k':>4} {'r':>4} {'start':>7} {'end':>7} {'lat':>6} " + " ".join(f"{x:>8}" for x in labels))
+    big = meta[:, 1] + meta[:, 2] > 64   # fronts of the blocked workgroup kernel (marked "b")
     for l in sorted(set(lev[ok])):
-        sel = ok & (lev == l)
-        B = A[sel][:, :len(labels) + 1].astype(float)
-        B[B == 0] = np.nan
-        d = np.diff(B, axis=1) / 100.0
-        med = np.nanmedian(d, axis=0)
-        print(f"{l:3d} {sel.sum():6d} {np.median(meta[sel, 1]):4.0f} {np.median(meta[sel, 2]):4.0f} "
-              f"{(A[sel, 0].min() - t0) / 100:7.1f} {(end[sel].max() - t0) / 100:7.1f} "
-              f"{np.median(end[sel] - A[sel, 0]) / 100:6.2f} " + " ".join(f"{v:8.2f}" for v in med))
+        for kind in ((False, True) if (ok & (lev == l) & big).any() else (None,)):
+            sel = ok & (lev == l) & (True if kind is None else (big == kind))
+            if not sel.any():
+                continue
+            B = A[sel][:, :len(labels) + 1].astype(float)
+            B[B == 0] = np.nan
+            d = np.diff(B, axis=1) / 100.0
+            med = np.nanmedian(d, axis=0)
+            tag = "b" if kind else " "
+            print(f"{l:2d}{tag} {sel.sum():6d} {np.median(meta[sel, 1]):4.0f} {np.median(meta[sel, 2]):4.0f} "
+                  f"{(A[sel, 0].min() - t0) / 100:7.1f} {(end[sel].max() - t0) / 100:7.1f} "
+                  f"{np.median(end[sel] - A[sel, 0]) / 100:6.2f} " + " ".join(f"{v:8.2f}" for v in med))
