@@ -125,7 +125,7 @@ template <typename T> __device__ __forceinline__ void odo_fetch_data(const LinPa
     const int k = o.ent >> 1;
 #pragma unroll
     for (int v = 0; v < 3; ++v) o.z[v] = P.o_z[3 * k + v];
-    const V2<T>* u = (const V2<T>*)(P.o_om + 6 * k);
+    const V2<T>* u = (const V2<T>*)(P.o_om + P.om_stride * k);
 #pragma unroll
     for (int v = 0; v < 3; ++v) { const V2<T> q = u[v]; o.u[2 * v] = q.x; o.u[2 * v + 1] = q.y; }
 }
@@ -423,8 +423,17 @@ __device__ __forceinline__ void landmark_bearing(const LinParams<T>& P, const V4
 template <typename T, bool HAS_W>
 __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int g, unsigned long long* st) {
     if (g >= P.n_lm_lanes) return;
-    const int l = P.ll_lm[g];
-    const int n = P.ll_cnt[g];
+    int l, n, p0;
+    if (P.ll_hdr) {   // (uniform: one value per launch)
+        const int2 h = P.ll_hdr[g];
+        l = h.x & 0xfffff;
+        n = (int)((uint32_t)h.x >> 20);
+        p0 = h.y;
+    } else {
+        l = P.ll_lm[g];
+        n = P.ll_cnt[g];
+        p0 = P.ll_run ? P.ll_run[g] : -1;
+    }
     const int sl = P.lw_base[g >> 6] + (g & 63);
     const int S = P.lw_stride[g >> 6];
     const int jl = n > 0 ? n - 1 : 0;
@@ -432,7 +441,6 @@ __device__ __forceinline__ void landmark_lane(const LinParams<T>& P, int g, unsi
     const V2<T> Lm = load2(P.lc + 2 * l);
     T hl[3] = {0, 0, 0}, gl[2] = {0, 0};
     const T* zp = P.lb_z;
-    const int p0 = P.ll_run ? P.ll_run[g] : -1;
     if (p0 >= 0) {
         // consecutive poses p0 + j: every load of the lane is independent of the others (one latency
         // per pair instead of the index -> pose chain). Paired registers, one pair ahead.

@@ -57,7 +57,9 @@ template <typename T> struct LinParams {
     const int32_t* o_src;
     const int32_t* o_dst;
     const T* o_z;             // [M_o][3]
-    const T* o_om;            // [M_o][6] upper triangle (00, 01, 02, 11, 12, 22)
+    const T* o_om;            // [M_o][6] upper triangle (00, 01, 02, 11, 12, 22), edge k's at om_stride k
+    int om_stride;            // 6, or 0 when every edge carries the same information (one row, read by all:
+                              // the reference dataset's and the synthetic worlds' diag(500, 500, 5000))
     // landmark lanes
     const int32_t* lw_base;   // [waves + 1]
     const int32_t* lw_stride; // [waves]
@@ -68,6 +70,9 @@ template <typename T> struct LinParams {
     // repeats; BlockLayout::lm_lane_run), else -1. Such a lane reads no index records: its pose
     // gathers depend on no load. Null: every lane reads its records.
     const int32_t* ll_run;
+    // [NL] per lane {landmark | count << 20, ll_run's value}: the three headers in one load (set when
+    // they fit; ll_lm / ll_cnt / ll_run are then null)
+    const int2* ll_hdr;
     const T* lb_z;            // [slots] measured bearing
     const T* lb_w;
     // outputs

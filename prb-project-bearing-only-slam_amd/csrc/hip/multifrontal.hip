@@ -1768,6 +1768,11 @@ __device__ __forceinline__ void factor_front_pan(const MfArgs& a, int s, double*
 #define BOS_MF_PAN 1
 #endif
 constexpr bool kPanel48 = BOS_MF_PAN != 0;
+// the class-64 level launches too (config 2's separators of 49-64 rows; config 3's side-stream class)
+#ifndef BOS_MF_PAN64
+#define BOS_MF_PAN64 1
+#endif
+constexpr bool kPanel64 = BOS_MF_PAN64 != 0;
 #ifndef BOS_MF_PAN_KP
 #define BOS_MF_PAN_KP 24
 #endif
@@ -1783,7 +1788,7 @@ constexpr int kPanelKP = BOS_MF_PAN_KP;
 #endif
 
 template <int MAXM, int KP, bool F32>
-__global__ __launch_bounds__(64, BOS_MF_PAN_WAVES) void mf_factor_pan(const MfArgs a) {
+__global__ __launch_bounds__(64, MAXM > 48 ? 2 : BOS_MF_PAN_WAVES) void mf_factor_pan(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * KP];
     __shared__ __attribute__((aligned(16))) double wv[MAXM];
@@ -2475,7 +2480,11 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
         }
         if (fork) {
             if ((e = hipStreamWaitEvent(d->side, d->ev_fork, 0)) != hipSuccess) return e;
-            hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(P.count(l, 3)), dim3(64), 0, d->side, d->args(P, l, 3, A, x));
+            if (kPanel64)
+                hipLaunchKernelGGL((mf_factor_pan<64, kPanelKP, F32>), dim3(P.count(l, 3)), dim3(64), 0, d->side,
+                                   d->args(P, l, 3, A, x));
+            else
+                hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(P.count(l, 3)), dim3(64), 0, d->side, d->args(P, l, 3, A, x));
             if (tiny16 && (n = P.count(l, 0)))
                 hipLaunchKernelGGL((mf_factor_reg<16, F32>), dim3(n), dim3(64), 0, d->side, d->args(P, l, 0, A, x));
             if ((e = hipEventRecord(d->ev_join, d->side)) != hipSuccess) return e;
@@ -2489,8 +2498,12 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
             else
                 hipLaunchKernelGGL((mf_factor_reg<48, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 2, A, x));
         }
-        if ((n = P.count(l, 3)) && !fork)
-            hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
+        if ((n = P.count(l, 3)) && !fork) {
+            if (kPanel64)
+                hipLaunchKernelGGL((mf_factor_pan<64, kPanelKP, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
+            else
+                hipLaunchKernelGGL((mf_factor_reg<64, F32>), dim3(n), dim3(64), 0, s, d->args(P, l, 3, A, x));
+        }
         if (fork && (e = hipStreamWaitEvent(s, d->ev_join, 0)) != hipSuccess) return e;
         if (fork2 && (e = hipStreamWaitEvent(s, d->ev_join2, 0)) != hipSuccess) return e;
         // larger fronts: up to kBlkMaxM rows the blocked workgroup kernel (MFMA; folds; forward step fused),

@@ -98,12 +98,13 @@ struct bos_solver {
     // J+H work lists (host/plan.hpp BlockLayout)
     int32_t *pw_base = nullptr, *pw_stride = nullptr, *pl_cnt = nullptr, *lw_base = nullptr, *lw_stride = nullptr, *ll_cnt = nullptr, *ll_lm = nullptr, *po_ptr = nullptr, *po_ent = nullptr, *po_oth = nullptr, *po_blk = nullptr, *csr_src = nullptr,
             *elim_ref = nullptr;
-    int32_t *pb_idx = nullptr, *lb_idx = nullptr, *ll_run = nullptr;
+    int32_t *pb_idx = nullptr, *lb_idx = nullptr, *ll_run = nullptr, *ll_hdr = nullptr;
     void *pb_z = nullptr, *pb_w = nullptr, *lb_z = nullptr, *lb_w = nullptr;
     int pose_blocks = 0;
     // odometry
     int32_t *o_src = nullptr, *o_dst = nullptr;
     void *o_z = nullptr, *o_om = nullptr;
+    int om_stride = 6;                         // 0: every edge has the same information (LinParams)
     // node layout
     int32_t* node_dof = nullptr;
     // system
@@ -231,8 +232,10 @@ template <typename T> bos::dev::LinParams<T> lin_params(const bos_solver* s) {
     p.pb_idx = s->pb_idx; p.pb_z = (const T*)s->pb_z; p.pb_w = (const T*)s->pb_w;
     p.po_ptr = s->po_ptr; p.po_ent = s->po_ent; p.po_oth = s->po_oth; p.po_blk = s->po_blk;
     p.o_src = s->o_src; p.o_dst = s->o_dst; p.o_z = (const T*)s->o_z; p.o_om = (const T*)s->o_om;
+    p.om_stride = s->om_stride;
     p.lw_base = s->lw_base; p.lw_stride = s->lw_stride; p.ll_cnt = s->ll_cnt; p.ll_lm = s->ll_lm;
     p.lb_idx = s->lb_idx; p.lb_z = (const T*)s->lb_z; p.lb_w = (const T*)s->lb_w; p.ll_run = s->ll_run;
+    p.ll_hdr = reinterpret_cast<const int2*>(s->ll_hdr);
     p.hval = (T*)s->d_val;
     p.b = (T*)s->d_b;
     p.off_ldiag = (int)P.blk.off_ldiag; p.off_pl = (int)P.blk.off_pl; p.off_pp = (int)P.blk.off_pp;
@@ -1110,7 +1113,7 @@ int bos_destroy(bos_solver* s) {
     drop_graph(s);
     for (void** f : s->jh_fields) *f = nullptr;   // inside jh_arena
     void* bufs[] = {s->d_pose, s->d_lm, s->d_pc, s->d_pth, s->d_lc, s->pw_base, s->pw_stride, s->pl_cnt, s->lw_base, s->lw_stride, s->ll_cnt, s->ll_lm,
-                    s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w, s->ll_run,
+                    s->po_ptr, s->po_ent, s->po_oth, s->po_blk, s->csr_src, s->elim_ref, s->pb_idx, s->pb_z, s->pb_w, s->lb_idx, s->lb_z, s->lb_w, s->ll_run, s->ll_hdr,
                     s->o_src, s->o_dst, s->o_z, s->o_om, s->node_dof, s->d_val, s->obs ? nullptr : s->d_b, s->d_sys,
                     s->d_val64, s->d_csr64,
                     s->d_rhs, s->d_rowptr, s->d_colind, s->d_Lptr, s->d_Lind, s->d_pivQ,
@@ -1314,8 +1317,25 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
                 if (B.lane_pose[i] >= 0 && B.po_chain[B.lane_pose[i]]) plc[i * B.lpp] |= bos::dev::kOdoChain;
         stage.add(&s->pw_base, B.pose_lanes.w_base); stage.add(&s->pl_cnt, plc);
         stage.add(&s->pw_stride, B.pose_lanes.w_stride); stage.add(&s->lw_stride, B.lm_lanes.w_stride);
-        stage.add(&s->lw_base, B.lm_lanes.w_base); stage.add(&s->ll_cnt, B.lm_lanes.cnt);
-        stage.add(&s->ll_lm, B.lm_lane_lm); stage.add(&s->ll_run, B.lm_lane_run);
+        stage.add(&s->lw_base, B.lm_lanes.w_base);
+        {   // a landmark lane's header in one 8-byte record {landmark | count << 20, first pose of the
+            // lane's consecutive run or -1} when they fit (one load instead of three; LinParams::ll_hdr)
+            const size_t nl = B.lm_lane_lm.size();
+            bool fits = nl < ((size_t)1 << 20);
+            for (size_t g = 0; g < nl && fits; ++g)
+                fits = B.lm_lane_lm[g] >= 0 && B.lm_lane_lm[g] < (1 << 20) && B.lm_lanes.cnt[g] >= 0 && B.lm_lanes.cnt[g] < (1 << 12);
+            if (fits && nl > 0) {
+                std::vector<int32_t> hdr(2 * nl);
+                for (size_t g = 0; g < nl; ++g) {
+                    hdr[2 * g] = (int32_t)((uint32_t)B.lm_lane_lm[g] | ((uint32_t)B.lm_lanes.cnt[g] << 20));
+                    hdr[2 * g + 1] = B.lm_lane_run.empty() ? -1 : B.lm_lane_run[g];
+                }
+                stage.add(&s->ll_hdr, hdr);
+            } else {
+                stage.add(&s->ll_cnt, B.lm_lanes.cnt);
+                stage.add(&s->ll_lm, B.lm_lane_lm); stage.add(&s->ll_run, B.lm_lane_run);
+            }
+        }
         stage.add(&s->po_ptr, B.po_ptr); stage.add(&s->po_ent, po_ent); stage.add(&s->po_oth, po_oth);
         stage.add(&s->po_blk, po_blk); stage.add(&s->pb_idx, pbi); stage_Tv(&s->pb_z, pbz);
         stage.add(&s->lb_idx, lbi); stage_Tv(&s->lb_z, lbz);
@@ -1356,10 +1376,19 @@ int bos_create(const bos_problem* pb, const bos_options* opt_in, bos_solver** ou
         // one zero edge of padding (the J+H's unconditional reads of entry 0 when there is none)
         std::vector<double> oz(pb->odom_z, pb->odom_z + 3 * (size_t)s->Mo), om(6 * (size_t)s->Mo + 6, 0.0);
         oz.resize(3 * (size_t)s->Mo + 3, 0.0);
+        bool same = true;   // every edge's information equal (bit for bit): one row, om_stride 0
         for (int k = 0; k < s->Mo; ++k) {
             const double* m = pb->odom_omega + 9 * (size_t)k;
             const double u[6] = {m[0], m[1], m[2], m[4], m[5], m[8]};
-            for (int q = 0; q < 6; ++q) om[6 * (size_t)k + q] = u[q];
+            for (int q = 0; q < 6; ++q) {
+                om[6 * (size_t)k + q] = u[q];
+                same = same && std::memcmp(&om[6 * (size_t)k + q], &om[q], sizeof(double)) == 0;
+            }
+        }
+        s->om_stride = 6;
+        if (same && s->Mo > 0) {   // the J+H then reads 24 (fp32) / 48 bytes of information in all, not per edge
+            om.resize(12);
+            s->om_stride = 0;
         }
         stage.add(&s->o_src, os); stage.add(&s->o_dst, od); stage_Tv(&s->o_z, oz); stage_Tv(&s->o_om, om);
     }
