@@ -202,6 +202,14 @@ __device__ __forceinline__ void assemble_wave(const MfArgs& a, int q0_, int q1, 
     }
 }
 
+// lane l's double, broadcast to the wave (l uniform)
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __global__ __launch_bounds__(kMfBlock) void mf_factor_level(const MfArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int s = a.level[blockIdx.x];
@@ -314,6 +322,34 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if (lane == 0) t[j] = acc;
     }
+    if (k <= 64) {
+        // L11 staged in LDS (column i at stride k + 1) by all waves, then the triangular solve on
+        // wave 0 alone, lane i holding t_i: no barrier and no global load in the sequential chain
+        // (config 2's separators: k = 20-40, 16-21 us per launch with a barrier pair and a global
+        // diagonal load per column). Same operations in the same order: bit-identical x.
+        double* S = t + k;
+        for (int e = tid; e < k * k; e += kMfBlock) {
+            const int i = e / k, j = e - i * k;
+            if (j >= i) S[j + i * (k + 1)] = Ls[j + (int64_t)i * m];
+        }
+        __syncthreads();
+        if (wave) return;
+        const bool on = lane < k;
+        double ti = on ? t[lane] : 0.0;
+        const double wi = on ? a.x[c0 + lane] : 0.0;
+        const double di = on ? S[lane * (k + 2)] : 1.0;
+        double xi = 0.0;
+        for (int j = k - 1; j >= 0; --j) {
+            const double xj = readlane_d(wi - ti, j) / readlane_d(di, j);
+            if (lane == j) xi = xj;
+            if (lane < j) ti += S[j + lane * (k + 1)] * xj;
+        }
+        if (on) {
+            a.x[c0 + lane] = xi;
+            if (a.xtag[s]) tag_pair(a.xg + 2 * (int64_t)(c0 + lane), xi, *a.epoch);
+        }
+        return;
+    }
     for (int j = tid; j < k; j += kMfBlock) w[j] = a.x[c0 + j];
     __syncthreads();
     for (int j = k - 1; j >= 0; --j) {
@@ -334,12 +370,6 @@ __global__ __launch_bounds__(kMfBlock) void mf_backward_level(const MfArgs a) {
 // the (lower) front in a compile-time-indexed array; each column step broadcasts the pivot column
 // through a small LDS buffer (one store per lane, broadcast reads). LDS otherwise only stages the
 // assembly. F: packed front (MAXM (MAXM + 1) / 2), colbuf: 2 MAXM.
-__device__ __forceinline__ double readlane_d(double x, int l) {
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 
 // 1 / sqrt(d) for d > 0 in the normal range: hardware estimate refined by two Newton steps
 // (quadratic convergence: full double precision, within an ulp or two of 1.0 / sqrt(d)).
@@ -835,9 +865,7 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
 }
 
 template <bool F32>
-__global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int s = a.level[blockIdx.x];
+__device__ __forceinline__ void factor_front_blk(const MfArgs& a, const int s, double* lds) {
     const int k = a.k[s], r = a.r[s], m = k + r;   // m <= kBlkMaxM (mf_create / the launch check it)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     // LDS: the small buffers first (fixed, 16-byte aligned offsets), then the front
@@ -1093,6 +1121,12 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
         else a.u[a.u_off[s] + (i - k)] = w[i];
     }
     stamp(6);
+}
+
+template <bool F32>
+__global__ __launch_bounds__(kMfBlock) void mf_factor_blk(const MfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    factor_front_blk<F32>(a, a.level[blockIdx.x], lds);
 }
 
 // ---- dataflow (work-queue) kernels: one launch walks a whole tree range. A wavefront takes the
@@ -1787,6 +1821,12 @@ constexpr int kPanelKP = BOS_MF_PAN_KP;
 #define BOS_MF_PAN_WAVES 3
 #endif
 
+template <int MAXM, int KP> struct WaveLds {
+    double F[MAXM * (MAXM + 1) / 2];
+    double colbuf[2 * (KP > 0 ? KP : MAXM)];
+    double wv[MAXM];
+    FoldBuf fb;
+};
 template <int MAXM, int KP, bool F32>
 __global__ __launch_bounds__(64, MAXM > 48 ? 2 : BOS_MF_PAN_WAVES) void mf_factor_pan(const MfArgs a) {
     __shared__ __attribute__((aligned(16))) double F[MAXM * (MAXM + 1) / 2];
@@ -1795,6 +1835,53 @@ __global__ __launch_bounds__(64, MAXM > 48 ? 2 : BOS_MF_PAN_WAVES) void mf_facto
     __shared__ FoldBuf fb;
     factor_front_pan<MAXM, KP, F32>(a, a.level[blockIdx.x], F, colbuf, wv, &fb, threadIdx.x);
 }
+
+// One wave front of class 3, 2, 1 or 0 with its LDS at slot (mf_factor_mixb)
+template <int MAXM, int KP, bool F32>
+__device__ __forceinline__ void wave_front(const MfArgs& a, int s, char* slot, int lane) {
+    auto* L = reinterpret_cast<WaveLds<MAXM, KP>*>(slot);
+    if constexpr (KP > 0)
+        factor_front_pan<MAXM, KP, F32>(a, s, L->F, L->colbuf, L->wv, &L->fb, lane);
+    else
+        factor_front_reg<MAXM, kModeLevel, F32>(a, s, L->F, L->colbuf, L->wv, &L->fb, lane, nullptr);
+}
+
+#ifndef BOS_MF_MIXB   // (A/B builds: -DBOS_MF_MIXB=0 keeps the blocked fronts on the second side stream)
+#define BOS_MF_MIXB 1
+#endif
+constexpr bool kMixB = BOS_MF_MIXB != 0;
+
+// A level with blocked fronts (65-128 rows, config 2's separators) and few fronts in all: ONE launch
+// of four-wave workgroups instead of the blocked launch on a second side stream beside the wave
+// fronts (each level then paid a fork and a join, ~10 us per level at config 2). The first n4
+// workgroups each factor one blocked front (factor_front_blk, the whole dynamic LDS), each of the
+// others one wave front of class 3, 2, 1 or 0 on its first wave (the other three leave at once; two
+// wave fronts in one workgroup computed wrong factors). Registers are the blocked
+// path's (1 wave per SIMD), so the host uses it only when the level fits the GPU in one round (one
+// workgroup per CU); dynamic LDS max(blocked front, one class-64 front).
+template <bool F32>
+__global__ __launch_bounds__(kMfBlock) void mf_factor_mixb(const MfArgs a, const int32_t* blk_list, int n4, int4 n, int4 o) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int b = blockIdx.x;
+    if (b < n4) {   // (uniform per workgroup)
+        factor_front_blk<F32>(a, blk_list[b], lds);
+        return;
+    }
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    char* slot = reinterpret_cast<char*>(lds);
+    const int32_t* lst = a.level;
+    int i = b - n4;
+    if (i < n.w) { wave_front<64, kPanel64 ? kPanelKP : 0, F32>(a, lst[o.w + i], slot, lane); return; }
+    i -= n.w;
+    if (i < n.z) { wave_front<48, kPanel48 ? kPanelKP : 0, F32>(a, lst[o.z + i], slot, lane); return; }
+    i -= n.z;
+    if (i < n.y) { wave_front<32, 0, F32>(a, lst[o.y + i], slot, lane); return; }
+    i -= n.y;
+    if (i < n.x) wave_front<16, 0, F32>(a, lst[o.x + i], slot, lane);
+}
+constexpr int kMixbWaveLds = (int)sizeof(WaveLds<64, kPanel64 ? kPanelKP : 0>);
+
 
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
 // L panel (m x k). The rows below the supernode are ancestors' dofs, already final in x.
@@ -2134,6 +2221,7 @@ constexpr int kSolveWideLevel = BOS_MF_SOLVE_WIDE;
 constexpr int kFactorWideLevel = BOS_MF_FACTOR_WIDE;
 struct MfDevice {
     int nlevels = 0, nsuper = 0, ncu = 256;
+    bool mixb = false;            // mf_factor_mixb too (a level's blocked and wave fronts in one launch)
     bool blk = false;             // mf_factor_blk may take its (up to 132 KB of) dynamic LDS
     // a level's largest fronts (class 64: few, one latency-bound round) run on a side stream beside
     // the level's other classes
@@ -2205,7 +2293,7 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
                     if (m <= kLdsCapM) P.lds_factor[lc] = std::max(P.lds_factor[lc], m * m * 8);
                     if (c == 4) P.lds_blk[l] = std::max(P.lds_blk[l], blk_lds_bytes(m));
                     P.lds_fwd[lc] = std::max(P.lds_fwd[lc], m * 8);
-                    P.lds_bwd[lc] = std::max(P.lds_bwd[lc], 2 * k * 8);
+                    P.lds_bwd[lc] = std::max(P.lds_bwd[lc], (2 * k + (k <= 64 ? k * (k + 1) : 0)) * 8);
                 }
             }
             // longest fronts first (estimated by flops plus folded rows): the launch's tail is
@@ -2317,8 +2405,13 @@ int mf_create(const Multifrontal& F, const int8_t* owner, int rank, MfDevice** o
                                      blk_lds) == hipSuccess &&
                  hipFuncSetAttribute((const void*)mf_factor_blk<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      blk_lds) == hipSuccess;
+        d->mixb = d->blk &&
+                  hipFuncSetAttribute((const void*)mf_factor_mixb<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      blk_lds) == hipSuccess &&
+                  hipFuncSetAttribute((const void*)mf_factor_mixb<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      blk_lds) == hipSuccess;
+        (void)hipGetLastError();
         if (!d->blk) {
-            (void)hipGetLastError();
             // the plan folds landmarks into fronts of up to kMfBlkMaxM rows, which only mf_factor_blk eliminates
             for (int s = 0; s < F.nsuper; ++s)
                 if (F.k[s] + F.r[s] > kMfWaveMaxM && !F.fold_cnt.empty() && F.fold_cnt[s] > 0) {
@@ -2463,6 +2556,22 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
     if (P.ptr.empty()) return hipSuccess;
     for (int l = 0; l < std::min(P.flow_lev0, d->nlevels); ++l) {
         int n;
+        // a level with blocked fronts and few fronts in all (config 2): one launch for all of them
+        const int n4 = P.count(l, 4), nwf = P.count(l, 0, 4);
+        if (kMixB && d->mixb && n4 > 0 && n4 + nwf <= d->ncu) {
+            const int4 nw = make_int4(P.count(l, 0), P.count(l, 1), P.count(l, 2), P.count(l, 3));
+            const int4 ow = make_int4(0, P.count(l, 0), P.count(l, 0, 2), P.count(l, 0, 3));
+            hipLaunchKernelGGL((mf_factor_mixb<F32>), dim3(n4 + nwf), dim3(kMfBlock), std::max(P.lds_blk[l], kMixbWaveLds),
+                               s, d->args(P, l, 0, A, x), d->args(P, l, 4, A, x).level, n4, nw, ow);
+            if ((n = P.count(l, 5))) {   // fronts above kBlkMaxM rows (fallback plans)
+                hipLaunchKernelGGL(mf_factor_level, dim3(n), dim3(kMfBlock), P.lds_factor[l * kClasses + 5], s,
+                                   d->args(P, l, 5, A, x));
+                hipLaunchKernelGGL(mf_forward_level, dim3(n), dim3(kMfBlock), P.lds_fwd[l * kClasses + 5], s,
+                                   d->args(P, l, 5, A, x));
+            }
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            continue;
+        }
         const bool fork = d->side && P.count(l, 3) > 0;
         // the level's blocked fronts (config 2's separators: a few workgroups, each one latency-bound
         // front) on a second side stream, beside the wave fronts instead of after them

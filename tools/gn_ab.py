@@ -6,6 +6,7 @@ median device-stamped phases of 50 synchronous steps, synchronous GN it/s (bos_t
     python tools/gn_ab.py <libA.so> <libB.so> [<libC.so> ...] [rounds]
 
 A variant may carry environment settings for its process: <lib.so>@NAME=VALUE[@NAME=VALUE...].
+BOS_AB_CONFIG=c2 in the environment: config 2 (fp64 J+H and solve) instead.
 """
 import os
 import subprocess
@@ -20,8 +21,12 @@ def child(lib, label):
     import bos
     bos.LIB_PATH = os.path.abspath(lib)
     bos.ALLOW_MISSING_SYMBOLS = True
-    P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
-    S = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, device=0)
+    if os.environ.get("BOS_AB_CONFIG") == "c2":   # config 2 (fp64), bench.py --config c2's world
+        P = bos.synthetic(1000, 2000, 20)
+        S = bos.Solver(P, precision=bos.BOS_FP64, solver=bos.BOS_SOLVER_SCHUR, device=0)
+    else:
+        P = bos.synthetic(num_poses=100000, num_landmarks=200000, bearings_per_pose=10, seed=0xB05EED01 + 3)
+        S = bos.Solver(P, precision=bos.BOS_FP32, solver=bos.BOS_SOLVER_SCHUR, device=0)
     init = S.get_state()
     S.step()
     S.set_state(*init)

@@ -11,6 +11,7 @@
 #   bash tools/gpu_run.sh final TAG              the driver's order (smoke, GPU suite, bench fp32 + fp64), then
 #                                                the profile set (tools/gpu_profile.sh TAG)
 #   bash tools/gpu_run.sh c2                     bench.py --config c2 (config 2, fp64, one GPU, vs the CPU backend)
+#   bash tools/gpu_run.sh c2trace [LIB]          kernel timeline of one config-2 GN step (tools/c2_steps.py + c2_timeline.py)
 #   bash tools/gpu_run.sh ladder                 the N > 1 exchange ladder on the one GPU: two ranks with the default
 #                                                p2p, two with --exchange rccl (RCCL refuses ranks sharing a device:
 #                                                falls back to the gloo host exchange)
@@ -63,6 +64,11 @@ case $step in
       bash tools/gpu_profile.sh $1 > gpurun_out/final_profile.log 2>&1 ;;
   c2)
     timeout -k 10 300 python bench.py --config c2 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
+  c2trace)
+    lib=${1:-prb-project-bearing-only-slam_amd/lib/libbos.so}
+    BOS_LIB=$lib timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c2 -- \
+      python3 tools/c2_steps.py 20 > gpurun_out/trace_c2.log 2>&1 &&
+      python3 tools/c2_timeline.py gpurun_out/trace_c2 > gpurun_out/c2_timeline.txt 2>&1 ;;
   ladder)
     FLAGS="--same-device --steps 20 --warmup 3 --no-cpu-baseline --no-gn-other --tri-steps 0 --replay-steps 20 --cold-steps 0"
     timeout -k 10 400 python bench.py --gpus 2 $FLAGS > gpurun_out/ladder_p2p.json 2> gpurun_out/ladder_p2p.err &&
