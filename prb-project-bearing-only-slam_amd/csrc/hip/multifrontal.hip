@@ -430,9 +430,28 @@ struct FoldVals32 {
     int flags;   // block present << 0 | a00, a10, a11 present << 2, 3, 4
     double x0, x1;
 };
-template <bool F32> using FoldValsT = typename std::conditional<F32, FoldVals32, FoldVals>::type;
+// The fp64 build's values as loaded and their presence in flags (as FoldVals32): the selects are
+// applied by fold_decode when the chunk is processed, so the loads stay in flight until then (a
+// select right after the loads made the wave wait for them in the chunk that issued them, one
+// memory latency per chunk: config 2's blocked-front folds, 33 us at level 0)
+struct FoldVals64 {
+    double h[6], a00, a10, a11, x0, x1;
+    int flags;   // block present << 0 | a00, a10, a11 present << 2, 3, 4
+};
+template <bool F32> using FoldValsT = typename std::conditional<F32, FoldVals32, FoldVals64>::type;
 
-__device__ __forceinline__ FoldVals fold_decode(const FoldVals& v) { return v; }
+__device__ __forceinline__ FoldVals fold_decode(const FoldVals64& v) {
+    FoldVals d;
+    const bool blk = v.flags & 1;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) d.h[e] = blk ? v.h[e] : 0.0;
+    d.a00 = (v.flags & 4) ? v.a00 : 0.0;
+    d.a10 = (v.flags & 8) ? v.a10 : 0.0;
+    d.a11 = (v.flags & 16) ? v.a11 : 0.0;
+    d.x0 = v.x0;
+    d.x1 = v.x1;
+    return d;
+}
 __device__ __forceinline__ FoldVals fold_decode(const FoldVals32& v) {
     FoldVals d;
     const bool blk = v.flags & 1;
@@ -472,21 +491,17 @@ __device__ __forceinline__ FoldValsT<F32> fold_vals(const MfArgs& a, const int4&
     // every load unconditional (indices clamped to valid ones), the value selected afterwards: a
     // predicated load would be a branch with its wait inside, and the next chunk's values must stay
     // in flight while the current chunk is processed
+    // (selected by fold_decode, see FoldVals64)
     const int b = max(r0.x, 0);
-    double h[6];
+    FoldVals64 v;
 #pragma unroll
-    for (int e = 0; e < 6; ++e) h[e] = a.A[b + e];
-    const double a00 = a.A[max(r0.z, 0)], a10 = a.A[max(r0.w, 0)];
-    const double a11 = a.A[max(r1.x, 0)];
-    const double x0 = a.x[r1.y], x1 = a.x[r1.y + 1];   // (lanes past the groups: their last group's)
-    FoldVals v;
-#pragma unroll
-    for (int e = 0; e < 6; ++e) v.h[e] = r0.x >= 0 ? h[e] : 0.0;
-    v.a00 = r0.z >= 0 ? a00 : 0.0;
-    v.a10 = r0.w >= 0 ? a10 : 0.0;
-    v.a11 = r1.x >= 0 ? a11 : 0.0;
-    v.x0 = x0;
-    v.x1 = x1;
+    for (int e = 0; e < 6; ++e) v.h[e] = a.A[b + e];
+    v.a00 = a.A[max(r0.z, 0)];
+    v.a10 = a.A[max(r0.w, 0)];
+    v.a11 = a.A[max(r1.x, 0)];
+    v.x0 = a.x[r1.y];   // (lanes past the groups: their last group's)
+    v.x1 = a.x[r1.y + 1];
+    v.flags = (r0.x >= 0 ? 1 : 0) | (r0.z >= 0 ? 4 : 0) | (r0.w >= 0 ? 8 : 0) | (r1.x >= 0 ? 16 : 0);
     return v;
     }
 }
@@ -698,7 +713,7 @@ constexpr int kBlkTiles = 9;   // 16 x 16 lower tiles per wave: (8 * 9 / 2 = 36 
 inline int blk_lds_bytes(int m) { return (m * m + kBlkMaxM + 2 * fold_chunk_landmarks(kBlkMaxM) + 2 + 2 * kBlkNb) * 8; }
 // children whose update matrices the blocked kernel prefetches (values and front positions, kBlkXU per
 // thread: r <= 63), issued before the fold; more (or larger) children take the plain loop
-constexpr int kBlkXCh = 4, kBlkXU = 8;
+constexpr int kBlkXCh = 2, kBlkXU = 8;
 
 // The folded landmark children of a workgroup front (Schur ordering), the workgroup form of
 // fold_children: per chunk (<= kFoldChunk observing poses, <= fold_chunk_landmarks(m) landmarks)
@@ -712,7 +727,9 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
                                                  int tid, dbl4 acc[kBlkTiles], double& wacc) {
     constexpr int cap = fold_chunk_landmarks(kBlkMaxM);
     constexpr int WS = 2 * cap + 1;   // W row stride (odd: no bank conflicts)
-    const int wave = tid >> 6, lane = tid & 63;
+    // the wave index as a scalar: branches on it are uniform, so a value loaded on wave 0's path lands in
+    // its loop-carried register (a divergent branch merged the paths with copies that waited for the loads)
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int nbt = (m + 15) >> 4, ntiles = nbt * (nbt + 1) / 2;
 #pragma unroll
     for (int u = 0; u < kBlkTiles; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -722,39 +739,62 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
     const int ch0 = a.fold_cptr[s], ch1 = a.fold_cptr[s + 1];
     int nbad = 0;
     ChunkTable tb;
-    int n = 0, nn = 0;
-    int4 r0, r1, n0, n1;
-    FoldValsT<F32> v;
     auto rec = [&](int c, int cnt, int4& q0, int4& q1) {
         const int q = tb.at(c) + min(lane, max(cnt - 1, 0));
         q0 = fold_rec_load(a, q, 0);
         q1 = fold_rec_load(a, q, 1);
     };
     auto len = [&](int c) { return c < ch1 ? tb.at(c + 1) - tb.at(c) : 0; };
-    if (wave == 0) {
-        tb.load(a, ch0, lane);
-        n = len(ch0);
-        rec(ch0, n, r0, r1);
-        v = fold_vals<F32>(a, r0, r1, lane < n);
-        nn = len(ch0 + 1);
-        rec(ch0 + 1, nn, n0, n1);
+    // Wave 0 alone walks the records (the other waves wait at the barrier), so no other wave hides its
+    // memory latency: the values are loaded two chunks ahead and the records three, in two register
+    // sets that alternate by chunk (the loop is unrolled by two, so a set keeps its registers: a
+    // rotation of loop-carried registers made the compiler copy the freshly loaded values at the
+    // chunk's end, a copy that waits for the loads).
+    struct Set {
+        FoldValsT<F32> v;   // values of the chunk this set holds
+        int4 m;             // its records' second half (meta)
+        int n;              // its rows
+        int4 p0, p1;        // records of the chunk that refills the set next
+        int np;
+    } A, B;
+    // (every wave issues the record and value loads, wave 0 alone uses them: loads under a branch on
+    // the wave left the registers to be merged with the other waves' path at the branch's end — copies
+    // that waited for the loads)
+    tb.load(a, ch0, lane);
+    {
+        int4 q0;
+        A.n = len(ch0);
+        rec(ch0, A.n, q0, A.m);
+        A.v = fold_vals<F32>(a, q0, A.m, lane < A.n);
+        B.n = len(ch0 + 1);
+        rec(ch0 + 1, B.n, q0, B.m);
+        B.v = fold_vals<F32>(a, q0, B.m, lane < B.n);
+        A.np = len(ch0 + 2);
+        rec(ch0 + 2, A.np, A.p0, A.p1);
     }
+    // the prologue's loads waited for here: the loop's top is then reached only from its back edge with
+    // loads pending, and waits there for the values of two chunks ago alone (see fold_children)
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     __syncthreads();   // (W cleared)
-    for (int ch = ch0; ch < ch1; ++ch) {   // (uniform over the workgroup)
+    // chunk ch from set X; X is refilled with chunk ch + 2's values, Y's records with chunk ch + 3's
+    auto chunk = [&](int ch, Set& X, Set& Y) {
         int pos = 0, lml = 0, ncur = 0;
+        if (ch + 4 - tb.base > 63) tb.reload(a, ch, lane);
+        FoldVals d = fold_decode(X.v);
+        // the decoded values formed here, before the loads into X's registers are issued (left to
+        // the compiler, the selects sank to their uses and X.v stayed live past the new loads)
+        asm volatile("" : "+v"(d.h[0]), "+v"(d.h[1]), "+v"(d.h[2]), "+v"(d.h[3]), "+v"(d.h[4]), "+v"(d.h[5]),
+                     "+v"(d.a00), "+v"(d.a10), "+v"(d.a11), "+v"(d.x0), "+v"(d.x1));
+        const int4 q1 = X.m;
+        ncur = X.n;
+        // the records first, then the values: the memory counter retires in order, so the next
+        // chunk's wait for these records must not include these values
+        Y.np = len(ch + 3);
+        rec(ch + 3, Y.np, Y.p0, Y.p1);
+        X.v = fold_vals<F32>(a, X.p0, X.p1, lane < X.np);
+        X.m = X.p1;
+        X.n = X.np;
         if (wave == 0) {
-            if (ch + 3 - tb.base > 63) tb.reload(a, ch, lane);
-            const FoldVals d = fold_decode(v);
-            const int4 q1 = r1;
-            ncur = n;
-            // the next chunk: values now (its records arrived during this one), records of ch + 2
-            v = fold_vals<F32>(a, n0, n1, lane < nn);
-            r0 = n0;
-            r1 = n1;
-            const int n2 = len(ch + 2);
-            rec(ch + 2, n2, n0, n1);
-            n = nn;
-            nn = n2;
             const int t = q1.z & 63, rc = (q1.z >> 6) & 63;
             pos = (q1.z >> kFoldPosShift) & kFoldPosMask;
             lml = (q1.z >> kFoldLmShift) & 63;
@@ -817,15 +857,19 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
         // columns with every LDS read issued up front: the same sums in the same order (the extra
         // terms add exact zeros), one LDS latency instead of one per column.
         if (tid < m && (tid >> 4) >= blo && (tid >> 4) <= bhi) {   // u-vector part: -(W y) at this thread's row
-            double wr[2 * cap], yr[2 * cap];
-#pragma unroll
-            for (int q = 0; q < 2 * cap; ++q) {
-                wr[q] = W[tid * WS + q];
-                yr[q] = ybuf[q];
-            }
+            // (in two halves: all 4 cap reads at once held 112 registers at the kernel's peak)
             double wsum = 0.0;
 #pragma unroll
-            for (int q = 0; q < 2 * cap; ++q) wsum += wr[q] * yr[q];
+            for (int h = 0; h < 2; ++h) {
+                double wr[cap], yr[cap];
+#pragma unroll
+                for (int q = 0; q < cap; ++q) {
+                    wr[q] = W[tid * WS + h * cap + q];
+                    yr[q] = ybuf[h * cap + q];
+                }
+#pragma unroll
+                for (int q = 0; q < cap; ++q) wsum += wr[q] * yr[q];
+            }
             wacc -= wsum;
         }
         // W W^T, 4 columns per MFMA step: tile (bi, bj) of wave + 4 u; lane l feeds row 16 b + (l & 15),
@@ -860,6 +904,11 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
                 W[(pos + g) * WS + 2 * lml + 1] = 0.0;
             }
         }
+    };
+    for (int ch = ch0; ch < ch1; ch += 2) {   // (uniform over the workgroup)
+        chunk(ch, A, B);
+        if (ch + 1 >= ch1) break;   // (a break: the loop's back edge always follows chunk ch + 1)
+        chunk(ch + 1, B, A);
     }
     if (wave == 0 && nbad) atomicAdd(a.info, nbad);
 }
@@ -867,7 +916,7 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
 template <bool F32>
 __device__ __forceinline__ void factor_front_blk(const MfArgs& a, const int s, double* lds) {
     const int k = a.k[s], r = a.r[s], m = k + r;   // m <= kBlkMaxM (mf_create / the launch check it)
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     // LDS: the small buffers first (fixed, 16-byte aligned offsets), then the front
     double* colbuf = lds;                                             // panel pair broadcast (kBlkNb pairs)
     double* ybuf = colbuf + 2 * kBlkNb;                               // the fold's y of one chunk
