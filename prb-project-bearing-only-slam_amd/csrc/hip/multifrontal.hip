@@ -2376,19 +2376,22 @@ int build_prog(const Multifrontal& F, const std::vector<int8_t>& sel, int id, Pr
         }
         P.bptr[l + 1] = (int32_t)blst.size();
     }
-    // dataflow ranges: the factor flow starts at the lowest level (>= 2) from which every front of
-    // the program is <= kFlowMaxM, and above the wide levels
+    // dataflow ranges: the factor flow starts at the lowest level (>= 2) from which every front is
+    // <= kFlowMaxM, and above the wide levels. Both decided on the whole tree, not on this program's
+    // fronts: a front is then factored by the same kernel (per-level or flow) whatever the partition,
+    // and the per-level class-48 kernel (mf_factor_pan: trailing update on MFMA) and the flow's
+    // rounding differ, so a sharded step equals the one-GPU step bit for bit only this way.
     P.flow_lev0 = L;
     while (P.flow_lev0 > 2) {
         bool small = true;
         for (int q = F.level_ptr[P.flow_lev0 - 1]; q < F.level_ptr[P.flow_lev0] && small; ++q)
-            small = !mine(F.level[q]) || F.k[F.level[q]] + F.r[F.level[q]] <= kFlowMaxM;
+            small = F.k[F.level[q]] + F.r[F.level[q]] <= kFlowMaxM;
         if (!small) break;
         --P.flow_lev0;
     }
     {
         int wide = std::min(2, L);
-        while (wide < L && mine_in_level(wide) >= kFactorWideLevel) ++wide;
+        while (wide < L && F.level_ptr[wide + 1] - F.level_ptr[wide] >= kFactorWideLevel) ++wide;
         P.flow_lev0 = std::max(P.flow_lev0, wide);
     }
     std::vector<int32_t> ofac, ofwd;
