@@ -175,7 +175,7 @@ def solver_model(P, phase, world):
             "frac_of_chain_bound": t_chain / t_solve_us, "frac_of_bytes_bound": t_bytes / t_solve_us}
 
 
-PROFILE_TAG = "r05"   # profiles/<tag>_pmc_linearize_<prec>_<mode>.json, written by tools/pmc_summary.py
+PROFILE_TAG = "r06"   # profiles/<tag>_pmc_linearize_<prec>_<mode>.json, written by tools/pmc_summary.py
 
 
 def lib_sha256():
