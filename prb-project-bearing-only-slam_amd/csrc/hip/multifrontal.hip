@@ -706,7 +706,11 @@ __device__ __forceinline__ void fold_store(const FoldAcc<MAXM>& acc, double* F, 
 // extend-added with their update matrices (no separate forward launch). mf_factor_level (with
 // mf_forward_level) kept the front in global scratch above 90 rows and took ~140 us per level launch
 // at config 2; it remains for m > kBlkMaxM (fallback plans).
-constexpr int kBlkMaxM = kMfBlkMaxM, kBlkNb = 16;
+#ifndef BOS_MF_BLK_NB   // (A/B builds: the blocked kernel's panel width, a multiple of 4)
+#define BOS_MF_BLK_NB 16
+#endif
+constexpr int kBlkMaxM = kMfBlkMaxM, kBlkNb = BOS_MF_BLK_NB;
+static_assert(kBlkNb % 4 == 0 && kBlkNb <= 64, "panel width: MFMA steps of 4 columns, one pair per lane");
 constexpr int kBlkTiles = 9;   // 16 x 16 lower tiles per wave: (8 * 9 / 2 = 36 for 128 rows) / 4 waves
 // dynamic LDS of a front of m rows: F (m x m), w (kBlkMaxM), the fold's chunk y and landmark count,
 // the panel's column broadcast (kBlkNb)
