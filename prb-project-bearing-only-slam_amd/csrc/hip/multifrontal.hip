@@ -781,8 +781,24 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     __syncthreads();   // (W cleared)
     // chunk ch from set X; X is refilled with chunk ch + 2's values, Y's records with chunk ch + 3's
+#ifdef BOS_MF_BLK_FOLD_CYCLES   // (diagnostics: wave 0's cycles per chunk phase, tools/blk_fold_cycles.py)
+    unsigned long long cyc[5] = {0, 0, 0, 0, 0};
+    auto now = [&]() {
+        unsigned long long t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return t;
+    };
+#define BLK_CYC(i, t) cyc[i] += (t)
+#else
+#define BLK_CYC(i, t)
+#endif
     auto chunk = [&](int ch, Set& X, Set& Y) {
         int pos = 0, lml = 0, ncur = 0;
+#ifdef BOS_MF_BLK_FOLD_CYCLES
+        const unsigned long long c0 = now();
+#endif
         if (ch + 4 - tb.base > 63) tb.reload(a, ch, lane);
         FoldVals d = fold_decode(X.v);
         // the decoded values formed here, before the loads into X's registers are issued (left to
@@ -854,7 +870,13 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
                 nlb[2] = hi >> 4;
             }
         }
+#ifdef BOS_MF_BLK_FOLD_CYCLES
+        const unsigned long long c1 = now();
+#endif
         __syncthreads();
+#ifdef BOS_MF_BLK_FOLD_CYCLES
+        const unsigned long long c2 = now();
+#endif
         const int kc = 2 * nlb[0], blo = nlb[1], bhi = nlb[2];
         // The chunk's W columns past kc are zero (never written in this chunk, cleared after the last)
         // and y is finite there (zeroed before the first chunk), so both loops run over all 2 cap
@@ -900,7 +922,14 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
                         acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(oka ? av[st] : 0.0, okb ? bv[st] : 0.0, acc[u], 0, 0, 0);
             }
         }
+#ifdef BOS_MF_BLK_FOLD_CYCLES
+        const unsigned long long c3 = now();
+#endif
         __syncthreads();
+#ifdef BOS_MF_BLK_FOLD_CYCLES
+        const unsigned long long c4 = now();
+        BLK_CYC(0, c1 - c0); BLK_CYC(1, c2 - c1); BLK_CYC(2, c3 - c2); BLK_CYC(3, c4 - c3); BLK_CYC(4, 1);
+#endif
         if (wave == 0 && lane < ncur) {   // clear this chunk's W entries (wave 0 writes the next chunk's after)
 #pragma unroll
             for (int g = 0; g < 3; ++g) {
@@ -914,6 +943,11 @@ __device__ __forceinline__ void fold_children_wg(const MfArgs& a, int s, double*
         if (ch + 1 >= ch1) break;   // (a break: the loop's back edge always follows chunk ch + 1)
         chunk(ch + 1, B, A);
     }
+#ifdef BOS_MF_BLK_FOLD_CYCLES
+    if (tid == 0 && g_pivot_bwd)
+        for (int i = 0; i < 5; ++i) g_pivot_bwd[8 * (int64_t)s + i] = cyc[i];
+#endif
+#undef BLK_CYC
     if (wave == 0 && nbad) atomicAdd(a.info, nbad);
 }
 
