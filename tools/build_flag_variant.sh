@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build libbos.so of the working tree with extra compile flags (e.g. -DBOS_MF_MIX=0) into
+# Build libbos.so of the working tree with extra compile flags (e.g. -DBOS_MF_MIXB=0) into
 # gpurun_exp/libbos_<name>.so for A/B runs (tools/gn_ab.py), from a temporary copy of the package.
 # Usage: tools/build_flag_variant.sh name "FLAGS"
 set -e
