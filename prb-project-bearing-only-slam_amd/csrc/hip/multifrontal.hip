@@ -1954,6 +1954,19 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_mixb(const MfArgs a, const
         factor_front_blk<F32>(a, blk_list[b], lds);
         return;
     }
+#ifdef BOS_DIAG_PAIR   // (diagnostics: class-2 fronts two per workgroup, on waves 0 and BOS_DIAG_PAIR)
+    {
+        const int wv = threadIdx.x >> 6;
+        int i = b - n4;
+        if (i >= n.w && i - n.w < (n.z + 1) / 2) {
+            const int j = 2 * (i - n.w) + (wv == BOS_DIAG_PAIR ? 1 : 0);
+            if ((wv == 0 || wv == BOS_DIAG_PAIR) && j < n.z)
+                wave_front<48, kPanel48 ? kPanelKP : 0, F32>(a, a.level[o.z + j],
+                                                             reinterpret_cast<char*>(lds) + wv * 10400 * 1, threadIdx.x & 63);
+            return;
+        }
+    }
+#endif
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x;
     char* slot = reinterpret_cast<char*>(lds);
@@ -1961,13 +1974,22 @@ __global__ __launch_bounds__(kMfBlock) void mf_factor_mixb(const MfArgs a, const
     int i = b - n4;
     if (i < n.w) { wave_front<64, kPanel64 ? kPanelKP : 0, F32>(a, lst[o.w + i], slot, lane); return; }
     i -= n.w;
+#ifdef BOS_DIAG_PAIR
+    i -= (n.z + 1) / 2;
+#else
     if (i < n.z) { wave_front<48, kPanel48 ? kPanelKP : 0, F32>(a, lst[o.z + i], slot, lane); return; }
     i -= n.z;
+#endif
     if (i < n.y) { wave_front<32, 0, F32>(a, lst[o.y + i], slot, lane); return; }
     i -= n.y;
     if (i < n.x) wave_front<16, 0, F32>(a, lst[o.x + i], slot, lane);
 }
+#ifdef BOS_DIAG_PAIR
+constexpr int kMixbWaveLds = 4 * 10400;
+static_assert(sizeof(WaveLds<48, kPanel48 ? kPanelKP : 0>) <= 10400, "diagnostic slot");
+#else
 constexpr int kMixbWaveLds = (int)sizeof(WaveLds<64, kPanel64 ? kPanelKP : 0>);
+#endif
 
 
 // Backward substitution of one front by one wavefront (any m); LDS: x_own[k] | t[k] | x_rows[r] |
@@ -2647,7 +2669,11 @@ hipError_t mf_factor_t(MfDevice* d, int which, const double* A, double* x, hipSt
     for (int l = 0; l < std::min(P.flow_lev0, d->nlevels); ++l) {
         int n;
         // a level with blocked fronts and few fronts in all (config 2): one launch for all of them
+#ifdef BOS_DIAG_PAIR
+        const int n4 = P.count(l, 4), nwf = P.count(l, 0, 4) - P.count(l, 2) + (P.count(l, 2) + 1) / 2;
+#else
         const int n4 = P.count(l, 4), nwf = P.count(l, 0, 4);
+#endif
         if (kMixB && d->mixb && n4 > 0 && n4 + nwf <= d->ncu) {
             const int4 nw = make_int4(P.count(l, 0), P.count(l, 1), P.count(l, 2), P.count(l, 3));
             const int4 ow = make_int4(0, P.count(l, 0), P.count(l, 0, 2), P.count(l, 0, 3));
